@@ -1,0 +1,46 @@
+/* mnl_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference fields::step() hot path (PMack10/meep_nl,
+ * src/step.cpp:35-140) used as the parity checker for the HIP product path.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library.  Nothing under meep_nl_amd/ links or calls it.
+ *
+ * Parity pinning: see oracle/mnl_oracle.cpp header and DESIGN.md section
+ * "Oracle".  The grid, component numbering and the canonical host layout
+ * (Z fastest, (n+1) points per present direction, src/vec.cpp:482-494) are
+ * the same as include/meep_nl_amd.h so that arrays compare element-wise.
+ */
+#ifndef MNL_ORACLE_H
+#define MNL_ORACLE_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_sim orc_sim;
+
+const char *orc_last_error(void);
+orc_sim *orc_new(int dim, const int n[3], double a, double courant, const int io[3]);
+void orc_free(orc_sim *s);
+int orc_add_pml(orc_sim *s, int dir, int side, double thickness, double R, double mean_stretch);
+int orc_set_chi1inv(orc_sim *s, int comp, int dir, const double *arr);
+int orc_set_chi2(orc_sim *s, int comp, const double *arr);
+int orc_set_chi3(orc_sim *s, int comp, const double *arr);
+int orc_add_lorentzian(orc_sim *s, double omega0, double gamma, int drude, const double *sx,
+                       const double *sy, const double *sz);
+int orc_add_point_source(orc_sim *s, int comp, int kind, const double *params, int nparams,
+                         const double pos[3], double amp_re, double amp_im, int is_integrated);
+int orc_require_component(orc_sim *s, int comp);
+int orc_step(orc_sim *s, int nsteps);
+int orc_get_field(orc_sim *s, int comp, const double pos[3], double *out);
+int orc_copy_component(orc_sim *s, int comp, double *out, size_t n);
+int orc_set_threads(int nthreads);
+long long orc_t(orc_sim *s);
+double orc_dt(orc_sim *s);
+size_t orc_ntot(orc_sim *s);
+long long orc_nr_failures(orc_sim *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,243 @@
+"""ctypes wrapper of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+import this module.  The product path (``meep_nl_amd``) never does.
+
+The oracle restates the reference ``fields::step()`` (src/step.cpp:35-140)
+chunk by chunk on the CPU; see oracle/mnl_oracle.cpp for the citations.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+# component numbering shared with include/meep_nl_amd.h
+Ex, Ey, Ez, Hx, Hy, Hz, Dx, Dy, Dz, Bx, By, Bz = range(12)
+X, Y, Z = 0, 1, 2
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        c_int, c_double, c_void = ctypes.c_int, ctypes.c_double, ctypes.c_void_p
+        dptr = ctypes.POINTER(ctypes.c_double)
+        iptr = ctypes.POINTER(ctypes.c_int)
+        L.orc_last_error.restype = ctypes.c_char_p
+        L.orc_new.restype = c_void
+        L.orc_new.argtypes = [c_int, iptr, c_double, c_double, iptr]
+        L.orc_free.argtypes = [c_void]
+        L.orc_add_pml.argtypes = [c_void, c_int, c_int, c_double, c_double, c_double]
+        L.orc_set_chi1inv.argtypes = [c_void, c_int, c_int, dptr]
+        L.orc_set_chi2.argtypes = [c_void, c_int, dptr]
+        L.orc_set_chi3.argtypes = [c_void, c_int, dptr]
+        L.orc_add_lorentzian.argtypes = [c_void, c_double, c_double, c_int, dptr, dptr, dptr]
+        L.orc_add_point_source.argtypes = [c_void, c_int, c_int, dptr, c_int, dptr, c_double,
+                                           c_double, c_int]
+        L.orc_require_component.argtypes = [c_void, c_int]
+        L.orc_step.argtypes = [c_void, c_int]
+        L.orc_get_field.argtypes = [c_void, c_int, dptr, dptr]
+        L.orc_copy_component.argtypes = [c_void, c_int, dptr, ctypes.c_size_t]
+        L.orc_t.restype = ctypes.c_longlong
+        L.orc_t.argtypes = [c_void]
+        L.orc_dt.restype = c_double
+        L.orc_dt.argtypes = [c_void]
+        L.orc_ntot.restype = ctypes.c_size_t
+        L.orc_ntot.argtypes = [c_void]
+        L.orc_nr_failures.restype = ctypes.c_longlong
+        L.orc_nr_failures.argtypes = [c_void]
+        L.orc_set_threads.argtypes = [c_int]
+        _LIB = L
+    return _LIB
+
+
+def _chk(rc):
+    if rc != 0:
+        raise RuntimeError(lib().orc_last_error().decode())
+
+
+def _dp(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def set_threads(n):
+    return lib().orc_set_threads(int(n))
+
+
+class Oracle:
+    """One oracle simulation on a Meep-style grid_volume.
+
+    ``dim`` 1 uses the Z direction only (Meep's D1), 2 uses X,Y, 3 uses X,Y,Z.
+    ``io`` is the little corner in half-pixel units (0 = Meep default origin,
+    ``-n`` per direction = ``center_origin()`` for even n).
+    """
+
+    def __init__(self, dim, n, a, courant=0.5, io=(0, 0, 0)):
+        self.dim = dim
+        self.n = [int(v) for v in n]
+        self.a = float(a)
+        self.io = [int(v) for v in io]
+        na = (ctypes.c_int * 3)(*self.n)
+        ia = (ctypes.c_int * 3)(*self.io)
+        self.h = lib().orc_new(dim, na, self.a, float(courant), ia)
+        if not self.h:
+            raise RuntimeError(lib().orc_last_error().decode())
+        self.has = [dim >= 2, dim >= 2, dim != 2]
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_free(self.h)
+            self.h = None
+
+    # ---- geometry helpers (canonical layout: Z fastest, n+1 points per present dir)
+    def shape(self):
+        return tuple(self.n[d] + 1 for d in range(3) if self.has[d])
+
+    def shift(self, c, d):
+        if not self.has[d]:
+            return 0
+        t = c // 3
+        if t in (0, 2):
+            return 1 if d == c % 3 else 0
+        return 1 if d != c % 3 else 0
+
+    def coords(self, c):
+        """Positions (in length units) of every array point of component c."""
+        axes = []
+        for d in range(3):
+            if self.has[d]:
+                j = np.arange(self.n[d] + 1)
+                axes.append((self.io[d] + 2 * j + self.shift(c, d)) * (0.5 / self.a))
+        return np.meshgrid(*axes, indexing="ij")
+
+    # ---- structure
+    def add_pml(self, thickness, dirs=(0, 1, 2), sides=(0, 1), R=1e-15, mean_stretch=1.0):
+        for d in dirs:
+            for s in sides:
+                _chk(lib().orc_add_pml(self.h, d, s, thickness, R, mean_stretch))
+
+    def set_chi1inv(self, comp, d, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        self._keep = getattr(self, "_keep", []) + [arr]
+        _chk(lib().orc_set_chi1inv(self.h, comp, d, _dp(arr)))
+
+    def set_epsilon_fn(self, fn):
+        """Non-averaged epsilon (eps_averaging=False): chi1inv = 1/eps(loc)."""
+        for c in (Ex, Ey, Ez):
+            if self.dim == 1 and c != Ex:
+                continue
+            pts = self.coords(c)
+            self.set_chi1inv(c, c % 3, 1.0 / fn(*pts))
+
+    def set_chi2(self, comp, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        _chk(lib().orc_set_chi2(self.h, comp, _dp(arr)))
+
+    def set_chi3(self, comp, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        _chk(lib().orc_set_chi3(self.h, comp, _dp(arr)))
+
+    def add_lorentzian(self, omega0, gamma, sigmas, drude=False):
+        s = [None if v is None else np.ascontiguousarray(v, dtype=np.float64).ravel()
+             for v in sigmas]
+        _chk(lib().orc_add_lorentzian(self.h, omega0, gamma, int(drude), *[_dp(v) for v in s]))
+
+    # ---- fields
+    def add_point_source(self, comp, kind, params, pos, amp=1.0, is_integrated=False):
+        p = np.ascontiguousarray(params, dtype=np.float64)
+        pos = np.ascontiguousarray(list(pos) + [0.0] * (3 - len(pos)), dtype=np.float64)
+        amp = complex(amp)
+        _chk(lib().orc_add_point_source(self.h, comp, kind, _dp(p), len(p), _dp(pos), amp.real,
+                                        amp.imag, int(is_integrated)))
+
+    def add_gaussian_source(self, comp, freq, width, start, end, pos, amp=1.0,
+                            is_integrated=False):
+        self.add_point_source(comp, 0, [freq, width, start, end], pos, amp, is_integrated)
+
+    def legacy_point_source(self, comp, freq, width, peaktime, cutoff, pos, amp):
+        """fields::add_point_source(c, freq, width, peaktime, cutoff, vec, amp) -- the
+        deprecated C++ form used by tests/known_results.cpp (src/sources.cpp:189-211).
+        C++ src_time default is_integrated=true (src/meep.hpp:950-951)."""
+        width = width / freq
+        dt = self.dt
+        cutoff = (1.0 / self.a) + cutoff * width
+        if peaktime <= 0.0:
+            peaktime = self.t * dt + cutoff
+        peaktime += (-dt * 0.5) if comp in (Hx, Hy, Hz) else dt
+        self.add_gaussian_source(comp, freq, width, peaktime - cutoff, peaktime + cutoff, pos, amp,
+                                 is_integrated=comp not in (Hx, Hy, Hz))
+
+    def require_component(self, comp):
+        _chk(lib().orc_require_component(self.h, comp))
+
+    def step(self, n=1):
+        _chk(lib().orc_step(self.h, int(n)))
+
+    @property
+    def t(self):
+        return lib().orc_t(self.h)
+
+    @property
+    def dt(self):
+        return lib().orc_dt(self.h)
+
+    def time(self):
+        return self.t * self.dt
+
+    def round_time(self):
+        return float(np.float32(self.t * self.dt))
+
+    def get_field(self, comp, pos):
+        pos = np.ascontiguousarray(list(pos) + [0.0] * (3 - len(pos)), dtype=np.float64)
+        out = ctypes.c_double()
+        _chk(lib().orc_get_field(self.h, comp, _dp(pos), ctypes.byref(out)))
+        return out.value
+
+    def get_array(self, comp):
+        nt = lib().orc_ntot(self.h)
+        out = np.zeros(nt, dtype=np.float64)
+        _chk(lib().orc_copy_component(self.h, comp, _dp(out), nt))
+        return out.reshape(self.shape())
+
+    def nr_random_fallbacks(self):
+        return lib().orc_nr_failures(self.h)
+
+    def center(self):
+        """grid_volume::center() (src/vec.cpp:1089-1103): io + round_down_to_even(n)."""
+        out = []
+        for d in range(3):
+            if self.has[d]:
+                n = self.n[d] - (self.n[d] & 1)
+                out.append((self.io[d] + n) * (0.5 / self.a))
+            else:
+                out.append(0.0)
+        return out
+
+
+def meep_vol(dim, sizes, a, center_origin=False, courant=0.5):
+    """vol1d/vol2d/vol3d (src/vec.cpp:904-931) [+ center_origin]."""
+    n = [0, 0, 0]
+    if dim == 1:
+        n[2] = int(sizes[0] * a + 0.5)
+    elif dim == 2:
+        n[0] = 1 if sizes[0] == 0 else int(sizes[0] * a + 0.5)
+        n[1] = 1 if sizes[1] == 0 else int(sizes[1] * a + 0.5)
+    else:
+        n = [1 if s == 0 else int(s * a + 0.5) for s in sizes]
+    io = [0, 0, 0]
+    if center_origin:
+        io = [-(v - (v & 1)) for v in n]
+    return Oracle(dim, n, a, courant, io)
