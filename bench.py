@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X fields::step() hot path (BASELINE.json metric).
+
+Workload (weak scaling): BASELINE configs[2] -- 3-D dielectric waveguide
+(eps = 12 core |y|,|z| < 0.5 along x, eps_averaging=False) + PML(1.0) on all
+faces, resolution 10, fp64, real fields, Ez Gaussian current source
+(GaussianSource(0.15, fwidth=0.1)) at (0.05, 0.05, 0.05).  Each GPU owns a
+512^3-cell z-slab: the global grid is 512 x 512 x (512*N), so N=1 is exactly
+the 512^3 headline and per-GPU work is fixed as N grows.
+
+A "step" is one fields::step() (src/step.cpp:35-140) over the whole grid.
+value = (all cells * K) / max-over-ranks wall time, in Mcells*steps/s.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--size S] [--vacuum]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (with "roofline" and "cpu_baseline").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--size", type=int, default=512, help="cells per side of each GPU's slab")
+    ap.add_argument("--vacuum", action="store_true", help="north-star vacuum variant (no core)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def build_fields(args, rank, world, local_rank, nid):
+    from meep_nl_amd import core
+    res = 10.0
+    n = [args.size, args.size, args.size * world]
+    io = [-(v - (v & 1)) for v in n]  # center_origin()
+    gv = core.GridVolume(3, n, res, io)
+    s = core.Structure(gv, 0.5)
+    s.add_pml(1.0)
+    if not args.vacuum:
+        big = 1e9
+        s.set_box(0, [-big, big, -0.5 + 1e-12, 0.5 - 1e-12, -0.5 + 1e-12, 0.5 - 1e-12], 12.0)
+    f = core.Fields(s, device=local_rank, rank=rank, nranks=world, nccl_id=nid)
+    f.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0,
+                          is_integrated=False)
+    return gv, s, f
+
+
+def cpu_baseline(args):
+    """Time the oracle (CPU restatement, oracle/) on a bounded sample of the same
+    workload on this host's cores."""
+    from oracle import oracle as orc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 64))
+    orc.set_threads(threads)
+    import numpy as np
+    L = 128
+    o = orc.Oracle(3, [L, L, L], 10.0, 0.5, [-L, -L, -L])
+    o.add_pml(1.0)
+    if not args.vacuum:
+        for c in (0, 1, 2):
+            x, y, z = o.coords(c)
+            o.set_chi1inv(c, c, np.where((np.abs(y) < 0.5) & (np.abs(z) < 0.5), 1 / 12.0, 1.0))
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    o.step(2)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        o.step(2)
+        steps += 2
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or steps >= 400:
+            break
+    v = L ** 3 * steps / el / 1e6
+    return {"value": round(v, 2), "unit": "Mcells*steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ CPU restatement, {L}^3 {'vacuum' if args.vacuum else 'waveguide'}"
+                      f"+PML(1.0), {steps} steps in {el:.1f} s, OpenMP {threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    nid = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from meep_nl_amd import core
+        obj = [core.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        nid = obj[0]
+    gv, s, f = build_fields(args, rank, world, local_rank, nid)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    f.step(args.warmup)
+    barrier()
+    f.set_profiling(True)
+    t0 = time.perf_counter()
+    f.step(args.steps)  # returns after the device work is complete (stream synchronized)
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    n_launch, k_ms, k_bytes = f.kernel_stats(0)
+    bpc, cells_local = f.traffic_model()
+    total_cells = float(gv.n[0]) * gv.n[1] * gv.n[2]
+    value = total_cells * args.steps / el / 1e6
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+    avg_ms = k_ms / max(n_launch, 1)
+    achieved = k_bytes / (avg_ms * 1e-3) / 1e9 if n_launch else 0.0
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            with open(tpath) as fh:
+                tj = json.load(fh)
+            if tj.get("size") == args.size and tj.get("vacuum", False) == args.vacuum:
+                traffic = tj.get("curl_b_interior_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "curl_kernel<B, interior> (step_db(B_stuff))",
+            "bytes_per_launch": k_bytes, "avg_launch_ms": round(avg_ms, 4),
+            "launches": n_launch}
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        try:
+            cpu = cpu_baseline(args)
+        except Exception as e:  # the baseline must never hide the GPU number
+            cpu = {"error": str(e)}
+    out = {
+        "metric": "Mcells*steps/s (Yee cells x timesteps / s)",
+        "value": round(value, 1),
+        "unit": "Mcells*steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Gaussian point source; fields start at zero)",
+        "config": {
+            "workload": ("C3 3-D dielectric waveguide eps=12 core + PML(1.0)" if not args.vacuum
+                         else "C3-vacuum 3-D vacuum + PML(1.0)") +
+                        f", {args.size}x{args.size}x({args.size}*N) cells, res 10, real fields, "
+                        "Ez Gaussian current at (0.05,0.05,0.05)",
+            "grid": list(gv.n), "per_gpu_cells": args.size ** 3, "parallelism": f"z-slab x{world}",
+            "model_bytes_per_cell_step": bpc},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+    sys.stdout.flush()
+    if dist is not None:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

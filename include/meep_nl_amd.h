@@ -1,0 +1,156 @@
+/* meep_nl_amd.h -- C-ABI of the MI355X-native fields::step() hot path.
+ *
+ * Drop-in boundary for the reference's time-stepping core (PMack10/meep_nl =
+ * MIT Meep 1.30 + chi(2) Newton-Raphson fork).  Plain pointers and sizes only;
+ * no torch / HIP types.  Each entry cites the reference interface it replaces.
+ *
+ * Conventions
+ *   - components: MNL_EX..MNL_BZ (E, H, D, B x,y,z).  NOT the reference enum
+ *     order (src/meep/vec.hpp:31-56 interleaves Er/Ep); bindings map by name.
+ *   - grids: dim 1 = Z only (Meep D1), 2 = X,Y (Meep D2), 3 = X,Y,Z.
+ *     n[d] cells, resolution a, little corner io[d] in half-pixels
+ *     (grid_volume io, src/meep/vec.hpp:1014-1180; io = -n for center_origin).
+ *   - host arrays use the reference's per-chunk layout for the whole cell:
+ *     (n_d+1) points per present direction, Z fastest, X slowest
+ *     (grid_volume::set_strides, src/vec.cpp:482-494).  Entry j of a
+ *     component c sits at half-pixel io + 2 j + yee_shift(c).
+ *   - every call returns 0 on success, nonzero on error; mnl_last_error()
+ *     returns the message ("meep: ..." as meep::abort, src/mympi.cpp:244-262).
+ *   - the product path has no CPU fallback: creating fields without a HIP
+ *     device fails.
+ */
+#ifndef MEEP_NL_AMD_H
+#define MEEP_NL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  MNL_EX = 0, MNL_EY, MNL_EZ, MNL_HX, MNL_HY, MNL_HZ,
+  MNL_DX, MNL_DY, MNL_DZ, MNL_BX, MNL_BY, MNL_BZ, MNL_NUM_COMPONENTS
+};
+enum { MNL_X = 0, MNL_Y = 1, MNL_Z = 2 };
+enum { MNL_LOW = 0, MNL_HIGH = 1 };
+enum { MNL_SRC_GAUSSIAN = 0, MNL_SRC_CONTINUOUS = 1 };
+
+typedef struct mnl_structure mnl_structure;
+typedef struct mnl_fields mnl_fields;
+
+/* Thread-local message of the last failing call (meep::abort text). */
+const char *mnl_last_error(void);
+/* ABI version (major*100+minor). */
+int mnl_version(void);
+/* Number of visible HIP devices (0 on a host without GPU). */
+int mnl_device_count(int *count);
+
+/* ---- structure (replaces meep::structure, src/meep.hpp:809-920) ---------- */
+
+/* structure(grid_volume, eps, boundary_region, symmetry=identity, num_chunks,
+ * Courant) -- src/structure.cpp:49-64; grid_volume from vol1d/vol2d/vol3d
+ * (src/vec.cpp:904-931).  Vacuum, no PML until set below. */
+mnl_structure *mnl_structure_create(int dim, const int n[3], double a, double courant,
+                                    const int io[3]);
+void mnl_structure_destroy(mnl_structure *s);
+
+/* pml(thickness, d, side, Rasymptotic, mean_stretch) with the quadratic
+ * profile -- src/structure.cpp:285-301, applied per chunk by
+ * structure_chunk::use_pml (src/structure.cpp:661-691). */
+int mnl_structure_add_pml(mnl_structure *s, int dir, int side, double thickness,
+                          double R_asymptotic, double mean_stretch);
+
+/* structure_chunk::set_chi1inv row (src/anisotropic_averaging.cpp:211-298)
+ * for E component comp and direction dir; host array in the layout above
+ * (values at every point, ghosts included).  Off-diagonal entries are
+ * accepted but only their presence/zeros enter the arithmetic, exactly as in
+ * the fork (src/step_generic.cpp:631-633, 730-760). NULL resets to trivial. */
+int mnl_structure_set_chi1inv(mnl_structure *s, int comp, int dir, const double *host);
+/* structure_chunk::set_chi2 / set_chi3 (src/structure.cpp:795-866).  chi3 is
+ * inert in the fork (src/step_generic.cpp:829-886) and only recorded. */
+int mnl_structure_set_chi2(mnl_structure *s, int comp, const double *host);
+int mnl_structure_set_chi3(mnl_structure *s, int comp, const double *host);
+/* structure::add_susceptibility(sigma, E_stuff, lorentzian_susceptibility(
+ * omega0, gamma, drude)) -- src/anisotropic_averaging.cpp:300-372, isotropic
+ * (diagonal sigma per E component; NULL = 0). */
+int mnl_structure_add_lorentzian(mnl_structure *s, double omega0, double gamma, int drude,
+                                 const double *sigma_x, const double *sigma_y,
+                                 const double *sigma_z);
+/* Fill chi1inv/chi2/Lorentz-sigma of axis-aligned boxes on the device (fast
+ * setup for large grids; same values as passing 1/eps(loc) arrays with
+ * eps_averaging=False).  box = {xmin,xmax,ymin,ymax,zmin,zmax} in length
+ * units; later boxes win.  kind: 0 = epsilon (value = eps), 1 = chi2,
+ * 2 = chi3, 3 = Lorentz sigma of susceptibility #index. */
+int mnl_structure_set_box(mnl_structure *s, int kind, int index, const double box[6],
+                          double value);
+
+/* ---- fields (replaces meep::fields, src/meep.hpp:1731-2330) -------------- */
+
+/* fields(structure*) + use_real_fields() (src/fields.cpp:32-89, 144-156) on
+ * HIP device `device` (-1 = current).  Real fields only. */
+mnl_fields *mnl_fields_create(mnl_structure *s, int device);
+/* Distributed variant: one process per GPU, z-slab (3-D) / y-slab (2-D)
+ * decomposition of the global grid described by `s` (every rank passes the
+ * same global structure).  nccl_id: 128-byte RCCL unique id from rank 0
+ * (mnl_comm_unique_id), shared by the caller (e.g. torch.distributed). */
+mnl_fields *mnl_fields_create_dist(mnl_structure *s, int device, int rank, int nranks,
+                                   const void *nccl_id);
+int mnl_comm_unique_id(void *out128);
+void mnl_fields_destroy(mnl_fields *f);
+
+/* add_volume_source(c, src_time, volume(p,p), amp) for a point p
+ * (src/sources.cpp:455-494, weights: src/loop_in_chunks.cpp:263-500).
+ * kind GAUSSIAN: params = {freq, width, start_time, end_time} ->
+ *   gaussian_src_time(f, w, st, et) (src/sources.cpp:85-96).
+ * kind CONTINUOUS: params = {freq_re, freq_im, width, start, end, slowness}
+ *   -> continuous_src_time (src/meep.hpp:1038-1056, src/sources.cpp:121-141).
+ * is_integrated: dipole (E = eps^-1 (D - P_src)) vs current (D -= J dt)
+ * (src/update_eh.cpp:136-146, src/step.cpp:296-319). */
+int mnl_fields_add_point_source(mnl_fields *f, int comp, int kind, const double *params,
+                                int nparams, const double pos[3], double amp_re, double amp_im,
+                                int is_integrated);
+/* fields::require_component (src/fields.cpp:566-586). */
+int mnl_fields_require_component(mnl_fields *f, int comp);
+/* fields::step() x nsteps (src/step.cpp:35-140).  Collective for
+ * distributed fields.  NaN/Inf check of the D energy density at the cell
+ * centre (src/step.cpp:138-139) runs once per call. */
+int mnl_fields_step(mnl_fields *f, int nsteps);
+/* t (timesteps) and dt; time() = t*dt, round_time() = float(t*dt)
+ * (src/meep.hpp:1891-1892). */
+int mnl_fields_time(mnl_fields *f, long long *t, double *dt);
+/* fields::get_field(c, vec) with 8-point interpolation
+ * (src/monitor.cpp:127-160, src/vec.cpp:558-621).  Distributed: every rank
+ * returns the global value (sum over ranks, as get_field(..., parallel=true)). */
+int mnl_fields_get_field(mnl_fields *f, int comp, const double pos[3], double *out);
+/* Copy the whole-cell array of a component (layout above, ghosts = 0 as in
+ * the reference) into a caller-owned buffer of n doubles; H components read
+ * B where H==B (src/fields.cpp:493-517).  Distributed: only rank-owned planes
+ * are filled, the rest is 0 (sum over ranks gives the global array). */
+int mnl_fields_copy_component(mnl_fields *f, int comp, double *host, size_t n);
+/* Number of entries of the whole-cell array of comp. */
+size_t mnl_fields_ntot(mnl_fields *f);
+/* Per-sub-step GPU time in ms accumulated since creation (time_sink
+ * FieldUpdateB/H/D/E, BoundarySteppingB/H, src/meep.hpp:1610-1633);
+ * out[6]. */
+int mnl_fields_timers(mnl_fields *f, double out[6]);
+/* Newton-Raphson attempts that fell back to random seeds (never in the
+ * reference runs recorded in SURVEY.md; counted instead of printed). */
+int mnl_fields_nr_fallbacks(mnl_fields *f, long long *count);
+/* Algorithmic bytes per owned cell per step of this configuration
+ * (DESIGN.md "Roofline") and owned cells of this rank. */
+int mnl_fields_traffic_model(mnl_fields *f, double *bytes_per_cell_step, double *owned_cells);
+/* Enable HIP-event timing around every sub-step kernel group (on the stream
+ * the kernels run on) and reset the accumulated timers. */
+int mnl_fields_set_profiling(mnl_fields *f, int on);
+/* Accumulated launches / total ms of the interior curl kernel (which = 0:
+ * curl B = step_db(B_stuff), 1: curl D = step_db(D_stuff)) since the last
+ * mnl_fields_set_profiling, and its algorithmic bytes per launch. */
+int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, double *total_ms,
+                            double *bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,13 @@
+"""meep_nl_amd -- MI355X-native fields::step() hot path of PMack10/meep_nl.
+
+``meep_nl_amd.Simulation`` mirrors the meep.Simulation subset that drives the
+time stepper; ``meep_nl_amd.core`` mirrors the C++ structure/fields API.
+Both call libmnl.so (HIP kernels for gfx950 + C-ABI, include/meep_nl_amd.h).
+"""
+from .core import (Bx, By, Bz, Dx, Dy, Dz, Ex, Ey, Ez, Fields, GridVolume, Hx, Hy, Hz,
+                   Structure, X, Y, Z, device_count)
+from .simulation import (ALL, Block, ContinuousSource, DrudeSusceptibility, GaussianSource,
+                         High, LorentzianSusceptibility, Low, Medium, PML, Simulation, Source,
+                         Vector3, Volume, air, inf, vacuum)
+
+__version__ = "0.1.0"

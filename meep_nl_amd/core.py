@@ -1,0 +1,278 @@
+"""Low-level mirror of the reference C++ API (meep::structure / meep::fields).
+
+Mirrors src/meep.hpp:809-920 (structure) and 1731-2330 (fields) for the
+hot-path subset: grid_volume construction (vol1d/vol2d/vol3d +
+center_origin), pml(), set_chi1inv / set_epsilon, set_chi2 / set_chi3,
+add_susceptibility(lorentzian), add_point_source / add_volume_source (point),
+step(), time()/round_time(), get_field(), and raw component arrays.
+
+Arrays use the reference's own per-chunk layout for the whole cell
+((n+1) points per present direction, Z fastest; src/vec.cpp:482-494).
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+Ex, Ey, Ez, Hx, Hy, Hz, Dx, Dy, Dz, Bx, By, Bz = range(12)
+X, Y, Z = 0, 1, 2
+COMPONENT_NAMES = ["ex", "ey", "ez", "hx", "hy", "hz", "dx", "dy", "dz", "bx", "by", "bz"]
+
+
+class GridVolume:
+    """grid_volume for Cartesian D1 (Z), D2 (X,Y), D3 (X,Y,Z)."""
+
+    def __init__(self, dim, n, a, io=(0, 0, 0)):
+        self.dim = int(dim)
+        self.has = [dim >= 2, dim >= 2, dim != 2]
+        self.n = [int(n[d]) if self.has[d] else 0 for d in range(3)]
+        self.io = [int(io[d]) if self.has[d] else 0 for d in range(3)]
+        self.a = float(a)
+
+    @classmethod
+    def vol(cls, dim, sizes, a, center_origin=False):
+        """vol1d/vol2d/vol3d (src/vec.cpp:904-931) [+ center_origin (vec.hpp:1150)]."""
+        n = [0, 0, 0]
+        if dim == 1:
+            n[2] = int(sizes[0] * a + 0.5)
+        elif dim == 2:
+            n[0] = 1 if sizes[0] == 0 else int(sizes[0] * a + 0.5)
+            n[1] = 1 if sizes[1] == 0 else int(sizes[1] * a + 0.5)
+        else:
+            n = [1 if s == 0 else int(s * a + 0.5) for s in sizes]
+        io = [-(v - (v & 1)) for v in n] if center_origin else [0, 0, 0]
+        return cls(dim, n, a, io)
+
+    def shape(self):
+        return tuple(self.n[d] + 1 for d in range(3) if self.has[d])
+
+    def ntot(self):
+        return int(np.prod(self.shape()))
+
+    def shift(self, c, d):
+        if not self.has[d]:
+            return 0
+        t = c // 3
+        if t in (0, 2):
+            return 1 if d == c % 3 else 0
+        return 1 if d != c % 3 else 0
+
+    def coords(self, c):
+        axes = []
+        for d in range(3):
+            if self.has[d]:
+                j = np.arange(self.n[d] + 1)
+                axes.append((self.io[d] + 2 * j + self.shift(c, d)) * (0.5 / self.a))
+        return np.meshgrid(*axes, indexing="ij")
+
+    def center(self):
+        """grid_volume::center() (src/vec.cpp:1089-1103)."""
+        out = []
+        for d in range(3):
+            if self.has[d]:
+                n = self.n[d] - (self.n[d] & 1)
+                out.append((self.io[d] + n) * (0.5 / self.a))
+            else:
+                out.append(0.0)
+        return out
+
+
+class Structure:
+    """meep::structure for one grid_volume (no symmetry, PML chunks implicit)."""
+
+    def __init__(self, gv, courant=0.5):
+        self.gv = gv
+        self.courant = float(courant)
+        na = (ctypes.c_int * 3)(*gv.n)
+        ia = (ctypes.c_int * 3)(*gv.io)
+        self.h = lib().mnl_structure_create(gv.dim, na, gv.a, self.courant, ia)
+        if not self.h:
+            raise RuntimeError(lib().mnl_last_error().decode())
+        self._nsus = 0
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().mnl_structure_destroy(self.h)
+            self.h = None
+
+    def add_pml(self, thickness, dirs=(0, 1, 2), sides=(0, 1), R=1e-15, mean_stretch=1.0):
+        for d in dirs:
+            for s in sides:
+                check(lib().mnl_structure_add_pml(self.h, d, s, float(thickness), R, mean_stretch))
+
+    def _arr(self, a):
+        return np.ascontiguousarray(np.broadcast_to(a, self.gv.shape()), dtype=np.float64).ravel()
+
+    def set_chi1inv(self, comp, d, arr):
+        check(lib().mnl_structure_set_chi1inv(self.h, comp, d, None if arr is None else ptr(self._arr(arr))))
+
+    def set_epsilon_fn(self, fn):
+        """set_epsilon without averaging: chi1inv = 1/eps(location) per E component."""
+        for c in (Ex, Ey, Ez):
+            if self.gv.dim == 1 and c != Ex:
+                continue
+            self.set_chi1inv(c, c % 3, 1.0 / fn(*self.gv.coords(c)))
+
+    def set_chi2(self, comp, arr):
+        check(lib().mnl_structure_set_chi2(self.h, comp, ptr(self._arr(arr))))
+
+    def set_chi3(self, comp, arr):
+        check(lib().mnl_structure_set_chi3(self.h, comp, ptr(self._arr(arr))))
+
+    def add_lorentzian(self, omega0, gamma, sigmas, drude=False):
+        s = [None if v is None else self._arr(v) for v in sigmas]
+        check(lib().mnl_structure_add_lorentzian(self.h, omega0, gamma, int(drude),
+                                                 *[ptr(v) for v in s]))
+        self._nsus += 1
+        return self._nsus - 1
+
+    def set_box(self, kind, box, value, index=0):
+        b = np.ascontiguousarray(box, dtype=np.float64)
+        check(lib().mnl_structure_set_box(self.h, kind, index, ptr(b), float(value)))
+
+
+class Fields:
+    """meep::fields with use_real_fields() on one MI355X (or one z-slab of it)."""
+
+    def __init__(self, structure, device=-1, rank=0, nranks=1, nccl_id=None):
+        self.s = structure
+        self.gv = structure.gv
+        if nranks > 1:
+            self.h = lib().mnl_fields_create_dist(structure.h, device, rank, nranks, nccl_id)
+        else:
+            self.h = lib().mnl_fields_create(structure.h, device)
+        if not self.h:
+            raise RuntimeError(lib().mnl_last_error().decode())
+        self.rank, self.nranks = rank, nranks
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().mnl_fields_destroy(self.h)
+            self.h = None
+
+    # -- sources
+    def add_point_source(self, comp, kind, params, pos, amp=1.0, is_integrated=False):
+        p = np.ascontiguousarray(params, dtype=np.float64)
+        pos = np.ascontiguousarray(list(pos) + [0.0] * (3 - len(pos)), dtype=np.float64)
+        amp = complex(amp)
+        check(lib().mnl_fields_add_point_source(self.h, comp, kind, ptr(p), len(p), ptr(pos),
+                                                amp.real, amp.imag, int(is_integrated)))
+
+    def add_gaussian_source(self, comp, freq, width, start, end, pos, amp=1.0,
+                            is_integrated=False):
+        """gaussian_src_time(f, w, start, end) (src/sources.cpp:85-96)."""
+        self.add_point_source(comp, 0, [freq, width, start, end], pos, amp, is_integrated)
+
+    def add_continuous_source(self, comp, freq, width, start, end, slowness, pos, amp=1.0,
+                              is_integrated=False):
+        f = complex(freq)
+        self.add_point_source(comp, 1, [f.real, f.imag, width, start, end, slowness], pos, amp,
+                              is_integrated)
+
+    def legacy_point_source(self, comp, freq, width, peaktime, cutoff, pos, amp):
+        """Deprecated C++ fields::add_point_source(c, freq, width, peaktime, cutoff,
+        vec, amp) (src/sources.cpp:189-211); C++ sources are integrated by default
+        (src/meep.hpp:950-951), magnetic ones are not."""
+        width = width / freq
+        dt = self.dt
+        cutoff = (1.0 / self.gv.a) + cutoff * width
+        if peaktime <= 0.0:
+            peaktime = self.t * dt + cutoff
+        peaktime += (-dt * 0.5) if comp in (Hx, Hy, Hz) else dt
+        self.add_gaussian_source(comp, freq, width, peaktime - cutoff, peaktime + cutoff, pos,
+                                 amp, is_integrated=comp not in (Hx, Hy, Hz))
+
+    def require_component(self, comp):
+        check(lib().mnl_fields_require_component(self.h, comp))
+
+    # -- stepping
+    def step(self, n=1):
+        check(lib().mnl_fields_step(self.h, int(n)))
+
+    def _time(self):
+        t = ctypes.c_longlong()
+        dt = ctypes.c_double()
+        check(lib().mnl_fields_time(self.h, ctypes.byref(t), ctypes.byref(dt)))
+        return t.value, dt.value
+
+    @property
+    def t(self):
+        return self._time()[0]
+
+    @property
+    def dt(self):
+        return self._time()[1]
+
+    def time(self):
+        t, dt = self._time()
+        return t * dt
+
+    def round_time(self):
+        t, dt = self._time()
+        return float(np.float32(t * dt))
+
+    # -- monitors
+    def get_field(self, comp, pos):
+        pos = np.ascontiguousarray(list(pos) + [0.0] * (3 - len(pos)), dtype=np.float64)
+        out = ctypes.c_double()
+        check(lib().mnl_fields_get_field(self.h, comp, ptr(pos), ctypes.byref(out)))
+        return out.value
+
+    def get_array(self, comp):
+        nt = lib().mnl_fields_ntot(self.h)
+        out = np.zeros(nt, dtype=np.float64)
+        check(lib().mnl_fields_copy_component(self.h, comp, ptr(out), nt))
+        return out.reshape(self.gv.shape())
+
+    def center(self):
+        return self.gv.center()
+
+    # -- instrumentation
+    def timers(self):
+        out = np.zeros(6)
+        check(lib().mnl_fields_timers(self.h, ptr(out)))
+        return dict(zip(["FieldUpdateB", "FieldUpdateH", "FieldUpdateD", "FieldUpdateE",
+                         "Sources", "BoundarySteppingHalo"], out.tolist()))
+
+    def nr_fallbacks(self):
+        v = ctypes.c_longlong()
+        check(lib().mnl_fields_nr_fallbacks(self.h, ctypes.byref(v)))
+        return v.value
+
+    def set_profiling(self, on=True):
+        check(lib().mnl_fields_set_profiling(self.h, int(on)))
+
+    def kernel_stats(self, which=0):
+        n = ctypes.c_longlong()
+        ms = ctypes.c_double()
+        b = ctypes.c_double()
+        check(lib().mnl_fields_kernel_stats(self.h, which, ctypes.byref(n), ctypes.byref(ms),
+                                            ctypes.byref(b)))
+        return n.value, ms.value, b.value
+
+    def traffic_model(self):
+        b = ctypes.c_double()
+        c = ctypes.c_double()
+        check(lib().mnl_fields_traffic_model(self.h, ctypes.byref(b), ctypes.byref(c)))
+        return b.value, c.value
+
+
+def device_count():
+    n = ctypes.c_int()
+    try:
+        check(lib().mnl_device_count(ctypes.byref(n)))
+    except (RuntimeError, OSError):
+        return 0
+    return n.value
+
+
+def unique_id():
+    buf = ctypes.create_string_buffer(128)
+    check(lib().mnl_comm_unique_id(buf))
+    return buf.raw
+
+
+__all__ = ["GridVolume", "Structure", "Fields", "device_count", "unique_id", "math"]

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build meep_nl_amd/libmnl.so for gfx950 (MI355X).  hipcc for the kernels,
+# g++ for the host side (see mnl_host.cpp header for why).
+set -e
+HERE="$(cd "$(dirname "$0")" && pwd)"
+OUT="$HERE/../libmnl.so"
+ROCM=${ROCM_PATH:-/opt/rocm}
+TMP="$HERE/_obj"
+mkdir -p "$TMP"
+ARCH=${MNL_ARCH:-gfx950}
+hipcc --offload-arch=$ARCH -O3 -ffp-contract=off -fPIC -std=c++17 -Wall \
+  -c "$HERE/mnl_kernels.hip" -o "$TMP/mnl_kernels.o"
+CXXF="-O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$ROCM/include"
+g++ $CXXF -c "$HERE/mnl_host.cpp" -o "$TMP/mnl_host.o"
+g++ $CXXF -c "$HERE/mnl_comm.cpp" -o "$TMP/mnl_comm.o"
+hipcc --offload-arch=$ARCH -shared -fPIC -o "$OUT" "$TMP/mnl_kernels.o" "$TMP/mnl_host.o" \
+  "$TMP/mnl_comm.o" -L$ROCM/lib -lrccl -Wl,-rpath,$ROCM/lib
+echo "built $OUT"

@@ -1,0 +1,1595 @@
+// mnl_host.cpp -- C-ABI (include/meep_nl_amd.h) and host orchestration of the
+// MI355X fields::step() path.  Built with g++ (not hipcc) on purpose: the
+// per-step source amplitudes use std::complex / libm exactly as the reference
+// does (src/sources.cpp:72-160, src/step.cpp:296-319), so the values handed
+// to the GPU are bit-identical to the reference's.
+//
+// Owns: structure description, PML chunk/zone tables (src/structure.cpp:
+// 96-140, 509-523, 656-691), device allocation (one fp64 SoA buffer per
+// component), the per-step launch sequence (src/step.cpp:35-140), point-source
+// weights (src/loop_in_chunks.cpp:263-500) and get_field interpolation
+// (src/vec.cpp:558-621, src/monitor.cpp:127-160).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/meep_nl_amd.h"
+#include "mnl_comm.hpp"
+#include "mnl_internal.hpp"
+
+using namespace mnl;
+typedef std::complex<double> cplx;
+
+namespace {
+
+const double pi = 3.141592653589793238462643383276;  // meep::pi
+thread_local std::string g_err;
+
+int fail(const std::string &m) {
+  g_err = "meep: " + m;
+  return -1;
+}
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess)                                                         \
+      return fail(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x); \
+  } while (0)
+
+inline int cdir(int c) { return c % 3; }
+inline int ctype(int c) { return c / 3; }
+
+// ------------------------------------------------------------- source time
+// gaussian_src_time / continuous_src_time (src/sources.cpp:85-141,
+// src/meep.hpp:937-1056).
+struct SrcTime {
+  int kind = 0;
+  bool is_integrated = false;
+  double freq = 0, width = 0, peak_time = 0, cutoff = 0;
+  cplx cfreq;
+  double cwidth = 0, start_time = 0, end_time = 0, slowness = 3;
+  double cur_time = NAN;
+  cplx cur_dipole, cur_current;
+
+  cplx dipole(double time) const {
+    if (kind == 0) {
+      double tt = time - peak_time;
+      if (float(fabs(tt)) > cutoff) return 0.0;
+      cplx amp = 1.0 / cplx(0, -2 * pi * freq);
+      return exp(-tt * tt / (2 * width * width)) * std::polar(1.0, -2 * pi * freq * tt) * amp;
+    }
+    float rtime = float(time);
+    if (rtime < start_time || rtime > end_time) return 0.0;
+    cplx amp = 1.0 / (cplx(0, -1.0) * (2 * pi) * cfreq);
+    if (cwidth == 0.0) return exp(cplx(0, -1.0) * (2 * pi) * cfreq * time) * amp;
+    double ts = (time - start_time) / cwidth - slowness;
+    double te = (end_time - time) / cwidth - slowness;
+    return exp(cplx(0, -1.0) * (2 * pi) * cfreq * time) * amp * (1.0 + tanh(ts)) *
+           (1.0 + tanh(te)) * 0.25;
+  }
+  void update(double time, double dt) {  // src_time::update, src/meep.hpp:972-978
+    if (time != cur_time) {
+      cur_dipole = dipole(time);
+      cur_current = (dipole(time + dt) - dipole(time)) / dt;
+      cur_time = time;
+    }
+  }
+  bool same(const SrcTime &o) const {
+    return kind == o.kind && is_integrated == o.is_integrated && freq == o.freq &&
+           width == o.width && peak_time == o.peak_time && cutoff == o.cutoff &&
+           cfreq == o.cfreq && cwidth == o.cwidth && start_time == o.start_time &&
+           end_time == o.end_time && slowness == o.slowness;
+  }
+};
+
+struct SrcGroup {  // src_vol (src/meep_internals.hpp:49-82) over the whole cell
+  int comp;        // E or H component
+  int st;
+  std::vector<long long> gidx;  // global canonical index of comp
+  std::vector<int> jglob;       // 3 global indices per point
+  std::vector<cplx> amp;
+};
+
+struct Lorentz {
+  double omega0, gamma;
+  int drude;
+  std::vector<double> sigma[3];  // canonical arrays (empty = 0)
+};
+
+struct BoxSpec {
+  int kind, index;
+  double box[6];
+  double value;
+};
+
+}  // namespace
+
+// =============================================================== structure
+struct mnl_structure {
+  int dim;
+  int n[3];
+  int io[3];
+  bool has[3];
+  double a, courant, dt;
+  double pml_thick[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+  double pml_R[3][2], pml_stretch[3][2];
+  std::vector<double> chi1inv[3][3];  // [E comp][dir], canonical
+  std::vector<double> chi2[3], chi3[3];
+  std::vector<Lorentz> lor;
+  std::vector<BoxSpec> boxes;
+  size_t ntot;
+
+  int shift(int c, int d) const {
+    if (!has[d]) return 0;
+    int t = ctype(c);
+    if (t == T_E || t == T_D) return d == cdir(c);
+    return d != cdir(c);
+  }
+  long long cstride(int d) const {
+    if (!has[d]) return 0;
+    long long nz = has[2] ? n[2] + 1 : 1, ny = has[1] ? n[1] + 1 : 1;
+    return d == 2 ? 1 : (d == 1 ? nz : nz * ny);
+  }
+};
+
+// =============================================================== fields
+struct mnl_fields {
+  mnl_structure S;  // copy of the global structure description
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int rank = 0, nranks = 1;
+  std::unique_ptr<Comm> comm;
+  int slab_dir = 2;  // direction decomposed across ranks
+  DevGrid g;
+  DevFields f;
+  size_t nlocal = 0;  // doubles per local array
+  bool allocated[MNL_NUM_COMPONENTS] = {false};
+  bool pml_any[3] = {false, false, false};
+  std::vector<uint8_t> h_flag[3], h_zone[3];
+  std::vector<double> h_sig[3], h_kap[3], h_siginv[3];
+  std::vector<void *> dev_allocs;
+  Box interior;
+  std::vector<Box> shell;
+  CurlPlan planB, planD;
+  bool nr = false;
+  // sources
+  std::vector<SrcTime> srcs;
+  std::vector<SrcGroup> groups;
+  bool src_dirty = true;
+  std::vector<long long> srcB_idx, srcD_idx, isrc_idx;  // local linear indices
+  std::vector<int> srcB_comp, srcD_comp, isrc_comp;
+  std::vector<std::pair<int, int>> srcB_ref, srcD_ref, isrc_ref;  // (group, point)
+  long long *d_srcB_idx = nullptr, *d_srcD_idx = nullptr;
+  int *d_srcB_comp = nullptr, *d_srcD_comp = nullptr;
+  double *d_vals = nullptr;
+  size_t d_vals_cap = 0;
+  long long t = 0;
+  double dt;
+  // timers / profiling
+  bool profiling = false;
+  double timer_ms[8] = {0};
+  long long timer_count[8] = {0};
+  std::vector<hipEvent_t> ev_pool;
+  unsigned long long *d_nr_fallbacks = nullptr;
+  double *d_scratch = nullptr;  // canonical-size staging buffer
+  size_t scratch_cap = 0;
+
+  ~mnl_fields() {
+    if (device >= 0) hipSetDevice(device);
+    for (void *p : dev_allocs) hipFree(p);
+    for (auto e : ev_pool) hipEventDestroy(e);
+    if (d_scratch) hipFree(d_scratch);
+    if (d_vals) hipFree(d_vals);
+    comm.reset();
+    if (stream) hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+template <class T>
+int dev_alloc(mnl_fields *F, T **p, size_t n, bool zero = true) {
+  void *q = nullptr;
+  hipError_t e = hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T));
+  if (e != hipSuccess) return fail(std::string("hipMalloc failed: ") + hipGetErrorString(e));
+  if (zero) {
+    e = hipMemsetAsync(q, 0, std::max<size_t>(n, 1) * sizeof(T), F->stream);
+    if (e != hipSuccess) return fail(std::string("hipMemset failed: ") + hipGetErrorString(e));
+  }
+  F->dev_allocs.push_back(q);
+  *p = (T *)q;
+  return 0;
+}
+
+// ------------------------------------------------------------- PML zones
+// structure::use_pml + effort volumes (src/structure.cpp:509-523, 118-137)
+// and structure_chunk::use_pml (src/structure.cpp:656-691) folded into
+// per-direction tables over the global half-coordinate q = p - io.
+inline double pml_x(int i, double dx, double bloc, double a) {
+  double here = i * 0.5 / a;
+  return (0.5 / a * ((int)(dx * (2 * a) + 0.5) - (int)(fabs(bloc - here) * (2 * a) + 0.5)));
+}
+
+struct ZoneIv {
+  int c0, c1, zone;  // chunk covers half-coords [c0, c1] relative to io
+};
+
+std::vector<ZoneIv> zone_intervals(const mnl_structure &S, int d) {
+  std::vector<ZoneIv> iv;
+  int n2 = 2 * S.n[d];
+  int nlo = 0, nhi = 0;
+  if (S.n[d] > 1 && S.pml_thick[d][0] > 0) nlo = int(S.pml_thick[d][0] * S.a + 1 + 0.5);
+  if (S.n[d] > 1 && S.pml_thick[d][1] > 0) nhi = int(S.pml_thick[d][1] * S.a + 1 + 0.5);
+  int lo_end = nlo ? 2 * nlo : 0, hi_start = nhi ? n2 - 2 * nhi : n2;
+  if (nlo) iv.push_back({0, lo_end, 0});
+  if (hi_start > lo_end) iv.push_back({lo_end, hi_start, 1});
+  if (nhi) iv.push_back({hi_start, n2, 2});
+  return iv;
+}
+
+int build_pml_tables(mnl_fields *F) {
+  const mnl_structure &S = F->S;
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    int nq = 2 * S.n[d] + 2;
+    F->h_flag[d].assign(nq, 0);
+    F->h_zone[d].assign(nq, 1);
+    F->h_sig[d].assign(nq, 0.0);
+    F->h_kap[d].assign(nq, 1.0);
+    F->h_siginv[d].assign(nq, 1.0);
+    auto ivs = zone_intervals(S, d);
+    int nlo = 0, nhi = 0;
+    for (auto &z : ivs) {
+      if (z.zone == 0) nlo = 1;
+      if (z.zone == 2) nhi = 1;
+    }
+    if ((nlo || nhi) && ivs.size() < size_t(1 + nlo + nhi))
+      return fail("PML layers overlap (2*int(thickness*a+1.5) > cells along a direction)");
+    for (auto &z : ivs) {
+      // chunk-local profile, chunk io_c = io + c0, n_c = (c1-c0)/2
+      int io_c = S.io[d] + z.c0, big_c = S.io[d] + z.c1;
+      std::vector<double> sig, kap, siginv;
+      bool flag = false;
+      for (int side = 0; side < 2; side++) {
+        double dx = S.pml_thick[d][side];
+        if (dx <= 0.0 || S.n[d] <= 1) continue;
+        double bloc = (side == 0 ? S.io[d] : S.io[d] + 2 * S.n[d]) * (0.5 * (1.0 / S.a));
+        double prefac = (-log(S.pml_R[d][side])) / (4 * dx * (1. / 3.));
+        double kappa_prefac = (S.pml_stretch[d][side] - 1) / (1. / 4.);
+        bool found = false;
+        for (int i = io_c; i <= big_c + 1; ++i)
+          if (pml_x(i, dx, bloc, S.a) > 0) {
+            found = true;
+            break;
+          }
+        if (!found) continue;
+        flag = true;
+        int nc = big_c - io_c + 2;
+        sig.assign(nc, 0.0);
+        kap.assign(nc, 1.0);
+        siginv.assign(nc, 1.0);
+        for (int i = io_c; i <= big_c + 1; ++i) {
+          int idx = i - io_c;
+          double x = pml_x(i, dx, bloc, S.a);
+          if (x > 0) {
+            double u = x / dx;
+            double sp = u * u;
+            sig[idx] = 0.5 * F->dt * prefac * sp;
+            kap[idx] = 1 + kappa_prefac * sp * (x / dx);
+            siginv[idx] = 1 / (kap[idx] + sig[idx]);
+          }
+        }
+      }
+      // owned half-coords of this chunk: (c0, c1]
+      for (int q = z.c0 + 1; q <= z.c1; q++) {
+        F->h_zone[d][q] = (uint8_t)z.zone;
+        if (flag) {
+          F->h_flag[d][q] = 1;
+          F->h_sig[d][q] = sig[q - z.c0];
+          F->h_kap[d][q] = kap[q - z.c0];
+          F->h_siginv[d][q] = siginv[q - z.c0];
+        }
+      }
+      if (flag) F->pml_any[d] = true;
+    }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------- grid / boxes
+void setup_grid(mnl_fields *F) {
+  const mnl_structure &S = F->S;
+  DevGrid &g = F->g;
+  memset(&g, 0, sizeof(g));
+  g.dim = S.dim;
+  int nax = 0;
+  for (int d = 0; d < 3; d++) g.ax[d] = S.has[d] ? nax++ : -1;
+  // slab direction = slowest present direction
+  F->slab_dir = S.has[2] ? 2 : 1;
+  int lo_cell = 0, hi_cell = S.n[F->slab_dir];
+  if (F->nranks > 1) {
+    int ncell = S.n[F->slab_dir];
+    int base = ncell / F->nranks, rem = ncell % F->nranks;
+    lo_cell = F->rank * base + std::min(F->rank, rem);
+    hi_cell = lo_cell + base + (F->rank < rem ? 1 : 0);
+  }
+  int Nax[3] = {1, 1, 1};
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    g.nglob[d] = S.n[d];
+    g.wall[d] = 1;
+    if (d == F->slab_dir) {
+      g.off[d] = lo_cell;
+      Nax[g.ax[d]] = hi_cell - lo_cell + 1;
+      int nloc = hi_cell - lo_cell;
+      g.owned_lo_sh[d] = 0;
+      g.owned_hi_sh[d] = nloc - 1;
+      g.owned_lo_un[d] = 1;
+      g.owned_hi_un[d] = (hi_cell == S.n[d]) ? nloc - 1 : nloc;  // global wall plane excluded
+    } else {
+      g.off[d] = 0;
+      Nax[g.ax[d]] = S.n[d] + 1;
+      g.owned_lo_sh[d] = 0;
+      g.owned_hi_sh[d] = S.n[d] - 1;
+      g.owned_lo_un[d] = 1;
+      g.owned_hi_un[d] = S.n[d] - 1;
+    }
+  }
+  for (int k = 0; k < 3; k++) g.N[k] = Nax[k];
+  long long p0 = (g.N[0] + 15) / 16 * 16;
+  if (g.N[1] == 1 && g.N[2] == 1) p0 = g.N[0];
+  g.st[0] = 1;
+  g.st[1] = p0;
+  g.st[2] = p0 * g.N[1];
+  F->nlocal = size_t(p0) * g.N[1] * g.N[2];
+  for (int d = 0; d < 3; d++) g.sdir[d] = g.ax[d] >= 0 ? g.st[g.ax[d]] : 0;
+}
+
+void setup_boxes(mnl_fields *F) {
+  const mnl_structure &S = F->S;
+  DevGrid &g = F->g;
+  int ilo[3] = {0, 0, 0}, ihi[3] = {0, 0, 0};  // per device axis, local
+  bool none = false;
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    int n = S.n[d];
+    std::vector<char> good(n + 1);
+    for (int j = 0; j <= n; j++) {
+      int q0 = 2 * j, q1 = 2 * j + 1;
+      bool ok = F->h_flag[d][q0] == 0 && F->h_flag[d][q1] == 0;
+      if (F->nr) ok = ok && F->h_zone[d][q0] == 1 && F->h_zone[d][q1] == 1;
+      good[j] = ok;
+    }
+    int lo = 0;
+    while (lo <= n && !good[lo]) lo++;
+    int hi = n;
+    while (hi >= 0 && !good[hi]) hi--;
+    for (int j = lo; j <= hi; j++)
+      if (!good[j]) lo = hi + 1;  // non-contiguous: no interior
+    if (lo > hi) none = true;
+    int a = g.ax[d];
+    int l = lo - g.off[d], h = hi - g.off[d];
+    l = std::max(l, 0);
+    h = std::min(h, g.N[a] - 1);
+    if (l > h) none = true;
+    ilo[a] = l;
+    ihi[a] = h;
+  }
+  Box full;
+  for (int k = 0; k < 3; k++) full.lo[k] = 0, full.hi[k] = g.N[k] - 1;
+  F->shell.clear();
+  if (none) {
+    F->interior = full;
+    F->interior.hi[0] = -1;  // empty
+    F->shell.push_back(full);
+    return;
+  }
+  Box in = full;
+  for (int k = 0; k < 3; k++)
+    if (g.N[k] > 1 || ihi[k] >= ilo[k]) in.lo[k] = ilo[k], in.hi[k] = ihi[k];
+  F->interior = in;
+  // onion shell decomposition, slowest axis first
+  Box cur = full;
+  for (int k = 2; k >= 0; k--) {
+    if (in.lo[k] > cur.lo[k]) {
+      Box b = cur;
+      b.hi[k] = in.lo[k] - 1;
+      F->shell.push_back(b);
+    }
+    if (in.hi[k] < cur.hi[k]) {
+      Box b = cur;
+      b.lo[k] = in.hi[k] + 1;
+      F->shell.push_back(b);
+    }
+    cur.lo[k] = in.lo[k];
+    cur.hi[k] = in.hi[k];
+  }
+}
+
+// ------------------------------------------------------------- allocation
+bool is_like(int dim, int c1, int c2) {  // src/fields.cpp:473-491
+  if (dim != 2) return true;
+  auto tm = [](int c) {
+    return c == MNL_HX || c == MNL_HY || c == MNL_BX || c == MNL_BY || c == MNL_EZ ||
+           c == MNL_DZ;
+  };
+  return !(tm(c1) ^ tm(c2));
+}
+bool has_field(const mnl_structure &S, int c) {
+  if (S.dim == 1) return c == MNL_EX || c == MNL_HY || c == MNL_DX || c == MNL_BY;
+  return true;
+}
+
+void make_plans(mnl_fields *F) {
+  // src/fields.cpp:438-471: comp d of B/D gets term1 (comp (d+2)%3 along (d+1)%3)
+  // if that direction exists and the partner is allocated, term2 likewise.
+  const mnl_structure &S = F->S;
+  for (int t = 0; t < 2; t++) {
+    CurlPlan &p = t == 0 ? F->planB : F->planD;
+    int ft = t == 0 ? T_B : T_D, src = t == 0 ? T_E : T_H;
+    for (int d = 0; d < 3; d++) {
+      p.present[d] = F->allocated[3 * ft + d];
+      int terms = 0;
+      int c1 = (d + 2) % 3, dir1 = (d + 1) % 3, c2 = (d + 1) % 3, dir2 = (d + 2) % 3;
+      if (S.has[dir1] && F->allocated[3 * src + c1]) terms |= 1;
+      if (S.has[dir2] && F->allocated[3 * src + c2]) terms |= 2;
+      p.terms[d] = terms;
+      if (!terms) p.present[d] = 0;
+    }
+  }
+  for (int d = 0; d < 3; d++) {
+    F->f.ecomp_present[d] = F->allocated[3 * T_E + d];
+    F->f.hcomp_present[d] = F->allocated[3 * T_H + d];
+  }
+}
+
+int alloc_component(mnl_fields *F, int c) {
+  int t = ctype(c), d = cdir(c);
+  if (F->allocated[c]) return 0;
+  double **slot = nullptr;
+  switch (t) {
+    case T_E: slot = &F->f.E[d]; break;
+    case T_D: slot = &F->f.D[d]; break;
+    case T_B: slot = &F->f.B[d]; break;
+    case T_H: slot = nullptr; break;
+  }
+  if (slot && !*slot)
+    if (dev_alloc(F, slot, F->nlocal)) return -1;
+  if (t == T_H) {
+    if (!F->f.B[d] && dev_alloc(F, &F->f.B[d], F->nlocal)) return -1;
+    if (F->pml_any[d]) {  // H separate in chunks with PML along d (src/update_eh.cpp:204-209)
+      if (dev_alloc(F, &F->f.H[d], F->nlocal)) return -1;
+      if (dev_alloc(F, &F->f.WH[d], F->nlocal)) return -1;
+    }
+  }
+  if (t == T_E && F->pml_any[d] && !F->f.WE[d])
+    if (dev_alloc(F, &F->f.WE[d], F->nlocal)) return -1;
+  if (t == T_B || t == T_D) {
+    int du = (d + 2) % 3;  // dsigu = cycle(d,2): f_u auxiliary (src/step_db.cpp:71-75)
+    double **u = t == T_B ? &F->f.UB[d] : &F->f.UD[d];
+    if (F->S.has[du] && F->pml_any[du] && !*u)
+      if (dev_alloc(F, u, F->nlocal)) return -1;
+  }
+  F->allocated[c] = true;
+  return 0;
+}
+
+int require_component(mnl_fields *F, int c) {  // src/fields.cpp:566-586
+  for (int ca = 0; ca < MNL_NUM_COMPONENTS; ca++) {
+    if (!has_field(F->S, ca) || !is_like(F->S.dim, c, ca)) continue;
+    if (alloc_component(F, ca)) return -1;
+  }
+  // polarizations: P for every allocated E comp with nontrivial sigma
+  for (int k = 0; k < F->f.npol; k++) {
+    const Lorentz &L = F->S.lor[F->S.lor.size() - 1 - k];
+    PolDev &pd = F->f.pol[k];
+    for (int d = 0; d < 3; d++)
+      if (F->allocated[d] && !L.sigma[d].empty() && pd.sigma[d] && !pd.P[d]) {
+        if (dev_alloc(F, &pd.P[d], F->nlocal)) return -1;
+        if (dev_alloc(F, &pd.Pp[d], F->nlocal)) return -1;
+      }
+  }
+  make_plans(F);
+  return 0;
+}
+
+// upload a canonical host array into a device-layout buffer of this rank
+int upload_canonical(mnl_fields *F, double *dst, const std::vector<double> &host, int comp) {
+  size_t nt = F->S.ntot;
+  if (F->scratch_cap < nt) {
+    if (F->d_scratch) hipFree(F->d_scratch);
+    HIPCHK(hipMalloc(&F->d_scratch, nt * sizeof(double)));
+    F->scratch_cap = nt;
+  }
+  HIPCHK(hipMemcpyAsync(F->d_scratch, host.data(), nt * sizeof(double), hipMemcpyHostToDevice,
+                        F->stream));
+  if (k_from_canonical(dst, F->d_scratch, F->g, ctype(comp), cdir(comp), 0, F->stream))
+    return fail("from_canonical kernel launch failed");
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+bool all_eq(const std::vector<double> &v, double x) {
+  for (double y : v)
+    if (y != x) return false;
+  return true;
+}
+
+// Is a chi1inv row entry nontrivial inside the reference chunk that covers
+// zone box (zx,zy,zz)?  Chunk array points: [io_c+shift, big_c+shift]
+// (src/anisotropic_averaging.cpp:246-296 trivial test over LOOP_OVER_VOL).
+bool nontrivial_in_zone(const mnl_structure &S, const std::vector<double> &arr, int comp,
+                        const ZoneIv *zv[3], double trivial) {
+  int lo[3], hi[3];
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) {
+      lo[d] = hi[d] = 0;
+      continue;
+    }
+    // points j with io+2j+sh in [io + c0 + sh, io + c1 + sh]  <=>  j in [c0/2, c1/2]
+    lo[d] = zv[d]->c0 / 2;
+    hi[d] = zv[d]->c1 / 2;
+  }
+  for (int x = lo[0]; x <= hi[0]; x++)
+    for (int y = lo[1]; y <= hi[1]; y++)
+      for (int z = lo[2]; z <= hi[2]; z++) {
+        long long i = x * S.cstride(0) + y * S.cstride(1) + z * S.cstride(2);
+        if (arr[i] != trivial) return true;
+      }
+  (void)comp;
+  return false;
+}
+
+int setup_materials(mnl_fields *F) {
+  const mnl_structure &S = F->S;
+  DevFields &f = F->f;
+  // Newton-Raphson needed? chi2 nontrivial and both off-diagonal rows present.
+  F->nr = false;
+  for (int c = 0; c < 3; c++) {
+    if (S.chi2[c].empty() || all_eq(S.chi2[c], 0.0)) continue;
+    int d1 = (c + 1) % 3, d2 = (c + 2) % 3;
+    if (!S.chi1inv[c][d1].empty() && !all_eq(S.chi1inv[c][d1], 0.0) &&
+        !S.chi1inv[c][d2].empty() && !all_eq(S.chi1inv[c][d2], 0.0))
+      F->nr = true;
+  }
+  bool box_eps = false;
+  for (auto &b : S.boxes) box_eps = box_eps || b.kind == 0;
+  for (int c = 0; c < 3; c++) {
+    if (!has_field(S, c)) continue;
+    const auto &diag = S.chi1inv[c][c];
+    bool need = (!diag.empty() && !all_eq(diag, 1.0)) || F->nr || box_eps;
+    if (need) {
+      double *p;
+      if (dev_alloc(F, &p, F->nlocal)) return -1;
+      if (!diag.empty()) {
+        if (upload_canonical(F, p, diag, c)) return -1;
+      } else if (k_fill(p, 1.0, F->nlocal, F->stream))
+        return fail("fill failed");
+      f.inveps[c] = p;
+    }
+    if (F->nr) {
+      for (int k = 0; k < 2; k++) {
+        int dd = (c + 1 + k) % 3;
+        const auto &od = S.chi1inv[c][dd];
+        if (od.empty()) continue;
+        double *p;
+        if (dev_alloc(F, &p, F->nlocal)) return -1;
+        if (upload_canonical(F, p, od, c)) return -1;
+        f.offd[c][k] = p;
+      }
+    }
+    if (F->nr && !S.chi2[c].empty() && !all_eq(S.chi2[c], 0.0)) {
+      double *p;
+      if (dev_alloc(F, &p, F->nlocal)) return -1;
+      if (upload_canonical(F, p, S.chi2[c], c)) return -1;
+      f.chi2[c] = p;
+    }
+  }
+  // offdiag presence per reference chunk (zone box)
+  std::vector<uint8_t> oz(27, 0);
+  if (F->nr) {
+    std::vector<ZoneIv> ivs[3];
+    for (int d = 0; d < 3; d++) {
+      if (S.has[d])
+        ivs[d] = zone_intervals(S, d);
+      else
+        ivs[d] = {{0, 0, 1}};
+    }
+    for (auto &zx : ivs[0])
+      for (auto &zy : ivs[1])
+        for (auto &zz : ivs[2]) {
+          const ZoneIv *zv[3] = {&zx, &zy, &zz};
+          int zb = zx.zone * 9 + zy.zone * 3 + zz.zone;
+          for (int c = 0; c < 3; c++)
+            for (int k = 0; k < 2; k++) {
+              int dd = (c + 1 + k) % 3;
+              const auto &od = S.chi1inv[c][dd];
+              if (!od.empty() && nontrivial_in_zone(S, od, c, zv, 0.0)) oz[zb] |= 1 << (3 * c + k);
+            }
+        }
+  }
+  uint8_t *doz;
+  if (dev_alloc(F, &doz, 27)) return -1;
+  HIPCHK(hipMemcpyAsync(doz, oz.data(), 27, hipMemcpyHostToDevice, F->stream));
+  f.offd_zone = doz;
+  f.nr_enabled = F->nr ? 1 : 0;
+  // Lorentzian susceptibilities: pol list = reverse add order
+  // (src/anisotropic_averaging.cpp:368-369, src/fields.cpp:266-282)
+  int nl = (int)S.lor.size();
+  if (nl > MAX_POL) return fail("too many susceptibilities");
+  f.npol = nl;
+  bool box_sig = false;
+  for (auto &b : S.boxes) box_sig = box_sig || b.kind == 3;
+  for (int k = 0; k < nl; k++) {
+    const Lorentz &L = S.lor[nl - 1 - k];
+    PolDev &pd = f.pol[k];
+    const double omega2pi = 2 * pi * L.omega0, g2pi = L.gamma * 2 * pi;
+    pd.omega0dtsqr = omega2pi * omega2pi * F->dt * F->dt;
+    pd.gamma1inv = 1 / (1 + g2pi * F->dt / 2);
+    pd.gamma1 = (1 - g2pi * F->dt / 2);
+    pd.omega0dtsqr_denom = L.drude ? 0 : pd.omega0dtsqr;
+    for (int d = 0; d < 3; d++) {
+      if (L.sigma[d].empty() || !has_field(S, d)) continue;
+      double *p;
+      if (dev_alloc(F, &p, F->nlocal)) return -1;
+      if (upload_canonical(F, p, L.sigma[d], d)) return -1;
+      pd.sigma[d] = p;
+    }
+    (void)box_sig;
+  }
+  // geometry boxes (device rasterisation)
+  for (auto &b : S.boxes) {
+    double lo[3] = {b.box[0], b.box[2], b.box[4]}, hi[3] = {b.box[1], b.box[3], b.box[5]};
+    for (int c = 0; c < 3; c++) {
+      if (!has_field(S, c)) continue;
+      double *dst = nullptr;
+      int invert = 0;
+      if (b.kind == 0) {
+        dst = const_cast<double *>(f.inveps[c]);
+        invert = 1;
+      } else if (b.kind == 1)
+        dst = const_cast<double *>(f.chi2[c]);
+      else if (b.kind == 3 && b.index < nl)
+        dst = const_cast<double *>(f.pol[nl - 1 - b.index].sigma[c]);
+      if (!dst) continue;
+      if (k_box_fill(dst, F->g, T_E, c, lo, hi, b.value, invert, S.a, S.io, F->stream))
+        return fail("box fill failed");
+    }
+  }
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+int upload_pml(mnl_fields *F) {
+  for (int d = 0; d < 3; d++) {
+    if (!F->S.has[d] || !F->pml_any[d]) continue;
+    size_t nq = F->h_flag[d].size();
+    uint8_t *fl, *zn;
+    double *sg, *kp, *si;
+    if (dev_alloc(F, &fl, nq) || dev_alloc(F, &zn, nq) || dev_alloc(F, &sg, nq) ||
+        dev_alloc(F, &kp, nq) || dev_alloc(F, &si, nq))
+      return -1;
+    HIPCHK(hipMemcpyAsync(fl, F->h_flag[d].data(), nq, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(zn, F->h_zone[d].data(), nq, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(sg, F->h_sig[d].data(), nq * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(kp, F->h_kap[d].data(), nq * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(si, F->h_siginv[d].data(), nq * 8, hipMemcpyHostToDevice, F->stream));
+    F->f.pml.flag[d] = fl;
+    F->f.pml.sig[d] = sg;
+    F->f.pml.kap[d] = kp;
+    F->f.pml.siginv[d] = si;
+    F->f.zone[d] = zn;
+  }
+  for (int d = 0; d < 3; d++) {  // zone tables are needed by the NR kernel everywhere
+    if (!F->S.has[d] || F->f.zone[d]) continue;
+    size_t nq = F->h_zone[d].size();
+    uint8_t *zn;
+    if (dev_alloc(F, &zn, nq)) return -1;
+    HIPCHK(hipMemcpyAsync(zn, F->h_zone[d].data(), nq, hipMemcpyHostToDevice, F->stream));
+    F->f.zone[d] = zn;
+  }
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+// ------------------------------------------------------------- sources
+// Point-source weights: loop_in_chunks for a zero-size volume
+// (src/loop_in_chunks.cpp:339-500, compute_boundary_weights 263-300) on the
+// whole cell (the chunk split of the reference gives the same weights).
+int add_point_source(mnl_fields *F, int c, int st, const double pos[3], cplx amp0) {
+  const mnl_structure &S = F->S;
+  cplx amp = amp0;
+  for (int d = 0; d < 3; d++)
+    if (S.has[d]) amp *= S.a;  // src/sources.cpp:484-487
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  double s0[3], s1[3], e0[3], e1[3];
+  for (int d = 0; d < 3; d++) {
+    s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
+    if (!S.has[d]) continue;
+    int sh = S.shift(c, d);
+    int iyee_c = 1 - sh;
+    double yee_c = 1 * (0.5 * (1.0 / S.a)) - sh * (0.5 * (1.0 / S.a));
+    double P = pos[d] + yee_c;
+    is[d] = 1 + 2 * int(floor(P * S.a - .5)) - iyee_c;
+    ie[d] = 1 + 2 * int(ceil(P * S.a - .5)) - iyee_c;
+    double w0 = 1. - pos[d] * S.a + 0.5 * is[d];
+    double w1 = 1. + pos[d] * S.a - 0.5 * ie[d];
+    s0[d] = w0, s1[d] = w1, e0[d] = w1, e1[d] = w0;
+  }
+  int isc[3], iec[3];
+  double s0c[3], s1c[3], e0c[3], e1c[3];
+  for (int d = 0; d < 3; d++) {
+    s0c[d] = s1c[d] = e0c[d] = e1c[d] = 1.0;
+    if (!S.has[d]) {
+      isc[d] = iec[d] = 0;
+      continue;
+    }
+    int sh = S.shift(c, d);
+    int uoc = S.io[d] + 2 - sh, ubo = S.io[d] + 2 * S.n[d] - sh;
+    isc[d] = std::max(is[d], uoc);
+    iec[d] = std::min(ie[d], ubo);
+    if (isc[d] > iec[d]) return 0;  // outside the cell
+    if (isc[d] == is[d]) {
+      s0c[d] = s0[d];
+      s1c[d] = s1[d];
+    } else if (isc[d] == is[d] + 2) {
+      s0c[d] = s1[d];
+    }
+    if (iec[d] == ie[d]) {
+      e0c[d] = e0[d];
+      e1c[d] = e1[d];
+    } else if (iec[d] == ie[d] - 2) {
+      e0c[d] = e1[d];
+    }
+    if (iec[d] == isc[d]) {
+      double w = std::min(s0c[d], e0c[d]);
+      s0c[d] = e0c[d] = s1c[d] = e1c[d] = w;
+    } else if (iec[d] == isc[d] + 2) {
+      double w = std::min(s0c[d], e1c[d]);
+      s0c[d] = w, e1c[d] = w;
+      w = std::min(s1c[d], e0c[d]);
+      s1c[d] = w, e0c[d] = w;
+    } else if (iec[d] == isc[d] + 4) {
+      double w = std::min(s1c[d], e1c[d]);
+      s1c[d] = w, e1c[d] = w;
+    }
+  }
+  int yd[3];
+  if (S.dim == 2)
+    yd[0] = 2, yd[1] = 0, yd[2] = 1;
+  else
+    yd[0] = 0, yd[1] = 1, yd[2] = 2;
+  int ln[3];
+  for (int k = 0; k < 3; k++) ln[k] = S.has[yd[k]] ? (iec[yd[k]] - isc[yd[k]]) / 2 + 1 : 1;
+  auto W1 = [&](int k, int i) -> double {
+    int d = yd[k], n = ln[k];
+    if (i > 1 && i < n - 2) return 1.0;
+    if (i == 0) return s0c[d];
+    if (i == 1) return s1c[d];
+    if (i == n - 1) return e0c[d];
+    if (i == n - 2) return e1c[d];
+    return 1.0;
+  };
+  SrcGroup grp;
+  grp.comp = c;
+  grp.st = st;
+  for (int i1 = 0; i1 < ln[0]; i1++)
+    for (int i2 = 0; i2 < ln[1]; i2++)
+      for (int i3 = 0; i3 < ln[2]; i3++) {
+        int p[3] = {0, 0, 0}, ii[3] = {i1, i2, i3};
+        for (int k = 0; k < 3; k++)
+          if (S.has[yd[k]]) p[yd[k]] = isc[yd[k]] + 2 * ii[k];
+        bool own = true;
+        int jg[3] = {0, 0, 0};
+        long long gi = 0;
+        for (int d = 0; d < 3; d++)
+          if (S.has[d]) {
+            int o = p[d] - S.io[d];
+            if (!(o > 0 && o <= 2 * S.n[d])) own = false;
+            jg[d] = (p[d] - S.io[d] - S.shift(c, d)) / 2;
+            gi += jg[d] * S.cstride(d);
+          }
+        if (!own) continue;
+        double wgt = (W1(2, i3) * (W1(1, i2) * ((1.0) * W1(0, i1))));
+        grp.amp.push_back(wgt * (amp * std::conj(cplx(1.0))) * cplx(1.0));
+        grp.gidx.push_back(gi);
+        for (int d = 0; d < 3; d++) grp.jglob.push_back(jg[d]);
+      }
+  if (grp.gidx.empty()) return 0;
+  for (auto &o : F->groups)  // src_vol::combinable merge (src/fields.cpp:588-597)
+    if (o.comp == grp.comp && o.st == grp.st && o.gidx == grp.gidx) {
+      for (size_t i = 0; i < o.amp.size(); i++) o.amp[i] += grp.amp[i];
+      F->src_dirty = true;
+      return 0;
+    }
+  F->groups.push_back(std::move(grp));
+  F->src_dirty = true;
+  return 0;
+}
+
+// local linear index of a global point of component c, or -1 if not owned by this rank
+long long local_index(const mnl_fields *F, int c, const int jg[3], bool include_wall) {
+  const DevGrid &g = F->g;
+  long long li = 0;
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    int j = jg[d] - g.off[d];
+    int sh = F->S.shift(c, d);
+    int lo = sh ? g.owned_lo_sh[d] : g.owned_lo_un[d];
+    int hi = sh ? g.owned_hi_sh[d] : g.owned_hi_un[d];
+    if (include_wall && !sh && jg[d] == g.nglob[d] && j >= 0 && j < g.N[g.ax[d]]) hi = j;
+    if (j < lo || j > hi) return -1;
+    li += (long long)j * g.st[g.ax[d]];
+  }
+  return li;
+}
+
+int build_source_lists(mnl_fields *F) {
+  F->srcB_idx.clear(), F->srcD_idx.clear(), F->isrc_idx.clear();
+  F->srcB_comp.clear(), F->srcD_comp.clear(), F->isrc_comp.clear();
+  F->srcB_ref.clear(), F->srcD_ref.clear(), F->isrc_ref.clear();
+  for (size_t gi = 0; gi < F->groups.size(); gi++) {
+    const SrcGroup &G = F->groups[gi];
+    const SrcTime &st = F->srcs[G.st];
+    int c = G.comp;
+    bool mag = ctype(c) == T_H;
+    for (size_t j = 0; j < G.gidx.size(); j++) {
+      const int *jg = &G.jglob[3 * j];
+      int tgt = mag ? 3 * T_B + cdir(c) : 3 * T_D + cdir(c);
+      long long li = local_index(F, tgt, jg, false);
+      if (li < 0) continue;
+      if (st.is_integrated && !mag) {
+        F->isrc_idx.push_back(li);
+        F->isrc_comp.push_back(cdir(c));
+        F->isrc_ref.push_back({(int)gi, (int)j});
+      } else if (!st.is_integrated) {
+        auto &I = mag ? F->srcB_idx : F->srcD_idx;
+        auto &C = mag ? F->srcB_comp : F->srcD_comp;
+        auto &R = mag ? F->srcB_ref : F->srcD_ref;
+        I.push_back(li);
+        C.push_back(cdir(c));
+        R.push_back({(int)gi, (int)j});
+      }
+    }
+  }
+  if (F->isrc_idx.size() > (size_t)MAX_ISRC)
+    return fail("too many integrated source points (max 64)");
+  auto up = [&](long long **dI, int **dC, const std::vector<long long> &I,
+                const std::vector<int> &C) -> int {
+    if (I.empty()) return 0;
+    if (dev_alloc(F, dI, I.size(), false) || dev_alloc(F, dC, C.size(), false)) return -1;
+    HIPCHK(hipMemcpyAsync(*dI, I.data(), I.size() * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(*dC, C.data(), C.size() * 4, hipMemcpyHostToDevice, F->stream));
+    return 0;
+  };
+  if (up(&F->d_srcB_idx, &F->d_srcB_comp, F->srcB_idx, F->srcB_comp)) return -1;
+  if (up(&F->d_srcD_idx, &F->d_srcD_comp, F->srcD_idx, F->srcD_comp)) return -1;
+  F->src_dirty = false;
+  return 0;
+}
+
+// ------------------------------------------------------------- interpolation
+inline int my_round(double x) { return int(floor(fabs(x) + 0.5) * (x < 0 ? -1 : 1)); }
+
+void interpolate(const mnl_structure &S, int c, const double pc[3], int locs[8][3], double w[8]) {
+  const double SMALL = 1e-13;
+  double p[3] = {0, 0, 0}, midv[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
+  int middle[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    double ys = S.shift(c, d) * (0.5 * (1.0 / S.a));
+    p[d] = (pc[d] - ys) * S.a;
+    middle[d] = ((int)floor(p[d])) * 2 + 1 + S.shift(c, d);
+    midv[d] = middle[d] * (0.5 * (1.0 / S.a));
+    dv[d] = (pc[d] - midv[d]) * (2 * S.a);
+  }
+  int already = 1;
+  for (int i = 0; i < 8; i++) {
+    for (int d = 0; d < 3; d++) locs[i][d] = S.has[d] ? my_round(midv[d] * 2 * S.a) : 0;
+    w[i] = 1.0;
+  }
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    for (int i = 0; i < already; i++) {
+      for (int e = 0; e < 3; e++) locs[already + i][e] = locs[i][e];
+      w[already + i] = w[i];
+      locs[i][d] = middle[d] - 1;
+      w[i] *= 0.5 * (1.0 - dv[d]);
+      locs[already + i][d] = middle[d] + 1;
+      w[already + i] *= 0.5 * (1.0 + dv[d]);
+    }
+    already *= 2;
+  }
+  for (int i = already; i < 8; i++) w[i] = 0.0;
+  double total = 0.0;
+  for (int i = 0; i < already; i++) total += w[i];
+  for (int i = 0; i < already; i++) w[i] += (1.0 - total) * (1.0 / already);
+  for (int i = 0; i < already; i++) {
+    if (w[i] < 0.0 || w[i] < SMALL) w[i] = 0.0;
+  }
+  int l = already, off = 0;
+  while (l) {
+    if (fabs(w[off]) < 2e-15) {
+      w[off] = w[off + l - 1];
+      for (int e = 0; e < 3; e++) locs[off][e] = locs[off + l - 1][e];
+      w[off + l - 1] = 0.0;
+      for (int e = 0; e < 3; e++) locs[off + l - 1][e] = 0;
+    } else
+      off += 1;
+    l -= 1;
+  }
+  bool all_same = true;
+  for (int i = 0; i < 8 && w[i]; i++)
+    if (w[i] != w[0]) all_same = false;
+  if (all_same) {
+    int nw = 0;
+    for (int i = 0; i < 8 && w[i]; i++) nw++;
+    for (int i = 0; i < 8 && w[i]; i++) w[i] = 1.0 / nw;
+  }
+}
+
+// value of component c at absolute half-coords p (0 if not owned by this rank)
+int value_at(mnl_fields *F, int c, const int p[3], double *out) {
+  const mnl_structure &S = F->S;
+  *out = 0.0;
+  int jg[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++)
+    if (S.has[d]) {
+      int o = p[d] - S.io[d];
+      if (!(o > 0 && o <= 2 * S.n[d])) return 0;  // not owned by the cell
+      jg[d] = (p[d] - S.io[d] - S.shift(c, d)) / 2;
+    }
+  if (!F->allocated[c]) return 0;
+  long long li = local_index(F, c, jg, true);
+  if (li < 0) return 0;
+  int t = ctype(c), d = cdir(c);
+  const double *src = nullptr;
+  switch (t) {
+    case T_E: src = F->f.E[d]; break;
+    case T_D: src = F->f.D[d]; break;
+    case T_B: src = F->f.B[d]; break;
+    case T_H: {
+      src = F->f.B[d];
+      if (F->f.H[d] && S.has[d]) {
+        int q = 2 * jg[d];
+        if (F->h_flag[d][q]) src = F->f.H[d];
+      }
+      break;
+    }
+  }
+  if (!src) return 0;
+  HIPCHK(hipStreamSynchronize(F->stream));
+  HIPCHK(hipMemcpy(out, src + li, sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int get_field(mnl_fields *F, int c, const double pos[3], double *out, bool reduce) {
+  int locs[8][3];
+  double w[8];
+  double pp[3] = {pos[0], pos[1], pos[2]};
+  if (F->S.dim == 1) pp[0] = pp[1] = 0;
+  if (F->S.dim == 2) pp[2] = 0;
+  interpolate(F->S, c, pp, locs, w);
+  cplx res = 0.0;
+  for (int i = 0; i < 8 && w[i]; i++) {
+    double v;
+    if (value_at(F, c, locs[i], &v)) return -1;
+    res += w[i] * cplx(v);
+  }
+  double r = real(res);
+  if (reduce && F->nranks > 1) {
+    if (F->comm->allreduce_sum(&r, 1, F->stream)) return fail("allreduce failed");
+  }
+  *out = r;
+  return 0;
+}
+
+// ------------------------------------------------------------- halo exchange
+// step_boundaries replacement for the slab decomposition (src/step.cpp:226-288):
+// kind 0 (before curl B): E comps unshifted along the slab axis need the low
+//   ghost plane (local 0) <- rank-1's top owned plane (local nloc).
+// kind 1 (before curl D): B (and separate H) comps shifted along the slab axis
+//   need the high ghost plane (local nloc) <- rank+1's first plane (local 0).
+// kind 2 (before NR E update): D comps (and Lorentz P), both directions.
+int exchange(mnl_fields *F, int kind) {
+  const DevGrid &g = F->g;
+  const int sd = F->slab_dir, ax = g.ax[sd];
+  const size_t plane = (size_t)g.st[ax];
+  const int nloc = g.N[ax] - 1;
+  const int up = F->rank + 1 < F->nranks ? F->rank + 1 : -1;
+  const int dn = F->rank > 0 ? F->rank - 1 : -1;
+  struct Item {
+    double *p;
+    bool low_ghost;  // true: send top plane up, receive plane 0 from below
+  };
+  std::vector<Item> items;
+  for (int c = 0; c < 3; c++) {
+    if (kind == 0) {
+      if (c != sd && F->f.E[c] && F->allocated[c]) items.push_back({F->f.E[c], true});
+    } else if (kind == 1) {
+      if (c != sd && F->f.B[c] && F->allocated[3 * T_H + c]) {
+        items.push_back({F->f.B[c], false});
+        if (F->f.H[c]) items.push_back({F->f.H[c], false});
+      }
+    } else {
+      if (F->f.D[c] && F->allocated[3 * T_D + c]) items.push_back({F->f.D[c], c != sd});
+      for (int k = 0; k < F->f.npol; k++)
+        if (F->f.pol[k].P[c]) items.push_back({F->f.pol[k].P[c], c != sd});
+    }
+  }
+  if (items.empty()) return 0;
+  Comm &cm = *F->comm;
+  if (cm.group_start()) return -1;
+  for (auto &it : items) {
+    if (it.low_ghost) {
+      if (up >= 0 && cm.send(it.p + (size_t)nloc * plane, plane, up, F->stream)) return -1;
+      if (dn >= 0 && cm.recv(it.p, plane, dn, F->stream)) return -1;
+    } else {
+      if (dn >= 0 && cm.send(it.p, plane, dn, F->stream)) return -1;
+      if (up >= 0 && cm.recv(it.p + (size_t)nloc * plane, plane, up, F->stream)) return -1;
+    }
+  }
+  return cm.group_end();
+}
+
+// ------------------------------------------------------------- stepping
+enum { TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT };
+
+struct EvPair {
+  hipEvent_t a, b;
+  int cat;
+};
+
+int step_batch(mnl_fields *F, int nsteps) {
+  if (F->src_dirty && build_source_lists(F)) return -1;
+  const double dt = F->dt;
+  // per-step source values, computed on the host exactly as the reference
+  size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
+  size_t per = nB + nD + nI;
+  const int CH = 1024;
+  std::vector<EvPair> evs;
+  size_t evi = 0;
+  auto ev_begin = [&](int cat) -> int {
+    if (!F->profiling) return -1;
+    while (F->ev_pool.size() < 2 * (evi + 1)) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return -1;
+      F->ev_pool.push_back(e);
+    }
+    EvPair p{F->ev_pool[2 * evi], F->ev_pool[2 * evi + 1], cat};
+    hipEventRecord(p.a, F->stream);
+    evs.push_back(p);
+    evi++;
+    return (int)evs.size() - 1;
+  };
+  auto ev_end = [&](int k) {
+    if (k >= 0) hipEventRecord(evs[k].b, F->stream);
+  };
+  auto flush_events = [&]() -> int {
+    if (!F->profiling || evs.empty()) return 0;
+    HIPCHK(hipStreamSynchronize(F->stream));
+    for (auto &p : evs) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, p.a, p.b);
+      F->timer_ms[p.cat] += ms;
+      F->timer_count[p.cat] += 1;
+    }
+    evs.clear();
+    evi = 0;
+    return 0;
+  };
+  for (int s0 = 0; s0 < nsteps; s0 += CH) {
+    int ns = std::min(CH, nsteps - s0);
+    if (per) {
+      std::vector<double> vals((size_t)ns * per);
+      for (int s = 0; s < ns; s++) {
+        long long tt = F->t + s;
+        double time = tt * dt;
+        double *vB = &vals[(size_t)s * per], *vD = vB + nB, *vI = vD + nD;
+        for (auto &st : F->srcs) st.update(time, dt);  // calc_sources(time())
+        for (size_t k = 0; k < nB; k++) {
+          const SrcGroup &G = F->groups[F->srcB_ref[k].first];
+          const cplx A = (G.amp[F->srcB_ref[k].second] * F->srcs[G.st].cur_current) * dt;
+          vB[k] = real(A);
+        }
+        for (auto &st : F->srcs) st.update(time + 0.5 * dt, dt);
+        for (size_t k = 0; k < nD; k++) {
+          const SrcGroup &G = F->groups[F->srcD_ref[k].first];
+          const cplx A = (G.amp[F->srcD_ref[k].second] * F->srcs[G.st].cur_current) * dt;
+          vD[k] = real(A);
+        }
+        for (auto &st : F->srcs) st.update(time + dt, dt);
+        for (size_t k = 0; k < nI; k++) {
+          const SrcGroup &G = F->groups[F->isrc_ref[k].first];
+          const cplx A = G.amp[F->isrc_ref[k].second] * F->srcs[G.st].cur_dipole;
+          vI[k] = real(A);
+        }
+      }
+      size_t bytes = vals.size() * sizeof(double);
+      if (F->d_vals_cap < vals.size()) {
+        HIPCHK(hipStreamSynchronize(F->stream));
+        if (F->d_vals) hipFree(F->d_vals);
+        HIPCHK(hipMalloc(&F->d_vals, bytes));
+        F->d_vals_cap = vals.size();
+      }
+      HIPCHK(hipMemcpyAsync(F->d_vals, vals.data(), bytes, hipMemcpyHostToDevice, F->stream));
+      HIPCHK(hipStreamSynchronize(F->stream));  // vals is a host temporary
+    }
+    for (int s = 0; s < ns; s++) {
+      DevFields &f = F->f;
+      const DevGrid &g = F->g;
+      SrcDev sB{(int)nB, F->d_srcB_idx, F->d_srcB_comp, F->d_vals};
+      SrcDev sD{(int)nD, F->d_srcD_idx, F->d_srcD_comp, F->d_vals + nB};
+      ISrcDev is;
+      is.n = (int)nI;
+      for (size_t k = 0; k < nI; k++) is.idx[k] = F->isrc_idx[k], is.comp[k] = F->isrc_comp[k];
+      is.val = F->d_vals + nB + nD;
+      // per-step tables are strided by `per`: encode via pointer offset + stride trick
+      // (kernels index val[step*n + k]; use a dedicated stride by shifting base per step)
+      sB.val = F->d_vals + (size_t)s * per;
+      sD.val = F->d_vals + (size_t)s * per + nB;
+      is.val = F->d_vals + (size_t)s * per + nB + nD;
+      // ---- B: halo of E (low ghost), curl, sources
+      if (F->nranks > 1) {
+        int k = ev_begin(TM_HALO);
+        if (exchange(F, 0)) return fail("E halo exchange failed");
+        ev_end(k);
+      }
+      int k = ev_begin(TM_BINT);
+      if (k_curl(T_B, false, F->interior, g, f, F->planB, F->S.courant, F->stream))
+        return fail("curl B launch failed");
+      ev_end(k);
+      k = ev_begin(TM_B);
+      for (auto &b : F->shell)
+        if (k_curl(T_B, true, b, g, f, F->planB, F->S.courant, F->stream))
+          return fail("curl B launch failed");
+      ev_end(k);
+      if (nB && k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
+      // ---- H
+      k = ev_begin(TM_H);
+      bool anyH = false;
+      for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
+      if (anyH)
+        for (auto &b : F->shell)
+          if (k_update_h(b, g, f, F->stream)) return fail("update H launch failed");
+      ev_end(k);
+      if (F->nranks > 1) {
+        int kk = ev_begin(TM_HALO);
+        if (exchange(F, 1)) return fail("H halo exchange failed");
+        ev_end(kk);
+      }
+      // ---- D
+      k = ev_begin(TM_DINT);
+      if (k_curl(T_D, false, F->interior, g, f, F->planD, F->S.courant, F->stream))
+        return fail("curl D launch failed");
+      ev_end(k);
+      k = ev_begin(TM_D);
+      for (auto &b : F->shell)
+        if (k_curl(T_D, true, b, g, f, F->planD, F->S.courant, F->stream))
+          return fail("curl D launch failed");
+      ev_end(k);
+      if (nD && k_source(T_D, g, f, sD, 0, F->stream)) return fail("source launch failed");
+      if (F->nr && F->nranks > 1) {
+        if (exchange(F, 2)) return fail("D halo exchange failed");
+      }
+      // ---- E (+ Lorentzian P)
+      k = ev_begin(TM_E);
+      bool fuse = !F->nr;
+      if (k_update_e(false, F->interior, g, f, is, 0, fuse, F->stream))
+        return fail("update E launch failed");
+      for (auto &b : F->shell)
+        if (k_update_e(true, b, g, f, is, 0, fuse, F->stream)) return fail("update E launch failed");
+      if (!fuse && f.npol) {
+        if (k_update_pols(F->interior, g, f, F->stream)) return fail("pols launch failed");
+        for (auto &b : F->shell)
+          if (k_update_pols(b, g, f, F->stream)) return fail("pols launch failed");
+      }
+      ev_end(k);
+    }
+    F->t += ns;
+    if (flush_events() != 0) return -1;
+  }
+  HIPCHK(hipStreamSynchronize(F->stream));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int nan_check(mnl_fields *F) {
+  // fields::step: abort if get_field(D_EnergyDensity, center) is not finite
+  // (src/step.cpp:138-139, src/monitor.cpp:96-113)
+  const mnl_structure &S = F->S;
+  double cen[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++)
+    if (S.has[d]) {
+      int n = S.n[d] - (S.n[d] & 1);
+      cen[d] = (S.io[d] + n) * (0.5 * (1.0 / S.a));
+    }
+  double sum = 0;
+  for (int d = 0; d < 3; d++) {
+    if (!F->allocated[d] || !F->allocated[3 * T_D + d]) continue;
+    double e, dd;
+    if (get_field(F, d, cen, &e, true) || get_field(F, 3 * T_D + d, cen, &dd, true)) return -1;
+    sum += real(std::conj(cplx(e)) * cplx(dd));
+  }
+  if (!std::isfinite(sum * 0.5)) return fail("simulation fields are NaN or Inf");
+  return 0;
+}
+
+int finalize_fields(mnl_fields *F) {
+  if (build_pml_tables(F)) return -1;
+  setup_grid(F);
+  if (upload_pml(F)) return -1;
+  if (setup_materials(F)) return -1;
+  setup_boxes(F);
+  if (dev_alloc(F, &F->d_nr_fallbacks, 1)) return -1;
+  F->f.nr_fallbacks = F->d_nr_fallbacks;
+  make_plans(F);
+  return 0;
+}
+
+mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, const void *id) {
+  if (!s) {
+    fail("null structure");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    fail("no HIP device available (the MI355X path has no CPU fallback)");
+    return nullptr;
+  }
+  std::unique_ptr<mnl_fields> F(new mnl_fields());
+  F->S = *s;
+  F->dt = s->dt;
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) device = 0;
+  }
+  if (device >= ndev) {
+    fail("device index out of range");
+    return nullptr;
+  }
+  F->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&F->stream, hipStreamNonBlocking) != hipSuccess) {
+    fail("cannot create HIP stream");
+    return nullptr;
+  }
+  memset(&F->f, 0, sizeof(F->f));
+  F->rank = rank;
+  F->nranks = nranks;
+  if (nranks > 1) {
+    F->comm.reset(new Comm());
+    if (F->comm->init(rank, nranks, id)) {
+      fail("RCCL communicator init failed");
+      return nullptr;
+    }
+  }
+  if (finalize_fields(F.get())) return nullptr;
+  return F.release();
+}
+
+int check_comp(int c) {
+  if (c < 0 || c >= MNL_NUM_COMPONENTS) return fail("invalid component");
+  return 0;
+}
+
+}  // namespace
+
+// =============================================================== C ABI
+extern "C" {
+
+const char *mnl_last_error(void) { return g_err.c_str(); }
+int mnl_version(void) { return 100; }
+
+int mnl_device_count(int *count) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return 0;
+}
+
+mnl_structure *mnl_structure_create(int dim, const int n[3], double a, double courant,
+                                    const int io[3]) {
+  if (dim < 1 || dim > 3) {
+    fail("dim must be 1, 2 or 3");
+    return nullptr;
+  }
+  if (!(a > 0) || !(courant > 0)) {
+    fail("resolution and Courant must be positive");
+    return nullptr;
+  }
+  mnl_structure *s = new mnl_structure();
+  s->dim = dim;
+  s->has[0] = dim >= 2;
+  s->has[1] = dim >= 2;
+  s->has[2] = dim != 2;
+  for (int d = 0; d < 3; d++) {
+    s->n[d] = s->has[d] ? n[d] : 0;
+    s->io[d] = s->has[d] ? io[d] : 0;
+    if (s->has[d] && s->n[d] < 2) {
+      delete s;
+      fail("need at least 2 cells along every present direction");
+      return nullptr;
+    }
+    for (int k = 0; k < 2; k++) s->pml_R[d][k] = 1e-15, s->pml_stretch[d][k] = 1.0;
+  }
+  s->a = a;
+  s->courant = courant;
+  s->dt = courant / a;  // src/structure.cpp:110
+  s->ntot = 1;
+  for (int d = 0; d < 3; d++)
+    if (s->has[d]) s->ntot *= size_t(s->n[d] + 1);
+  return s;
+}
+
+void mnl_structure_destroy(mnl_structure *s) { delete s; }
+
+int mnl_structure_add_pml(mnl_structure *s, int dir, int side, double thickness, double R,
+                          double mean_stretch) {
+  if (!s || dir < 0 || dir > 2 || side < 0 || side > 1) return fail("bad pml direction/side");
+  if (thickness < 0) return fail("invalid boundary absorbers for this grid_volume");
+  if (!s->has[dir]) return 0;
+  s->pml_thick[dir][side] = thickness;
+  s->pml_R[dir][side] = R;
+  s->pml_stretch[dir][side] = mean_stretch;
+  return 0;
+}
+
+int mnl_structure_set_chi1inv(mnl_structure *s, int comp, int dir, const double *host) {
+  if (!s || comp < MNL_EX || comp > MNL_EZ || dir < 0 || dir > 2)
+    return fail("chi1inv: E components only");
+  if (host)
+    s->chi1inv[comp][dir].assign(host, host + s->ntot);
+  else
+    s->chi1inv[comp][dir].clear();
+  return 0;
+}
+int mnl_structure_set_chi2(mnl_structure *s, int comp, const double *host) {
+  if (!s || comp < MNL_EX || comp > MNL_EZ) return fail("chi2: E components only");
+  s->chi2[comp].assign(host, host + s->ntot);
+  return 0;
+}
+int mnl_structure_set_chi3(mnl_structure *s, int comp, const double *host) {
+  if (!s || comp < MNL_EX || comp > MNL_EZ) return fail("chi3: E components only");
+  s->chi3[comp].assign(host, host + s->ntot);  // inert in the fork
+  return 0;
+}
+int mnl_structure_add_lorentzian(mnl_structure *s, double omega0, double gamma, int drude,
+                                 const double *sx, const double *sy, const double *sz) {
+  if (!s) return fail("null structure");
+  if ((int)s->lor.size() >= MAX_POL) return fail("too many susceptibilities (max 4)");
+  Lorentz L;
+  L.omega0 = omega0;
+  L.gamma = gamma;
+  L.drude = drude;
+  const double *sv[3] = {sx, sy, sz};
+  for (int d = 0; d < 3; d++)
+    if (sv[d]) {
+      L.sigma[d].assign(sv[d], sv[d] + s->ntot);
+      if (all_eq(L.sigma[d], 0.0)) L.sigma[d].clear();
+    }
+  s->lor.push_back(std::move(L));
+  return 0;
+}
+int mnl_structure_set_box(mnl_structure *s, int kind, int index, const double box[6],
+                          double value) {
+  if (!s || kind < 0 || kind > 3) return fail("bad box kind");
+  BoxSpec b;
+  b.kind = kind;
+  b.index = index;
+  memcpy(b.box, box, sizeof(b.box));
+  b.value = value;
+  if (kind == 3) {  // make sure the susceptibility has a sigma array to fill
+    if (index < 0 || index >= (int)s->lor.size()) return fail("box: no such susceptibility");
+    for (int d = 0; d < 3; d++)
+      if (s->lor[index].sigma[d].empty()) s->lor[index].sigma[d].assign(s->ntot, 0.0);
+  }
+  if (kind == 1) {
+    for (int d = 0; d < 3; d++)
+      if (s->chi2[d].empty()) s->chi2[d].assign(s->ntot, 0.0);
+  }
+  s->boxes.push_back(b);
+  return 0;
+}
+
+mnl_fields *mnl_fields_create(mnl_structure *s, int device) {
+  return create_common(s, device, 0, 1, nullptr);
+}
+mnl_fields *mnl_fields_create_dist(mnl_structure *s, int device, int rank, int nranks,
+                                   const void *id) {
+  if (nranks < 1 || rank < 0 || rank >= nranks) {
+    fail("bad rank/nranks");
+    return nullptr;
+  }
+  return create_common(s, device, rank, nranks, id);
+}
+int mnl_comm_unique_id(void *out128) { return Comm::unique_id(out128) ? fail("ncclGetUniqueId failed") : 0; }
+
+void mnl_fields_destroy(mnl_fields *f) { delete f; }
+
+int mnl_fields_add_point_source(mnl_fields *F, int comp, int kind, const double *p, int np,
+                                const double pos[3], double amp_re, double amp_im,
+                                int is_integrated) {
+  if (!F || check_comp(comp)) return -1;
+  if (!(ctype(comp) == T_E || ctype(comp) == T_H)) return fail("sources must be E or H components");
+  if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  SrcTime st;
+  if (kind == MNL_SRC_GAUSSIAN) {
+    if (np < 4) return fail("gaussian source needs 4 parameters");
+    // gaussian_src_time(f, w, st, et) (src/sources.cpp:85-96)
+    st.kind = 0;
+    st.freq = p[0];
+    st.width = p[1];
+    st.peak_time = 0.5 * (p[2] + p[3]);
+    st.cutoff = (p[3] - p[2]) * 0.5;
+    while (exp(-st.cutoff * st.cutoff / (2 * st.width * st.width)) < 1e-100) st.cutoff *= 0.9;
+    st.cutoff = float(st.cutoff);
+  } else if (kind == MNL_SRC_CONTINUOUS) {
+    if (np < 6) return fail("continuous source needs 6 parameters");
+    st.kind = 1;
+    st.cfreq = cplx(p[0], p[1]);
+    st.cwidth = p[2];
+    st.start_time = float(p[3]);
+    st.end_time = float(p[4]);
+    st.slowness = p[5];
+  } else
+    return fail("unknown source kind");
+  st.is_integrated = is_integrated != 0;
+  int idx = -1;
+  for (size_t i = 0; i < F->srcs.size(); i++)
+    if (F->srcs[i].same(st)) idx = (int)i;
+  if (idx < 0) {
+    F->srcs.push_back(st);
+    idx = (int)F->srcs.size() - 1;
+  }
+  if (require_component(F, comp)) return -1;
+  double pp[3] = {pos[0], pos[1], pos[2]};
+  if (F->S.dim == 1) pp[0] = pp[1] = 0;
+  if (F->S.dim == 2) pp[2] = 0;
+  return add_point_source(F, comp, idx, pp, cplx(amp_re, amp_im));
+}
+
+int mnl_fields_require_component(mnl_fields *F, int comp) {
+  if (!F || check_comp(comp)) return -1;
+  if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  return require_component(F, comp);
+}
+
+int mnl_fields_step(mnl_fields *F, int nsteps) {
+  if (!F) return fail("null fields");
+  if (nsteps <= 0) return 0;
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  if (step_batch(F, nsteps)) return -1;
+  return nan_check(F);
+}
+
+int mnl_fields_time(mnl_fields *F, long long *t, double *dt) {
+  if (!F) return fail("null fields");
+  if (t) *t = F->t;
+  if (dt) *dt = F->dt;
+  return 0;
+}
+
+int mnl_fields_get_field(mnl_fields *F, int comp, const double pos[3], double *out) {
+  if (!F || check_comp(comp)) return -1;
+  if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  return get_field(F, comp, pos, out, true);
+}
+
+size_t mnl_fields_ntot(mnl_fields *F) { return F ? F->S.ntot : 0; }
+
+int mnl_fields_copy_component(mnl_fields *F, int comp, double *host, size_t n) {
+  if (!F || check_comp(comp)) return -1;
+  if (n < F->S.ntot) return fail("output buffer too small");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  memset(host, 0, F->S.ntot * sizeof(double));
+  if (!has_field(F->S, comp) || !F->allocated[comp]) return 0;
+  int t = ctype(comp), d = cdir(comp);
+  const double *src = nullptr, *hsep = nullptr;
+  switch (t) {
+    case T_E: src = F->f.E[d]; break;
+    case T_D: src = F->f.D[d]; break;
+    case T_B: src = F->f.B[d]; break;
+    case T_H:
+      src = F->f.B[d];
+      hsep = F->f.H[d];
+      break;
+  }
+  if (!src) return 0;
+  size_t nt = F->S.ntot;
+  if (F->scratch_cap < nt) {
+    if (F->d_scratch) hipFree(F->d_scratch);
+    HIPCHK(hipMalloc(&F->d_scratch, nt * sizeof(double)));
+    F->scratch_cap = nt;
+  }
+  HIPCHK(hipMemsetAsync(F->d_scratch, 0, nt * sizeof(double), F->stream));
+  if (k_to_canonical(F->d_scratch, src, hsep, F->g, t, d, F->f, F->stream))
+    return fail("to_canonical launch failed");
+  HIPCHK(hipMemcpyAsync(host, F->d_scratch, nt * sizeof(double), hipMemcpyDeviceToHost, F->stream));
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+int mnl_fields_timers(mnl_fields *F, double out[6]) {
+  if (!F) return fail("null fields");
+  out[0] = F->timer_ms[TM_B] + F->timer_ms[TM_BINT];
+  out[1] = F->timer_ms[TM_H];
+  out[2] = F->timer_ms[TM_D] + F->timer_ms[TM_DINT];
+  out[3] = F->timer_ms[TM_E];
+  out[4] = F->timer_ms[TM_SRC];
+  out[5] = F->timer_ms[TM_HALO];
+  return 0;
+}
+
+int mnl_fields_nr_fallbacks(mnl_fields *F, long long *count) {
+  if (!F) return fail("null fields");
+  unsigned long long v = 0;
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  HIPCHK(hipMemcpy(&v, F->d_nr_fallbacks, sizeof(v), hipMemcpyDeviceToHost));
+  *count = (long long)v;
+  return 0;
+}
+
+int mnl_fields_set_profiling(mnl_fields *F, int on) {
+  if (!F) return fail("null fields");
+  F->profiling = on != 0;
+  for (int k = 0; k < 8; k++) F->timer_ms[k] = 0, F->timer_count[k] = 0;
+  return 0;
+}
+
+int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, double *total_ms,
+                            double *bytes_per_launch) {
+  if (!F || which < 0 || which > 1) return fail("bad kernel id");
+  int cat = which == 0 ? TM_BINT : TM_DINT;
+  *launches = F->timer_count[cat];
+  *total_ms = F->timer_ms[cat];
+  // algorithmic bytes of the interior curl: read 3 source comps + read/write 3
+  // updated comps per owned point (DESIGN.md "Roofline")
+  double pts = 1;
+  for (int k = 0; k < 3; k++) pts *= double(F->interior.hi[k] - F->interior.lo[k] + 1);
+  if (F->interior.hi[0] < F->interior.lo[0]) pts = 0;
+  int ncomp = 0;
+  const CurlPlan &p = which == 0 ? F->planB : F->planD;
+  for (int d = 0; d < 3; d++) ncomp += p.present[d] ? 1 : 0;
+  int nsrc = 0;
+  for (int d = 0; d < 3; d++) nsrc += F->allocated[3 * (which == 0 ? T_E : T_H) + d] ? 1 : 0;
+  *bytes_per_launch = pts * 8.0 * (nsrc + 2 * ncomp);
+  return 0;
+}
+
+int mnl_fields_traffic_model(mnl_fields *F, double *bpc, double *cells) {
+  if (!F) return fail("null fields");
+  // minimal per-step traffic of the unfused sub-step kernels in the interior:
+  // curl B: E(3) + B(3) read, B(3) written; curl D: H=B(3) + D(3) read, D(3)
+  // written; E update: D(3) (+eps^-1 3) read, E(3) written (+P terms).
+  double n = 0;
+  for (int d = 0; d < 3; d++) n += F->allocated[d] ? 1 : 0;
+  double b = 8.0 * (3 * n) * 2 + 8.0 * (2 * n);
+  for (int d = 0; d < 3; d++)
+    if (F->f.inveps[d]) b += 8.0;
+  for (int k = 0; k < F->f.npol; k++)
+    for (int d = 0; d < 3; d++)
+      if (F->f.pol[k].P[d]) b += 8.0 * 5;
+  *bpc = b;
+  double c = 1;
+  for (int d = 0; d < 3; d++)
+    if (F->S.has[d]) {
+      if (d == F->slab_dir && F->nranks > 1)
+        c *= double(F->g.owned_hi_sh[d] - F->g.owned_lo_sh[d] + 1);
+      else
+        c *= F->S.n[d];
+    }
+  *cells = c;
+  return 0;
+}
+
+}  // extern "C"

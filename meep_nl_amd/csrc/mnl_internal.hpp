@@ -1,0 +1,123 @@
+// mnl_internal.hpp -- plain-data structures shared by the host orchestration
+// (mnl_host.cpp, built with g++) and the HIP kernels (mnl_kernels.hip, built
+// with hipcc for gfx950).  No HIP types appear here so both compilers agree
+// on the layout.
+//
+// Data layout in HBM (DESIGN.md "Layout"): one structure-of-arrays fp64
+// buffer per field component over the rank-local index box
+// [0,N0) x [0,N1) x [0,N2), device axis 0 fastest.  Axis k is the k-th present
+// direction in X,Y,Z order, so in 3-D X is contiguous and Z is the slab /
+// plane axis (a ghost plane is one contiguous block for the halo exchange).
+// Axis-0 rows are padded to a multiple of 16 doubles (128 B lines).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace mnl {
+
+constexpr int MAX_POL = 4;    // Lorentzian susceptibilities per structure
+constexpr int MAX_ISRC = 64;  // integrated-source points handled inside the E kernel
+constexpr int MAX_BOX = 7;    // interior + 6 shell boxes
+
+enum { T_E = 0, T_H = 1, T_D = 2, T_B = 3 };
+
+struct Box {
+  int lo[3];  // inclusive local index bounds per device axis
+  int hi[3];
+};
+
+struct DevGrid {
+  int dim;
+  int ax[3];            // device axis of direction X,Y,Z (-1 = absent)
+  int N[3];             // local points per device axis
+  long long st[3];      // strides per device axis (st[0] = 1)
+  long long sdir[3];    // stride per direction X,Y,Z (0 if absent)
+  int off[3];           // global index of local index 0, per direction
+  int nglob[3];         // global cells per direction
+  int wall[3];          // 1: metallic wall plane (global index n) excluded from updates
+  int owned_lo_sh[3];   // per direction: local owned range of shifted components
+  int owned_hi_sh[3];
+  int owned_lo_un[3];   // ... of unshifted components (wall excluded)
+  int owned_hi_un[3];
+};
+
+// Which neighbours enter each curl update (src/fields.cpp:438-471 plan with
+// the NULL-pointer swap of step_curl, src/step_generic.cpp:76-80).
+// terms: bit0 = g1 term (comp (d+2)%3 along dir (d+1)%3), bit1 = g2 term
+// (comp (d+1)%3 along dir (d+2)%3).  present = component allocated.
+struct CurlPlan {
+  int present[3];
+  int terms[3];
+};
+
+struct PmlDev {
+  const uint8_t *flag[3];  // per direction, indexed by global half-coordinate q
+  const double *sig[3];
+  const double *kap[3];
+  const double *siginv[3];
+};
+
+struct PolDev {
+  double gamma1inv, gamma1, omega0dtsqr, omega0dtsqr_denom;
+  double *P[3];
+  double *Pp[3];
+  const double *sigma[3];
+};
+
+struct DevFields {
+  double *E[3], *D[3], *B[3], *H[3];
+  double *UB[3], *UD[3], *WE[3], *WH[3];
+  const double *inveps[3];   // diagonal chi1inv of E comps (null = trivial)
+  const double *offd[3][2];  // chi1inv[ec][cycle(d,1)], [cycle(d,2)] (null = absent)
+  const double *chi2[3];
+  int npol;
+  PolDev pol[MAX_POL];       // in reference pol-list order (reverse of add order)
+  PmlDev pml;
+  int ecomp_present[3];
+  int hcomp_present[3];
+  int nr_enabled;
+  // per zone box (3x3x3 over X,Y,Z zones lo/mid/hi): bit (3*c + k) set if
+  // chi1inv[Ec][cycle(c,k+1)] is allocated (non-trivial) in that chunk.
+  const uint8_t *offd_zone;
+  const uint8_t *zone[3];    // per direction, global half-coordinate q -> zone 0/1/2
+  unsigned long long *nr_fallbacks;
+};
+
+// Point sources in rank-local linear indices.
+struct SrcDev {
+  int n;
+  const long long *idx;
+  const int *comp;          // direction 0..2 of the D/B component
+  const double *val;        // [step][n] value subtracted this step
+};
+
+struct ISrcDev {             // integrated sources, read by the E kernel
+  int n;
+  long long idx[MAX_ISRC];
+  int comp[MAX_ISRC];
+  const double *val;         // [step][n] dipole value real(amp*dipole(t+dt))
+};
+
+// Host-side launchers implemented in mnl_kernels.hip.
+struct Launch {
+  void *stream;  // hipStream_t
+};
+
+int k_curl(int ft, bool shell, const Box &b, const DevGrid &g, const DevFields &f,
+           const CurlPlan &p, double courant, void *stream);
+int k_update_h(const Box &b, const DevGrid &g, const DevFields &f, void *stream);
+int k_update_e(bool shell, const Box &b, const DevGrid &g, const DevFields &f,
+               const ISrcDev &is, int step, bool fuse_pols, void *stream);
+int k_update_pols(const Box &b, const DevGrid &g, const DevFields &f, void *stream);
+int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int step,
+             void *stream);
+int k_fill(double *p, double v, size_t n, void *stream);
+int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_type,
+                     int comp_dir, int zlo_glob, void *stream);
+int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
+                   int comp_type, int comp_dir, const DevFields &f, void *stream);
+int k_box_fill(double *dst, const DevGrid &g, int comp_type, int comp_dir, const double *pos_lo,
+               const double *pos_hi, double value, int invert, double a, const int *io,
+               void *stream);
+
+}  // namespace mnl

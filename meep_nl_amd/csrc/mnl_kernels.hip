@@ -1,0 +1,647 @@
+// mnl_kernels.hip -- gfx950 kernels of the fields::step() hot path.
+//
+// Global-grid formulation of the reference's chunked update:
+// the reference splits PML regions into their own chunks and runs a different
+// loop body per chunk (src/step_generic.cpp:69-253, 576-906).  Here one
+// kernel per sub-step covers the rank-local grid; the interior box (no
+// component of any point lies in a PML chunk, H == B) runs the lean body,
+// the <= 6 shell boxes run the general body, which looks the per-point chunk
+// flags up in tiny per-direction tables.  Arithmetic follows the reference
+// expression by expression and the library is compiled with
+// -ffp-contract=off, so results are bitwise those of the CPU reference.
+//
+// All kernels are HBM-bound fp64 stencils (0.1-0.2 flop/byte): no MFMA.
+#include <hip/hip_runtime.h>
+
+#include "mnl_internal.hpp"
+
+namespace mnl {
+
+#define MNL_BX 64
+#define MNL_BY 4
+
+__device__ __forceinline__ int shift_of(int type, int c, int d) {
+  // grid_volume::iyee_shift (src/meep/vec.hpp:1133-1141)
+  return (type == T_E || type == T_D) ? (d == c) : (d != c);
+}
+
+struct Pt {
+  int j[3];       // local index per direction (0 for absent)
+  long long idx;  // linear index
+};
+
+__device__ __forceinline__ bool make_pt(const Box &b, const DevGrid &g, Pt &p) {
+  int i0 = b.lo[0] + blockIdx.x * MNL_BX + threadIdx.x;
+  int i1 = b.lo[1] + blockIdx.y * MNL_BY + threadIdx.y;
+  int i2 = b.lo[2] + blockIdx.z;
+  if (i0 > b.hi[0] || i1 > b.hi[1]) return false;
+  int ii[3] = {i0, i1, i2};
+#pragma unroll
+  for (int d = 0; d < 3; d++) p.j[d] = g.ax[d] >= 0 ? ii[g.ax[d]] : 0;
+  p.idx = (long long)i0 + (long long)i1 * g.st[1] + (long long)i2 * g.st[2];
+  return true;
+}
+
+// little_owned_corner0 .. big_corner (src/meep/vec.hpp:1102-1104), with the
+// metallic wall plane left untouched (it is zeroed by zero_metal in the
+// reference, src/boundaries.cpp:304-339, and never becomes nonzero).
+__device__ __forceinline__ bool owned(const DevGrid &g, int type, int c, const Pt &p) {
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    if (shift_of(type, c, d)) {
+      if (p.j[d] < g.owned_lo_sh[d] || p.j[d] > g.owned_hi_sh[d]) return false;
+    } else {
+      if (p.j[d] < g.owned_lo_un[d] || p.j[d] > g.owned_hi_un[d]) return false;
+    }
+  }
+  return true;
+}
+
+// global half-coordinate (relative to the cell's little corner) of a point
+__device__ __forceinline__ int qcoord(const DevGrid &g, const Pt &p, int type, int c, int d) {
+  return 2 * (p.j[d] + g.off[d]) + shift_of(type, c, d);
+}
+
+__device__ __forceinline__ bool pml_at(const DevFields &f, const DevGrid &g, int d, int q) {
+  return g.ax[d] >= 0 && f.pml.flag[d] != nullptr && f.pml.flag[d][q] != 0;
+}
+
+// ----------------------------------------------------------------- curl B / D
+// fields_chunk::step_db -> step_curl (src/step_db.cpp:44-146,
+// src/step_generic.cpp:69-253, conductivity-free branches).  Component d of
+// B (D): g1 = E (H) comp (d+2)%3 along dir (d+1)%3, g2 = comp (d+1)%3 along
+// dir (d+2)%3; D uses negated strides (src/step_db.cpp:81-84).
+template <int FT, bool SHELL>
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, DevGrid g, DevFields f,
+                                                               CurlPlan pl, double C) {
+  Pt p;
+  if (!make_pt(b, g, p)) return;
+  const long long i = p.idx;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (!pl.present[d]) continue;
+    if (!owned(g, FT, d, p)) continue;
+    const int c1 = (d + 2) % 3, dir1 = (d + 1) % 3;
+    const int c2 = (d + 1) % 3, dir2 = (d + 2) % 3;
+    long long s1 = g.sdir[dir1], s2 = g.sdir[dir2];
+    const double *g1, *g2;
+    if (FT == T_B) {
+      g1 = f.E[c1];
+      g2 = f.E[c2];
+    } else {
+      s1 = -s1;
+      s2 = -s2;
+      g1 = f.B[c1];
+      g2 = f.B[c2];
+      if (SHELL) {  // H separate only in chunks with PML along the H direction
+        if (f.H[c1] && pml_at(f, g, c1, qcoord(g, p, T_H, c1, c1))) g1 = f.H[c1];
+        if (f.H[c2] && pml_at(f, g, c2, qcoord(g, p, T_H, c2, c2))) g2 = f.H[c2];
+      }
+    }
+    double T, dtdx = C;
+    const int terms = pl.terms[d];
+    if (terms == 3) {
+      T = g1[i + s1] - g1[i] + g2[i] - g2[i + s2];
+    } else if (terms == 1) {
+      T = g1[i + s1] - g1[i];
+    } else {  // g1 == NULL: swap and flip the sign (src/step_generic.cpp:76-80)
+      T = g2[i + s2] - g2[i];
+      dtdx = -C;
+    }
+    double *F = FT == T_B ? f.B[d] : f.D[d];
+    if (!SHELL) {
+      F[i] -= dtdx * T;
+      continue;
+    }
+    const int dsig = (d + 1) % 3, dsigu = (d + 2) % 3;
+    const int k = qcoord(g, p, FT, d, dsig), ku = qcoord(g, p, FT, d, dsigu);
+    const bool ps = pml_at(f, g, dsig, k), pu = pml_at(f, g, dsigu, ku);
+    if (!ps && !pu) {
+      F[i] -= dtdx * T;
+    } else if (!ps) {
+      double *U = FT == T_B ? f.UB[d] : f.UD[d];
+      const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu],
+                   *siginvu = f.pml.siginv[dsigu];
+      double fprev = U[i];
+      double fu = fprev - dtdx * T;
+      U[i] = fu;
+      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * F[i] + fu - fprev);
+    } else if (!pu) {
+      const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
+      F[i] = ((kap[k] - sig[k]) * F[i] - dtdx * T) * siginv[k];
+    } else {
+      double *U = FT == T_B ? f.UB[d] : f.UD[d];
+      const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
+      const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu],
+                   *siginvu = f.pml.siginv[dsigu];
+      double fprev = U[i];
+      double fu = ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
+      U[i] = fu;
+      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * F[i] + fu - fprev);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- H from B
+// update_eh(H_stuff) in PML chunks: W auxiliary field, mu = 1
+// (src/update_eh.cpp:186-259, src/step_generic.cpp:717-724).
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_h_kernel(Box b, DevGrid g, DevFields f) {
+  Pt p;
+  if (!make_pt(b, g, p)) return;
+  const long long i = p.idx;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (!f.hcomp_present[d] || !f.H[d]) continue;
+    if (!owned(g, T_H, d, p)) continue;
+    const int kw = qcoord(g, p, T_H, d, d);
+    if (!pml_at(f, g, d, kw)) continue;
+    double fwprev = f.WH[d][i];
+    double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
+    double fw = f.B[d][i];
+    f.WH[d][i] = fw;
+    f.H[d][i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+  }
+}
+
+// ----------------------------------------------------------------- chi(2) NR
+// runNR / newtonRaphson (src/newton_raphson.cpp:93-359) in registers.
+struct NRP {
+  double A, B, F, G, H;  // C = D = E = 0 for the 43m tensor used by the fork
+};
+
+__device__ __forceinline__ void nr_eq(double x, double y, double z, const NRP &p1, const NRP &p2,
+                                      const NRP &p3, double F[3]) {
+  // newton_raphson.cpp:144-148
+  F[0] = p1.A - (p1.B * x + p1.F * y * z + p1.G * x * z + p1.H * x * y);
+  F[1] = p2.A - (p2.B * y + p2.F * y * z + p2.G * x * z + p2.H * x * y);
+  F[2] = p3.A - (p3.B * z + p3.F * y * z + p3.G * x * z + p3.H * x * y);
+}
+
+__device__ bool nr_solve(double x, double y, double z, const NRP &p1, const NRP &p2,
+                         const NRP &p3, double *fw, double *fw_2, double *fw_3, double tol1,
+                         double tol2, double tol3, int max_it) {
+  for (int iter = 0; iter < max_it; iter++) {
+    double F[3], A[3][3];
+    nr_eq(x, y, z, p1, p2, p3, F);
+    // jacobian, newton_raphson.cpp:157-161
+    A[0][0] = -p1.B - p1.G * z - p1.H * y;
+    A[0][1] = -p1.F * z - p1.H * x;
+    A[0][2] = -p1.F * y - p1.G * x;
+    A[1][0] = -p2.G * z - p2.H * y;
+    A[1][1] = -p2.B - p2.F * z - p2.H * x;
+    A[1][2] = -p2.F * y - p2.G * x;
+    A[2][0] = -p3.G * z - p3.H * y;
+    A[2][1] = -p3.F * z - p3.H * x;
+    A[2][2] = -p3.B - p3.F * y - p3.G * x;
+    // solveLinearSystem, newton_raphson.cpp:170-194
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int q = r + 1; q < 3; q++) {
+        double factor = A[q][r] / A[r][r];
+#pragma unroll
+        for (int k = r; k < 3; k++) A[q][k] -= factor * A[r][k];
+        F[q] -= factor * F[r];
+      }
+    double dl[3];
+#pragma unroll
+    for (int r = 2; r >= 0; r--) {
+      dl[r] = F[r];
+#pragma unroll
+      for (int q = r + 1; q < 3; q++) dl[r] -= A[r][q] * dl[q];
+      dl[r] /= A[r][r];
+    }
+    x -= dl[0];
+    y -= dl[1];
+    z -= dl[2];
+    if (fabs(dl[0]) < tol1 && fabs(dl[1]) < tol2 && fabs(dl[2]) < tol3) {
+      double ax = fabs(x), ay = fabs(y), az = fabs(z);
+      double fcp = (ax > ay ? (ax > az ? ax : az) : (ay > az ? ay : az)) * 1e-4;
+      double fc[3];
+      nr_eq(x, y, z, p1, p2, p3, fc);
+      if (fc[0] <= fcp && fc[1] <= fcp && fc[2] <= fcp) {
+        *fw = x;
+        *fw_2 = y;
+        *fw_3 = z;
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
+__device__ double nr_random(unsigned long long &st) {
+  // deterministic replacement of the std::random_device fallback
+  // (newton_raphson.cpp:196-206, 331-336); see DESIGN.md "Divergences".
+  auto next = [&]() {
+    unsigned long long z = (st += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  double u1 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+  double u2 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+  double u3 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+  double gg = sqrt(-2.0 * log(u1)) * cos(2 * 3.141592653589793238462643383276 * u2);
+  return exp(1.0 + 90.0 * gg) * (2.0 * u3 - 1.0);
+}
+
+__device__ void run_nr(double seed1, double seed2, double seed3, double *fw, double *fw_2,
+                       double *fw_3, const NRP &p1, const NRP &p2, const NRP &p3,
+                       unsigned long long rng, unsigned long long *fallbacks) {
+  const double TOL = 1e-8, seedMax = 1e33;
+  int max_it = 250;
+  double tol1 = fmax(fabs(TOL * (*fw)) * 0.0001, TOL);
+  double tol2 = fmax(fabs(TOL * (*fw_2)) * 0.0001, TOL);
+  double tol3 = fmax(fabs(TOL * (*fw_3)) * 0.0001, TOL);
+  double s1 = seed1, s2 = seed2, s3 = seed3;
+  for (int a = 0; a < 100; ++a) {
+    if (nr_solve(s1, s2, s3, p1, p2, p3, fw, fw_2, fw_3, tol1, tol2, tol3, max_it)) return;
+    switch (a) {  // newton_raphson.cpp:266-338
+      case 0: s1 = seed1 * seedMax; max_it = 600; break;
+      case 1: s1 = seed1; s2 = seed2 * seedMax; break;
+      case 2: s2 = seed2; s3 = seed3 * seedMax; break;
+      case 3: s3 = seed3; s1 = -seed1 * seedMax; break;
+      case 4: s1 = seed1; s2 = -seed2 * seedMax; break;
+      case 5: s2 = seed2; s3 = -seed3 * seedMax; break;
+      case 6: s1 = seed1 * seedMax; s2 = seed2 * seedMax; s3 = seed3; break;
+      case 7: s1 = seed1 * seedMax; s2 = seed2; s3 = seed3 * seedMax; break;
+      case 8: s1 = seed1; s2 = seed2 * seedMax; s3 = seed3 * seedMax; break;
+      case 9: s1 = -seed1 * seedMax; s2 = -seed2 * seedMax; s3 = seed3; break;
+      case 10: s1 = -seed1 * seedMax; s2 = seed2; s3 = -seed3 * seedMax; break;
+      case 11: s1 = seed1; s2 = -seed2 * seedMax; s3 = -seed3 * seedMax; break;
+      case 12: s1 = seed1 * seedMax; s2 = seed2 * seedMax; s3 = seed3 * seedMax; break;
+      case 13: s1 = -seed1 * seedMax; s2 = -seed2 * seedMax; s3 = -seed3 * seedMax; break;
+      default:
+        atomicAdd(fallbacks, 1ull);
+        s1 = nr_random(rng);
+        s2 = nr_random(rng);
+        s3 = nr_random(rng);
+        break;
+    }
+  }
+}
+
+// f_minus_p value of D component c at linear index n (src/update_eh.cpp:122-154)
+template <bool ISRC>
+__device__ __forceinline__ double dmp_at(const DevFields &f, const ISrcDev &is, int step, int c,
+                                         long long n) {
+  double v = f.D[c][n];
+  for (int k = 0; k < f.npol; k++)
+    if (f.pol[k].P[c]) v -= f.pol[k].P[c][n];
+  if (ISRC) {
+    for (int k = 0; k < is.n; k++)
+      if (is.comp[k] == c && is.idx[k] == n) v -= is.val[(long long)step * is.n + k];
+  }
+  return v;
+}
+
+// ----------------------------------------------------------------- E from D
+// update_eh(E_stuff) -> step_update_EDHB (src/update_eh.cpp:67-283,
+// src/step_generic.cpp:576-906) + lorentzian update_P (src/susceptibility.cpp:
+// 188-262) fused when no Newton-Raphson neighbour reads are needed.
+template <bool SHELL, bool NR, bool ISRC, bool FUSEPOL>
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, DevGrid g, DevFields f,
+                                                                   ISrcDev is, int step) {
+  Pt p;
+  if (!make_pt(b, g, p)) return;
+  const long long i = p.idx;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (!f.ecomp_present[d]) continue;
+    if (!owned(g, T_E, d, p)) continue;
+    const double gs = dmp_at<ISRC>(f, is, step, d, i);
+    const double *u = f.inveps[d];
+    double *E = f.E[d];
+    bool pml = false;
+    int kw = 0;
+    if (SHELL) {
+      kw = qcoord(g, p, T_E, d, d);
+      pml = pml_at(f, g, d, kw);
+    }
+    double wv;  // the W field read by update_pols (f_w if allocated, else E)
+    if (pml) {
+      double fwprev = f.WE[d][i];
+      double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
+      double fw = u ? (gs * u[i]) : gs;
+      f.WE[d][i] = fw;
+      E[i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+      wv = fw;
+    } else {
+      bool done = false;
+      if (NR) {
+        // 3x3 chi1inv + chi2 branch (src/step_generic.cpp:730-816)
+        int zb = 13;
+        if (SHELL) {
+          int z3[3];
+#pragma unroll
+          for (int e = 0; e < 3; e++) z3[e] = g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, d, e)] : 1;
+          zb = z3[0] * 9 + z3[1] * 3 + z3[2];
+        }
+        const int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
+        const bool have_off =
+            ((f.offd_zone[zb] >> (3 * d)) & 3) == 3 && f.chi2[d] && f.ecomp_present[d1] &&
+            f.ecomp_present[d2];
+        if (have_off) {
+          const double *u1 = f.offd[d][0], *u2 = f.offd[d][1];
+          double chi2new = f.chi2[d][i];
+          int zc = (u[i] == 0) + (u1[i] == 0) + (u2[i] == 0);
+          if (!(chi2new == 0 || zc > 1)) {
+            const long long s = g.sdir[d], s1 = g.sdir[d1], s2 = g.sdir[d2];
+            double gs_2 = (dmp_at<ISRC>(f, is, step, d1, i) + dmp_at<ISRC>(f, is, step, d1, i + s) +
+                           dmp_at<ISRC>(f, is, step, d1, i - s1) +
+                           dmp_at<ISRC>(f, is, step, d1, i + (s - s1))) *
+                          0.25;
+            double gs_3 = (dmp_at<ISRC>(f, is, step, d2, i) + dmp_at<ISRC>(f, is, step, d2, i + s) +
+                           dmp_at<ISRC>(f, is, step, d2, i - s2) +
+                           dmp_at<ISRC>(f, is, step, d2, i + (s - s2))) *
+                          0.25;
+            double us = 1 / u[i];
+            double us_2 = us, us_3 = us;
+            double dummy1 = 0.0, dummy2 = 0.0;
+            double fv = E[i];
+            unsigned long long rng = 0x9E3779B97F4A7C15ull ^ (unsigned long long)i * 31ull ^
+                                     ((unsigned long long)step << 40) ^ (unsigned long long)d;
+            if (d == 0) {
+              NRP p1 = {gs, us, chi2new, 0.0, 0.0};
+              NRP p2 = {gs_2, us_2, 0.0, chi2new, 0.0};
+              NRP p3 = {gs_3, us_3, 0.0, 0.0, chi2new};
+              run_nr(fv, gs_2 * u[i], gs_3 * u[i], &fv, &dummy1, &dummy2, p1, p2, p3, rng,
+                     f.nr_fallbacks);
+            } else if (d == 1) {
+              NRP p1 = {gs_3, us_3, chi2new, 0.0, 0.0};
+              NRP p2 = {gs, us, 0.0, chi2new, 0.0};
+              NRP p3 = {gs_2, us_2, 0.0, 0.0, chi2new};
+              run_nr(gs_3 * u[i], fv, gs_2 * u[i], &dummy1, &fv, &dummy2, p1, p2, p3, rng,
+                     f.nr_fallbacks);
+            } else {
+              NRP p1 = {gs_2, us_2, chi2new, 0.0, 0.0};
+              NRP p2 = {gs_3, us_3, 0.0, chi2new, 0.0};
+              NRP p3 = {gs, us, 0.0, 0.0, chi2new};
+              run_nr(gs_2 * u[i], gs_3 * u[i], fv, &dummy1, &dummy1, &fv, p1, p2, p3, rng,
+                     f.nr_fallbacks);
+            }
+            E[i] = fv;
+            done = true;
+          }
+        }
+      }
+      if (!done) E[i] = u ? (gs * u[i]) : gs;
+      wv = E[i];
+    }
+    if (FUSEPOL) {
+      for (int k = 0; k < f.npol; k++) {
+        const PolDev &pd = f.pol[k];
+        if (!pd.P[d]) continue;
+        double pcur = pd.P[d][i];
+        pd.P[d][i] = pd.gamma1inv * (pcur * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * pd.Pp[d][i] +
+                                     pd.omega0dtsqr * (pd.sigma[d][i] * wv));
+        pd.Pp[d][i] = pcur;
+      }
+    }
+  }
+}
+
+// lorentzian update_P, isotropic (src/susceptibility.cpp:251-258), used after
+// the Newton-Raphson E update (which reads neighbouring D - P).
+template <bool SHELL>
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, DevGrid g, DevFields f) {
+  Pt p;
+  if (!make_pt(b, g, p)) return;
+  const long long i = p.idx;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (!f.ecomp_present[d]) continue;
+    if (!owned(g, T_E, d, p)) continue;
+    bool pml = false;
+    if (SHELL) pml = pml_at(f, g, d, qcoord(g, p, T_E, d, d));
+    const double wv = pml ? f.WE[d][i] : f.E[d][i];
+    for (int k = 0; k < f.npol; k++) {
+      const PolDev &pd = f.pol[k];
+      if (!pd.P[d]) continue;
+      double pcur = pd.P[d][i];
+      pd.P[d][i] = pd.gamma1inv * (pcur * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * pd.Pp[d][i] +
+                                   pd.omega0dtsqr * (pd.sigma[d][i] * wv));
+      pd.Pp[d][i] = pcur;
+    }
+  }
+}
+
+// ----------------------------------------------------------------- sources
+// fields_chunk::step_source (src/step.cpp:296-319): f -= real(amp*J*dt),
+// applied in source-list order by a single lane (exact sequential semantics).
+struct Ptr3 {
+  double *p[3];
+};
+__global__ void source_kernel(Ptr3 pt, SrcDev s, int step) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const double *v = s.val + (long long)step * s.n;
+  for (int k = 0; k < s.n; k++) pt.p[s.comp[k]][s.idx[k]] -= v[k];
+}
+
+__global__ void fill_kernel(double *p, double v, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+// canonical (Z fastest, whole cell) <-> device layout (rank-local box)
+__global__ void from_canonical_kernel(double *dst, const double *src, DevGrid g, long long cs0,
+                                      long long cs1, long long cs2) {
+  int i0 = blockIdx.x * MNL_BX + threadIdx.x;
+  int i1 = blockIdx.y * MNL_BY + threadIdx.y;
+  int i2 = blockIdx.z;
+  if (i0 >= g.N[0] || i1 >= g.N[1]) return;
+  int ii[3] = {i0, i1, i2};
+  long long cidx = 0;
+  long long cs[3] = {cs0, cs1, cs2};
+  for (int d = 0; d < 3; d++)
+    if (g.ax[d] >= 0) cidx += (long long)(ii[g.ax[d]] + g.off[d]) * cs[d];
+  dst[(long long)i0 + i1 * g.st[1] + i2 * g.st[2]] = src[cidx];
+}
+
+__global__ void to_canonical_kernel(double *dst, const double *src, const double *hsep, DevGrid g,
+                                    DevFields f, int type, int c, long long cs0, long long cs1,
+                                    long long cs2) {
+  int i0 = blockIdx.x * MNL_BX + threadIdx.x;
+  int i1 = blockIdx.y * MNL_BY + threadIdx.y;
+  int i2 = blockIdx.z;
+  if (i0 >= g.N[0] || i1 >= g.N[1]) return;
+  int ii[3] = {i0, i1, i2};
+  Pt p;
+  for (int d = 0; d < 3; d++) p.j[d] = g.ax[d] >= 0 ? ii[g.ax[d]] : 0;
+  // rank-owned planes only along every axis (ghost entries are filled by
+  // their owner; non-owned boundary entries are 0 in the reference).
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    int sh = shift_of(type, c, d);
+    int lo = sh ? g.owned_lo_sh[d] : g.owned_lo_un[d];
+    int hi = sh ? g.owned_hi_sh[d] : g.owned_hi_un[d];
+    if (!sh && g.wall[d] && p.j[d] + g.off[d] == g.nglob[d]) hi = p.j[d];  // wall plane (= 0)
+    if (p.j[d] < lo || p.j[d] > hi) return;
+  }
+  long long cidx = 0;
+  long long cs[3] = {cs0, cs1, cs2};
+  for (int d = 0; d < 3; d++)
+    if (g.ax[d] >= 0) cidx += (long long)(p.j[d] + g.off[d]) * cs[d];
+  long long i = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
+  double v = src[i];
+  if (hsep && pml_at(f, g, c, qcoord(g, p, T_H, c, c))) v = hsep[i];
+  dst[cidx] = v;
+}
+
+__global__ void box_fill_kernel(double *dst, DevGrid g, int type, int c, double x0, double x1,
+                                double y0, double y1, double z0, double z1, double value,
+                                int invert, double a, int io0, int io1, int io2) {
+  int i0 = blockIdx.x * MNL_BX + threadIdx.x;
+  int i1 = blockIdx.y * MNL_BY + threadIdx.y;
+  int i2 = blockIdx.z;
+  if (i0 >= g.N[0] || i1 >= g.N[1]) return;
+  int ii[3] = {i0, i1, i2};
+  double lo[3] = {x0, y0, z0}, hi[3] = {x1, y1, z1};
+  int io[3] = {io0, io1, io2};
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    int jj = ii[g.ax[d]] + g.off[d];
+    double pos = (io[d] + 2 * jj + shift_of(type, c, d)) * (0.5 * (1.0 / a));
+    if (pos < lo[d] || pos > hi[d]) return;
+  }
+  dst[(long long)i0 + i1 * g.st[1] + i2 * g.st[2]] = invert ? 1.0 / value : value;
+}
+
+// ----------------------------------------------------------------- launchers
+static dim3 grid_for(const Box &b) {
+  int n0 = b.hi[0] - b.lo[0] + 1, n1 = b.hi[1] - b.lo[1] + 1, n2 = b.hi[2] - b.lo[2] + 1;
+  return dim3((n0 + MNL_BX - 1) / MNL_BX, (n1 + MNL_BY - 1) / MNL_BY, n2);
+}
+static bool empty(const Box &b) {
+  for (int k = 0; k < 3; k++)
+    if (b.hi[k] < b.lo[k]) return true;
+  return false;
+}
+static int rc() { return hipGetLastError() == hipSuccess ? 0 : -1; }
+
+int k_curl(int ft, bool shell, const Box &b, const DevGrid &g, const DevFields &f,
+           const CurlPlan &p, double courant, void *stream) {
+  if (empty(b)) return 0;
+  dim3 blk(MNL_BX, MNL_BY), grd = grid_for(b);
+  hipStream_t s = (hipStream_t)stream;
+  if (ft == T_B) {
+    if (shell)
+      curl_kernel<T_B, true><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+    else
+      curl_kernel<T_B, false><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+  } else {
+    if (shell)
+      curl_kernel<T_D, true><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+    else
+      curl_kernel<T_D, false><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+  }
+  return rc();
+}
+
+int k_update_h(const Box &b, const DevGrid &g, const DevFields &f, void *stream) {
+  if (empty(b)) return 0;
+  update_h_kernel<<<grid_for(b), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(b, g, f);
+  return rc();
+}
+
+template <bool SHELL>
+static void launch_e(const Box &b, const DevGrid &g, const DevFields &f, const ISrcDev &is,
+                     int step, bool fuse, hipStream_t s) {
+  dim3 blk(MNL_BX, MNL_BY), grd = grid_for(b);
+  const bool nr = f.nr_enabled != 0, isrc = is.n > 0;
+  if (nr) {
+    if (isrc)
+      update_e_kernel<SHELL, true, true, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+    else
+      update_e_kernel<SHELL, true, false, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+  } else if (fuse) {
+    if (isrc)
+      update_e_kernel<SHELL, false, true, true><<<grd, blk, 0, s>>>(b, g, f, is, step);
+    else
+      update_e_kernel<SHELL, false, false, true><<<grd, blk, 0, s>>>(b, g, f, is, step);
+  } else {
+    if (isrc)
+      update_e_kernel<SHELL, false, true, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+    else
+      update_e_kernel<SHELL, false, false, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+  }
+}
+
+int k_update_e(bool shell, const Box &b, const DevGrid &g, const DevFields &f, const ISrcDev &is,
+               int step, bool fuse_pols, void *stream) {
+  if (empty(b)) return 0;
+  if (shell)
+    launch_e<true>(b, g, f, is, step, fuse_pols, (hipStream_t)stream);
+  else
+    launch_e<false>(b, g, f, is, step, fuse_pols, (hipStream_t)stream);
+  return rc();
+}
+
+int k_update_pols(const Box &b, const DevGrid &g, const DevFields &f, void *stream) {
+  if (empty(b)) return 0;
+  update_pols_kernel<true><<<grid_for(b), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(b, g, f);
+  return rc();
+}
+
+int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int step,
+             void *stream) {
+  (void)g;
+  if (s.n == 0) return 0;
+  Ptr3 pt;
+  for (int d = 0; d < 3; d++) pt.p[d] = ft == T_D ? f.D[d] : f.B[d];
+  source_kernel<<<1, 64, 0, (hipStream_t)stream>>>(pt, s, step);
+  return rc();
+}
+
+int k_fill(double *p, double v, size_t n, void *stream) {
+  if (n == 0) return 0;
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  fill_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(p, v, n);
+  return rc();
+}
+
+static void canon_strides(const DevGrid &g, long long cs[3]) {
+  // canonical whole-cell layout: Z fastest, then Y, then X (src/vec.cpp:482-494)
+  long long nz = g.ax[2] >= 0 ? g.nglob[2] + 1 : 1;
+  long long ny = g.ax[1] >= 0 ? g.nglob[1] + 1 : 1;
+  cs[2] = g.ax[2] >= 0 ? 1 : 0;
+  cs[1] = g.ax[1] >= 0 ? nz : 0;
+  cs[0] = g.ax[0] >= 0 ? nz * ny : 0;
+}
+
+int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_type, int comp_dir,
+                     int zlo_glob, void *stream) {
+  (void)comp_type;
+  (void)comp_dir;
+  (void)zlo_glob;
+  long long cs[3];
+  canon_strides(g, cs);
+  dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
+  from_canonical_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(dst, src, g, cs[0],
+                                                                               cs[1], cs[2]);
+  return rc();
+}
+
+int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
+                   int comp_type, int comp_dir, const DevFields &f, void *stream) {
+  long long cs[3];
+  canon_strides(g, cs);
+  dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
+  to_canonical_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(
+      dst, src, hsep, g, f, comp_type, comp_dir, cs[0], cs[1], cs[2]);
+  return rc();
+}
+
+int k_box_fill(double *dst, const DevGrid &g, int comp_type, int comp_dir, const double *lo,
+               const double *hi, double value, int invert, double a, const int *io, void *stream) {
+  dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
+  box_fill_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(
+      dst, g, comp_type, comp_dir, lo[0], hi[0], lo[1], hi[1], lo[2], hi[2], value, invert, a,
+      io[0], io[1], io[2]);
+  return rc();
+}
+
+}  // namespace mnl

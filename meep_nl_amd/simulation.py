@@ -1,0 +1,363 @@
+"""Python drop-in for the meep.Simulation subset that drives fields::step().
+
+Mirrors python/simulation.py (Simulation.__init__ 1228-1256, init_sim
+2449-2512, _run_until 2795-2855, round_time/meep_time 2609-2636) and
+python/source.py (Source.add_source 132-158, GaussianSource 262-332,
+ContinuousSource) for Cartesian 1-D/2-D/3-D cells with real fields, PML,
+non-averaged block geometry (epsilon, chi2, chi3, Lorentzian/Drude E
+susceptibilities) and point sources.  Everything runs on the MI355X through
+libmnl.so; there is no CPU path.
+"""
+import math
+import os
+import warnings
+
+import numpy as np
+
+from . import core
+from .core import Bx, By, Bz, Dx, Dy, Dz, Ex, Ey, Ez, Hx, Hy, Hz, X, Y, Z
+
+ALL = -1
+Low, High = 0, 1
+inf = 1.0e20
+
+
+class Vector3:
+    def __init__(self, x=0.0, y=0.0, z=0.0):
+        self.x, self.y, self.z = float(x), float(y), float(z)
+
+    def __iter__(self):
+        return iter((self.x, self.y, self.z))
+
+    def __getitem__(self, i):
+        return (self.x, self.y, self.z)[i]
+
+    def __add__(self, o):
+        return Vector3(self.x + o[0], self.y + o[1], self.z + o[2])
+
+    def __sub__(self, o):
+        return Vector3(self.x - o[0], self.y - o[1], self.z - o[2])
+
+    def __mul__(self, s):
+        return Vector3(self.x * s, self.y * s, self.z * s)
+
+    __rmul__ = __mul__
+
+    def __eq__(self, o):
+        return tuple(self) == tuple(o)
+
+    def __repr__(self):
+        return f"Vector3({self.x}, {self.y}, {self.z})"
+
+
+class Volume:
+    def __init__(self, center=Vector3(), size=Vector3()):
+        self.center = Vector3(*center)
+        self.size = Vector3(*size)
+
+
+# ---------------------------------------------------------------- materials
+class LorentzianSusceptibility:
+    """lorentzian_susceptibility(frequency, gamma) with constant sigma
+    (python/geom.py LorentzianSusceptibility; src/susceptibility.cpp:188-262)."""
+
+    drude = False
+
+    def __init__(self, frequency=0.0, gamma=0.0, sigma=1.0, sigma_diag=None):
+        self.frequency = float(frequency)
+        self.gamma = float(gamma)
+        sd = sigma_diag if sigma_diag is not None else Vector3(sigma, sigma, sigma)
+        self.sigma_diag = Vector3(*sd)
+
+    def key(self):
+        return (self.frequency, self.gamma, self.drude)
+
+
+class DrudeSusceptibility(LorentzianSusceptibility):
+    drude = True
+
+
+class Medium:
+    def __init__(self, epsilon=1.0, epsilon_diag=None, epsilon_offdiag=None, E_chi2=0.0,
+                 E_chi3=0.0, chi2=None, chi3=None, E_susceptibilities=(), index=None, mu=1.0):
+        if index is not None:
+            epsilon = index * index
+        self.epsilon_diag = Vector3(*(epsilon_diag if epsilon_diag is not None else
+                                      (epsilon, epsilon, epsilon)))
+        self.epsilon_offdiag = Vector3(*(epsilon_offdiag if epsilon_offdiag is not None else
+                                         (0, 0, 0)))
+        self.E_chi2 = float(chi2 if chi2 is not None else E_chi2)
+        self.E_chi3 = float(chi3 if chi3 is not None else E_chi3)
+        self.E_susceptibilities = list(E_susceptibilities)
+        if mu != 1.0:
+            raise NotImplementedError("magnetic materials (mu != 1) are outside the hot-path scope")
+
+
+vacuum = air = Medium()
+
+
+class Block:
+    def __init__(self, size=Vector3(), center=Vector3(), material=Medium(), **kw):
+        self.size = Vector3(*size)
+        self.center = Vector3(*center)
+        self.material = material
+        if any(k in kw for k in ("e1", "e2", "e3")):
+            raise NotImplementedError("only axis-aligned blocks are supported")
+
+    def contains(self, x, y, z):
+        c, s = self.center, self.size
+        return ((np.abs(x - c.x) <= 0.5 * s.x) & (np.abs(y - c.y) <= 0.5 * s.y) &
+                (np.abs(z - c.z) <= 0.5 * s.z))
+
+
+class PML:
+    def __init__(self, thickness, direction=ALL, side=ALL, R_asymptotic=1e-15, mean_stretch=1.0):
+        self.thickness = float(thickness)
+        self.direction = direction
+        self.side = side
+        self.R_asymptotic = R_asymptotic
+        self.mean_stretch = mean_stretch
+
+
+# ---------------------------------------------------------------- sources
+class SourceTime:
+    is_integrated = False
+
+
+class GaussianSource(SourceTime):
+    """python/source.py:262-332 -> gaussian_src_time(f, w, start, start+2w*cutoff)."""
+
+    def __init__(self, frequency=None, width=0, fwidth=float("inf"), start_time=0, cutoff=5.0,
+                 is_integrated=False, wavelength=None):
+        if frequency is None and wavelength is None:
+            raise ValueError("Must set either frequency or wavelength in GaussianSource.")
+        self.frequency = 1 / wavelength if wavelength else float(frequency)
+        self.width = max(width, 1 / fwidth)
+        self.start_time = start_time
+        self.cutoff = cutoff
+        self.is_integrated = is_integrated
+
+    def params(self):
+        return 0, [self.frequency, self.width, self.start_time,
+                   self.start_time + 2 * self.width * self.cutoff]
+
+
+class ContinuousSource(SourceTime):
+    def __init__(self, frequency=None, start_time=0, end_time=inf, width=0, fwidth=float("inf"),
+                 slowness=3.0, is_integrated=False, wavelength=None):
+        if frequency is None and wavelength is None:
+            raise ValueError("Must set either frequency or wavelength in ContinuousSource.")
+        self.frequency = 1 / wavelength if wavelength else frequency
+        self.start_time, self.end_time = start_time, end_time
+        self.width = max(width, 1 / fwidth)
+        self.slowness = slowness
+        self.is_integrated = is_integrated
+
+    def params(self):
+        f = complex(self.frequency)
+        return 1, [f.real, f.imag, self.width, self.start_time, self.end_time, self.slowness]
+
+
+class Source:
+    def __init__(self, src, component, center=None, volume=None, size=Vector3(), amplitude=1.0,
+                 amp_func=None):
+        self.src = src
+        self.component = component
+        if volume is not None:
+            center, size = volume.center, volume.size
+        self.center = Vector3(*(center if center is not None else (0, 0, 0)))
+        self.size = Vector3(*size)
+        self.amplitude = complex(amplitude)
+        if amp_func is not None or any(v != 0 for v in self.size):
+            raise NotImplementedError("only point sources (size 0, no amp_func) are in scope")
+
+    def add_source(self, fields):  # python/source.py:132-158
+        kind, p = self.src.params()
+        fields.add_point_source(self.component, kind, p, tuple(self.center), self.amplitude,
+                                self.src.is_integrated)
+
+
+# ---------------------------------------------------------------- distributed
+def _dist_context():
+    """(rank, world, local_rank, nccl_id) when launched one process per GPU by
+    torch.distributed.run, else None."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    obj = [core.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return rank, world, int(os.environ.get("LOCAL_RANK", rank)), obj[0]
+
+
+# ---------------------------------------------------------------- Simulation
+class Simulation:
+    def __init__(self, cell_size, resolution, geometry=(), sources=(), boundary_layers=(),
+                 default_material=Medium(), Courant=0.5, eps_averaging=True, dimensions=None,
+                 force_complex_fields=False, k_point=False, symmetries=(), parallel=None,
+                 **kwargs):
+        self.cell_size = Vector3(*cell_size)
+        self.resolution = float(resolution)
+        self.geometry = list(geometry)
+        self.sources = list(sources)
+        self.boundary_layers = list(boundary_layers)
+        self.default_material = default_material
+        self.Courant = float(Courant)
+        self.eps_averaging = eps_averaging
+        if force_complex_fields or k_point or symmetries:
+            raise NotImplementedError("complex fields / Bloch k_point / symmetries are out of scope")
+        if dimensions is None:
+            dimensions = 3 if self.cell_size.z != 0 else 2
+            if self.cell_size.x == 0 and self.cell_size.y == 0:
+                dimensions = 1
+        self.dimensions = dimensions
+        self.parallel = parallel
+        self.fields = None
+        self.structure = None
+
+    # -- structure
+    def _create_grid_volume(self):
+        sz = self.cell_size
+        sizes = [sz.z] if self.dimensions == 1 else ([sz.x, sz.y] if self.dimensions == 2
+                                                     else [sz.x, sz.y, sz.z])
+        return core.GridVolume.vol(self.dimensions, sizes, self.resolution, center_origin=True)
+
+    def _materials_at(self, gv, c):
+        """Per-point material of E component c (no subpixel averaging)."""
+        pts = gv.coords(c)
+        full = [np.zeros(gv.shape()) for _ in range(3)]
+        k = 0
+        for d in range(3):
+            if gv.has[d]:
+                full[d] = pts[k]
+                k += 1
+        idx = np.full(gv.shape(), -1, dtype=np.int32)
+        for i, g in enumerate(self.geometry):
+            idx[g.contains(*full)] = i
+        mats = [self.default_material] + [g.material for g in self.geometry]
+        return idx + 1, mats
+
+    def _init_structure(self):
+        gv = self._create_grid_volume()
+        s = core.Structure(gv, self.Courant)
+        for layer in self.boundary_layers:
+            if not isinstance(layer, PML):
+                raise NotImplementedError("only PML boundary layers are supported")
+            dirs = (0, 1, 2) if layer.direction == ALL else (layer.direction,)
+            sides = (0, 1) if layer.side == ALL else (layer.side,)
+            s.add_pml(layer.thickness, dirs, sides, layer.R_asymptotic, layer.mean_stretch)
+        media = [self.default_material] + [g.material for g in self.geometry]
+        uniform = len(self.geometry) == 0
+        if self.eps_averaging and not uniform:
+            warnings.warn("eps_averaging (subpixel smoothing) is not implemented; materials are "
+                          "sampled at the Yee points as with eps_averaging=False", RuntimeWarning)
+        need_eps = any(m.epsilon_diag != Vector3(1, 1, 1) or m.epsilon_offdiag != Vector3()
+                       for m in media)
+        need_chi2 = any(m.E_chi2 != 0 for m in media)
+        need_chi3 = any(m.E_chi3 != 0 for m in media)
+        sus_keys = []
+        for m in media:
+            for su in m.E_susceptibilities:
+                if su.key() not in sus_keys:
+                    sus_keys.append(su.key())
+        comps = (Ex,) if self.dimensions == 1 else (Ex, Ey, Ez)
+        sus_sig = {k: [None, None, None] for k in sus_keys}
+        for c in comps:
+            d = c % 3
+            which, mats = self._materials_at(gv, c)
+            def table(f):
+                return np.array([f(m) for m in mats], dtype=np.float64)[which]
+            if need_eps:
+                # chi1inv row of the inverse permittivity tensor of each medium
+                # (Medium.epsilon_diag / epsilon_offdiag = (xy, xz, yz)); the fork only
+                # uses the diagonal value and whether off-diagonal entries are zero.
+                inv = []
+                for m in mats:
+                    e, o = m.epsilon_diag, m.epsilon_offdiag
+                    T = np.array([[e.x, o.x, o.y], [o.x, e.y, o.z], [o.y, o.z, e.z]])
+                    inv.append(np.linalg.inv(T) if any(v != 0 for v in o) else
+                               np.diag([1.0 / e.x, 1.0 / e.y, 1.0 / e.z]))
+                inv = np.array(inv)
+                s.set_chi1inv(c, d, inv[:, d, d][which])
+                if any(m.epsilon_offdiag != Vector3() for m in mats):
+                    for k in (1, 2):
+                        dd = (d + k) % 3
+                        s.set_chi1inv(c, dd, inv[:, d, dd][which])
+            if need_chi3:
+                s.set_chi3(c, table(lambda m: m.E_chi3))
+            if need_chi2:
+                s.set_chi2(c, table(lambda m: m.E_chi2))
+            for key in sus_keys:
+                def sig(m, key=key):
+                    for su in m.E_susceptibilities:
+                        if su.key() == key:
+                            return su.sigma_diag[d]
+                    return 0.0
+                sus_sig[key][d] = table(sig)
+        for key in sus_keys:
+            s.add_lorentzian(key[0], key[1], sus_sig[key], drude=key[2])
+        self.structure = s
+        return s
+
+    def init_sim(self):
+        if self.fields is not None:
+            return
+        if self.structure is None:
+            self._init_structure()
+        ctx = _dist_context() if self.parallel is not False else None
+        if ctx:
+            rank, world, local, nid = ctx
+            self.fields = core.Fields(self.structure, device=local, rank=rank, nranks=world,
+                                      nccl_id=nid)
+        else:
+            self.fields = core.Fields(self.structure)
+        for src in self.sources:
+            src.add_source(self.fields)
+
+    # -- time
+    def meep_time(self):
+        self.init_sim()
+        return self.fields.time()
+
+    def round_time(self):
+        self.init_sim()
+        return self.fields.round_time()
+
+    @property
+    def timestep(self):
+        self.init_sim()
+        return self.fields.t
+
+    # -- running
+    def run(self, *step_funcs, until=None):
+        """Simulation.run(until=T) / _run_until (python/simulation.py:2795-2855)."""
+        self.init_sim()
+        if until is None:
+            raise ValueError("run() needs until=")
+        t, dt = self.fields._time()
+        t0 = float(np.float32(t * dt))
+        stop = t0 + until
+        if not step_funcs:
+            n = 0
+            while float(np.float32((t + n) * dt)) < stop:
+                n += 1
+            self.fields.step(n)
+            return
+        while self.round_time() < stop:
+            for fn in step_funcs:
+                fn(self)
+            self.fields.step(1)
+        for fn in step_funcs:
+            fn(self)
+
+    # -- monitors
+    def get_field_point(self, c, pt):
+        self.init_sim()
+        return self.fields.get_field(c, tuple(pt))
+
+    def get_array(self, component=Ez):
+        self.init_sim()
+        return self.fields.get_array(component)

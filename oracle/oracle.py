@@ -167,6 +167,12 @@ class Oracle:
                             is_integrated=False):
         self.add_point_source(comp, 0, [freq, width, start, end], pos, amp, is_integrated)
 
+    def add_continuous_source(self, comp, freq, width, start, end, slowness, pos, amp=1.0,
+                              is_integrated=False):
+        f = complex(freq)
+        self.add_point_source(comp, 1, [f.real, f.imag, width, start, end, slowness], pos, amp,
+                              is_integrated)
+
     def legacy_point_source(self, comp, freq, width, peaktime, cutoff, pos, amp):
         """fields::add_point_source(c, freq, width, peaktime, cutoff, vec, amp) -- the
         deprecated C++ form used by tests/known_results.cpp (src/sources.cpp:189-211).

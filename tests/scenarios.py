@@ -1,0 +1,266 @@
+"""Identical scenarios for the CPU oracle and the HIP product (parity tests).
+
+Both backends expose the same small interface (add_pml, set_chi1inv,
+set_chi2, set_chi3, add_lorentzian, add_gaussian_source,
+add_continuous_source, legacy_point_source, step, get_field, get_array,
+center, t, dt, time, round_time).  Sizes are chosen so the oracle finishes
+in seconds.
+"""
+import math
+
+import numpy as np
+
+from oracle import oracle as orc
+
+E_COMPS = (0, 1, 2)
+ALL_COMPS = tuple(range(12))
+
+
+def make_oracle(dim, n, a, courant=0.5, io=(0, 0, 0)):
+    return orc.Oracle(dim, n, a, courant, io)
+
+
+class ProductSim:
+    """Adapter: meep_nl_amd.core Structure + Fields behind the oracle interface."""
+
+    def __init__(self, dim, n, a, courant=0.5, io=(0, 0, 0)):
+        from meep_nl_amd import core
+        self.core = core
+        self.gv = core.GridVolume(dim, n, a, io)
+        self.s = core.Structure(self.gv, courant)
+        self.f = None
+        self.dim = dim
+
+    def _fields(self):
+        if self.f is None:
+            self.f = self.core.Fields(self.s)
+        return self.f
+
+    def shape(self):
+        return self.gv.shape()
+
+    def coords(self, c):
+        return self.gv.coords(c)
+
+    def center(self):
+        return self.gv.center()
+
+    def add_pml(self, *a, **k):
+        self.s.add_pml(*a, **k)
+
+    def set_chi1inv(self, c, d, arr):
+        self.s.set_chi1inv(c, d, arr)
+
+    def set_chi2(self, c, arr):
+        self.s.set_chi2(c, arr)
+
+    def set_chi3(self, c, arr):
+        self.s.set_chi3(c, arr)
+
+    def add_lorentzian(self, *a, **k):
+        self.s.add_lorentzian(*a, **k)
+
+    def add_gaussian_source(self, *a, **k):
+        self._fields().add_gaussian_source(*a, **k)
+
+    def add_continuous_source(self, *a, **k):
+        self._fields().add_continuous_source(*a, **k)
+
+    def legacy_point_source(self, *a, **k):
+        self._fields().legacy_point_source(*a, **k)
+
+    def require_component(self, c):
+        self._fields().require_component(c)
+
+    def step(self, n=1):
+        self._fields().step(n)
+
+    def get_field(self, c, p):
+        return self._fields().get_field(c, p)
+
+    def get_array(self, c):
+        return self._fields().get_array(c)
+
+    @property
+    def t(self):
+        return self._fields().t
+
+    @property
+    def dt(self):
+        return self._fields().dt
+
+    def time(self):
+        return self._fields().time()
+
+    def round_time(self):
+        return self._fields().round_time()
+
+    def nr_random_fallbacks(self):
+        return self._fields().nr_fallbacks()
+
+
+def vol(make, dim, sizes, a, center_origin=False, courant=0.5):
+    n = [0, 0, 0]
+    if dim == 1:
+        n[2] = int(sizes[0] * a + 0.5)
+    elif dim == 2:
+        n[0] = int(sizes[0] * a + 0.5)
+        n[1] = int(sizes[1] * a + 0.5)
+    else:
+        n = [int(s * a + 0.5) for s in sizes]
+    io = [-(v - (v & 1)) for v in n] if center_origin else [0, 0, 0]
+    return make(dim, n, a, courant, io)
+
+
+# ------------------------------------------------------------------ scenarios
+# Each returns the simulation object after stepping.
+
+def sc_cfg1(make, steps=500):
+    """Config 1 (BASELINE configs[0]): 2-D 200x200 vacuum, Ez Gaussian current at the
+    origin, metallic walls, real fields."""
+    o = vol(make, 2, [20, 20], 10, center_origin=True)
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0, 0), 1.0, is_integrated=False)
+    o.step(steps)
+    return o
+
+
+def sc_vacuum_pml_3d(make, L=3.2, steps=60, dpml=1.0):
+    """Config 2 shape scaled down: vacuum box + PML on all faces, Ez Gaussian current at
+    (0.05,0.05,0.05)."""
+    o = vol(make, 3, [L, L, L], 10, center_origin=True)
+    o.add_pml(dpml)
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    o.step(steps)
+    return o
+
+
+def sc_waveguide_3d(make, L=3.2, steps=40, eps=12.0):
+    """Config 3 shape scaled down: eps=12 core |y|,|z| < 0.5 along x, PML, no averaging."""
+    o = vol(make, 3, [L, L, L], 10, center_origin=True)
+    o.add_pml(1.0)
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        e = np.where((np.abs(y) < 0.5) & (np.abs(z) < 0.5), eps, 1.0)
+        o.set_chi1inv(c, c, 1.0 / e)
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    o.step(steps)
+    return o
+
+
+def sc_kerr_lorentz_3d(make, L=3.2, steps=60):
+    """Config 4 shape scaled down: slab |z|<0.6 eps 2.25, chi3 1e-2 (inert in the fork),
+    Lorentzian(1.1, 0.05, sigma 0.5), PML, Ex Gaussian at z=-1.0, amp 50."""
+    o = vol(make, 3, [L, L, L], 10, center_origin=True)
+    o.add_pml(1.0)
+    sig = []
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        inside = np.abs(z) < 0.6
+        o.set_chi1inv(c, c, np.where(inside, 1 / 2.25, 1.0))
+        o.set_chi3(c, np.where(inside, 1e-2, 0.0))
+        sig.append(np.where(inside, 0.5, 0.0))
+    o.add_lorentzian(1.1, 0.05, sig)
+    o.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -1.0), 50.0)
+    o.step(steps)
+    return o
+
+
+def sc_nr_probe(make, c2=0.5, steps=40):
+    """SURVEY.md 8(c) chi(2) Newton-Raphson probe (integrated legacy source)."""
+    o = vol(make, 3, [1, 1, 1], 10)
+    for c in E_COMPS:
+        for d in range(3):
+            o.set_chi1inv(c, d, np.full(o.shape(), 0.25 if d == c else 1e-3))
+        if c2:
+            o.set_chi2(c, np.full(o.shape(), c2))
+    cen = o.center()
+    o.legacy_point_source(2, 0.5, 0.5, 0.0, 3.0, [cen[0] + 0.05, cen[1] + 0.05, cen[2] + 0.05],
+                          5.0)
+    o.step(steps)
+    return o
+
+
+def sc_nr_pml_dispersive(make, steps=30):
+    """chi2 NR next to a PML with a Lorentzian background and an integrated source
+    (exercises the zone tables and the split E / P kernels)."""
+    o = vol(make, 3, [2.6, 2.6, 2.6], 10, center_origin=True)
+    o.add_pml(0.6)
+    sig = []
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        inside = (np.abs(x) < 0.5) & (np.abs(y) < 0.5) & (np.abs(z) < 0.5)
+        for d in range(3):
+            if d == c:
+                o.set_chi1inv(c, d, np.where(inside, 0.25, 1.0))
+            else:
+                o.set_chi1inv(c, d, np.where(inside, 1e-3, 0.0))
+        o.set_chi2(c, np.where(inside, 0.5, 0.0))
+        sig.append(np.where(np.abs(z) < 0.3, 0.2, 0.0))
+    o.add_lorentzian(0.9, 0.1, sig)
+    o.legacy_point_source(2, 0.5, 0.5, 0.0, 3.0, (0.05, 0.05, 0.05), 5.0)
+    o.step(steps)
+    return o
+
+
+def sc_known_metallic_3d(make):
+    o = vol(make, 3, [1, 1, 1], 10)
+    o.legacy_point_source(2, 0.2, 3.0, 0.0, 2.0, o.center(), complex(0, -2 * math.pi * 0.2))
+    while o.round_time() < 10.0:
+        o.step()
+    return o
+
+
+def sc_known_pml_2d(make):
+    o = vol(make, 2, [3, 3], 10)
+    o.add_pml(1.0)
+    o.legacy_point_source(2, 0.2, 3.0, 0.0, 2.0, o.center(), complex(0, -2 * math.pi * 0.2))
+    n = 0
+    while float(np.float32((n) * (0.5 / 10))) < 30.0:
+        n += 1
+    o.step(n)
+    return o
+
+
+def sc_polariton_1d(make):
+    o = vol(make, 1, [1], 10)
+    o.add_lorentzian(0.3, 0.1, [np.full(o.shape(), 7.63), None, None])
+    o.legacy_point_source(0, 0.2, 3.0, 0.0, 2.0, o.center(), complex(0, -2 * math.pi * 0.2))
+    n = 0
+    while float(np.float32(n * (0.5 / 10))) < 10.0:
+        n += 1
+    o.step(n)
+    return o
+
+
+def sc_te_magnetic_2d(make, steps=80):
+    """2-D TE (Hz source, non-integrated magnetic current) + one-sided PML, odd grid."""
+    o = vol(make, 2, [2.3, 1.9], 10)
+    o.add_pml(0.5, dirs=(0,), sides=(1,))
+    o.add_pml(0.4, dirs=(1,), sides=(0,))
+    o.add_gaussian_source(5, 0.4, 3.0, 0.0, 30.0, (1.03, 0.77), 2.0)
+    o.add_continuous_source(5, 0.3, 2.0, 0.0, 1e20, 3.0, (0.5, 1.2), 0.7)
+    o.step(steps)
+    return o
+
+
+def sc_multi_source_3d(make, steps=50):
+    """Several sources: off-grid position (interpolation weights), duplicate
+    (merged amplitudes), integrated + current, magnetic, near the PML edge."""
+    o = vol(make, 3, [3.0, 2.6, 2.2], 10, center_origin=True)
+    o.add_pml(0.8)
+    o.add_gaussian_source(2, 0.2, 4.0, 0.0, 40.0, (0.013, -0.037, 0.021), 1.0)
+    o.add_gaussian_source(2, 0.2, 4.0, 0.0, 40.0, (0.013, -0.037, 0.021), 0.5)
+    o.add_gaussian_source(0, 0.25, 4.0, 0.0, 40.0, (0.3, 0.2, -0.1), 1.0, is_integrated=True)
+    o.add_gaussian_source(4, 0.3, 4.0, 0.0, 40.0, (-0.2, 0.1, 0.15), complex(0.3, 0.7))
+    o.add_gaussian_source(1, 0.3, 4.0, 0.0, 40.0, (1.0, -0.7, 0.6), 1.0)
+    o.step(steps)
+    return o
+
+
+def compare_all(a, b, comps=ALL_COMPS):
+    """Max abs difference per component between two backends."""
+    out = {}
+    for c in comps:
+        x, y = a.get_array(c), b.get_array(c)
+        out[c] = float(np.max(np.abs(x - y))) if x.size else 0.0
+    return out

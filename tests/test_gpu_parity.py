@@ -1,0 +1,107 @@
+"""GPU parity: HIP product path vs the CPU oracle on identical inputs.
+
+Tolerance: the product is compiled with -ffp-contract=off and follows the
+reference's expression order, so arrays are required to be BITWISE equal
+(max |diff| == 0).  Golden reference values (tests/golden) are required bit
+for bit as well, except known_results (rel 1e-5 as in the reference test).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from scenarios import (ALL_COMPS, ProductSim, compare_all, make_oracle, sc_cfg1,
+                       sc_kerr_lorentz_3d, sc_known_metallic_3d, sc_known_pml_2d,
+                       sc_multi_source_3d, sc_nr_pml_dispersive, sc_nr_probe, sc_polariton_1d,
+                       sc_te_magnetic_2d, sc_vacuum_pml_3d, sc_waveguide_3d)
+
+pytestmark = pytest.mark.gpu
+
+
+def _bitwise(prod, orc, comps=ALL_COMPS):
+    diffs = compare_all(prod, orc, comps)
+    bad = {c: d for c, d in diffs.items() if d != 0.0}
+    assert not bad, f"max|diff| per component: {bad}"
+
+
+def test_cfg1_golden_and_arrays(golden):
+    g = golden["survey_cfg1"]
+    p = sc_cfg1(ProductSim)
+    assert p.get_field(2, (0.5, 0.3)) == g["ez_0p5_0p3"]
+    assert p.get_field(2, (0.0, 0.0)) == g["ez_0_0"]
+    ss = 0.0
+    for ix in range(-95, 96, 5):
+        for iy in range(-95, 96, 5):
+            v = p.get_field(2, (ix * 0.1, iy * 0.1))
+            ss += v * v
+    assert ss == g["sumsq_39x39"]
+    o = sc_cfg1(make_oracle, steps=500)
+    _bitwise(p, o, comps=(2, 3, 4, 8, 9, 10))
+
+
+def test_vacuum_pml_3d():
+    _bitwise(sc_vacuum_pml_3d(ProductSim), sc_vacuum_pml_3d(make_oracle))
+
+
+def test_waveguide_3d():
+    _bitwise(sc_waveguide_3d(ProductSim), sc_waveguide_3d(make_oracle))
+
+
+def test_kerr_lorentz_3d():
+    _bitwise(sc_kerr_lorentz_3d(ProductSim), sc_kerr_lorentz_3d(make_oracle))
+
+
+def test_nr_probe_golden(golden):
+    g = golden["survey_nr"]
+    for c2, key in ((0.0, "ex_chi2_0"), (0.5, "ex_chi2_0p5")):
+        p = sc_nr_probe(ProductSim, c2)
+        cen = p.center()
+        v = p.get_field(0, [cen[0] + 0.21, cen[1] + 0.13, cen[2] + 0.07])
+        assert v == g[key]
+        assert p.nr_random_fallbacks() == 0
+        _bitwise(p, sc_nr_probe(make_oracle, c2))
+
+
+def test_nr_pml_dispersive():
+    _bitwise(sc_nr_pml_dispersive(ProductSim), sc_nr_pml_dispersive(make_oracle))
+
+
+def test_known_results(golden):
+    kr = golden["known_results"]
+    p = sc_known_metallic_3d(ProductSim)
+    v = p.get_field(2, p.center())
+    assert abs(v - kr["metallic_3d_ez"]) < abs(kr["metallic_3d_ez"]) * kr["rel_tol"]
+    p = sc_known_pml_2d(ProductSim)
+    v = p.get_field(2, p.center())
+    assert abs(v - kr["pml_2d_tm_ez"]) < abs(kr["pml_2d_tm_ez"]) * kr["rel_tol"]
+    _bitwise(p, sc_known_pml_2d(make_oracle), comps=(2, 3, 4, 8, 9, 10))
+
+
+def test_polariton_1d(golden):
+    kr = golden["known_results"]
+    p = sc_polariton_1d(ProductSim)
+    v = p.get_field(0, p.center())
+    assert abs(v - kr["polariton_1d_ex"]) < abs(kr["polariton_1d_ex"]) * kr["rel_tol"]
+    _bitwise(p, sc_polariton_1d(make_oracle), comps=(0, 4, 6, 10))
+
+
+def test_te_magnetic_2d():
+    _bitwise(sc_te_magnetic_2d(ProductSim), sc_te_magnetic_2d(make_oracle),
+             comps=(0, 1, 5, 6, 7, 11))
+
+
+def test_multi_source_3d():
+    _bitwise(sc_multi_source_3d(ProductSim), sc_multi_source_3d(make_oracle))
+
+
+def test_simulation_api_matches_core():
+    import meep_nl_amd as mp
+    sim = mp.Simulation(cell_size=mp.Vector3(2.0, 2.0, 0), resolution=10,
+                        sources=[mp.Source(mp.GaussianSource(0.15, fwidth=0.1), mp.Ez,
+                                           center=mp.Vector3())])
+    sim.run(until=5.0)
+    p = ProductSim(2, [20, 20, 0], 10, 0.5, [-20, -20, 0])
+    p.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0, 0), 1.0)
+    p.step(sim.timestep)
+    np.testing.assert_array_equal(sim.get_array(mp.Ez), p.get_array(2))
+    assert sim.meep_time() == pytest.approx(sim.timestep * 0.05)
