@@ -98,6 +98,14 @@ mnl_fields *mnl_fields_create(mnl_structure *s, int device);
 mnl_fields *mnl_fields_create_dist(mnl_structure *s, int device, int rank, int nranks,
                                    const void *nccl_id);
 int mnl_comm_unique_id(void *out128);
+/* Several slabs of one grid in ONE process on one device (one host thread per
+ * slab calling mnl_fields_step concurrently): same decomposition and exchange
+ * code as mnl_fields_create_dist, transport = device copies + host barriers.
+ * Used to validate the multi-GPU path on a single MI355X. */
+void *mnl_local_hub_create(int nranks);
+void mnl_local_hub_destroy(void *hub);
+mnl_fields *mnl_fields_create_local(mnl_structure *s, int device, int rank, int nranks,
+                                    void *hub);
 void mnl_fields_destroy(mnl_fields *f);
 
 /* add_volume_source(c, src_time, volume(p,p), amp) for a point p

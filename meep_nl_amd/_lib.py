@@ -31,6 +31,9 @@ _SIGS = {
     "mnl_fields_create": (c_void, [c_void, c_int]),
     "mnl_fields_create_dist": (c_void, [c_void, c_int, c_int, c_int, ctypes.c_char_p]),
     "mnl_comm_unique_id": (c_int, [ctypes.c_char_p]),
+    "mnl_local_hub_create": (c_void, [c_int]),
+    "mnl_local_hub_destroy": (None, [c_void]),
+    "mnl_fields_create_local": (c_void, [c_void, c_int, c_int, c_int, c_void]),
     "mnl_fields_destroy": (None, [c_void]),
     "mnl_fields_add_point_source": (c_int, [c_void, c_int, c_int, dptr, c_int, dptr, c_double,
                                             c_double, c_int]),

@@ -137,10 +137,12 @@ class Structure:
 class Fields:
     """meep::fields with use_real_fields() on one MI355X (or one z-slab of it)."""
 
-    def __init__(self, structure, device=-1, rank=0, nranks=1, nccl_id=None):
+    def __init__(self, structure, device=-1, rank=0, nranks=1, nccl_id=None, hub=None):
         self.s = structure
         self.gv = structure.gv
-        if nranks > 1:
+        if nranks > 1 and hub is not None:
+            self.h = lib().mnl_fields_create_local(structure.h, device, rank, nranks, hub.h)
+        elif nranks > 1:
             self.h = lib().mnl_fields_create_dist(structure.h, device, rank, nranks, nccl_id)
         else:
             self.h = lib().mnl_fields_create(structure.h, device)
@@ -258,6 +260,20 @@ class Fields:
         c = ctypes.c_double()
         check(lib().mnl_fields_traffic_model(self.h, ctypes.byref(b), ctypes.byref(c)))
         return b.value, c.value
+
+
+class LocalHub:
+    """In-process slab group (mnl_local_hub_create): several z-slabs of one grid on
+    one GPU, stepped by one host thread each."""
+
+    def __init__(self, nranks):
+        self.h = lib().mnl_local_hub_create(int(nranks))
+        self.nranks = nranks
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().mnl_local_hub_destroy(self.h)
+            self.h = None
 
 
 def device_count():

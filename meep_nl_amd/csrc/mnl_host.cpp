@@ -158,6 +158,7 @@ struct mnl_fields {
   std::vector<void *> dev_allocs;
   Box interior;
   std::vector<Box> shell;
+  BoxList shell_list;
   CurlPlan planB, planD;
   bool nr = false;
   // sources
@@ -351,6 +352,22 @@ void setup_grid(mnl_fields *F) {
   g.st[2] = p0 * g.N[1];
   F->nlocal = size_t(p0) * g.N[1] * g.N[2];
   for (int d = 0; d < 3; d++) g.sdir[d] = g.ax[d] >= 0 ? g.st[g.ax[d]] : 0;
+}
+
+void make_shell_list(mnl_fields *F) {
+  BoxList &bl = F->shell_list;
+  memset(&bl, 0, sizeof(bl));
+  long long acc = 0;
+  for (auto &b : F->shell) {
+    bool emp = false;
+    for (int k = 0; k < 3; k++) emp = emp || b.hi[k] < b.lo[k];
+    if (emp) continue;
+    bl.b[bl.n] = b;
+    bl.start[bl.n] = acc;
+    acc += (long long)(b.hi[0] - b.lo[0] + 1) * (b.hi[1] - b.lo[1] + 1) * (b.hi[2] - b.lo[2] + 1);
+    bl.n++;
+  }
+  bl.start[bl.n] = acc;
 }
 
 void setup_boxes(mnl_fields *F) {
@@ -1037,7 +1054,7 @@ int exchange(mnl_fields *F, int kind) {
       if (up >= 0 && cm.recv(it.p + (size_t)nloc * plane, plane, up, F->stream)) return -1;
     }
   }
-  return cm.group_end();
+  return cm.group_end(F->stream);
 }
 
 // ------------------------------------------------------------- stepping
@@ -1143,23 +1160,21 @@ int step_batch(mnl_fields *F, int nsteps) {
         if (exchange(F, 0)) return fail("E halo exchange failed");
         ev_end(k);
       }
+      const BoxList *sl = &F->shell_list;
       int k = ev_begin(TM_BINT);
-      if (k_curl(T_B, false, F->interior, g, f, F->planB, F->S.courant, F->stream))
+      if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream))
         return fail("curl B launch failed");
       ev_end(k);
       k = ev_begin(TM_B);
-      for (auto &b : F->shell)
-        if (k_curl(T_B, true, b, g, f, F->planB, F->S.courant, F->stream))
-          return fail("curl B launch failed");
+      if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream))
+        return fail("curl B launch failed");
       ev_end(k);
       if (nB && k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
       // ---- H
       k = ev_begin(TM_H);
       bool anyH = false;
       for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
-      if (anyH)
-        for (auto &b : F->shell)
-          if (k_update_h(b, g, f, F->stream)) return fail("update H launch failed");
+      if (anyH && k_update_h(*sl, g, f, F->stream)) return fail("update H launch failed");
       ev_end(k);
       if (F->nranks > 1) {
         int kk = ev_begin(TM_HALO);
@@ -1168,13 +1183,12 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       // ---- D
       k = ev_begin(TM_DINT);
-      if (k_curl(T_D, false, F->interior, g, f, F->planD, F->S.courant, F->stream))
+      if (k_curl(T_D, F->interior, nullptr, g, f, F->planD, F->S.courant, F->stream))
         return fail("curl D launch failed");
       ev_end(k);
       k = ev_begin(TM_D);
-      for (auto &b : F->shell)
-        if (k_curl(T_D, true, b, g, f, F->planD, F->S.courant, F->stream))
-          return fail("curl D launch failed");
+      if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream))
+        return fail("curl D launch failed");
       ev_end(k);
       if (nD && k_source(T_D, g, f, sD, 0, F->stream)) return fail("source launch failed");
       if (F->nr && F->nranks > 1) {
@@ -1183,14 +1197,13 @@ int step_batch(mnl_fields *F, int nsteps) {
       // ---- E (+ Lorentzian P)
       k = ev_begin(TM_E);
       bool fuse = !F->nr;
-      if (k_update_e(false, F->interior, g, f, is, 0, fuse, F->stream))
+      if (k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream) ||
+          k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream))
         return fail("update E launch failed");
-      for (auto &b : F->shell)
-        if (k_update_e(true, b, g, f, is, 0, fuse, F->stream)) return fail("update E launch failed");
       if (!fuse && f.npol) {
-        if (k_update_pols(F->interior, g, f, F->stream)) return fail("pols launch failed");
-        for (auto &b : F->shell)
-          if (k_update_pols(b, g, f, F->stream)) return fail("pols launch failed");
+        if (k_update_pols(F->interior, nullptr, g, f, F->stream) ||
+            k_update_pols(F->interior, sl, g, f, F->stream))
+          return fail("pols launch failed");
       }
       ev_end(k);
     }
@@ -1229,13 +1242,15 @@ int finalize_fields(mnl_fields *F) {
   if (upload_pml(F)) return -1;
   if (setup_materials(F)) return -1;
   setup_boxes(F);
+  make_shell_list(F);
   if (dev_alloc(F, &F->d_nr_fallbacks, 1)) return -1;
   F->f.nr_fallbacks = F->d_nr_fallbacks;
   make_plans(F);
   return 0;
 }
 
-mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, const void *id) {
+mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, const void *id,
+                          LocalHub *hub = nullptr) {
   if (!s) {
     fail("null structure");
     return nullptr;
@@ -1265,8 +1280,8 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   F->nranks = nranks;
   if (nranks > 1) {
     F->comm.reset(new Comm());
-    if (F->comm->init(rank, nranks, id)) {
-      fail("RCCL communicator init failed");
+    if (hub ? F->comm->init_local(rank, nranks, hub) : F->comm->init(rank, nranks, id)) {
+      fail(hub ? "local slab group init failed" : "RCCL communicator init failed");
       return nullptr;
     }
   }
@@ -1408,6 +1423,22 @@ mnl_fields *mnl_fields_create_dist(mnl_structure *s, int device, int rank, int n
     return nullptr;
   }
   return create_common(s, device, rank, nranks, id);
+}
+void *mnl_local_hub_create(int nranks) {
+  if (nranks < 1) {
+    fail("bad nranks");
+    return nullptr;
+  }
+  return local_hub_create(nranks);
+}
+void mnl_local_hub_destroy(void *hub) { local_hub_destroy((LocalHub *)hub); }
+mnl_fields *mnl_fields_create_local(mnl_structure *s, int device, int rank, int nranks,
+                                    void *hub) {
+  if (!hub || nranks < 1 || rank < 0 || rank >= nranks) {
+    fail("bad rank/nranks/hub");
+    return nullptr;
+  }
+  return create_common(s, device, rank, nranks, nullptr, (LocalHub *)hub);
 }
 int mnl_comm_unique_id(void *out128) { return Comm::unique_id(out128) ? fail("ncclGetUniqueId failed") : 0; }
 

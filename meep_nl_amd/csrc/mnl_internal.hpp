@@ -26,6 +26,14 @@ struct Box {
   int hi[3];
 };
 
+// Shell boxes of one sub-step, launched together: thread t belongs to box b
+// with start[b] <= t < start[b+1] and is unravelled axis-0 fastest inside it.
+struct BoxList {
+  int n;
+  Box b[MAX_BOX - 1];
+  long long start[MAX_BOX];
+};
+
 struct DevGrid {
   int dim;
   int ax[3];            // device axis of direction X,Y,Z (-1 = absent)
@@ -103,12 +111,14 @@ struct Launch {
   void *stream;  // hipStream_t
 };
 
-int k_curl(int ft, bool shell, const Box &b, const DevGrid &g, const DevFields &f,
+// interior: one box on a 3-D grid; shell: all shell boxes in one launch
+int k_curl(int ft, const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
            const CurlPlan &p, double courant, void *stream);
-int k_update_h(const Box &b, const DevGrid &g, const DevFields &f, void *stream);
-int k_update_e(bool shell, const Box &b, const DevGrid &g, const DevFields &f,
+int k_update_h(const BoxList &shell, const DevGrid &g, const DevFields &f, void *stream);
+int k_update_e(const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
                const ISrcDev &is, int step, bool fuse_pols, void *stream);
-int k_update_pols(const Box &b, const DevGrid &g, const DevFields &f, void *stream);
+int k_update_pols(const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
+                  void *stream);
 int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int step,
              void *stream);
 int k_fill(double *p, double v, size_t n, void *stream);

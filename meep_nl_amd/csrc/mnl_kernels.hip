@@ -42,6 +42,32 @@ __device__ __forceinline__ bool make_pt(const Box &b, const DevGrid &g, Pt &p) {
   return true;
 }
 
+__device__ __forceinline__ bool make_pt_lin(const BoxList &bl, const DevGrid &g, Pt &p) {
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= bl.start[bl.n]) return false;
+  int k = 0;
+#pragma unroll
+  for (int q = 1; q < MAX_BOX - 1; q++)
+    if (q < bl.n && t >= bl.start[q]) k = q;
+  const Box &b = bl.b[k];
+  long long l = t - bl.start[k];
+  const long long n0 = b.hi[0] - b.lo[0] + 1, n1 = b.hi[1] - b.lo[1] + 1;
+  int i0 = b.lo[0] + (int)(l % n0);
+  l /= n0;
+  int i1 = b.lo[1] + (int)(l % n1);
+  int i2 = b.lo[2] + (int)(l / n1);
+  int ii[3] = {i0, i1, i2};
+#pragma unroll
+  for (int d = 0; d < 3; d++) p.j[d] = g.ax[d] >= 0 ? ii[g.ax[d]] : 0;
+  p.idx = (long long)i0 + (long long)i1 * g.st[1] + (long long)i2 * g.st[2];
+  return true;
+}
+
+template <bool SHELL>
+__device__ __forceinline__ bool map_pt(const Box &b, const BoxList &bl, const DevGrid &g, Pt &p) {
+  return SHELL ? make_pt_lin(bl, g, p) : make_pt(b, g, p);
+}
+
 // little_owned_corner0 .. big_corner (src/meep/vec.hpp:1102-1104), with the
 // metallic wall plane left untouched (it is zeroed by zero_metal in the
 // reference, src/boundaries.cpp:304-339, and never becomes nonzero).
@@ -73,10 +99,10 @@ __device__ __forceinline__ bool pml_at(const DevFields &f, const DevGrid &g, int
 // B (D): g1 = E (H) comp (d+2)%3 along dir (d+1)%3, g2 = comp (d+1)%3 along
 // dir (d+2)%3; D uses negated strides (src/step_db.cpp:81-84).
 template <int FT, bool SHELL>
-__global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, DevGrid g, DevFields f,
-                                                               CurlPlan pl, double C) {
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl, DevGrid g,
+                                                               DevFields f, CurlPlan pl, double C) {
   Pt p;
-  if (!make_pt(b, g, p)) return;
+  if (!map_pt<SHELL>(b, bl, g, p)) return;
   const long long i = p.idx;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
@@ -146,9 +172,9 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, DevGrid g, 
 // ----------------------------------------------------------------- H from B
 // update_eh(H_stuff) in PML chunks: W auxiliary field, mu = 1
 // (src/update_eh.cpp:186-259, src/step_generic.cpp:717-724).
-__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_h_kernel(Box b, DevGrid g, DevFields f) {
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_h_kernel(BoxList bl, DevGrid g, DevFields f) {
   Pt p;
-  if (!make_pt(b, g, p)) return;
+  if (!make_pt_lin(bl, g, p)) return;
   const long long i = p.idx;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
@@ -302,10 +328,11 @@ __device__ __forceinline__ double dmp_at(const DevFields &f, const ISrcDev &is, 
 // src/step_generic.cpp:576-906) + lorentzian update_P (src/susceptibility.cpp:
 // 188-262) fused when no Newton-Raphson neighbour reads are needed.
 template <bool SHELL, bool NR, bool ISRC, bool FUSEPOL>
-__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, DevGrid g, DevFields f,
-                                                                   ISrcDev is, int step) {
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList bl, DevGrid g,
+                                                                   DevFields f, ISrcDev is,
+                                                                   int step) {
   Pt p;
-  if (!make_pt(b, g, p)) return;
+  if (!map_pt<SHELL>(b, bl, g, p)) return;
   const long long i = p.idx;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
@@ -406,9 +433,10 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, DevGrid
 // lorentzian update_P, isotropic (src/susceptibility.cpp:251-258), used after
 // the Newton-Raphson E update (which reads neighbouring D - P).
 template <bool SHELL>
-__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, DevGrid g, DevFields f) {
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, BoxList bl, DevGrid g,
+                                                                      DevFields f) {
   Pt p;
-  if (!make_pt(b, g, p)) return;
+  if (!map_pt<SHELL>(b, bl, g, p)) return;
   const long long i = p.idx;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
@@ -521,67 +549,94 @@ static bool empty(const Box &b) {
 }
 static int rc() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 
-int k_curl(int ft, bool shell, const Box &b, const DevGrid &g, const DevFields &f,
+static dim3 lin_grid(const BoxList &bl) {
+  long long n = bl.start[bl.n];
+  return dim3((unsigned)((n + 255) / 256));
+}
+
+int k_curl(int ft, const Box &in, const BoxList *sh, const DevGrid &g, const DevFields &f,
            const CurlPlan &p, double courant, void *stream) {
-  if (empty(b)) return 0;
-  dim3 blk(MNL_BX, MNL_BY), grd = grid_for(b);
   hipStream_t s = (hipStream_t)stream;
-  if (ft == T_B) {
-    if (shell)
-      curl_kernel<T_B, true><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+  BoxList none{};
+  if (!sh) {
+    if (empty(in)) return 0;
+    dim3 blk(MNL_BX, MNL_BY), grd = grid_for(in);
+    if (ft == T_B)
+      curl_kernel<T_B, false><<<grd, blk, 0, s>>>(in, none, g, f, p, courant);
     else
-      curl_kernel<T_B, false><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+      curl_kernel<T_D, false><<<grd, blk, 0, s>>>(in, none, g, f, p, courant);
   } else {
-    if (shell)
-      curl_kernel<T_D, true><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+    if (sh->n == 0 || sh->start[sh->n] == 0) return 0;
+    if (ft == T_B)
+      curl_kernel<T_B, true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f, p, courant);
     else
-      curl_kernel<T_D, false><<<grd, blk, 0, s>>>(b, g, f, p, courant);
+      curl_kernel<T_D, true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f, p, courant);
   }
   return rc();
 }
 
-int k_update_h(const Box &b, const DevGrid &g, const DevFields &f, void *stream) {
-  if (empty(b)) return 0;
-  update_h_kernel<<<grid_for(b), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(b, g, f);
+int k_update_h(const BoxList &sh, const DevGrid &g, const DevFields &f, void *stream) {
+  if (sh.n == 0 || sh.start[sh.n] == 0) return 0;
+  update_h_kernel<<<lin_grid(sh), 256, 0, (hipStream_t)stream>>>(sh, g, f);
   return rc();
+}
+
+template <bool SHELL, bool NR, bool ISRC, bool FUSE>
+static void launch_e1(const Box &in, const BoxList &bl, const DevGrid &g, const DevFields &f,
+                      const ISrcDev &is, int step, hipStream_t s) {
+  if (SHELL)
+    update_e_kernel<true, NR, ISRC, FUSE><<<lin_grid(bl), 256, 0, s>>>(in, bl, g, f, is, step);
+  else
+    update_e_kernel<false, NR, ISRC, FUSE><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(
+        in, bl, g, f, is, step);
 }
 
 template <bool SHELL>
-static void launch_e(const Box &b, const DevGrid &g, const DevFields &f, const ISrcDev &is,
-                     int step, bool fuse, hipStream_t s) {
-  dim3 blk(MNL_BX, MNL_BY), grd = grid_for(b);
+static void launch_e(const Box &in, const BoxList &bl, const DevGrid &g, const DevFields &f,
+                     const ISrcDev &is, int step, bool fuse, hipStream_t s) {
   const bool nr = f.nr_enabled != 0, isrc = is.n > 0;
   if (nr) {
     if (isrc)
-      update_e_kernel<SHELL, true, true, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+      launch_e1<SHELL, true, true, false>(in, bl, g, f, is, step, s);
     else
-      update_e_kernel<SHELL, true, false, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+      launch_e1<SHELL, true, false, false>(in, bl, g, f, is, step, s);
   } else if (fuse) {
     if (isrc)
-      update_e_kernel<SHELL, false, true, true><<<grd, blk, 0, s>>>(b, g, f, is, step);
+      launch_e1<SHELL, false, true, true>(in, bl, g, f, is, step, s);
     else
-      update_e_kernel<SHELL, false, false, true><<<grd, blk, 0, s>>>(b, g, f, is, step);
+      launch_e1<SHELL, false, false, true>(in, bl, g, f, is, step, s);
   } else {
     if (isrc)
-      update_e_kernel<SHELL, false, true, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+      launch_e1<SHELL, false, true, false>(in, bl, g, f, is, step, s);
     else
-      update_e_kernel<SHELL, false, false, false><<<grd, blk, 0, s>>>(b, g, f, is, step);
+      launch_e1<SHELL, false, false, false>(in, bl, g, f, is, step, s);
   }
 }
 
-int k_update_e(bool shell, const Box &b, const DevGrid &g, const DevFields &f, const ISrcDev &is,
-               int step, bool fuse_pols, void *stream) {
-  if (empty(b)) return 0;
-  if (shell)
-    launch_e<true>(b, g, f, is, step, fuse_pols, (hipStream_t)stream);
-  else
-    launch_e<false>(b, g, f, is, step, fuse_pols, (hipStream_t)stream);
+int k_update_e(const Box &in, const BoxList *sh, const DevGrid &g, const DevFields &f,
+               const ISrcDev &is, int step, bool fuse_pols, void *stream) {
+  BoxList none{};
+  if (!sh) {
+    if (empty(in)) return 0;
+    launch_e<false>(in, none, g, f, is, step, fuse_pols, (hipStream_t)stream);
+  } else {
+    if (sh->n == 0 || sh->start[sh->n] == 0) return 0;
+    launch_e<true>(in, *sh, g, f, is, step, fuse_pols, (hipStream_t)stream);
+  }
   return rc();
 }
 
-int k_update_pols(const Box &b, const DevGrid &g, const DevFields &f, void *stream) {
-  if (empty(b)) return 0;
-  update_pols_kernel<true><<<grid_for(b), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(b, g, f);
+int k_update_pols(const Box &in, const BoxList *sh, const DevGrid &g, const DevFields &f,
+                  void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  BoxList none{};
+  if (!sh) {
+    if (empty(in)) return 0;
+    update_pols_kernel<false><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(in, none, g, f);
+  } else {
+    if (sh->n == 0 || sh->start[sh->n] == 0) return 0;
+    update_pols_kernel<true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f);
+  }
   return rc();
 }
 

@@ -99,6 +99,84 @@ class ProductSim:
         return self._fields().nr_fallbacks()
 
 
+class GroupSim(ProductSim):
+    """nranks z-slabs (y-slabs in 2-D) of one grid on one GPU, one host thread per
+    slab (mnl_fields_create_local): the multi-GPU decomposition and halo exchange
+    with the RCCL transport swapped for device copies."""
+
+    NRANKS = 2
+
+    def __init__(self, dim, n, a, courant=0.5, io=(0, 0, 0)):
+        super().__init__(dim, n, a, courant, io)
+        self.nranks = self.NRANKS
+        self.fs = None
+
+    def _all(self):
+        if self.fs is None:
+            self.hub = self.core.LocalHub(self.nranks)
+            self.fs = [self.core.Fields(self.s, rank=r, nranks=self.nranks, hub=self.hub)
+                       for r in range(self.nranks)]
+        return self.fs
+
+    def _fields(self):
+        return self._all()[0]
+
+    def _par(self, fn):
+        import threading
+        out = [None] * self.nranks
+        err = []
+
+        def run(r):
+            try:
+                out[r] = fn(self.fs[r])
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+        th = [threading.Thread(target=run, args=(r,)) for r in range(self.nranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            raise err[0]
+        return out
+
+    def add_gaussian_source(self, *a, **k):
+        for f in self._all():
+            f.add_gaussian_source(*a, **k)
+
+    def add_continuous_source(self, *a, **k):
+        for f in self._all():
+            f.add_continuous_source(*a, **k)
+
+    def legacy_point_source(self, *a, **k):
+        for f in self._all():
+            f.legacy_point_source(*a, **k)
+
+    def require_component(self, c):
+        for f in self._all():
+            f.require_component(c)
+
+    def step(self, n=1):
+        self._all()
+        self._par(lambda f: f.step(n))
+
+    def get_field(self, c, p):
+        self._all()
+        vals = self._par(lambda f: f.get_field(c, p))
+        assert all(v == vals[0] for v in vals)
+        return vals[0]
+
+    def get_array(self, c):
+        return sum(f.get_array(c) for f in self._all())
+
+    def nr_random_fallbacks(self):
+        return sum(f.nr_fallbacks() for f in self._all())
+
+
+class GroupSim3(GroupSim):
+    NRANKS = 3
+
+
 def vol(make, dim, sizes, a, center_origin=False, courant=0.5):
     n = [0, 0, 0]
     if dim == 1:
