@@ -142,7 +142,8 @@ def main():
             traffic = None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "curl_kernel<B, interior> (step_db(B_stuff))",
+            "kernel": ("fused_kernel (curl B + curl D + E=chi1inv*D, one pass over the interior)"
+                       if f.fused_active() else "curl_kernel<B, interior> (step_db(B_stuff))"),
             "bytes_per_launch": k_bytes, "avg_launch_ms": round(avg_ms, 4),
             "launches": n_launch}
     cpu = None

@@ -149,12 +149,19 @@ int mnl_fields_nr_fallbacks(mnl_fields *f, long long *count);
 /* Algorithmic bytes per owned cell per step of this configuration
  * (DESIGN.md "Roofline") and owned cells of this rank. */
 int mnl_fields_traffic_model(mnl_fields *f, double *bytes_per_cell_step, double *owned_cells);
+/* Allow (1, default) or forbid (0) the fused single-pass interior kernel
+ * (used automatically for 3-D non-dispersive, non-NR configurations without
+ * magnetic or integrated sources).  Results are identical either way. */
+int mnl_fields_set_fused(mnl_fields *f, int allow);
+/* 1 if the last step ran the fused interior kernel, else 0. */
+int mnl_fields_mode(mnl_fields *f, int *fused);
 /* Enable HIP-event timing around every sub-step kernel group (on the stream
  * the kernels run on) and reset the accumulated timers. */
 int mnl_fields_set_profiling(mnl_fields *f, int on);
-/* Accumulated launches / total ms of the interior curl kernel (which = 0:
- * curl B = step_db(B_stuff), 1: curl D = step_db(D_stuff)) since the last
- * mnl_fields_set_profiling, and its algorithmic bytes per launch. */
+/* Accumulated launches / total ms of the dominant interior kernel since the
+ * last mnl_fields_set_profiling, and its algorithmic bytes per launch.
+ * which = 0: fused step kernel (fused mode) or curl B = step_db(B_stuff);
+ * which = 1: curl D = step_db(D_stuff) (unfused mode). */
 int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch);
 

@@ -46,6 +46,8 @@ _SIGS = {
     "mnl_fields_timers": (c_int, [c_void, dptr]),
     "mnl_fields_nr_fallbacks": (c_int, [c_void, llptr]),
     "mnl_fields_set_profiling": (c_int, [c_void, c_int]),
+    "mnl_fields_set_fused": (c_int, [c_void, c_int]),
+    "mnl_fields_mode": (c_int, [c_void, iptr]),
     "mnl_fields_kernel_stats": (c_int, [c_void, c_int, llptr, dptr, dptr]),
     "mnl_fields_traffic_model": (c_int, [c_void, dptr, dptr]),
 }

@@ -244,6 +244,14 @@ class Fields:
         check(lib().mnl_fields_nr_fallbacks(self.h, ctypes.byref(v)))
         return v.value
 
+    def fused_active(self):
+        v = ctypes.c_int()
+        check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
+        return bool(v.value)
+
+    def set_fused(self, allow=True):
+        check(lib().mnl_fields_set_fused(self.h, int(allow)))
+
     def set_profiling(self, on=True):
         check(lib().mnl_fields_set_profiling(self.h, int(on)))
 

@@ -159,6 +159,13 @@ struct mnl_fields {
   Box interior;
   std::vector<Box> shell;
   BoxList shell_list;
+  // fused interior mode (DESIGN.md "Fused interior")
+  bool fused = false;        // currently stepping in fused mode
+  Box fusedF;                // fused region (local indices)
+  BoxList fused_shell;       // everything else
+  double *pp_B[3] = {nullptr, nullptr, nullptr}, *pp_D[3] = {nullptr, nullptr, nullptr};
+  int fused_zchunk = 64;
+  bool allow_fused = true;
   CurlPlan planB, planD;
   bool nr = false;
   // sources
@@ -195,6 +202,8 @@ struct mnl_fields {
 };
 
 namespace {
+
+bool in_fused_box(const mnl_fields *F, int c, const int jg[3]);
 
 template <class T>
 int dev_alloc(mnl_fields *F, T **p, size_t n, bool zero = true) {
@@ -480,13 +489,16 @@ int alloc_component(mnl_fields *F, int c) {
   }
   if (slot && !*slot)
     if (dev_alloc(F, slot, F->nlocal)) return -1;
+  if (t == T_D) F->f.Dn[d] = F->f.D[d];
   if (t == T_H) {
     if (!F->f.B[d] && dev_alloc(F, &F->f.B[d], F->nlocal)) return -1;
+    F->f.Bn[d] = F->f.B[d];
     if (F->pml_any[d]) {  // H separate in chunks with PML along d (src/update_eh.cpp:204-209)
       if (dev_alloc(F, &F->f.H[d], F->nlocal)) return -1;
       if (dev_alloc(F, &F->f.WH[d], F->nlocal)) return -1;
     }
   }
+  if (t == T_B) F->f.Bn[d] = F->f.B[d];
   if (t == T_E && F->pml_any[d] && !F->f.WE[d])
     if (dev_alloc(F, &F->f.WE[d], F->nlocal)) return -1;
   if (t == T_B || t == T_D) {
@@ -984,6 +996,17 @@ int value_at(mnl_fields *F, int c, const int p[3], double *out) {
   }
   if (!src) return 0;
   HIPCHK(hipStreamSynchronize(F->stream));
+  if (in_fused_box(F, c, jg)) {  // E = chi1inv * D inside the fused region
+    double dv = 0, uv = 1;
+    HIPCHK(hipMemcpy(&dv, F->f.D[d] + li, sizeof(double), hipMemcpyDeviceToHost));
+    if (F->f.inveps[d]) {
+      HIPCHK(hipMemcpy(&uv, F->f.inveps[d] + li, sizeof(double), hipMemcpyDeviceToHost));
+      *out = dv * uv;
+    } else {
+      *out = dv;
+    }
+    return 0;
+  }
   HIPCHK(hipMemcpy(out, src + li, sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
@@ -1032,12 +1055,12 @@ int exchange(mnl_fields *F, int kind) {
     if (kind == 0) {
       if (c != sd && F->f.E[c] && F->allocated[c]) items.push_back({F->f.E[c], true});
     } else if (kind == 1) {
-      if (c != sd && F->f.B[c] && F->allocated[3 * T_H + c]) {
-        items.push_back({F->f.B[c], false});
+      if (c != sd && F->f.Bn[c] && F->allocated[3 * T_H + c]) {
+        items.push_back({F->f.Bn[c], false});
         if (F->f.H[c]) items.push_back({F->f.H[c], false});
       }
     } else {
-      if (F->f.D[c] && F->allocated[3 * T_D + c]) items.push_back({F->f.D[c], c != sd});
+      if (F->f.Dn[c] && F->allocated[3 * T_D + c]) items.push_back({F->f.Dn[c], c != sd});
       for (int k = 0; k < F->f.npol; k++)
         if (F->f.pol[k].P[c]) items.push_back({F->f.pol[k].P[c], c != sd});
     }
@@ -1058,6 +1081,99 @@ int exchange(mnl_fields *F, int kind) {
 }
 
 // ------------------------------------------------------------- stepping
+// ------------------------------------------------------------- fused mode
+// F = interior box without its low layer (whose B the fused kernel recomputes
+// as a halo) and restricted to planes where every component is owned and
+// updated (local [1, N-2] per axis).
+void make_fused_boxes(mnl_fields *F) {
+  const DevGrid &g = F->g;
+  Box fb = F->interior;
+  for (int k = 0; k < 3; k++) {
+    fb.lo[k] = std::max(fb.lo[k] + 1, 1);
+    fb.hi[k] = std::min(fb.hi[k], g.N[k] - 2);
+  }
+  F->fusedF = fb;
+  // onion shell around F, slowest axis first
+  std::vector<Box> sh;
+  Box cur;
+  for (int k = 0; k < 3; k++) cur.lo[k] = 0, cur.hi[k] = g.N[k] - 1;
+  for (int k = 2; k >= 0; k--) {
+    if (fb.lo[k] > cur.lo[k]) {
+      Box b = cur;
+      b.hi[k] = fb.lo[k] - 1;
+      sh.push_back(b);
+    }
+    if (fb.hi[k] < cur.hi[k]) {
+      Box b = cur;
+      b.lo[k] = fb.hi[k] + 1;
+      sh.push_back(b);
+    }
+    cur.lo[k] = fb.lo[k];
+    cur.hi[k] = fb.hi[k];
+  }
+  BoxList &bl = F->fused_shell;
+  memset(&bl, 0, sizeof(bl));
+  long long acc = 0;
+  for (auto &b : sh) {
+    bl.b[bl.n] = b;
+    bl.start[bl.n] = acc;
+    acc += (long long)(b.hi[0] - b.lo[0] + 1) * (b.hi[1] - b.lo[1] + 1) * (b.hi[2] - b.lo[2] + 1);
+    bl.n++;
+  }
+  bl.start[bl.n] = acc;
+}
+
+bool fused_possible(mnl_fields *F) {
+  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->f.npol > 0) return false;
+  if (!F->srcB_idx.empty() || !F->isrc_idx.empty()) return false;
+  for (int c = 0; c < MNL_NUM_COMPONENTS; c++)
+    if (!F->allocated[c]) return false;
+  if (F->interior.hi[0] < F->interior.lo[0]) return false;
+  make_fused_boxes(F);
+  for (int k = 0; k < 3; k++)
+    if (F->fusedF.hi[k] < F->fusedF.lo[k]) return false;
+  return true;
+}
+
+int set_fused(mnl_fields *F, bool on) {
+  DevFields &f = F->f;
+  if (on == F->fused) return 0;
+  if (on) {
+    for (int d = 0; d < 3; d++) {
+      if (!F->pp_B[d] && dev_alloc(F, &F->pp_B[d], F->nlocal)) return -1;
+      if (!F->pp_D[d] && dev_alloc(F, &F->pp_D[d], F->nlocal)) return -1;
+      // the second buffer starts as a copy (ghost/wall entries that no kernel writes)
+      HIPCHK(hipMemcpyAsync(F->pp_B[d], f.B[d], F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
+      HIPCHK(hipMemcpyAsync(F->pp_D[d], f.D[d], F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
+      f.Bn[d] = F->pp_B[d];
+      f.Dn[d] = F->pp_D[d];
+    }
+  } else {
+    // materialise E inside F, then step in place again
+    if (k_materialize_e(F->fusedF, F->g, f, F->stream)) return fail("materialize E failed");
+    for (int d = 0; d < 3; d++) {
+      F->pp_B[d] = f.Bn[d];  // the non-current buffer
+      F->pp_D[d] = f.Dn[d];
+      f.Bn[d] = f.B[d];
+      f.Dn[d] = f.D[d];
+    }
+  }
+  F->fused = on;
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
+  if (!F->fused || ctype(c) != T_E) return false;
+  const DevGrid &g = F->g;
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    int j = jg[d] - g.off[d], a = g.ax[d];
+    if (j < F->fusedF.lo[a] || j > F->fusedF.hi[a]) return false;
+  }
+  return true;
+}
+
 enum { TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT };
 
 struct EvPair {
@@ -1067,6 +1183,7 @@ struct EvPair {
 
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
+  if (set_fused(F, fused_possible(F))) return -1;
   const double dt = F->dt;
   // per-step source values, computed on the host exactly as the reference
   size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
@@ -1160,10 +1277,29 @@ int step_batch(mnl_fields *F, int nsteps) {
         if (exchange(F, 0)) return fail("E halo exchange failed");
         ev_end(k);
       }
-      const BoxList *sl = &F->shell_list;
+      const BoxList *sl = F->fused ? &F->fused_shell : &F->shell_list;
       int k = ev_begin(TM_BINT);
-      if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream))
+      if (F->fused) {
+        FusedArgs fa;
+        fa.F = F->fusedF;
+        fa.zchunk = F->fused_zchunk;
+        fa.C = F->S.courant;
+        fa.st1 = g.st[1];
+        fa.st2 = g.st[2];
+        for (int d = 0; d < 3; d++) {
+          fa.Bo[d] = f.B[d];
+          fa.Bn[d] = f.Bn[d];
+          fa.Do[d] = f.D[d];
+          fa.Dn[d] = f.Dn[d];
+          fa.E[d] = f.E[d];
+          fa.u[d] = f.inveps[d];
+        }
+        if ((fa.u[0] != nullptr) != (fa.u[1] != nullptr) || (fa.u[0] != nullptr) != (fa.u[2] != nullptr))
+          return fail("fused kernel needs all or no chi1inv arrays");
+        if (k_fused(fa, F->stream)) return fail("fused kernel launch failed");
+      } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {
         return fail("curl B launch failed");
+      }
       ev_end(k);
       k = ev_begin(TM_B);
       if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream))
@@ -1183,7 +1319,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       // ---- D
       k = ev_begin(TM_DINT);
-      if (k_curl(T_D, F->interior, nullptr, g, f, F->planD, F->S.courant, F->stream))
+      if (!F->fused && k_curl(T_D, F->interior, nullptr, g, f, F->planD, F->S.courant, F->stream))
         return fail("curl D launch failed");
       ev_end(k);
       k = ev_begin(TM_D);
@@ -1197,7 +1333,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       // ---- E (+ Lorentzian P)
       k = ev_begin(TM_E);
       bool fuse = !F->nr;
-      if (k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream) ||
+      if ((!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) ||
           k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream))
         return fail("update E launch failed");
       if (!fuse && f.npol) {
@@ -1206,6 +1342,11 @@ int step_batch(mnl_fields *F, int nsteps) {
           return fail("pols launch failed");
       }
       ev_end(k);
+      if (F->fused)
+        for (int d = 0; d < 3; d++) {
+          std::swap(f.B[d], f.Bn[d]);
+          std::swap(f.D[d], f.Dn[d]);
+        }
     }
     F->t += ns;
     if (flush_events() != 0) return -1;
@@ -1285,6 +1426,8 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
       return nullptr;
     }
   }
+  if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(1, atoi(zc));
+  if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
   if (finalize_fields(F.get())) return nullptr;
   return F.release();
 }
@@ -1543,7 +1686,9 @@ int mnl_fields_copy_component(mnl_fields *F, int comp, double *host, size_t n) {
     F->scratch_cap = nt;
   }
   HIPCHK(hipMemsetAsync(F->d_scratch, 0, nt * sizeof(double), F->stream));
-  if (k_to_canonical(F->d_scratch, src, hsep, F->g, t, d, F->f, F->stream))
+  const bool fe = F->fused && t == T_E;
+  if (k_to_canonical(F->d_scratch, src, hsep, F->g, t, d, F->f, fe ? &F->fusedF : nullptr,
+                     fe ? F->f.D[d] : nullptr, fe ? F->f.inveps[d] : nullptr, F->stream))
     return fail("to_canonical launch failed");
   HIPCHK(hipMemcpyAsync(host, F->d_scratch, nt * sizeof(double), hipMemcpyDeviceToHost, F->stream));
   HIPCHK(hipStreamSynchronize(F->stream));
@@ -1570,6 +1715,14 @@ int mnl_fields_nr_fallbacks(mnl_fields *F, long long *count) {
   return 0;
 }
 
+int mnl_fields_set_fused(mnl_fields *F, int allow) {
+  if (!F) return fail("null fields");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  F->allow_fused = allow != 0;
+  if (!F->allow_fused) return set_fused(F, false);
+  return 0;
+}
+
 int mnl_fields_set_profiling(mnl_fields *F, int on) {
   if (!F) return fail("null fields");
   F->profiling = on != 0;
@@ -1583,11 +1736,18 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
   int cat = which == 0 ? TM_BINT : TM_DINT;
   *launches = F->timer_count[cat];
   *total_ms = F->timer_ms[cat];
-  // algorithmic bytes of the interior curl: read 3 source comps + read/write 3
-  // updated comps per owned point (DESIGN.md "Roofline")
+  const Box &b = (F->fused && which == 0) ? F->fusedF : F->interior;
   double pts = 1;
-  for (int k = 0; k < 3; k++) pts *= double(F->interior.hi[k] - F->interior.lo[k] + 1);
-  if (F->interior.hi[0] < F->interior.lo[0]) pts = 0;
+  for (int k = 0; k < 3; k++) pts *= double(b.hi[k] - b.lo[k] + 1);
+  if (b.hi[0] < b.lo[0]) pts = 0;
+  if (F->fused && which == 0) {
+    // fused step: read B(3), D(3), chi1inv(3 if present); write B(3), D(3)
+    int nu = 0;
+    for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
+    *bytes_per_launch = pts * 8.0 * (12 + nu);
+    return 0;
+  }
+  // interior curl: read 3 source comps + read/write the updated comps
   int ncomp = 0;
   const CurlPlan &p = which == 0 ? F->planB : F->planD;
   for (int d = 0; d < 3; d++) ncomp += p.present[d] ? 1 : 0;
@@ -1597,19 +1757,31 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
   return 0;
 }
 
+int mnl_fields_mode(mnl_fields *F, int *fused) {
+  if (!F) return fail("null fields");
+  *fused = F->fused ? 1 : 0;
+  return 0;
+}
+
 int mnl_fields_traffic_model(mnl_fields *F, double *bpc, double *cells) {
   if (!F) return fail("null fields");
-  // minimal per-step traffic of the unfused sub-step kernels in the interior:
-  // curl B: E(3) + B(3) read, B(3) written; curl D: H=B(3) + D(3) read, D(3)
-  // written; E update: D(3) (+eps^-1 3) read, E(3) written (+P terms).
+  // Minimal per-step HBM traffic per interior cell of the kernels in use
+  // (DESIGN.md "Roofline"): fused: B, D read+write, chi1inv read;
+  // unfused: curl B reads E(3)+B(3), writes B(3); curl D reads H=B(3)+D(3),
+  // writes D(3); E update reads D(3) (+chi1inv 3), writes E(3) (+P terms).
   double n = 0;
   for (int d = 0; d < 3; d++) n += F->allocated[d] ? 1 : 0;
-  double b = 8.0 * (3 * n) * 2 + 8.0 * (2 * n);
-  for (int d = 0; d < 3; d++)
-    if (F->f.inveps[d]) b += 8.0;
-  for (int k = 0; k < F->f.npol; k++)
-    for (int d = 0; d < 3; d++)
-      if (F->f.pol[k].P[d]) b += 8.0 * 5;
+  int nu = 0;
+  for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
+  double b;
+  if (F->fused) {
+    b = 8.0 * (4 * n + nu);
+  } else {
+    b = 8.0 * (3 * n) * 2 + 8.0 * (2 * n) + 8.0 * nu;
+    for (int k = 0; k < F->f.npol; k++)
+      for (int d = 0; d < 3; d++)
+        if (F->f.pol[k].P[d]) b += 8.0 * 5;
+  }
   *bpc = b;
   double c = 1;
   for (int d = 0; d < 3; d++)

@@ -73,7 +73,11 @@ struct PolDev {
 };
 
 struct DevFields {
+  // B, D: field at the start of the step (read); Bn, Dn: where the update
+  // writes.  Unfused stepping updates in place (Bn == B, Dn == D); the fused
+  // interior kernel ping-pongs them and the host swaps after each step.
   double *E[3], *D[3], *B[3], *H[3];
+  double *Bn[3], *Dn[3];
   double *UB[3], *UD[3], *WE[3], *WH[3];
   const double *inveps[3];   // diagonal chi1inv of E comps (null = trivial)
   const double *offd[3][2];  // chi1inv[ec][cycle(d,1)], [cycle(d,2)] (null = absent)
@@ -121,11 +125,29 @@ int k_update_pols(const Box &in, const BoxList *shell, const DevGrid &g, const D
                   void *stream);
 int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int step,
              void *stream);
+// Fused interior step (curl B -> H=B -> curl D -> E=chi1inv*D never stored)
+// over box F, 3-D, no PML/dispersion/NR inside F (DESIGN.md "Fused interior").
+struct FusedArgs {
+  Box F;
+  int zchunk;
+  double C;
+  long long st1, st2;
+  const double *Bo[3];
+  double *Bn[3];
+  const double *Do[3];
+  double *Dn[3];
+  const double *E[3];
+  const double *u[3];
+};
+int k_fused(const FusedArgs &a, void *stream);
+// E = chi1inv * D over box F (leaving fused mode / readout)
+int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *stream);
 int k_fill(double *p, double v, size_t n, void *stream);
 int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_type,
                      int comp_dir, int zlo_glob, void *stream);
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
-                   int comp_type, int comp_dir, const DevFields &f, void *stream);
+                   int comp_type, int comp_dir, const DevFields &f, const Box *fusedF,
+                   const double *dsrc, const double *usrc, void *stream);
 int k_box_fill(double *dst, const DevGrid &g, int comp_type, int comp_dir, const double *pos_lo,
                const double *pos_hi, double value, int invert, double a, const int *io,
                void *stream);

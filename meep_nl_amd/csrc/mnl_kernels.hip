@@ -118,8 +118,8 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
     } else {
       s1 = -s1;
       s2 = -s2;
-      g1 = f.B[c1];
-      g2 = f.B[c2];
+      g1 = f.Bn[c1];  // H == B (new) outside PML chunks
+      g2 = f.Bn[c2];
       if (SHELL) {  // H separate only in chunks with PML along the H direction
         if (f.H[c1] && pml_at(f, g, c1, qcoord(g, p, T_H, c1, c1))) g1 = f.H[c1];
         if (f.H[c2] && pml_at(f, g, c2, qcoord(g, p, T_H, c2, c2))) g2 = f.H[c2];
@@ -135,16 +135,17 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
       T = g2[i + s2] - g2[i];
       dtdx = -C;
     }
-    double *F = FT == T_B ? f.B[d] : f.D[d];
+    const double *Fo = FT == T_B ? f.B[d] : f.D[d];
+    double *F = FT == T_B ? f.Bn[d] : f.Dn[d];
     if (!SHELL) {
-      F[i] -= dtdx * T;
+      F[i] = Fo[i] - dtdx * T;
       continue;
     }
     const int dsig = (d + 1) % 3, dsigu = (d + 2) % 3;
     const int k = qcoord(g, p, FT, d, dsig), ku = qcoord(g, p, FT, d, dsigu);
     const bool ps = pml_at(f, g, dsig, k), pu = pml_at(f, g, dsigu, ku);
     if (!ps && !pu) {
-      F[i] -= dtdx * T;
+      F[i] = Fo[i] - dtdx * T;
     } else if (!ps) {
       double *U = FT == T_B ? f.UB[d] : f.UD[d];
       const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu],
@@ -152,10 +153,10 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
       double fprev = U[i];
       double fu = fprev - dtdx * T;
       U[i] = fu;
-      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * F[i] + fu - fprev);
+      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
     } else if (!pu) {
       const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
-      F[i] = ((kap[k] - sig[k]) * F[i] - dtdx * T) * siginv[k];
+      F[i] = ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
     } else {
       double *U = FT == T_B ? f.UB[d] : f.UD[d];
       const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
       double fprev = U[i];
       double fu = ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
       U[i] = fu;
-      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * F[i] + fu - fprev);
+      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
     }
   }
 }
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_h_kernel(BoxList bl, De
     if (!pml_at(f, g, d, kw)) continue;
     double fwprev = f.WH[d][i];
     double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
-    double fw = f.B[d][i];
+    double fw = f.Bn[d][i];
     f.WH[d][i] = fw;
     f.H[d][i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
   }
@@ -313,7 +314,7 @@ __device__ void run_nr(double seed1, double seed2, double seed3, double *fw, dou
 template <bool ISRC>
 __device__ __forceinline__ double dmp_at(const DevFields &f, const ISrcDev &is, int step, int c,
                                          long long n) {
-  double v = f.D[c][n];
+  double v = f.Dn[c][n];
   for (int k = 0; k < f.npol; k++)
     if (f.pol[k].P[c]) v -= f.pol[k].P[c][n];
   if (ISRC) {
@@ -490,7 +491,8 @@ __global__ void from_canonical_kernel(double *dst, const double *src, DevGrid g,
 
 __global__ void to_canonical_kernel(double *dst, const double *src, const double *hsep, DevGrid g,
                                     DevFields f, int type, int c, long long cs0, long long cs1,
-                                    long long cs2) {
+                                    long long cs2, Box Fb, int use_fb, const double *dsrc,
+                                    const double *usrc) {
   int i0 = blockIdx.x * MNL_BX + threadIdx.x;
   int i1 = blockIdx.y * MNL_BY + threadIdx.y;
   int i2 = blockIdx.z;
@@ -515,6 +517,9 @@ __global__ void to_canonical_kernel(double *dst, const double *src, const double
   long long i = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
   double v = src[i];
   if (hsep && pml_at(f, g, c, qcoord(g, p, T_H, c, c))) v = hsep[i];
+  if (use_fb && i0 >= Fb.lo[0] && i0 <= Fb.hi[0] && i1 >= Fb.lo[1] && i1 <= Fb.hi[1] &&
+      i2 >= Fb.lo[2] && i2 <= Fb.hi[2])  // fused interior: E = chi1inv * D (never stored)
+    v = usrc ? (dsrc[i] * usrc[i]) : dsrc[i];
   dst[cidx] = v;
 }
 
@@ -645,8 +650,149 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
   (void)g;
   if (s.n == 0) return 0;
   Ptr3 pt;
-  for (int d = 0; d < 3; d++) pt.p[d] = ft == T_D ? f.D[d] : f.B[d];
+  for (int d = 0; d < 3; d++) pt.p[d] = ft == T_D ? f.Dn[d] : f.Bn[d];
   source_kernel<<<1, 64, 0, (hipStream_t)stream>>>(pt, s, step);
+  return rc();
+}
+
+
+// ----------------------------------------------------------------- fused step
+// One pass over the interior box F for a whole fields::step() of a
+// non-dispersive, PML-free region (src/step.cpp:66-110 restricted to such
+// chunks): curl B (step_curl, src/step_generic.cpp:106-109), H == B, curl D
+// (same loop, negated strides), E = chi1inv * D (src/step_generic.cpp:
+// 888-903).  E is never stored inside F: it is recomputed as D*u whenever it
+// is read, which is bit-identical to the stored value of the reference.
+//
+// Work decomposition (2.5-D): a workgroup owns a (FX-1) x (FY-1) tile of
+// (x,y) columns plus a one-column low halo in x and y, and marches z over
+// `zchunk` planes (plus one halo plane below).  Per plane: E_k of the tile +
+// high halo goes to LDS, every thread computes B_new for its column (halo
+// threads too: those values are only needed for the D update and are
+// recomputed, not stored), B_new goes to LDS, then the inner threads update
+// D using B_new of the x-1 / y-1 neighbours (LDS) and of plane k-1
+// (registers).  HBM traffic per cell: read B, D, u, write B, D (15 x 8 B).
+#define FX 64
+#define FY 16
+
+template <bool HAS_U>
+__global__ __launch_bounds__(FX *FY) void fused_kernel(FusedArgs a) {
+  __shared__ double sE[3][FY + 1][FX + 1];
+  __shared__ double sB[3][FY][FX];
+  const int tx = threadIdx.x, ty = threadIdx.y;
+  const int gx = a.F.lo[0] - 1 + blockIdx.x * (FX - 1) + tx;
+  const int gy = a.F.lo[1] - 1 + blockIdx.y * (FY - 1) + ty;
+  const int z0 = a.F.lo[2] + blockIdx.z * a.zchunk;
+  const int z1 = min(z0 + a.zchunk, a.F.hi[2] + 1);
+  const bool load_ok = gx <= a.F.hi[0] + 1 && gy <= a.F.hi[1] + 1;
+  const bool col_ok = gx <= a.F.hi[0] && gy <= a.F.hi[1];
+  const bool inner = col_ok && tx >= 1 && ty >= 1;
+  const long long base = (long long)gx + (long long)gy * a.st1;
+  const double C = a.C;
+  auto inF = [&](int x, int y, int z) {
+    return x >= a.F.lo[0] && x <= a.F.hi[0] && y >= a.F.lo[1] && y <= a.F.hi[1] &&
+           z >= a.F.lo[2] && z <= a.F.hi[2];
+  };
+  auto e_at = [&](int c, int x, int y, int z, long long i) -> double {
+    if (inF(x, y, z)) {
+      double d = a.Do[c][i];
+      return HAS_U ? (d * a.u[c][i]) : d;
+    }
+    return a.E[c][i];
+  };
+  double Ek[3] = {0, 0, 0}, Ek1[3] = {0, 0, 0}, Dk[3] = {0, 0, 0}, Dk1[3] = {0, 0, 0};
+  double Hm[3] = {0, 0, 0};
+  if (load_ok) {
+    const int z = z0 - 1;
+    const long long i = base + (long long)z * a.st2;
+    for (int c = 0; c < 3; c++) Ek[c] = e_at(c, gx, gy, z, i);
+  }
+  for (int k = z0 - 1; k < z1; k++) {
+    const long long i = base + (long long)k * a.st2;
+    // own column, plane k+1 (and D there, for the D update of the next plane)
+    if (load_ok) {
+      const long long i1 = i + a.st2;
+      const bool f1 = inF(gx, gy, k + 1);
+      for (int c = 0; c < 3; c++) {
+        if (f1) {
+          double d = a.Do[c][i1];
+          Dk1[c] = d;
+          Ek1[c] = HAS_U ? (d * a.u[c][i1]) : d;
+        } else {
+          Ek1[c] = a.E[c][i1];
+        }
+      }
+      for (int c = 0; c < 3; c++) sE[c][ty][tx] = Ek[c];
+      if (tx == FX - 1 && col_ok) {
+        sE[1][ty][FX] = e_at(1, gx + 1, gy, k, i + 1);
+        sE[2][ty][FX] = e_at(2, gx + 1, gy, k, i + 1);
+      }
+      if (ty == FY - 1 && col_ok) {
+        sE[0][FY][tx] = e_at(0, gx, gy + 1, k, i + a.st1);
+        sE[2][FY][tx] = e_at(2, gx, gy + 1, k, i + a.st1);
+      }
+    }
+    __syncthreads();
+    double Bx = 0, By = 0, Bz = 0;
+    if (col_ok) {
+      const double Ex = sE[0][ty][tx], Ey = sE[1][ty][tx], Ez = sE[2][ty][tx];
+      const double Ez_yp = sE[2][ty + 1][tx], Ex_yp = sE[0][ty + 1][tx];
+      const double Ey_xp = sE[1][ty][tx + 1], Ez_xp = sE[2][ty][tx + 1];
+      Bx = a.Bo[0][i] - C * (Ez_yp - Ez + Ey - Ek1[1]);
+      By = a.Bo[1][i] - C * (Ek1[0] - Ex + Ez - Ez_xp);
+      Bz = a.Bo[2][i] - C * (Ey_xp - Ey + Ex - Ex_yp);
+      if (inner && k >= z0) {
+        a.Bn[0][i] = Bx;
+        a.Bn[1][i] = By;
+        a.Bn[2][i] = Bz;
+      }
+      sB[0][ty][tx] = Bx;
+      sB[1][ty][tx] = By;
+      sB[2][ty][tx] = Bz;
+    }
+    __syncthreads();
+    if (inner && k >= z0) {
+      const double Hz_ym = sB[2][ty - 1][tx], Hx_ym = sB[0][ty - 1][tx];
+      const double Hz_xm = sB[2][ty][tx - 1], Hy_xm = sB[1][ty][tx - 1];
+      a.Dn[0][i] = Dk[0] - C * (Hz_ym - Bz + By - Hm[1]);
+      a.Dn[1][i] = Dk[1] - C * (Hm[0] - Bx + Bz - Hz_xm);
+      a.Dn[2][i] = Dk[2] - C * (Hy_xm - By + Bx - Hx_ym);
+    }
+    Hm[0] = Bx;
+    Hm[1] = By;
+    Hm[2] = Bz;
+    for (int c = 0; c < 3; c++) {
+      Ek[c] = Ek1[c];
+      Dk[c] = Dk1[c];
+    }
+  }
+}
+
+int k_fused(const FusedArgs &a, void *stream) {
+  int n0 = a.F.hi[0] - a.F.lo[0] + 1, n1 = a.F.hi[1] - a.F.lo[1] + 1,
+      n2 = a.F.hi[2] - a.F.lo[2] + 1;
+  if (n0 <= 0 || n1 <= 0 || n2 <= 0) return 0;
+  dim3 grd((n0 + FX - 2) / (FX - 1), (n1 + FY - 2) / (FY - 1), (n2 + a.zchunk - 1) / a.zchunk);
+  hipStream_t s = (hipStream_t)stream;
+  if (a.u[0])
+    fused_kernel<true><<<grd, dim3(FX, FY), 0, s>>>(a);
+  else
+    fused_kernel<false><<<grd, dim3(FX, FY), 0, s>>>(a);
+  return rc();
+}
+
+__global__ void materialize_e_kernel(Box b, DevGrid g, DevFields f) {
+  Pt p;
+  if (!make_pt(b, g, p)) return;
+  for (int c = 0; c < 3; c++) {
+    const double d = f.D[c][p.idx];
+    f.E[c][p.idx] = f.inveps[c] ? (d * f.inveps[c][p.idx]) : d;
+  }
+}
+
+int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *stream) {
+  if (empty(F)) return 0;
+  materialize_e_kernel<<<grid_for(F), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(F, g, f);
   return rc();
 }
 
@@ -681,12 +827,16 @@ int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_
 }
 
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
-                   int comp_type, int comp_dir, const DevFields &f, void *stream) {
+                   int comp_type, int comp_dir, const DevFields &f, const Box *fusedF,
+                   const double *dsrc, const double *usrc, void *stream) {
   long long cs[3];
   canon_strides(g, cs);
   dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
+  Box fb{};
+  if (fusedF) fb = *fusedF;
   to_canonical_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(
-      dst, src, hsep, g, f, comp_type, comp_dir, cs[0], cs[1], cs[2]);
+      dst, src, hsep, g, f, comp_type, comp_dir, cs[0], cs[1], cs[2], fb, fusedF ? 1 : 0, dsrc,
+      usrc);
   return rc();
 }
 

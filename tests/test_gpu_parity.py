@@ -10,7 +10,7 @@ import math
 import numpy as np
 import pytest
 
-from scenarios import (ALL_COMPS, ProductSim, compare_all, make_oracle, sc_cfg1,
+from scenarios import (ALL_COMPS, ProductSim, compare_all, make_oracle, sc_big_box_3d, sc_cfg1,
                        sc_kerr_lorentz_3d, sc_known_metallic_3d, sc_known_pml_2d,
                        sc_multi_source_3d, sc_nr_pml_dispersive, sc_nr_probe, sc_polariton_1d,
                        sc_te_magnetic_2d, sc_vacuum_pml_3d, sc_waveguide_3d)
@@ -105,3 +105,30 @@ def test_simulation_api_matches_core():
     p.step(sim.timestep)
     np.testing.assert_array_equal(sim.get_array(mp.Ez), p.get_array(2))
     assert sim.meep_time() == pytest.approx(sim.timestep * 0.05)
+
+
+@pytest.mark.parametrize("zchunk", ["64", "7"])
+def test_fused_many_tiles(monkeypatch, zchunk):
+    """The fused interior kernel over many (x,y) tiles and z-chunks (zchunk 7 puts a
+    chunk seam every 7 planes) must stay bitwise equal to the oracle."""
+    monkeypatch.setenv("MNL_FUSED_ZCHUNK", zchunk)
+    p = sc_big_box_3d(ProductSim)
+    assert p._fields().kernel_stats(0)[0] >= 0
+    _bitwise(p, sc_big_box_3d(make_oracle))
+
+
+def test_fused_vs_unfused(monkeypatch):
+    monkeypatch.setenv("MNL_NO_FUSED", "1")
+    a = sc_big_box_3d(ProductSim, steps=16)
+    monkeypatch.delenv("MNL_NO_FUSED")
+    b = sc_big_box_3d(ProductSim, steps=16)
+    _bitwise(a, b)
+
+
+def test_fused_mode_toggle():
+    """Adding a magnetic (non-fusable) source mid-run switches the fused interior
+    off (E is materialised from D) and the run continues bitwise."""
+    def add_h(o):
+        o.add_gaussian_source(4, 0.3, 3.0, 0.0, 30.0, (1.0, 0.3, -1.1), 0.8)
+    _bitwise(sc_big_box_3d(ProductSim, steps=24, extra=add_h),
+             sc_big_box_3d(make_oracle, steps=24, extra=add_h))
