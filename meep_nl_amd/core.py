@@ -149,6 +149,7 @@ class Fields:
         if not self.h:
             raise RuntimeError(lib().mnl_last_error().decode())
         self.rank, self.nranks = rank, nranks
+        self._hub = hub  # the hub must outlive the fields of its slabs
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -26,6 +26,12 @@ struct LocalHub {
   std::vector<std::vector<double>> red;
 
   explicit LocalHub(int nr) : n(nr), sends(nr), ev_send(nr, nullptr), ev_done(nr, nullptr), red(nr) {}
+  ~LocalHub() {
+    for (auto e : ev_send)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : ev_done)
+      if (e) (void)hipEventDestroy(e);
+  }
   void barrier() {
     std::unique_lock<std::mutex> lk(m);
     long long g = gen;
@@ -67,8 +73,13 @@ int Comm::init_local(int r, int n, LocalHub *hub) {
   nranks = n;
   hub_ = hub;
   if (!hub || hub->n != n) return -1;
-  if (hipEventCreateWithFlags(&hub->ev_send[r], hipEventDisableTiming) != hipSuccess) return -1;
-  if (hipEventCreateWithFlags(&hub->ev_done[r], hipEventDisableTiming) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lk(hub->m);
+  if (!hub->ev_send[r] &&
+      hipEventCreateWithFlags(&hub->ev_send[r], hipEventDisableTiming) != hipSuccess)
+    return -1;
+  if (!hub->ev_done[r] &&
+      hipEventCreateWithFlags(&hub->ev_done[r], hipEventDisableTiming) != hipSuccess)
+    return -1;
   return 0;
 }
 
@@ -158,11 +169,7 @@ int Comm::allreduce_sum(double *host, int n, void *stream) {
 Comm::~Comm() {
   if (comm_) ncclCommDestroy((ncclComm_t)comm_);
   if (dscratch_) hipFree(dscratch_);
-  if (hub_) {
-    if (hub_->ev_send[rank]) hipEventDestroy(hub_->ev_send[rank]);
-    if (hub_->ev_done[rank]) hipEventDestroy(hub_->ev_done[rank]);
-    hub_->ev_send[rank] = hub_->ev_done[rank] = nullptr;
-  }
+  // events belong to the hub (it may be destroyed before or after us)
 }
 
 }  // namespace mnl

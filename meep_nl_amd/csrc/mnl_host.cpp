@@ -1159,6 +1159,8 @@ int set_fused(mnl_fields *F, bool on) {
     }
   }
   F->fused = on;
+  f.fused = on ? 1 : 0;
+  f.fF = F->fusedF;
   HIPCHK(hipStreamSynchronize(F->stream));
   return 0;
 }

@@ -93,6 +93,9 @@ struct DevFields {
   const uint8_t *offd_zone;
   const uint8_t *zone[3];    // per direction, global half-coordinate q -> zone 0/1/2
   unsigned long long *nr_fallbacks;
+  // fused interior active: E inside box fF is not stored and reads as D*chi1inv
+  int fused;
+  Box fF;
 };
 
 // Point sources in rank-local linear indices.

@@ -93,6 +93,39 @@ __device__ __forceinline__ bool pml_at(const DevFields &f, const DevGrid &g, int
   return g.ax[d] >= 0 && f.pml.flag[d] != nullptr && f.pml.flag[d][q] != 0;
 }
 
+// Apply one curl update with the per-point PML branch selection of step_curl
+// (src/step_generic.cpp:84-252, cnd == NULL).
+template <int FT>
+__device__ __forceinline__ void curl_apply(const DevFields &f, const DevGrid &g, const Pt &p, int d,
+                                           long long i, double T, double dtdx) {
+  const double *Fo = FT == T_B ? f.B[d] : f.D[d];
+  double *F = FT == T_B ? f.Bn[d] : f.Dn[d];
+  const int dsig = (d + 1) % 3, dsigu = (d + 2) % 3;
+  const int k = qcoord(g, p, FT, d, dsig), ku = qcoord(g, p, FT, d, dsigu);
+  const bool ps = pml_at(f, g, dsig, k), pu = pml_at(f, g, dsigu, ku);
+  if (!ps && !pu) {
+    F[i] = Fo[i] - dtdx * T;
+  } else if (!ps) {
+    double *U = FT == T_B ? f.UB[d] : f.UD[d];
+    const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
+    double fprev = U[i];
+    double fu = fprev - dtdx * T;
+    U[i] = fu;
+    F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
+  } else if (!pu) {
+    const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
+    F[i] = ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
+  } else {
+    double *U = FT == T_B ? f.UB[d] : f.UD[d];
+    const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
+    const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
+    double fprev = U[i];
+    double fu = ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
+    U[i] = fu;
+    F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
+  }
+}
+
 // ----------------------------------------------------------------- curl B / D
 // fields_chunk::step_db -> step_curl (src/step_db.cpp:44-146,
 // src/step_generic.cpp:69-253, conductivity-free branches).  Component d of
@@ -115,6 +148,33 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
     if (FT == T_B) {
       g1 = f.E[c1];
       g2 = f.E[c2];
+      if (SHELL && f.fused) {  // E is not stored inside the fused box: E = D*chi1inv
+        const int x = p.j[0], y = p.j[1], z = p.j[2];
+        auto inF = [&](int dd) {
+          const int xx = x + (dd == 0), yy = y + (dd == 1), zz = z + (dd == 2);
+          return xx >= f.fF.lo[0] && xx <= f.fF.hi[0] && yy >= f.fF.lo[1] && yy <= f.fF.hi[1] &&
+                 zz >= f.fF.lo[2] && zz <= f.fF.hi[2];
+        };
+        auto e_at = [&](int c, long long n, int dd) -> double {
+          if (inF(dd)) {
+            const double dv = f.D[c][n];
+            return f.inveps[c] ? (dv * f.inveps[c][n]) : dv;
+          }
+          return f.E[c][n];
+        };
+        const int terms = pl.terms[d];
+        double T, dtdx = C;
+        if (terms == 3) {
+          T = e_at(c1, i + s1, dir1) - e_at(c1, i, -1) + e_at(c2, i, -1) - e_at(c2, i + s2, dir2);
+        } else if (terms == 1) {
+          T = e_at(c1, i + s1, dir1) - e_at(c1, i, -1);
+        } else {
+          T = e_at(c2, i + s2, dir2) - e_at(c2, i, -1);
+          dtdx = -C;
+        }
+        curl_apply<FT>(f, g, p, d, i, T, dtdx);
+        continue;
+      }
     } else {
       s1 = -s1;
       s2 = -s2;
@@ -135,38 +195,13 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
       T = g2[i + s2] - g2[i];
       dtdx = -C;
     }
-    const double *Fo = FT == T_B ? f.B[d] : f.D[d];
-    double *F = FT == T_B ? f.Bn[d] : f.Dn[d];
     if (!SHELL) {
+      const double *Fo = FT == T_B ? f.B[d] : f.D[d];
+      double *F = FT == T_B ? f.Bn[d] : f.Dn[d];
       F[i] = Fo[i] - dtdx * T;
       continue;
     }
-    const int dsig = (d + 1) % 3, dsigu = (d + 2) % 3;
-    const int k = qcoord(g, p, FT, d, dsig), ku = qcoord(g, p, FT, d, dsigu);
-    const bool ps = pml_at(f, g, dsig, k), pu = pml_at(f, g, dsigu, ku);
-    if (!ps && !pu) {
-      F[i] = Fo[i] - dtdx * T;
-    } else if (!ps) {
-      double *U = FT == T_B ? f.UB[d] : f.UD[d];
-      const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu],
-                   *siginvu = f.pml.siginv[dsigu];
-      double fprev = U[i];
-      double fu = fprev - dtdx * T;
-      U[i] = fu;
-      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
-    } else if (!pu) {
-      const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
-      F[i] = ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
-    } else {
-      double *U = FT == T_B ? f.UB[d] : f.UD[d];
-      const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
-      const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu],
-                   *siginvu = f.pml.siginv[dsigu];
-      double fprev = U[i];
-      double fu = ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
-      U[i] = fu;
-      F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
-    }
+    curl_apply<FT>(f, g, p, d, i, T, dtdx);
   }
 }
 
