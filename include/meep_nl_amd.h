@@ -98,6 +98,8 @@ mnl_fields *mnl_fields_create(mnl_structure *s, int device);
 mnl_fields *mnl_fields_create_dist(mnl_structure *s, int device, int rank, int nranks,
                                    const void *nccl_id);
 int mnl_comm_unique_id(void *out128);
+/* Cells [lo, hi) of the slab axis owned by `rank` (host-only helper). */
+int mnl_slab_range(int ncell, int rank, int nranks, int *lo, int *hi);
 /* Several slabs of one grid in ONE process on one device (one host thread per
  * slab calling mnl_fields_step concurrently): same decomposition and exchange
  * code as mnl_fields_create_dist, transport = device copies + host barriers.

@@ -31,6 +31,7 @@ _SIGS = {
     "mnl_fields_create": (c_void, [c_void, c_int]),
     "mnl_fields_create_dist": (c_void, [c_void, c_int, c_int, c_int, ctypes.c_char_p]),
     "mnl_comm_unique_id": (c_int, [ctypes.c_char_p]),
+    "mnl_slab_range": (c_int, [c_int, c_int, c_int, iptr, iptr]),
     "mnl_local_hub_create": (c_void, [c_int]),
     "mnl_local_hub_destroy": (None, [c_void]),
     "mnl_fields_create_local": (c_void, [c_void, c_int, c_int, c_int, c_void]),

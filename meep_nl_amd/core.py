@@ -294,6 +294,12 @@ def device_count():
     return n.value
 
 
+def slab_range(ncell, rank, nranks):
+    lo, hi = ctypes.c_int(), ctypes.c_int()
+    check(lib().mnl_slab_range(ncell, rank, nranks, ctypes.byref(lo), ctypes.byref(hi)))
+    return lo.value, hi.value
+
+
 def unique_id():
     buf = ctypes.create_string_buffer(128)
     check(lib().mnl_comm_unique_id(buf))

@@ -315,6 +315,13 @@ int build_pml_tables(mnl_fields *F) {
 }
 
 // ------------------------------------------------------------- grid / boxes
+// Equal split of the slab-axis cells over ranks (first `rem` ranks get one more).
+void slab_range(int ncell, int rank, int nranks, int *lo, int *hi) {
+  int base = ncell / nranks, rem = ncell % nranks;
+  *lo = rank * base + std::min(rank, rem);
+  *hi = *lo + base + (rank < rem ? 1 : 0);
+}
+
 void setup_grid(mnl_fields *F) {
   const mnl_structure &S = F->S;
   DevGrid &g = F->g;
@@ -325,12 +332,7 @@ void setup_grid(mnl_fields *F) {
   // slab direction = slowest present direction
   F->slab_dir = S.has[2] ? 2 : 1;
   int lo_cell = 0, hi_cell = S.n[F->slab_dir];
-  if (F->nranks > 1) {
-    int ncell = S.n[F->slab_dir];
-    int base = ncell / F->nranks, rem = ncell % F->nranks;
-    lo_cell = F->rank * base + std::min(F->rank, rem);
-    hi_cell = lo_cell + base + (F->rank < rem ? 1 : 0);
-  }
+  slab_range(S.n[F->slab_dir], F->rank, F->nranks, &lo_cell, &hi_cell);
   int Nax[3] = {1, 1, 1};
   for (int d = 0; d < 3; d++) {
     if (!S.has[d]) continue;
@@ -1584,6 +1586,11 @@ mnl_fields *mnl_fields_create_local(mnl_structure *s, int device, int rank, int 
     return nullptr;
   }
   return create_common(s, device, rank, nranks, nullptr, (LocalHub *)hub);
+}
+int mnl_slab_range(int ncell, int rank, int nranks, int *lo, int *hi) {
+  if (nranks < 1 || rank < 0 || rank >= nranks || ncell < nranks) return fail("bad slab split");
+  slab_range(ncell, rank, nranks, lo, hi);
+  return 0;
 }
 int mnl_comm_unique_id(void *out128) { return Comm::unique_id(out128) ? fail("ncclGetUniqueId failed") : 0; }
 
