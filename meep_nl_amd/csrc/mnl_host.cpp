@@ -164,7 +164,11 @@ struct mnl_fields {
   Box fusedF;                // fused region (local indices)
   BoxList fused_shell;       // everything else
   double *pp_B[3] = {nullptr, nullptr, nullptr}, *pp_D[3] = {nullptr, nullptr, nullptr};
-  int fused_zchunk = 64;
+  int fused_zchunk = 0;
+  int fused_bpc = 1;
+  int fused_dist = 1;
+  unsigned long long *d_fused_ctr = nullptr;  // work-item counter of the fused kernel
+  unsigned long long fused_ctr_base = 0;
   bool allow_fused = true;
   CurlPlan planB, planD;
   bool nr = false;
@@ -1131,6 +1135,8 @@ bool fused_possible(mnl_fields *F) {
   for (int c = 0; c < MNL_NUM_COMPONENTS; c++)
     if (!F->allocated[c]) return false;
   if (F->interior.hi[0] < F->interior.lo[0]) return false;
+  // the fused kernel addresses arrays with 32-bit byte offsets
+  if (F->nlocal * 8 >= 0xFFFFFFF0ull) return false;
   make_fused_boxes(F);
   for (int k = 0; k < 3; k++)
     if (F->fusedF.hi[k] < F->fusedF.lo[k]) return false;
@@ -1141,6 +1147,11 @@ int set_fused(mnl_fields *F, bool on) {
   DevFields &f = F->f;
   if (on == F->fused) return 0;
   if (on) {
+    if (!F->d_fused_ctr) {
+      if (dev_alloc(F, &F->d_fused_ctr, 1)) return -1;
+      HIPCHK(hipMemsetAsync(F->d_fused_ctr, 0, sizeof(unsigned long long), F->stream));
+      F->fused_ctr_base = 0;
+    }
     for (int d = 0; d < 3; d++) {
       if (!F->pp_B[d] && dev_alloc(F, &F->pp_B[d], F->nlocal)) return -1;
       if (!F->pp_D[d] && dev_alloc(F, &F->pp_D[d], F->nlocal)) return -1;
@@ -1287,6 +1298,9 @@ int step_batch(mnl_fields *F, int nsteps) {
         FusedArgs fa;
         fa.F = F->fusedF;
         fa.zchunk = F->fused_zchunk;
+        fa.blocks_per_cu = F->fused_bpc;
+        fa.dist = F->fused_dist;
+        fa.nelem = (long long)F->nlocal;
         fa.C = F->S.courant;
         fa.st1 = g.st[1];
         fa.st2 = g.st[2];
@@ -1300,7 +1314,11 @@ int step_batch(mnl_fields *F, int nsteps) {
         }
         if ((fa.u[0] != nullptr) != (fa.u[1] != nullptr) || (fa.u[0] != nullptr) != (fa.u[2] != nullptr))
           return fail("fused kernel needs all or no chi1inv arrays");
-        if (k_fused(fa, F->stream)) return fail("fused kernel launch failed");
+        fa.ctr = F->d_fused_ctr;
+        fa.ctr_base = F->fused_ctr_base;
+        unsigned long long used = 0;
+        if (k_fused(fa, F->stream, &used)) return fail("fused kernel launch failed");
+        F->fused_ctr_base += used;
       } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {
         return fail("curl B launch failed");
       }
@@ -1430,7 +1448,9 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
       return nullptr;
     }
   }
-  if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(1, atoi(zc));
+  if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(0, atoi(zc));
+  if (const char *bp = getenv("MNL_FUSED_BPC")) F->fused_bpc = std::max(1, atoi(bp));
+  if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
   if (finalize_fields(F.get())) return nullptr;
   return F.release();

@@ -132,7 +132,10 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
 // over box F, 3-D, no PML/dispersion/NR inside F (DESIGN.md "Fused interior").
 struct FusedArgs {
   Box F;
-  int zchunk;
+  int zchunk;         // > 0: force a segment seam every zchunk planes (tests)
+  int blocks_per_cu;  // persistent workgroups per CU (default 1)
+  int dist;           // prefetch distance in planes (1 or 2)
+  long long nelem;    // elements per field array (selects 32-bit offsets)
   double C;
   long long st1, st2;
   const double *Bo[3];
@@ -141,8 +144,10 @@ struct FusedArgs {
   double *Dn[3];
   const double *E[3];
   const double *u[3];
+  unsigned long long *ctr;      // work-item counter (monotone across launches)
+  unsigned long long ctr_base;  // counter value at the start of this launch
 };
-int k_fused(const FusedArgs &a, void *stream);
+int k_fused(const FusedArgs &a, void *stream, unsigned long long *consumed);
 // E = chi1inv * D over box F (leaving fused mode / readout)
 int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *stream);
 int k_fill(double *p, double v, size_t n, void *stream);

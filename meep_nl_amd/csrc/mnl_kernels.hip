@@ -699,120 +699,293 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
 // 888-903).  E is never stored inside F: it is recomputed as D*u whenever it
 // is read, which is bit-identical to the stored value of the reference.
 //
-// Work decomposition (2.5-D): a workgroup owns a (FX-1) x (FY-1) tile of
-// (x,y) columns plus a one-column low halo in x and y, and marches z over
-// `zchunk` planes (plus one halo plane below).  Per plane: E_k of the tile +
-// high halo goes to LDS, every thread computes B_new for its column (halo
-// threads too: those values are only needed for the D update and are
-// recomputed, not stored), B_new goes to LDS, then the inner threads update
-// D using B_new of the x-1 / y-1 neighbours (LDS) and of plane k-1
-// (registers).  HBM traffic per cell: read B, D, u, write B, D (15 x 8 B).
+// Work decomposition (2.5-D z-march).  A work item is a column tile of 64
+// (x) x 14 (y) cells and a chunk of zchunk z-planes.  Tiles start on 128-byte
+// boundaries in x (x0 = 16*floor(F.lo/16) + 64*t), so every row a wave loads
+// or stores is exactly four whole cache lines: partial-line writes (two
+// workgroups sharing a line at different times) cost ~20 % of HBM bandwidth
+// on this access pattern (tools/micro/stream_bench.hip: aligned 5.95 TB/s vs
+// misaligned 4.70 TB/s).  A 1024-thread workgroup is 16 waves:
+//   waves 0..14: one row each, lane = column (x0+lane).  Row 0 is the y-1
+//                halo row (B_new recomputed, nothing stored); rows 1..14 own.
+//   wave 15:     lanes 0..13  the x-1 halo column of rows 1..14 (B_new recomputed),
+//                lanes 16..30 E of the x+64 column (rows 0..14),
+//                lane 31      E(x0-1, y+15).
+//   wave 14 also loads the y+1 row of E.
+// LDS holds E(k) of the (66 x 16) footprint and B_new(k) of the (65 x 15)
+// footprint.  Items are handed out by an atomic counter in chunk-major order,
+// so workgroups sweep z roughly in lockstep and the halo lines a tile shares
+// with its neighbours are read from the last-level cache, not HBM.
+//
+// Memory pipeline: everything plane k needs from HBM (D,u or E of plane k+1,
+// B of plane k, the halo E of plane k) is one "batch"; batches are issued DIST
+// planes ahead into a register ring.  The loop body has no data-dependent
+// branches around memory operations: loads past the chunk are clamped to valid
+// planes, and stores of lanes/planes that must not write go through buffer
+// stores with an out-of-range offset (dropped by the hardware).  That keeps
+// the compiler's vmcnt accounting exact (in-order counter: a conditional store
+// would force a full drain at the join).
+// HBM traffic per cell: read B, D, u, write B, D (15 x 8 B).
 #define FX 64
-#define FY 16
+#define FR 15  // rows per tile incl. the y-1 halo row
+#define FOWN (FR - 1)
 
-template <bool HAS_U>
-__global__ __launch_bounds__(FX *FY) void fused_kernel(FusedArgs a) {
-  __shared__ double sE[3][FY + 1][FX + 1];
-  __shared__ double sB[3][FY][FX];
-  const int tx = threadIdx.x, ty = threadIdx.y;
-  const int gx = a.F.lo[0] - 1 + blockIdx.x * (FX - 1) + tx;
-  const int gy = a.F.lo[1] - 1 + blockIdx.y * (FY - 1) + ty;
-  const int z0 = a.F.lo[2] + blockIdx.z * a.zchunk;
-  const int z1 = min(z0 + a.zchunk, a.F.hi[2] + 1);
-  const bool load_ok = gx <= a.F.hi[0] + 1 && gy <= a.F.hi[1] + 1;
-  const bool col_ok = gx <= a.F.hi[0] && gy <= a.F.hi[1];
-  const bool inner = col_ok && tx >= 1 && ty >= 1;
-  const long long base = (long long)gx + (long long)gy * a.st1;
+typedef unsigned int mnl_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double ldg(const double *p, unsigned off) {
+  return *(const double *)((const char *)p + off);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mnl_u2, v), r, off, 0, 0);
+}
+constexpr unsigned MNL_OOB = 0xFFFFFFF0u;  // > any valid byte offset (arrays < 4 GiB)
+
+struct FBatch {  // what B(k) needs besides E(k): own raw at k+1, B_old(k), halo raw at k
+  double d0, d1, d2, u0, u1, u2, b0, b1, b2, h0, h1, hu0, hu1;
+  bool f, hf;
+};
+
+struct FusedGeom {
+  int xb, ntx, nty, nch, zc;
+  long long total;
+};
+__host__ __device__ inline FusedGeom fused_geom(const Box &F, int zchunk) {
+  FusedGeom g;
+  g.xb = F.lo[0] & ~15;
+  g.ntx = (F.hi[0] - g.xb) / FX + 1;
+  g.nty = (F.hi[1] - F.lo[1] + FOWN) / FOWN;
+  const int nz = F.hi[2] - F.lo[2] + 1;
+  g.zc = zchunk > 0 ? zchunk : 32;
+  g.nch = (nz + g.zc - 1) / g.zc;
+  g.total = (long long)g.ntx * g.nty * g.nch;
+  return g;
+}
+
+template <bool HAS_U, int DIST>
+__global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
+  __shared__ double sE[3][FR + 1][FX + 2];
+  __shared__ double sB[3][FR][FX + 1];
+  __shared__ long long s_item;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int flo0 = a.F.lo[0], flo1 = a.F.lo[1], flo2 = a.F.lo[2];
+  const int fhi0 = a.F.hi[0], fhi1 = a.F.hi[1], fhi2 = a.F.hi[2];
+  const FusedGeom G = fused_geom(a.F, a.zchunk);
+  const long long ntile = (long long)G.ntx * G.nty;
+  const unsigned s2 = (unsigned)(a.st2 * 8);  // byte stride of one z plane
   const double C = a.C;
-  auto inF = [&](int x, int y, int z) {
-    return x >= a.F.lo[0] && x <= a.F.hi[0] && y >= a.F.lo[1] && y <= a.F.hi[1] &&
-           z >= a.F.lo[2] && z <= a.F.hi[2];
-  };
-  auto e_at = [&](int c, int x, int y, int z, long long i) -> double {
-    if (inF(x, y, z)) {
-      double d = a.Do[c][i];
-      return HAS_U ? (d * a.u[c][i]) : d;
-    }
-    return a.E[c][i];
-  };
-  double Ek[3] = {0, 0, 0}, Ek1[3] = {0, 0, 0}, Dk[3] = {0, 0, 0}, Dk1[3] = {0, 0, 0};
-  double Hm[3] = {0, 0, 0};
-  if (load_ok) {
-    const int z = z0 - 1;
-    const long long i = base + (long long)z * a.st2;
-    for (int c = 0; c < 3; c++) Ek[c] = e_at(c, gx, gy, z, i);
+  const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
+  __amdgpu_buffer_rsrc_t rB[3], rD[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    rB[c] = __builtin_amdgcn_make_buffer_rsrc(a.Bn[c], 0, (int)nrec, 0x00020000);
+    rD[c] = __builtin_amdgcn_make_buffer_rsrc(a.Dn[c], 0, (int)nrec, 0x00020000);
   }
-  for (int k = z0 - 1; k < z1; k++) {
-    const long long i = base + (long long)k * a.st2;
-    // own column, plane k+1 (and D there, for the D update of the next plane)
-    if (load_ok) {
-      const long long i1 = i + a.st2;
-      const bool f1 = inF(gx, gy, k + 1);
-      for (int c = 0; c < 3; c++) {
-        if (f1) {
-          double d = a.Do[c][i1];
-          Dk1[c] = d;
-          Ek1[c] = HAS_U ? (d * a.u[c][i1]) : d;
-        } else {
-          Ek1[c] = a.E[c][i1];
+  // lane roles (fixed for the kernel)
+  int row, col;         // own-like lanes: footprint row / LDS column
+  bool ownlike;         // computes E->LDS and B_new
+  int hrow = 0, hcol = 0, hc0 = 0, hdx = 0, hdy = 0;  // halo slot: LDS target, comps, offset
+  bool hslot = false;
+  if (w < FR) {
+    row = w;
+    col = lane + 1;
+    ownlike = true;
+    if (w == FR - 1) {  // y+1 row
+      hslot = true;
+      hrow = FR;
+      hcol = col;
+      hc0 = 0;
+      hdx = lane;
+      hdy = FR;
+    }
+  } else {
+    row = lane + 1;
+    col = 0;
+    ownlike = lane < FOWN;
+    if (lane >= 16 && lane < 16 + FR) {  // x+64 column
+      hslot = true;
+      hrow = lane - 16;
+      hcol = FX + 1;
+      hc0 = 1;
+      hdx = FX;
+      hdy = lane - 16;
+    } else if (lane == 31) {  // E(x0-1, y0+FR)
+      hslot = true;
+      hrow = FR;
+      hcol = 0;
+      hc0 = 0;
+      hdx = -1;
+      hdy = FR;
+    }
+  }
+  const int ox = (w < FR) ? lane : -1;  // own-like column offset from x0
+  const int oy = row;                    // own-like row offset from y0
+  const double *hE0 = a.E[hc0], *hE1 = a.E[2], *hD0 = a.Do[hc0], *hD1 = a.Do[2];
+  const double *hU0 = a.u[HAS_U ? hc0 : 0], *hU1 = a.u[HAS_U ? 2 : 0];
+  const unsigned safe = (unsigned)((flo0 + (long long)flo1 * a.st1) * 8);
+  auto zin = [&](int z) { return z >= flo2 && z <= fhi2; };
+  auto e_of = [](double d, double u, bool fz) { return (HAS_U && fz) ? d * u : d; };
+
+  for (;;) {
+    if (threadIdx.x == 0) s_item = (long long)(atomicAdd(a.ctr, 1ULL) - a.ctr_base);
+    __syncthreads();  // also separates LDS use of consecutive items
+    const long long item = s_item;
+    if (item >= G.total) break;
+    const int ch = (int)(item / ntile);
+    const int tile = (int)(item % ntile);
+    const int zs = flo2 + ch * G.zc, ze = min(zs + G.zc, fhi2 + 1);  // planes [zs, ze)
+    const int x0 = G.xb + (tile % G.ntx) * FX, y0 = flo1 - 1 + (tile / G.ntx) * FOWN;
+
+    const int gx = x0 + ox, gy = y0 + oy;
+    const bool valid = ownlike && gx >= flo0 - 1 && gx <= fhi0 + 1 && gy >= flo1 - 1 &&
+                       gy <= fhi1 + 1;
+    const bool colF = valid && gx >= flo0 && gx <= fhi0 && gy >= flo1 && gy <= fhi1;
+    const bool store = colF && w < FR && row >= 1;
+    const unsigned cb = (unsigned)((gx + (long long)gy * a.st1) * 8);
+    const unsigned cbl = valid ? cb : safe;
+    const int hx = x0 + hdx, hy = y0 + hdy;
+    const bool hvalid = hslot && hx >= flo0 - 1 && hx <= fhi0 + 1 && hy >= flo1 - 1 &&
+                        hy <= fhi1 + 1;
+    const bool hF = hvalid && hx >= flo0 && hx <= fhi0 && hy >= flo1 && hy <= fhi1;
+    const unsigned hbl = hvalid ? (unsigned)((hx + (long long)hy * a.st1) * 8) : cbl;
+
+    auto load = [&](int k) -> FBatch {
+      FBatch q;
+      const int z1 = k + 1;
+      q.f = colF && zin(z1);
+      const unsigned o = cbl + (unsigned)z1 * s2;
+      q.d0 = ldg(q.f ? a.Do[0] : a.E[0], o);
+      q.d1 = ldg(q.f ? a.Do[1] : a.E[1], o);
+      q.d2 = ldg(q.f ? a.Do[2] : a.E[2], o);
+      if (HAS_U) {
+        q.u0 = ldg(a.u[0], o);
+        q.u1 = ldg(a.u[1], o);
+        q.u2 = ldg(a.u[2], o);
+      } else {
+        q.u0 = q.u1 = q.u2 = 1.0;
+      }
+      const unsigned ob = cbl + (unsigned)k * s2;
+      q.b0 = ldg(a.Bo[0], ob);
+      q.b1 = ldg(a.Bo[1], ob);
+      q.b2 = ldg(a.Bo[2], ob);
+      q.hf = hF && zin(k);
+      const unsigned oh = hbl + (unsigned)k * s2;
+      q.h0 = ldg(q.hf ? hD0 : hE0, oh);
+      q.h1 = ldg(q.hf ? hD1 : hE1, oh);
+      if (HAS_U) {
+        q.hu0 = ldg(hU0, oh);
+        q.hu1 = ldg(hU1, oh);
+      } else {
+        q.hu0 = q.hu1 = 1.0;
+      }
+      return q;
+    };
+
+    // prologue: E(zs-1) and the first DIST batches
+    double ex, ey, ez;
+    {
+      const int z = zs - 1;
+      const bool f0 = colF && zin(z);
+      const unsigned o = cbl + (unsigned)z * s2;
+      ex = ldg(f0 ? a.Do[0] : a.E[0], o);
+      ey = ldg(f0 ? a.Do[1] : a.E[1], o);
+      ez = ldg(f0 ? a.Do[2] : a.E[2], o);
+      if (HAS_U && f0) {
+        ex *= ldg(a.u[0], o);
+        ey *= ldg(a.u[1], o);
+        ez *= ldg(a.u[2], o);
+      }
+    }
+    FBatch q[DIST + 1];
+#pragma unroll
+    for (int j = 0; j < DIST; j++) q[j] = load(min(zs - 1 + j, ze - 1));
+    double dx = 0, dy = 0, dz = 0, hmx = 0, hmy = 0;
+    const int rowm = row > 0 ? row - 1 : 0, colm = col > 0 ? col - 1 : 0;
+    const int ngrp = (ze - zs + 1 + DIST) / (DIST + 1);  // iterations k = zs-1 .. ze-1, padded
+    for (int g = 0; g < ngrp; g++) {
+#pragma unroll
+      for (int j = 0; j <= DIST; j++) {
+        const int k = zs - 1 + g * (DIST + 1) + j;
+        q[(j + DIST) % (DIST + 1)] = load(min(k + DIST, ze - 1));
+        const FBatch &c = q[j];
+        const double e1x = e_of(c.d0, c.u0, c.f), e1y = e_of(c.d1, c.u1, c.f),
+                     e1z = e_of(c.d2, c.u2, c.f);
+        if (ownlike) {
+          sE[0][row][col] = ex;
+          sE[1][row][col] = ey;
+          sE[2][row][col] = ez;
         }
+        if (hslot) {
+          sE[hc0][hrow][hcol] = e_of(c.h0, c.hu0, c.hf);
+          sE[2][hrow][hcol] = e_of(c.h1, c.hu1, c.hf);
+        }
+        __syncthreads();
+        const double Ez_yp = sE[2][row + 1][col], Ex_yp = sE[0][row + 1][col];
+        const double Ey_xp = sE[1][row][col + 1], Ez_xp = sE[2][row][col + 1];
+        const double Bx = c.b0 - C * (Ez_yp - ez + ey - e1y);
+        const double By = c.b1 - C * (e1x - ex + ez - Ez_xp);
+        const double Bz = c.b2 - C * (Ey_xp - ey + ex - Ex_yp);
+        const unsigned os = (store && k >= zs && k < ze) ? cb + (unsigned)k * s2 : MNL_OOB;
+        bst(rB[0], os, Bx);
+        bst(rB[1], os, By);
+        bst(rB[2], os, Bz);
+        if (ownlike) {
+          sB[0][row][col] = Bx;
+          sB[1][row][col] = By;
+          sB[2][row][col] = Bz;
+        }
+        __syncthreads();
+        const double Hz_ym = sB[2][rowm][col], Hx_ym = sB[0][rowm][col];
+        const double Hz_xm = sB[2][row][colm], Hy_xm = sB[1][row][colm];
+        bst(rD[0], os, dx - C * (Hz_ym - Bz + By - hmy));
+        bst(rD[1], os, dy - C * (hmx - Bx + Bz - Hz_xm));
+        bst(rD[2], os, dz - C * (Hy_xm - By + Bx - Hx_ym));
+        hmx = Bx;
+        hmy = By;
+        dx = c.d0;
+        dy = c.d1;
+        dz = c.d2;
+        ex = e1x;
+        ey = e1y;
+        ez = e1z;
       }
-      for (int c = 0; c < 3; c++) sE[c][ty][tx] = Ek[c];
-      if (tx == FX - 1 && col_ok) {
-        sE[1][ty][FX] = e_at(1, gx + 1, gy, k, i + 1);
-        sE[2][ty][FX] = e_at(2, gx + 1, gy, k, i + 1);
-      }
-      if (ty == FY - 1 && col_ok) {
-        sE[0][FY][tx] = e_at(0, gx, gy + 1, k, i + a.st1);
-        sE[2][FY][tx] = e_at(2, gx, gy + 1, k, i + a.st1);
-      }
-    }
-    __syncthreads();
-    double Bx = 0, By = 0, Bz = 0;
-    if (col_ok) {
-      const double Ex = sE[0][ty][tx], Ey = sE[1][ty][tx], Ez = sE[2][ty][tx];
-      const double Ez_yp = sE[2][ty + 1][tx], Ex_yp = sE[0][ty + 1][tx];
-      const double Ey_xp = sE[1][ty][tx + 1], Ez_xp = sE[2][ty][tx + 1];
-      Bx = a.Bo[0][i] - C * (Ez_yp - Ez + Ey - Ek1[1]);
-      By = a.Bo[1][i] - C * (Ek1[0] - Ex + Ez - Ez_xp);
-      Bz = a.Bo[2][i] - C * (Ey_xp - Ey + Ex - Ex_yp);
-      if (inner && k >= z0) {
-        a.Bn[0][i] = Bx;
-        a.Bn[1][i] = By;
-        a.Bn[2][i] = Bz;
-      }
-      sB[0][ty][tx] = Bx;
-      sB[1][ty][tx] = By;
-      sB[2][ty][tx] = Bz;
-    }
-    __syncthreads();
-    if (inner && k >= z0) {
-      const double Hz_ym = sB[2][ty - 1][tx], Hx_ym = sB[0][ty - 1][tx];
-      const double Hz_xm = sB[2][ty][tx - 1], Hy_xm = sB[1][ty][tx - 1];
-      a.Dn[0][i] = Dk[0] - C * (Hz_ym - Bz + By - Hm[1]);
-      a.Dn[1][i] = Dk[1] - C * (Hm[0] - Bx + Bz - Hz_xm);
-      a.Dn[2][i] = Dk[2] - C * (Hy_xm - By + Bx - Hx_ym);
-    }
-    Hm[0] = Bx;
-    Hm[1] = By;
-    Hm[2] = Bz;
-    for (int c = 0; c < 3; c++) {
-      Ek[c] = Ek1[c];
-      Dk[c] = Dk1[c];
     }
   }
 }
 
-int k_fused(const FusedArgs &a, void *stream) {
-  int n0 = a.F.hi[0] - a.F.lo[0] + 1, n1 = a.F.hi[1] - a.F.lo[1] + 1,
-      n2 = a.F.hi[2] - a.F.lo[2] + 1;
-  if (n0 <= 0 || n1 <= 0 || n2 <= 0) return 0;
-  dim3 grd((n0 + FX - 2) / (FX - 1), (n1 + FY - 2) / (FY - 1), (n2 + a.zchunk - 1) / a.zchunk);
+static int fused_grid_blocks(int bpc) {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256 * bpc;
+  if (!cus[dev]) {
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return 256 * bpc;
+    cus[dev] = pr.multiProcessorCount;
+  }
+  return cus[dev] * bpc;
+}
+
+int k_fused(const FusedArgs &a, void *stream, unsigned long long *consumed) {
+  *consumed = 0;
+  for (int d = 0; d < 3; d++)
+    if (a.F.hi[d] < a.F.lo[d]) return 0;
+  if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr) return 1;  // host guarantees < 4 GiB arrays
+  const FusedGeom G = fused_geom(a.F, a.zchunk);
+  long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
+  if (nb > G.total) nb = G.total;
+  dim3 grd((unsigned)nb), blk(1024);
   hipStream_t s = (hipStream_t)stream;
-  if (a.u[0])
-    fused_kernel<true><<<grd, dim3(FX, FY), 0, s>>>(a);
-  else
-    fused_kernel<false><<<grd, dim3(FX, FY), 0, s>>>(a);
+  const bool d2 = a.dist == 2;
+  if (a.u[0]) {
+    if (d2)
+      fused_kernel<true, 2><<<grd, blk, 0, s>>>(a);
+    else
+      fused_kernel<true, 1><<<grd, blk, 0, s>>>(a);
+  } else {
+    if (d2)
+      fused_kernel<false, 2><<<grd, blk, 0, s>>>(a);
+    else
+      fused_kernel<false, 1><<<grd, blk, 0, s>>>(a);
+  }
+  *consumed = (unsigned long long)(G.total + nb);  // every workgroup takes one failing item
   return rc();
 }
 
