@@ -155,7 +155,8 @@ int mnl_fields_traffic_model(mnl_fields *f, double *bytes_per_cell_step, double 
  * (used automatically for 3-D non-dispersive, non-NR configurations without
  * magnetic or integrated sources).  Results are identical either way. */
 int mnl_fields_set_fused(mnl_fields *f, int allow);
-/* 1 if the last step ran the fused interior kernel, else 0. */
+/* bit 0: the last step ran the fused interior kernel; bit 1: it read chi1inv
+ * through the palette (DESIGN.md "chi1inv palette"). */
 int mnl_fields_mode(mnl_fields *f, int *fused);
 /* Enable HIP-event timing around every sub-step kernel group (on the stream
  * the kernels run on) and reset the accumulated timers. */

@@ -248,7 +248,13 @@ class Fields:
     def fused_active(self):
         v = ctypes.c_int()
         check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
-        return bool(v.value)
+        return bool(v.value & 1)
+
+    def fused_palette(self):
+        """True if the fused kernel reads chi1inv through the byte palette."""
+        v = ctypes.c_int()
+        check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
+        return bool(v.value & 2)
 
     def set_fused(self, allow=True):
         check(lib().mnl_fields_set_fused(self.h, int(allow)))

@@ -18,6 +18,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <set>
+#include <unordered_set>
 #include <string>
 #include <vector>
 
@@ -169,6 +171,9 @@ struct mnl_fields {
   int fused_dist = 1;
   unsigned long long *d_fused_ctr = nullptr;  // work-item counter of the fused kernel
   unsigned long long fused_ctr_base = 0;
+  bool palette_tried = false;
+  unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedF (null: f64 chi1inv)
+  double *d_utab = nullptr;    // 3 x 256 palette values
   bool allow_fused = true;
   CurlPlan planB, planD;
   bool nr = false;
@@ -1143,6 +1148,62 @@ bool fused_possible(mnl_fields *F) {
   return true;
 }
 
+// chi1inv palette for the fused kernel (DESIGN.md "chi1inv palette"): at most
+// 256 distinct values per component, candidates taken from the structure (1.0
+// default, user chi1inv arrays, 1/eps of geometry boxes) and verified cell by
+// cell on the device (bitwise), so a missing value just disables the palette.
+int build_palette(mnl_fields *F) {
+  if (F->palette_tried) return 0;
+  F->palette_tried = true;
+  const mnl_structure &S = F->S;
+  DevFields &f = F->f;
+  if (!f.inveps[0] || !f.inveps[1] || !f.inveps[2]) return 0;
+  if (const char *np = getenv("MNL_NO_PALETTE"))
+    if (atoi(np)) return 0;
+  std::vector<double> tab(3 * 256, 0.0);
+  int n[3];
+  for (int c = 0; c < 3; c++) {
+    std::set<uint64_t> cand;
+    auto bits = [](double v) {
+      uint64_t u;
+      memcpy(&u, &v, 8);
+      return u;
+    };
+    cand.insert(bits(1.0));
+    const auto &diag = S.chi1inv[c][c];
+    if (!diag.empty()) {
+      std::unordered_set<uint64_t> us;
+      for (double v : diag) {
+        us.insert(bits(v));
+        if (us.size() > 256) return 0;
+      }
+      cand.insert(us.begin(), us.end());
+    }
+    for (auto &b : S.boxes)
+      if (b.kind == 0) cand.insert(bits(1.0 / b.value));
+    if (cand.size() > 256) return 0;
+    n[c] = (int)cand.size();
+    int k = 0;
+    for (uint64_t u : cand) memcpy(&tab[256 * c + k++], &u, 8);  // ascending bit patterns
+  }
+  unsigned *uidx;
+  double *utab;
+  int *bad;
+  if (dev_alloc(F, &uidx, F->nlocal) || dev_alloc(F, &utab, 3 * 256) || dev_alloc(F, &bad, 1))
+    return -1;
+  HIPCHK(hipMemcpyAsync(utab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, F->stream));
+  const double *u[3] = {f.inveps[0], f.inveps[1], f.inveps[2]};
+  if (k_build_uidx(uidx, u, utab, n, F->fusedF, F->g.st[1], F->g.st[2], bad, F->stream))
+    return fail("palette index build failed");
+  int hbad = 0;
+  HIPCHK(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, F->stream));
+  HIPCHK(hipStreamSynchronize(F->stream));
+  if (hbad) return 0;
+  F->d_uidx = uidx;
+  F->d_utab = utab;
+  return 0;
+}
+
 int set_fused(mnl_fields *F, bool on) {
   DevFields &f = F->f;
   if (on == F->fused) return 0;
@@ -1152,6 +1213,7 @@ int set_fused(mnl_fields *F, bool on) {
       HIPCHK(hipMemsetAsync(F->d_fused_ctr, 0, sizeof(unsigned long long), F->stream));
       F->fused_ctr_base = 0;
     }
+    if (build_palette(F)) return -1;
     for (int d = 0; d < 3; d++) {
       if (!F->pp_B[d] && dev_alloc(F, &F->pp_B[d], F->nlocal)) return -1;
       if (!F->pp_D[d] && dev_alloc(F, &F->pp_D[d], F->nlocal)) return -1;
@@ -1314,6 +1376,8 @@ int step_batch(mnl_fields *F, int nsteps) {
         }
         if ((fa.u[0] != nullptr) != (fa.u[1] != nullptr) || (fa.u[0] != nullptr) != (fa.u[2] != nullptr))
           return fail("fused kernel needs all or no chi1inv arrays");
+        fa.uidx = F->d_uidx;
+        fa.utab = F->d_utab;
         fa.ctr = F->d_fused_ctr;
         fa.ctr_base = F->fused_ctr_base;
         unsigned long long used = 0;
@@ -1770,10 +1834,11 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
   for (int k = 0; k < 3; k++) pts *= double(b.hi[k] - b.lo[k] + 1);
   if (b.hi[0] < b.lo[0]) pts = 0;
   if (F->fused && which == 0) {
-    // fused step: read B(3), D(3), chi1inv(3 if present); write B(3), D(3)
+    // fused step: read B(3), D(3), chi1inv(3 doubles, or one 4-byte palette
+    // index word); write B(3), D(3)
     int nu = 0;
     for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
-    *bytes_per_launch = pts * 8.0 * (12 + nu);
+    *bytes_per_launch = pts * (8.0 * 12 + (F->d_uidx ? 4.0 : 8.0 * nu));
     return 0;
   }
   // interior curl: read 3 source comps + read/write the updated comps
@@ -1788,7 +1853,7 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
 
 int mnl_fields_mode(mnl_fields *F, int *fused) {
   if (!F) return fail("null fields");
-  *fused = F->fused ? 1 : 0;
+  *fused = (F->fused ? 1 : 0) | (F->fused && F->d_uidx ? 2 : 0);
   return 0;
 }
 
@@ -1804,7 +1869,7 @@ int mnl_fields_traffic_model(mnl_fields *F, double *bpc, double *cells) {
   for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
   double b;
   if (F->fused) {
-    b = 8.0 * (4 * n + nu);
+    b = 8.0 * (4 * n) + (F->d_uidx ? 4.0 : 8.0 * nu);  // palette: one 4-byte index word
   } else {
     b = 8.0 * (3 * n) * 2 + 8.0 * (2 * n) + 8.0 * nu;
     for (int k = 0; k < F->f.npol; k++)

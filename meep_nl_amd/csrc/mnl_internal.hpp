@@ -144,10 +144,14 @@ struct FusedArgs {
   double *Dn[3];
   const double *E[3];
   const double *u[3];
+  const unsigned *uidx;         // chi1inv palette indices (nullptr: use u / none)
+  const double *utab;           // palette, 3 x 256 doubles
   unsigned long long *ctr;      // work-item counter (monotone across launches)
   unsigned long long ctr_base;  // counter value at the start of this launch
 };
 int k_fused(const FusedArgs &a, void *stream, unsigned long long *consumed);
+int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
+                 const Box &F, long long st1, long long st2, int *bad, void *stream);
 // E = chi1inv * D over box F (leaving fused mode / readout)
 int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *stream);
 int k_fill(double *p, double v, size_t n, void *stream);

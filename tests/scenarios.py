@@ -225,15 +225,23 @@ def sc_waveguide_3d(make, L=3.2, steps=40, eps=12.0):
     return o
 
 
-def sc_big_box_3d(make, sizes=(14.0, 4.1, 15.3), steps=30, dpml=0.7, eps=6.0, extra=None):
+def sc_big_box_3d(make, sizes=(14.0, 4.1, 15.3), steps=30, dpml=0.7, eps=6.0, extra=None,
+                  random_eps=False):
     """Non-cubic grid spanning many fused tiles in x, y and z; dielectric slab across
-    the PML boundary; optional callback(o) after half the steps (mode toggles)."""
+    the PML boundary; optional callback(o) after half the steps (mode toggles).
+    random_eps: seeded random eps in [1, 12] in the slab (thousands of distinct
+    chi1inv values: more than the fused kernel's 256-entry palette)."""
     o = vol(make, 3, list(sizes), 10, center_origin=True)
     o.add_pml(dpml)
     for c in E_COMPS:
         x, y, z = o.coords(c)
         inside = (np.abs(y) < 0.8) & (z > -0.4) & (z < 3.0)
-        o.set_chi1inv(c, c, np.where(inside, 1.0 / eps, 1.0))
+        if random_eps:
+            rng = np.random.default_rng(1234 + c)
+            val = 1.0 / rng.uniform(1.0, 12.0, size=x.shape)
+        else:
+            val = 1.0 / eps
+        o.set_chi1inv(c, c, np.where(inside, val, 1.0))
     o.add_gaussian_source(2, 0.25, 4.0, 0.0, 40.0, (0.37, -0.21, 0.05), 1.0)
     o.add_gaussian_source(0, 0.3, 4.0, 0.0, 40.0, (-3.3, 0.6, 2.15), 0.6)
     o.step(steps // 2)

@@ -132,3 +132,32 @@ def test_fused_mode_toggle():
         o.add_gaussian_source(4, 0.3, 3.0, 0.0, 30.0, (1.0, 0.3, -1.1), 0.8)
     _bitwise(sc_big_box_3d(ProductSim, steps=24, extra=add_h),
              sc_big_box_3d(make_oracle, steps=24, extra=add_h))
+
+
+def test_fused_palette_used():
+    """Two distinct chi1inv values: the fused kernel reads them through the byte
+    palette (4 B/cell instead of 24) and stays bitwise equal to the oracle."""
+    p = sc_big_box_3d(ProductSim, steps=12)
+    f = p._fields()
+    assert f.fused_active() and f.fused_palette()
+    _bitwise(p, sc_big_box_3d(make_oracle, steps=12))
+
+
+def test_fused_f64_chi1inv(monkeypatch):
+    monkeypatch.setenv("MNL_NO_PALETTE", "1")
+    p = sc_big_box_3d(ProductSim, steps=12)
+    assert p._fields().fused_active() and not p._fields().fused_palette()
+    _bitwise(p, sc_big_box_3d(make_oracle, steps=12))
+
+
+def test_fused_many_distinct_chi1inv():
+    """More distinct chi1inv values than the palette holds: f64 chi1inv path."""
+    p = sc_big_box_3d(ProductSim, steps=12, random_eps=True)
+    assert p._fields().fused_active() and not p._fields().fused_palette()
+    _bitwise(p, sc_big_box_3d(make_oracle, steps=12, random_eps=True))
+
+
+@pytest.mark.parametrize("dist", ["1", "2"])
+def test_fused_prefetch_distance(monkeypatch, dist):
+    monkeypatch.setenv("MNL_FUSED_DIST", dist)
+    _bitwise(sc_big_box_3d(ProductSim, steps=10), sc_big_box_3d(make_oracle, steps=10))
