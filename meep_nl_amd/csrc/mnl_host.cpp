@@ -169,9 +169,10 @@ struct mnl_fields {
   int fused_zchunk = 0;
   int fused_bpc = 1;
   int fused_dist = 1;
+  int fused_nq = 1;
   unsigned long long *d_fused_ctr = nullptr;  // work-item counter of the fused kernel
-  unsigned long long fused_ctr_base = 0;
   bool palette_tried = false;
+  bool dsrc_in_shell = false;  // a D source point lies outside the interior box
   unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedF (null: f64 chi1inv)
   double *d_utab = nullptr;    // 3 x 256 palette values
   bool allow_fused = true;
@@ -1209,9 +1210,7 @@ int set_fused(mnl_fields *F, bool on) {
   if (on == F->fused) return 0;
   if (on) {
     if (!F->d_fused_ctr) {
-      if (dev_alloc(F, &F->d_fused_ctr, 1)) return -1;
-      HIPCHK(hipMemsetAsync(F->d_fused_ctr, 0, sizeof(unsigned long long), F->stream));
-      F->fused_ctr_base = 0;
+      if (dev_alloc(F, &F->d_fused_ctr, 8 * 16)) return -1;  // 8 queue counters, 128 B apart
     }
     if (build_palette(F)) return -1;
     for (int d = 0; d < 3; d++) {
@@ -1261,6 +1260,18 @@ struct EvPair {
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
   if (set_fused(F, fused_possible(F))) return -1;
+  {  // does a D source point lie in the shell (outside the box the interior kernels own)?
+    const Box &ib = F->fused ? F->fusedF : F->interior;
+    F->dsrc_in_shell = false;
+    for (long long idx : F->srcD_idx) {
+      const long long i2 = idx / F->g.st[2], r = idx % F->g.st[2];
+      const long long i1 = r / F->g.st[1], i0 = r % F->g.st[1];
+      const long long ii[3] = {i0, i1, i2};
+      bool in = true;
+      for (int a = 0; a < 3; a++) in = in && ii[a] >= ib.lo[a] && ii[a] <= ib.hi[a];
+      if (!in) F->dsrc_in_shell = true;
+    }
+  }
   const double dt = F->dt;
   // per-step source values, computed on the host exactly as the reference
   size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
@@ -1362,6 +1373,7 @@ int step_batch(mnl_fields *F, int nsteps) {
         fa.zchunk = F->fused_zchunk;
         fa.blocks_per_cu = F->fused_bpc;
         fa.dist = F->fused_dist;
+        fa.nqueues = F->fused_nq;
         fa.nelem = (long long)F->nlocal;
         fa.C = F->S.courant;
         fa.st1 = g.st[1];
@@ -1379,16 +1391,15 @@ int step_batch(mnl_fields *F, int nsteps) {
         fa.uidx = F->d_uidx;
         fa.utab = F->d_utab;
         fa.ctr = F->d_fused_ctr;
-        fa.ctr_base = F->fused_ctr_base;
-        unsigned long long used = 0;
-        if (k_fused(fa, F->stream, &used)) return fail("fused kernel launch failed");
-        F->fused_ctr_base += used;
+        if (k_fused(fa, F->stream)) return fail("fused kernel launch failed");
       } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {
         return fail("curl B launch failed");
       }
       ev_end(k);
+      // shell curl B; the PML H update rides along when no B source sits between
+      const bool fuseH = nB == 0;
       k = ev_begin(TM_B);
-      if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream))
+      if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream, fuseH))
         return fail("curl B launch failed");
       ev_end(k);
       if (nB && k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
@@ -1396,7 +1407,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       k = ev_begin(TM_H);
       bool anyH = false;
       for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
-      if (anyH && k_update_h(*sl, g, f, F->stream)) return fail("update H launch failed");
+      if (!fuseH && anyH && k_update_h(*sl, g, f, F->stream)) return fail("update H launch failed");
       ev_end(k);
       if (F->nranks > 1) {
         int kk = ev_begin(TM_HALO);
@@ -1408,8 +1419,10 @@ int step_batch(mnl_fields *F, int nsteps) {
       if (!F->fused && k_curl(T_D, F->interior, nullptr, g, f, F->planD, F->S.courant, F->stream))
         return fail("curl D launch failed");
       ev_end(k);
+      // shell curl D; the shell E update rides along when it only reads its own D
+      const bool fuseE = !F->nr && f.npol == 0 && nI == 0 && !F->dsrc_in_shell;
       k = ev_begin(TM_D);
-      if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream))
+      if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream, fuseE))
         return fail("curl D launch failed");
       ev_end(k);
       if (nD && k_source(T_D, g, f, sD, 0, F->stream)) return fail("source launch failed");
@@ -1420,7 +1433,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       k = ev_begin(TM_E);
       bool fuse = !F->nr;
       if ((!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) ||
-          k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream))
+          (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream)))
         return fail("update E launch failed");
       if (!fuse && f.npol) {
         if (k_update_pols(F->interior, nullptr, g, f, F->stream) ||
@@ -1515,6 +1528,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(0, atoi(zc));
   if (const char *bp = getenv("MNL_FUSED_BPC")) F->fused_bpc = std::max(1, atoi(bp));
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
+  if (const char *fq = getenv("MNL_FUSED_QUEUES")) F->fused_nq = atoi(fq) == 8 ? 8 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
   if (finalize_fields(F.get())) return nullptr;
   return F.release();

@@ -119,8 +119,11 @@ struct Launch {
 };
 
 // interior: one box on a 3-D grid; shell: all shell boxes in one launch
+// fuseup (shell only): apply the per-point H (after B) / E (after D) update in
+// the same kernel (no B sources; no NR, susceptibilities, integrated sources
+// or D sources in the shell)
 int k_curl(int ft, const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
-           const CurlPlan &p, double courant, void *stream);
+           const CurlPlan &p, double courant, void *stream, bool fuseup = false);
 int k_update_h(const BoxList &shell, const DevGrid &g, const DevFields &f, void *stream);
 int k_update_e(const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
                const ISrcDev &is, int step, bool fuse_pols, void *stream);
@@ -135,6 +138,7 @@ struct FusedArgs {
   int zchunk;         // > 0: force a segment seam every zchunk planes (tests)
   int blocks_per_cu;  // persistent workgroups per CU (default 1)
   int dist;           // prefetch distance in planes (1 or 2)
+  int nqueues;        // work queues: 1 (global, default) or 8 (one per XCD)
   long long nelem;    // elements per field array (selects 32-bit offsets)
   double C;
   long long st1, st2;
@@ -146,10 +150,9 @@ struct FusedArgs {
   const double *u[3];
   const unsigned *uidx;         // chi1inv palette indices (nullptr: use u / none)
   const double *utab;           // palette, 3 x 256 doubles
-  unsigned long long *ctr;      // work-item counter (monotone across launches)
-  unsigned long long ctr_base;  // counter value at the start of this launch
+  unsigned long long *ctr;      // 8 work-queue counters (128 B apart), reset per launch
 };
-int k_fused(const FusedArgs &a, void *stream, unsigned long long *consumed);
+int k_fused(const FusedArgs &a, void *stream);
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
                  const Box &F, long long st1, long long st2, int *bad, void *stream);
 // E = chi1inv * D over box F (leaving fused mode / readout)

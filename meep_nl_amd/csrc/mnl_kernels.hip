@@ -96,25 +96,26 @@ __device__ __forceinline__ bool pml_at(const DevFields &f, const DevGrid &g, int
 // Apply one curl update with the per-point PML branch selection of step_curl
 // (src/step_generic.cpp:84-252, cnd == NULL).
 template <int FT>
-__device__ __forceinline__ void curl_apply(const DevFields &f, const DevGrid &g, const Pt &p, int d,
-                                           long long i, double T, double dtdx) {
+__device__ __forceinline__ double curl_apply(const DevFields &f, const DevGrid &g, const Pt &p,
+                                             int d, long long i, double T, double dtdx) {
   const double *Fo = FT == T_B ? f.B[d] : f.D[d];
   double *F = FT == T_B ? f.Bn[d] : f.Dn[d];
   const int dsig = (d + 1) % 3, dsigu = (d + 2) % 3;
   const int k = qcoord(g, p, FT, d, dsig), ku = qcoord(g, p, FT, d, dsigu);
   const bool ps = pml_at(f, g, dsig, k), pu = pml_at(f, g, dsigu, ku);
+  double nv;
   if (!ps && !pu) {
-    F[i] = Fo[i] - dtdx * T;
+    nv = Fo[i] - dtdx * T;
   } else if (!ps) {
     double *U = FT == T_B ? f.UB[d] : f.UD[d];
     const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
     double fprev = U[i];
     double fu = fprev - dtdx * T;
     U[i] = fu;
-    F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
+    nv = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
   } else if (!pu) {
     const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
-    F[i] = ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
+    nv = ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
   } else {
     double *U = FT == T_B ? f.UB[d] : f.UD[d];
     const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
@@ -122,7 +123,43 @@ __device__ __forceinline__ void curl_apply(const DevFields &f, const DevGrid &g,
     double fprev = U[i];
     double fu = ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
     U[i] = fu;
-    F[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
+    nv = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
+  }
+  F[i] = nv;
+  return nv;
+}
+
+// The per-point update that follows a curl in the same sub-step, fused into
+// the shell curl kernel when nothing (a source, a neighbour read) sits between
+// them: H from B (update_h_kernel below) and, without chi(2) Newton-Raphson,
+// susceptibilities or integrated sources, E from D (update_e_kernel below).
+template <int FT>
+__device__ __forceinline__ void fused_point_update(const DevFields &f, const DevGrid &g,
+                                                   const Pt &p, int d, long long i, double nv) {
+  if (FT == T_B) {  // update_eh(H_stuff), src/update_eh.cpp:186-259
+    if (!f.hcomp_present[d] || !f.H[d]) return;
+    const int kw = qcoord(g, p, T_H, d, d);
+    if (!pml_at(f, g, d, kw)) return;
+    double fwprev = f.WH[d][i];
+    double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
+    double fw = nv;
+    f.WH[d][i] = fw;
+    f.H[d][i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+  } else {  // update_eh(E_stuff), diagonal chi1inv, no P (src/step_generic.cpp:576-906)
+    if (!f.ecomp_present[d]) return;
+    const double gs = nv;
+    const double *u = f.inveps[d];
+    double *E = f.E[d];
+    const int kw = qcoord(g, p, T_E, d, d);
+    if (pml_at(f, g, d, kw)) {
+      double fwprev = f.WE[d][i];
+      double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
+      double fw = u ? (gs * u[i]) : gs;
+      f.WE[d][i] = fw;
+      E[i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+    } else {
+      E[i] = u ? (gs * u[i]) : gs;
+    }
   }
 }
 
@@ -131,69 +168,68 @@ __device__ __forceinline__ void curl_apply(const DevFields &f, const DevGrid &g,
 // src/step_generic.cpp:69-253, conductivity-free branches).  Component d of
 // B (D): g1 = E (H) comp (d+2)%3 along dir (d+1)%3, g2 = comp (d+1)%3 along
 // dir (d+2)%3; D uses negated strides (src/step_db.cpp:81-84).
-template <int FT, bool SHELL>
+template <int FT, bool SHELL, bool FUSEUP>
 __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl, DevGrid g,
                                                                DevFields f, CurlPlan pl, double C) {
   Pt p;
   if (!map_pt<SHELL>(b, bl, g, p)) return;
   const long long i = p.idx;
-#pragma unroll
-  for (int d = 0; d < 3; d++) {
+  // shell launches are component-parallel (blockIdx.y = component): one
+  // dependent load chain per thread instead of three
+  const int dlo = SHELL ? (int)blockIdx.y : 0, dhi = SHELL ? (int)blockIdx.y + 1 : 3;
+  for (int d = dlo; d < dhi; d++) {
     if (!pl.present[d]) continue;
     if (!owned(g, FT, d, p)) continue;
     const int c1 = (d + 2) % 3, dir1 = (d + 1) % 3;
     const int c2 = (d + 1) % 3, dir2 = (d + 2) % 3;
     long long s1 = g.sdir[dir1], s2 = g.sdir[dir2];
-    const double *g1, *g2;
-    if (FT == T_B) {
-      g1 = f.E[c1];
-      g2 = f.E[c2];
-      if (SHELL && f.fused) {  // E is not stored inside the fused box: E = D*chi1inv
-        const int x = p.j[0], y = p.j[1], z = p.j[2];
-        auto inF = [&](int dd) {
-          const int xx = x + (dd == 0), yy = y + (dd == 1), zz = z + (dd == 2);
-          return xx >= f.fF.lo[0] && xx <= f.fF.hi[0] && yy >= f.fF.lo[1] && yy <= f.fF.hi[1] &&
-                 zz >= f.fF.lo[2] && zz <= f.fF.hi[2];
-        };
-        auto e_at = [&](int c, long long n, int dd) -> double {
-          if (inF(dd)) {
-            const double dv = f.D[c][n];
-            return f.inveps[c] ? (dv * f.inveps[c][n]) : dv;
-          }
-          return f.E[c][n];
-        };
-        const int terms = pl.terms[d];
-        double T, dtdx = C;
-        if (terms == 3) {
-          T = e_at(c1, i + s1, dir1) - e_at(c1, i, -1) + e_at(c2, i, -1) - e_at(c2, i + s2, dir2);
-        } else if (terms == 1) {
-          T = e_at(c1, i + s1, dir1) - e_at(c1, i, -1);
-        } else {
-          T = e_at(c2, i + s2, dir2) - e_at(c2, i, -1);
-          dtdx = -C;
+    const int terms = pl.terms[d];
+    double T, dtdx = C;
+    if (FT == T_B && SHELL && f.fused) {  // E is not stored inside the fused box: E = D*chi1inv
+      const int x = p.j[0], y = p.j[1], z = p.j[2];
+      auto inF = [&](int dd) {
+        const int xx = x + (dd == 0), yy = y + (dd == 1), zz = z + (dd == 2);
+        return xx >= f.fF.lo[0] && xx <= f.fF.hi[0] && yy >= f.fF.lo[1] && yy <= f.fF.hi[1] &&
+               zz >= f.fF.lo[2] && zz <= f.fF.hi[2];
+      };
+      auto e_at = [&](int c, long long n, int dd) -> double {
+        if (inF(dd)) {
+          const double dv = f.D[c][n];
+          return f.inveps[c] ? (dv * f.inveps[c][n]) : dv;
         }
-        curl_apply<FT>(f, g, p, d, i, T, dtdx);
-        continue;
+        return f.E[c][n];
+      };
+      if (terms == 3) {
+        T = e_at(c1, i + s1, dir1) - e_at(c1, i, -1) + e_at(c2, i, -1) - e_at(c2, i + s2, dir2);
+      } else if (terms == 1) {
+        T = e_at(c1, i + s1, dir1) - e_at(c1, i, -1);
+      } else {
+        T = e_at(c2, i + s2, dir2) - e_at(c2, i, -1);
+        dtdx = -C;
       }
     } else {
-      s1 = -s1;
-      s2 = -s2;
-      g1 = f.Bn[c1];  // H == B (new) outside PML chunks
-      g2 = f.Bn[c2];
-      if (SHELL) {  // H separate only in chunks with PML along the H direction
-        if (f.H[c1] && pml_at(f, g, c1, qcoord(g, p, T_H, c1, c1))) g1 = f.H[c1];
-        if (f.H[c2] && pml_at(f, g, c2, qcoord(g, p, T_H, c2, c2))) g2 = f.H[c2];
+      const double *g1, *g2;
+      if (FT == T_B) {
+        g1 = f.E[c1];
+        g2 = f.E[c2];
+      } else {
+        s1 = -s1;
+        s2 = -s2;
+        g1 = f.Bn[c1];  // H == B (new) outside PML chunks
+        g2 = f.Bn[c2];
+        if (SHELL) {  // H separate only in chunks with PML along the H direction
+          if (f.H[c1] && pml_at(f, g, c1, qcoord(g, p, T_H, c1, c1))) g1 = f.H[c1];
+          if (f.H[c2] && pml_at(f, g, c2, qcoord(g, p, T_H, c2, c2))) g2 = f.H[c2];
+        }
       }
-    }
-    double T, dtdx = C;
-    const int terms = pl.terms[d];
-    if (terms == 3) {
-      T = g1[i + s1] - g1[i] + g2[i] - g2[i + s2];
-    } else if (terms == 1) {
-      T = g1[i + s1] - g1[i];
-    } else {  // g1 == NULL: swap and flip the sign (src/step_generic.cpp:76-80)
-      T = g2[i + s2] - g2[i];
-      dtdx = -C;
+      if (terms == 3) {
+        T = g1[i + s1] - g1[i] + g2[i] - g2[i + s2];
+      } else if (terms == 1) {
+        T = g1[i + s1] - g1[i];
+      } else {  // g1 == NULL: swap and flip the sign (src/step_generic.cpp:76-80)
+        T = g2[i + s2] - g2[i];
+        dtdx = -C;
+      }
     }
     if (!SHELL) {
       const double *Fo = FT == T_B ? f.B[d] : f.D[d];
@@ -201,7 +237,8 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
       F[i] = Fo[i] - dtdx * T;
       continue;
     }
-    curl_apply<FT>(f, g, p, d, i, T, dtdx);
+    const double nv = curl_apply<FT>(f, g, p, d, i, T, dtdx);
+    if (FUSEUP) fused_point_update<FT>(f, g, p, d, i, nv);
   }
 }
 
@@ -595,22 +632,31 @@ static dim3 lin_grid(const BoxList &bl) {
 }
 
 int k_curl(int ft, const Box &in, const BoxList *sh, const DevGrid &g, const DevFields &f,
-           const CurlPlan &p, double courant, void *stream) {
+           const CurlPlan &p, double courant, void *stream, bool fuseup) {
   hipStream_t s = (hipStream_t)stream;
   BoxList none{};
   if (!sh) {
     if (empty(in)) return 0;
     dim3 blk(MNL_BX, MNL_BY), grd = grid_for(in);
     if (ft == T_B)
-      curl_kernel<T_B, false><<<grd, blk, 0, s>>>(in, none, g, f, p, courant);
+      curl_kernel<T_B, false, false><<<grd, blk, 0, s>>>(in, none, g, f, p, courant);
     else
-      curl_kernel<T_D, false><<<grd, blk, 0, s>>>(in, none, g, f, p, courant);
+      curl_kernel<T_D, false, false><<<grd, blk, 0, s>>>(in, none, g, f, p, courant);
   } else {
     if (sh->n == 0 || sh->start[sh->n] == 0) return 0;
-    if (ft == T_B)
-      curl_kernel<T_B, true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f, p, courant);
-    else
-      curl_kernel<T_D, true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f, p, courant);
+    dim3 grd = lin_grid(*sh);
+    grd.y = 3;
+    if (ft == T_B) {
+      if (fuseup)
+        curl_kernel<T_B, true, true><<<grd, 256, 0, s>>>(in, *sh, g, f, p, courant);
+      else
+        curl_kernel<T_B, true, false><<<grd, 256, 0, s>>>(in, *sh, g, f, p, courant);
+    } else {
+      if (fuseup)
+        curl_kernel<T_D, true, true><<<grd, 256, 0, s>>>(in, *sh, g, f, p, courant);
+      else
+        curl_kernel<T_D, true, false><<<grd, 256, 0, s>>>(in, *sh, g, f, p, courant);
+    }
   }
   return rc();
 }
@@ -836,11 +882,30 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   }
   auto pu = [&](unsigned ui, int c) -> double { return sU[UMODE == 2 ? c : 0][(ui >> (8 * c)) & 255]; };
 
+  // per-XCD work queues (speed only: any block may take any item): queue q
+  // holds the tiles [q*ntile/8, (q+1)*ntile/8) of every chunk, chunk-major, so
+  // the blocks of one XCD sweep neighbouring tiles together and the halo lines
+  // they share hit that XCD's L2.  An empty queue sends the block to the others.
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  const int NQ = a.nqueues == 1 ? 1 : 8;  // 1: one global chunk-major queue
+  xcc = NQ == 1 ? 0 : (xcc & 7);
   for (;;) {
-    if (threadIdx.x == 0) s_item = (long long)(atomicAdd(a.ctr, 1ULL) - a.ctr_base);
+    if (threadIdx.x == 0) {
+      long long it = -1;
+      for (int r = 0; r < NQ && it < 0; r++) {
+        const int qq = (int)((xcc + r) % NQ);
+        const long long lo = ntile * qq / NQ, nq = ntile * (qq + 1) / NQ - lo;
+        if (nq <= 0) continue;
+        const unsigned long long v = atomicAdd(a.ctr + 16 * qq, 1ULL);
+        if ((long long)v < nq * G.nch)
+          it = ((long long)(v / nq) * ntile) + lo + (long long)(v % nq);  // chunk*ntile + tile
+      }
+      s_item = it;
+    }
     __syncthreads();  // also separates LDS use of consecutive items
     const long long item = s_item;
-    if (item >= G.total) break;
+    if (item < 0) break;
     const int ch = (int)(item / ntile);
     const int tile = (int)(item % ntile);
     const int zs = flo2 + ch * G.zc, ze = min(zs + G.zc, fhi2 + 1);  // planes [zs, ze)
@@ -1046,12 +1111,15 @@ static int fused_grid_blocks(int bpc) {
   return cus[dev] * bpc;
 }
 
-int k_fused(const FusedArgs &a, void *stream, unsigned long long *consumed) {
-  *consumed = 0;
+int k_fused(const FusedArgs &a, void *stream) {
   for (int d = 0; d < 3; d++)
     if (a.F.hi[d] < a.F.lo[d]) return 0;
   if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr) return 1;  // host guarantees < 4 GiB arrays
   const FusedGeom G = fused_geom(a.F, a.zchunk);
+  // 8 queue counters, one per 128-byte line
+  if (hipMemsetAsync(a.ctr, 0, 8 * 16 * sizeof(unsigned long long), (hipStream_t)stream) !=
+      hipSuccess)
+    return 1;
   long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
   if (nb > G.total) nb = G.total;
   dim3 grd((unsigned)nb), blk(1024);
@@ -1072,7 +1140,6 @@ int k_fused(const FusedArgs &a, void *stream, unsigned long long *consumed) {
   else
     MNL_LAUNCH_FUSED(0);
 #undef MNL_LAUNCH_FUSED
-  *consumed = (unsigned long long)(G.total + nb);  // every workgroup takes one failing item
   return rc();
 }
 
