@@ -785,6 +785,25 @@ __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned off, doub
 }
 constexpr unsigned MNL_OOB = 0xFFFFFFF0u;  // > any valid byte offset (arrays < 4 GiB)
 
+// Kernel-argument pointers copied into SGPRs.  Without this hipcc turns a
+// per-lane choice between two argument pointers into a per-lane load of the
+// pointer from the kernarg segment, which puts a dependent memory round trip
+// in front of every field load.
+typedef const double __attribute__((address_space(1))) *gdp;  // global (not flat) pointer
+typedef const unsigned __attribute__((address_space(1))) *gup;
+__device__ __forceinline__ gdp sgpr_ptr(const void *p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (gdp)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double ldg(gdp p, unsigned off) {
+  return *(gdp)((const char __attribute__((address_space(1))) *)p + off);
+}
+__device__ __forceinline__ unsigned ldu(gup p, unsigned off) {
+  return *(gup)((const char __attribute__((address_space(1))) *)p + off);
+}
+
 struct FBatch {  // what B(k) needs besides E(k): own raw at k+1, B_old(k), halo raw at k
   double d0, d1, d2, u0, u1, u2, b0, b1, b2, h0, h1, hu0, hu1;
   unsigned ui, hui;  // UMODE 2: chi1inv palette indices (byte per component)
@@ -820,6 +839,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   __shared__ double sB[3][FR][FX + 1];
   __shared__ long long s_item;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool hwave = __builtin_amdgcn_readfirstlane(w) >= FR - 1;  // wave-uniform
   const int flo0 = a.F.lo[0], flo1 = a.F.lo[1], flo2 = a.F.lo[2];
   const int fhi0 = a.F.hi[0], fhi1 = a.F.hi[1], fhi2 = a.F.hi[2];
   const FusedGeom G = fused_geom(a.F, a.zchunk);
@@ -872,8 +892,17 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   }
   const int ox = (w < FR) ? lane : -1;  // own-like column offset from x0
   const int oy = row;                    // own-like row offset from y0
-  const double *hE0 = a.E[hc0], *hE1 = a.E[2], *hD0 = a.Do[hc0], *hD1 = a.Do[2];
-  const double *hU0 = a.u[HAS_U ? hc0 : 0], *hU1 = a.u[HAS_U ? 2 : 0];
+  gdp Dv[3], Ev[3], Uv[3], Bv[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    Dv[c] = sgpr_ptr(a.Do[c]);
+    Ev[c] = sgpr_ptr(a.E[c]);
+    Uv[c] = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[c]) : nullptr;
+    Bv[c] = sgpr_ptr(a.Bo[c]);
+  }
+  const gup uix = (gup)sgpr_ptr(a.uidx);
+  const gdp hE0 = hc0 ? Ev[1] : Ev[0], hE1 = Ev[2], hD0 = hc0 ? Dv[1] : Dv[0], hD1 = Dv[2];
+  const gdp hU0 = hc0 ? Uv[1] : Uv[0], hU1 = Uv[2];
   const unsigned safe = (unsigned)((flo0 + (long long)flo1 * a.st1) * 8);
   auto zin = [&](int z) { return z >= flo2 && z <= fhi2; };
   auto e_of = [](double d, double u, bool fz) { return (HAS_U && fz) ? d * u : d; };
@@ -923,39 +952,47 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
                         hy <= fhi1 + 1;
     const bool hF = hvalid && hx >= flo0 && hx <= fhi0 && hy >= flo1 && hy <= fhi1;
     const unsigned hbl = hvalid ? (unsigned)((hx + (long long)hy * a.st1) * 8) : cbl;
+    // per-lane source of E inside F's z range: D (then E = D*u) or stored E
+    const gdp pO0 = colF ? Dv[0] : Ev[0], pO1 = colF ? Dv[1] : Ev[1], pO2 = colF ? Dv[2] : Ev[2];
+    const gdp pH0 = hF ? hD0 : hE0, pH1 = hF ? hD1 : hE1;
 
     auto load = [&](int k) -> FBatch {
       FBatch q;
       const int z1 = k + 1;
       q.f = colF && zin(z1);
       const unsigned o = cbl + (unsigned)z1 * s2;
-      q.d0 = ldg(q.f ? a.Do[0] : a.E[0], o);
-      q.d1 = ldg(q.f ? a.Do[1] : a.E[1], o);
-      q.d2 = ldg(q.f ? a.Do[2] : a.E[2], o);
+      const bool zf = zin(z1);  // uniform
+      q.d0 = ldg(zf ? pO0 : Ev[0], o);
+      q.d1 = ldg(zf ? pO1 : Ev[1], o);
+      q.d2 = ldg(zf ? pO2 : Ev[2], o);
       if (UMODE == 2) {
-        q.ui = *(const unsigned *)((const char *)a.uidx + (o >> 1));
+        q.ui = ldu(uix, o >> 1);
       } else if (HAS_U) {
-        q.u0 = ldg(a.u[0], o);
-        q.u1 = ldg(a.u[1], o);
-        q.u2 = ldg(a.u[2], o);
+        q.u0 = ldg(Uv[0], o);
+        q.u1 = ldg(Uv[1], o);
+        q.u2 = ldg(Uv[2], o);
       } else {
         q.u0 = q.u1 = q.u2 = 1.0;
       }
       const unsigned ob = cbl + (unsigned)k * s2;
-      q.b0 = ldg(a.Bo[0], ob);
-      q.b1 = ldg(a.Bo[1], ob);
-      q.b2 = ldg(a.Bo[2], ob);
+      q.b0 = ldg(Bv[0], ob);
+      q.b1 = ldg(Bv[1], ob);
+      q.b2 = ldg(Bv[2], ob);
       q.hf = hF && zin(k);
-      const unsigned oh = hbl + (unsigned)k * s2;
-      q.h0 = ldg(q.hf ? hD0 : hE0, oh);
-      q.h1 = ldg(q.hf ? hD1 : hE1, oh);
-      if (UMODE == 2) {
-        q.hui = *(const unsigned *)((const char *)a.uidx + (oh >> 1));
-      } else if (HAS_U) {
-        q.hu0 = ldg(hU0, oh);
-        q.hu1 = ldg(hU1, oh);
-      } else {
-        q.hu0 = q.hu1 = 1.0;
+      q.h0 = q.h1 = 0.0;
+      q.hu0 = q.hu1 = 1.0;
+      q.hui = 0;
+      if (hwave) {  // only waves FR-1 and FR carry halo slots
+        const unsigned oh = hbl + (unsigned)k * s2;
+        const bool zk = zin(k);  // uniform
+        q.h0 = ldg(zk ? pH0 : hE0, oh);
+        q.h1 = ldg(zk ? pH1 : hE1, oh);
+        if (UMODE == 2) {
+          q.hui = ldu(uix, oh >> 1);
+        } else if (HAS_U) {
+          q.hu0 = ldg(hU0, oh);
+          q.hu1 = ldg(hU1, oh);
+        }
       }
       return q;
     };
@@ -966,20 +1003,20 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
       const int z = zs - 1;
       const bool f0 = colF && zin(z);
       const unsigned o = cbl + (unsigned)z * s2;
-      ex = ldg(f0 ? a.Do[0] : a.E[0], o);
-      ey = ldg(f0 ? a.Do[1] : a.E[1], o);
-      ez = ldg(f0 ? a.Do[2] : a.E[2], o);
+      ex = ldg(f0 ? Dv[0] : Ev[0], o);
+      ey = ldg(f0 ? Dv[1] : Ev[1], o);
+      ez = ldg(f0 ? Dv[2] : Ev[2], o);
       if (UMODE == 2) {
-        const unsigned ui = *(const unsigned *)((const char *)a.uidx + (o >> 1));
+        const unsigned ui = ldu(uix, o >> 1);
         if (f0) {  // palette visible: stored before the item loop's barrier
           ex *= pu(ui, 0);
           ey *= pu(ui, 1);
           ez *= pu(ui, 2);
         }
       } else if (HAS_U && f0) {
-        ex *= ldg(a.u[0], o);
-        ey *= ldg(a.u[1], o);
-        ez *= ldg(a.u[2], o);
+        ex *= ldg(Uv[0], o);
+        ey *= ldg(Uv[1], o);
+        ez *= ldg(Uv[2], o);
       }
     }
     FBatch q[DIST + 1];
