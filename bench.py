@@ -130,15 +130,19 @@ def main():
         return
     avg_ms = k_ms / max(n_launch, 1)
     achieved = k_bytes / (avg_ms * 1e-3) / 1e9 if n_launch else 0.0
-    traffic = None
+    traffic = None  # HBM bytes per launch from the committed PMC profile of THIS kernel source
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
+            import hashlib
             with open(tpath) as fh:
                 tj = json.load(fh)
-            if tj.get("size") == args.size and tj.get("vacuum", False) == args.vacuum:
-                traffic = tj.get("curl_b_interior_bytes_per_launch")
-        except (OSError, ValueError):
+            with open(os.path.join(ROOT, "meep_nl_amd", "csrc", "mnl_kernels.hip"), "rb") as fh:
+                khash = hashlib.sha256(fh.read()).hexdigest()[:16]
+            if (tj.get("size") == args.size and tj.get("vacuum", False) == args.vacuum
+                    and tj.get("kernels_hash") == khash):
+                traffic = round(tj["hbm_bytes_per_launch"])
+        except (OSError, ValueError, KeyError):
             traffic = None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

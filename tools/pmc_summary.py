@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_pmc.sh run (gpurun_out/prof_<tag>/) into profiles/.
+
+Per kernel: calls, average duration (kernel-trace stats pass), HBM bytes per
+launch from the PMC passes, corrected as MI355X_MICROARCH.md prescribes and
+as calibrated on this pool with tools/micro/fetch_calib.hip (profiles/
+r01_fetch_calibration.json): FETCH_SIZE (KiB) reports exactly half of the
+bytes read for 4-, 8- and 16-byte-per-lane loads -> bytes = 2 * 1024 * FETCH_SIZE;
+WRITE_SIZE (KiB) is exact -> bytes = 1024 * WRITE_SIZE.
+
+  python tools/pmc_summary.py gpurun_out/prof_r01 profiles/r01_pmc_512wg.json \
+      [--traffic profiles/pmc_traffic.json --size 512 --kernel fused_kernel]
+
+--traffic also writes the file bench.py reads for roofline.traffic, keyed by the
+hash of meep_nl_amd/csrc/mnl_kernels.hip so a stale profile is never reported
+for a changed kernel.
+"""
+import argparse
+import collections
+import csv
+import glob
+import hashlib
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernels_hash():
+    with open(os.path.join(ROOT, "meep_nl_amd", "csrc", "mnl_kernels.hip"), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("mnl::", "")
+
+
+def counters(d):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            out[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--traffic")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--vacuum", action="store_true")
+    ap.add_argument("--kernel", default="fused_kernel")
+    a = ap.parse_args()
+    res = {}
+    for f in glob.glob(os.path.join(a.src, "stats", "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Name"])
+            res.setdefault(k, {})
+            res[k]["calls"] = int(r["Calls"])
+            res[k]["avg_ms"] = float(r["AverageNs"]) / 1e6
+    fe, wr = counters(os.path.join(a.src, "fetch")), counters(os.path.join(a.src, "write"))
+    sq, tcc = counters(os.path.join(a.src, "sq")), counters(os.path.join(a.src, "tcc"))
+    for k in set(fe) | set(wr):
+        e = res.setdefault(k, {})
+        if fe[k]["FETCH_SIZE"]:
+            e["read_bytes"] = 2 * 1024 * sum(fe[k]["FETCH_SIZE"]) / len(fe[k]["FETCH_SIZE"])
+        if wr[k]["WRITE_SIZE"]:
+            e["write_bytes"] = 1024 * sum(wr[k]["WRITE_SIZE"]) / len(wr[k]["WRITE_SIZE"])
+        if "read_bytes" in e and "write_bytes" in e:
+            e["hbm_bytes"] = e["read_bytes"] + e["write_bytes"]
+            if e.get("avg_ms"):
+                e["hbm_GBps"] = e["hbm_bytes"] / (e["avg_ms"] * 1e-3) / 1e9
+        for src in (sq, tcc):
+            for c, v in src.get(k, {}).items():
+                e[c] = sum(v) / len(v)
+    doc = {"source": a.src, "kernels_hash": kernels_hash(),
+           "corrections": "read = 2*1024*FETCH_SIZE, write = 1024*WRITE_SIZE (calibrated)",
+           "kernels": res}
+    with open(a.dst, "w") as fh:
+        json.dump(doc, fh, indent=1, sort_keys=True)
+    print(json.dumps({k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
+                          for kk, vv in v.items() if kk in ("avg_ms", "hbm_bytes", "hbm_GBps")}
+                      for k, v in res.items()}, indent=1))
+    if a.traffic:
+        ks = [k for k in res if k.startswith(a.kernel) and "hbm_bytes" in res[k]]
+        if ks:
+            k = ks[0]
+            with open(a.traffic, "w") as fh:
+                json.dump({"kernels_hash": kernels_hash(), "size": a.size, "vacuum": a.vacuum,
+                           "kernel": k, "hbm_bytes_per_launch": res[k]["hbm_bytes"],
+                           "profile": os.path.basename(a.dst)}, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
