@@ -31,6 +31,7 @@ using namespace mnl;
 typedef std::complex<double> cplx;
 
 namespace {
+constexpr int FX_HOST = 64;  // fused tile width (FX in mnl_kernels.hip)
 
 const double pi = 3.141592653589793238462643383276;  // meep::pi
 thread_local std::string g_err;
@@ -161,11 +162,20 @@ struct mnl_fields {
   Box interior;
   std::vector<Box> shell;
   BoxList shell_list;
-  // fused interior mode (DESIGN.md "Fused interior")
+  // fused mode (DESIGN.md "Fused step")
   bool fused = false;        // currently stepping in fused mode
-  Box fusedF;                // fused region (local indices)
-  BoxList fused_shell;       // everything else
+  Box fusedG;                // fused domain (local indices)
+  Box fusedL;                // lean box (no PML, every component owned)
+  BoxList fused_shell;       // everything else (multi-rank: the top plane)
+  FusedArgs fgeo;            // tile / chunk bounds (filled by make_fused_boxes)
+  std::vector<int> gitems;   // general-kernel items
+  int *d_gitems = nullptr;
+  size_t d_gitems_cap = 0;
+  long long lean_cells = 0, gen_cells = 0;
+  FusedTab d_tab{};          // per-direction PML coefficient tables for the fused kernels
   double *pp_B[3] = {nullptr, nullptr, nullptr}, *pp_D[3] = {nullptr, nullptr, nullptr};
+  double *pp_E[3] = {nullptr, nullptr, nullptr}, *pp_H[3] = {nullptr, nullptr, nullptr};
+  double *pp_UB[3] = {nullptr, nullptr, nullptr};
   int fused_zchunk = 0;
   int fused_bpc = 1;
   int fused_dist = 1;
@@ -173,7 +183,7 @@ struct mnl_fields {
   unsigned long long *d_fused_ctr = nullptr;  // work-item counter of the fused kernel
   bool palette_tried = false;
   bool dsrc_in_shell = false;  // a D source point lies outside the interior box
-  unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedF (null: f64 chi1inv)
+  unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedG (null: f64 chi1inv)
   double *d_utab = nullptr;    // 3 x 256 palette values
   bool allow_fused = true;
   CurlPlan planB, planD;
@@ -193,8 +203,8 @@ struct mnl_fields {
   double dt;
   // timers / profiling
   bool profiling = false;
-  double timer_ms[8] = {0};
-  long long timer_count[8] = {0};
+  double timer_ms[16] = {0};
+  long long timer_count[16] = {0};
   std::vector<hipEvent_t> ev_pool;
   unsigned long long *d_nr_fallbacks = nullptr;
   double *d_scratch = nullptr;  // canonical-size staging buffer
@@ -206,6 +216,7 @@ struct mnl_fields {
     for (auto e : ev_pool) hipEventDestroy(e);
     if (d_scratch) hipFree(d_scratch);
     if (d_vals) hipFree(d_vals);
+    if (d_gitems) hipFree(d_gitems);
     comm.reset();
     if (stream) hipStreamDestroy(stream);
   }
@@ -511,6 +522,8 @@ int alloc_component(mnl_fields *F, int c) {
     }
   }
   if (t == T_B) F->f.Bn[d] = F->f.B[d];
+  if (t == T_E) F->f.En[d] = F->f.E[d];
+  if (t == T_H) F->f.Hn[d] = F->f.H[d];
   if (t == T_E && F->pml_any[d] && !F->f.WE[d])
     if (dev_alloc(F, &F->f.WE[d], F->nlocal)) return -1;
   if (t == T_B || t == T_D) {
@@ -518,6 +531,7 @@ int alloc_component(mnl_fields *F, int c) {
     double **u = t == T_B ? &F->f.UB[d] : &F->f.UD[d];
     if (F->S.has[du] && F->pml_any[du] && !*u)
       if (dev_alloc(F, u, F->nlocal)) return -1;
+    if (t == T_B) F->f.UBn[d] = F->f.UB[d];
   }
   F->allocated[c] = true;
   return 0;
@@ -1069,7 +1083,7 @@ int exchange(mnl_fields *F, int kind) {
     } else if (kind == 1) {
       if (c != sd && F->f.Bn[c] && F->allocated[3 * T_H + c]) {
         items.push_back({F->f.Bn[c], false});
-        if (F->f.H[c]) items.push_back({F->f.H[c], false});
+        if (F->f.H[c]) items.push_back({F->f.Hn[c], false});
       }
     } else {
       if (F->f.Dn[c] && F->allocated[3 * T_D + c]) items.push_back({F->f.Dn[c], c != sd});
@@ -1094,45 +1108,163 @@ int exchange(mnl_fields *F, int kind) {
 
 // ------------------------------------------------------------- stepping
 // ------------------------------------------------------------- fused mode
-// F = interior box without its low layer (whose B the fused kernel recomputes
-// as a halo) and restricted to planes where every component is owned and
-// updated (local [1, N-2] per axis).
-void make_fused_boxes(mnl_fields *F) {
+// G = [0, N-2] per axis: every owned point except the top plane of a rank
+// with an upper neighbour (its D needs the neighbour's new B first); that
+// plane is the shell, stepped by the shell kernels around the halo exchange.
+// L = interior box (no PML chunk along any direction) within [1, N-2]: tiles
+// whose whole footprint lies in L run the lean kernel.
+static void split_range(std::vector<int> &b, int lo, int hi_excl, int step, int align) {
+  // append starts covering [lo, hi_excl) in pieces of at most `step`, starts aligned
+  int x = lo;
+  while (x < hi_excl) {
+    b.push_back(x);
+    int nx = std::min(hi_excl, ((x + step) / align) * align);
+    if (nx <= x) nx = std::min(hi_excl, x + step);
+    x = nx;
+  }
+}
+
+bool make_fused_boxes(mnl_fields *F) {
   const DevGrid &g = F->g;
-  Box fb = F->interior;
+  Box G, L;
   for (int k = 0; k < 3; k++) {
-    fb.lo[k] = std::max(fb.lo[k] + 1, 1);
-    fb.hi[k] = std::min(fb.hi[k], g.N[k] - 2);
+    G.lo[k] = 0;
+    G.hi[k] = g.N[k] - 2;
+    if (G.hi[k] < G.lo[k]) return false;
+    L.lo[k] = std::max(F->interior.lo[k], 1);
+    L.hi[k] = std::min(F->interior.hi[k], g.N[k] - 2);
   }
-  F->fusedF = fb;
-  // onion shell around F, slowest axis first
-  std::vector<Box> sh;
-  Box cur;
-  for (int k = 0; k < 3; k++) cur.lo[k] = 0, cur.hi[k] = g.N[k] - 1;
-  for (int k = 2; k >= 0; k--) {
-    if (fb.lo[k] > cur.lo[k]) {
-      Box b = cur;
-      b.hi[k] = fb.lo[k] - 1;
-      sh.push_back(b);
-    }
-    if (fb.hi[k] < cur.hi[k]) {
-      Box b = cur;
-      b.lo[k] = fb.hi[k] + 1;
-      sh.push_back(b);
-    }
-    cur.lo[k] = fb.lo[k];
-    cur.hi[k] = fb.hi[k];
+  if (F->interior.hi[0] < F->interior.lo[0])
+    for (int k = 0; k < 3; k++) L.lo[k] = 1, L.hi[k] = 0;
+  F->fusedG = G;
+  F->fusedL = L;
+  FusedArgs &a = F->fgeo;
+  memset(&a, 0, sizeof(a));
+  a.G = G;
+  a.L = L;
+  const int zc = std::min(F->fused_zchunk > 0 ? F->fused_zchunk : 32, FUSED_MAXCH);
+  // ---- x tiles (64 columns, starts on 16-double = 128-byte boundaries)
+  std::vector<int> xb;
+  int lx_first = (L.lo[0] + 1 + 15) / 16 * 16, nlx = 0;
+  while (lx_first + nlx * FX_HOST + FX_HOST <= L.hi[0]) nlx++;
+  if (nlx == 0) {
+    split_range(xb, G.lo[0], G.hi[0] + 1, FX_HOST, 16);
+    a.lx0 = 0, a.lx1 = -1;
+  } else {
+    split_range(xb, G.lo[0], lx_first, FX_HOST, 16);
+    a.lx0 = (int)xb.size();
+    for (int t = 0; t < nlx; t++) xb.push_back(lx_first + FX_HOST * t);
+    a.lx1 = (int)xb.size() - 1;
+    split_range(xb, lx_first + FX_HOST * nlx, G.hi[0] + 1, FX_HOST, 16);
   }
+  // ---- lean row tiles (14 own rows; footprint y0-1 .. y0+14 inside L)
+  std::vector<int> yb;
+  int ly_first = L.lo[1] + 1, nly = 0;
+  while (ly_first + nly * 14 + 14 <= L.hi[1]) nly++;
+  for (int t = 0; t <= nly; t++) yb.push_back(ly_first + 14 * t);
+  a.ly0 = 0, a.ly1 = nly - 1;
+  // ---- general row tiles (<= GEN_ROWS-1 rows), aligned with the lean row range
+  std::vector<int> gyb;
+  const int gstep = 10;
+  int gly0 = -1, gly1 = -2;  // general row tiles inside the lean row range
+  if (nly == 0) {
+    split_range(gyb, G.lo[1], G.hi[1] + 1, gstep, 1);
+  } else {
+    split_range(gyb, G.lo[1], ly_first, gstep, 1);
+    gly0 = (int)gyb.size();
+    split_range(gyb, ly_first, ly_first + 14 * nly, gstep, 1);
+    gly1 = (int)gyb.size() - 1;
+    split_range(gyb, ly_first + 14 * nly, G.hi[1] + 1, gstep, 1);
+  }
+  // ---- z chunks: lean chunks have planes zs-1 .. ze inside L
+  std::vector<int> zb;
+  int lz_first = L.lo[2] + 1;
+  std::vector<int> lean_starts;
+  for (int z = lz_first; z < L.hi[2]; z += zc) lean_starts.push_back(z);
+  if (lean_starts.empty() || nlx == 0 || nly == 0) {
+    split_range(zb, G.lo[2], G.hi[2] + 1, std::min(zc, FUSED_MAXCH), 1);
+    a.lz0 = 0, a.lz1 = -1;
+    a.lx0 = 0, a.lx1 = -1;
+    a.ly0 = 0, a.ly1 = -1;
+    gly0 = -1, gly1 = -2;
+  } else {
+    split_range(zb, G.lo[2], lz_first, FUSED_MAXCH, 1);
+    a.lz0 = (int)zb.size();
+    for (int z : lean_starts) zb.push_back(z);
+    a.lz1 = (int)zb.size() - 1;
+    split_range(zb, L.hi[2], G.hi[2] + 1, FUSED_MAXCH, 1);  // last lean chunk ends at L.hi
+  }
+  if ((int)xb.size() > FUSED_MAXX || (int)yb.size() > FUSED_MAXY ||
+      (int)gyb.size() > FUSED_MAXGY || (int)zb.size() > FUSED_MAXZ)
+    return false;
+  a.nx = (int)xb.size();
+  a.ny = (int)yb.size() - 1;
+  a.ngy = (int)gyb.size();
+  a.nch = (int)zb.size();
+  for (size_t i = 0; i < xb.size(); i++) a.xb[i] = xb[i];
+  a.xb[xb.size()] = G.hi[0] + 1;
+  for (size_t i = 0; i < yb.size(); i++) a.yb[i] = yb[i];
+  for (size_t i = 0; i < gyb.size(); i++) a.gyb[i] = gyb[i];
+  a.gyb[gyb.size()] = G.hi[1] + 1;
+  for (size_t i = 0; i < zb.size(); i++) a.zb[i] = zb[i];
+  a.zb[zb.size()] = G.hi[2] + 1;
+  // ---- general items (chunk-major, then rows, then columns) and cell counts
+  F->gitems.clear();
+  F->lean_cells = F->gen_cells = 0;
+  for (int ch = 0; ch < a.nch; ch++)
+    for (int ty = 0; ty < a.ngy; ty++)
+      for (int tx = 0; tx < a.nx; tx++) {
+        const long long cells = (long long)(a.xb[tx + 1] - a.xb[tx]) *
+                                (a.gyb[ty + 1] - a.gyb[ty]) * (a.zb[ch + 1] - a.zb[ch]);
+        const bool lean = tx >= a.lx0 && tx <= a.lx1 && ch >= a.lz0 && ch <= a.lz1 &&
+                          ty >= gly0 && ty <= gly1;
+        if (lean) {
+          F->lean_cells += cells;
+          continue;
+        }
+        F->gen_cells += cells;
+        F->gitems.push_back(tx | (ty << 8) | (ch << 16));
+      }
+  a.ngen = (int)F->gitems.size();
+  for (int k = 0; k < 3; k++) {
+    a.N[k] = g.N[k];
+    a.off[k] = g.off[k];
+    a.osh_lo[k] = g.owned_lo_sh[k];
+    a.osh_hi[k] = std::min(g.owned_hi_sh[k], G.hi[k]);
+    a.oun_lo[k] = g.owned_lo_un[k];
+    a.oun_hi[k] = std::min(g.owned_hi_un[k], G.hi[k]);
+  }
+  // ---- shell: the top plane of a rank with an upper neighbour
   BoxList &bl = F->fused_shell;
   memset(&bl, 0, sizeof(bl));
-  long long acc = 0;
-  for (auto &b : sh) {
-    bl.b[bl.n] = b;
-    bl.start[bl.n] = acc;
-    acc += (long long)(b.hi[0] - b.lo[0] + 1) * (b.hi[1] - b.lo[1] + 1) * (b.hi[2] - b.lo[2] + 1);
-    bl.n++;
+  if (F->nranks > 1 && F->rank + 1 < F->nranks) {
+    Box b;
+    for (int k = 0; k < 3; k++) b.lo[k] = 0, b.hi[k] = g.N[k] - 1;
+    b.lo[2] = b.hi[2] = g.N[2] - 1;
+    bl.b[0] = b;
+    bl.start[0] = 0;
+    bl.start[1] = (long long)g.N[0] * g.N[1];
+    bl.n = 1;
   }
-  bl.start[bl.n] = acc;
+  return true;
+}
+
+// E of component c at global point jg is implicit (chi1inv * D) in fused mode
+bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
+  if (!F->fused || ctype(c) != T_E) return false;
+  const DevGrid &g = F->g;
+  const int d = cdir(c);
+  for (int e = 0; e < 3; e++) {
+    if (g.ax[e] < 0) continue;
+    const int j = jg[e] - g.off[e];
+    if (j < F->fusedG.lo[g.ax[e]] || j > F->fusedG.hi[g.ax[e]]) return false;
+    const bool sh = e == d;
+    if (sh ? (j < g.owned_lo_sh[e] || j > g.owned_hi_sh[e])
+           : (j < g.owned_lo_un[e] || j > g.owned_hi_un[e]))
+      return false;
+  }
+  const int q = 2 * jg[d] + 1;  // E_d is shifted along d
+  return !(F->S.has[d] && F->h_flag[d][q]);
 }
 
 bool fused_possible(mnl_fields *F) {
@@ -1140,13 +1272,59 @@ bool fused_possible(mnl_fields *F) {
   if (!F->srcB_idx.empty() || !F->isrc_idx.empty()) return false;
   for (int c = 0; c < MNL_NUM_COMPONENTS; c++)
     if (!F->allocated[c]) return false;
-  if (F->interior.hi[0] < F->interior.lo[0]) return false;
-  // the fused kernel addresses arrays with 32-bit byte offsets
+  for (int d = 0; d < 3; d++)  // separate H wherever PML lies along its direction
+    if (F->pml_any[d] && (!F->f.H[d] || !F->f.WH[d] || !F->f.WE[d])) return false;
+  const int nu = (F->f.inveps[0] ? 1 : 0) + (F->f.inveps[1] ? 1 : 0) + (F->f.inveps[2] ? 1 : 0);
+  if (nu != 0 && nu != 3) return false;
+  // the fused kernels address arrays with 32-bit byte offsets
   if (F->nlocal * 8 >= 0xFFFFFFF0ull) return false;
-  make_fused_boxes(F);
-  for (int k = 0; k < 3; k++)
-    if (F->fusedF.hi[k] < F->fusedF.lo[k]) return false;
+  if (!make_fused_boxes(F)) return false;
+  // a D source on a W-form E point would need E recomputed after the source
+  const DevGrid &g = F->g;
+  for (size_t k = 0; k < F->srcD_idx.size(); k++) {
+    const long long idx = F->srcD_idx[k];
+    const int d = F->srcD_comp[k];
+    const long long i2 = idx / g.st[2], r = idx % g.st[2];
+    const int jg[3] = {(int)(r % g.st[1]) + g.off[0], (int)(r / g.st[1]) + g.off[1],
+                       (int)i2 + g.off[2]};
+    bool inG = true;
+    for (int e = 0; e < 3; e++)
+      inG = inG && jg[e] - g.off[e] >= F->fusedG.lo[e] && jg[e] - g.off[e] <= F->fusedG.hi[e];
+    if (inG && F->pml_any[d] && F->h_flag[d][2 * jg[d] + 1]) return false;
+  }
   return true;
+}
+
+// per-direction PML tables of the fused kernels (identity where no PML)
+int upload_fused_tables(mnl_fields *F) {
+  if (F->d_tab.flag[0]) return 0;
+  for (int d = 0; d < 3; d++) {
+    const size_t nq = 2 * (size_t)std::max(F->S.n[d], 0) + 2;
+    std::vector<uint8_t> fl(nq, 0);
+    std::vector<double> kms(nq, 1.0), kps(nq, 1.0), si(nq, 1.0);
+    if (F->S.has[d] && !F->h_flag[d].empty())
+      for (size_t q = 0; q < nq; q++) {
+        fl[q] = F->h_flag[d][q];
+        kms[q] = F->h_kap[d][q] - F->h_sig[d][q];
+        kps[q] = F->h_kap[d][q] + F->h_sig[d][q];
+        si[q] = F->h_siginv[d][q];
+      }
+    uint8_t *dfl;
+    double *dkms, *dkps, *dsi;
+    if (dev_alloc(F, &dfl, nq) || dev_alloc(F, &dkms, nq) || dev_alloc(F, &dkps, nq) ||
+        dev_alloc(F, &dsi, nq))
+      return -1;
+    HIPCHK(hipMemcpyAsync(dfl, fl.data(), nq, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(dkms, kms.data(), nq * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(dkps, kps.data(), nq * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(dsi, si.data(), nq * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+    F->d_tab.flag[d] = dfl;
+    F->d_tab.kms[d] = dkms;
+    F->d_tab.kps[d] = dkps;
+    F->d_tab.siginv[d] = dsi;
+  }
+  return 0;
 }
 
 // chi1inv palette for the fused kernel (DESIGN.md "chi1inv palette"): at most
@@ -1194,7 +1372,7 @@ int build_palette(mnl_fields *F) {
     return -1;
   HIPCHK(hipMemcpyAsync(utab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, F->stream));
   const double *u[3] = {f.inveps[0], f.inveps[1], f.inveps[2]};
-  if (k_build_uidx(uidx, u, utab, n, F->fusedF, F->g.st[1], F->g.st[2], bad, F->stream))
+  if (k_build_uidx(uidx, u, utab, n, F->fusedG, F->g.st[1], F->g.st[2], bad, F->stream))
     return fail("palette index build failed");
   int hbad = 0;
   HIPCHK(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, F->stream));
@@ -1209,48 +1387,61 @@ int set_fused(mnl_fields *F, bool on) {
   DevFields &f = F->f;
   if (on == F->fused) return 0;
   if (on) {
-    if (!F->d_fused_ctr) {
-      if (dev_alloc(F, &F->d_fused_ctr, 8 * 16)) return -1;  // 8 queue counters, 128 B apart
+    if (!F->d_fused_ctr) {  // 8 lean queue counters + 1 general counter, 128 B apart
+      if (dev_alloc(F, &F->d_fused_ctr, 9 * 16)) return -1;
     }
+    if (upload_fused_tables(F)) return -1;
+    if (F->d_gitems_cap < F->gitems.size()) {
+      if (F->d_gitems) hipFree(F->d_gitems);
+      F->d_gitems = nullptr;
+      HIPCHK(hipMalloc(&F->d_gitems, F->gitems.size() * sizeof(int)));
+      F->d_gitems_cap = F->gitems.size();
+    }
+    if (!F->gitems.empty())
+      HIPCHK(hipMemcpyAsync(F->d_gitems, F->gitems.data(), F->gitems.size() * sizeof(int),
+                            hipMemcpyHostToDevice, F->stream));
     if (build_palette(F)) return -1;
+    // ping-pong partners; the second buffer starts as a copy (ghost / wall entries
+    // that no kernel writes)
+    auto pair = [&](double **pp, double *cur, double **next) -> int {
+      if (!cur) return 0;
+      if (!*pp && dev_alloc(F, pp, F->nlocal, false)) return -1;
+      HIPCHK(hipMemcpyAsync(*pp, cur, F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
+      *next = *pp;
+      return 0;
+    };
     for (int d = 0; d < 3; d++) {
-      if (!F->pp_B[d] && dev_alloc(F, &F->pp_B[d], F->nlocal)) return -1;
-      if (!F->pp_D[d] && dev_alloc(F, &F->pp_D[d], F->nlocal)) return -1;
-      // the second buffer starts as a copy (ghost/wall entries that no kernel writes)
-      HIPCHK(hipMemcpyAsync(F->pp_B[d], f.B[d], F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
-      HIPCHK(hipMemcpyAsync(F->pp_D[d], f.D[d], F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
-      f.Bn[d] = F->pp_B[d];
-      f.Dn[d] = F->pp_D[d];
+      if (pair(&F->pp_B[d], f.B[d], &f.Bn[d]) || pair(&F->pp_D[d], f.D[d], &f.Dn[d]) ||
+          pair(&F->pp_E[d], f.E[d], &f.En[d]) || pair(&F->pp_H[d], f.H[d], &f.Hn[d]) ||
+          pair(&F->pp_UB[d], f.UB[d], &f.UBn[d]))
+        return -1;
     }
+    f.fG = F->fusedG;
+    f.fused = 1;
   } else {
-    // materialise E inside F, then step in place again
-    if (k_materialize_e(F->fusedF, F->g, f, F->stream)) return fail("materialize E failed");
+    // materialise implicit E and the W aux fields over G (needs f.fused == 1),
+    // then step in place again
+    if (k_materialize_e(F->fusedG, F->g, f, F->stream)) return fail("materialize E failed");
     for (int d = 0; d < 3; d++) {
-      F->pp_B[d] = f.Bn[d];  // the non-current buffer
+      F->pp_B[d] = f.Bn[d];  // the non-current buffers
       F->pp_D[d] = f.Dn[d];
+      if (f.E[d]) F->pp_E[d] = f.En[d];
+      if (f.H[d]) F->pp_H[d] = f.Hn[d];
+      if (f.UB[d]) F->pp_UB[d] = f.UBn[d];
       f.Bn[d] = f.B[d];
       f.Dn[d] = f.D[d];
+      f.En[d] = f.E[d];
+      f.Hn[d] = f.H[d];
+      f.UBn[d] = f.UB[d];
     }
+    f.fused = 0;
   }
   F->fused = on;
-  f.fused = on ? 1 : 0;
-  f.fF = F->fusedF;
   HIPCHK(hipStreamSynchronize(F->stream));
   return 0;
 }
 
-bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
-  if (!F->fused || ctype(c) != T_E) return false;
-  const DevGrid &g = F->g;
-  for (int d = 0; d < 3; d++) {
-    if (g.ax[d] < 0) continue;
-    int j = jg[d] - g.off[d], a = g.ax[d];
-    if (j < F->fusedF.lo[a] || j > F->fusedF.hi[a]) return false;
-  }
-  return true;
-}
-
-enum { TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT };
+enum { TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT, TM_GEN, TM_N };
 
 struct EvPair {
   hipEvent_t a, b;
@@ -1261,7 +1452,7 @@ int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
   if (set_fused(F, fused_possible(F))) return -1;
   {  // does a D source point lie in the shell (outside the box the interior kernels own)?
-    const Box &ib = F->fused ? F->fusedF : F->interior;
+    const Box &ib = F->fused ? F->fusedG : F->interior;
     F->dsrc_in_shell = false;
     for (long long idx : F->srcD_idx) {
       const long long i2 = idx / F->g.st[2], r = idx % F->g.st[2];
@@ -1368,9 +1559,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       const BoxList *sl = F->fused ? &F->fused_shell : &F->shell_list;
       int k = ev_begin(TM_BINT);
       if (F->fused) {
-        FusedArgs fa;
-        fa.F = F->fusedF;
-        fa.zchunk = F->fused_zchunk;
+        FusedArgs &fa = F->fgeo;  // geometry from make_fused_boxes; pointers per step
         fa.blocks_per_cu = F->fused_bpc;
         fa.dist = F->fused_dist;
         fa.nqueues = F->fused_nq;
@@ -1384,14 +1573,29 @@ int step_batch(mnl_fields *F, int nsteps) {
           fa.Do[d] = f.D[d];
           fa.Dn[d] = f.Dn[d];
           fa.E[d] = f.E[d];
+          fa.En[d] = f.En[d];
+          fa.Ho[d] = f.H[d];
+          fa.Hn[d] = f.Hn[d];
+          fa.UBo[d] = f.UB[d];
+          fa.UBn[d] = f.UBn[d];
+          fa.UD[d] = f.UD[d];
           fa.u[d] = f.inveps[d];
         }
-        if ((fa.u[0] != nullptr) != (fa.u[1] != nullptr) || (fa.u[0] != nullptr) != (fa.u[2] != nullptr))
-          return fail("fused kernel needs all or no chi1inv arrays");
+        fa.tab = F->d_tab;
+        fa.gitems = F->d_gitems;
         fa.uidx = F->d_uidx;
         fa.utab = F->d_utab;
         fa.ctr = F->d_fused_ctr;
-        if (k_fused(fa, F->stream)) return fail("fused kernel launch failed");
+        int kr = k_fused(fa, 0, F->stream);
+        if (kr)
+          return fail("fused kernel launch failed (" + std::to_string(kr) + ", " +
+                      hipGetErrorString(hipGetLastError()) + ")");
+        ev_end(k);
+        k = ev_begin(TM_GEN);
+        kr = k_fused(fa, 1, F->stream);
+        if (kr)
+          return fail("fused general kernel launch failed (" + std::to_string(kr) + ", " +
+                      hipGetErrorString(hipGetLastError()) + ")");
       } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {
         return fail("curl B launch failed");
       }
@@ -1445,6 +1649,9 @@ int step_batch(mnl_fields *F, int nsteps) {
         for (int d = 0; d < 3; d++) {
           std::swap(f.B[d], f.Bn[d]);
           std::swap(f.D[d], f.Dn[d]);
+          std::swap(f.E[d], f.En[d]);
+          std::swap(f.H[d], f.Hn[d]);
+          std::swap(f.UB[d], f.UBn[d]);
         }
     }
     F->t += ns;
@@ -1794,7 +2001,7 @@ int mnl_fields_copy_component(mnl_fields *F, int comp, double *host, size_t n) {
   }
   HIPCHK(hipMemsetAsync(F->d_scratch, 0, nt * sizeof(double), F->stream));
   const bool fe = F->fused && t == T_E;
-  if (k_to_canonical(F->d_scratch, src, hsep, F->g, t, d, F->f, fe ? &F->fusedF : nullptr,
+  if (k_to_canonical(F->d_scratch, src, hsep, F->g, t, d, F->f, fe ? &F->fusedG : nullptr,
                      fe ? F->f.D[d] : nullptr, fe ? F->f.inveps[d] : nullptr, F->stream))
     return fail("to_canonical launch failed");
   HIPCHK(hipMemcpyAsync(host, F->d_scratch, nt * sizeof(double), hipMemcpyDeviceToHost, F->stream));
@@ -1833,28 +2040,77 @@ int mnl_fields_set_fused(mnl_fields *F, int allow) {
 int mnl_fields_set_profiling(mnl_fields *F, int on) {
   if (!F) return fail("null fields");
   F->profiling = on != 0;
-  for (int k = 0; k < 8; k++) F->timer_ms[k] = 0, F->timer_count[k] = 0;
+  for (int k = 0; k < 16; k++) F->timer_ms[k] = 0, F->timer_count[k] = 0;
   return 0;
+}
+
+// Algorithmic HBM bytes of one fused step over G (DESIGN.md "Fused step"):
+// every point reads B, D and writes B, D (96 B) + chi1inv (4 B palette word
+// or 3 doubles); PML state is counted per (point, component) where the
+// reference keeps it: f_u of B / D, separate H, W-form E (read + write 16 B).
+// lean: the same for the lean tiles only (no PML state there).
+void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
+  const DevGrid &g = F->g;
+  const FusedArgs &a = F->fgeo;
+  int nu = 0;
+  for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
+  const double ub = F->d_uidx ? 4.0 : 8.0 * nu;
+  *lean_bytes = double(F->lean_cells) * (96.0 + ub);
+  double extra = 0;
+  // count of local indices j in [lo, hi] of axis e with an optional flag condition
+  auto cnt = [&](int e, int lo, int hi, int qshift, bool need_flag) -> double {
+    double n = 0;
+    for (int j = lo; j <= hi; j++) {
+      if (need_flag) {
+        if (!F->S.has[e] || F->h_flag[e].empty()) continue;
+        if (!F->h_flag[e][2 * (j + g.off[e]) + qshift]) continue;
+      }
+      n += 1;
+    }
+    return n;
+  };
+  for (int c = 0; c < 3; c++)
+    for (int kind = 0; kind < 4; kind++) {
+      // kind 0: f_u of B_c (flag along c+2, shifted); 1: H_c (along c, unshifted);
+      // 2: f_u of D_c (along c+2, unshifted); 3: W-form E_c (along c, shifted)
+      const bool btype = kind < 2;
+      const int fe = (kind == 0 || kind == 2) ? (c + 2) % 3 : c;
+      const int qs = (kind == 0 || kind == 3) ? 1 : 0;
+      double n = 1;
+      for (int e = 0; e < 3; e++) {
+        const bool sh = btype ? (e != c) : (e == c);
+        const int lo = sh ? a.osh_lo[e] : a.oun_lo[e], hi = sh ? a.osh_hi[e] : a.oun_hi[e];
+        n *= cnt(e, lo, hi, qs, e == fe);
+      }
+      extra += 16.0 * n;
+    }
+  double gcells = 1;
+  for (int e = 0; e < 3; e++) gcells *= double(F->fusedG.hi[e] - F->fusedG.lo[e] + 1);
+  *gen_bytes = (gcells - double(F->lean_cells)) * (96.0 + ub) + extra;
 }
 
 int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch) {
-  if (!F || which < 0 || which > 1) return fail("bad kernel id");
-  int cat = which == 0 ? TM_BINT : TM_DINT;
+  if (!F || which < 0 || which > 2) return fail("bad kernel id");
+  // 0: lean fused kernel (or interior curl B when unfused), 1: interior curl D
+  // (unfused), 2: general fused kernel
+  int cat = which == 0 ? TM_BINT : (which == 1 ? TM_DINT : TM_GEN);
   *launches = F->timer_count[cat];
   *total_ms = F->timer_ms[cat];
-  const Box &b = (F->fused && which == 0) ? F->fusedF : F->interior;
+  if (F->fused && which != 1) {
+    double lb, gb;
+    fused_bytes(F, &lb, &gb);
+    *bytes_per_launch = which == 0 ? lb : gb;
+    return 0;
+  }
+  if (which == 2) {
+    *bytes_per_launch = 0;
+    return 0;
+  }
+  const Box &b = F->interior;
   double pts = 1;
   for (int k = 0; k < 3; k++) pts *= double(b.hi[k] - b.lo[k] + 1);
   if (b.hi[0] < b.lo[0]) pts = 0;
-  if (F->fused && which == 0) {
-    // fused step: read B(3), D(3), chi1inv(3 doubles, or one 4-byte palette
-    // index word); write B(3), D(3)
-    int nu = 0;
-    for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
-    *bytes_per_launch = pts * (8.0 * 12 + (F->d_uidx ? 4.0 : 8.0 * nu));
-    return 0;
-  }
   // interior curl: read 3 source comps + read/write the updated comps
   int ncomp = 0;
   const CurlPlan &p = which == 0 ? F->planB : F->planD;
@@ -1882,8 +2138,11 @@ int mnl_fields_traffic_model(mnl_fields *F, double *bpc, double *cells) {
   int nu = 0;
   for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
   double b;
-  if (F->fused) {
-    b = 8.0 * (4 * n) + (F->d_uidx ? 4.0 : 8.0 * nu);  // palette: one 4-byte index word
+  if (F->fused) {  // whole fused step over G per G point (PML state included)
+    double lb, gb, gc = 1;
+    fused_bytes(F, &lb, &gb);
+    for (int e = 0; e < 3; e++) gc *= double(F->fusedG.hi[e] - F->fusedG.lo[e] + 1);
+    b = (lb + gb) / gc;
   } else {
     b = 8.0 * (3 * n) * 2 + 8.0 * (2 * n) + 8.0 * nu;
     for (int k = 0; k < F->f.npol; k++)

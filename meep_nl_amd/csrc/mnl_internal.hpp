@@ -78,6 +78,9 @@ struct DevFields {
   // interior kernel ping-pongs them and the host swaps after each step.
   double *E[3], *D[3], *B[3], *H[3];
   double *Bn[3], *Dn[3];
+  // fused mode also ping-pongs stored E, separate H and the f_u of B (the
+  // fused kernel recomputes halo points from their old values); unfused: == E, H, UB
+  double *En[3], *Hn[3], *UBn[3];
   double *UB[3], *UD[3], *WE[3], *WH[3];
   const double *inveps[3];   // diagonal chi1inv of E comps (null = trivial)
   const double *offd[3][2];  // chi1inv[ec][cycle(d,1)], [cycle(d,2)] (null = absent)
@@ -93,9 +96,10 @@ struct DevFields {
   const uint8_t *offd_zone;
   const uint8_t *zone[3];    // per direction, global half-coordinate q -> zone 0/1/2
   unsigned long long *nr_fallbacks;
-  // fused interior active: E inside box fF is not stored and reads as D*chi1inv
+  // fused mode active: inside box fG, E is implicit (chi1inv * D, not stored)
+  // wherever it is owned and not in a PML chunk along its own direction
   int fused;
-  Box fF;
+  Box fG;
 };
 
 // Point sources in rank-local linear indices.
@@ -131,13 +135,37 @@ int k_update_pols(const Box &in, const BoxList *shell, const DevGrid &g, const D
                   void *stream);
 int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int step,
              void *stream);
-// Fused interior step (curl B -> H=B -> curl D -> E=chi1inv*D never stored)
-// over box F, 3-D, no PML/dispersion/NR inside F (DESIGN.md "Fused interior").
+// Fused step (DESIGN.md "Fused step"): one pass per fields::step() over box G
+// (curl B -> H -> curl D -> E, 3-D, no dispersion/NR/B sources).  G is tiled
+// into 64 x 14 column tiles and z chunks whose bounds come from the host
+// (xb/yb/zb, inclusive starts, last entry = end + 1).  Tiles whose whole
+// footprint lies in the lean box L (no PML, every component owned) run the
+// lean body; every other tile runs the general body (per-point PML branch
+// selection, H/E W updates, per-component ownership).  Inside G, E of a point
+// is implicit (= chi1inv * D, never stored) unless the point is owned and in
+// a PML chunk along the E direction (then it is stored, ping-pong).
+constexpr int FUSED_MAXX = 64, FUSED_MAXY = 192, FUSED_MAXZ = 192;
+constexpr int FUSED_MAXCH = 64;  // longest general chunk (planes)
+constexpr int FUSED_MAXGY = 256;
+struct FusedTab {                // per direction, indexed by global half-coordinate q
+  const uint8_t *flag[3];        // PML chunk along the direction (f_u / W branches)
+  const double *kms[3];          // kap - sig
+  const double *kps[3];          // kap + sig
+  const double *siginv[3];       // 1 / (kap + sig)
+};
 struct FusedArgs {
-  Box F;
-  int zchunk;         // > 0: force a segment seam every zchunk planes (tests)
+  Box L;              // lean box
+  Box G;              // fused domain (stores only inside G)
+  int nx, ny, nch;    // tiles along x, y; chunks along z
+  int xb[FUSED_MAXX + 1], yb[FUSED_MAXY + 1], zb[FUSED_MAXZ + 1];
+  int ngy;            // general-kernel row tiles (at most 10 rows each)
+  int gyb[FUSED_MAXGY + 1];
+  int lx0, lx1, ly0, ly1, lz0, lz1;  // lean tile / chunk index ranges (inclusive)
+  int N[3];           // local points per axis (array extents)
+  int off[3];         // global index of local index 0 per axis
+  int osh_lo[3], osh_hi[3], oun_lo[3], oun_hi[3];  // owned ranges within G per axis
   int blocks_per_cu;  // persistent workgroups per CU (default 1)
-  int dist;           // prefetch distance in planes (1 or 2)
+  int dist;           // lean-body prefetch distance in planes (1 or 2)
   int nqueues;        // work queues: 1 (global, default) or 8 (one per XCD)
   long long nelem;    // elements per field array (selects 32-bit offsets)
   double C;
@@ -146,13 +174,24 @@ struct FusedArgs {
   double *Bn[3];
   const double *Do[3];
   double *Dn[3];
-  const double *E[3];
+  const double *E[3];   // stored E (old)
+  double *En[3];        // stored E (new)
+  const double *Ho[3];  // separate H (null: H == B along that component)
+  double *Hn[3];
+  const double *UBo[3];  // f_u of B (null: no PML along cycle(d,2))
+  double *UBn[3];
+  double *UD[3];         // f_u of D, updated in place (only the owner reads it)
   const double *u[3];
   const unsigned *uidx;         // chi1inv palette indices (nullptr: use u / none)
   const double *utab;           // palette, 3 x 256 doubles
-  unsigned long long *ctr;      // 8 work-queue counters (128 B apart), reset per launch
+  FusedTab tab;
+  const int *gitems;            // general items: tx | ty << 8 | ch << 16
+  int ngen;
+  unsigned long long *ctr;      // 9 work-queue counters (128 B apart), reset per launch
 };
-int k_fused(const FusedArgs &a, void *stream);
+// which: 0 = lean tiles, 1 = general tiles (both read old / write new buffers only,
+// so either order is valid)
+int k_fused(const FusedArgs &a, int which, void *stream);
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
                  const Box &F, long long st1, long long st2, int *bad, void *stream);
 // E = chi1inv * D over box F (leaving fused mode / readout)

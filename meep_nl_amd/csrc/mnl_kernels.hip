@@ -93,6 +93,18 @@ __device__ __forceinline__ bool pml_at(const DevFields &f, const DevGrid &g, int
   return g.ax[d] >= 0 && f.pml.flag[d] != nullptr && f.pml.flag[d][q] != 0;
 }
 
+// Fused mode: E of comp c at p is not stored but equals chi1inv * D (DESIGN.md
+// "Fused step"): p inside the fused domain G, E_c owned there and not in a
+// PML chunk along c (where E carries W-form history and is stored).
+__device__ __forceinline__ bool e_implicit(const DevFields &f, const DevGrid &g, int c,
+                                           const Pt &p) {
+  if (!f.fused) return false;
+#pragma unroll
+  for (int d = 0; d < 3; d++)
+    if (p.j[d] < f.fG.lo[d] || p.j[d] > f.fG.hi[d]) return false;
+  return owned(g, T_E, c, p) && !pml_at(f, g, c, qcoord(g, p, T_E, c, c));
+}
+
 // Apply one curl update with the per-point PML branch selection of step_curl
 // (src/step_generic.cpp:84-252, cnd == NULL).
 template <int FT>
@@ -107,22 +119,24 @@ __device__ __forceinline__ double curl_apply(const DevFields &f, const DevGrid &
   if (!ps && !pu) {
     nv = Fo[i] - dtdx * T;
   } else if (!ps) {
-    double *U = FT == T_B ? f.UB[d] : f.UD[d];
+    const double *U = FT == T_B ? f.UB[d] : f.UD[d];
+    double *Un = FT == T_B ? f.UBn[d] : f.UD[d];
     const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
     double fprev = U[i];
     double fu = fprev - dtdx * T;
-    U[i] = fu;
+    Un[i] = fu;
     nv = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
   } else if (!pu) {
     const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
     nv = ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
   } else {
-    double *U = FT == T_B ? f.UB[d] : f.UD[d];
+    const double *U = FT == T_B ? f.UB[d] : f.UD[d];
+    double *Un = FT == T_B ? f.UBn[d] : f.UD[d];
     const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
     const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
     double fprev = U[i];
     double fu = ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
-    U[i] = fu;
+    Un[i] = fu;
     nv = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
   }
   F[i] = nv;
@@ -144,21 +158,21 @@ __device__ __forceinline__ void fused_point_update(const DevFields &f, const Dev
     double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
     double fw = nv;
     f.WH[d][i] = fw;
-    f.H[d][i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+    f.Hn[d][i] = f.H[d][i] + ((kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev);
   } else {  // update_eh(E_stuff), diagonal chi1inv, no P (src/step_generic.cpp:576-906)
     if (!f.ecomp_present[d]) return;
     const double gs = nv;
     const double *u = f.inveps[d];
-    double *E = f.E[d];
+    double *En = f.En[d];
     const int kw = qcoord(g, p, T_E, d, d);
     if (pml_at(f, g, d, kw)) {
       double fwprev = f.WE[d][i];
       double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
       double fw = u ? (gs * u[i]) : gs;
       f.WE[d][i] = fw;
-      E[i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+      En[i] = f.E[d][i] + ((kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev);
     } else {
-      E[i] = u ? (gs * u[i]) : gs;
+      En[i] = u ? (gs * u[i]) : gs;
     }
   }
 }
@@ -186,14 +200,10 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
     const int terms = pl.terms[d];
     double T, dtdx = C;
     if (FT == T_B && SHELL && f.fused) {  // E is not stored inside the fused box: E = D*chi1inv
-      const int x = p.j[0], y = p.j[1], z = p.j[2];
-      auto inF = [&](int dd) {
-        const int xx = x + (dd == 0), yy = y + (dd == 1), zz = z + (dd == 2);
-        return xx >= f.fF.lo[0] && xx <= f.fF.hi[0] && yy >= f.fF.lo[1] && yy <= f.fF.hi[1] &&
-               zz >= f.fF.lo[2] && zz <= f.fF.hi[2];
-      };
       auto e_at = [&](int c, long long n, int dd) -> double {
-        if (inF(dd)) {
+        Pt q = p;
+        if (dd >= 0) q.j[dd] += 1;
+        if (e_implicit(f, g, c, q)) {
           const double dv = f.D[c][n];
           return f.inveps[c] ? (dv * f.inveps[c][n]) : dv;
         }
@@ -218,8 +228,8 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
         g1 = f.Bn[c1];  // H == B (new) outside PML chunks
         g2 = f.Bn[c2];
         if (SHELL) {  // H separate only in chunks with PML along the H direction
-          if (f.H[c1] && pml_at(f, g, c1, qcoord(g, p, T_H, c1, c1))) g1 = f.H[c1];
-          if (f.H[c2] && pml_at(f, g, c2, qcoord(g, p, T_H, c2, c2))) g2 = f.H[c2];
+          if (f.H[c1] && pml_at(f, g, c1, qcoord(g, p, T_H, c1, c1))) g1 = f.Hn[c1];
+          if (f.H[c2] && pml_at(f, g, c2, qcoord(g, p, T_H, c2, c2))) g2 = f.Hn[c2];
         }
       }
       if (terms == 3) {
@@ -259,7 +269,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_h_kernel(BoxList bl, De
     double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
     double fw = f.Bn[d][i];
     f.WH[d][i] = fw;
-    f.H[d][i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+    f.Hn[d][i] = f.H[d][i] + ((kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev);
   }
 }
 
@@ -413,7 +423,8 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
     if (!owned(g, T_E, d, p)) continue;
     const double gs = dmp_at<ISRC>(f, is, step, d, i);
     const double *u = f.inveps[d];
-    double *E = f.E[d];
+    const double *E = f.E[d];
+    double *En = f.En[d];
     bool pml = false;
     int kw = 0;
     if (SHELL) {
@@ -426,7 +437,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
       double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
       double fw = u ? (gs * u[i]) : gs;
       f.WE[d][i] = fw;
-      E[i] += (kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev;
+      En[i] = E[i] + ((kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev);
       wv = fw;
     } else {
       bool done = false;
@@ -482,13 +493,13 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
               run_nr(gs_2 * u[i], gs_3 * u[i], fv, &dummy1, &dummy1, &fv, p1, p2, p3, rng,
                      f.nr_fallbacks);
             }
-            E[i] = fv;
+            En[i] = fv;
             done = true;
           }
         }
       }
-      if (!done) E[i] = u ? (gs * u[i]) : gs;
-      wv = E[i];
+      if (!done) En[i] = u ? (gs * u[i]) : gs;
+      wv = En[i];
     }
     if (FUSEPOL) {
       for (int k = 0; k < f.npol; k++) {
@@ -517,7 +528,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, BoxL
     if (!owned(g, T_E, d, p)) continue;
     bool pml = false;
     if (SHELL) pml = pml_at(f, g, d, qcoord(g, p, T_E, d, d));
-    const double wv = pml ? f.WE[d][i] : f.E[d][i];
+    const double wv = pml ? f.WE[d][i] : f.En[d][i];
     for (int k = 0; k < f.npol; k++) {
       const PolDev &pd = f.pol[k];
       if (!pd.P[d]) continue;
@@ -589,8 +600,8 @@ __global__ void to_canonical_kernel(double *dst, const double *src, const double
   long long i = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
   double v = src[i];
   if (hsep && pml_at(f, g, c, qcoord(g, p, T_H, c, c))) v = hsep[i];
-  if (use_fb && i0 >= Fb.lo[0] && i0 <= Fb.hi[0] && i1 >= Fb.lo[1] && i1 <= Fb.hi[1] &&
-      i2 >= Fb.lo[2] && i2 <= Fb.hi[2])  // fused interior: E = chi1inv * D (never stored)
+  p.idx = i;
+  if (use_fb && type == T_E && e_implicit(f, g, c, p))  // fused: E = chi1inv * D (not stored)
     v = usrc ? (dsrc[i] * usrc[i]) : dsrc[i];
   dst[cidx] = v;
 }
@@ -815,20 +826,458 @@ struct FBatch {  // what B(k) needs besides E(k): own raw at k+1, B_old(k), halo
 // palette holds the very same doubles, so E = D * u is bit-identical, and the
 // kernel reads 4 B of chi1inv per cell instead of 24 (120 -> 100 B per cell).
 
-struct FusedGeom {
-  int xb, ntx, nty, nch, zc;
-  long long total;
+// Lean-body geometry of one work item (see FusedArgs: bounds come from the host).
+struct ItemGeo {
+  int x0, x1;  // tile columns [x0, x1] (x0 128-byte aligned)
+  int y0;      // halo row; own rows y0+1 .. y1
+  int y1;
+  int zs, ze;  // planes [zs, ze)
 };
-__host__ __device__ inline FusedGeom fused_geom(const Box &F, int zchunk) {
-  FusedGeom g;
-  g.xb = F.lo[0] & ~15;
-  g.ntx = (F.hi[0] - g.xb) / FX + 1;
-  g.nty = (F.hi[1] - F.lo[1] + FOWN) / FOWN;
-  const int nz = F.hi[2] - F.lo[2] + 1;
-  g.zc = zchunk > 0 ? zchunk : 32;
-  g.nch = (nz + g.zc - 1) / g.zc;
-  g.total = (long long)g.ntx * g.nty * g.nch;
-  return g;
+
+// PML coefficient table entry of one half-coordinate (FusedTab), staged in LDS
+struct TabE {
+  double kms, si, kps;
+};
+constexpr int TPX = FX + 2, TPZ = FUSED_MAXCH + 2;
+
+// curl update with the per-point branch selection of step_curl
+// (src/step_generic.cpp:84-252), written branch-free: outside a PML chunk
+// along dsig the tables hold kap = 1, sig = 0, siginv = 1, so
+// ((kap - sig) * X - dtdx * T) * siginv is bitwise X - dtdx * T; the f_u form
+// (chunk with PML along dsigu) is selected by its flag.  Returns the new field;
+// *un is the new f_u (valid when pu).
+__device__ __forceinline__ double pml_curl(double fo, double uo, double T, double C, bool pu,
+                                           double kms_a, double si_a, double kms_u,
+                                           double si_u, double *un) {
+  const double X = pu ? uo : fo;
+  const double t = (kms_a * X - C * T) * si_a;
+  *un = t;
+  return pu ? si_u * (kms_u * fo + t - uo) : t;
+}
+
+template <int UMODE>
+struct GBatch {  // general body: B(k) needs these besides E(k) (own: D(k+1), u(k+1), B_old(k))
+  double d0, d1, d2, u0, u1, u2, b0, b1, b2, h0, h1, hu0, hu1;
+  unsigned ui, hui;
+  bool hi0, hi2;  // halo E implicit (chi1inv * D) for comps hc0 / 2
+};
+struct GAux {  // general body, PML state of plane k (own lanes), loaded masked
+  double es0, es1, es2;  // stored E_old(k+1)
+  double ub0, ub1, ub2;  // f_u of B, old, plane k
+  double ho0, ho1, ho2;  // separate H, old, plane k
+  double ud0, ud1, ud2;  // f_u of D, plane k
+};
+
+// General body over one item: any mix of PML chunks, walls, ghosts and owned
+// ranges (src/step_generic.cpp:69-253 and 576-906 per point; H and E by
+// update_eh, src/update_eh.cpp:67-363, with the W aux of PML chunks
+// represented by its value: W_H == B_old, W_E == chi1inv * D_old, which the
+// reference stores one step earlier).
+template <int UMODE, int GR>
+__device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo &it,
+                                                        double (*sE)[GR + 1][FX + 2],
+                                                        double (*sB)[GR][FX + 1],
+                                                        const double (*sU)[256], TabE (*sTx)[2],
+                                                        TabE (*sTy)[2], TabE (*sTz)[2],
+                                                        unsigned char (*sFx)[2],
+                                                        unsigned char (*sFy)[2],
+                                                        unsigned char (*sFz)[2]) {
+  constexpr bool HAS_U = UMODE != 0;
+  constexpr int GOWN = GR - 1, TPY = GR + 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool hwave = __builtin_amdgcn_readfirstlane(w) >= GR - 1;
+  const double C = a.C;
+  const unsigned s2 = (unsigned)(a.st2 * 8);
+  const int x0 = it.x0, y0 = it.y0, zs = it.zs, ze = it.ze;
+  const int zlo = zs - 1;  // z table position 0
+  // ---- PML tables of this item's footprint -> LDS
+  for (int i = threadIdx.x; i < 2 * (TPX + TPY + TPZ); i += blockDim.x) {
+    int ax, pos, base;
+    if (i < 2 * TPX) {
+      ax = 0, pos = i >> 1, base = x0 - 1;
+    } else if (i < 2 * (TPX + TPY)) {
+      ax = 1, pos = (i - 2 * TPX) >> 1, base = y0;
+    } else {
+      ax = 2, pos = (i - 2 * (TPX + TPY)) >> 1, base = zlo;
+    }
+    const int s = i & 1;
+    const int jj = min(max(base + pos, 0), a.N[ax] - 1);
+    const int q = 2 * (jj + a.off[ax]) + s;
+    TabE e;
+    e.kms = a.tab.kms[ax][q];
+    e.si = a.tab.siginv[ax][q];
+    e.kps = a.tab.kps[ax][q];
+    const unsigned char fl = a.tab.flag[ax][q];
+    if (ax == 0) {
+      sTx[pos][s] = e;
+      sFx[pos][s] = fl;
+    } else if (ax == 1) {
+      sTy[pos][s] = e;
+      sFy[pos][s] = fl;
+    } else {
+      sTz[pos][s] = e;
+      sFz[pos][s] = fl;
+    }
+  }
+  __syncthreads();
+
+  // ---- lane roles (as the lean body)
+  int row, col;
+  bool ownlike;
+  int hrow = 0, hcol = 0, hc0 = 0, hdx = 0, hdy = 0;
+  bool hslot = false;
+  if (w < GR) {
+    row = w;
+    col = lane + 1;
+    ownlike = true;
+    if (w == GR - 1) {
+      hslot = true, hrow = GR, hcol = col, hc0 = 0, hdx = lane, hdy = GR;
+    }
+  } else {
+    row = lane + 1;
+    col = 0;
+    ownlike = lane < GOWN;
+    if (lane >= 16 && lane < 16 + GR) {
+      hslot = true, hrow = lane - 16, hcol = FX + 1, hc0 = 1, hdx = FX, hdy = lane - 16;
+    } else if (lane == 31) {
+      hslot = true, hrow = GR, hcol = 0, hc0 = 0, hdx = -1, hdy = GR;
+    }
+  }
+  const int ox = (w < GR) ? lane : -1, oy = row;
+  const int gx = x0 + ox, gy = y0 + oy;
+  const bool inA = ownlike && gx >= 0 && gx < a.N[0] && gy >= 0 && gy < a.N[1];
+  const unsigned cb = (unsigned)((gx + (long long)gy * a.st1) * 8);
+  const unsigned cbl = inA ? cb : 0u;
+  const int px = ox + 1, py = oy;  // table positions
+  auto rng = [](int v, int lo, int hi) { return v >= lo && v <= hi; };
+  // per-axis ownership (within G) of this lane's point: bit0 = shifted comps, bit1 = unshifted
+  const unsigned ownx = (rng(gx, a.osh_lo[0], a.osh_hi[0]) ? 1u : 0u) |
+                        (rng(gx, a.oun_lo[0], a.oun_hi[0]) ? 2u : 0u);
+  const unsigned owny = (rng(gy, a.osh_lo[1], a.osh_hi[1]) ? 1u : 0u) |
+                        (rng(gy, a.oun_lo[1], a.oun_hi[1]) ? 2u : 0u);
+  const bool stl = ownlike && w < GR && row >= 1 && gx >= x0 && gx <= it.x1 && gy <= it.y1;
+  // halo slot point (E of comps hc0 and 2 at (hx, hy, k))
+  const int hx = x0 + hdx, hy = y0 + hdy;
+  const bool hA = hslot && hx >= 0 && hx < a.N[0] && hy >= 0 && hy < a.N[1];
+  const unsigned hbl = hA ? (unsigned)((hx + (long long)hy * a.st1) * 8) : cbl;
+  const int hpx = hdx + 1, hpy = hdy;
+  const unsigned hownx = (rng(hx, a.osh_lo[0], a.osh_hi[0]) ? 1u : 0u) |
+                         (rng(hx, a.oun_lo[0], a.oun_hi[0]) ? 2u : 0u);
+  const unsigned howny = (rng(hy, a.osh_lo[1], a.osh_hi[1]) ? 1u : 0u) |
+                         (rng(hy, a.oun_lo[1], a.oun_hi[1]) ? 2u : 0u);
+  auto ownz_of = [&](int z) -> unsigned {
+    return (rng(z, a.osh_lo[2], a.osh_hi[2]) ? 1u : 0u) | (rng(z, a.oun_lo[2], a.oun_hi[2]) ? 2u : 0u);
+  };
+  // ownership of E/D comp c (shifted along c) and B/H comp c (shifted off c)
+  auto own_e = [](int c, unsigned ox_, unsigned oy_, unsigned oz_) {
+    return ((c == 0 ? ox_ : ox_ >> 1) & (c == 1 ? oy_ : oy_ >> 1) & (c == 2 ? oz_ : oz_ >> 1) & 1u) != 0;
+  };
+  auto own_b = [](int c, unsigned ox_, unsigned oy_, unsigned oz_) {
+    return ((c == 0 ? ox_ >> 1 : ox_) & (c == 1 ? oy_ >> 1 : oy_) & (c == 2 ? oz_ >> 1 : oz_) & 1u) != 0;
+  };
+  const int zmax = a.N[2] - 1;
+  auto zc = [&](int z) { return min(max(z, 0), zmax); };
+  auto tpz = [&](int z) { return min(max(z - zlo, 0), TPZ - 1); };
+  // E_old of comp c at a point is implicit (chi1inv * D) when owned in G and not W-PML
+  auto impl = [&](int c, unsigned ox_, unsigned oy_, unsigned oz_, bool wf) {
+    return own_e(c, ox_, oy_, oz_) && !wf;
+  };
+  gdp Dv[3], Ev[3], Uv[3], Bv[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    Dv[c] = sgpr_ptr(a.Do[c]);
+    Ev[c] = sgpr_ptr(a.E[c]);
+    Uv[c] = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[c]) : nullptr;
+    Bv[c] = sgpr_ptr(a.Bo[c]);
+  }
+  const gup uix = (gup)sgpr_ptr(a.uidx);
+  auto pu_ = [&](unsigned ui, int c) -> double { return sU[UMODE == 2 ? c : 0][(ui >> (8 * c)) & 255]; };
+  // W flags of E comps (PML chunk along own direction, shifted coordinate)
+  const bool wx = sFx[px][1] != 0, wy = sFy[py][1] != 0;
+  const bool hwx = sFx[hpx][1] != 0, hwy = sFy[hpy][1] != 0;
+
+  auto load = [&](int k) -> GBatch<UMODE> {
+    GBatch<UMODE> q;
+    const int z1 = zc(k + 1);
+    const unsigned o = cbl + (unsigned)z1 * s2;
+    q.d0 = ldg(Dv[0], o);
+    q.d1 = ldg(Dv[1], o);
+    q.d2 = ldg(Dv[2], o);
+    if (UMODE == 2) {
+      q.ui = ldu(uix, o >> 1);
+    } else if (HAS_U) {
+      q.u0 = ldg(Uv[0], o);
+      q.u1 = ldg(Uv[1], o);
+      q.u2 = ldg(Uv[2], o);
+    } else {
+      q.u0 = q.u1 = q.u2 = 1.0;
+    }
+    const unsigned ob = cbl + (unsigned)zc(k) * s2;
+    q.b0 = ldg(Bv[0], ob);
+    q.b1 = ldg(Bv[1], ob);
+    q.b2 = ldg(Bv[2], ob);
+    q.h0 = q.h1 = 0.0;
+    q.hu0 = q.hu1 = 1.0;
+    q.hui = 0;
+    q.hi0 = q.hi2 = false;
+    if (hwave) {
+      const int kk = zc(k);
+      const unsigned oh = hbl + (unsigned)kk * s2;
+      const unsigned oz = ownz_of(k);
+      const bool wz = sFz[tpz(k)][1] != 0;
+      const bool i0 = hA && impl(hc0, hownx, howny, oz, hc0 == 0 ? hwx : hwy);
+      const bool i2 = hA && impl(2, hownx, howny, oz, wz);
+      q.h0 = ldg(i0 ? (hc0 ? Dv[1] : Dv[0]) : (hc0 ? Ev[1] : Ev[0]), oh);
+      q.h1 = ldg(i2 ? Dv[2] : Ev[2], oh);
+      if (UMODE == 2) {
+        q.hui = ldu(uix, oh >> 1);
+      } else if (HAS_U) {
+        q.hu0 = ldg(hc0 ? Uv[1] : Uv[0], oh);
+        q.hu1 = ldg(Uv[2], oh);
+      }
+      q.hi0 = i0;
+      q.hi2 = i2;
+    }
+    return q;
+  };
+  // masked aux loads: a lane that needs no value reads its own B_old line (cache hit)
+  auto load_aux = [&](int k) -> GAux {
+    GAux x;
+    const unsigned ob = cbl + (unsigned)zc(k) * s2;
+    const unsigned o1 = cbl + (unsigned)zc(k + 1) * s2;
+    const int pz = tpz(k), pz1 = tpz(k + 1);
+    const unsigned oz1 = ownz_of(k + 1);
+    const bool wz1 = sFz[pz1][1] != 0;
+    const bool e0 = inA && !impl(0, ownx, owny, oz1, wx), e1 = inA && !impl(1, ownx, owny, oz1, wy),
+               e2 = inA && !impl(2, ownx, owny, oz1, wz1);
+    x.es0 = e0 ? ldg(Ev[0], o1) : 0.0;
+    x.es1 = e1 ? ldg(Ev[1], o1) : 0.0;
+    x.es2 = e2 ? ldg(Ev[2], o1) : 0.0;
+    // f_u of B comp c: PML chunk along cycle(c,2), shifted coordinate
+    const bool fxs = sFx[px][1] != 0, fys = sFy[py][1] != 0, fzs = sFz[pz][1] != 0;
+    const bool fxu = sFx[px][0] != 0, fyu = sFy[py][0] != 0, fzu = sFz[pz][0] != 0;
+    const bool u0 = inA && fzs, u1 = inA && fxs, u2 = inA && fys;
+    x.ub0 = u0 ? ldg(sgpr_ptr(a.UBo[0]), ob) : 0.0;
+    x.ub1 = u1 ? ldg(sgpr_ptr(a.UBo[1]), ob) : 0.0;
+    x.ub2 = u2 ? ldg(sgpr_ptr(a.UBo[2]), ob) : 0.0;
+    // separate H of comp c: PML chunk along c, unshifted coordinate
+    const bool h0 = inA && fxu, h1 = inA && fyu, h2 = inA && fzu;
+    x.ho0 = h0 ? ldg(sgpr_ptr(a.Ho[0]), ob) : 0.0;
+    x.ho1 = h1 ? ldg(sgpr_ptr(a.Ho[1]), ob) : 0.0;
+    x.ho2 = h2 ? ldg(sgpr_ptr(a.Ho[2]), ob) : 0.0;
+    // f_u of D comp c: PML chunk along cycle(c,2), unshifted coordinate (owner lanes only)
+    const bool d0 = stl && fzu, d1 = stl && fxu, d2 = stl && fyu;
+    x.ud0 = d0 ? ldg(sgpr_ptr(a.UD[0]), ob) : 0.0;
+    x.ud1 = d1 ? ldg(sgpr_ptr(a.UD[1]), ob) : 0.0;
+    x.ud2 = d2 ? ldg(sgpr_ptr(a.UD[2]), ob) : 0.0;
+    return x;
+  };
+  // conditional stores (no prefetch pipeline here, so exec-masked stores cost nothing extra)
+  auto stg = [](double *p, unsigned off, double v) {
+    *(double __attribute__((address_space(1))) *)((char __attribute__((address_space(1))) *)
+                                                       sgpr_ptr(p) + off) = v;
+  };
+
+  // prologue: E_old(zs-1)
+  double ex, ey, ez;
+  {
+    const int z = zlo;
+    const unsigned o = cbl + (unsigned)zc(z) * s2;
+    const unsigned oz = ownz_of(z);
+    const bool wz = sFz[tpz(z)][1] != 0;
+    const bool i0 = inA && impl(0, ownx, owny, oz, wx), i1 = inA && impl(1, ownx, owny, oz, wy),
+               i2 = inA && impl(2, ownx, owny, oz, wz);
+    ex = ldg(i0 ? Dv[0] : Ev[0], o);
+    ey = ldg(i1 ? Dv[1] : Ev[1], o);
+    ez = ldg(i2 ? Dv[2] : Ev[2], o);
+    if (UMODE == 2) {
+      const unsigned ui = ldu(uix, o >> 1);
+      if (i0) ex *= pu_(ui, 0);
+      if (i1) ey *= pu_(ui, 1);
+      if (i2) ez *= pu_(ui, 2);
+    } else if (HAS_U) {
+      if (i0) ex *= ldg(Uv[0], o);
+      if (i1) ey *= ldg(Uv[1], o);
+      if (i2) ez *= ldg(Uv[2], o);
+    }
+  }
+  double dx = 0, dy = 0, dz = 0, hmx = 0, hmy = 0;
+  unsigned uik = 0;             // palette word of plane k (UMODE 2)
+  double uk0 = 1, uk1 = 1, uk2 = 1;  // chi1inv of plane k (UMODE 1)
+  const int rowm = row > 0 ? row - 1 : 0, colm = col > 0 ? col - 1 : 0;
+  for (int k = zlo; k < ze; k++) {
+    {
+      const int kl = k;
+      const GAux ax = load_aux(kl);
+      const GBatch<UMODE> c = load(kl);
+      const int pz = tpz(kl), pz1 = tpz(kl + 1);
+      const unsigned oz = ownz_of(kl), oz1 = ownz_of(kl + 1);
+      const bool wz1 = sFz[pz1][1] != 0;
+      // E_old(k+1) of this lane
+      double e1x, e1y, e1z;
+      {
+        const bool i0 = inA && impl(0, ownx, owny, oz1, wx), i1 = inA && impl(1, ownx, owny, oz1, wy),
+                   i2 = inA && impl(2, ownx, owny, oz1, wz1);
+        double v0 = c.d0, v1 = c.d1, v2 = c.d2;
+        if (UMODE == 2) {
+          v0 = v0 * pu_(c.ui, 0);
+          v1 = v1 * pu_(c.ui, 1);
+          v2 = v2 * pu_(c.ui, 2);
+        } else if (HAS_U) {
+          v0 = v0 * c.u0;
+          v1 = v1 * c.u1;
+          v2 = v2 * c.u2;
+        }
+        e1x = i0 ? v0 : ax.es0;
+        e1y = i1 ? v1 : ax.es1;
+        e1z = i2 ? v2 : ax.es2;
+      }
+      if (ownlike) {
+        sE[0][row][col] = ex;
+        sE[1][row][col] = ey;
+        sE[2][row][col] = ez;
+      }
+      if (hslot) {
+        double h0 = c.h0, h1 = c.h1;
+        if (UMODE == 2) {
+          if (c.hi0) h0 = h0 * pu_(c.hui, hc0);
+          if (c.hi2) h1 = h1 * pu_(c.hui, 2);
+        } else if (HAS_U) {
+          if (c.hi0) h0 = h0 * c.hu0;
+          if (c.hi2) h1 = h1 * c.hu1;
+        }
+        sE[hc0][hrow][hcol] = h0;
+        sE[2][hrow][hcol] = h1;
+      }
+      __syncthreads();
+      // ---- curl B (E_old) with PML branches, then H
+      const TabE tx_s = sTx[px][1], ty_s = sTy[py][1], tz_s = sTz[pz][1];
+      const TabE tx_u = sTx[px][0], ty_u = sTy[py][0], tz_u = sTz[pz][0];
+      const bool fxs = sFx[px][1] != 0, fys = sFy[py][1] != 0, fzs = sFz[pz][1] != 0;
+      const bool fxu = sFx[px][0] != 0, fyu = sFy[py][0] != 0, fzu = sFz[pz][0] != 0;
+      const double Ez_yp = sE[2][row + 1][col], Ex_yp = sE[0][row + 1][col];
+      const double Ey_xp = sE[1][row][col + 1], Ez_xp = sE[2][row][col + 1];
+      double ubx, uby, ubz;
+      // B_c: dsig = cycle(c,1), dsigu = cycle(c,2); f_u flag along dsigu
+      const double Bx = pml_curl(c.b0, ax.ub0, Ez_yp - ez + ey - e1y, C, fzs, ty_s.kms, ty_s.si,
+                                 tz_s.kms, tz_s.si, &ubx);
+      const double By = pml_curl(c.b1, ax.ub1, e1x - ex + ez - Ez_xp, C, fxs, tz_s.kms, tz_s.si,
+                                 tx_s.kms, tx_s.si, &uby);
+      const double Bz = pml_curl(c.b2, ax.ub2, Ey_xp - ey + ex - Ex_yp, C, fys, tx_s.kms, tx_s.si,
+                                 ty_s.kms, ty_s.si, &ubz);
+      // H_c (update_eh H_stuff): separate where the chunk has PML along c
+      const double Hx = fxu ? ax.ho0 + (tx_u.kps * Bx - tx_u.kms * c.b0) : Bx;
+      const double Hy = fyu ? ax.ho1 + (ty_u.kps * By - ty_u.kms * c.b1) : By;
+      const double Hz = fzu ? ax.ho2 + (tz_u.kps * Bz - tz_u.kms * c.b2) : Bz;
+      const bool kin = k >= zs && k < ze;
+      const bool sk = stl && kin;
+      {
+        const unsigned ok = cb + (unsigned)kl * s2;
+        const unsigned o0 = (sk && own_b(0, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned o1 = (sk && own_b(1, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned o2 = (sk && own_b(2, ownx, owny, oz)) ? ok : MNL_OOB;
+        if (o0 != MNL_OOB) stg(a.Bn[0], o0, Bx);
+        if (o1 != MNL_OOB) stg(a.Bn[1], o1, By);
+        if (o2 != MNL_OOB) stg(a.Bn[2], o2, Bz);
+        if (fzs && o0 != MNL_OOB) stg(a.UBn[0], o0, ubx);
+        if (fxs && o1 != MNL_OOB) stg(a.UBn[1], o1, uby);
+        if (fys && o2 != MNL_OOB) stg(a.UBn[2], o2, ubz);
+        if (fxu && o0 != MNL_OOB) stg(a.Hn[0], o0, Hx);
+        if (fyu && o1 != MNL_OOB) stg(a.Hn[1], o1, Hy);
+        if (fzu && o2 != MNL_OOB) stg(a.Hn[2], o2, Hz);
+      }
+      if (ownlike) {
+        sB[0][row][col] = Hx;
+        sB[1][row][col] = Hy;
+        sB[2][row][col] = Hz;
+      }
+      __syncthreads();
+      // ---- curl D (H_new) with PML branches, then E where W-PML
+      const double Hz_ym = sB[2][rowm][col], Hx_ym = sB[0][rowm][col];
+      const double Hz_xm = sB[2][row][colm], Hy_xm = sB[1][row][colm];
+      double udx, udy, udz;
+      const double Dx = pml_curl(dx, ax.ud0, Hz_ym - Hz + Hy - hmy, C, fzu, ty_u.kms, ty_u.si,
+                                 tz_u.kms, tz_u.si, &udx);
+      const double Dy = pml_curl(dy, ax.ud1, hmx - Hx + Hz - Hz_xm, C, fxu, tz_u.kms, tz_u.si,
+                                 tx_u.kms, tx_u.si, &udy);
+      const double Dz = pml_curl(dz, ax.ud2, Hy_xm - Hy + Hx - Hx_ym, C, fyu, tx_u.kms, tx_u.si,
+                                 ty_u.kms, ty_u.si, &udz);
+      {
+        const unsigned ok = cb + (unsigned)kl * s2;
+        const unsigned o0 = (sk && own_e(0, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned o1 = (sk && own_e(1, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned o2 = (sk && own_e(2, ownx, owny, oz)) ? ok : MNL_OOB;
+        if (o0 != MNL_OOB) stg(a.Dn[0], o0, Dx);
+        if (o1 != MNL_OOB) stg(a.Dn[1], o1, Dy);
+        if (o2 != MNL_OOB) stg(a.Dn[2], o2, Dz);
+        if (fzu && o0 != MNL_OOB) stg(a.UD[0], o0, udx);
+        if (fxu && o1 != MNL_OOB) stg(a.UD[1], o1, udy);
+        if (fyu && o2 != MNL_OOB) stg(a.UD[2], o2, udz);
+        // E in PML chunks along its own direction (W form, src/step_generic.cpp:
+        // 576-600 fw = chi1inv * D; W_E(old) == chi1inv * D_old)
+        double k0 = 1, k1 = 1, k2 = 1;
+        if (UMODE == 2) {
+          k0 = pu_(uik, 0), k1 = pu_(uik, 1), k2 = pu_(uik, 2);
+        } else if (HAS_U) {
+          k0 = uk0, k1 = uk1, k2 = uk2;
+        }
+        const double fw0 = HAS_U ? Dx * k0 : Dx, fp0 = HAS_U ? dx * k0 : dx;
+        const double fw1 = HAS_U ? Dy * k1 : Dy, fp1 = HAS_U ? dy * k1 : dy;
+        const double fw2 = HAS_U ? Dz * k2 : Dz, fp2 = HAS_U ? dz * k2 : dz;
+        if (fxs && o0 != MNL_OOB) stg(a.En[0], o0, ex + (tx_s.kps * fw0 - tx_s.kms * fp0));
+        if (fys && o1 != MNL_OOB) stg(a.En[1], o1, ey + (ty_s.kps * fw1 - ty_s.kms * fp1));
+        if (fzs && o2 != MNL_OOB) stg(a.En[2], o2, ez + (tz_s.kps * fw2 - tz_s.kms * fp2));
+      }
+      hmx = Hx;
+      hmy = Hy;
+      dx = c.d0;
+      dy = c.d1;
+      dz = c.d2;
+      if (UMODE == 2) {
+        uik = c.ui;
+      } else if (HAS_U) {
+        uk0 = c.u0, uk1 = c.u1, uk2 = c.u2;
+      }
+      ex = e1x;
+      ey = e1y;
+      ez = e1z;
+    }
+  }
+}
+
+// General tiles: items from the host-built list a.gitems (tx | ty << 8 | ch << 16,
+// ty indexing a.gyb).  GR rows per tile (incl. the y-1 halo row), GR+1 waves:
+// fewer waves than the lean kernel so each lane gets 168 VGPRs.
+constexpr int GEN_ROWS = 11;
+template <int UMODE>
+__global__ __launch_bounds__(64 * (GEN_ROWS + 1)) void fused_general_kernel(FusedArgs a) {
+  constexpr int GR = GEN_ROWS;
+  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
+  __shared__ double sE[3][GR + 1][FX + 2];
+  __shared__ double sB[3][GR][FX + 1];
+  __shared__ TabE sTx[TPX][2], sTy[GR + 1][2], sTz[TPZ][2];
+  __shared__ unsigned char sFx[TPX][2], sFy[GR + 1][2], sFz[TPZ][2];
+  __shared__ int s_item;
+  if (UMODE == 2)
+    for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) sU[i >> 8][i & 255] = a.utab[i];
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = atomicAdd(a.ctr + 16 * 8, 1ULL);
+      s_item = (long long)v < a.ngen ? a.gitems[v] : -1;
+    }
+    __syncthreads();  // also separates LDS use of consecutive items
+    const int item = s_item;
+    if (item < 0) break;
+    const int tx = item & 255, ty = (item >> 8) & 255, ch = item >> 16;
+    ItemGeo itg;
+    itg.x0 = a.xb[tx];
+    itg.x1 = a.xb[tx + 1] - 1;
+    itg.y0 = a.gyb[ty] - 1;
+    itg.y1 = a.gyb[ty + 1] - 1;
+    itg.zs = a.zb[ch];
+    itg.ze = a.zb[ch + 1];
+    fused_general<UMODE, GR>(a, itg, sE, sB, sU, sTx, sTy, sTz, sFx, sFy, sFz);
+  }
 }
 
 template <int UMODE, int DIST>
@@ -840,10 +1289,10 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   __shared__ long long s_item;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool hwave = __builtin_amdgcn_readfirstlane(w) >= FR - 1;  // wave-uniform
-  const int flo0 = a.F.lo[0], flo1 = a.F.lo[1], flo2 = a.F.lo[2];
-  const int fhi0 = a.F.hi[0], fhi1 = a.F.hi[1], fhi2 = a.F.hi[2];
-  const FusedGeom G = fused_geom(a.F, a.zchunk);
-  const long long ntile = (long long)G.ntx * G.nty;
+  const int flo0 = a.L.lo[0], flo1 = a.L.lo[1], flo2 = a.L.lo[2];
+  const int fhi0 = a.L.hi[0], fhi1 = a.L.hi[1], fhi2 = a.L.hi[2];
+  const int nlx = a.lx1 - a.lx0 + 1, nlch = a.lz1 - a.lz0 + 1;
+  const long long ntile = (long long)nlx * (a.ly1 - a.ly0 + 1);
   const unsigned s2 = (unsigned)(a.st2 * 8);  // byte stride of one z plane
   const double C = a.C;
   const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
@@ -927,7 +1376,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
         const long long lo = ntile * qq / NQ, nq = ntile * (qq + 1) / NQ - lo;
         if (nq <= 0) continue;
         const unsigned long long v = atomicAdd(a.ctr + 16 * qq, 1ULL);
-        if ((long long)v < nq * G.nch)
+        if ((long long)v < nq * nlch)
           it = ((long long)(v / nq) * ntile) + lo + (long long)(v % nq);  // chunk*ntile + tile
       }
       s_item = it;
@@ -935,10 +1384,19 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
     __syncthreads();  // also separates LDS use of consecutive items
     const long long item = s_item;
     if (item < 0) break;
-    const int ch = (int)(item / ntile);
+    const int ch = a.lz0 + (int)(item / ntile);
     const int tile = (int)(item % ntile);
-    const int zs = flo2 + ch * G.zc, ze = min(zs + G.zc, fhi2 + 1);  // planes [zs, ze)
-    const int x0 = G.xb + (tile % G.ntx) * FX, y0 = flo1 - 1 + (tile / G.ntx) * FOWN;
+    const int tx = a.lx0 + tile % nlx, ty = a.ly0 + tile / nlx;
+    ItemGeo itg;
+    itg.x0 = a.xb[tx];
+    itg.x1 = a.xb[tx + 1] - 1;
+    itg.y0 = a.yb[ty] - 1;
+    itg.y1 = a.yb[ty + 1] - 1;
+    itg.zs = a.zb[ch];
+    itg.ze = a.zb[ch + 1];
+    // ---------------- lean body: the whole footprint lies in L
+    const int zs = itg.zs, ze = itg.ze;  // planes [zs, ze)
+    const int x0 = itg.x0, y0 = itg.y0;
 
     const int gx = x0 + ox, gy = y0 + oy;
     const bool valid = ownlike && gx >= flo0 - 1 && gx <= fhi0 + 1 && gy >= flo1 - 1 &&
@@ -952,7 +1410,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
                         hy <= fhi1 + 1;
     const bool hF = hvalid && hx >= flo0 && hx <= fhi0 && hy >= flo1 && hy <= fhi1;
     const unsigned hbl = hvalid ? (unsigned)((hx + (long long)hy * a.st1) * 8) : cbl;
-    // per-lane source of E inside F's z range: D (then E = D*u) or stored E
+    // per-lane source of E inside L's z range: D (then E = D*u) or stored E
     const gdp pO0 = colF ? Dv[0] : Ev[0], pO1 = colF ? Dv[1] : Ev[1], pO2 = colF ? Dv[2] : Ev[2];
     const gdp pH0 = hF ? hD0 : hE0, pH1 = hF ? hD1 : hE1;
 
@@ -1148,21 +1606,48 @@ static int fused_grid_blocks(int bpc) {
   return cus[dev] * bpc;
 }
 
-int k_fused(const FusedArgs &a, void *stream) {
+int k_fused(const FusedArgs &a, int which, void *stream) {
   for (int d = 0; d < 3; d++)
-    if (a.F.hi[d] < a.F.lo[d]) return 0;
-  if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr) return 1;  // host guarantees < 4 GiB arrays
-  const FusedGeom G = fused_geom(a.F, a.zchunk);
-  // 8 queue counters, one per 128-byte line
-  if (hipMemsetAsync(a.ctr, 0, 8 * 16 * sizeof(unsigned long long), (hipStream_t)stream) !=
-      hipSuccess)
-    return 1;
-  long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
-  if (nb > G.total) nb = G.total;
-  dim3 grd((unsigned)nb), blk(1024);
+    if (a.G.hi[d] < a.G.lo[d]) return 0;
+  if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr) return 2;  // host guarantees < 4 GiB arrays
+  if (a.nx < 1 || a.nx > FUSED_MAXX || a.ny < 0 || a.ny > FUSED_MAXY || a.nch < 1 ||
+      a.nch > FUSED_MAXZ || a.ngy < 1 || a.ngy > FUSED_MAXGY)
+    return 3;
+  for (int t = 0; t < a.nx; t++)  // tiles at most 64 columns wide, 128-byte aligned
+    if (a.xb[t + 1] - a.xb[t] > FX || a.xb[t + 1] <= a.xb[t] || (a.xb[t] & 15)) return 4;
+  for (int t = 0; t < a.ny; t++)
+    if (a.yb[t + 1] - a.yb[t] > FOWN || a.yb[t + 1] <= a.yb[t]) return 5;
+  for (int t = 0; t < a.ngy; t++)
+    if (a.gyb[t + 1] - a.gyb[t] > GEN_ROWS - 1 || a.gyb[t + 1] <= a.gyb[t]) return 6;
+  for (int t = 0; t < a.nch; t++)
+    if (a.zb[t + 1] <= a.zb[t] || a.zb[t + 1] - a.zb[t] > FUSED_MAXCH) return 7;
   hipStream_t s = (hipStream_t)stream;
-  const bool d2 = a.dist == 2;
   const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
+  if (which == 1) {  // general tiles
+    if (a.ngen <= 0) return 0;
+    if (hipMemsetAsync(a.ctr + 16 * 8, 0, 16 * sizeof(unsigned long long), s) != hipSuccess)
+      return 1;
+    long long ng = fused_grid_blocks(1);
+    if (ng > a.ngen) ng = a.ngen;
+    if (um == 2)
+      fused_general_kernel<2><<<dim3((unsigned)ng), dim3(64 * (GEN_ROWS + 1)), 0, s>>>(a);
+    else if (um == 1)
+      fused_general_kernel<1><<<dim3((unsigned)ng), dim3(64 * (GEN_ROWS + 1)), 0, s>>>(a);
+    else
+      fused_general_kernel<0><<<dim3((unsigned)ng), dim3(64 * (GEN_ROWS + 1)), 0, s>>>(a);
+    return hipPeekAtLastError() == hipSuccess ? 0 : 9;
+  }
+  const bool anylean = a.lx1 >= a.lx0 && a.ly1 >= a.ly0 && a.lz1 >= a.lz0;
+  const long long total = anylean ? (long long)(a.lx1 - a.lx0 + 1) * (a.ly1 - a.ly0 + 1) *
+                                        (a.lz1 - a.lz0 + 1)
+                                  : 0;
+  if (total == 0) return 0;
+  // 8 lean queue counters, one per 128-byte line
+  if (hipMemsetAsync(a.ctr, 0, 8 * 16 * sizeof(unsigned long long), s) != hipSuccess) return 1;
+  long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
+  if (nb > total) nb = total;
+  dim3 grd((unsigned)nb), blk(1024);
+  const bool d2 = a.dist == 2;
 #define MNL_LAUNCH_FUSED(U)                                   \
   do {                                                        \
     if (d2)                                                   \
@@ -1177,15 +1662,23 @@ int k_fused(const FusedArgs &a, void *stream) {
   else
     MNL_LAUNCH_FUSED(0);
 #undef MNL_LAUNCH_FUSED
-  return rc();
+  return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 
+// Leaving fused mode (or reading out): over G, E = chi1inv * D where it is
+// implicit, and the PML W aux fields get the values the reference holds
+// (W_E = chi1inv * D, W_H = B: the last fw of update_eh).
 __global__ void materialize_e_kernel(Box b, DevGrid g, DevFields f) {
   Pt p;
   if (!make_pt(b, g, p)) return;
   for (int c = 0; c < 3; c++) {
     const double d = f.D[c][p.idx];
-    f.E[c][p.idx] = f.inveps[c] ? (d * f.inveps[c][p.idx]) : d;
+    const double e = f.inveps[c] ? (d * f.inveps[c][p.idx]) : d;
+    if (e_implicit(f, g, c, p)) f.E[c][p.idx] = e;
+    if (f.WE[c] && owned(g, T_E, c, p) && pml_at(f, g, c, qcoord(g, p, T_E, c, c)))
+      f.WE[c][p.idx] = e;
+    if (f.WH[c] && owned(g, T_H, c, p) && pml_at(f, g, c, qcoord(g, p, T_H, c, c)))
+      f.WH[c][p.idx] = f.B[c][p.idx];
   }
 }
 
