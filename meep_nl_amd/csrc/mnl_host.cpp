@@ -1143,79 +1143,86 @@ bool make_fused_boxes(mnl_fields *F) {
   a.G = G;
   a.L = L;
   const int zc = std::min(F->fused_zchunk > 0 ? F->fused_zchunk : 32, FUSED_MAXCH);
-  // ---- x tiles (64 columns, starts on 16-double = 128-byte boundaries)
+  // ---- x tiles (<= 64 columns, starts on 16-double = 128-byte boundaries).  Lean
+  // tiles store columns [lx_first, x_end]: footprint x0-1 .. x1+1 inside L (the
+  // lanes past x1 load but only feed values that are never stored).
   std::vector<int> xb;
-  int lx_first = (L.lo[0] + 1 + 15) / 16 * 16, nlx = 0;
-  while (lx_first + nlx * FX_HOST + FX_HOST <= L.hi[0]) nlx++;
-  if (nlx == 0) {
+  const int lx_first = (L.lo[0] + 1 + 15) / 16 * 16;
+  const int x_end = (L.hi[0] / 16) * 16 - 1;
+  const int ly_first = L.lo[1] + 1, y_end = L.hi[1] - 1;
+  const int lz_first = L.lo[2] + 1;
+  std::vector<int> lean_starts;
+  for (int z = lz_first; z < L.hi[2]; z += zc) lean_starts.push_back(z);
+  const bool anylean = x_end >= lx_first && y_end >= ly_first && !lean_starts.empty();
+  std::vector<int> yb, gyb, zb;
+  const int gstep = FUSED_GW_ROWS;  // general wide-tile rows
+  int gly0 = -1, gly1 = -2;  // general row tiles inside the lean row range
+  if (!anylean) {
     split_range(xb, G.lo[0], G.hi[0] + 1, FX_HOST, 16);
     a.lx0 = 0, a.lx1 = -1;
+    yb.push_back(0);
+    a.ly0 = 0, a.ly1 = -1;
+    split_range(gyb, G.lo[1], G.hi[1] + 1, gstep, 1);
+    split_range(zb, G.lo[2], G.hi[2] + 1, zc, 1);
+    a.lz0 = 0, a.lz1 = -1;
   } else {
     split_range(xb, G.lo[0], lx_first, FX_HOST, 16);
     a.lx0 = (int)xb.size();
-    for (int t = 0; t < nlx; t++) xb.push_back(lx_first + FX_HOST * t);
+    split_range(xb, lx_first, x_end + 1, FX_HOST, 16);
     a.lx1 = (int)xb.size() - 1;
-    split_range(xb, lx_first + FX_HOST * nlx, G.hi[0] + 1, FX_HOST, 16);
-  }
-  // ---- lean row tiles (14 own rows; footprint y0-1 .. y0+14 inside L)
-  std::vector<int> yb;
-  int ly_first = L.lo[1] + 1, nly = 0;
-  while (ly_first + nly * 14 + 14 <= L.hi[1]) nly++;
-  for (int t = 0; t <= nly; t++) yb.push_back(ly_first + 14 * t);
-  a.ly0 = 0, a.ly1 = nly - 1;
-  // ---- general row tiles (<= GEN_ROWS-1 rows), aligned with the lean row range
-  std::vector<int> gyb;
-  const int gstep = 10;
-  int gly0 = -1, gly1 = -2;  // general row tiles inside the lean row range
-  if (nly == 0) {
-    split_range(gyb, G.lo[1], G.hi[1] + 1, gstep, 1);
-  } else {
+    split_range(xb, x_end + 1, G.hi[0] + 1, FX_HOST, 16);
+    // lean row tiles: 14 own rows (the last may be shorter), rows y0-1 .. y1+1 inside L
+    split_range(yb, ly_first, y_end + 1, 14, 1);
+    a.ly0 = 0, a.ly1 = (int)yb.size() - 1;
+    yb.push_back(y_end + 1);
     split_range(gyb, G.lo[1], ly_first, gstep, 1);
     gly0 = (int)gyb.size();
-    split_range(gyb, ly_first, ly_first + 14 * nly, gstep, 1);
+    split_range(gyb, ly_first, y_end + 1, gstep, 1);
     gly1 = (int)gyb.size() - 1;
-    split_range(gyb, ly_first + 14 * nly, G.hi[1] + 1, gstep, 1);
-  }
-  // ---- z chunks: lean chunks have planes zs-1 .. ze inside L
-  std::vector<int> zb;
-  int lz_first = L.lo[2] + 1;
-  std::vector<int> lean_starts;
-  for (int z = lz_first; z < L.hi[2]; z += zc) lean_starts.push_back(z);
-  if (lean_starts.empty() || nlx == 0 || nly == 0) {
-    split_range(zb, G.lo[2], G.hi[2] + 1, std::min(zc, FUSED_MAXCH), 1);
-    a.lz0 = 0, a.lz1 = -1;
-    a.lx0 = 0, a.lx1 = -1;
-    a.ly0 = 0, a.ly1 = -1;
-    gly0 = -1, gly1 = -2;
-  } else {
-    split_range(zb, G.lo[2], lz_first, FUSED_MAXCH, 1);
+    split_range(gyb, y_end + 1, G.hi[1] + 1, gstep, 1);
+    // z chunks: lean chunks have planes zs-1 .. ze inside L
+    split_range(zb, G.lo[2], lz_first, zc, 1);
     a.lz0 = (int)zb.size();
     for (int z : lean_starts) zb.push_back(z);
     a.lz1 = (int)zb.size() - 1;
-    split_range(zb, L.hi[2], G.hi[2] + 1, FUSED_MAXCH, 1);  // last lean chunk ends at L.hi
+    split_range(zb, L.hi[2], G.hi[2] + 1, zc, 1);  // the last lean chunk ends at L.hi
   }
-  if ((int)xb.size() > FUSED_MAXX || (int)yb.size() > FUSED_MAXY ||
-      (int)gyb.size() > FUSED_MAXGY || (int)zb.size() > FUSED_MAXZ)
+  // narrow (16-column) general tiles take rows in tiles of FUSED_GN_ROWS
+  std::vector<int> nyb;
+  split_range(nyb, G.lo[1], G.hi[1] + 1, FUSED_GN_ROWS, 1);
+  if ((int)xb.size() > FUSED_MAXX || (int)yb.size() > FUSED_MAXY + 1 ||
+      (int)gyb.size() > FUSED_MAXGY || (int)nyb.size() > FUSED_MAXNY ||
+      (int)zb.size() > FUSED_MAXZ)
     return false;
   a.nx = (int)xb.size();
   a.ny = (int)yb.size() - 1;
   a.ngy = (int)gyb.size();
+  a.nny = (int)nyb.size();
   a.nch = (int)zb.size();
   for (size_t i = 0; i < xb.size(); i++) a.xb[i] = xb[i];
   a.xb[xb.size()] = G.hi[0] + 1;
   for (size_t i = 0; i < yb.size(); i++) a.yb[i] = yb[i];
   for (size_t i = 0; i < gyb.size(); i++) a.gyb[i] = gyb[i];
   a.gyb[gyb.size()] = G.hi[1] + 1;
+  for (size_t i = 0; i < nyb.size(); i++) a.nyb[i] = nyb[i];
+  a.nyb[nyb.size()] = G.hi[1] + 1;
   for (size_t i = 0; i < zb.size(); i++) a.zb[i] = zb[i];
   a.zb[zb.size()] = G.hi[2] + 1;
-  // ---- general items (chunk-major, then rows, then columns) and cell counts
+  // ---- general items (chunk-major, then rows, then columns) and cell counts:
+  // wide tiles first, then the 16-column tiles
   F->gitems.clear();
   F->lean_cells = F->gen_cells = 0;
-  for (int ch = 0; ch < a.nch; ch++)
+  std::vector<int> narrow;
+  auto narrow_tx = [&](int tx) {
+    return a.xb[tx + 1] - a.xb[tx] <= 16 && (tx < a.lx0 || tx > a.lx1);
+  };
+  for (int ch = 0; ch < a.nch; ch++) {
+    const long long nz = a.zb[ch + 1] - a.zb[ch];
     for (int ty = 0; ty < a.ngy; ty++)
       for (int tx = 0; tx < a.nx; tx++) {
-        const long long cells = (long long)(a.xb[tx + 1] - a.xb[tx]) *
-                                (a.gyb[ty + 1] - a.gyb[ty]) * (a.zb[ch + 1] - a.zb[ch]);
+        const int wx = a.xb[tx + 1] - a.xb[tx];
+        if (narrow_tx(tx)) continue;
+        const long long cells = (long long)wx * (a.gyb[ty + 1] - a.gyb[ty]) * nz;
         const bool lean = tx >= a.lx0 && tx <= a.lx1 && ch >= a.lz0 && ch <= a.lz1 &&
                           ty >= gly0 && ty <= gly1;
         if (lean) {
@@ -1225,7 +1232,17 @@ bool make_fused_boxes(mnl_fields *F) {
         F->gen_cells += cells;
         F->gitems.push_back(tx | (ty << 8) | (ch << 16));
       }
+    for (int ty = 0; ty < a.nny; ty++)
+      for (int tx = 0; tx < a.nx; tx++) {
+        const int wx = a.xb[tx + 1] - a.xb[tx];
+        if (!narrow_tx(tx)) continue;
+        F->gen_cells += (long long)wx * (a.nyb[ty + 1] - a.nyb[ty]) * nz;
+        narrow.push_back(tx | (ty << 8) | (ch << 16));
+      }
+  }
+  a.ngen_n = (int)narrow.size();
   a.ngen = (int)F->gitems.size();
+  F->gitems.insert(F->gitems.end(), narrow.begin(), narrow.end());
   for (int k = 0; k < 3; k++) {
     a.N[k] = g.N[k];
     a.off[k] = g.off[k];
@@ -1387,8 +1404,8 @@ int set_fused(mnl_fields *F, bool on) {
   DevFields &f = F->f;
   if (on == F->fused) return 0;
   if (on) {
-    if (!F->d_fused_ctr) {  // 8 lean queue counters + 1 general counter, 128 B apart
-      if (dev_alloc(F, &F->d_fused_ctr, 9 * 16)) return -1;
+    if (!F->d_fused_ctr) {  // 8 lean queue counters + 2 general counters, 128 B apart
+      if (dev_alloc(F, &F->d_fused_ctr, 10 * 16)) return -1;
     }
     if (upload_fused_tables(F)) return -1;
     if (F->d_gitems_cap < F->gitems.size()) {

@@ -144,9 +144,11 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
 // selection, H/E W updates, per-component ownership).  Inside G, E of a point
 // is implicit (= chi1inv * D, never stored) unless the point is owned and in
 // a PML chunk along the E direction (then it is stored, ping-pong).
-constexpr int FUSED_MAXX = 64, FUSED_MAXY = 192, FUSED_MAXZ = 192;
+constexpr int FUSED_MAXX = 64, FUSED_MAXY = 160, FUSED_MAXZ = 160;
 constexpr int FUSED_MAXCH = 64;  // longest general chunk (planes)
-constexpr int FUSED_MAXGY = 256;
+constexpr int FUSED_MAXGY = 224, FUSED_MAXNY = 64;
+constexpr int FUSED_GW_ROWS = 10;  // general kernel, wide tiles: own rows per tile
+constexpr int FUSED_GN_ROWS = 39;  // general kernel, 16-column tiles: own rows per tile
 struct FusedTab {                // per direction, indexed by global half-coordinate q
   const uint8_t *flag[3];        // PML chunk along the direction (f_u / W branches)
   const double *kms[3];          // kap - sig
@@ -158,8 +160,10 @@ struct FusedArgs {
   Box G;              // fused domain (stores only inside G)
   int nx, ny, nch;    // tiles along x, y; chunks along z
   int xb[FUSED_MAXX + 1], yb[FUSED_MAXY + 1], zb[FUSED_MAXZ + 1];
-  int ngy;            // general-kernel row tiles (at most 10 rows each)
+  int ngy;            // general wide-tile rows (<= FUSED_GW_ROWS each)
   int gyb[FUSED_MAXGY + 1];
+  int nny;            // general 16-column-tile rows (<= FUSED_GN_ROWS each)
+  int nyb[FUSED_MAXNY + 1];
   int lx0, lx1, ly0, ly1, lz0, lz1;  // lean tile / chunk index ranges (inclusive)
   int N[3];           // local points per axis (array extents)
   int off[3];         // global index of local index 0 per axis
@@ -185,9 +189,9 @@ struct FusedArgs {
   const unsigned *uidx;         // chi1inv palette indices (nullptr: use u / none)
   const double *utab;           // palette, 3 x 256 doubles
   FusedTab tab;
-  const int *gitems;            // general items: tx | ty << 8 | ch << 16
-  int ngen;
-  unsigned long long *ctr;      // 9 work-queue counters (128 B apart), reset per launch
+  const int *gitems;            // general items: tx | ty << 8 | ch << 16; wide, then narrow
+  int ngen, ngen_n;
+  unsigned long long *ctr;      // 10 work-queue counters (128 B apart), reset per launch
 };
 // which: 0 = lean tiles, 1 = general tiles (both read old / write new buffers only,
 // so either order is valid)

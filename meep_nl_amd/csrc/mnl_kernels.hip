@@ -873,19 +873,21 @@ struct GAux {  // general body, PML state of plane k (own lanes), loaded masked
 // update_eh, src/update_eh.cpp:67-363, with the W aux of PML chunks
 // represented by its value: W_H == B_old, W_E == chi1inv * D_old, which the
 // reference stores one step earlier).
-template <int UMODE, int GR>
+template <int UMODE, int TX, int R, int NW>
 __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo &it,
-                                                        double (*sE)[GR + 1][FX + 2],
-                                                        double (*sB)[GR][FX + 1],
-                                                        const double (*sU)[256], TabE (*sTx)[2],
-                                                        TabE (*sTy)[2], TabE (*sTz)[2],
-                                                        unsigned char (*sFx)[2],
-                                                        unsigned char (*sFy)[2],
-                                                        unsigned char (*sFz)[2]) {
+                                              double (*sE)[R + 1][TX + 2],
+                                              double (*sB)[R][TX + 1], const double (*sU)[256],
+                                              TabE (*sTx)[2], TabE (*sTy)[2], TabE (*sTz)[2],
+                                              unsigned char (*sFx)[2], unsigned char (*sFy)[2],
+                                              unsigned char (*sFz)[2]) {
+  // Tile: TX columns x R rows (row 0 = the y-1 halo row), own waves 0..NW-1 hold
+  // 64/TX rows each (lane -> column lane % TX); the waves after them hold the
+  // x-1 column (B recomputed), the E of the x+TX column and the corner.
   constexpr bool HAS_U = UMODE != 0;
-  constexpr int GOWN = GR - 1, TPY = GR + 1;
+  constexpr int RPW = 64 / TX, TPX = TX + 2, TPY = R + 1;
+  static_assert(NW * RPW == R, "rows");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const bool hwave = __builtin_amdgcn_readfirstlane(w) >= GR - 1;
+  const bool hwave = __builtin_amdgcn_readfirstlane(w) >= NW - 1;
   const double C = a.C;
   const unsigned s2 = (unsigned)(a.st2 * 8);
   const int x0 = it.x0, y0 = it.y0, zs = it.zs, ze = it.ze;
@@ -921,31 +923,34 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   }
   __syncthreads();
 
-  // ---- lane roles (as the lean body)
-  int row, col;
-  bool ownlike;
+  // ---- lane roles
+  int row = 0, col = 0, ox = -1;
+  bool ownlike = false;
   int hrow = 0, hcol = 0, hc0 = 0, hdx = 0, hdy = 0;
   bool hslot = false;
-  if (w < GR) {
-    row = w;
-    col = lane + 1;
+  if (w < NW) {
+    row = w * RPW + lane / TX;
+    ox = lane % TX;
+    col = ox + 1;
     ownlike = true;
-    if (w == GR - 1) {
-      hslot = true, hrow = GR, hcol = col, hc0 = 0, hdx = lane, hdy = GR;
+    if (row == R - 1) {  // also loads E of the y+R row
+      hslot = true, hrow = R, hcol = col, hc0 = 0, hdx = ox, hdy = R;
     }
   } else {
-    row = lane + 1;
-    col = 0;
-    ownlike = lane < GOWN;
-    if (lane >= 16 && lane < 16 + GR) {
-      hslot = true, hrow = lane - 16, hcol = FX + 1, hc0 = 1, hdx = FX, hdy = lane - 16;
-    } else if (lane == 31) {
-      hslot = true, hrow = GR, hcol = 0, hc0 = 0, hdx = -1, hdy = GR;
+    const int h = (w - NW) * 64 + lane;
+    if (h < R - 1) {  // x-1 column of own rows 1..R-1
+      ownlike = true, row = h + 1, col = 0, ox = -1;
+    } else if (h < 2 * R - 1) {  // E of the x+TX column, rows 0..R-1
+      hslot = true, hrow = h - (R - 1), hcol = TX + 1, hc0 = 1, hdx = TX, hdy = hrow;
+    } else if (h == 2 * R - 1) {  // E(x0-1, y0+R)
+      hslot = true, hrow = R, hcol = 0, hc0 = 0, hdx = -1, hdy = R;
     }
   }
-  const int ox = (w < GR) ? lane : -1, oy = row;
+  const int oy = row;
   const int gx = x0 + ox, gy = y0 + oy;
-  const bool inA = ownlike && gx >= 0 && gx < a.N[0] && gy >= 0 && gy < a.N[1];
+  // lanes past the tile's columns x1+1 / rows y1+1 (narrow or short tiles) load nothing
+  const bool inA = ownlike && gx >= 0 && gx < a.N[0] && gy >= 0 && gy < a.N[1] &&
+                   gx <= it.x1 + 1 && gy <= it.y1 + 1;
   const unsigned cb = (unsigned)((gx + (long long)gy * a.st1) * 8);
   const unsigned cbl = inA ? cb : 0u;
   const int px = ox + 1, py = oy;  // table positions
@@ -955,10 +960,11 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
                         (rng(gx, a.oun_lo[0], a.oun_hi[0]) ? 2u : 0u);
   const unsigned owny = (rng(gy, a.osh_lo[1], a.osh_hi[1]) ? 1u : 0u) |
                         (rng(gy, a.oun_lo[1], a.oun_hi[1]) ? 2u : 0u);
-  const bool stl = ownlike && w < GR && row >= 1 && gx >= x0 && gx <= it.x1 && gy <= it.y1;
+  const bool stl = ownlike && w < NW && row >= 1 && gx >= x0 && gx <= it.x1 && gy <= it.y1;
   // halo slot point (E of comps hc0 and 2 at (hx, hy, k))
   const int hx = x0 + hdx, hy = y0 + hdy;
-  const bool hA = hslot && hx >= 0 && hx < a.N[0] && hy >= 0 && hy < a.N[1];
+  const bool hA = hslot && hx >= 0 && hx < a.N[0] && hy >= 0 && hy < a.N[1] &&
+                  hx <= it.x1 + 1 && hy <= it.y1 + 1;
   const unsigned hbl = hA ? (unsigned)((hx + (long long)hy * a.st1) * 8) : cbl;
   const int hpx = hdx + 1, hpy = hdy;
   const unsigned hownx = (rng(hx, a.osh_lo[0], a.osh_hi[0]) ? 1u : 0u) |
@@ -1105,6 +1111,8 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   unsigned uik = 0;             // palette word of plane k (UMODE 2)
   double uk0 = 1, uk1 = 1, uk2 = 1;  // chi1inv of plane k (UMODE 1)
   const int rowm = row > 0 ? row - 1 : 0, colm = col > 0 ? col - 1 : 0;
+  // one plane per iteration, loads issued at its top (no register room for a
+  // prefetch ring at 12 waves; the other waves of the CU cover the latency)
   for (int k = zlo; k < ze; k++) {
     {
       const int kl = k;
@@ -1245,25 +1253,38 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   }
 }
 
-// General tiles: items from the host-built list a.gitems (tx | ty << 8 | ch << 16,
-// ty indexing a.gyb).  GR rows per tile (incl. the y-1 halo row), GR+1 waves:
-// fewer waves than the lean kernel so each lane gets 168 VGPRs.
-constexpr int GEN_ROWS = 11;
-template <int UMODE>
-__global__ __launch_bounds__(64 * (GEN_ROWS + 1)) void fused_general_kernel(FusedArgs a) {
-  constexpr int GR = GEN_ROWS;
+// General tiles: items from the host-built list a.gitems (tx | ty << 8 | ch << 16).
+// TX = 64: tiles of <= 64 columns x FUSED_GW_ROWS rows (ty indexes a.gyb);
+// TX = 16: the narrow x-face tiles, 16 columns x FUSED_GN_ROWS rows (ty indexes
+// a.nyb), four rows per wave so a plane step does as much work as a wide tile.
+// 12 waves either way (168 VGPRs per lane).
+template <int TX>
+struct GenShape {
+  static constexpr int NW = TX == 64 ? FUSED_GW_ROWS + 1 : (FUSED_GN_ROWS + 1) / 4;
+  static constexpr int R = NW * (64 / TX);
+  static constexpr int WAVES = NW + (2 * R + 63) / 64;
+};
+static_assert(GenShape<64>::R - 1 == FUSED_GW_ROWS && GenShape<16>::R - 1 == FUSED_GN_ROWS,
+              "general tile rows");
+template <int UMODE, int TX>
+__global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel(FusedArgs a) {
+  constexpr int R = GenShape<TX>::R, NW = GenShape<TX>::NW;
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
-  __shared__ double sE[3][GR + 1][FX + 2];
-  __shared__ double sB[3][GR][FX + 1];
-  __shared__ TabE sTx[TPX][2], sTy[GR + 1][2], sTz[TPZ][2];
-  __shared__ unsigned char sFx[TPX][2], sFy[GR + 1][2], sFz[TPZ][2];
+  __shared__ double sE[3][R + 1][TX + 2];
+  __shared__ double sB[3][R][TX + 1];
+  __shared__ TabE sTx[TX + 2][2], sTy[R + 1][2], sTz[TPZ][2];
+  __shared__ unsigned char sFx[TX + 2][2], sFy[R + 1][2], sFz[TPZ][2];
   __shared__ int s_item;
   if (UMODE == 2)
     for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) sU[i >> 8][i & 255] = a.utab[i];
+  const int base = TX == 64 ? 0 : a.ngen;
+  const int n = TX == 64 ? a.ngen : a.ngen_n;
+  unsigned long long *ctr = a.ctr + 16 * (TX == 64 ? 8 : 9);
+  const int *yb = TX == 64 ? a.gyb : a.nyb;
   for (;;) {
     if (threadIdx.x == 0) {
-      const unsigned long long v = atomicAdd(a.ctr + 16 * 8, 1ULL);
-      s_item = (long long)v < a.ngen ? a.gitems[v] : -1;
+      const unsigned long long v = atomicAdd(ctr, 1ULL);
+      s_item = (long long)v < n ? a.gitems[base + v] : -1;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
@@ -1272,11 +1293,11 @@ __global__ __launch_bounds__(64 * (GEN_ROWS + 1)) void fused_general_kernel(Fuse
     ItemGeo itg;
     itg.x0 = a.xb[tx];
     itg.x1 = a.xb[tx + 1] - 1;
-    itg.y0 = a.gyb[ty] - 1;
-    itg.y1 = a.gyb[ty + 1] - 1;
+    itg.y0 = yb[ty] - 1;
+    itg.y1 = yb[ty + 1] - 1;
     itg.zs = a.zb[ch];
     itg.ze = a.zb[ch + 1];
-    fused_general<UMODE, GR>(a, itg, sE, sB, sU, sTx, sTy, sTz, sFx, sFy, sFz);
+    fused_general<UMODE, TX, R, NW>(a, itg, sE, sB, sU, sTx, sTy, sTz, sFx, sFy, sFz);
   }
 }
 
@@ -1394,7 +1415,8 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
     itg.y1 = a.yb[ty + 1] - 1;
     itg.zs = a.zb[ch];
     itg.ze = a.zb[ch + 1];
-    // ---------------- lean body: the whole footprint lies in L
+    // ---------------- lean body: rows y0-1 .. y1+1, columns x0-1 .. x1+1, planes
+    // zs-1 .. ze lie in L (lanes past x1 / y1 only feed values that are not stored)
     const int zs = itg.zs, ze = itg.ze;  // planes [zs, ze)
     const int x0 = itg.x0, y0 = itg.y0;
 
@@ -1402,7 +1424,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
     const bool valid = ownlike && gx >= flo0 - 1 && gx <= fhi0 + 1 && gy >= flo1 - 1 &&
                        gy <= fhi1 + 1;
     const bool colF = valid && gx >= flo0 && gx <= fhi0 && gy >= flo1 && gy <= fhi1;
-    const bool store = colF && w < FR && row >= 1;
+    const bool store = colF && w < FR && row >= 1 && gx <= itg.x1 && gy <= itg.y1;
     const unsigned cb = (unsigned)((gx + (long long)gy * a.st1) * 8);
     const unsigned cbl = valid ? cb : safe;
     const int hx = x0 + hdx, hy = y0 + hdy;
@@ -1611,30 +1633,43 @@ int k_fused(const FusedArgs &a, int which, void *stream) {
     if (a.G.hi[d] < a.G.lo[d]) return 0;
   if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr) return 2;  // host guarantees < 4 GiB arrays
   if (a.nx < 1 || a.nx > FUSED_MAXX || a.ny < 0 || a.ny > FUSED_MAXY || a.nch < 1 ||
-      a.nch > FUSED_MAXZ || a.ngy < 1 || a.ngy > FUSED_MAXGY)
+      a.nch > FUSED_MAXZ || a.ngy < 1 || a.ngy > FUSED_MAXGY || a.nny < 0 || a.nny > FUSED_MAXNY)
     return 3;
   for (int t = 0; t < a.nx; t++)  // tiles at most 64 columns wide, 128-byte aligned
     if (a.xb[t + 1] - a.xb[t] > FX || a.xb[t + 1] <= a.xb[t] || (a.xb[t] & 15)) return 4;
   for (int t = 0; t < a.ny; t++)
     if (a.yb[t + 1] - a.yb[t] > FOWN || a.yb[t + 1] <= a.yb[t]) return 5;
   for (int t = 0; t < a.ngy; t++)
-    if (a.gyb[t + 1] - a.gyb[t] > GEN_ROWS - 1 || a.gyb[t + 1] <= a.gyb[t]) return 6;
+    if (a.gyb[t + 1] - a.gyb[t] > FUSED_GW_ROWS || a.gyb[t + 1] <= a.gyb[t]) return 6;
+  for (int t = 0; t < a.nny; t++)
+    if (a.nyb[t + 1] - a.nyb[t] > FUSED_GN_ROWS || a.nyb[t + 1] <= a.nyb[t]) return 6;
   for (int t = 0; t < a.nch; t++)
     if (a.zb[t + 1] <= a.zb[t] || a.zb[t + 1] - a.zb[t] > FUSED_MAXCH) return 7;
   hipStream_t s = (hipStream_t)stream;
   const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
-  if (which == 1) {  // general tiles
-    if (a.ngen <= 0) return 0;
-    if (hipMemsetAsync(a.ctr + 16 * 8, 0, 16 * sizeof(unsigned long long), s) != hipSuccess)
+  if (which == 1) {  // general tiles: wide, then narrow
+    if (a.ngen + a.ngen_n <= 0) return 0;
+    if (hipMemsetAsync(a.ctr + 16 * 8, 0, 2 * 16 * sizeof(unsigned long long), s) != hipSuccess)
       return 1;
-    long long ng = fused_grid_blocks(1);
-    if (ng > a.ngen) ng = a.ngen;
-    if (um == 2)
-      fused_general_kernel<2><<<dim3((unsigned)ng), dim3(64 * (GEN_ROWS + 1)), 0, s>>>(a);
-    else if (um == 1)
-      fused_general_kernel<1><<<dim3((unsigned)ng), dim3(64 * (GEN_ROWS + 1)), 0, s>>>(a);
-    else
-      fused_general_kernel<0><<<dim3((unsigned)ng), dim3(64 * (GEN_ROWS + 1)), 0, s>>>(a);
+    const long long cus = fused_grid_blocks(1);
+    if (a.ngen > 0) {
+      const dim3 g((unsigned)std::min<long long>(cus, a.ngen)), b(64 * GenShape<64>::WAVES);
+      if (um == 2)
+        fused_general_kernel<2, 64><<<g, b, 0, s>>>(a);
+      else if (um == 1)
+        fused_general_kernel<1, 64><<<g, b, 0, s>>>(a);
+      else
+        fused_general_kernel<0, 64><<<g, b, 0, s>>>(a);
+    }
+    if (a.ngen_n > 0) {
+      const dim3 g((unsigned)std::min<long long>(cus, a.ngen_n)), b(64 * GenShape<16>::WAVES);
+      if (um == 2)
+        fused_general_kernel<2, 16><<<g, b, 0, s>>>(a);
+      else if (um == 1)
+        fused_general_kernel<1, 16><<<g, b, 0, s>>>(a);
+      else
+        fused_general_kernel<0, 16><<<g, b, 0, s>>>(a);
+    }
     return hipPeekAtLastError() == hipSuccess ? 0 : 9;
   }
   const bool anylean = a.lx1 >= a.lx0 && a.ly1 >= a.ly0 && a.lz1 >= a.lz0;

@@ -23,4 +23,5 @@ run fetch --pmc FETCH_SIZE || exit $?
 run write --pmc WRITE_SIZE || exit $?
 run sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY || exit $?
 run tcc --pmc TCC_HIT_sum TCC_MISS_sum || exit $?
+run sq2 --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_INSTS_BRANCH || exit $?
 exit 0

@@ -61,6 +61,7 @@ def main():
             res[k]["avg_ms"] = float(r["AverageNs"]) / 1e6
     fe, wr = counters(os.path.join(a.src, "fetch")), counters(os.path.join(a.src, "write"))
     sq, tcc = counters(os.path.join(a.src, "sq")), counters(os.path.join(a.src, "tcc"))
+    sq2 = counters(os.path.join(a.src, "sq2"))
     for k in set(fe) | set(wr):
         e = res.setdefault(k, {})
         if fe[k]["FETCH_SIZE"]:
@@ -71,7 +72,7 @@ def main():
             e["hbm_bytes"] = e["read_bytes"] + e["write_bytes"]
             if e.get("avg_ms"):
                 e["hbm_GBps"] = e["hbm_bytes"] / (e["avg_ms"] * 1e-3) / 1e9
-        for src in (sq, tcc):
+        for src in (sq, tcc, sq2):
             for c, v in src.get(k, {}).items():
                 e[c] = sum(v) / len(v)
     doc = {"source": a.src, "kernels_hash": kernels_hash(),
