@@ -173,6 +173,11 @@ struct mnl_fields {
   size_t d_gitems_cap = 0;
   long long lean_cells = 0, gen_cells = 0;
   FusedTab d_tab{};          // per-direction PML coefficient tables for the fused kernels
+  // multi-rank fused stepping: chunk 0 on s_aux, halo exchange on s_comm,
+  // overlapped with the interior kernels on `stream` (DESIGN.md "Multi-GPU")
+  hipStream_t s_aux = nullptr, s_comm = nullptr;
+  hipEvent_t ev_start = nullptr, ev_early = nullptr, ev_x1 = nullptr, ev_shell = nullptr,
+             ev_x0 = nullptr;
   double *pp_B[3] = {nullptr, nullptr, nullptr}, *pp_D[3] = {nullptr, nullptr, nullptr};
   double *pp_E[3] = {nullptr, nullptr, nullptr}, *pp_H[3] = {nullptr, nullptr, nullptr};
   double *pp_UB[3] = {nullptr, nullptr, nullptr};
@@ -183,6 +188,8 @@ struct mnl_fields {
   unsigned long long *d_fused_ctr = nullptr;  // work-item counter of the fused kernel
   bool palette_tried = false;
   bool dsrc_in_shell = false;  // a D source point lies outside the interior box
+  bool any_srcB = false, any_isrc = false;  // anywhere in the cell (all ranks agree)
+  bool any_dsrc_w = false;  // a D current source on a W-form (PML-along-E) point
   unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedG (null: f64 chi1inv)
   double *d_utab = nullptr;    // 3 x 256 palette values
   bool allow_fused = true;
@@ -218,6 +225,10 @@ struct mnl_fields {
     if (d_vals) hipFree(d_vals);
     if (d_gitems) hipFree(d_gitems);
     comm.reset();
+    for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
+      if (e) hipEventDestroy(e);
+    if (s_aux) hipStreamDestroy(s_aux);
+    if (s_comm) hipStreamDestroy(s_comm);
     if (stream) hipStreamDestroy(stream);
   }
 };
@@ -888,6 +899,19 @@ long long local_index(const mnl_fields *F, int c, const int jg[3], bool include_
 }
 
 int build_source_lists(mnl_fields *F) {
+  // whole-cell facts (the same on every rank): what keeps the step unfused
+  F->any_srcB = F->any_isrc = F->any_dsrc_w = false;
+  for (const SrcGroup &G : F->groups) {
+    const bool mag = ctype(G.comp) == T_H, integ = F->srcs[G.st].is_integrated;
+    if (mag && !integ) F->any_srcB = true;
+    if (!mag && integ) F->any_isrc = true;
+    if (!mag && !integ) {
+      const int d = cdir(G.comp);
+      if (F->S.has[d] && F->pml_any[d])
+        for (size_t j = 0; j < G.gidx.size(); j++)
+          if (F->h_flag[d][2 * G.jglob[3 * j + d] + 1]) F->any_dsrc_w = true;
+    }
+  }
   F->srcB_idx.clear(), F->srcD_idx.clear(), F->isrc_idx.clear();
   F->srcB_comp.clear(), F->srcD_comp.clear(), F->isrc_comp.clear();
   F->srcB_ref.clear(), F->srcD_ref.clear(), F->isrc_ref.clear();
@@ -1065,7 +1089,8 @@ int get_field(mnl_fields *F, int c, const double pos[3], double *out, bool reduc
 // kind 1 (before curl D): B (and separate H) comps shifted along the slab axis
 //   need the high ghost plane (local nloc) <- rank+1's first plane (local 0).
 // kind 2 (before NR E update): D comps (and Lorentz P), both directions.
-int exchange(mnl_fields *F, int kind) {
+int exchange(mnl_fields *F, int kind, hipStream_t st = nullptr) {
+  if (!st) st = F->stream;
   const DevGrid &g = F->g;
   const int sd = F->slab_dir, ax = g.ax[sd];
   const size_t plane = (size_t)g.st[ax];
@@ -1096,14 +1121,14 @@ int exchange(mnl_fields *F, int kind) {
   if (cm.group_start()) return -1;
   for (auto &it : items) {
     if (it.low_ghost) {
-      if (up >= 0 && cm.send(it.p + (size_t)nloc * plane, plane, up, F->stream)) return -1;
-      if (dn >= 0 && cm.recv(it.p, plane, dn, F->stream)) return -1;
+      if (up >= 0 && cm.send(it.p + (size_t)nloc * plane, plane, up, st)) return -1;
+      if (dn >= 0 && cm.recv(it.p, plane, dn, st)) return -1;
     } else {
-      if (dn >= 0 && cm.send(it.p, plane, dn, F->stream)) return -1;
-      if (up >= 0 && cm.recv(it.p + (size_t)nloc * plane, plane, up, F->stream)) return -1;
+      if (dn >= 0 && cm.send(it.p, plane, dn, st)) return -1;
+      if (up >= 0 && cm.recv(it.p + (size_t)nloc * plane, plane, up, st)) return -1;
     }
   }
-  return cm.group_end(F->stream);
+  return cm.group_end(st);
 }
 
 // ------------------------------------------------------------- stepping
@@ -1241,6 +1266,11 @@ bool make_fused_boxes(mnl_fields *F) {
       }
   }
   a.ngen_n = (int)narrow.size();
+  a.ngen_e = a.ngen_ne = 0;
+  for (int v : F->gitems)
+    if ((v >> 16) == 0) a.ngen_e++;
+  for (int v : narrow)
+    if ((v >> 16) == 0) a.ngen_ne++;
   a.ngen = (int)F->gitems.size();
   F->gitems.insert(F->gitems.end(), narrow.begin(), narrow.end());
   for (int k = 0; k < 3; k++) {
@@ -1286,7 +1316,7 @@ bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
 
 bool fused_possible(mnl_fields *F) {
   if (!F->allow_fused || F->S.dim != 3 || F->nr || F->f.npol > 0) return false;
-  if (!F->srcB_idx.empty() || !F->isrc_idx.empty()) return false;
+  if (F->any_srcB || F->any_isrc || F->any_dsrc_w) return false;
   for (int c = 0; c < MNL_NUM_COMPONENTS; c++)
     if (!F->allocated[c]) return false;
   for (int d = 0; d < 3; d++)  // separate H wherever PML lies along its direction
@@ -1296,20 +1326,18 @@ bool fused_possible(mnl_fields *F) {
   // the fused kernels address arrays with 32-bit byte offsets
   if (F->nlocal * 8 >= 0xFFFFFFF0ull) return false;
   if (!make_fused_boxes(F)) return false;
-  // a D source on a W-form E point would need E recomputed after the source
-  const DevGrid &g = F->g;
-  for (size_t k = 0; k < F->srcD_idx.size(); k++) {
-    const long long idx = F->srcD_idx[k];
-    const int d = F->srcD_comp[k];
-    const long long i2 = idx / g.st[2], r = idx % g.st[2];
-    const int jg[3] = {(int)(r % g.st[1]) + g.off[0], (int)(r / g.st[1]) + g.off[1],
-                       (int)i2 + g.off[2]};
-    bool inG = true;
-    for (int e = 0; e < 3; e++)
-      inG = inG && jg[e] - g.off[e] >= F->fusedG.lo[e] && jg[e] - g.off[e] <= F->fusedG.hi[e];
-    if (inG && F->pml_any[d] && F->h_flag[d][2 * jg[d] + 1]) return false;
-  }
   return true;
+}
+
+// fused mode only if every rank can (the ranks' exchange sequences differ by mode)
+bool fused_agreed(mnl_fields *F) {
+  bool ok = fused_possible(F);
+  if (F->nranks > 1) {
+    double v = ok ? 1.0 : 0.0;
+    if (F->comm->allreduce_sum(&v, 1, F->stream)) return false;
+    ok = v == double(F->nranks);
+  }
+  return ok;
 }
 
 // per-direction PML tables of the fused kernels (identity where no PML)
@@ -1404,8 +1432,8 @@ int set_fused(mnl_fields *F, bool on) {
   DevFields &f = F->f;
   if (on == F->fused) return 0;
   if (on) {
-    if (!F->d_fused_ctr) {  // 8 lean queue counters + 2 general counters, 128 B apart
-      if (dev_alloc(F, &F->d_fused_ctr, 10 * 16)) return -1;
+    if (!F->d_fused_ctr) {  // 8 lean queue counters + 4 general counters, 128 B apart
+      if (dev_alloc(F, &F->d_fused_ctr, 12 * 16)) return -1;
     }
     if (upload_fused_tables(F)) return -1;
     if (F->d_gitems_cap < F->gitems.size()) {
@@ -1465,9 +1493,118 @@ struct EvPair {
   int cat;
 };
 
+// kernel arguments of one fused step (geometry from make_fused_boxes, pointers now)
+FusedArgs &fused_args(mnl_fields *F) {
+  FusedArgs &fa = F->fgeo;
+  const DevFields &f = F->f;
+  fa.blocks_per_cu = F->fused_bpc;
+  fa.dist = F->fused_dist;
+  fa.nqueues = F->fused_nq;
+  fa.nelem = (long long)F->nlocal;
+  fa.C = F->S.courant;
+  fa.st1 = F->g.st[1];
+  fa.st2 = F->g.st[2];
+  for (int d = 0; d < 3; d++) {
+    fa.Bo[d] = f.B[d];
+    fa.Bn[d] = f.Bn[d];
+    fa.Do[d] = f.D[d];
+    fa.Dn[d] = f.Dn[d];
+    fa.E[d] = f.E[d];
+    fa.En[d] = f.En[d];
+    fa.Ho[d] = f.H[d];
+    fa.Hn[d] = f.Hn[d];
+    fa.UBo[d] = f.UB[d];
+    fa.UBn[d] = f.UBn[d];
+    fa.UD[d] = f.UD[d];
+    fa.u[d] = f.inveps[d];
+  }
+  fa.tab = F->d_tab;
+  fa.gitems = F->d_gitems;
+  fa.uidx = F->d_uidx;
+  fa.utab = F->d_utab;
+  fa.ctr = F->d_fused_ctr;
+  return fa;
+}
+
+int fused_fail(const char *what, int kr) {
+  return fail(std::string(what) + " (" + std::to_string(kr) + ", " +
+              hipGetErrorString(hipGetLastError()) + ")");
+}
+
+// streams / events of the overlapped multi-rank step; the E ghost plane is made
+// valid once (kind 0) since each step ends with the exchange for the next one
+int multi_begin(mnl_fields *F) {
+  if (!F->s_comm) {
+    HIPCHK(hipStreamCreateWithFlags(&F->s_comm, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
+    for (hipEvent_t *e : {&F->ev_start, &F->ev_early, &F->ev_x1, &F->ev_shell, &F->ev_x0})
+      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  HIPCHK(hipEventRecord(F->ev_start, F->stream));
+  HIPCHK(hipStreamWaitEvent(F->s_comm, F->ev_start, 0));
+  if (exchange(F, 0, F->s_comm)) return fail("E halo exchange failed");
+  HIPCHK(hipEventRecord(F->ev_x0, F->s_comm));
+  return 0;
+}
+
+// One fused step of a rank with neighbours.  Chunk 0 (planes 0..1: the B that
+// the lower neighbour needs) runs first on s_aux; its B/H plane goes down while
+// the interior runs on the main stream; the top plane (shell) follows once the
+// upper neighbour's plane has arrived, and its E goes up for the next step.
+template <class EB, class EE>
+int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) {
+  DevFields &f = F->f;
+  const DevGrid &g = F->g;
+  FusedArgs &fa = fused_args(F);
+  HIPCHK(hipEventRecord(F->ev_start, F->stream));
+  HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
+  HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_x0, 0));
+  int kr = k_fused(fa, 2, F->s_aux);
+  if (kr) return fused_fail("fused early kernel launch failed", kr);
+  HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
+  HIPCHK(hipStreamWaitEvent(F->s_comm, F->ev_early, 0));
+  if (exchange(F, 1, F->s_comm)) return fail("H halo exchange failed");
+  HIPCHK(hipEventRecord(F->ev_x1, F->s_comm));
+  int k = ev_begin(TM_BINT);
+  kr = k_fused(fa, 0, F->stream);
+  if (kr) return fused_fail("fused kernel launch failed", kr);
+  ev_end(k);
+  k = ev_begin(TM_GEN);
+  kr = k_fused(fa, 3, F->stream);
+  if (kr) return fused_fail("fused general kernel launch failed", kr);
+  ev_end(k);
+  const BoxList *sl = &F->fused_shell;
+  if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream, true))
+    return fail("curl B launch failed");
+  HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x1, 0));
+  const bool fuseE = !F->dsrc_in_shell;
+  if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream, fuseE))
+    return fail("curl D launch failed");
+  if (sD.n && k_source(T_D, g, f, sD, 0, F->stream)) return fail("source launch failed");
+  if (!fuseE) {
+    ISrcDev is;
+    is.n = 0;
+    is.val = nullptr;
+    if (k_update_e(F->interior, sl, g, f, is, 0, true, F->stream))
+      return fail("update E launch failed");
+  }
+  HIPCHK(hipEventRecord(F->ev_shell, F->stream));
+  for (int d = 0; d < 3; d++) {
+    std::swap(f.B[d], f.Bn[d]);
+    std::swap(f.D[d], f.Dn[d]);
+    std::swap(f.E[d], f.En[d]);
+    std::swap(f.H[d], f.Hn[d]);
+    std::swap(f.UB[d], f.UBn[d]);
+  }
+  HIPCHK(hipStreamWaitEvent(F->s_comm, F->ev_shell, 0));
+  if (exchange(F, 0, F->s_comm)) return fail("E halo exchange failed");
+  HIPCHK(hipEventRecord(F->ev_x0, F->s_comm));
+  return 0;
+}
+
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
-  if (set_fused(F, fused_possible(F))) return -1;
+  if (set_fused(F, fused_agreed(F))) return -1;
   {  // does a D source point lie in the shell (outside the box the interior kernels own)?
     const Box &ib = F->fused ? F->fusedG : F->interior;
     F->dsrc_in_shell = false;
@@ -1480,6 +1617,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       if (!in) F->dsrc_in_shell = true;
     }
   }
+  if (F->fused && F->nranks > 1 && multi_begin(F)) return -1;
   const double dt = F->dt;
   // per-step source values, computed on the host exactly as the reference
   size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
@@ -1567,6 +1705,10 @@ int step_batch(mnl_fields *F, int nsteps) {
       sB.val = F->d_vals + (size_t)s * per;
       sD.val = F->d_vals + (size_t)s * per + nB;
       is.val = F->d_vals + (size_t)s * per + nB + nD;
+      if (F->fused && F->nranks > 1) {
+        if (step_fused_multi(F, sD, ev_begin, ev_end)) return -1;
+        continue;
+      }
       // ---- B: halo of E (low ghost), curl, sources
       if (F->nranks > 1) {
         int k = ev_begin(TM_HALO);
@@ -1576,33 +1718,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       const BoxList *sl = F->fused ? &F->fused_shell : &F->shell_list;
       int k = ev_begin(TM_BINT);
       if (F->fused) {
-        FusedArgs &fa = F->fgeo;  // geometry from make_fused_boxes; pointers per step
-        fa.blocks_per_cu = F->fused_bpc;
-        fa.dist = F->fused_dist;
-        fa.nqueues = F->fused_nq;
-        fa.nelem = (long long)F->nlocal;
-        fa.C = F->S.courant;
-        fa.st1 = g.st[1];
-        fa.st2 = g.st[2];
-        for (int d = 0; d < 3; d++) {
-          fa.Bo[d] = f.B[d];
-          fa.Bn[d] = f.Bn[d];
-          fa.Do[d] = f.D[d];
-          fa.Dn[d] = f.Dn[d];
-          fa.E[d] = f.E[d];
-          fa.En[d] = f.En[d];
-          fa.Ho[d] = f.H[d];
-          fa.Hn[d] = f.Hn[d];
-          fa.UBo[d] = f.UB[d];
-          fa.UBn[d] = f.UBn[d];
-          fa.UD[d] = f.UD[d];
-          fa.u[d] = f.inveps[d];
-        }
-        fa.tab = F->d_tab;
-        fa.gitems = F->d_gitems;
-        fa.uidx = F->d_uidx;
-        fa.utab = F->d_utab;
-        fa.ctr = F->d_fused_ctr;
+        FusedArgs &fa = fused_args(F);
         int kr = k_fused(fa, 0, F->stream);
         if (kr)
           return fail("fused kernel launch failed (" + std::to_string(kr) + ", " +
@@ -1673,6 +1789,10 @@ int step_batch(mnl_fields *F, int nsteps) {
     }
     F->t += ns;
     if (flush_events() != 0) return -1;
+  }
+  if (F->s_comm) {
+    HIPCHK(hipStreamSynchronize(F->s_comm));
+    HIPCHK(hipStreamSynchronize(F->s_aux));
   }
   HIPCHK(hipStreamSynchronize(F->stream));
   HIPCHK(hipGetLastError());

@@ -190,11 +190,14 @@ struct FusedArgs {
   const double *utab;           // palette, 3 x 256 doubles
   FusedTab tab;
   const int *gitems;            // general items: tx | ty << 8 | ch << 16; wide, then narrow
-  int ngen, ngen_n;
-  unsigned long long *ctr;      // 10 work-queue counters (128 B apart), reset per launch
+  int ngen, ngen_n;             // wide / narrow item counts (chunk-major order)
+  int ngen_e, ngen_ne;          // leading items of chunk 0 (the early launch of multi-rank steps)
+  int gbeg, gend, ctr_line;     // set per launch by k_fused: item range and counter line
+  unsigned long long *ctr;      // 12 work-queue counters (128 B apart), reset per launch
 };
-// which: 0 = lean tiles, 1 = general tiles (both read old / write new buffers only,
-// so either order is valid)
+// which: 0 = lean tiles, 1 = all general tiles, 2 = general tiles of chunk 0
+// only (early launch), 3 = the other general tiles.  Every launch reads old /
+// writes new buffers only, on disjoint points, so any order is valid.
 int k_fused(const FusedArgs &a, int which, void *stream);
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
                  const Box &F, long long st1, long long st2, int *bad, void *stream);

@@ -1111,8 +1111,9 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   unsigned uik = 0;             // palette word of plane k (UMODE 2)
   double uk0 = 1, uk1 = 1, uk2 = 1;  // chi1inv of plane k (UMODE 1)
   const int rowm = row > 0 ? row - 1 : 0, colm = col > 0 ? col - 1 : 0;
-  // one plane per iteration, loads issued at its top (no register room for a
-  // prefetch ring at 12 waves; the other waves of the CU cover the latency)
+  // one plane per iteration, loads issued at its top (a prefetch ring does not fit
+  // in 168 VGPRs without spills and measured no faster; the other waves of the CU
+  // cover the latency)
   for (int k = zlo; k < ze; k++) {
     {
       const int kl = k;
@@ -1277,9 +1278,8 @@ __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel
   __shared__ int s_item;
   if (UMODE == 2)
     for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) sU[i >> 8][i & 255] = a.utab[i];
-  const int base = TX == 64 ? 0 : a.ngen;
-  const int n = TX == 64 ? a.ngen : a.ngen_n;
-  unsigned long long *ctr = a.ctr + 16 * (TX == 64 ? 8 : 9);
+  const int base = a.gbeg, n = a.gend - a.gbeg;
+  unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
   const int *yb = TX == 64 ? a.gyb : a.nyb;
   for (;;) {
     if (threadIdx.x == 0) {
@@ -1647,28 +1647,36 @@ int k_fused(const FusedArgs &a, int which, void *stream) {
     if (a.zb[t + 1] <= a.zb[t] || a.zb[t + 1] - a.zb[t] > FUSED_MAXCH) return 7;
   hipStream_t s = (hipStream_t)stream;
   const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
-  if (which == 1) {  // general tiles: wide, then narrow
-    if (a.ngen + a.ngen_n <= 0) return 0;
-    if (hipMemsetAsync(a.ctr + 16 * 8, 0, 2 * 16 * sizeof(unsigned long long), s) != hipSuccess)
+  if (which >= 1) {  // general tiles: wide, then narrow
+    // item ranges in a.gitems: wide [0, ngen), narrow [ngen, ngen + ngen_n); chunk-0
+    // items lead each list
+    int wb = 0, we = a.ngen, nb_ = a.ngen, ne = a.ngen + a.ngen_n, line = 8;
+    if (which == 2) we = a.ngen_e, ne = a.ngen + a.ngen_ne, line = 10;
+    if (which == 3) wb = a.ngen_e, nb_ = a.ngen + a.ngen_ne;
+    if (hipMemsetAsync(a.ctr + 16 * line, 0, 2 * 16 * sizeof(unsigned long long), s) !=
+        hipSuccess)
       return 1;
     const long long cus = fused_grid_blocks(1);
-    if (a.ngen > 0) {
-      const dim3 g((unsigned)std::min<long long>(cus, a.ngen)), b(64 * GenShape<64>::WAVES);
+    FusedArgs g = a;
+    if (we > wb) {
+      g.gbeg = wb, g.gend = we, g.ctr_line = line;
+      const dim3 gr((unsigned)std::min<long long>(cus, we - wb)), b(64 * GenShape<64>::WAVES);
       if (um == 2)
-        fused_general_kernel<2, 64><<<g, b, 0, s>>>(a);
+        fused_general_kernel<2, 64><<<gr, b, 0, s>>>(g);
       else if (um == 1)
-        fused_general_kernel<1, 64><<<g, b, 0, s>>>(a);
+        fused_general_kernel<1, 64><<<gr, b, 0, s>>>(g);
       else
-        fused_general_kernel<0, 64><<<g, b, 0, s>>>(a);
+        fused_general_kernel<0, 64><<<gr, b, 0, s>>>(g);
     }
-    if (a.ngen_n > 0) {
-      const dim3 g((unsigned)std::min<long long>(cus, a.ngen_n)), b(64 * GenShape<16>::WAVES);
+    if (ne > nb_) {
+      g.gbeg = nb_, g.gend = ne, g.ctr_line = line + 1;
+      const dim3 gr((unsigned)std::min<long long>(cus, ne - nb_)), b(64 * GenShape<16>::WAVES);
       if (um == 2)
-        fused_general_kernel<2, 16><<<g, b, 0, s>>>(a);
+        fused_general_kernel<2, 16><<<gr, b, 0, s>>>(g);
       else if (um == 1)
-        fused_general_kernel<1, 16><<<g, b, 0, s>>>(a);
+        fused_general_kernel<1, 16><<<gr, b, 0, s>>>(g);
       else
-        fused_general_kernel<0, 16><<<g, b, 0, s>>>(a);
+        fused_general_kernel<0, 16><<<gr, b, 0, s>>>(g);
     }
     return hipPeekAtLastError() == hipSuccess ? 0 : 9;
   }

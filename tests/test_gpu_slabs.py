@@ -42,3 +42,28 @@ def test_slabs_2d():
 
 def test_slabs_1d():
     _bitwise(sc_polariton_1d(GroupSim), sc_polariton_1d(make_oracle), comps=(0, 4, 6, 10))
+
+
+@pytest.mark.parametrize("G", [GroupSim, GroupSim3])
+def test_slabs_fused_big_box(G):
+    """Fused stepping across slabs: lean, wide and 16-column general tiles on every
+    rank, chunk 0 on the side stream, the top plane after the B/H exchange, and the
+    E exchange at the end of each step (DESIGN.md "Multi-GPU")."""
+    from scenarios import sc_big_box_3d
+    _bitwise(sc_big_box_3d(G, steps=16), sc_big_box_3d(make_oracle, steps=16))
+
+
+def test_slabs_fused_toggle():
+    """A magnetic source added mid-run switches every slab out of fused mode
+    (implicit E and the W aux fields are materialised) and stepping continues."""
+    from scenarios import sc_big_box_3d
+
+    def add_h(o):
+        o.add_gaussian_source(4, 0.3, 3.0, 0.0, 30.0, (1.0, 0.3, -1.1), 0.8)
+    _bitwise(sc_big_box_3d(GroupSim3, steps=12, extra=add_h),
+             sc_big_box_3d(make_oracle, steps=12, extra=add_h))
+
+
+def test_slabs_waveguide():
+    from scenarios import sc_waveguide_3d
+    _bitwise(sc_waveguide_3d(GroupSim3), sc_waveguide_3d(make_oracle))
