@@ -35,8 +35,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=512, help="cells per side of each GPU's slab")
     ap.add_argument("--vacuum", action="store_true", help="north-star vacuum variant (no core)")
+    ap.add_argument("--workload", choices=["waveguide", "vacuum", "kerr"], default=None,
+                    help="kerr: BASELINE configs[3] (chi3 + Lorentzian slab, unfused path)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-events", action="store_true",
+                    help="diagnostics: no per-kernel HIP events in the timed region")
     return ap.parse_args()
 
 
@@ -48,6 +52,17 @@ def build_fields(args, rank, world, local_rank, nid):
     gv = core.GridVolume(3, n, res, io)
     s = core.Structure(gv, 0.5)
     s.add_pml(1.0)
+    if args.workload == "kerr":  # |z| < 2: eps 2.25, chi3 1e-2, Lorentzian(1.1, 0.05, 0.5)
+        big = 1e9
+        slab = [-big, big, -big, big, -2.0, 2.0]
+        s.set_box(0, slab, 2.25)
+        s.set_box(2, slab, 1e-2)
+        k = s.add_lorentzian(1.1, 0.05, [None, None, None])
+        s.set_box(3, slab, 0.5, index=k)
+        f = core.Fields(s, device=local_rank, rank=rank, nranks=world, nccl_id=nid)
+        f.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -3.0), 50.0,
+                              is_integrated=False)
+        return gv, s, f
     if not args.vacuum:
         big = 1e9
         s.set_box(0, [-big, big, -0.5 + 1e-12, 0.5 - 1e-12, -0.5 + 1e-12, 0.5 - 1e-12], 12.0)
@@ -89,6 +104,10 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
+    if args.workload == "vacuum":
+        args.vacuum = True
+    if args.workload is None:
+        args.workload = "vacuum" if args.vacuum else "waveguide"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -110,7 +129,7 @@ def main():
 
     f.step(args.warmup)
     barrier()
-    f.set_profiling(True)
+    f.set_profiling(not args.no_events)
     t0 = time.perf_counter()
     f.step(args.steps)  # returns after the device work is complete (stream synchronized)
     barrier()
@@ -146,7 +165,9 @@ def main():
             traffic = None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": ("fused_kernel (lean tiles: curl B + curl D + E=chi1inv*D, one pass)"
+            "kernel": (("fused_kernel + fused_general_kernel concurrently (whole step, one pass)"
+                        if f.kernel_stats(2)[0] == 0 else
+                        "fused_kernel (lean tiles: curl B + curl D + E=chi1inv*D, one pass)")
                        if f.fused_active() else "curl_kernel<B, interior> (step_db(B_stuff))"),
             "bytes_per_launch": k_bytes, "avg_launch_ms": round(avg_ms, 4),
             "launches": n_launch}
@@ -159,7 +180,7 @@ def main():
                 "bytes_per_launch": g_bytes, "avg_launch_ms": round(g_avg, 4),
                 "achieved": round(g_bytes / (g_avg * 1e-3) / 1e9, 1)}
     cpu = None
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and args.workload != "kerr":
         try:
             cpu = cpu_baseline(args)
         except Exception as e:  # the baseline must never hide the GPU number
@@ -178,10 +199,13 @@ def main():
         "dtype": "f64",
         "data": "synthetic (Gaussian point source; fields start at zero)",
         "config": {
-            "workload": ("C3 3-D dielectric waveguide eps=12 core + PML(1.0)" if not args.vacuum
-                         else "C3-vacuum 3-D vacuum + PML(1.0)") +
-                        f", {args.size}x{args.size}x({args.size}*N) cells, res 10, real fields, "
-                        "Ez Gaussian current at (0.05,0.05,0.05)",
+            "workload": {"waveguide": "C3 3-D dielectric waveguide eps=12 core + PML(1.0)",
+                         "vacuum": "C3-vacuum 3-D vacuum + PML(1.0)",
+                         "kerr": "C4 3-D Kerr chi3 + Lorentzian slab |z|<2 + PML(1.0), "
+                                 "Ex source at z=-3"}[args.workload] +
+                        f", {args.size}x{args.size}x({args.size}*N) cells, res 10, real fields" +
+                        (", Ez Gaussian current at (0.05,0.05,0.05)"
+                         if args.workload != "kerr" else ""),
             "grid": list(gv.n), "per_gpu_cells": args.size ** 3, "parallelism": f"z-slab x{world}",
             "model_bytes_per_cell_step": bpc},
         "roofline": roof,

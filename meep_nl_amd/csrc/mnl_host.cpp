@@ -185,6 +185,8 @@ struct mnl_fields {
   int fused_bpc = 1;
   int fused_dist = 1;
   int fused_nq = 1;
+  int gen_cus = -1;  // CUs for the general kernel running beside the lean one (0: serial)
+  bool fused_concurrent = false;  // last fused step ran lean + general concurrently
   unsigned long long *d_fused_ctr = nullptr;  // work-item counter of the fused kernel
   bool palette_tried = false;
   bool dsrc_in_shell = false;  // a D source point lies outside the interior box
@@ -1531,6 +1533,14 @@ int fused_fail(const char *what, int kr) {
               hipGetErrorString(hipGetLastError()) + ")");
 }
 
+// CUs given to the general kernel when it runs beside the lean one: its share
+// of the step's work (general tile-planes cost ~2.5x a lean cell's bandwidth
+// time per cell), or MNL_GEN_CUS; 0 = run the two kernels one after the other
+int gen_split(const mnl_fields *F) {
+  if (F->gen_cus >= 0) return F->gen_cus;
+  return 0;
+}
+
 // streams / events of the overlapped multi-rank step; the E ghost plane is made
 // valid once (kind 0) since each step ends with the exchange for the next one
 int multi_begin(mnl_fields *F) {
@@ -1719,16 +1729,37 @@ int step_batch(mnl_fields *F, int nsteps) {
       int k = ev_begin(TM_BINT);
       if (F->fused) {
         FusedArgs &fa = fused_args(F);
-        int kr = k_fused(fa, 0, F->stream);
-        if (kr)
-          return fail("fused kernel launch failed (" + std::to_string(kr) + ", " +
-                      hipGetErrorString(hipGetLastError()) + ")");
-        ev_end(k);
-        k = ev_begin(TM_GEN);
-        kr = k_fused(fa, 1, F->stream);
-        if (kr)
-          return fail("fused general kernel launch failed (" + std::to_string(kr) + ", " +
-                      hipGetErrorString(hipGetLastError()) + ")");
+        const int split = gen_split(F);
+        int kr;
+        if (split > 0) {
+          // general tiles on `split` CUs of a side stream, lean tiles on the others,
+          // concurrently (disjoint points, old buffers read-only)
+          if (!F->s_aux) {
+            HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming));
+          }
+          HIPCHK(hipEventRecord(F->ev_start, F->stream));
+          HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
+          fa.wg_limit = split;
+          kr = k_fused(fa, 1, F->s_aux);
+          if (kr) return fused_fail("fused general kernel launch failed", kr);
+          HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
+          fa.wg_limit = k_cu_count() - split;
+          kr = k_fused(fa, 0, F->stream);
+          fa.wg_limit = 0;
+          if (kr) return fused_fail("fused kernel launch failed", kr);
+          HIPCHK(hipStreamWaitEvent(F->stream, F->ev_early, 0));
+          F->fused_concurrent = true;
+        } else {
+          F->fused_concurrent = false;
+          kr = k_fused(fa, 0, F->stream);
+          if (kr) return fused_fail("fused kernel launch failed", kr);
+          ev_end(k);
+          k = ev_begin(TM_GEN);
+          kr = k_fused(fa, 1, F->stream);
+          if (kr) return fused_fail("fused general kernel launch failed", kr);
+        }
       } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {
         return fail("curl B launch failed");
       }
@@ -1874,6 +1905,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
   if (const char *fq = getenv("MNL_FUSED_QUEUES")) F->fused_nq = atoi(fq) == 8 ? 8 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
+  if (const char *gc = getenv("MNL_GEN_CUS")) F->gen_cus = std::max(0, atoi(gc));
   if (finalize_fields(F.get())) return nullptr;
   return F.release();
 }
@@ -2237,7 +2269,8 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
   if (F->fused && which != 1) {
     double lb, gb;
     fused_bytes(F, &lb, &gb);
-    *bytes_per_launch = which == 0 ? lb : gb;
+    // concurrent lean + general: the timed span covers both kernels
+    *bytes_per_launch = which == 0 ? (F->fused_concurrent ? lb + gb : lb) : gb;
     return 0;
   }
   if (which == 2) {

@@ -169,6 +169,8 @@ struct FusedArgs {
   int off[3];         // global index of local index 0 per axis
   int osh_lo[3], osh_hi[3], oun_lo[3], oun_hi[3];  // owned ranges within G per axis
   int blocks_per_cu;  // persistent workgroups per CU (default 1)
+  int wg_limit;       // > 0: at most this many persistent workgroups (CU split between
+                      // the lean and general kernels running concurrently)
   int dist;           // lean-body prefetch distance in planes (1 or 2)
   int nqueues;        // work queues: 1 (global, default) or 8 (one per XCD)
   long long nelem;    // elements per field array (selects 32-bit offsets)
@@ -199,6 +201,7 @@ struct FusedArgs {
 // only (early launch), 3 = the other general tiles.  Every launch reads old /
 // writes new buffers only, on disjoint points, so any order is valid.
 int k_fused(const FusedArgs &a, int which, void *stream);
+int k_cu_count();
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
                  const Box &F, long long st1, long long st2, int *bad, void *stream);
 // E = chi1inv * D over box F (leaving fused mode / readout)

@@ -1616,6 +1616,13 @@ int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, co
   return rc();
 }
 
+int k_cu_count() {
+  int dev = 0;
+  hipDeviceProp_t pr;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) return 256;
+  return pr.multiProcessorCount;
+}
+
 static int fused_grid_blocks(int bpc) {
   static int cus[64] = {0};
   int dev = 0;
@@ -1656,7 +1663,8 @@ int k_fused(const FusedArgs &a, int which, void *stream) {
     if (hipMemsetAsync(a.ctr + 16 * line, 0, 2 * 16 * sizeof(unsigned long long), s) !=
         hipSuccess)
       return 1;
-    const long long cus = fused_grid_blocks(1);
+    long long cus = fused_grid_blocks(1);
+    if (a.wg_limit > 0 && cus > a.wg_limit) cus = a.wg_limit;
     FusedArgs g = a;
     if (we > wb) {
       g.gbeg = wb, g.gend = we, g.ctr_line = line;
@@ -1688,6 +1696,7 @@ int k_fused(const FusedArgs &a, int which, void *stream) {
   // 8 lean queue counters, one per 128-byte line
   if (hipMemsetAsync(a.ctr, 0, 8 * 16 * sizeof(unsigned long long), s) != hipSuccess) return 1;
   long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
+  if (a.wg_limit > 0 && nb > a.wg_limit) nb = a.wg_limit;
   if (nb > total) nb = total;
   dim3 grd((unsigned)nb), blk(1024);
   const bool d2 = a.dist == 2;
