@@ -732,6 +732,26 @@ int setup_materials(mnl_fields *F) {
         return fail("box fill failed");
     }
   }
+  // where each susceptibility can be nonzero (DESIGN.md "Dispersive E update")
+  if (nl > 0) {
+    int *dbox;
+    if (dev_alloc(F, &dbox, 6 * nl, false)) return -1;
+    std::vector<int> init(6 * nl);
+    for (int k = 0; k < nl; k++)
+      for (int e = 0; e < 3; e++) init[6 * k + e] = INT32_MAX, init[6 * k + 3 + e] = -1;
+    HIPCHK(hipMemcpyAsync(dbox, init.data(), init.size() * 4, hipMemcpyHostToDevice, F->stream));
+    for (int k = 0; k < nl; k++) {
+      const double *sg[3] = {f.pol[k].sigma[0], f.pol[k].sigma[1], f.pol[k].sigma[2]};
+      if (k_nonzero_box(sg, F->g, dbox + 6 * k, F->stream)) return fail("sigma box failed");
+    }
+    HIPCHK(hipMemcpyAsync(init.data(), dbox, init.size() * 4, hipMemcpyDeviceToHost, F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+    for (int k = 0; k < nl; k++)
+      for (int e = 0; e < 3; e++) {
+        f.pol[k].nz.lo[e] = init[6 * k + e];
+        f.pol[k].nz.hi[e] = init[6 * k + 3 + e];
+      }
+  }
   HIPCHK(hipStreamSynchronize(F->stream));
   return 0;
 }

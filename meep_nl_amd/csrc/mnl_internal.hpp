@@ -70,6 +70,10 @@ struct PolDev {
   double *P[3];
   double *Pp[3];
   const double *sigma[3];
+  // box (local indices per direction) holding every point with sigma != 0; outside
+  // it P and Pprev stay 0 (update_P with sigma = 0 from 0), so the E update
+  // neither reads nor writes them there
+  Box nz;
 };
 
 struct DevFields {
@@ -212,6 +216,8 @@ int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
                    int comp_type, int comp_dir, const DevFields &f, const Box *fusedF,
                    const double *dsrc, const double *usrc, void *stream);
+// bounding box (local indices per direction, as Pt::j) of the points where any array is nonzero
+int k_nonzero_box(const double *const a[3], const DevGrid &g, int *dev_box6, void *stream);
 int k_box_fill(double *dst, const DevGrid &g, int comp_type, int comp_dir, const double *pos_lo,
                const double *pos_hi, double value, int invert, double a, const int *io,
                void *stream);

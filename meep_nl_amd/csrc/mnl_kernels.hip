@@ -393,6 +393,33 @@ __device__ void run_nr(double seed1, double seed2, double seed3, double *fw, dou
 }
 
 // f_minus_p value of D component c at linear index n (src/update_eh.cpp:122-154)
+__device__ __forceinline__ bool in_box(const Box &b, const Pt &p) {
+  return p.j[0] >= b.lo[0] && p.j[0] <= b.hi[0] && p.j[1] >= b.lo[1] && p.j[1] <= b.hi[1] &&
+         p.j[2] >= b.lo[2] && p.j[2] <= b.hi[2];
+}
+// bit k set: pol k may have nonzero P at p (device axes == directions in 3-D;
+// in 1-D/2-D the absent directions have j = 0 and a box spanning 0)
+__device__ __forceinline__ unsigned pol_mask(const DevFields &f, const Pt &p) {
+  unsigned m = 0;
+  for (int k = 0; k < f.npol; k++)
+    if (in_box(f.pol[k].nz, p)) m |= 1u << k;
+  return m;
+}
+
+// f_minus_p at the point itself, skipping polarizations that are 0 there
+template <bool ISRC>
+__device__ __forceinline__ double dmp_own(const DevFields &f, const ISrcDev &is, int step, int c,
+                                          long long n, unsigned pm) {
+  double v = f.Dn[c][n];
+  for (int k = 0; k < f.npol; k++)
+    if (((pm >> k) & 1) && f.pol[k].P[c]) v -= f.pol[k].P[c][n];
+  if (ISRC) {
+    for (int k = 0; k < is.n; k++)
+      if (is.comp[k] == c && is.idx[k] == n) v -= is.val[(long long)step * is.n + k];
+  }
+  return v;
+}
+
 template <bool ISRC>
 __device__ __forceinline__ double dmp_at(const DevFields &f, const ISrcDev &is, int step, int c,
                                          long long n) {
@@ -417,11 +444,12 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
   Pt p;
   if (!map_pt<SHELL>(b, bl, g, p)) return;
   const long long i = p.idx;
+  const unsigned pm = pol_mask(f, p);
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     if (!f.ecomp_present[d]) continue;
     if (!owned(g, T_E, d, p)) continue;
-    const double gs = dmp_at<ISRC>(f, is, step, d, i);
+    const double gs = dmp_own<ISRC>(f, is, step, d, i, pm);
     const double *u = f.inveps[d];
     const double *E = f.E[d];
     double *En = f.En[d];
@@ -504,7 +532,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
     if (FUSEPOL) {
       for (int k = 0; k < f.npol; k++) {
         const PolDev &pd = f.pol[k];
-        if (!pd.P[d]) continue;
+        if (!pd.P[d] || !((pm >> k) & 1)) continue;
         double pcur = pd.P[d][i];
         pd.P[d][i] = pd.gamma1inv * (pcur * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * pd.Pp[d][i] +
                                      pd.omega0dtsqr * (pd.sigma[d][i] * wv));
@@ -531,7 +559,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, BoxL
     const double wv = pml ? f.WE[d][i] : f.En[d][i];
     for (int k = 0; k < f.npol; k++) {
       const PolDev &pd = f.pol[k];
-      if (!pd.P[d]) continue;
+      if (!pd.P[d] || !in_box(pd.nz, p)) continue;
       double pcur = pd.P[d][i];
       pd.P[d][i] = pd.gamma1inv * (pcur * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * pd.Pp[d][i] +
                                    pd.omega0dtsqr * (pd.sigma[d][i] * wv));
@@ -1781,6 +1809,30 @@ int k_to_canonical(double *dst, const double *src, const double *hsep, const Dev
   to_canonical_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(
       dst, src, hsep, g, f, comp_type, comp_dir, cs[0], cs[1], cs[2], fb, fusedF ? 1 : 0, dsrc,
       usrc);
+  return rc();
+}
+
+__global__ void nonzero_box_kernel(const double *a0, const double *a1, const double *a2,
+                                   DevGrid g, int *box) {
+  int i0 = blockIdx.x * MNL_BX + threadIdx.x;
+  int i1 = blockIdx.y * MNL_BY + threadIdx.y;
+  int i2 = blockIdx.z;
+  if (i0 >= g.N[0] || i1 >= g.N[1]) return;
+  const long long i = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
+  const bool nz = (a0 && a0[i] != 0.0) || (a1 && a1[i] != 0.0) || (a2 && a2[i] != 0.0);
+  if (!nz) return;
+  const int ii[3] = {i0, i1, i2};
+  for (int d = 0; d < 3; d++) {  // per direction, like Pt::j
+    const int j = g.ax[d] >= 0 ? ii[g.ax[d]] : 0;
+    atomicMin(box + d, j);
+    atomicMax(box + 3 + d, j);
+  }
+}
+
+int k_nonzero_box(const double *const a[3], const DevGrid &g, int *box, void *stream) {
+  dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
+  nonzero_box_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(a[0], a[1], a[2], g,
+                                                                           box);
   return rc();
 }
 
