@@ -1197,10 +1197,28 @@ bool make_fused_boxes(mnl_fields *F) {
   const int lx_first = (L.lo[0] + 1 + 15) / 16 * 16;
   const int x_end = (L.hi[0] / 16) * 16 - 1;
   const int ly_first = L.lo[1] + 1, y_end = L.hi[1] - 1;
+  // z segments: lean chunks need planes zs-1 .. ze inside L and away from the
+  // polarization box (where E is stored and P updated: general kernels only)
   const int lz_first = L.lo[2] + 1;
-  std::vector<int> lean_starts;
-  for (int z = lz_first; z < L.hi[2]; z += zc) lean_starts.push_back(z);
-  const bool anylean = x_end >= lx_first && y_end >= ly_first && !lean_starts.empty();
+  std::vector<std::pair<int, int>> lean_seg;  // [zs, ze) ranges of lean planes
+  {
+    int pzl = INT32_MAX, pzh = -1;
+    for (int k = 0; k < F->f.npol; k++)
+      if (F->f.pol[k].nz.lo[2] <= F->f.pol[k].nz.hi[2]) {
+        pzl = std::min(pzl, F->f.pol[k].nz.lo[2]);
+        pzh = std::max(pzh, F->f.pol[k].nz.hi[2]);
+      }
+    auto add = [&](int a0, int a1) {
+      if (a1 > a0) lean_seg.push_back({a0, a1});
+    };
+    if (pzh < 0) {
+      add(lz_first, L.hi[2]);
+    } else {
+      add(lz_first, std::min(L.hi[2], pzl - 1));
+      add(std::max(lz_first, pzh + 2), L.hi[2]);
+    }
+  }
+  const bool anylean = x_end >= lx_first && y_end >= ly_first && !lean_seg.empty();
   std::vector<int> yb, gyb, zb;
   const int gstep = FUSED_GW_ROWS;  // general wide-tile rows
   int gly0 = -1, gly1 = -2;  // general row tiles inside the lean row range
@@ -1211,7 +1229,7 @@ bool make_fused_boxes(mnl_fields *F) {
     a.ly0 = 0, a.ly1 = -1;
     split_range(gyb, G.lo[1], G.hi[1] + 1, gstep, 1);
     split_range(zb, G.lo[2], G.hi[2] + 1, zc, 1);
-    a.lz0 = 0, a.lz1 = -1;
+    a.nlzr = 0;
   } else {
     split_range(xb, G.lo[0], lx_first, FX_HOST, 16);
     a.lx0 = (int)xb.size();
@@ -1227,12 +1245,18 @@ bool make_fused_boxes(mnl_fields *F) {
     split_range(gyb, ly_first, y_end + 1, gstep, 1);
     gly1 = (int)gyb.size() - 1;
     split_range(gyb, y_end + 1, G.hi[1] + 1, gstep, 1);
-    // z chunks: lean chunks have planes zs-1 .. ze inside L
-    split_range(zb, G.lo[2], lz_first, zc, 1);
-    a.lz0 = (int)zb.size();
-    for (int z : lean_starts) zb.push_back(z);
-    a.lz1 = (int)zb.size() - 1;
-    split_range(zb, L.hi[2], G.hi[2] + 1, zc, 1);  // the last lean chunk ends at L.hi
+    // z chunks: general between the lean segments
+    a.nlzr = 0;
+    int z = G.lo[2];
+    for (auto &sg : lean_seg) {
+      split_range(zb, z, sg.first, zc, 1);
+      a.lzr[a.nlzr][0] = (int)zb.size();
+      split_range(zb, sg.first, sg.second, zc, 1);
+      a.lzr[a.nlzr][1] = (int)zb.size() - 1;
+      a.nlzr++;
+      z = sg.second;
+    }
+    split_range(zb, z, G.hi[2] + 1, zc, 1);
   }
   // narrow (16-column) general tiles take rows in tiles of FUSED_GN_ROWS
   std::vector<int> nyb;
@@ -1260,6 +1284,11 @@ bool make_fused_boxes(mnl_fields *F) {
   F->gitems.clear();
   F->lean_cells = F->gen_cells = 0;
   std::vector<int> narrow;
+  auto lean_ch = [&](int ch) {
+    for (int r = 0; r < a.nlzr; r++)
+      if (ch >= a.lzr[r][0] && ch <= a.lzr[r][1]) return true;
+    return false;
+  };
   auto narrow_tx = [&](int tx) {
     return a.xb[tx + 1] - a.xb[tx] <= 16 && (tx < a.lx0 || tx > a.lx1);
   };
@@ -1270,8 +1299,8 @@ bool make_fused_boxes(mnl_fields *F) {
         const int wx = a.xb[tx + 1] - a.xb[tx];
         if (narrow_tx(tx)) continue;
         const long long cells = (long long)wx * (a.gyb[ty + 1] - a.gyb[ty]) * nz;
-        const bool lean = tx >= a.lx0 && tx <= a.lx1 && ch >= a.lz0 && ch <= a.lz1 &&
-                          ty >= gly0 && ty <= gly1;
+        const bool lean = tx >= a.lx0 && tx <= a.lx1 && lean_ch(ch) && ty >= gly0 &&
+                          ty <= gly1;
         if (lean) {
           F->lean_cells += cells;
           continue;
@@ -1332,13 +1361,35 @@ bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
            : (j < g.owned_lo_un[e] || j > g.owned_hi_un[e]))
       return false;
   }
+  for (int k = 0; k < F->f.npol; k++) {  // E is stored inside the polarization boxes
+    const Box &b = F->f.pol[k].nz;
+    bool in = true;
+    for (int e = 0; e < 3; e++) {
+      const int j = g.ax[e] >= 0 ? jg[e] - g.off[e] : 0;
+      in = in && j >= b.lo[e] && j <= b.hi[e];
+    }
+    if (in) return false;
+  }
   const int q = 2 * jg[d] + 1;  // E_d is shifted along d
   return !(F->S.has[d] && F->h_flag[d][q]);
 }
 
 bool fused_possible(mnl_fields *F) {
-  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->f.npol > 0) return false;
+  if (!F->allow_fused || F->S.dim != 3 || F->nr) return false;
   if (F->any_srcB || F->any_isrc || F->any_dsrc_w) return false;
+  // a D source inside a polarization box would need E recomputed after it
+  // (local check; fused_agreed makes the decision collective)
+  for (size_t k = 0; k < F->srcD_idx.size(); k++) {
+    const long long idx = F->srcD_idx[k];
+    const long long i2 = idx / F->g.st[2], r = idx % F->g.st[2];
+    const int j[3] = {(int)(r % F->g.st[1]), (int)(r / F->g.st[1]), (int)i2};
+    for (int q = 0; q < F->f.npol; q++) {
+      const Box &b = F->f.pol[q].nz;
+      bool in = true;
+      for (int e = 0; e < 3; e++) in = in && j[e] >= b.lo[e] && j[e] <= b.hi[e];
+      if (in) return false;
+    }
+  }
   for (int c = 0; c < MNL_NUM_COMPONENTS; c++)
     if (!F->allocated[c]) return false;
   for (int d = 0; d < 3; d++)  // separate H wherever PML lies along its direction
@@ -1541,6 +1592,14 @@ FusedArgs &fused_args(mnl_fields *F) {
     fa.u[d] = f.inveps[d];
   }
   fa.tab = F->d_tab;
+  fa.npol = f.npol;
+  for (int k = 0; k < MAX_POL; k++) fa.pol[k] = f.pol[k];
+  for (int e = 0; e < 3; e++) fa.pbox.lo[e] = INT32_MAX, fa.pbox.hi[e] = -1;
+  for (int k = 0; k < f.npol; k++)
+    for (int e = 0; e < 3; e++) {
+      fa.pbox.lo[e] = std::min(fa.pbox.lo[e], f.pol[k].nz.lo[e]);
+      fa.pbox.hi[e] = std::max(fa.pbox.hi[e], f.pol[k].nz.hi[e]);
+    }
   fa.gitems = F->d_gitems;
   fa.uidx = F->d_uidx;
   fa.utab = F->d_utab;
@@ -1607,7 +1666,7 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
   if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream, true))
     return fail("curl B launch failed");
   HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x1, 0));
-  const bool fuseE = !F->dsrc_in_shell;
+  const bool fuseE = !F->dsrc_in_shell && f.npol == 0;
   if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream, fuseE))
     return fail("curl D launch failed");
   if (sD.n && k_source(T_D, g, f, sD, 0, F->stream)) return fail("source launch failed");
@@ -2273,6 +2332,19 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
       }
       extra += 16.0 * n;
     }
+  // polarization boxes: stored E (read + write), P and Pprev (read + write) and
+  // sigma (read) per component and susceptibility
+  for (int k = 0; k < F->f.npol; k++) {
+    const Box &b = F->f.pol[k].nz;
+    double n = 1;
+    for (int e = 0; e < 3; e++) {
+      const int lo = std::max(b.lo[e], F->fusedG.lo[e]), hi = std::min(b.hi[e], F->fusedG.hi[e]);
+      n *= hi >= lo ? double(hi - lo + 1) : 0.0;
+    }
+    int nc = 0;
+    for (int d = 0; d < 3; d++) nc += F->f.pol[k].P[d] ? 1 : 0;
+    extra += n * nc * (40.0 + (k == 0 ? 16.0 : 0.0));
+  }
   double gcells = 1;
   for (int e = 0; e < 3; e++) gcells *= double(F->fusedG.hi[e] - F->fusedG.lo[e] + 1);
   *gen_bytes = (gcells - double(F->lean_cells)) * (96.0 + ub) + extra;

@@ -150,7 +150,7 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
 // a PML chunk along the E direction (then it is stored, ping-pong).
 constexpr int FUSED_MAXX = 64, FUSED_MAXY = 160, FUSED_MAXZ = 160;
 constexpr int FUSED_MAXCH = 64;  // longest general chunk (planes)
-constexpr int FUSED_MAXGY = 224, FUSED_MAXNY = 64;
+constexpr int FUSED_MAXGY = 160, FUSED_MAXNY = 64;
 constexpr int FUSED_GW_ROWS = 10;  // general kernel, wide tiles: own rows per tile
 constexpr int FUSED_GN_ROWS = 39;  // general kernel, 16-column tiles: own rows per tile
 struct FusedTab {                // per direction, indexed by global half-coordinate q
@@ -168,7 +168,8 @@ struct FusedArgs {
   int gyb[FUSED_MAXGY + 1];
   int nny;            // general 16-column-tile rows (<= FUSED_GN_ROWS each)
   int nyb[FUSED_MAXNY + 1];
-  int lx0, lx1, ly0, ly1, lz0, lz1;  // lean tile / chunk index ranges (inclusive)
+  int lx0, lx1, ly0, ly1;      // lean x / y tile index ranges (inclusive)
+  int nlzr, lzr[4][2];         // lean chunk index ranges (inclusive), up to 4
   int N[3];           // local points per axis (array extents)
   int off[3];         // global index of local index 0 per axis
   int osh_lo[3], osh_hi[3], oun_lo[3], oun_hi[3];  // owned ranges within G per axis
@@ -195,6 +196,10 @@ struct FusedArgs {
   const unsigned *uidx;         // chi1inv palette indices (nullptr: use u / none)
   const double *utab;           // palette, 3 x 256 doubles
   FusedTab tab;
+  // isotropic Lorentzian susceptibilities (update_pols), E stored inside pbox
+  int npol;
+  PolDev pol[MAX_POL];
+  Box pbox;                     // union of the pols' nonzero boxes (empty: lo > hi)
   const int *gitems;            // general items: tx | ty << 8 | ch << 16; wide, then narrow
   int ngen, ngen_n;             // wide / narrow item counts (chunk-major order)
   int ngen_e, ngen_ne;          // leading items of chunk 0 (the early launch of multi-rank steps)

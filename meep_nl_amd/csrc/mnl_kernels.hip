@@ -102,6 +102,12 @@ __device__ __forceinline__ bool e_implicit(const DevFields &f, const DevGrid &g,
 #pragma unroll
   for (int d = 0; d < 3; d++)
     if (p.j[d] < f.fG.lo[d] || p.j[d] > f.fG.hi[d]) return false;
+  for (int k = 0; k < f.npol; k++) {  // stored inside a polarization's nonzero box
+    const Box &b = f.pol[k].nz;
+    if (p.j[0] >= b.lo[0] && p.j[0] <= b.hi[0] && p.j[1] >= b.lo[1] && p.j[1] <= b.hi[1] &&
+        p.j[2] >= b.lo[2] && p.j[2] <= b.hi[2])
+      return false;
+  }
   return owned(g, T_E, c, p) && !pml_at(f, g, c, qcoord(g, p, T_E, c, c));
 }
 
@@ -901,7 +907,7 @@ struct GAux {  // general body, PML state of plane k (own lanes), loaded masked
 // update_eh, src/update_eh.cpp:67-363, with the W aux of PML chunks
 // represented by its value: W_H == B_old, W_E == chi1inv * D_old, which the
 // reference stores one step earlier).
-template <int UMODE, int TX, int R, int NW>
+template <int UMODE, int TX, int R, int NW, bool POL>
 __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo &it,
                                               double (*sE)[R + 1][TX + 2],
                                               double (*sB)[R][TX + 1], const double (*sU)[256],
@@ -999,6 +1005,12 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
                          (rng(hx, a.oun_lo[0], a.oun_hi[0]) ? 2u : 0u);
   const unsigned howny = (rng(hy, a.osh_lo[1], a.osh_hi[1]) ? 1u : 0u) |
                          (rng(hy, a.oun_lo[1], a.oun_hi[1]) ? 2u : 0u);
+  // polarization box (E stored there, P updated in the E phase)
+  const bool pxy = POL && gx >= a.pbox.lo[0] && gx <= a.pbox.hi[0] && gy >= a.pbox.lo[1] &&
+                   gy <= a.pbox.hi[1];
+  const bool hpxy = POL && hx >= a.pbox.lo[0] && hx <= a.pbox.hi[0] && hy >= a.pbox.lo[1] &&
+                    hy <= a.pbox.hi[1];
+  auto pz_in = [&](int z) { return POL && z >= a.pbox.lo[2] && z <= a.pbox.hi[2]; };
   auto ownz_of = [&](int z) -> unsigned {
     return (rng(z, a.osh_lo[2], a.osh_hi[2]) ? 1u : 0u) | (rng(z, a.oun_lo[2], a.oun_hi[2]) ? 2u : 0u);
   };
@@ -1059,8 +1071,9 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
       const unsigned oh = hbl + (unsigned)kk * s2;
       const unsigned oz = ownz_of(k);
       const bool wz = sFz[tpz(k)][1] != 0;
-      const bool i0 = hA && impl(hc0, hownx, howny, oz, hc0 == 0 ? hwx : hwy);
-      const bool i2 = hA && impl(2, hownx, howny, oz, wz);
+      const bool hp = hpxy && pz_in(k);
+      const bool i0 = hA && impl(hc0, hownx, howny, oz, (hc0 == 0 ? hwx : hwy) || hp);
+      const bool i2 = hA && impl(2, hownx, howny, oz, wz || hp);
       q.h0 = ldg(i0 ? (hc0 ? Dv[1] : Dv[0]) : (hc0 ? Ev[1] : Ev[0]), oh);
       q.h1 = ldg(i2 ? Dv[2] : Ev[2], oh);
       if (UMODE == 2) {
@@ -1082,8 +1095,10 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
     const int pz = tpz(k), pz1 = tpz(k + 1);
     const unsigned oz1 = ownz_of(k + 1);
     const bool wz1 = sFz[pz1][1] != 0;
-    const bool e0 = inA && !impl(0, ownx, owny, oz1, wx), e1 = inA && !impl(1, ownx, owny, oz1, wy),
-               e2 = inA && !impl(2, ownx, owny, oz1, wz1);
+    const bool p1 = pxy && pz_in(k + 1);
+    const bool e0 = inA && !impl(0, ownx, owny, oz1, wx || p1),
+               e1 = inA && !impl(1, ownx, owny, oz1, wy || p1),
+               e2 = inA && !impl(2, ownx, owny, oz1, wz1 || p1);
     x.es0 = e0 ? ldg(Ev[0], o1) : 0.0;
     x.es1 = e1 ? ldg(Ev[1], o1) : 0.0;
     x.es2 = e2 ? ldg(Ev[2], o1) : 0.0;
@@ -1119,8 +1134,10 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
     const unsigned o = cbl + (unsigned)zc(z) * s2;
     const unsigned oz = ownz_of(z);
     const bool wz = sFz[tpz(z)][1] != 0;
-    const bool i0 = inA && impl(0, ownx, owny, oz, wx), i1 = inA && impl(1, ownx, owny, oz, wy),
-               i2 = inA && impl(2, ownx, owny, oz, wz);
+    const bool p0 = pxy && pz_in(z);
+    const bool i0 = inA && impl(0, ownx, owny, oz, wx || p0),
+               i1 = inA && impl(1, ownx, owny, oz, wy || p0),
+               i2 = inA && impl(2, ownx, owny, oz, wz || p0);
     ex = ldg(i0 ? Dv[0] : Ev[0], o);
     ey = ldg(i1 ? Dv[1] : Ev[1], o);
     ez = ldg(i2 ? Dv[2] : Ev[2], o);
@@ -1153,8 +1170,10 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
       // E_old(k+1) of this lane
       double e1x, e1y, e1z;
       {
-        const bool i0 = inA && impl(0, ownx, owny, oz1, wx), i1 = inA && impl(1, ownx, owny, oz1, wy),
-                   i2 = inA && impl(2, ownx, owny, oz1, wz1);
+        const bool p1 = pxy && pz_in(kl + 1);
+        const bool i0 = inA && impl(0, ownx, owny, oz1, wx || p1),
+                   i1 = inA && impl(1, ownx, owny, oz1, wy || p1),
+                   i2 = inA && impl(2, ownx, owny, oz1, wz1 || p1);
         double v0 = c.d0, v1 = c.d1, v2 = c.d2;
         if (UMODE == 2) {
           v0 = v0 * pu_(c.ui, 0);
@@ -1258,12 +1277,58 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
         } else if (HAS_U) {
           k0 = uk0, k1 = uk1, k2 = uk2;
         }
-        const double fw0 = HAS_U ? Dx * k0 : Dx, fp0 = HAS_U ? dx * k0 : dx;
-        const double fw1 = HAS_U ? Dy * k1 : Dy, fp1 = HAS_U ? dy * k1 : dy;
-        const double fw2 = HAS_U ? Dz * k2 : Dz, fp2 = HAS_U ? dz * k2 : dz;
-        if (fxs && o0 != MNL_OOB) stg(a.En[0], o0, ex + (tx_s.kps * fw0 - tx_s.kms * fp0));
-        if (fys && o1 != MNL_OOB) stg(a.En[1], o1, ey + (ty_s.kps * fw1 - ty_s.kms * fp1));
-        if (fzs && o2 != MNL_OOB) stg(a.En[2], o2, ez + (tz_s.kps * fw2 - tz_s.kms * fp2));
+        if (!(POL && pxy && pz_in(kl))) {
+          const double fw0 = HAS_U ? Dx * k0 : Dx, fp0 = HAS_U ? dx * k0 : dx;
+          const double fw1 = HAS_U ? Dy * k1 : Dy, fp1 = HAS_U ? dy * k1 : dy;
+          const double fw2 = HAS_U ? Dz * k2 : Dz, fp2 = HAS_U ? dz * k2 : dz;
+          if (fxs && o0 != MNL_OOB) stg(a.En[0], o0, ex + (tx_s.kps * fw0 - tx_s.kms * fp0));
+          if (fys && o1 != MNL_OOB) stg(a.En[1], o1, ey + (ty_s.kps * fw1 - ty_s.kms * fp1));
+          if (fzs && o2 != MNL_OOB) stg(a.En[2], o2, ez + (tz_s.kps * fw2 - tz_s.kms * fp2));
+        } else {
+          // inside the polarization box: E = chi1inv * (D - sum P) (W form in PML),
+          // then lorentzian update_P with W = E (or f_w) -- src/update_eh.cpp:84-146,
+          // src/step_generic.cpp:576-906, src/susceptibility.cpp:188-262
+          const double Dn3[3] = {Dx, Dy, Dz}, Do3[3] = {dx, dy, dz}, Eo3[3] = {ex, ey, ez};
+          const double kk3[3] = {k0, k1, k2};
+          const unsigned oo3[3] = {o0, o1, o2};
+          const bool w3[3] = {fxs, fys, fzs};
+          const TabE tw3[3] = {tx_s, ty_s, tz_s};
+#pragma unroll
+          for (int cc = 0; cc < 3; cc++) {
+            const unsigned oc = oo3[cc];
+            if (oc == MNL_OOB) continue;
+            double pv[MAX_POL], ppv[MAX_POL];
+            double gs = Dn3[cc], gp = Do3[cc];
+            for (int q = 0; q < a.npol; q++) {
+              const PolDev &pd = a.pol[q];
+              pv[q] = pd.P[cc] ? ldg(sgpr_ptr(pd.P[cc]), oc) : 0.0;
+              ppv[q] = pd.P[cc] ? ldg(sgpr_ptr(pd.Pp[cc]), oc) : 0.0;
+              if (pd.P[cc]) {
+                gs = gs - pv[q];
+                gp = gp - ppv[q];
+              }
+            }
+            const double fw = HAS_U ? gs * kk3[cc] : gs;
+            double wv;
+            if (w3[cc]) {
+              const double fp = HAS_U ? gp * kk3[cc] : gp;
+              stg(a.En[cc], oc, Eo3[cc] + (tw3[cc].kps * fw - tw3[cc].kms * fp));
+              wv = fw;
+            } else {
+              stg(a.En[cc], oc, fw);
+              wv = fw;
+            }
+            for (int q = 0; q < a.npol; q++) {
+              const PolDev &pd = a.pol[q];
+              if (!pd.P[cc]) continue;
+              const double sg = ldg(sgpr_ptr(pd.sigma[cc]), oc);
+              stg(pd.P[cc], oc,
+                  pd.gamma1inv * (pv[q] * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * ppv[q] +
+                                  pd.omega0dtsqr * (sg * wv)));
+              stg(pd.Pp[cc], oc, pv[q]);
+            }
+          }
+        }
       }
       hmx = Hx;
       hmy = Hy;
@@ -1295,7 +1360,7 @@ struct GenShape {
 };
 static_assert(GenShape<64>::R - 1 == FUSED_GW_ROWS && GenShape<16>::R - 1 == FUSED_GN_ROWS,
               "general tile rows");
-template <int UMODE, int TX>
+template <int UMODE, int TX, bool POL>
 __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel(FusedArgs a) {
   constexpr int R = GenShape<TX>::R, NW = GenShape<TX>::NW;
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
@@ -1325,7 +1390,7 @@ __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel
     itg.y1 = yb[ty + 1] - 1;
     itg.zs = a.zb[ch];
     itg.ze = a.zb[ch + 1];
-    fused_general<UMODE, TX, R, NW>(a, itg, sE, sB, sU, sTx, sTy, sTz, sFx, sFy, sFz);
+    fused_general<UMODE, TX, R, NW, POL>(a, itg, sE, sB, sU, sTx, sTy, sTz, sFx, sFy, sFz);
   }
 }
 
@@ -1340,7 +1405,9 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   const bool hwave = __builtin_amdgcn_readfirstlane(w) >= FR - 1;  // wave-uniform
   const int flo0 = a.L.lo[0], flo1 = a.L.lo[1], flo2 = a.L.lo[2];
   const int fhi0 = a.L.hi[0], fhi1 = a.L.hi[1], fhi2 = a.L.hi[2];
-  const int nlx = a.lx1 - a.lx0 + 1, nlch = a.lz1 - a.lz0 + 1;
+  int nlch = 0;
+  for (int r = 0; r < a.nlzr; r++) nlch += a.lzr[r][1] - a.lzr[r][0] + 1;
+  const int nlx = a.lx1 - a.lx0 + 1;
   const long long ntile = (long long)nlx * (a.ly1 - a.ly0 + 1);
   const unsigned s2 = (unsigned)(a.st2 * 8);  // byte stride of one z plane
   const double C = a.C;
@@ -1433,7 +1500,15 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
     __syncthreads();  // also separates LDS use of consecutive items
     const long long item = s_item;
     if (item < 0) break;
-    const int ch = a.lz0 + (int)(item / ntile);
+    int ch = (int)(item / ntile);  // lean chunk ordinal -> chunk index
+    for (int r = 0; r < a.nlzr; r++) {
+      const int n = a.lzr[r][1] - a.lzr[r][0] + 1;
+      if (ch < n) {
+        ch += a.lzr[r][0];
+        break;
+      }
+      ch -= n;
+    }
     const int tile = (int)(item % ntile);
     const int tx = a.lx0 + tile % nlx, ty = a.ly0 + tile / nlx;
     ItemGeo itg;
@@ -1663,6 +1738,27 @@ static int fused_grid_blocks(int bpc) {
   return cus[dev] * bpc;
 }
 
+template <int TX>
+static void launch_general(const FusedArgs &g, int um, dim3 gr, dim3 b, hipStream_t s) {
+  const bool pol = g.npol > 0;
+  if (um == 2) {
+    if (pol)
+      fused_general_kernel<2, TX, true><<<gr, b, 0, s>>>(g);
+    else
+      fused_general_kernel<2, TX, false><<<gr, b, 0, s>>>(g);
+  } else if (um == 1) {
+    if (pol)
+      fused_general_kernel<1, TX, true><<<gr, b, 0, s>>>(g);
+    else
+      fused_general_kernel<1, TX, false><<<gr, b, 0, s>>>(g);
+  } else {
+    if (pol)
+      fused_general_kernel<0, TX, true><<<gr, b, 0, s>>>(g);
+    else
+      fused_general_kernel<0, TX, false><<<gr, b, 0, s>>>(g);
+  }
+}
+
 int k_fused(const FusedArgs &a, int which, void *stream) {
   for (int d = 0; d < 3; d++)
     if (a.G.hi[d] < a.G.lo[d]) return 0;
@@ -1697,28 +1793,19 @@ int k_fused(const FusedArgs &a, int which, void *stream) {
     if (we > wb) {
       g.gbeg = wb, g.gend = we, g.ctr_line = line;
       const dim3 gr((unsigned)std::min<long long>(cus, we - wb)), b(64 * GenShape<64>::WAVES);
-      if (um == 2)
-        fused_general_kernel<2, 64><<<gr, b, 0, s>>>(g);
-      else if (um == 1)
-        fused_general_kernel<1, 64><<<gr, b, 0, s>>>(g);
-      else
-        fused_general_kernel<0, 64><<<gr, b, 0, s>>>(g);
+      launch_general<64>(g, um, gr, b, s);
     }
     if (ne > nb_) {
       g.gbeg = nb_, g.gend = ne, g.ctr_line = line + 1;
       const dim3 gr((unsigned)std::min<long long>(cus, ne - nb_)), b(64 * GenShape<16>::WAVES);
-      if (um == 2)
-        fused_general_kernel<2, 16><<<gr, b, 0, s>>>(g);
-      else if (um == 1)
-        fused_general_kernel<1, 16><<<gr, b, 0, s>>>(g);
-      else
-        fused_general_kernel<0, 16><<<gr, b, 0, s>>>(g);
+      launch_general<16>(g, um, gr, b, s);
     }
     return hipPeekAtLastError() == hipSuccess ? 0 : 9;
   }
-  const bool anylean = a.lx1 >= a.lx0 && a.ly1 >= a.ly0 && a.lz1 >= a.lz0;
-  const long long total = anylean ? (long long)(a.lx1 - a.lx0 + 1) * (a.ly1 - a.ly0 + 1) *
-                                        (a.lz1 - a.lz0 + 1)
+  long long nlch = 0;
+  for (int r = 0; r < a.nlzr; r++) nlch += a.lzr[r][1] - a.lzr[r][0] + 1;
+  const bool anylean = a.lx1 >= a.lx0 && a.ly1 >= a.ly0 && nlch > 0;
+  const long long total = anylean ? (long long)(a.lx1 - a.lx0 + 1) * (a.ly1 - a.ly0 + 1) * nlch
                                   : 0;
   if (total == 0) return 0;
   // 8 lean queue counters, one per 128-byte line
@@ -1755,8 +1842,13 @@ __global__ void materialize_e_kernel(Box b, DevGrid g, DevFields f) {
     const double d = f.D[c][p.idx];
     const double e = f.inveps[c] ? (d * f.inveps[c][p.idx]) : d;
     if (e_implicit(f, g, c, p)) f.E[c][p.idx] = e;
-    if (f.WE[c] && owned(g, T_E, c, p) && pml_at(f, g, c, qcoord(g, p, T_E, c, c)))
-      f.WE[c][p.idx] = e;
+    if (f.WE[c] && owned(g, T_E, c, p) && pml_at(f, g, c, qcoord(g, p, T_E, c, c))) {
+      // W_E = chi1inv * (D - P) of the last E update; P then was today's Pprev
+      double gp = d;
+      for (int k = 0; k < f.npol; k++)
+        if (f.pol[k].P[c] && in_box(f.pol[k].nz, p)) gp = gp - f.pol[k].Pp[c][p.idx];
+      f.WE[c][p.idx] = f.inveps[c] ? (gp * f.inveps[c][p.idx]) : gp;
+    }
     if (f.WH[c] && owned(g, T_H, c, p) && pml_at(f, g, c, qcoord(g, p, T_H, c, c)))
       f.WH[c][p.idx] = f.B[c][p.idx];
   }

@@ -368,3 +368,25 @@ def compare_all(a, b, comps=ALL_COMPS):
         x, y = a.get_array(c), b.get_array(c)
         out[c] = float(np.max(np.abs(x - y))) if x.size else 0.0
     return out
+
+
+def sc_big_lorentz_3d(make, steps=24, extra=None):
+    """Big non-cubic box with a dispersive slab (Lorentzian + eps, across the x/y PML)
+    between lean regions: the fused step's polarization box (E stored, P updated in
+    the general kernels) next to lean tiles; optional callback(o) mid-run."""
+    o = vol(make, 3, [14.0, 4.1, 15.3], 10, center_origin=True)
+    o.add_pml(0.7)
+    sig = []
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        inside = (z > 1.0) & (z < 3.0)
+        o.set_chi1inv(c, c, np.where(inside, 1 / 2.25, 1.0))
+        sig.append(np.where(inside, 0.5, 0.0))
+    o.add_lorentzian(1.1, 0.05, sig)
+    o.add_gaussian_source(0, 0.3, 4.0, 0.0, 40.0, (0.05, 0.05, -1.0), 50.0)
+    o.add_gaussian_source(2, 0.25, 4.0, 0.0, 40.0, (2.3, -0.4, 4.5), 5.0)
+    o.step(steps // 2)
+    if extra:
+        extra(o)
+    o.step(steps - steps // 2)
+    return o

@@ -161,3 +161,22 @@ def test_fused_many_distinct_chi1inv():
 def test_fused_prefetch_distance(monkeypatch, dist):
     monkeypatch.setenv("MNL_FUSED_DIST", dist)
     _bitwise(sc_big_box_3d(ProductSim, steps=10), sc_big_box_3d(make_oracle, steps=10))
+
+
+def test_fused_lorentz_big_box():
+    """Lorentzian slab inside a big box: fused step with the polarization box in the
+    general kernels and lean tiles around it, bitwise."""
+    from scenarios import sc_big_lorentz_3d
+    p = sc_big_lorentz_3d(ProductSim)
+    assert p._fields().fused_active()
+    _bitwise(p, sc_big_lorentz_3d(make_oracle))
+
+
+def test_fused_lorentz_toggle():
+    """Leaving fused mode inside the polarization box materialises W_E from Pprev."""
+    from scenarios import sc_big_lorentz_3d
+
+    def add_h(o):
+        o.add_gaussian_source(4, 0.3, 3.0, 0.0, 30.0, (1.0, 0.3, 2.2), 0.8)
+    _bitwise(sc_big_lorentz_3d(ProductSim, extra=add_h),
+             sc_big_lorentz_3d(make_oracle, extra=add_h))

@@ -67,3 +67,8 @@ def test_slabs_fused_toggle():
 def test_slabs_waveguide():
     from scenarios import sc_waveguide_3d
     _bitwise(sc_waveguide_3d(GroupSim3), sc_waveguide_3d(make_oracle))
+
+
+def test_slabs_fused_lorentz():
+    from scenarios import sc_big_lorentz_3d
+    _bitwise(sc_big_lorentz_3d(GroupSim3, steps=16), sc_big_lorentz_3d(make_oracle, steps=16))
