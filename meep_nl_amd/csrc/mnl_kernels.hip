@@ -907,7 +907,7 @@ struct GAux {  // general body, PML state of plane k (own lanes), loaded masked
 // update_eh, src/update_eh.cpp:67-363, with the W aux of PML chunks
 // represented by its value: W_H == B_old, W_E == chi1inv * D_old, which the
 // reference stores one step earlier).
-template <int UMODE, int TX, int R, int NW, bool POL>
+template <int UMODE, int TX, int R, int NW, int POL>
 __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo &it,
                                               double (*sE)[R + 1][TX + 2],
                                               double (*sB)[R][TX + 1], const double (*sU)[256],
@@ -1293,6 +1293,39 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
           const unsigned oo3[3] = {o0, o1, o2};
           const bool w3[3] = {fxs, fys, fzs};
           const TabE tw3[3] = {tx_s, ty_s, tz_s};
+          if (POL == 1) {  // one susceptibility: all loads first, one memory wait
+            const PolDev &pd = a.pol[0];
+            double pv[3], ppv[3], sg[3];
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) {
+              const bool on = oo3[cc] != MNL_OOB && pd.P[cc];
+              const unsigned oc = on ? oo3[cc] : cbl;
+              pv[cc] = on ? ldg(sgpr_ptr(pd.P[cc]), oc) : 0.0;
+              ppv[cc] = on ? ldg(sgpr_ptr(pd.Pp[cc]), oc) : 0.0;
+              sg[cc] = on ? ldg(sgpr_ptr(pd.sigma[cc]), oc) : 0.0;
+            }
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) {
+              const unsigned oc = oo3[cc];
+              if (oc == MNL_OOB) continue;
+              const bool hp = pd.P[cc] != nullptr;
+              const double gs = hp ? Dn3[cc] - pv[cc] : Dn3[cc];
+              const double fw = HAS_U ? gs * kk3[cc] : gs;
+              if (w3[cc]) {
+                const double gp = hp ? Do3[cc] - ppv[cc] : Do3[cc];
+                const double fp = HAS_U ? gp * kk3[cc] : gp;
+                stg(a.En[cc], oc, Eo3[cc] + (tw3[cc].kps * fw - tw3[cc].kms * fp));
+              } else {
+                stg(a.En[cc], oc, fw);
+              }
+              if (hp) {
+                stg(pd.P[cc], oc,
+                    pd.gamma1inv * (pv[cc] * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * ppv[cc] +
+                                    pd.omega0dtsqr * (sg[cc] * fw)));
+                stg(pd.Pp[cc], oc, pv[cc]);
+              }
+            }
+          } else {
 #pragma unroll
           for (int cc = 0; cc < 3; cc++) {
             const unsigned oc = oo3[cc];
@@ -1328,6 +1361,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
               stg(pd.Pp[cc], oc, pv[q]);
             }
           }
+          }
         }
       }
       hmx = Hx;
@@ -1360,7 +1394,7 @@ struct GenShape {
 };
 static_assert(GenShape<64>::R - 1 == FUSED_GW_ROWS && GenShape<16>::R - 1 == FUSED_GN_ROWS,
               "general tile rows");
-template <int UMODE, int TX, bool POL>
+template <int UMODE, int TX, int POL>
 __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel(FusedArgs a) {
   constexpr int R = GenShape<TX>::R, NW = GenShape<TX>::NW;
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
@@ -1738,25 +1772,23 @@ static int fused_grid_blocks(int bpc) {
   return cus[dev] * bpc;
 }
 
+template <int TX, int UM>
+static void launch_general_u(const FusedArgs &g, dim3 gr, dim3 b, hipStream_t s) {
+  if (g.npol == 0)
+    fused_general_kernel<UM, TX, 0><<<gr, b, 0, s>>>(g);
+  else if (g.npol == 1)
+    fused_general_kernel<UM, TX, 1><<<gr, b, 0, s>>>(g);
+  else
+    fused_general_kernel<UM, TX, 2><<<gr, b, 0, s>>>(g);
+}
 template <int TX>
 static void launch_general(const FusedArgs &g, int um, dim3 gr, dim3 b, hipStream_t s) {
-  const bool pol = g.npol > 0;
-  if (um == 2) {
-    if (pol)
-      fused_general_kernel<2, TX, true><<<gr, b, 0, s>>>(g);
-    else
-      fused_general_kernel<2, TX, false><<<gr, b, 0, s>>>(g);
-  } else if (um == 1) {
-    if (pol)
-      fused_general_kernel<1, TX, true><<<gr, b, 0, s>>>(g);
-    else
-      fused_general_kernel<1, TX, false><<<gr, b, 0, s>>>(g);
-  } else {
-    if (pol)
-      fused_general_kernel<0, TX, true><<<gr, b, 0, s>>>(g);
-    else
-      fused_general_kernel<0, TX, false><<<gr, b, 0, s>>>(g);
-  }
+  if (um == 2)
+    launch_general_u<TX, 2>(g, gr, b, s);
+  else if (um == 1)
+    launch_general_u<TX, 1>(g, gr, b, s);
+  else
+    launch_general_u<TX, 0>(g, gr, b, s);
 }
 
 int k_fused(const FusedArgs &a, int which, void *stream) {
