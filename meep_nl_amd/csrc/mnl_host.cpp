@@ -184,10 +184,11 @@ struct mnl_fields {
   int fused_zchunk = 0;
   int fused_bpc = 1;
   int fused_dist = 1;
-  int fused_nq = 1;
   int gen_cus = -1;  // CUs for the general kernel running beside the lean one (0: serial)
   bool fused_concurrent = false;  // last fused step ran lean + general concurrently
-  unsigned long long *d_fused_ctr = nullptr;  // work-item counter of the fused kernel
+  unsigned long long *d_fused_ctr = nullptr;  // work-item counters of the fused kernels
+  unsigned long long ctr_base[12] = {0};      // their values at the next launch
+  int stagger = 0, nstagger = 0;  // dev_alloc offset step (bytes) for field arrays
   bool palette_tried = false;
   bool dsrc_in_shell = false;  // a D source point lies outside the interior box
   bool any_srcB = false, any_isrc = false;  // anywhere in the cell (all ranks agree)
@@ -239,17 +240,23 @@ namespace {
 
 bool in_fused_box(const mnl_fields *F, int c, const int jg[3]);
 
+// Field-sized arrays start at staggered offsets (a multiple of 128 B, different
+// for every array) so that the many streams one fused step reads and writes at
+// the same element index do not start on the same HBM channel / bank.
 template <class T>
 int dev_alloc(mnl_fields *F, T **p, size_t n, bool zero = true) {
   void *q = nullptr;
-  hipError_t e = hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T));
+  const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  const bool big = bytes >= (size_t(64) << 20) && F->stagger > 0;
+  const size_t off = big ? (size_t(F->stagger) * F->nstagger++) % (size_t(1) << 20) : 0;
+  hipError_t e = hipMalloc(&q, bytes + (big ? (size_t(1) << 20) : 0));
   if (e != hipSuccess) return fail(std::string("hipMalloc failed: ") + hipGetErrorString(e));
   if (zero) {
-    e = hipMemsetAsync(q, 0, std::max<size_t>(n, 1) * sizeof(T), F->stream);
+    e = hipMemsetAsync((char *)q + off, 0, bytes, F->stream);
     if (e != hipSuccess) return fail(std::string("hipMemset failed: ") + hipGetErrorString(e));
   }
   F->dev_allocs.push_back(q);
-  *p = (T *)q;
+  *p = (T *)((char *)q + off);
   return 0;
 }
 
@@ -1572,7 +1579,6 @@ FusedArgs &fused_args(mnl_fields *F) {
   const DevFields &f = F->f;
   fa.blocks_per_cu = F->fused_bpc;
   fa.dist = F->fused_dist;
-  fa.nqueues = F->fused_nq;
   fa.nelem = (long long)F->nlocal;
   fa.C = F->S.courant;
   fa.st1 = F->g.st[1];
@@ -1648,18 +1654,18 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
   HIPCHK(hipEventRecord(F->ev_start, F->stream));
   HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
   HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_x0, 0));
-  int kr = k_fused(fa, 2, F->s_aux);
+  int kr = k_fused(fa, 2, F->s_aux, F->ctr_base);
   if (kr) return fused_fail("fused early kernel launch failed", kr);
   HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
   HIPCHK(hipStreamWaitEvent(F->s_comm, F->ev_early, 0));
   if (exchange(F, 1, F->s_comm)) return fail("H halo exchange failed");
   HIPCHK(hipEventRecord(F->ev_x1, F->s_comm));
   int k = ev_begin(TM_BINT);
-  kr = k_fused(fa, 0, F->stream);
+  kr = k_fused(fa, 0, F->stream, F->ctr_base);
   if (kr) return fused_fail("fused kernel launch failed", kr);
   ev_end(k);
   k = ev_begin(TM_GEN);
-  kr = k_fused(fa, 3, F->stream);
+  kr = k_fused(fa, 3, F->stream, F->ctr_base);
   if (kr) return fused_fail("fused general kernel launch failed", kr);
   ev_end(k);
   const BoxList *sl = &F->fused_shell;
@@ -1821,22 +1827,22 @@ int step_batch(mnl_fields *F, int nsteps) {
           HIPCHK(hipEventRecord(F->ev_start, F->stream));
           HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
           fa.wg_limit = split;
-          kr = k_fused(fa, 1, F->s_aux);
+          kr = k_fused(fa, 1, F->s_aux, F->ctr_base);
           if (kr) return fused_fail("fused general kernel launch failed", kr);
           HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
           fa.wg_limit = k_cu_count() - split;
-          kr = k_fused(fa, 0, F->stream);
+          kr = k_fused(fa, 0, F->stream, F->ctr_base);
           fa.wg_limit = 0;
           if (kr) return fused_fail("fused kernel launch failed", kr);
           HIPCHK(hipStreamWaitEvent(F->stream, F->ev_early, 0));
           F->fused_concurrent = true;
         } else {
           F->fused_concurrent = false;
-          kr = k_fused(fa, 0, F->stream);
+          kr = k_fused(fa, 0, F->stream, F->ctr_base);
           if (kr) return fused_fail("fused kernel launch failed", kr);
           ev_end(k);
           k = ev_begin(TM_GEN);
-          kr = k_fused(fa, 1, F->stream);
+          kr = k_fused(fa, 1, F->stream, F->ctr_base);
           if (kr) return fused_fail("fused general kernel launch failed", kr);
         }
       } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {
@@ -1982,9 +1988,9 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(0, atoi(zc));
   if (const char *bp = getenv("MNL_FUSED_BPC")) F->fused_bpc = std::max(1, atoi(bp));
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
-  if (const char *fq = getenv("MNL_FUSED_QUEUES")) F->fused_nq = atoi(fq) == 8 ? 8 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
   if (const char *gc = getenv("MNL_GEN_CUS")) F->gen_cus = std::max(0, atoi(gc));
+  if (const char *sg = getenv("MNL_STAGGER")) F->stagger = std::max(0, atoi(sg)) / 128 * 128;
   if (finalize_fields(F.get())) return nullptr;
   return F.release();
 }

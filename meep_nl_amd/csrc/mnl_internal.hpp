@@ -177,7 +177,6 @@ struct FusedArgs {
   int wg_limit;       // > 0: at most this many persistent workgroups (CU split between
                       // the lean and general kernels running concurrently)
   int dist;           // lean-body prefetch distance in planes (1 or 2)
-  int nqueues;        // work queues: 1 (global, default) or 8 (one per XCD)
   long long nelem;    // elements per field array (selects 32-bit offsets)
   double C;
   long long st1, st2;
@@ -204,12 +203,15 @@ struct FusedArgs {
   int ngen, ngen_n;             // wide / narrow item counts (chunk-major order)
   int ngen_e, ngen_ne;          // leading items of chunk 0 (the early launch of multi-rank steps)
   int gbeg, gend, ctr_line;     // set per launch by k_fused: item range and counter line
-  unsigned long long *ctr;      // 12 work-queue counters (128 B apart), reset per launch
+  unsigned long long cbase;     // counter value at launch start (counters are never reset)
+  unsigned long long *ctr;      // 12 work-queue counters (128 B apart); see cbase
 };
 // which: 0 = lean tiles, 1 = all general tiles, 2 = general tiles of chunk 0
 // only (early launch), 3 = the other general tiles.  Every launch reads old /
 // writes new buffers only, on disjoint points, so any order is valid.
-int k_fused(const FusedArgs &a, int which, void *stream);
+// bases[12]: host copy of each counter line's value, advanced by every launch
+// (items + workgroups), so no counter reset (memset launch) is needed per step
+int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bases);
 int k_cu_count();
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
                  const Box &F, long long st1, long long st2, int *bad, void *stream);

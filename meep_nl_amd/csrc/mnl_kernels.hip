@@ -1410,7 +1410,7 @@ __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel
   const int *yb = TX == 64 ? a.gyb : a.nyb;
   for (;;) {
     if (threadIdx.x == 0) {
-      const unsigned long long v = atomicAdd(ctr, 1ULL);
+      const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
       s_item = (long long)v < n ? a.gitems[base + v] : -1;
     }
     __syncthreads();  // also separates LDS use of consecutive items
@@ -1510,26 +1510,12 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   }
   auto pu = [&](unsigned ui, int c) -> double { return sU[UMODE == 2 ? c : 0][(ui >> (8 * c)) & 255]; };
 
-  // per-XCD work queues (speed only: any block may take any item): queue q
-  // holds the tiles [q*ntile/8, (q+1)*ntile/8) of every chunk, chunk-major, so
-  // the blocks of one XCD sweep neighbouring tiles together and the halo lines
-  // they share hit that XCD's L2.  An empty queue sends the block to the others.
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-  const int NQ = a.nqueues == 1 ? 1 : 8;  // 1: one global chunk-major queue
-  xcc = NQ == 1 ? 0 : (xcc & 7);
+  // one chunk-major work queue: consecutive items are neighbouring tiles of one
+  // chunk, so the workgroups sweep z roughly together
   for (;;) {
     if (threadIdx.x == 0) {
-      long long it = -1;
-      for (int r = 0; r < NQ && it < 0; r++) {
-        const int qq = (int)((xcc + r) % NQ);
-        const long long lo = ntile * qq / NQ, nq = ntile * (qq + 1) / NQ - lo;
-        if (nq <= 0) continue;
-        const unsigned long long v = atomicAdd(a.ctr + 16 * qq, 1ULL);
-        if ((long long)v < nq * nlch)
-          it = ((long long)(v / nq) * ntile) + lo + (long long)(v % nq);  // chunk*ntile + tile
-      }
-      s_item = it;
+      const unsigned long long v = atomicAdd(a.ctr, 1ULL) - a.cbase;
+      s_item = (long long)v < ntile * nlch ? (long long)v : -1;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const long long item = s_item;
@@ -1791,7 +1777,7 @@ static void launch_general(const FusedArgs &g, int um, dim3 gr, dim3 b, hipStrea
     launch_general_u<TX, 0>(g, gr, b, s);
 }
 
-int k_fused(const FusedArgs &a, int which, void *stream) {
+int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bases) {
   for (int d = 0; d < 3; d++)
     if (a.G.hi[d] < a.G.lo[d]) return 0;
   if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr) return 2;  // host guarantees < 4 GiB arrays
@@ -1816,21 +1802,20 @@ int k_fused(const FusedArgs &a, int which, void *stream) {
     int wb = 0, we = a.ngen, nb_ = a.ngen, ne = a.ngen + a.ngen_n, line = 8;
     if (which == 2) we = a.ngen_e, ne = a.ngen + a.ngen_ne, line = 10;
     if (which == 3) wb = a.ngen_e, nb_ = a.ngen + a.ngen_ne;
-    if (hipMemsetAsync(a.ctr + 16 * line, 0, 2 * 16 * sizeof(unsigned long long), s) !=
-        hipSuccess)
-      return 1;
     long long cus = fused_grid_blocks(1);
     if (a.wg_limit > 0 && cus > a.wg_limit) cus = a.wg_limit;
     FusedArgs g = a;
     if (we > wb) {
-      g.gbeg = wb, g.gend = we, g.ctr_line = line;
+      g.gbeg = wb, g.gend = we, g.ctr_line = line, g.cbase = bases[line];
       const dim3 gr((unsigned)std::min<long long>(cus, we - wb)), b(64 * GenShape<64>::WAVES);
       launch_general<64>(g, um, gr, b, s);
+      bases[line] += (unsigned long long)(we - wb) + gr.x;
     }
     if (ne > nb_) {
-      g.gbeg = nb_, g.gend = ne, g.ctr_line = line + 1;
+      g.gbeg = nb_, g.gend = ne, g.ctr_line = line + 1, g.cbase = bases[line + 1];
       const dim3 gr((unsigned)std::min<long long>(cus, ne - nb_)), b(64 * GenShape<16>::WAVES);
       launch_general<16>(g, um, gr, b, s);
+      bases[line + 1] += (unsigned long long)(ne - nb_) + gr.x;
     }
     return hipPeekAtLastError() == hipSuccess ? 0 : 9;
   }
@@ -1840,19 +1825,20 @@ int k_fused(const FusedArgs &a, int which, void *stream) {
   const long long total = anylean ? (long long)(a.lx1 - a.lx0 + 1) * (a.ly1 - a.ly0 + 1) * nlch
                                   : 0;
   if (total == 0) return 0;
-  // 8 lean queue counters, one per 128-byte line
-  if (hipMemsetAsync(a.ctr, 0, 8 * 16 * sizeof(unsigned long long), s) != hipSuccess) return 1;
   long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
   if (a.wg_limit > 0 && nb > a.wg_limit) nb = a.wg_limit;
   if (nb > total) nb = total;
   dim3 grd((unsigned)nb), blk(1024);
   const bool d2 = a.dist == 2;
+  FusedArgs l = a;
+  l.cbase = bases[0];
+  bases[0] += (unsigned long long)total + nb;
 #define MNL_LAUNCH_FUSED(U)                                   \
   do {                                                        \
     if (d2)                                                   \
-      fused_kernel<U, 2><<<grd, blk, 0, s>>>(a);              \
+      fused_kernel<U, 2><<<grd, blk, 0, s>>>(l);              \
     else                                                      \
-      fused_kernel<U, 1><<<grd, blk, 0, s>>>(a);              \
+      fused_kernel<U, 1><<<grd, blk, 0, s>>>(l);              \
   } while (0)
   if (um == 2)
     MNL_LAUNCH_FUSED(2);
