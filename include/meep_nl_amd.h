@@ -168,6 +168,25 @@ int mnl_fields_set_profiling(mnl_fields *f, int on);
 int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch);
 
+/* ---- DFT flux (src/dft.cpp; meep.hpp dft_flux) --------------------------
+ * fields::add_dft_flux (src/dft.cpp:578-640) for a volume_list: regions =
+ * nreg x {min x,y,z, max x,y,z, direction (0..2), weight}, nfreq frequencies
+ * (not angular), decimation 0 = the reference's automatic choice
+ * (src/dft.cpp:195-216).  The DFT is accumulated on the device after every
+ * decimated step (fields::update_dfts, src/dft.cpp:249-263); *handle gets the
+ * flux object's index. */
+int mnl_fields_add_dft_flux(mnl_fields *f, int nreg, const double *regions, const double *freqs,
+                            int nfreq, int decimation, int *handle);
+/* dft_flux::flux (src/dft.cpp:533-547), summed over ranks: out[nfreq]. */
+int mnl_fields_dft_flux(mnl_fields *f, int handle, double *out);
+/* Complex DFT values per list (which 0: E, 1: H), list order (next_in_dft),
+ * point-major then frequency, re/im interleaved: *n = points * nfreq. */
+int mnl_fields_dft_size(mnl_fields *f, int handle, long long *n);
+/* out[2 * n]; points another rank owns read 0 (sum over ranks to assemble). */
+int mnl_fields_dft_data(mnl_fields *f, int handle, int which, double *out, long long n);
+/* the decimation factor the object was created with */
+int mnl_fields_dft_decimation(mnl_fields *f, int handle, int *decimation);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,8 +6,9 @@ Both call libmnl.so (HIP kernels for gfx950 + C-ABI, include/meep_nl_amd.h).
 """
 from .core import (Bx, By, Bz, Dx, Dy, Dz, Ex, Ey, Ez, Fields, GridVolume, Hx, Hy, Hz,
                    Structure, X, Y, Z, device_count)
-from .simulation import (ALL, Block, ContinuousSource, DrudeSusceptibility, GaussianSource,
-                         High, LorentzianSusceptibility, Low, Medium, PML, Simulation, Source,
-                         Vector3, Volume, air, inf, vacuum)
+from .simulation import (ALL, AUTOMATIC, Block, ContinuousSource, DftFlux, DrudeSusceptibility,
+                         FluxRegion, GaussianSource, High, LorentzianSusceptibility, Low, Medium,
+                         PML, Simulation, Source, Vector3, Volume, air, get_flux_freqs,
+                         get_fluxes, inf, vacuum)
 
 __version__ = "0.1.0"

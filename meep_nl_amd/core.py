@@ -277,6 +277,41 @@ class Fields:
         return b.value, c.value
 
 
+    # -- DFT flux (fields::add_dft_flux, src/dft.cpp:578-640; dft_flux, src/dft.cpp:482-547)
+    def add_dft_flux(self, regions, freqs, decimation=0):
+        """regions: [(min xyz, max xyz, direction, weight)]; returns a handle.
+        The DFT is accumulated on the GPU after every decimated step."""
+        r = np.ascontiguousarray([list(lo) + list(hi) + [d, w] for lo, hi, d, w in regions],
+                                 dtype=np.float64).ravel()
+        f = np.ascontiguousarray(freqs, dtype=np.float64)
+        h = ctypes.c_int()
+        check(lib().mnl_fields_add_dft_flux(self.h, len(regions), ptr(r), ptr(f), len(f),
+                                            int(decimation), ctypes.byref(h)))
+        self._dft_nf = getattr(self, "_dft_nf", {})
+        self._dft_nf[h.value] = len(f)
+        return h.value
+
+    def flux(self, h):
+        """dft_flux::flux (src/dft.cpp:533-547), summed over ranks."""
+        out = np.zeros(self._dft_nf[h], dtype=np.float64)
+        check(lib().mnl_fields_dft_flux(self.h, h, ptr(out)))
+        return out
+
+    def dft_data(self, h, which):
+        """DFT values of the E (0) or H (1) chunk list, list order (complex); points
+        another rank owns read 0."""
+        n = ctypes.c_longlong()
+        check(lib().mnl_fields_dft_size(self.h, h, ctypes.byref(n)))
+        out = np.zeros(2 * n.value, dtype=np.float64)
+        check(lib().mnl_fields_dft_data(self.h, h, int(which), ptr(out), n.value))
+        return out[0::2] + 1j * out[1::2]
+
+    def dft_decimation(self, h):
+        v = ctypes.c_int()
+        check(lib().mnl_fields_dft_decimation(self.h, h, ctypes.byref(v)))
+        return v.value
+
+
 class LocalHub:
     """In-process slab group (mnl_local_hub_create): several z-slabs of one grid on
     one GPU, stepped by one host thread each."""

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <complex>
 #include <cstdio>
@@ -143,6 +144,39 @@ struct mnl_structure {
   }
 };
 
+// ------------------------------------------------------------- DFT flux
+// fields::add_dft_flux / add_dft / update_dfts / dft_flux::flux (src/dft.cpp:
+// 51-300, 533-547, 578-640; loop_in_chunks src/loop_in_chunks.cpp:225-520),
+// Cartesian, no symmetry, centered grid.  The point set, interpolation weights
+// and list order are those of the reference's single-process chunk layout
+// (PML regions broken off, structure.cpp:118-137), so every per-point DFT is
+// bitwise the reference's; each rank accumulates the points it owns on the
+// device, and flux() sums the pairs in list order on the host.
+struct DftChunkH {
+  int c;
+  cplx scale;
+  int avgmode;       // 0: point, 1: two Yee points, 2: four
+  size_t N, p0;      // points, first point in the flux object's point arrays
+};
+struct DftFluxH {
+  std::vector<double> omega;
+  int nfreq = 0, decim = 1;
+  std::vector<DftChunkH> E, H;        // list order (next_in_dft)
+  size_t npts = 0;                    // E points, then H points
+  std::vector<int> h_pj;              // 3 local indices per point (-1: not this rank's)
+  int *d_pj = nullptr, *d_pch = nullptr;
+  double *d_pw = nullptr;             // w * 0.25 / 0.5 / 1 per point
+  DftChunkDev *d_ch = nullptr;        // per chunk (E list, then H list)
+  double *d_dft = nullptr;            // npts * nfreq complex (re, im)
+  double *d_ph = nullptr;             // phases of one batch: [update][chunk][freq] complex
+  size_t ph_cap = 0;
+  int row = 0;                        // next phase row of this batch
+  ~DftFluxH() {
+    if (d_ph) (void)hipFree(d_ph);
+  }
+};
+
+
 // =============================================================== fields
 struct mnl_fields {
   mnl_structure S;  // copy of the global structure description
@@ -219,6 +253,7 @@ struct mnl_fields {
   unsigned long long *d_nr_fallbacks = nullptr;
   double *d_scratch = nullptr;  // canonical-size staging buffer
   size_t scratch_cap = 0;
+  std::vector<std::unique_ptr<DftFluxH>> dfts;  // DFT flux objects (add_dft_flux order)
 
   ~mnl_fields() {
     if (device >= 0) hipSetDevice(device);
@@ -987,6 +1022,357 @@ int build_source_lists(mnl_fields *F) {
 // ------------------------------------------------------------- interpolation
 inline int my_round(double x) { return int(floor(fabs(x) + 0.5) * (x < 0 ? -1 : 1)); }
 
+// compute_boundary_weights (src/loop_in_chunks.cpp:257-300), snap_empty_dimensions = false
+void dft_boundary_weights(const mnl_structure &S, const double wmin[3], const double wmax[3],
+                          const int is[3], const int ie[3], double s0[3], double e0[3],
+                          double s1[3], double e1[3]) {
+  for (int d = 0; d < 3; d++) {
+    s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
+    if (!S.has[d]) continue;
+    double w0 = 1. - wmin[d] * S.a + 0.5 * is[d];
+    double w1 = 1. + wmax[d] * S.a - 0.5 * ie[d];
+    if (ie[d] >= is[d] + 3 * 2) {
+      s0[d] = w0 * w0 / 2;
+      s1[d] = 1 - (1 - w0) * (1 - w0) / 2;
+      e0[d] = w1 * w1 / 2;
+      e1[d] = 1 - (1 - w1) * (1 - w1) / 2;
+    } else if (ie[d] == is[d] + 2 * 2) {
+      s0[d] = w0 * w0 / 2;
+      s1[d] = 1 - (1 - w0) * (1 - w0) / 2 - (1 - w1) * (1 - w1) / 2;
+      e0[d] = w1 * w1 / 2;
+      e1[d] = s1[d];
+    } else if (wmin[d] == wmax[d]) {
+      s0[d] = w0;
+      s1[d] = w1;
+      e0[d] = w1;
+      e1[d] = w0;
+    } else if (ie[d] == is[d] + 1 * 2) {
+      s0[d] = w0 * w0 / 2 - (1 - w1) * (1 - w1) / 2;
+      e0[d] = w1 * w1 / 2 - (1 - w0) * (1 - w0) / 2;
+      s1[d] = e0[d];
+      e1[d] = s0[d];
+    }
+  }
+}
+
+// the reference's chunks in creation order: x zones outer, then y, then z
+// (absolute little corner io and cell counts n per direction)
+std::vector<std::array<int, 6>> reference_chunks(const mnl_structure &S) {
+  std::vector<std::pair<int, int>> iv[3];
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) {
+      iv[d].push_back({0, 0});
+      continue;
+    }
+    for (auto &z : zone_intervals(S, d)) iv[d].push_back({S.io[d] + z.c0, (z.c1 - z.c0) / 2});
+  }
+  std::vector<std::array<int, 6>> out;
+  for (auto &ix : iv[0])
+    for (auto &iy : iv[1])
+      for (auto &iz : iv[2]) out.push_back({ix.first, iy.first, iz.first, ix.second, iy.second, iz.second});
+  return out;
+}
+
+// fields::add_dft for component c over [wmin, wmax] on the centered grid: the
+// chunks loop_in_chunks creates, prepended to `list` (their points appended to
+// the flux object's point arrays)
+void dft_add(mnl_fields *F, DftFluxH &o, int c, const double wmin[3], const double wmax[3],
+             bool incl, cplx stored_weight, double dt_factor, std::vector<DftChunkH> &list,
+             std::vector<double> &pw) {
+  const mnl_structure &S = F->S;
+  const DevGrid &g = F->g;
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    is[d] = 1 + 2 * int(floor(wmin[d] * S.a - .5));  // vec2diel_floor / ceil, equal_shift 0
+    ie[d] = 1 + 2 * int(ceil(wmax[d] * S.a - .5));
+  }
+  double s0[3], s1[3], e0[3], e1[3];
+  dft_boundary_weights(S, wmin, wmax, is, ie, s0, e0, s1, e1);
+  double dV0 = 1.0;
+  for (int d = 0; d < 3; d++)
+    if (S.has[d] && wmax[d] - wmin[d] > 0.0) dV0 *= 1.0 / S.a;
+  if (!F->allocated[c]) return;
+  int yd[3];  // yucky loop directions (3D: X,Y,Z; 2D: Z,X,Y; 1D: X,Y,Z)
+  if (S.dim == 2)
+    yd[0] = 2, yd[1] = 0, yd[2] = 1;
+  else
+    yd[0] = 0, yd[1] = 1, yd[2] = 2;
+  std::vector<DftChunkH> made;
+  for (auto &ch : reference_chunks(S)) {
+    int isc[3], iec[3];
+    double s0c[3], s1c[3], e0c[3], e1c[3];
+    bool emp = false;
+    for (int d = 0; d < 3; d++) {
+      s0c[d] = s1c[d] = e0c[d] = e1c[d] = 1.0;
+      if (!S.has[d]) {
+        isc[d] = iec[d] = 0;
+        continue;
+      }
+      const int uoc = S.io[d] + 1, coc = ch[d] + 1, cbo = ch[d] + 2 * ch[3 + d] - 1;
+      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
+      isc[d] = std::max(is[d], iscoS);
+      iec[d] = std::min(ie[d], iecoS);
+      if (isc[d] > iec[d]) emp = true;
+    }
+    if (emp) continue;
+    for (int d = 0; d < 3; d++) {
+      if (!S.has[d]) continue;
+      if (isc[d] == is[d]) {
+        s0c[d] = s0[d];
+        s1c[d] = s1[d];
+      } else if (isc[d] == is[d] + 2) {
+        s0c[d] = s1[d];
+      }
+      if (iec[d] == ie[d]) {
+        e0c[d] = e0[d];
+        e1c[d] = e1[d];
+      } else if (iec[d] == ie[d] - 2) {
+        e0c[d] = e1[d];
+      }
+      if (iec[d] == isc[d]) {
+        double w = std::min(s0c[d], e0c[d]);
+        s0c[d] = e0c[d] = s1c[d] = e1c[d] = w;
+      } else if (iec[d] == isc[d] + 2) {
+        double w = std::min(s0c[d], e1c[d]);
+        s0c[d] = w, e1c[d] = w;
+        w = std::min(s1c[d], e0c[d]);
+        s1c[d] = w, e0c[d] = w;
+      } else if (iec[d] == isc[d] + 4) {
+        double w = std::min(s1c[d], e1c[d]);
+        s1c[d] = w, e1c[d] = w;
+      }
+    }
+    DftChunkH dc;
+    dc.c = c;
+    dc.scale = stored_weight * cplx(1.0) * dt_factor;
+    int nun = 0;
+    for (int d = 0; d < 3; d++)
+      if (S.has[d] && !S.shift(c, d)) nun++;
+    dc.avgmode = nun;
+    long ln[3];
+    for (int k = 0; k < 3; k++) ln[k] = S.has[yd[k]] ? (iec[yd[k]] - isc[yd[k]]) / 2 + 1 : 1;
+    dc.N = size_t(ln[0] * ln[1] * ln[2]);
+    dc.p0 = 0;  // set when the lists are laid out
+    auto W1 = [&](int k, long i) -> double {
+      const int d = yd[k];
+      const long n = ln[k];
+      if (i > 1 && i < n - 2) return 1.0;
+      if (i == 0) return s0c[d];
+      if (i == 1) return s1c[d];
+      if (i == n - 1) return e0c[d];
+      if (i == n - 2) return e1c[d];
+      return 1.0;
+    };
+    const double fac = nun == 2 ? 0.25 : (nun == 1 ? 0.5 : 1.0);
+    // points in IVEC_LOOP_COUNTER order; local indices of the Yee base point
+    std::vector<int> pj;
+    std::vector<double> w;
+    for (long i1 = 0; i1 < ln[0]; i1++)
+      for (long i2 = 0; i2 < ln[1]; i2++)
+        for (long i3 = 0; i3 < ln[2]; i3++) {
+          const long ii[3] = {i1, i2, i3};
+          int p[3] = {0, 0, 0};  // centered point, absolute half-coords
+          for (int k = 0; k < 3; k++)
+            if (S.has[yd[k]]) p[yd[k]] = isc[yd[k]] + 2 * int(ii[k]);
+          double wt = incl ? (W1(2, i3) * (W1(1, i2) * ((dV0 + 0.0 * i2) * W1(0, i1)))) : 1.0;
+          w.push_back(wt * fac);
+          // this rank owns the centered point if its slab index is in the owned range
+          int j[3] = {0, 0, 0};
+          bool mine = true;
+          for (int d = 0; d < 3; d++) {
+            if (!S.has[d]) continue;
+            const int base = p[d] - (S.shift(c, d) ? 0 : 1);  // Yee point of c at/below p
+            j[d] = (base - S.io[d] - S.shift(c, d)) / 2 - g.off[d];
+            const int jc = (p[d] - S.io[d] - 1) / 2 - g.off[d];  // centered index
+            if (jc < g.owned_lo_sh[d] || jc > g.owned_hi_sh[d]) mine = false;
+          }
+          for (int d = 0; d < 3; d++) pj.push_back(mine ? j[d] : -1);
+        }
+    dc.p0 = o.h_pj.size() / 3;
+    o.h_pj.insert(o.h_pj.end(), pj.begin(), pj.end());
+    pw.insert(pw.end(), w.begin(), w.end());
+    made.push_back(dc);
+  }
+  for (auto &m : made) list.insert(list.begin(), m);
+}
+
+int dft_add_flux(mnl_fields *F, int nreg, const double *regions, const double *freqs, int nfreq,
+                 int decimation) {
+  if (F->src_dirty && build_source_lists(F)) return -1;
+  if (nreg < 1 || nfreq < 1) return fail("add_dft_flux: no regions / frequencies");
+  std::unique_ptr<DftFluxH> o(new DftFluxH);
+  o->nfreq = nfreq;
+  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
+  int decim = decimation;
+  if (decim == 0) {  // fields::add_dft (src/dft.cpp:190-213)
+    double src_freq_max = 0;
+    for (auto &st : F->srcs) {
+      const double fw = st.kind == 0 ? sqrt(-2.0 * log(1e-7)) / (st.width * pi) : 0.0;
+      if (fw == 0)
+        decim = 1;
+      else
+        src_freq_max =
+            std::max(src_freq_max, std::abs(st.kind == 0 ? st.freq : st.cfreq.real()) + 0.5 * fw);
+    }
+    double freq_max = 0;
+    for (int i = 0; i < nfreq; ++i) freq_max = std::max(freq_max, std::abs(freqs[i]));
+    bool nonlinear = false;  // structure_chunk::has_nonlinearities: nonzero chi2/chi3
+    for (int c = 0; c < 3; c++) {
+      for (double v : F->S.chi2[c]) nonlinear = nonlinear || v != 0.0;
+      for (double v : F->S.chi3[c]) nonlinear = nonlinear || v != 0.0;
+    }
+    for (auto &b : F->S.boxes) nonlinear = nonlinear || ((b.kind == 1 || b.kind == 2) && b.value != 0.0);
+    // (src/dft.cpp:207-210 overwrites the fwidth == 0 case above)
+    if ((freq_max > 0) && (src_freq_max > 0) && !nonlinear)
+      decim = std::max(1, int(std::floor(1 / (F->dt * (freq_max + src_freq_max)))));
+    else
+      decim = 1;
+  }
+  o->decim = decim;
+  const double dt_factor = F->dt / sqrt(2.0 * pi) * decim;
+  std::vector<double> pwE, pwH;
+  DftFluxH ho;  // H points collected separately, appended after the E points
+  for (int r = 0; r < nreg; r++) {
+    const double *R = regions + 8 * r;
+    const int d = int(R[6]);
+    const double wgt = R[7];
+    int cE[2], cH[2];
+    switch (d) {  // fields::add_dft_flux (src/dft.cpp:601-617)
+      case 0: cE[0] = MNL_EY, cE[1] = MNL_EZ, cH[0] = MNL_HZ, cH[1] = MNL_HY; break;
+      case 1: cE[0] = MNL_EZ, cE[1] = MNL_EX, cH[0] = MNL_HX, cH[1] = MNL_HZ; break;
+      default: cE[0] = MNL_EX, cE[1] = MNL_EY, cH[0] = MNL_HY, cH[1] = MNL_HX; break;
+    }
+    for (int i = 0; i < 2; ++i) {
+      dft_add(F, *o, cE[i], R, R + 3, true, cplx(wgt * double(1 - 2 * i)), dt_factor, o->E, pwE);
+      dft_add(F, ho, cH[i], R, R + 3, false, cplx(1.0), dt_factor, o->H, pwH);
+    }
+  }
+  // lay out: E points (creation order), then H points; chunks keep their p0
+  const size_t nE = o->h_pj.size() / 3;
+  for (auto &h : o->H) h.p0 += nE;
+  o->h_pj.insert(o->h_pj.end(), ho.h_pj.begin(), ho.h_pj.end());
+  pwE.insert(pwE.end(), pwH.begin(), pwH.end());
+  o->npts = o->h_pj.size() / 3;
+  // per-point chunk id: chunks numbered E list then H list
+  std::vector<int> pch(o->npts, 0);
+  std::vector<DftChunkDev> chd;
+  auto lay = [&](const std::vector<DftChunkH> &L) {
+    for (auto &dc : L) {
+      DftChunkDev cd;
+      cd.c = dc.c;
+      cd.avgmode = dc.avgmode;
+      cd.d1 = cd.d2 = -1;  // grid_volume::yee2cent_offsets order (X, Y, Z)
+      for (int dd = 0; dd < 3; dd++)
+        if (F->S.has[dd] && !F->S.shift(dc.c, dd)) (cd.d1 < 0 ? cd.d1 : cd.d2) = dd;
+      for (size_t k = 0; k < dc.N; k++) pch[dc.p0 + k] = (int)chd.size();
+      chd.push_back(cd);
+    }
+  };
+  lay(o->E);
+  lay(o->H);
+  if (o->npts) {
+    if (dev_alloc(F, &o->d_pj, o->h_pj.size(), false) || dev_alloc(F, &o->d_pch, o->npts, false) ||
+        dev_alloc(F, &o->d_pw, o->npts, false) || dev_alloc(F, &o->d_ch, chd.size(), false) ||
+        dev_alloc(F, &o->d_dft, 2 * o->npts * (size_t)nfreq))
+      return -1;
+    HIPCHK(hipMemcpyAsync(o->d_pj, o->h_pj.data(), o->h_pj.size() * 4, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(o->d_pch, pch.data(), pch.size() * 4, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(o->d_pw, pwE.data(), pwE.size() * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(o->d_ch, chd.data(), chd.size() * sizeof(DftChunkDev), hipMemcpyHostToDevice,
+                          F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+  }
+  F->dfts.push_back(std::move(o));
+  return int(F->dfts.size()) - 1;
+}
+
+// phases of every DFT update in steps [t0+1, t0+ns] -> device (one row per update)
+int dft_prepare(mnl_fields *F, long long t0, int ns) {
+  for (auto &op : F->dfts) {
+    DftFluxH &o = *op;
+    o.row = 0;
+    const size_t nch = o.E.size() + o.H.size();
+    std::vector<double> ph;
+    for (int s = 0; s < ns; s++) {
+      const long long t = t0 + s + 1;
+      if (t % o.decim) continue;
+      const double tE = t * F->dt, tH = tE - 0.5 * F->dt;  // fields::update_dfts
+      auto add = [&](const std::vector<DftChunkH> &L) {
+        for (auto &dc : L) {
+          const double tm = ctype(dc.c) == T_H ? tH : tE;
+          for (int i = 0; i < o.nfreq; i++) {
+            const cplx p = std::polar(1.0, o.omega[i] * tm) * dc.scale;
+            ph.push_back(p.real());
+            ph.push_back(p.imag());
+          }
+        }
+      };
+      add(o.E);
+      add(o.H);
+    }
+    if (ph.empty()) continue;
+    if (o.ph_cap < ph.size()) {
+      HIPCHK(hipStreamSynchronize(F->stream));
+      if (o.d_ph) hipFree(o.d_ph);
+      HIPCHK(hipMalloc(&o.d_ph, ph.size() * 8));
+      o.ph_cap = ph.size();
+    }
+    (void)nch;
+    HIPCHK(hipMemcpyAsync(o.d_ph, ph.data(), ph.size() * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+  }
+  return 0;
+}
+
+// after step t (fields::update_dfts, src/dft.cpp:249-263)
+int dft_update(mnl_fields *F, long long t) {
+  for (auto &op : F->dfts) {
+    DftFluxH &o = *op;
+    if (t % o.decim || !o.npts) continue;
+    const size_t nch = o.E.size() + o.H.size();
+    if (k_dft_update(o.d_pj, o.d_pw, o.d_pch, o.d_ch, o.d_dft,
+                     o.d_ph + 2 * (size_t)o.row * nch * o.nfreq, o.nfreq, (long long)o.npts, F->g,
+                     F->f, F->stream))
+      return fail("dft update launch failed");
+    o.row++;
+  }
+  return 0;
+}
+
+bool dft_due(const mnl_fields *F, long long t) {
+  for (auto &op : F->dfts)
+    if (op->npts && t % op->decim == 0) return true;
+  return false;
+}
+
+int dft_flux_values(mnl_fields *F, int h, double *out) {
+  if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
+  DftFluxH &o = *F->dfts[h];
+  const size_t nf = o.nfreq;
+  std::vector<double> v(2 * o.npts * nf);
+  if (!v.empty()) {
+    HIPCHK(hipMemcpyAsync(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost, F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+  }
+  for (size_t i = 0; i < nf; ++i) out[i] = 0;
+  for (size_t k = 0; k < o.E.size() && k < o.H.size(); k++)  // dft_flux::flux (src/dft.cpp:533-547)
+    for (size_t p = 0; p < o.E[k].N; ++p) {
+      const size_t pe = o.E[k].p0 + p, ph = o.H[k].p0 + p;
+      if (o.h_pj[3 * pe] < 0 && o.h_pj[3 * pe + 1] < 0 && o.h_pj[3 * pe + 2] < 0) continue;
+      for (size_t i = 0; i < nf; ++i) {
+        const cplx e(v[2 * (pe * nf + i)], v[2 * (pe * nf + i) + 1]);
+        const cplx hv(v[2 * (ph * nf + i)], v[2 * (ph * nf + i) + 1]);
+        out[i] += real(e * conj(hv));
+      }
+    }
+  if (F->nranks > 1)
+    for (size_t i0 = 0; i0 < nf; i0 += 64)
+      if (F->comm->allreduce_sum(out + i0, (int)std::min<size_t>(64, nf - i0), F->stream))
+        return fail("flux allreduce failed");
+  return 0;
+}
+
 void interpolate(const mnl_structure &S, int c, const double pc[3], int locs[8][3], double w[8]) {
   const double SMALL = 1e-13;
   double p[3] = {0, 0, 0}, midv[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
@@ -1118,6 +1504,8 @@ int get_field(mnl_fields *F, int c, const double pos[3], double *out, bool reduc
 // kind 1 (before curl D): B (and separate H) comps shifted along the slab axis
 //   need the high ghost plane (local nloc) <- rank+1's first plane (local 0).
 // kind 2 (before NR E update): D comps (and Lorentz P), both directions.
+// kind 3 (before a DFT update): H comps unshifted along the slab axis need the
+//   low ghost plane, which the centred-grid average reads (src/dft.cpp:281-287).
 int exchange(mnl_fields *F, int kind, hipStream_t st = nullptr) {
   if (!st) st = F->stream;
   const DevGrid &g = F->g;
@@ -1138,6 +1526,11 @@ int exchange(mnl_fields *F, int kind, hipStream_t st = nullptr) {
       if (c != sd && F->f.Bn[c] && F->allocated[3 * T_H + c]) {
         items.push_back({F->f.Bn[c], false});
         if (F->f.H[c]) items.push_back({F->f.Hn[c], false});
+      }
+    } else if (kind == 3) {  // DFT: H comps unshifted along the slab axis, low ghost
+      if (c == sd && F->allocated[3 * T_H + c]) {
+        items.push_back({F->f.B[c], true});
+        if (F->f.H[c]) items.push_back({F->f.H[c], true});
       }
     } else {
       if (F->f.Dn[c] && F->allocated[3 * T_D + c]) items.push_back({F->f.Dn[c], c != sd});
@@ -1490,7 +1883,7 @@ int build_palette(mnl_fields *F) {
     int k = 0;
     for (uint64_t u : cand) memcpy(&tab[256 * c + k++], &u, 8);  // ascending bit patterns
   }
-  unsigned *uidx;
+  unsigned *uidx = nullptr;
   double *utab;
   int *bad;
   if (dev_alloc(F, &uidx, F->nlocal) || dev_alloc(F, &utab, 3 * 256) || dev_alloc(F, &bad, 1))
@@ -1749,8 +2142,23 @@ int step_batch(mnl_fields *F, int nsteps) {
     evi = 0;
     return 0;
   };
+  // fields::update_dfts after t += 1 (src/step.cpp:125-127); a rank's averages
+  // read its low ghost planes, which must hold this step's values first
+  auto post_step = [&](int s) -> int {
+    const long long tn = F->t + s + 1;
+    if (!dft_due(F, tn)) return 0;
+    if (F->nranks > 1) {
+      if (F->fused)
+        HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
+      else if (exchange(F, 0))
+        return fail("E halo exchange failed");
+      if (exchange(F, 3)) return fail("DFT halo exchange failed");
+    }
+    return dft_update(F, tn);
+  };
   for (int s0 = 0; s0 < nsteps; s0 += CH) {
     int ns = std::min(CH, nsteps - s0);
+    if (!F->dfts.empty() && dft_prepare(F, F->t, ns)) return -1;
     if (per) {
       std::vector<double> vals((size_t)ns * per);
       for (int s = 0; s < ns; s++) {
@@ -1801,7 +2209,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       sD.val = F->d_vals + (size_t)s * per + nB;
       is.val = F->d_vals + (size_t)s * per + nB + nD;
       if (F->fused && F->nranks > 1) {
-        if (step_fused_multi(F, sD, ev_begin, ev_end)) return -1;
+        if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
         continue;
       }
       // ---- B: halo of E (low ghost), curl, sources
@@ -1902,6 +2310,7 @@ int step_batch(mnl_fields *F, int nsteps) {
           std::swap(f.H[d], f.Hn[d]);
           std::swap(f.UB[d], f.UBn[d]);
         }
+      if (post_step(s)) return -1;
     }
     F->t += ns;
     if (flush_events() != 0) return -1;
@@ -2392,6 +2801,62 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
 int mnl_fields_mode(mnl_fields *F, int *fused) {
   if (!F) return fail("null fields");
   *fused = (F->fused ? 1 : 0) | (F->fused && F->d_uidx ? 2 : 0);
+  return 0;
+}
+
+int mnl_fields_add_dft_flux(mnl_fields *F, int nreg, const double *regions, const double *freqs,
+                            int nfreq, int decimation, int *handle) {
+  if (!F || !regions || !freqs || !handle) return fail("null argument");
+  if (decimation < 0) return fail("decimation must be >= 0");
+  for (int r = 0; r < nreg; r++)
+    if (regions[8 * r + 6] < 0 || regions[8 * r + 6] > 2) return fail("bad flux direction");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  const int h = dft_add_flux(F, nreg, regions, freqs, nfreq, decimation);
+  if (h < 0) return -1;
+  *handle = h;
+  return 0;
+}
+
+int mnl_fields_dft_flux(mnl_fields *F, int h, double *out) {
+  if (!F || !out) return fail("null argument");
+  return dft_flux_values(F, h, out);
+}
+
+int mnl_fields_dft_size(mnl_fields *F, int h, long long *n) {
+  if (!F || !n) return fail("null argument");
+  if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
+  const DftFluxH &o = *F->dfts[h];
+  long long k = 0;
+  for (auto &dc : o.E) k += (long long)dc.N;
+  *n = k * o.nfreq;
+  return 0;
+}
+
+int mnl_fields_dft_data(mnl_fields *F, int h, int which, double *out, long long n) {
+  if (!F || !out) return fail("null argument");
+  if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
+  const DftFluxH &o = *F->dfts[h];
+  const size_t nf = o.nfreq;
+  std::vector<double> v(2 * o.npts * nf);
+  if (!v.empty()) {
+    HIPCHK(hipStreamSynchronize(F->stream));
+    HIPCHK(hipMemcpy(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost));
+  }
+  long long k = 0;
+  for (auto &dc : which ? o.H : o.E)
+    for (size_t p = 0; p < dc.N; p++)
+      for (size_t i = 0; i < nf; i++) {
+        if (k + 2 > 2 * n) return fail("dft buffer too small");
+        out[k++] = v[2 * ((dc.p0 + p) * nf + i)];
+        out[k++] = v[2 * ((dc.p0 + p) * nf + i) + 1];
+      }
+  return 0;
+}
+
+int mnl_fields_dft_decimation(mnl_fields *F, int h, int *decimation) {
+  if (!F || !decimation) return fail("null argument");
+  if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
+  *decimation = F->dfts[h]->decim;
   return 0;
 }
 

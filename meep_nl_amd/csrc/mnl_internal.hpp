@@ -121,6 +121,15 @@ struct ISrcDev {             // integrated sources, read by the E kernel
   const double *val;         // [step][n] dipole value real(amp*dipole(t+dt))
 };
 
+// One DFT chunk (dft_chunk, src/dft.cpp:51-128) as the update kernel sees it:
+// component, how many Yee points are averaged onto the cell centre and along
+// which directions (grid_volume::yee2cent_offsets, src/vec.cpp:333-344).
+struct DftChunkDev {
+  int c;        // MNL component (E or H)
+  int avgmode;  // 0, 1 (d1) or 2 (d1, d2)
+  int d1, d2;
+};
+
 // Host-side launchers implemented in mnl_kernels.hip.
 struct Launch {
   void *stream;  // hipStream_t
@@ -218,6 +227,10 @@ int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, co
 // E = chi1inv * D over box F (leaving fused mode / readout)
 int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *stream);
 int k_fill(double *p, double v, size_t n, void *stream);
+// dft_chunk::update_dft for every point of one flux object (src/dft.cpp:265-300)
+int k_dft_update(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch,
+                 double *dft, const double *ph, int nfreq, long long npts, const DevGrid &g,
+                 const DevFields &f, void *stream);
 int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_type,
                      int comp_dir, int zlo_glob, void *stream);
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,

@@ -872,7 +872,7 @@ struct ItemGeo {
 struct TabE {
   double kms, si, kps;
 };
-constexpr int TPX = FX + 2, TPZ = FUSED_MAXCH + 2;
+constexpr int TPZ = FUSED_MAXCH + 2;
 
 // curl update with the per-point branch selection of step_curl
 // (src/step_generic.cpp:84-252), written branch-free: outside a PML chunk
@@ -1875,6 +1875,71 @@ __global__ void materialize_e_kernel(Box b, DevGrid g, DevFields f) {
 int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *stream) {
   if (empty(F)) return 0;
   materialize_e_kernel<<<grid_for(F), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(F, g, f);
+  return rc();
+}
+
+// ----------------------------------------------------------------- DFT
+// dft_chunk::update_dft (src/dft.cpp:265-300): thread = (point, frequency).
+// The field is averaged from the Yee points onto the cell centre exactly as
+// the reference does, (w*0.25)*(((f0 + f1) + f2) + f3); in fused mode E is
+// read through the implicit-E rule.
+__global__ void dft_update_kernel(const int *pj, const double *pw, const int *pch,
+                                  const DftChunkDev *ch, double *dft, const double *ph, int nfreq,
+                                  long long npts, DevGrid g, DevFields f) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= npts * nfreq) return;
+  const long long p = t / nfreq;
+  const int i = (int)(t - p * nfreq);
+  if (pj[3 * p] < 0) return;  // another rank's point
+  const int k = pch[p];
+  const DftChunkDev cd = ch[k];
+  const int c = cd.c, d = c % 3;
+  const bool mag = c >= 3;
+  Pt P;
+  P.idx = 0;
+  for (int e = 0; e < 3; e++) {
+    P.j[e] = pj[3 * p + e];
+    P.idx += (long long)P.j[e] * g.sdir[e];
+  }
+  auto val = [&](const Pt &q) -> double {
+    if (mag) {
+      const bool sep = f.H[d] && pml_at(f, g, d, qcoord(g, q, T_H, d, d));
+      return sep ? f.H[d][q.idx] : f.B[d][q.idx];
+    }
+    if (e_implicit(f, g, d, q)) {
+      const double dv = f.D[d][q.idx];
+      return f.inveps[d] ? dv * f.inveps[d][q.idx] : dv;
+    }
+    return f.E[d][q.idx];
+  };
+  auto nb = [&](const Pt &q, int e) {
+    Pt r = q;
+    r.j[e] += 1;
+    r.idx += g.sdir[e];
+    return r;
+  };
+  double fr;
+  if (cd.avgmode == 2) {
+    const Pt q1 = nb(P, cd.d1), q2 = nb(P, cd.d2), q3 = nb(q1, cd.d2);
+    fr = pw[p] * (val(P) + val(q1) + val(q2) + val(q3));
+  } else if (cd.avgmode == 1) {
+    fr = pw[p] * (val(P) + val(nb(P, cd.d1)));
+  } else {
+    fr = pw[p] * val(P);
+  }
+  const double pr = ph[2 * ((long long)k * nfreq + i)], pim = ph[2 * ((long long)k * nfreq + i) + 1];
+  double *dd = dft + 2 * (p * nfreq + i);
+  dd[0] = dd[0] + fr * pr;
+  dd[1] = dd[1] + fr * pim;
+}
+
+int k_dft_update(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch,
+                 double *dft, const double *ph, int nfreq, long long npts, const DevGrid &g,
+                 const DevFields &f, void *stream) {
+  const long long n = npts * nfreq;
+  if (n <= 0) return 0;
+  dft_update_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      pj, pw, pch, ch, dft, ph, nfreq, npts, g, f);
   return rc();
 }
 

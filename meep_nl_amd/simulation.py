@@ -177,6 +177,95 @@ class Source:
                                 self.src.is_integrated)
 
 
+# ---------------------------------------------------------------- flux monitors
+AUTOMATIC = -1
+
+
+def fix_dft_args(args, i):
+    """(fcen, df, nfreq) -> frequency list (python/simulation.py:72-93)."""
+    if (len(args) > i + 2 and isinstance(args[i], (int, float))
+            and isinstance(args[i + 1], (int, float)) and isinstance(args[i + 2], int)):
+        fcen, df, nfreq = args[i], args[i + 1], args[i + 2]
+        freq = [fcen] if nfreq == 1 else np.linspace(fcen - 0.5 * df, fcen + 0.5 * df, nfreq)
+        return args[:i] + (freq,) + args[i + 3:]
+    if not isinstance(args[i], (np.ndarray, list, tuple)):
+        raise TypeError("add_dft functions only accept fcen,df,nfreq (3 numbers) or freq "
+                        "(array/list)")
+    return args
+
+
+class FluxRegion:
+    """python/simulation.py:510-570: a plane/line/point/volume and a flux direction."""
+
+    def __init__(self, center=None, size=Vector3(), direction=AUTOMATIC, weight=1.0,
+                 volume=None):
+        if center is None and volume is None:
+            raise ValueError("Either center or volume required")
+        if volume is not None:
+            center, size = volume.center, volume.size
+        self.center = Vector3(*center)
+        self.size = Vector3(*size)
+        self.direction = direction
+        self.weight = complex(weight)
+
+
+def _normal_direction(dim, size):
+    """volume::normal_direction (src/vec.cpp:227-262) for Cartesian cells."""
+    if dim == 1:
+        return Z
+    if dim == 2:
+        if size.x == 0 and size.y > 0:
+            return X
+        if size.x > 0 and size.y == 0:
+            return Y
+        # fields::normal_direction pads empty dims (src/dft.cpp:791-809): no further case in 2-D
+        raise RuntimeError("Could not determine normal direction for given grid_volume.")
+    zero = [size.x == 0, size.y == 0, size.z == 0]
+    if sum(zero) == 1:
+        return zero.index(True)
+    raise RuntimeError("Could not determine normal direction for given grid_volume.")
+
+
+class DftFlux:
+    """python/simulation.py:687-760 (flux object); the DFT lives on the GPU."""
+
+    def __init__(self, sim, freq, regions, decimation_factor):
+        self.sim = sim
+        self.freq = [float(f) for f in freq]
+        self.regions = list(regions)
+        self.decimation_factor = decimation_factor
+        self.handle = None
+
+    def _create(self):
+        sim = self.sim
+        regs = []
+        for r in self.regions:
+            if r.weight.imag != 0:
+                raise NotImplementedError("complex flux weights are out of scope (real fields)")
+            d = _normal_direction(sim.dimensions, r.size) if r.direction < 0 else r.direction
+            lo = [r.center[k] - 0.5 * r.size[k] for k in range(3)]
+            hi = [r.center[k] + 0.5 * r.size[k] for k in range(3)]
+            if sim.dimensions == 1:  # 1-D cells live on the z axis
+                lo, hi = [0.0, 0.0, lo[2]], [0.0, 0.0, hi[2]]
+            elif sim.dimensions == 2:
+                lo[2] = hi[2] = 0.0
+            regs.append((lo, hi, d, r.weight.real))
+        self.handle = sim.fields.add_dft_flux(regs, self.freq, self.decimation_factor)
+
+    def flux(self):
+        return list(self.sim.fields.flux(self.handle))
+
+
+def get_flux_freqs(f):
+    """python/simulation.py:6014-6019"""
+    return list(f.freq)
+
+
+def get_fluxes(f):
+    """python/simulation.py:6022-6027"""
+    return f.flux()
+
+
 # ---------------------------------------------------------------- distributed
 def _dist_context():
     """(rank, world, local_rank, nccl_id) when launched one process per GPU by
@@ -217,6 +306,7 @@ class Simulation:
         self.parallel = parallel
         self.fields = None
         self.structure = None
+        self.dft_objects = []
 
     # -- structure
     def _create_grid_volume(self):
@@ -352,6 +442,18 @@ class Simulation:
             self.fields.step(1)
         for fn in step_funcs:
             fn(self)
+
+    # -- flux spectra
+    def add_flux(self, *args, **kwargs):
+        """add_flux(fcen, df, nfreq, *FluxRegions) or add_flux(freq, *FluxRegions)
+        (python/simulation.py:3470-3505); initialises the fields first."""
+        args = fix_dft_args(args, 0)
+        freq, regions = args[0], args[1:]
+        flux = DftFlux(self, freq, regions, kwargs.get("decimation_factor", 0))
+        self.init_sim()
+        flux._create()
+        self.dft_objects.append(flux)
+        return flux
 
     # -- monitors
     def get_field_point(self, c, pt):

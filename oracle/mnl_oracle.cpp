@@ -364,6 +364,11 @@ struct Lorentz {
 
 }  // namespace
 
+namespace {
+struct DftFluxObj;
+}
+void update_dfts(orc_sim *s);
+
 struct orc_sim {
   GV gv;  // whole cell (user_volume == gv: no symmetry)
   double courant = 0.5, dt = 0.05;
@@ -394,6 +399,8 @@ struct orc_sim {
   bool conn_valid = false;
   std::vector<NRState> nr;
   long long nr_random = 0;
+  std::vector<std::unique_ptr<DftFluxObj>> dfts;  // add_dft_flux objects
+  ~orc_sim();
 };
 
 namespace {
@@ -1100,6 +1107,7 @@ void step_once(orc_sim *s) {  // fields::step, src/step.cpp:35-140
   step_boundaries_P(s);
   step_boundaries(s, T_E);
   s->t += 1;
+  update_dfts(s);
 }
 
 // ---------------------------------------------------------------- interpolation
@@ -1448,6 +1456,311 @@ int orc_add_point_source(orc_sim *s, int comp, int kind, const double *p, int np
   s->conn_valid = false;
   return 0;
 }
+
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- DFT flux
+// fields::add_dft_flux / add_dft / update_dfts / dft_flux::flux
+// (src/dft.cpp:51-300, 533-547, 578-640; src/loop_in_chunks.cpp:225-300,
+// 339-520) for Cartesian grids without symmetry, centered grid, real fields.
+namespace {
+struct DftChunk {
+  int ci;                  // chunk index
+  int c;                   // component
+  int is[3], ie[3];        // centered-grid corners of this chunk's piece
+  double s0[3], s1[3], e0[3], e1[3];
+  double dV0;
+  bool incl;               // include_dV_and_interp_weights
+  cplx scale;
+  long avg1, avg2;         // yee2cent_offsets in the chunk's strides
+  size_t N;
+  std::vector<cplx> dft;   // N * Nfreq
+};
+struct DftFluxObj {
+  std::vector<double> omega;
+  size_t nfreq = 0;
+  int decim = 1;
+  std::vector<DftChunk> E, H;  // in dft list order (next_in_dft)
+};
+
+// compute_boundary_weights (src/loop_in_chunks.cpp:257-300), snap_empty_dimensions = false
+void boundary_weights(const GV &G, const double wmin[3], const double wmax[3], const int is[3],
+                      const int ie[3], double s0[3], double e0[3], double s1[3], double e1[3]) {
+  for (int d = 0; d < 3; d++) {
+    s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
+    if (!G.has[d]) continue;
+    double w0 = 1. - wmin[d] * G.a + 0.5 * is[d];
+    double w1 = 1. + wmax[d] * G.a - 0.5 * ie[d];
+    if (ie[d] >= is[d] + 3 * 2) {
+      s0[d] = w0 * w0 / 2;
+      s1[d] = 1 - (1 - w0) * (1 - w0) / 2;
+      e0[d] = w1 * w1 / 2;
+      e1[d] = 1 - (1 - w1) * (1 - w1) / 2;
+    } else if (ie[d] == is[d] + 2 * 2) {
+      s0[d] = w0 * w0 / 2;
+      s1[d] = 1 - (1 - w0) * (1 - w0) / 2 - (1 - w1) * (1 - w1) / 2;
+      e0[d] = w1 * w1 / 2;
+      e1[d] = s1[d];
+    } else if (wmin[d] == wmax[d]) {
+      s0[d] = w0;
+      s1[d] = w1;
+      e0[d] = w1;
+      e1[d] = w0;
+    } else if (ie[d] == is[d] + 1 * 2) {
+      s0[d] = w0 * w0 / 2 - (1 - w1) * (1 - w1) / 2;
+      e0[d] = w1 * w1 / 2 - (1 - w0) * (1 - w0) / 2;
+      s1[d] = e0[d];
+      e1[d] = s0[d];
+    }
+  }
+}
+
+// yucky directions of the ivec loops (3D: X,Y,Z; 2D: Z,X,Y; 1D: X,Y,Z)
+void yucky(const GV &G, int yd[3]) {
+  if (G.dim == 2)
+    yd[0] = Z, yd[1] = X, yd[2] = Y;
+  else
+    yd[0] = X, yd[1] = Y, yd[2] = Z;
+}
+
+// fields::add_dft for component c over where (centered grid): one DftChunk per
+// intersecting chunk, prepended to `list` as loop_in_chunks creates them.
+void add_dft(orc_sim *s, int c, const double wmin[3], const double wmax[3], bool incl,
+             cplx stored_weight, double dt_factor, std::vector<DftChunk> &list, size_t nfreq) {
+  const GV &G = s->gv;
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!G.has[d]) continue;
+    is[d] = 1 + 2 * int(floor(wmin[d] * G.a - .5));  // vec2diel_floor, equal_shift 0
+    ie[d] = 1 + 2 * int(ceil(wmax[d] * G.a - .5));
+  }
+  double s0[3], s1[3], e0[3], e1[3];
+  boundary_weights(G, wmin, wmax, is, ie, s0, e0, s1, e1);
+  double dV0 = 1.0;
+  for (int d = 0; d < 3; d++)
+    if (G.has[d] && wmax[d] - wmin[d] > 0.0) dV0 *= G.inva;
+  std::vector<DftChunk> made;
+  for (size_t ci = 0; ci < s->chunks.size(); ci++) {
+    Chunk &ch = s->chunks[ci];
+    const GV &g = ch.gv;
+    if (!s->allocated[c]) continue;
+    int isc[3], iec[3];
+    double s0c[3], s1c[3], e0c[3], e1c[3];
+    bool empty = false;
+    for (int d = 0; d < 3; d++) {
+      s0c[d] = s1c[d] = e0c[d] = e1c[d] = 1.0;
+      if (!G.has[d]) {
+        isc[d] = iec[d] = 0;
+        continue;
+      }
+      const int uoc = G.io[d] + 1, coc = g.io[d] + 1, cbo = g.big(d) - 1;  // Centered: shift 1
+      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
+      isc[d] = std::max(is[d], iscoS);
+      iec[d] = std::min(ie[d], iecoS);
+      if (isc[d] > iec[d]) empty = true;
+    }
+    if (empty) continue;
+    for (int d = 0; d < 3; d++) {
+      if (!G.has[d]) continue;
+      if (isc[d] == is[d]) {
+        s0c[d] = s0[d];
+        s1c[d] = s1[d];
+      } else if (isc[d] == is[d] + 2) {
+        s0c[d] = s1[d];
+      }
+      if (iec[d] == ie[d]) {
+        e0c[d] = e0[d];
+        e1c[d] = e1[d];
+      } else if (iec[d] == ie[d] - 2) {
+        e0c[d] = e1[d];
+      }
+      if (iec[d] == isc[d]) {
+        double w = std::min(s0c[d], e0c[d]);
+        s0c[d] = e0c[d] = s1c[d] = e1c[d] = w;
+      } else if (iec[d] == isc[d] + 2) {
+        double w = std::min(s0c[d], e1c[d]);
+        s0c[d] = w, e1c[d] = w;
+        w = std::min(s1c[d], e0c[d]);
+        s1c[d] = w, e0c[d] = w;
+      } else if (iec[d] == isc[d] + 4) {
+        double w = std::min(s1c[d], e1c[d]);
+        s1c[d] = w, e1c[d] = w;
+      }
+    }
+    DftChunk dc;
+    dc.ci = (int)ci;
+    dc.c = c;
+    for (int d = 0; d < 3; d++) {
+      dc.is[d] = isc[d], dc.ie[d] = iec[d];
+      dc.s0[d] = s0c[d], dc.s1[d] = s1c[d], dc.e0[d] = e0c[d], dc.e1[d] = e1c[d];
+    }
+    dc.dV0 = dV0;
+    dc.incl = incl;
+    dc.scale = stored_weight * cplx(1.0) * dt_factor;  // phase_factor 1 (no symmetry / Bloch)
+    dc.avg1 = dc.avg2 = 0;  // grid_volume::yee2cent_offsets (src/vec.cpp:333-344)
+    for (int d = 0; d < 3; d++)
+      if (G.has[d] && !G.shift(c, d)) {
+        if (dc.avg1)
+          dc.avg2 = g.s[d];
+        else
+          dc.avg1 = g.s[d];
+      }
+    dc.N = 1;
+    for (int d = 0; d < 3; d++)
+      if (G.has[d]) dc.N *= size_t((iec[d] - isc[d]) / 2 + 1);
+    dc.dft.assign(dc.N * nfreq, cplx(0.0));
+    made.push_back(std::move(dc));
+  }
+  // each new chunk becomes the head of the list
+  for (auto it = made.begin(); it != made.end(); ++it) list.insert(list.begin(), std::move(*it));
+}
+
+// dft_chunk::update_dft (src/dft.cpp:265-300)
+void update_dft(orc_sim *s, DftChunk &dc, const std::vector<double> &omega, double time) {
+  const GV &G = s->gv;
+  Chunk &ch = s->chunks[dc.ci];
+  const realnum *f = ch.F(dc.c);
+  if (!f) return;
+  const size_t Nomega = omega.size();
+  std::vector<cplx> ph(Nomega);
+  for (size_t i = 0; i < Nomega; ++i) ph[i] = std::polar(1.0, omega[i] * time) * dc.scale;
+  int yd[3];
+  yucky(G, yd);
+  long ln[3], st[3], off = 0;
+  for (int k = 0; k < 3; k++) {
+    const int d = yd[k];
+    ln[k] = G.has[d] ? (dc.ie[d] - dc.is[d]) / 2 + 1 : 1;
+    st[k] = G.has[d] ? ch.gv.s[d] : 0;
+    if (G.has[d]) off += long((dc.is[d] - ch.gv.io[d]) / 2) * ch.gv.s[d];
+  }
+  auto W1 = [&](int k, long i) -> double {
+    const int d = yd[k];
+    const long n = ln[k];
+    if (i > 1 && i < n - 2) return 1.0;
+    if (i == 0) return dc.s0[d];
+    if (i == 1) return dc.s1[d];
+    if (i == n - 1) return dc.e0[d];
+    if (i == n - 2) return dc.e1[d];
+    return 1.0;
+  };
+  for (long i1 = 0; i1 < ln[0]; i1++)
+    for (long i2 = 0; i2 < ln[1]; i2++)
+      for (long i3 = 0; i3 < ln[2]; i3++) {
+        const long idx = off + i1 * st[0] + i2 * st[1] + i3 * st[2];
+        const size_t idx_dft = size_t((i1 * ln[1] + i2) * ln[2] + i3);
+        double w = dc.incl ? (W1(2, i3) * (W1(1, i2) * ((dc.dV0 + 0.0 * i2) * W1(0, i1)))) : 1.0;
+        realnum fr;
+        if (dc.avg2)
+          fr = (w * 0.25) * (f[idx] + f[idx + dc.avg1] + f[idx + dc.avg2] + f[idx + (dc.avg1 + dc.avg2)]);
+        else if (dc.avg1)
+          fr = (w * 0.5) * (f[idx] + f[idx + dc.avg1]);
+        else
+          fr = w * f[idx];
+        for (size_t i = 0; i < Nomega; ++i)
+          dc.dft[Nomega * idx_dft + i] += cplx{fr * ph[i].real(), fr * ph[i].imag()};
+      }
+}
+}  // namespace
+
+void update_dfts(orc_sim *s) {  // fields::update_dfts after t += 1 (src/step.cpp:125-127)
+  for (auto &o : s->dfts) {
+    if (s->t % o->decim) continue;
+    const double tE = s->t * s->dt, tH = tE - 0.5 * s->dt;
+    for (auto &dc : o->E) update_dft(s, dc, o->omega, is_magnetic(dc.c) ? tH : tE);
+    for (auto &dc : o->H) update_dft(s, dc, o->omega, is_magnetic(dc.c) ? tH : tE);
+  }
+}
+
+extern "C" {
+
+// regions: nreg x {min x,y,z, max x,y,z, direction (0..2), weight}
+int orc_add_dft_flux(orc_sim *s, int nreg, const double *regions, const double *freqs, int nfreq,
+                     int decimation) {
+  finalize(s);
+  if (nreg < 1 || nfreq < 1) return set_err("add_dft_flux: no regions / frequencies");
+  std::unique_ptr<DftFluxObj> o(new DftFluxObj);
+  o->nfreq = (size_t)nfreq;
+  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
+  int decim = decimation;
+  if (decim == 0) {  // fields::add_dft (src/dft.cpp:190-213)
+    double src_freq_max = 0;
+    for (auto &st : s->srcs) {
+      const double fw = st.kind == 0 ? sqrt(-2.0 * log(1e-7)) / (st.width * pi) : 0.0;
+      if (fw == 0)
+        decim = 1;
+      else
+        src_freq_max = std::max(src_freq_max, std::abs(st.kind == 0 ? st.freq : st.cfreq.real()) + 0.5 * fw);
+    }
+    double freq_max = 0;
+    for (int i = 0; i < nfreq; ++i) freq_max = std::max(freq_max, std::abs(freqs[i]));
+    bool nonlinear = false;
+    for (auto &ch : s->chunks)
+      for (int c = 0; c < NCOMP; c++) nonlinear = nonlinear || !ch.chi2[c].empty() || !ch.chi3[c].empty();
+    // (src/dft.cpp:207-210 overwrites the fwidth == 0 case above)
+    if ((freq_max > 0) && (src_freq_max > 0) && !nonlinear)
+      decim = std::max(1, int(std::floor(1 / (s->dt * (freq_max + src_freq_max)))));
+    else
+      decim = 1;
+  }
+  o->decim = decim;
+  const double dt_factor = s->dt / sqrt(2.0 * pi) * decim;
+  for (int r = 0; r < nreg; r++) {
+    const double *R = regions + 8 * r;
+    const int d = int(R[6]);
+    const double wgt = R[7];
+    int cE[2], cH[2];
+    switch (d) {  // fields::add_dft_flux (src/dft.cpp:601-617)
+      case X: cE[0] = Ey, cE[1] = Ez, cH[0] = Hz, cH[1] = Hy; break;
+      case Y: cE[0] = Ez, cE[1] = Ex, cH[0] = Hx, cH[1] = Hz; break;
+      default: cE[0] = Ex, cE[1] = Ey, cH[0] = Hy, cH[1] = Hx; break;
+    }
+    for (int i = 0; i < 2; ++i) {
+      add_dft(s, cE[i], R, R + 3, true, cplx(wgt * double(1 - 2 * i)), dt_factor, o->E, o->nfreq);
+      add_dft(s, cH[i], R, R + 3, false, cplx(1.0), dt_factor, o->H, o->nfreq);
+    }
+  }
+  s->dfts.push_back(std::move(o));
+  return int(s->dfts.size()) - 1;
+}
+
+int orc_dft_flux(orc_sim *s, int h, double *out) {  // dft_flux::flux (src/dft.cpp:533-547)
+  if (h < 0 || h >= (int)s->dfts.size()) return set_err("bad dft handle");
+  DftFluxObj &o = *s->dfts[h];
+  const size_t Nfreq = o.nfreq;
+  for (size_t i = 0; i < Nfreq; ++i) out[i] = 0;
+  for (size_t k = 0; k < o.E.size() && k < o.H.size(); k++)
+    for (size_t p = 0; p < o.E[k].N; ++p)
+      for (size_t i = 0; i < Nfreq; ++i)
+        out[i] += real(o.E[k].dft[p * Nfreq + i] * conj(o.H[k].dft[p * Nfreq + i]));
+  return 0;
+}
+
+// all DFT values of the E (which 0) or H (which 1) list, list order, re/im interleaved
+long long orc_dft_size(orc_sim *s, int h) {
+  if (h < 0 || h >= (int)s->dfts.size()) return -1;
+  long long n = 0;
+  for (auto &dc : s->dfts[h]->E) n += (long long)dc.dft.size();
+  return n;
+}
+int orc_dft_data(orc_sim *s, int h, int which, double *out, long long n) {
+  if (h < 0 || h >= (int)s->dfts.size()) return set_err("bad dft handle");
+  auto &L = which ? s->dfts[h]->H : s->dfts[h]->E;
+  long long k = 0;
+  for (auto &dc : L)
+    for (auto &v : dc.dft) {
+      if (k + 2 > 2 * n) return set_err("dft buffer too small");
+      out[k++] = v.real();
+      out[k++] = v.imag();
+    }
+  return 0;
+}
+int orc_dft_decimation(orc_sim *s, int h) {
+  if (h < 0 || h >= (int)s->dfts.size()) return -1;
+  return s->dfts[h]->decim;
+}
+
+orc_sim::~orc_sim() {}
 
 int orc_step(orc_sim *s, int nsteps) {
   finalize(s);

@@ -39,6 +39,14 @@ long long orc_t(orc_sim *s);
 double orc_dt(orc_sim *s);
 size_t orc_ntot(orc_sim *s);
 long long orc_nr_failures(orc_sim *s);
+/* DFT flux (fields::add_dft_flux, src/dft.cpp:578-640): regions = nreg x
+ * {min x,y,z, max x,y,z, direction, weight}; returns a handle >= 0. */
+int orc_add_dft_flux(orc_sim *s, int nreg, const double *regions, const double *freqs, int nfreq,
+                     int decimation);
+int orc_dft_flux(orc_sim *s, int h, double *out);
+long long orc_dft_size(orc_sim *s, int h);
+int orc_dft_data(orc_sim *s, int h, int which, double *out, long long n);
+int orc_dft_decimation(orc_sim *s, int h);
 
 #ifdef __cplusplus
 }

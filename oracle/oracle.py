@@ -58,6 +58,12 @@ def lib():
         L.orc_nr_failures.restype = ctypes.c_longlong
         L.orc_nr_failures.argtypes = [c_void]
         L.orc_set_threads.argtypes = [c_int]
+        L.orc_add_dft_flux.argtypes = [c_void, c_int, dptr, dptr, c_int, c_int]
+        L.orc_dft_flux.argtypes = [c_void, c_int, dptr]
+        L.orc_dft_size.restype = ctypes.c_longlong
+        L.orc_dft_size.argtypes = [c_void, c_int]
+        L.orc_dft_data.argtypes = [c_void, c_int, c_int, dptr, ctypes.c_longlong]
+        L.orc_dft_decimation.argtypes = [c_void, c_int]
         _LIB = L
     return _LIB
 
@@ -220,6 +226,34 @@ class Oracle:
 
     def nr_random_fallbacks(self):
         return lib().orc_nr_failures(self.h)
+
+    # ---- DFT flux (fields::add_dft_flux, src/dft.cpp:578-640)
+    def add_dft_flux(self, regions, freqs, decimation=0):
+        """regions: [(min xyz, max xyz, direction, weight)]; returns a handle."""
+        r = np.ascontiguousarray([list(lo) + list(hi) + [d, w] for lo, hi, d, w in regions],
+                                 dtype=np.float64).ravel()
+        f = np.ascontiguousarray(freqs, dtype=np.float64)
+        h = lib().orc_add_dft_flux(self.h, len(regions), _dp(r), _dp(f), len(f), int(decimation))
+        if h < 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        self._dft_nf = getattr(self, "_dft_nf", {})
+        self._dft_nf[h] = len(f)
+        return h
+
+    def flux(self, h):
+        out = np.zeros(self._dft_nf[h], dtype=np.float64)
+        _chk(lib().orc_dft_flux(self.h, h, _dp(out)))
+        return out
+
+    def dft_data(self, h, which):
+        """All DFT values of the E (0) or H (1) chunk list, in list order (complex)."""
+        n = lib().orc_dft_size(self.h, h)
+        out = np.zeros(2 * n, dtype=np.float64)
+        _chk(lib().orc_dft_data(self.h, h, int(which), _dp(out), n))
+        return out[0::2] + 1j * out[1::2]
+
+    def dft_decimation(self, h):
+        return lib().orc_dft_decimation(self.h, h)
 
     def center(self):
         """grid_volume::center() (src/vec.cpp:1089-1103): io + round_down_to_even(n)."""

@@ -98,6 +98,18 @@ class ProductSim:
     def nr_random_fallbacks(self):
         return self._fields().nr_fallbacks()
 
+    def add_dft_flux(self, regions, freqs, decimation=0):
+        return self._fields().add_dft_flux(regions, freqs, decimation)
+
+    def flux(self, h):
+        return self._fields().flux(h)
+
+    def dft_data(self, h, which):
+        return self._fields().dft_data(h, which)
+
+    def dft_decimation(self, h):
+        return self._fields().dft_decimation(h)
+
 
 class GroupSim(ProductSim):
     """nranks z-slabs (y-slabs in 2-D) of one grid on one GPU, one host thread per
@@ -171,6 +183,20 @@ class GroupSim(ProductSim):
 
     def nr_random_fallbacks(self):
         return sum(f.nr_fallbacks() for f in self._all())
+
+    def add_dft_flux(self, regions, freqs, decimation=0):
+        hs = [f.add_dft_flux(regions, freqs, decimation) for f in self._all()]
+        assert all(h == hs[0] for h in hs)
+        return hs[0]
+
+    def flux(self, h):
+        vals = self._par(lambda f: f.flux(h))  # every rank returns the allreduced sum
+        assert all(np.array_equal(v, vals[0]) for v in vals)
+        return vals[0]
+
+    def dft_data(self, h, which):
+        # each point is accumulated by the rank that owns it, the others hold 0
+        return sum(f.dft_data(h, which) for f in self._all())
 
 
 class GroupSim3(GroupSim):
@@ -390,3 +416,97 @@ def sc_big_lorentz_3d(make, steps=24, extra=None):
         extra(o)
     o.step(steps - steps // 2)
     return o
+
+
+# ------------------------------------------------------------------ DFT flux
+def flux_box_faces(lo, hi, dim):
+    """fields::add_dft_flux_box (src/dft.cpp:831-848): for each direction with extent,
+    the max face (+1) then the min face (-1) are prepended to the volume list; the
+    regions are returned in the list's iteration order."""
+    faces = []
+    for d in range(3):
+        if dim == 2 and d == 2:
+            continue
+        if hi[d] - lo[d] > 0:
+            mx_lo = list(lo)
+            mx_lo[d] = hi[d]
+            faces.insert(0, (mx_lo, list(hi), d, 1.0))
+            mn_hi = list(hi)
+            mn_hi[d] = lo[d]
+            faces.insert(0, (list(lo), mn_hi, d, -1.0))
+    return faces
+
+
+FLUX2D_FREQS = [0.230, 0.232, 0.238, 0.241, 0.248, 0.254, 0.256, 0.265, 0.269, 0.270]
+
+
+def sc_flux_2d(make, xmax=10.0, ymax=10.0, ttot=130.0):
+    """tests/flux.cpp:157-225 (flux_2d, second check): voltwo(10,10,8), pml(0.5),
+    vacuum (bump2 is 1 at z=0), Ez point source add_point_source(Ez, 0.25, 3.5, 0, 8,
+    (xmax/6+0.1, ymax/6+0.3), 1), two concentric DFT flux boxes around it, stepped
+    until time() >= 2*ttot.  Returns (sim, handle box1, handle box2)."""
+    o = vol(make, 2, [xmax, ymax], 8)
+    o.add_pml(0.5)
+    o.legacy_point_source(2, 0.25, 3.5, 0.0, 8.0, (xmax / 6 + 0.1, ymax / 6 + 0.3, 0.0), 1.0)
+    b1 = flux_box_faces([xmax / 6 - 0.4, ymax / 6 - 0.2, 0], [xmax / 6 + 0.6, ymax / 6 + 0.8, 0], 2)
+    b2 = flux_box_faces([xmax / 6 - 0.9, ymax / 6 - 0.7, 0], [xmax / 6 + 1.1, ymax / 6 + 1.3, 0], 2)
+    h1 = o.add_dft_flux(b1, FLUX2D_FREQS)
+    h2 = o.add_dft_flux(b2, FLUX2D_FREQS)
+    n = 0
+    while (n + 1) * o.dt < 2 * ttot:  # f.step(); while (f.time() < ttot) ...; ... < 2*ttot
+        n += 1
+    o.step(n + 1)
+    return o, h1, h2
+
+
+FLUX3D_FREQS = [0.1, 0.15, 0.2, 0.27]
+
+
+def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=None):
+    """Waveguide (eps 12 core along x) + PML with four DFT flux objects: a box around
+    the source (six faces, weights +-1), an x-normal plane across the whole cell
+    (through the PML), a z-normal plane inside the lower PML, and a y-direction
+    volume region (interpolation weights in all three directions).  Optional
+    Lorentzian slab (E stored inside the polarization box in fused mode) and a
+    callback(o) at half time.  The last object uses the automatic decimation
+    (src/dft.cpp:195-216).  Returns (sim, [handles])."""
+    sizes = sizes or [3.2, 3.2, 3.2]
+    o = vol(make, 3, sizes, 10, center_origin=True)
+    o.add_pml(1.0 if sizes[0] < 4 else 0.7)
+    sig = []
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        o.set_chi1inv(c, c, np.where((np.abs(y) < 0.5) & (np.abs(z) < 0.5), 1 / 12.0, 1.0))
+        sig.append(np.where(np.abs(z - 0.3) < 0.25, 0.5, 0.0))
+    if lorentz:
+        o.add_lorentzian(1.1, 0.05, sig)
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    o.add_gaussian_source(1, 0.2, 6.0, 0.0, 60.0, (-0.33, 0.12, 0.41), 0.7)
+    hx, hy, hz = [0.5 * s for s in sizes]
+    hs = [o.add_dft_flux(flux_box_faces([-0.42, -0.37, -0.33], [0.44, 0.51, 0.38], 3),
+                         FLUX3D_FREQS, decimation),
+          o.add_dft_flux([([0.83, -hy, -hz], [0.83, hy, hz], 0, 1.0)], FLUX3D_FREQS, decimation),
+          o.add_dft_flux([([-hx + 0.1, -hy + 0.3, -hz + 0.35], [hx - 0.2, hy - 0.1, -hz + 0.35],
+                           2, -0.5)], FLUX3D_FREQS, decimation),
+          o.add_dft_flux([([-0.61, -0.23, -0.17], [0.57, 0.29, 0.66], 1, 1.0)], FLUX3D_FREQS,
+                         0)]  # automatic decimation
+    o.step(steps // 2)
+    if extra:
+        extra(o)
+    o.step(steps - steps // 2)
+    return o, hs
+
+
+def sc_flux_1d(make, steps=1500, chi3=1e-2):
+    """1-D: 20 @ res 20, PML 1, chi3 (inert in the fork), Ex Gaussian near the left;
+    transmitted flux plane + a flux 'box' (two points) around the source."""
+    o = vol(make, 1, [20.0], 20, center_origin=True)
+    o.add_pml(1.0)
+    if chi3:
+        o.set_chi3(0, np.full(o.shape(), chi3))
+    o.add_gaussian_source(0, 1 / 3, 60.0 / 8, 0.0, 75.0, (0, 0, -8.0), 10.0)
+    fr = [0.25, 1 / 3, 0.4, 1.0]
+    hs = [o.add_dft_flux([([0, 0, 7.5], [0, 0, 7.5], 2, 1.0)], fr, 1),
+          o.add_dft_flux(flux_box_faces([0, 0, -8.5], [0, 0, -7.3], 3), fr, 0)]
+    o.step(steps)
+    return o, hs

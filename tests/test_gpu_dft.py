@@ -1,0 +1,102 @@
+"""GPU parity of the on-device DFT flux (fields::update_dfts,
+src/dft.cpp:249-300, and dft_flux::flux, src/dft.cpp:533-547) against the CPU
+oracle.
+
+Tolerance: every per-point DFT value (E and H lists, list order) is required
+BITWISE equal to the oracle's -- the kernel follows the reference's averaging
+and accumulation expression order and is built with -ffp-contract=off.  The
+flux spectrum is a host sum in list order: bitwise on one GPU; across slabs
+each rank sums its own points and the partial sums are added (as the
+reference's sum_to_all over processes), so it is compared at rel 1e-12.
+"""
+import numpy as np
+import pytest
+
+from scenarios import (GroupSim, GroupSim3, ProductSim, make_oracle, sc_flux_1d, sc_flux_2d,
+                       sc_flux_3d)
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+
+def _same_dft(p, o, hs, flux_exact=True):
+    for h in hs:
+        for which in (0, 1):
+            a, b = p.dft_data(h, which), o.dft_data(h, which)
+            assert a.shape == b.shape and a.size > 0
+            np.testing.assert_array_equal(a, b, err_msg=f"dft object {h} list {which}")
+        fa, fb = p.flux(h), o.flux(h)
+        if flux_exact:
+            np.testing.assert_array_equal(fa, fb)
+        else:
+            np.testing.assert_allclose(fa, fb, rtol=1e-12, atol=1e-300)
+        assert p.dft_decimation(h) == o.dft_decimation(h)
+
+
+def test_dft_flux_2d_concentric():
+    """tests/flux.cpp:157-225 on the GPU: bitwise to the oracle, and the reference's
+    own assertion (concentric boxes agree within 9 %)."""
+    p, h1, h2 = sc_flux_2d(ProductSim)
+    o, _, _ = sc_flux_2d(make_oracle)
+    _same_dft(p, o, [h1, h2])
+    f1, f2 = p.flux(h1), p.flux(h2)
+    assert np.all(np.abs(f1 - f2) <= 0.09 * np.abs(f2))
+
+
+def test_dft_flux_1d():
+    p, hs = sc_flux_1d(ProductSim)
+    o, _ = sc_flux_1d(make_oracle)
+    _same_dft(p, o, hs)
+
+
+def test_dft_flux_3d_fused():
+    """Fused stepping: E is implicit (chi1inv * D) inside the fused domain and the
+    DFT kernel must read it through the same rule."""
+    p, hs = sc_flux_3d(ProductSim)
+    assert p._fields().fused_active()
+    o, _ = sc_flux_3d(make_oracle)
+    _same_dft(p, o, hs)
+
+
+def test_dft_flux_3d_unfused(monkeypatch):
+    monkeypatch.setenv("MNL_NO_FUSED", "1")
+    p, hs = sc_flux_3d(ProductSim)
+    assert not p._fields().fused_active()
+    o, _ = sc_flux_3d(make_oracle)
+    _same_dft(p, o, hs)
+
+
+def test_dft_flux_3d_big_box():
+    """Many lean and general tiles, planes crossing tile and PML boundaries."""
+    p, hs = sc_flux_3d(ProductSim, sizes=[14.0, 4.1, 5.3], steps=30)
+    o, _ = sc_flux_3d(make_oracle, sizes=[14.0, 4.1, 5.3], steps=30)
+    _same_dft(p, o, hs)
+
+
+def test_dft_flux_3d_lorentz():
+    p, hs = sc_flux_3d(ProductSim, lorentz=True)
+    o, _ = sc_flux_3d(make_oracle, lorentz=True)
+    _same_dft(p, o, hs)
+
+
+def test_dft_flux_3d_mode_toggle():
+    """A magnetic source added mid-run turns fused stepping off (E materialised)."""
+    def add_h(o):
+        o.add_gaussian_source(4, 0.3, 3.0, 0.0, 30.0, (0.4, 0.3, -0.2), 0.8)
+    p, hs = sc_flux_3d(ProductSim, extra=add_h)
+    o, _ = sc_flux_3d(make_oracle, extra=add_h)
+    _same_dft(p, o, hs)
+
+
+@pytest.mark.parametrize("G", [GroupSim, GroupSim3])
+def test_dft_flux_slabs(G):
+    """z-slabs: points on a rank boundary average Yee values from the neighbour's
+    ghost plane (E low ghost, H_z low ghost exchanged before the DFT update)."""
+    p, hs = sc_flux_3d(G)
+    o, _ = sc_flux_3d(make_oracle)
+    _same_dft(p, o, hs, flux_exact=False)
+
+
+def test_dft_flux_slabs_2d():
+    p, h1, h2 = sc_flux_2d(GroupSim3, ttot=40.0)
+    o, _, _ = sc_flux_2d(make_oracle, ttot=40.0)
+    _same_dft(p, o, [h1, h2], flux_exact=False)

@@ -1,0 +1,69 @@
+"""CPU checks of the oracle's DFT-flux restatement (fields::add_dft_flux /
+update_dfts / dft_flux::flux, src/dft.cpp) and of the host-side flux helpers.
+
+Parity pin: the reference's own flux test tests/flux.cpp:157-225 (flux_2d,
+second check: the flux spectra through two concentric boxes around the
+source agree within 9 %) -- a property the fork passes.  No
+golden DFT values of the fork exist (tests/harmonics.cpp and
+python/tests/test_3rd_harm_1d.py need the upstream chi3 and fail on the fork),
+so per-point DFT values are pinned by the restatement plus this property.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from scenarios import (FLUX2D_FREQS, flux_box_faces, make_oracle, sc_flux_1d, sc_flux_2d, vol)
+
+
+def test_flux_2d_concentric_boxes():
+    """tests/flux.cpp:207-221: fl1[i] vs fl2[i], compare(..., 0.09, 0)."""
+    o, h1, h2 = sc_flux_2d(make_oracle)
+    assert o.t == 4160
+    f1, f2 = o.flux(h1), o.flux(h2)
+    assert f1.shape == (len(FLUX2D_FREQS),)
+    assert np.all(f1 > 0) and np.all(f2 > 0)
+    assert np.all(np.abs(f1 - f2) <= 0.09 * np.abs(f2))
+
+
+def _bw(width):  # gaussian_bandwidth (src/sources.cpp:67-70)
+    return math.sqrt(-2.0 * math.log(1e-7)) / (width * math.pi)
+
+
+def test_automatic_decimation():
+    """fields::add_dft decimation rule (src/dft.cpp:195-216): floor(1/(dt*(fmax +
+    max_src(|f| + fwidth/2)))) for linear media; sources with zero bandwidth are
+    ignored when a Gaussian is present; 1 with nonlinear media or CW only."""
+    o = vol(make_oracle, 2, [4, 4], 10)
+    o.add_gaussian_source(2, 0.3, 5.0, 0.0, 50.0, (1.0, 1.0, 0), 1.0)
+    o.add_continuous_source(2, 0.5, 0.0, 0.0, 1e20, 3.0, (2.0, 1.0, 0), 1.0)
+    h = o.add_dft_flux([([1, 0, 0], [1, 4, 0], 0, 1.0)], [0.2, 0.4])
+    expect = max(1, math.floor(1 / (o.dt * (0.4 + 0.3 + 0.5 * _bw(5.0)))))
+    assert o.dft_decimation(h) == expect and expect > 1
+    assert o.dft_decimation(o.add_dft_flux([([1, 0, 0], [1, 4, 0], 0, 1.0)], [0.2], 3)) == 3
+
+    cw = vol(make_oracle, 2, [4, 4], 10)
+    cw.add_continuous_source(2, 0.5, 0.0, 0.0, 1e20, 3.0, (2.0, 1.0, 0), 1.0)
+    assert cw.dft_decimation(cw.add_dft_flux([([1, 0, 0], [1, 4, 0], 0, 1.0)], [0.2])) == 1
+
+    o1, hs = sc_flux_1d(make_oracle, steps=2)  # chi3 != 0: has_nonlinearities
+    assert o1.dft_decimation(hs[1]) == 1
+
+
+def test_flux_box_faces_order():
+    """add_dft_flux_box prepends (max, +1) then (min, -1) per direction."""
+    f = flux_box_faces([0, 1, 2], [3, 4, 5], 3)
+    assert [(r[2], r[3]) for r in f] == [(2, -1.0), (2, 1.0), (1, -1.0), (1, 1.0),
+                                         (0, -1.0), (0, 1.0)]
+    assert f[1][0] == [0, 1, 5] and f[0][1] == [3, 4, 2]
+
+
+def test_flux_1d_plane_wave_direction():
+    """A pulse launched to the right carries positive flux through a plane on the
+    right; a two-point 'box' around the source sees outgoing flux."""
+    o, hs = sc_flux_1d(make_oracle, steps=1500)
+    tr = o.flux(hs[0])
+    assert tr[1] > 0
+    assert np.all(o.flux(hs[1])[:3] > 0)
+    e = o.dft_data(hs[0], 0)
+    assert e.shape == (2 * 4,) and np.any(e != 0)
