@@ -39,6 +39,9 @@ def parse():
                     help="kerr: BASELINE configs[3] (chi3 + Lorentzian slab, unfused path)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--flux", type=int, default=0,
+                    help="add N DFT flux planes (x-normal, whole cross-section; decimation 1)")
+    ap.add_argument("--nfreq", type=int, default=50, help="frequencies per flux plane")
     ap.add_argument("--no-events", action="store_true",
                     help="diagnostics: no per-kernel HIP events in the timed region")
     return ap.parse_args()
@@ -122,6 +125,13 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         nid = obj[0]
     gv, s, f = build_fields(args, rank, world, local_rank, nid)
+    if args.flux:  # on-device DFT flux monitors
+        hx = 0.5 * gv.n[0] / 10.0
+        hy, hz = 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
+        freqs = [0.1 + 0.1 * i / max(args.nfreq - 1, 1) for i in range(args.nfreq)]
+        for i in range(args.flux):
+            x = -hx + 2 * hx * (i + 1) / (args.flux + 1) + 0.05
+            f.add_dft_flux([([x, -hy, -hz], [x, hy, hz], 0, 1.0)], freqs, 1)
 
     def barrier():
         if dist is not None:
@@ -179,8 +189,15 @@ def main():
                 "kernel": "fused_general_kernel (PML / boundary tiles, same pass)",
                 "bytes_per_launch": g_bytes, "avg_launch_ms": round(g_avg, 4),
                 "achieved": round(g_bytes / (g_avg * 1e-3) / 1e9, 1)}
+    if args.flux:
+        d_n, d_ms, d_bytes = f.kernel_stats(3)
+        if d_n:
+            d_avg = d_ms / d_n
+            roof["dft"] = {"kernel": f"dft_update_kernel x{args.flux} planes, {args.nfreq} freqs",
+                           "bytes_per_step": d_bytes, "avg_step_ms": round(d_avg, 4),
+                           "achieved": round(d_bytes / (d_avg * 1e-3) / 1e9, 1)}
     cpu = None
-    if world == 1 and not args.no_cpu and args.workload != "kerr":
+    if world == 1 and not args.no_cpu and args.workload != "kerr" and not args.flux:
         try:
             cpu = cpu_baseline(args)
         except Exception as e:  # the baseline must never hide the GPU number
@@ -207,6 +224,7 @@ def main():
                         (", Ez Gaussian current at (0.05,0.05,0.05)"
                          if args.workload != "kerr" else ""),
             "grid": list(gv.n), "per_gpu_cells": args.size ** 3, "parallelism": f"z-slab x{world}",
+            "flux_planes": args.flux, "flux_nfreq": args.nfreq if args.flux else 0,
             "model_bytes_per_cell_step": bpc},
         "roofline": roof,
         "cpu_baseline": cpu,

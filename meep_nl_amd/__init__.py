@@ -8,7 +8,9 @@ from .core import (Bx, By, Bz, Dx, Dy, Dz, Ex, Ey, Ez, Fields, GridVolume, Hx, H
                    Structure, X, Y, Z, device_count)
 from .simulation import (ALL, AUTOMATIC, Block, ContinuousSource, DftFlux, DrudeSusceptibility,
                          FluxRegion, GaussianSource, High, LorentzianSusceptibility, Low, Medium,
-                         PML, Simulation, Source, Vector3, Volume, air, get_flux_freqs,
-                         get_fluxes, inf, vacuum)
+                         PML, Simulation, Source, Vector3, Volume, after_sources, after_time,
+                         air, at_beginning, at_end, at_every, before_time, combine_step_funcs,
+                         during_sources, get_flux_freqs, get_fluxes, inf, stop_after_walltime,
+                         stop_when_fields_decayed, vacuum, when_false, when_true)
 
 __version__ = "0.1.0"

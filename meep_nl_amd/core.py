@@ -134,6 +134,20 @@ class Structure:
         check(lib().mnl_structure_set_box(self.h, kind, index, ptr(b), float(value)))
 
 
+def _src_last_time(kind, params):
+    """src_time::last_time(): gaussian float(peak_time + cutoff) with the cutoff
+    shrink of gaussian_src_time(f, w, st, et) (src/sources.cpp:85-96,
+    src/meep.hpp:1024); continuous end_time (src/meep.hpp:1046)."""
+    if kind == 0:
+        w, st, et = params[1], params[2], params[3]
+        peak, cutoff = 0.5 * (st + et), (et - st) * 0.5
+        while math.exp(-cutoff * cutoff / (2 * w * w)) < 1e-100:
+            cutoff *= 0.9
+        cutoff = float(np.float32(cutoff))
+        return float(np.float32(peak + cutoff))
+    return float(params[4])
+
+
 class Fields:
     """meep::fields with use_real_fields() on one MI355X (or one z-slab of it)."""
 
@@ -163,6 +177,8 @@ class Fields:
         amp = complex(amp)
         check(lib().mnl_fields_add_point_source(self.h, comp, kind, ptr(p), len(p), ptr(pos),
                                                 amp.real, amp.imag, int(is_integrated)))
+        self._last_times = getattr(self, "_last_times", [])
+        self._last_times.append(_src_last_time(kind, list(params)))
 
     def add_gaussian_source(self, comp, freq, width, start, end, pos, amp=1.0,
                             is_integrated=False):
@@ -190,6 +206,10 @@ class Fields:
 
     def require_component(self, comp):
         check(lib().mnl_fields_require_component(self.h, comp))
+
+    def last_source_time(self):
+        """fields::last_source_time (src/bands.cpp:35-41): latest src_time::last_time()."""
+        return max([0.0] + getattr(self, "_last_times", []))
 
     # -- stepping
     def step(self, n=1):

@@ -22,6 +22,7 @@
 #include <set>
 #include <unordered_set>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/meep_nl_amd.h"
@@ -167,10 +168,15 @@ struct DftFluxH {
   int *d_pj = nullptr, *d_pch = nullptr;
   double *d_pw = nullptr;             // w * 0.25 / 0.5 / 1 per point
   DftChunkDev *d_ch = nullptr;        // per chunk (E list, then H list)
-  double *d_dft = nullptr;            // npts * nfreq complex (re, im)
+  double *d_dft = nullptr;            // [slot/64][freq][slot%64] complex (re, im)
   double *d_ph = nullptr;             // phases of one batch: [update][chunk][freq] complex
   size_t ph_cap = 0;
   int row = 0;                        // next phase row of this batch
+  std::vector<int> slot;              // device slot of each point (reference order -> slot)
+  double *d_fr = nullptr;             // [update][slot] sampled fields awaiting accumulation
+  int nbuf = 0;                       // buffered updates (rows row-nbuf .. row-1)
+  int kb = DFT_KB;                    // updates per accumulation
+  double bytes = 0;                   // algorithmic bytes of one update (DESIGN.md "DFT")
   ~DftFluxH() {
     if (d_ph) (void)hipFree(d_ph);
   }
@@ -1022,6 +1028,9 @@ int build_source_lists(mnl_fields *F) {
 // ------------------------------------------------------------- interpolation
 inline int my_round(double x) { return int(floor(fabs(x) + 0.5) * (x < 0 ? -1 : 1)); }
 
+// complex slot of (device slot, frequency) in the wave-blocked DFT array
+inline size_t dft_at(size_t p, size_t i, size_t nf) { return ((p >> 6) * nf + i) * 64 + (p & 63); }
+
 // compute_boundary_weights (src/loop_in_chunks.cpp:257-300), snap_empty_dimensions = false
 void dft_boundary_weights(const mnl_structure &S, const double wmin[3], const double wmax[3],
                           const int is[3], const int ie[3], double s0[3], double e0[3],
@@ -1230,6 +1239,7 @@ int dft_add_flux(mnl_fields *F, int nreg, const double *regions, const double *f
       decim = 1;
   }
   o->decim = decim;
+  if (const char *e = getenv("MNL_DFT_BLOCK")) o->kb = std::max(1, std::min(DFT_KB, atoi(e)));
   const double dt_factor = F->dt / sqrt(2.0 * pi) * decim;
   std::vector<double> pwE, pwH;
   DftFluxH ho;  // H points collected separately, appended after the E points
@@ -1271,14 +1281,43 @@ int dft_add_flux(mnl_fields *F, int nreg, const double *regions, const double *f
   };
   lay(o->E);
   lay(o->H);
+  // per point and update: 3 indices + chunk id + weight, the averaged field
+  // values, the sample written and read back, and 1/kb of a read-modify-write
+  // of one complex value per frequency (DESIGN.md "DFT")
+  for (const auto *L : {&o->E, &o->H})
+    for (auto &dc : *L)
+      o->bytes += double(dc.N) * (12 + 4 + 8 + 8.0 * (1 << dc.avgmode) + 16 +
+                                  (12 + 4 + 32.0 * nfreq) / o->kb);
+  // Device slots: the points sorted by component, then z, y, x (x fastest like
+  // the field arrays), so that a wave's field reads are as contiguous as the
+  // plane's orientation allows; other ranks' points last.  Only the storage
+  // order changes -- every point keeps its own reference-order accumulation.
+  std::vector<int> ord(o->npts);
+  for (size_t p = 0; p < o->npts; p++) ord[p] = (int)p;
+  auto key = [&](int p) {
+    const int *j = &o->h_pj[3 * (size_t)p];
+    return std::make_tuple(j[0] < 0, chd[pch[p]].c, j[2], j[1], j[0], p);
+  };
+  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return key(a) < key(b); });
+  o->slot.assign(o->npts, 0);
+  std::vector<int> spj(3 * o->npts), spch(o->npts);
+  std::vector<double> spw(o->npts);
+  for (size_t t = 0; t < o->npts; t++) {
+    const int p = ord[t];
+    o->slot[p] = (int)t;
+    for (int e = 0; e < 3; e++) spj[3 * t + e] = o->h_pj[3 * (size_t)p + e];
+    spch[t] = pch[p];
+    spw[t] = pwE[p];
+  }
   if (o->npts) {
     if (dev_alloc(F, &o->d_pj, o->h_pj.size(), false) || dev_alloc(F, &o->d_pch, o->npts, false) ||
         dev_alloc(F, &o->d_pw, o->npts, false) || dev_alloc(F, &o->d_ch, chd.size(), false) ||
-        dev_alloc(F, &o->d_dft, 2 * o->npts * (size_t)nfreq))
+        dev_alloc(F, &o->d_dft, 2 * ((o->npts + 63) & ~size_t(63)) * (size_t)nfreq) ||
+        dev_alloc(F, &o->d_fr, o->npts * (size_t)o->kb))
       return -1;
-    HIPCHK(hipMemcpyAsync(o->d_pj, o->h_pj.data(), o->h_pj.size() * 4, hipMemcpyHostToDevice, F->stream));
-    HIPCHK(hipMemcpyAsync(o->d_pch, pch.data(), pch.size() * 4, hipMemcpyHostToDevice, F->stream));
-    HIPCHK(hipMemcpyAsync(o->d_pw, pwE.data(), pwE.size() * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(o->d_pj, spj.data(), spj.size() * 4, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(o->d_pch, spch.data(), spch.size() * 4, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(o->d_pw, spw.data(), spw.size() * 8, hipMemcpyHostToDevice, F->stream));
     HIPCHK(hipMemcpyAsync(o->d_ch, chd.data(), chd.size() * sizeof(DftChunkDev), hipMemcpyHostToDevice,
                           F->stream));
     HIPCHK(hipStreamSynchronize(F->stream));
@@ -1325,17 +1364,30 @@ int dft_prepare(mnl_fields *F, long long t0, int ns) {
   return 0;
 }
 
+// accumulate the buffered updates of one flux object
+int dft_flush(mnl_fields *F, DftFluxH &o) {
+  if (!o.nbuf) return 0;
+  const size_t nch = o.E.size() + o.H.size();
+  const long long rstride = (long long)(nch * o.nfreq);
+  if (k_dft_accum(o.d_pj, o.d_pch, o.d_dft, o.d_fr, o.nbuf,
+                  o.d_ph + 2 * (size_t)(o.row - o.nbuf) * rstride, rstride, o.nfreq,
+                  (long long)o.npts, F->stream))
+    return fail("dft accumulate launch failed");
+  o.nbuf = 0;
+  return 0;
+}
+
 // after step t (fields::update_dfts, src/dft.cpp:249-263)
 int dft_update(mnl_fields *F, long long t) {
   for (auto &op : F->dfts) {
     DftFluxH &o = *op;
     if (t % o.decim || !o.npts) continue;
-    const size_t nch = o.E.size() + o.H.size();
-    if (k_dft_update(o.d_pj, o.d_pw, o.d_pch, o.d_ch, o.d_dft,
-                     o.d_ph + 2 * (size_t)o.row * nch * o.nfreq, o.nfreq, (long long)o.npts, F->g,
-                     F->f, F->stream))
-      return fail("dft update launch failed");
+    if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, o.d_fr + (size_t)o.nbuf * o.npts,
+                     (long long)o.npts, F->g, F->f, F->stream))
+      return fail("dft sample launch failed");
+    o.nbuf++;
     o.row++;
+    if (o.nbuf == o.kb && dft_flush(F, o)) return -1;
   }
   return 0;
 }
@@ -1350,7 +1402,7 @@ int dft_flux_values(mnl_fields *F, int h, double *out) {
   if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
   DftFluxH &o = *F->dfts[h];
   const size_t nf = o.nfreq;
-  std::vector<double> v(2 * o.npts * nf);
+  std::vector<double> v(2 * ((o.npts + 63) & ~size_t(63)) * nf);
   if (!v.empty()) {
     HIPCHK(hipMemcpyAsync(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost, F->stream));
     HIPCHK(hipStreamSynchronize(F->stream));
@@ -1361,8 +1413,9 @@ int dft_flux_values(mnl_fields *F, int h, double *out) {
       const size_t pe = o.E[k].p0 + p, ph = o.H[k].p0 + p;
       if (o.h_pj[3 * pe] < 0 && o.h_pj[3 * pe + 1] < 0 && o.h_pj[3 * pe + 2] < 0) continue;
       for (size_t i = 0; i < nf; ++i) {
-        const cplx e(v[2 * (pe * nf + i)], v[2 * (pe * nf + i) + 1]);
-        const cplx hv(v[2 * (ph * nf + i)], v[2 * (ph * nf + i) + 1]);
+        const size_t ie = dft_at(o.slot[pe], i, nf), ih = dft_at(o.slot[ph], i, nf);
+        const cplx e(v[2 * ie], v[2 * ie + 1]);
+        const cplx hv(v[2 * ih], v[2 * ih + 1]);
         out[i] += real(e * conj(hv));
       }
     }
@@ -1959,7 +2012,7 @@ int set_fused(mnl_fields *F, bool on) {
   return 0;
 }
 
-enum { TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT, TM_GEN, TM_N };
+enum { TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT, TM_GEN, TM_DFT, TM_DFTF, TM_N };
 
 struct EvPair {
   hipEvent_t a, b;
@@ -2154,7 +2207,10 @@ int step_batch(mnl_fields *F, int nsteps) {
         return fail("E halo exchange failed");
       if (exchange(F, 3)) return fail("DFT halo exchange failed");
     }
-    return dft_update(F, tn);
+    const int k = ev_begin(TM_DFT);
+    const int r = dft_update(F, tn);
+    ev_end(k);
+    return r;
   };
   for (int s0 = 0; s0 < nsteps; s0 += CH) {
     int ns = std::min(CH, nsteps - s0);
@@ -2311,6 +2367,12 @@ int step_batch(mnl_fields *F, int nsteps) {
           std::swap(f.UB[d], f.UBn[d]);
         }
       if (post_step(s)) return -1;
+    }
+    if (!F->dfts.empty()) {
+      const int k = ev_begin(TM_DFTF);
+      for (auto &o : F->dfts)
+        if (dft_flush(F, *o)) return -1;
+      ev_end(k);
     }
     F->t += ns;
     if (flush_events() != 0) return -1;
@@ -2767,7 +2829,15 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
 
 int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch) {
-  if (!F || which < 0 || which > 2) return fail("bad kernel id");
+  if (!F || which < 0 || which > 3) return fail("bad kernel id");
+  if (which == 3) {  // DFT updates of one step (all flux objects)
+    *launches = F->timer_count[TM_DFT];
+    *total_ms = F->timer_ms[TM_DFT] + F->timer_ms[TM_DFTF];
+    double b = 0;
+    for (auto &o : F->dfts) b += o->bytes;
+    *bytes_per_launch = b;
+    return 0;
+  }
   // 0: lean fused kernel (or interior curl B when unfused), 1: interior curl D
   // (unfused), 2: general fused kernel
   int cat = which == 0 ? TM_BINT : (which == 1 ? TM_DINT : TM_GEN);
@@ -2837,7 +2907,7 @@ int mnl_fields_dft_data(mnl_fields *F, int h, int which, double *out, long long 
   if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
   const DftFluxH &o = *F->dfts[h];
   const size_t nf = o.nfreq;
-  std::vector<double> v(2 * o.npts * nf);
+  std::vector<double> v(2 * ((o.npts + 63) & ~size_t(63)) * nf);
   if (!v.empty()) {
     HIPCHK(hipStreamSynchronize(F->stream));
     HIPCHK(hipMemcpy(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost));
@@ -2847,8 +2917,8 @@ int mnl_fields_dft_data(mnl_fields *F, int h, int which, double *out, long long 
     for (size_t p = 0; p < dc.N; p++)
       for (size_t i = 0; i < nf; i++) {
         if (k + 2 > 2 * n) return fail("dft buffer too small");
-        out[k++] = v[2 * ((dc.p0 + p) * nf + i)];
-        out[k++] = v[2 * ((dc.p0 + p) * nf + i) + 1];
+        out[k++] = v[2 * dft_at(o.slot[dc.p0 + p], i, nf)];
+        out[k++] = v[2 * dft_at(o.slot[dc.p0 + p], i, nf) + 1];
       }
   return 0;
 }

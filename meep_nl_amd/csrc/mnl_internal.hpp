@@ -227,10 +227,16 @@ int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, co
 // E = chi1inv * D over box F (leaving fused mode / readout)
 int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *stream);
 int k_fill(double *p, double v, size_t n, void *stream);
-// dft_chunk::update_dft for every point of one flux object (src/dft.cpp:265-300)
-int k_dft_update(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch,
-                 double *dft, const double *ph, int nfreq, long long npts, const DevGrid &g,
-                 const DevFields &f, void *stream);
+// dft_chunk::update_dft for every point of one flux object (src/dft.cpp:265-300),
+// blocked over up to DFT_KB updates: sample the averaged field of one update
+// into fr, then accumulate n buffered updates (phases: n rows, rstride
+// complex values apart) into the DFT array
+constexpr int DFT_KB = 16;
+constexpr int DFT_FT = 16;  // frequency tile of the accumulation
+int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch, double *fr,
+                 long long npts, const DevGrid &g, const DevFields &f, void *stream);
+int k_dft_accum(const int *pj, const int *pch, double *dft, const double *fr, int n,
+                const double *ph, long long rstride, int nfreq, long long npts, void *stream);
 int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_type,
                      int comp_dir, int zlo_glob, void *stream);
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,

@@ -1879,20 +1879,26 @@ int k_materialize_e(const Box &F, const DevGrid &g, const DevFields &f, void *st
 }
 
 // ----------------------------------------------------------------- DFT
-// dft_chunk::update_dft (src/dft.cpp:265-300): thread = (point, frequency).
-// The field is averaged from the Yee points onto the cell centre exactly as
-// the reference does, (w*0.25)*(((f0 + f1) + f2) + f3); in fused mode E is
-// read through the implicit-E rule.
-__global__ void dft_update_kernel(const int *pj, const double *pw, const int *pch,
-                                  const DftChunkDev *ch, double *dft, const double *ph, int nfreq,
-                                  long long npts, DevGrid g, DevFields f) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= npts * nfreq) return;
-  const long long p = t / nfreq;
-  const int i = (int)(t - p * nfreq);
+// dft_chunk::update_dft (src/dft.cpp:265-300), split in two so that the DFT
+// array is read and written once per KB updates instead of once per update:
+//  * dft_sample_kernel (every DFT step): the field averaged from the Yee points
+//    onto the cell centre exactly as the reference does,
+//    (w*0.25)*(((f0 + f1) + f2) + f3) with the weight product precomputed on the
+//    host, into slot u of a small per-point buffer (E read through the
+//    implicit-E rule in fused mode);
+//  * dft_accum_kernel (every KB updates, and at the end of every step batch):
+//    dft += fr_u * phase_u for u = 0..n-1 in update order -- the reference's
+//    sequential accumulation, same operations in the same order, in registers.
+// The DFT array is blocked by wave, [slot/64][freq][slot%64] complex, so a
+// wave's access to one frequency is one contiguous 1-KB span.
+__global__ void dft_sample_kernel(const int *__restrict__ pj, const double *__restrict__ pw,
+                                  const int *__restrict__ pch, const DftChunkDev *__restrict__ ch,
+                                  double *__restrict__ fr_out, long long npts, DevGrid g,
+                                  DevFields f) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npts) return;
   if (pj[3 * p] < 0) return;  // another rank's point
-  const int k = pch[p];
-  const DftChunkDev cd = ch[k];
+  const DftChunkDev cd = ch[pch[p]];
   const int c = cd.c, d = c % 3;
   const bool mag = c >= 3;
   Pt P;
@@ -1927,19 +1933,86 @@ __global__ void dft_update_kernel(const int *pj, const double *pw, const int *pc
   } else {
     fr = pw[p] * val(P);
   }
-  const double pr = ph[2 * ((long long)k * nfreq + i)], pim = ph[2 * ((long long)k * nfreq + i) + 1];
-  double *dd = dft + 2 * (p * nfreq + i);
-  dd[0] = dd[0] + fr * pr;
-  dd[1] = dd[1] + fr * pim;
+  fr_out[p] = fr;
 }
 
-int k_dft_update(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch,
-                 double *dft, const double *ph, int nfreq, long long npts, const DevGrid &g,
-                 const DevFields &f, void *stream) {
-  const long long n = npts * nfreq;
-  if (n <= 0) return 0;
-  dft_update_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      pj, pw, pch, ch, dft, ph, nfreq, npts, g, f);
+// Accumulation: one thread per point; a tile of DFT_FT frequencies is loaded
+// into registers at once (DFT_FT independent loads in flight), every buffered
+// update is added in order, and the tile is stored back.  When the whole wave
+// belongs to one chunk (the usual case: slots are sorted by component and
+// position) the phases are wave-uniform and come through scalar loads.
+// one tile of FT frequencies at i0: FT independent loads in flight, every
+// buffered update added in order, FT stores
+template <int FT>
+__device__ __forceinline__ void dft_accum_tile(double2 *__restrict__ dp,
+                                               const double2 *__restrict__ php,
+                                               const double *frv, int n, long long rstride,
+                                               int i0) {
+  double2 v[FT];
+#pragma unroll
+  for (int w = 0; w < FT; w++) v[w] = dp[(i0 + w) * 64];
+#pragma unroll
+  for (int u = 0; u < DFT_KB; u++) {
+    if (u < n) {
+#pragma unroll
+      for (int w = 0; w < FT; w++) {
+        const double2 q = php[u * rstride + i0 + w];
+        v[w].x = v[w].x + frv[u] * q.x;
+        v[w].y = v[w].y + frv[u] * q.y;
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < FT; w++) dp[(i0 + w) * 64] = v[w];
+}
+
+// tiles of DFT_FT frequencies, then the remainder in tiles of 8, 4, 2, 1
+__device__ __forceinline__ void dft_accum_point(double2 *__restrict__ dp,
+                                                const double2 *__restrict__ php,
+                                                const double *frv, int n, long long rstride,
+                                                int nfreq) {
+  int i0 = 0;
+  for (; i0 + DFT_FT <= nfreq; i0 += DFT_FT) dft_accum_tile<DFT_FT>(dp, php, frv, n, rstride, i0);
+  if (nfreq - i0 >= 8) dft_accum_tile<8>(dp, php, frv, n, rstride, i0), i0 += 8;
+  if (nfreq - i0 >= 4) dft_accum_tile<4>(dp, php, frv, n, rstride, i0), i0 += 4;
+  if (nfreq - i0 >= 2) dft_accum_tile<2>(dp, php, frv, n, rstride, i0), i0 += 2;
+  if (nfreq - i0 >= 1) dft_accum_tile<1>(dp, php, frv, n, rstride, i0);
+}
+
+__global__ void __launch_bounds__(256)
+    dft_accum_kernel(const int *__restrict__ pj, const int *__restrict__ pch,
+                     double2 *__restrict__ dft, const double *__restrict__ fr, int n,
+                     const double2 *__restrict__ ph, long long rstride, int nfreq,
+                     long long npts) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npts) return;
+  if (pj[3 * p] < 0) return;
+  double frv[DFT_KB];
+#pragma unroll
+  for (int u = 0; u < DFT_KB; u++) frv[u] = u < n ? fr[u * npts + p] : 0.0;
+  double2 *__restrict__ dp = dft + (p >> 6) * nfreq * 64 + (p & 63);
+  const int k = pch[p];
+  const int k0 = __builtin_amdgcn_readfirstlane(k);
+  if (__all(k == k0))  // phases are wave-uniform: scalar loads
+    dft_accum_point(dp, ph + (long long)k0 * nfreq, frv, n, rstride, nfreq);
+  else
+    dft_accum_point(dp, ph + (long long)k * nfreq, frv, n, rstride, nfreq);
+}
+
+int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch, double *fr,
+                 long long npts, const DevGrid &g, const DevFields &f, void *stream) {
+  if (npts <= 0) return 0;
+  dft_sample_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      pj, pw, pch, ch, fr, npts, g, f);
+  return rc();
+}
+
+int k_dft_accum(const int *pj, const int *pch, double *dft, const double *fr, int n,
+                const double *ph, long long rstride, int nfreq, long long npts, void *stream) {
+  if (npts <= 0 || n <= 0) return 0;
+  if (n > DFT_KB || nfreq < 1) return 2;
+  dft_accum_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      pj, pch, (double2 *)dft, fr, n, (const double2 *)ph, rstride, nfreq, npts);
   return rc();
 }
 

@@ -8,8 +8,11 @@ non-averaged block geometry (epsilon, chi2, chi3, Lorentzian/Drude E
 susceptibilities) and point sources.  Everything runs on the MI355X through
 libmnl.so; there is no CPU path.
 """
+import inspect
 import math
+import numbers
 import os
+import time
 import warnings
 
 import numpy as np
@@ -266,6 +269,141 @@ def get_fluxes(f):
     return f.flux()
 
 
+# ---------------------------------------------------------------- step functions
+def _num_args(func):
+    code = getattr(func, "__code__", None)
+    if code is None:
+        return 1
+    n = code.co_argcount
+    return n - 1 if inspect.ismethod(func) else n
+
+
+def _eval_step_func(sim, func, todo):
+    """python/simulation.py:4999-5008"""
+    n = _num_args(func)
+    if n == 1:
+        if todo == "step":
+            func(sim)
+    elif n == 2:
+        func(sim, todo)
+    else:
+        raise ValueError(f"Step function '{func.__name__}' requires 1 or 2 arguments")
+
+
+def _when_true_funcs(cond, *step_funcs):
+    def _true(sim, todo):
+        if todo == "finish" or cond(sim):
+            for f in step_funcs:
+                _eval_step_func(sim, f, todo)
+    return _true
+
+
+def after_sources(*step_funcs):
+    """python/simulation.py:5023-5035"""
+    def _after_sources(sim, todo):
+        if sim.round_time() >= sim.fields.last_source_time():
+            for f in step_funcs:
+                _eval_step_func(sim, f, todo)
+    return _after_sources
+
+
+def after_time(t, *step_funcs):
+    return _when_true_funcs(lambda sim: sim.round_time() >= t, *step_funcs)
+
+
+def before_time(t, *step_funcs):
+    return _when_true_funcs(lambda sim: sim.round_time() < t, *step_funcs)
+
+
+def when_true(cond, *step_funcs):
+    return _when_true_funcs(cond, *step_funcs)
+
+
+def when_false(cond, *step_funcs):
+    return _when_true_funcs(lambda sim: not cond(sim), *step_funcs)
+
+
+def at_beginning(*step_funcs):
+    closure = {"done": False}
+
+    def _beg(sim, todo):
+        if not closure["done"]:
+            for f in step_funcs:
+                _eval_step_func(sim, f, todo)
+            closure["done"] = True
+    return _beg
+
+
+def at_end(*step_funcs):
+    def _end(sim, todo):
+        if todo == "finish":
+            for f in step_funcs:
+                _eval_step_func(sim, f, "step")
+            for f in step_funcs:
+                _eval_step_func(sim, f, "finish")
+    return _end
+
+
+def at_every(dt, *step_funcs):
+    """python/simulation.py:5096-5110"""
+    closure = {"tlast": 0.0}
+
+    def _every(sim, todo):
+        t = sim.round_time()
+        if todo == "finish" or t >= closure["tlast"] + dt + (-0.5 * sim.fields.dt):
+            for f in step_funcs:
+                _eval_step_func(sim, f, todo)
+            closure["tlast"] = t
+    return _every
+
+
+def during_sources(*step_funcs):
+    closure = {"finished": False}
+
+    def _during(sim, todo):
+        if sim.round_time() < sim.fields.last_source_time():
+            for f in step_funcs:
+                _eval_step_func(sim, f, "step")
+        elif not closure["finished"]:
+            for f in step_funcs:
+                _eval_step_func(sim, f, "finish")
+            closure["finished"] = True
+    return _during
+
+
+def combine_step_funcs(*step_funcs):
+    def _combine(sim, todo):
+        for f in step_funcs:
+            _eval_step_func(sim, f, todo)
+    return _combine
+
+
+def stop_when_fields_decayed(dt=None, c=None, pt=None, decay_by=None):
+    """python/simulation.py:5225-5273: every dt time units compare the maximum
+    |c(pt)|^2 of the last interval with the maximum so far."""
+    if dt is None or c is None or pt is None or decay_by is None:
+        raise ValueError("dt, c, pt, and decay_by are all required.")
+    closure = {"max_abs": 0, "cur_max": 0, "t0": 0}
+
+    def _stop(sim):
+        v = sim.get_field_point(c, pt)
+        fabs = abs(v) * abs(v)
+        closure["cur_max"] = max(closure["cur_max"], fabs)
+        if sim.round_time() <= dt + closure["t0"]:
+            return False
+        old_cur = closure["cur_max"]
+        closure["cur_max"] = 0
+        closure["t0"] = sim.round_time()
+        closure["max_abs"] = max(closure["max_abs"], old_cur)
+        return old_cur <= closure["max_abs"] * decay_by
+    return _stop
+
+
+def stop_after_walltime(t):
+    start = time.time()
+    return lambda sim: time.time() - start > t
+
+
 # ---------------------------------------------------------------- distributed
 def _dist_context():
     """(rank, world, local_rank, nccl_id) when launched one process per GPU by
@@ -422,26 +560,60 @@ class Simulation:
         return self.fields.t
 
     # -- running
-    def run(self, *step_funcs, until=None):
-        """Simulation.run(until=T) / _run_until (python/simulation.py:2795-2855)."""
+    def run(self, *step_funcs, until=None, until_after_sources=None):
+        """Simulation.run (python/simulation.py:4502-4540): until= a time, a condition
+        function or a list of them; until_after_sources= the same, counted from the
+        end of the sources (_run_sources_until, 2857-2876)."""
         self.init_sim()
-        if until is None:
-            raise ValueError("run() needs until=")
-        t, dt = self.fields._time()
-        t0 = float(np.float32(t * dt))
-        stop = t0 + until
-        if not step_funcs:
+        if until_after_sources is not None:
+            self._run_sources_until(until_after_sources, step_funcs)
+        elif until is not None:
+            self._run_until(until, step_funcs)
+        else:
+            raise ValueError("Invalid run configuration")
+
+    def _run_until(self, cond, step_funcs):
+        """python/simulation.py:2795-2855: stop when any condition holds; a number T
+        means round_time() >= t0 + T.  Step functions run before every step, once
+        more after the loop, then with 'finish'."""
+        self.init_sim()
+        conds = list(cond) if isinstance(cond, (list, tuple)) else [cond]
+        step_funcs = list(step_funcs)
+        t0 = self.round_time()
+        if not step_funcs and all(isinstance(c, numbers.Number) for c in conds):
+            # every condition is a time: count the steps on the host, step in one call
+            stop = t0 + min(conds)
+            t, dt = self.fields._time()
             n = 0
             while float(np.float32((t + n) * dt)) < stop:
                 n += 1
             self.fields.step(n)
             return
-        while self.round_time() < stop:
+        for i, c in enumerate(conds):
+            if isinstance(c, numbers.Number):
+                conds[i] = (lambda T: lambda sim: sim.round_time() >= t0 + T)(c)
+            elif not callable(c):
+                raise TypeError(f"Stopping condition {c} is not a number or a function")
+        while not any(c(self) for c in conds):
             for fn in step_funcs:
-                fn(self)
+                _eval_step_func(self, fn, "step")
             self.fields.step(1)
         for fn in step_funcs:
-            fn(self)
+            _eval_step_func(self, fn, "step")
+        for fn in step_funcs:
+            _eval_step_func(self, fn, "finish")
+
+    def _run_sources_until(self, cond, step_funcs):
+        self.init_sim()
+        conds = list(cond) if isinstance(cond, (list, tuple)) else [cond]
+        ts = self.fields.last_source_time()
+        new = []
+        for c in conds:
+            if isinstance(c, numbers.Number):
+                new.append((ts - self.round_time()) + c)
+            else:
+                new.append((lambda f: lambda sim: f(sim) and sim.round_time() >= ts)(c))
+        self._run_until(new, step_funcs)
 
     # -- flux spectra
     def add_flux(self, *args, **kwargs):

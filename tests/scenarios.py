@@ -462,7 +462,7 @@ def sc_flux_2d(make, xmax=10.0, ymax=10.0, ttot=130.0):
 FLUX3D_FREQS = [0.1, 0.15, 0.2, 0.27]
 
 
-def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=None):
+def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=None, freqs=None):
     """Waveguide (eps 12 core along x) + PML with four DFT flux objects: a box around
     the source (six faces, weights +-1), an x-normal plane across the whole cell
     (through the PML), a z-normal plane inside the lower PML, and a y-direction
@@ -483,6 +483,7 @@ def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=No
     o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
     o.add_gaussian_source(1, 0.2, 6.0, 0.0, 60.0, (-0.33, 0.12, 0.41), 0.7)
     hx, hy, hz = [0.5 * s for s in sizes]
+    FLUX3D_FREQS = list(freqs) if freqs is not None else globals()["FLUX3D_FREQS"]
     hs = [o.add_dft_flux(flux_box_faces([-0.42, -0.37, -0.33], [0.44, 0.51, 0.38], 3),
                          FLUX3D_FREQS, decimation),
           o.add_dft_flux([([0.83, -hy, -hz], [0.83, hy, hz], 0, 1.0)], FLUX3D_FREQS, decimation),

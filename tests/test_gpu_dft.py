@@ -48,12 +48,25 @@ def test_dft_flux_1d():
     _same_dft(p, o, hs)
 
 
-def test_dft_flux_3d_fused():
+@pytest.mark.parametrize("block", ["1", "3", "16"])
+def test_dft_flux_3d_fused(monkeypatch, block):
     """Fused stepping: E is implicit (chi1inv * D) inside the fused domain and the
-    DFT kernel must read it through the same rule."""
+    DFT sample kernel must read it through the same rule.  block = updates
+    accumulated per pass over the DFT array (MNL_DFT_BLOCK; 3 does not divide
+    the step count)."""
+    monkeypatch.setenv("MNL_DFT_BLOCK", block)
     p, hs = sc_flux_3d(ProductSim)
     assert p._fields().fused_active()
     o, _ = sc_flux_3d(make_oracle)
+    _same_dft(p, o, hs)
+
+
+@pytest.mark.parametrize("nfreq", [1, 21, 40])
+def test_dft_flux_3d_nfreq(nfreq):
+    """Frequency counts that exercise every accumulation tile (16, 8, 4, 2, 1)."""
+    fr = list(np.linspace(0.05, 0.3, nfreq))
+    p, hs = sc_flux_3d(ProductSim, freqs=fr, steps=40)
+    o, _ = sc_flux_3d(make_oracle, freqs=fr, steps=40)
     _same_dft(p, o, hs)
 
 
@@ -100,3 +113,34 @@ def test_dft_flux_slabs_2d():
     p, h1, h2 = sc_flux_2d(GroupSim3, ttot=40.0)
     o, _, _ = sc_flux_2d(make_oracle, ttot=40.0)
     _same_dft(p, o, [h1, h2], flux_exact=False)
+
+
+def test_simulation_flux_until_after_sources():
+    """meep.Simulation drop-in: add_flux(fcen, df, nfreq, FluxRegion) +
+    run(until_after_sources=stop_when_fields_decayed(...)) (python/simulation.py
+    2857-2876, 3470-3505, 5225-5273); the fluxes equal the oracle's after the same
+    number of steps, bit for bit."""
+    import meep_nl_amd as mp
+    from scenarios import vol
+    fcen, df = 1 / 3, 0.2
+    sim = mp.Simulation(cell_size=mp.Vector3(0, 0, 20), resolution=20, dimensions=1,
+                        boundary_layers=[mp.PML(1.0)],
+                        default_material=mp.Medium(index=1, chi3=1e-2),
+                        sources=[mp.Source(mp.GaussianSource(fcen, fwidth=df), component=mp.Ex,
+                                           center=mp.Vector3(0, 0, -8.0))])
+    fr = mp.FluxRegion(center=mp.Vector3(0, 0, 8.0))
+    trans = sim.add_flux(fcen, 4 * df, 7, fr)
+    pt = mp.Vector3(0, 0, 8.0)
+    sim.run(until_after_sources=mp.stop_when_fields_decayed(5, mp.Ex, pt, 1e-3))
+    assert sim.round_time() >= sim.fields.last_source_time()
+    steps = sim.timestep
+    w = 1 / df
+    o = vol(make_oracle, 1, [20.0], 20, center_origin=True)
+    o.add_pml(1.0)
+    o.set_chi3(0, np.full(o.shape(), 1e-2))
+    o.add_gaussian_source(0, fcen, w, 0.0, 2 * w * 5.0, (0, 0, -8.0), 1.0)
+    freqs = np.linspace(fcen - 2 * df, fcen + 2 * df, 7)
+    h = o.add_dft_flux([([0, 0, 8.0], [0, 0, 8.0], 2, 1.0)], freqs, 0)
+    o.step(steps)
+    np.testing.assert_array_equal(np.array(mp.get_fluxes(trans)), o.flux(h))
+    np.testing.assert_array_equal(mp.get_flux_freqs(trans), freqs)
