@@ -2056,6 +2056,8 @@ FusedArgs &fused_args(mnl_fields *F) {
   fa.uidx = F->d_uidx;
   fa.utab = F->d_utab;
   fa.ctr = F->d_fused_ctr;
+  fa.ngrp = 8;
+  if (const char *e = getenv("MNL_LEAN_GROUPS")) fa.ngrp = atoi(e) == 1 ? 1 : 8;
   return fa;
 }
 

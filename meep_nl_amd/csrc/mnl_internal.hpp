@@ -213,6 +213,8 @@ struct FusedArgs {
   int ngen_e, ngen_ne;          // leading items of chunk 0 (the early launch of multi-rank steps)
   int gbeg, gend, ctr_line;     // set per launch by k_fused: item range and counter line
   unsigned long long cbase;     // counter value at launch start (counters are never reset)
+  int ngrp;                     // lean work queues (1 or 8: one per XCD group, blockIdx % 8)
+  unsigned long long cbg[8];    // lean queue g: counter line g's value at launch start
   unsigned long long *ctr;      // 12 work-queue counters (128 B apart); see cbase
 };
 // which: 0 = lean tiles, 1 = all general tiles, 2 = general tiles of chunk 0

@@ -1510,17 +1510,25 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   }
   auto pu = [&](unsigned ui, int c) -> double { return sU[UMODE == 2 ? c : 0][(ui >> (8 * c)) & 255]; };
 
-  // one chunk-major work queue: consecutive items are neighbouring tiles of one
-  // chunk, so the workgroups sweep z roughly together
+  // Work queues, chunk-major: consecutive items are neighbouring tiles of one
+  // chunk, so the workgroups sweep z roughly together.  With ngrp = 8 the
+  // workgroups sharing an XCD (blockIdx % 8, observed round-robin placement;
+  // speed only) own a contiguous range of each chunk's tiles (x fastest), so
+  // the halo lines neighbouring tiles share are fetched once into that XCD's L2.
+  const int grp = a.ngrp > 1 ? (int)(blockIdx.x % a.ngrp) : 0;
+  const long long gt0 = ntile * grp / a.ngrp, gt1 = ntile * (grp + 1) / a.ngrp;
+  const long long gtile = gt1 - gt0;
+  unsigned long long *gctr = a.ctr + 16 * grp;
+  const unsigned long long gbase = a.ngrp > 1 ? a.cbg[grp] : a.cbase;
   for (;;) {
     if (threadIdx.x == 0) {
-      const unsigned long long v = atomicAdd(a.ctr, 1ULL) - a.cbase;
-      s_item = (long long)v < ntile * nlch ? (long long)v : -1;
+      const unsigned long long v = atomicAdd(gctr, 1ULL) - gbase;
+      s_item = (long long)v < gtile * nlch ? (long long)v : -1;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const long long item = s_item;
     if (item < 0) break;
-    int ch = (int)(item / ntile);  // lean chunk ordinal -> chunk index
+    int ch = (int)(item / gtile);  // lean chunk ordinal -> chunk index
     for (int r = 0; r < a.nlzr; r++) {
       const int n = a.lzr[r][1] - a.lzr[r][0] + 1;
       if (ch < n) {
@@ -1529,7 +1537,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
       }
       ch -= n;
     }
-    const int tile = (int)(item % ntile);
+    const int tile = (int)(gt0 + item % gtile);
     const int tx = a.lx0 + tile % nlx, ty = a.ly0 + tile / nlx;
     ItemGeo itg;
     itg.x0 = a.xb[tx];
@@ -1831,8 +1839,19 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
   dim3 grd((unsigned)nb), blk(1024);
   const bool d2 = a.dist == 2;
   FusedArgs l = a;
+  const long long ntile = (long long)(a.lx1 - a.lx0 + 1) * (a.ly1 - a.ly0 + 1);
+  l.ngrp = (a.ngrp > 1 && ntile >= 4 * a.ngrp && nb >= a.ngrp) ? a.ngrp : 1;
   l.cbase = bases[0];
-  bases[0] += (unsigned long long)total + nb;
+  if (l.ngrp == 1) {
+    bases[0] += (unsigned long long)total + nb;
+  } else {
+    for (int g = 0; g < l.ngrp; g++) {
+      l.cbg[g] = bases[g];
+      const long long tiles = ntile * (g + 1) / l.ngrp - ntile * g / l.ngrp;
+      const long long blocks = (nb - g + l.ngrp - 1) / l.ngrp;  // blockIdx % ngrp == g
+      bases[g] += (unsigned long long)(tiles * nlch + blocks);
+    }
+  }
 #define MNL_LAUNCH_FUSED(U)                                   \
   do {                                                        \
     if (d2)                                                   \
