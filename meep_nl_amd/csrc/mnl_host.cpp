@@ -229,6 +229,10 @@ struct mnl_fields {
   unsigned long long *d_fused_ctr = nullptr;  // work-item counters of the fused kernels
   unsigned long long ctr_base[12] = {0};      // their values at the next launch
   int stagger = 0, nstagger = 0;  // dev_alloc offset step (bytes) for field arrays
+  void *arena = nullptr;           // optional single allocation for field-sized arrays
+  size_t arena_cap = 0, arena_used = 0, arena_gap = 0;
+  int arena_req = 0;               // MNL_ARENA: field arrays to reserve (0: off)
+  bool contig = false;             // MNL_CONTIG: physically contiguous field allocations
   bool palette_tried = false;
   bool dsrc_in_shell = false;  // a D source point lies outside the interior box
   bool any_srcB = false, any_isrc = false;  // anywhere in the cell (all ranks agree)
@@ -288,9 +292,39 @@ template <class T>
 int dev_alloc(mnl_fields *F, T **p, size_t n, bool zero = true) {
   void *q = nullptr;
   const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  if (F->arena_req > 0 && !F->arena && F->nlocal && bytes >= (size_t(64) << 20)) {
+    const size_t cap = size_t(F->arena_req) * (F->nlocal * 8 + F->arena_gap + 4096);
+    const hipError_t ea = F->contig ? hipExtMallocWithFlags(&F->arena, cap, hipDeviceMallocContiguous)
+                                    : hipMalloc(&F->arena, cap);
+    if (ea == hipSuccess) {
+      F->arena_cap = cap;
+      F->dev_allocs.push_back(F->arena);
+    } else {
+      F->arena_req = 0;
+      (void)hipGetLastError();
+    }
+  }
+  if (F->arena_cap && bytes >= (size_t(64) << 20)) {  // field-sized: bump-allocate in the arena
+    const size_t at = (F->arena_used + 255) & ~size_t(255);
+    if (at + bytes <= F->arena_cap) {
+      F->arena_used = at + bytes + F->arena_gap;
+      *p = (T *)((char *)F->arena + at);
+      if (zero) {
+        hipError_t e = hipMemsetAsync(*p, 0, bytes, F->stream);
+        if (e != hipSuccess) return fail(std::string("hipMemset failed: ") + hipGetErrorString(e));
+      }
+      return 0;
+    }
+  }
   const bool big = bytes >= (size_t(64) << 20) && F->stagger > 0;
   const size_t off = big ? (size_t(F->stagger) * F->nstagger++) % (size_t(1) << 20) : 0;
-  hipError_t e = hipMalloc(&q, bytes + (big ? (size_t(1) << 20) : 0));
+  const size_t nb = bytes + (big ? (size_t(1) << 20) : 0);
+  hipError_t e = hipErrorUnknown;
+  if (F->contig && bytes >= (size_t(64) << 20)) {
+    e = hipExtMallocWithFlags(&q, nb, hipDeviceMallocContiguous);
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  if (e != hipSuccess) e = hipMalloc(&q, nb);
   if (e != hipSuccess) return fail(std::string("hipMalloc failed: ") + hipGetErrorString(e));
   if (zero) {
     e = hipMemsetAsync((char *)q + off, 0, bytes, F->stream);
@@ -2464,6 +2498,9 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
   if (const char *gc = getenv("MNL_GEN_CUS")) F->gen_cus = std::max(0, atoi(gc));
   if (const char *sg = getenv("MNL_STAGGER")) F->stagger = std::max(0, atoi(sg)) / 128 * 128;
+  if (const char *ar = getenv("MNL_ARENA")) F->arena_req = std::max(0, atoi(ar));
+  if (const char *cg = getenv("MNL_CONTIG")) F->contig = atoi(cg) != 0;
+  if (const char *ag = getenv("MNL_ARENA_GAP")) F->arena_gap = std::max(0, atoi(ag)) / 128 * 128;
   if (finalize_fields(F.get())) return nullptr;
   return F.release();
 }
