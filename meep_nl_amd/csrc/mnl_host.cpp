@@ -227,7 +227,7 @@ struct mnl_fields {
   int gen_cus = -1;  // CUs for the general kernel running beside the lean one (0: serial)
   bool fused_concurrent = false;  // last fused step ran lean + general concurrently
   unsigned long long *d_fused_ctr = nullptr;  // work-item counters of the fused kernels
-  unsigned long long ctr_base[12] = {0};      // their values at the next launch
+  unsigned long long ctr_base[FUSED_NCTR] = {0};  // their values at the next launch
   int stagger = 0, nstagger = 0;  // dev_alloc offset step (bytes) for field arrays
   void *arena = nullptr;           // optional single allocation for field-sized arrays
   size_t arena_cap = 0, arena_used = 0, arena_gap = 0;
@@ -1992,8 +1992,8 @@ int set_fused(mnl_fields *F, bool on) {
   DevFields &f = F->f;
   if (on == F->fused) return 0;
   if (on) {
-    if (!F->d_fused_ctr) {  // 8 lean queue counters + 4 general counters, 128 B apart
-      if (dev_alloc(F, &F->d_fused_ctr, 12 * 16)) return -1;
+    if (!F->d_fused_ctr) {  // FUSED_NCTR work-queue counters, 128 B apart
+      if (dev_alloc(F, &F->d_fused_ctr, FUSED_NCTR * 16)) return -1;
     }
     if (upload_fused_tables(F)) return -1;
     if (F->d_gitems_cap < F->gitems.size()) {
@@ -2090,8 +2090,10 @@ FusedArgs &fused_args(mnl_fields *F) {
   fa.uidx = F->d_uidx;
   fa.utab = F->d_utab;
   fa.ctr = F->d_fused_ctr;
-  fa.ngrp = 8;
-  if (const char *e = getenv("MNL_LEAN_GROUPS")) fa.ngrp = atoi(e) == 1 ? 1 : 8;
+  fa.ngrp = 1;  // lean queue groups (MNL_LEAN_GROUPS); general: MNL_GEN_GROUPS
+  if (const char *e = getenv("MNL_LEAN_GROUPS")) fa.ngrp = atoi(e) == 8 ? 8 : 1;
+  fa.ngrp_gen = 1;
+  if (const char *e = getenv("MNL_GEN_GROUPS")) fa.ngrp_gen = atoi(e) == 8 ? 8 : 1;
   return fa;
 }
 

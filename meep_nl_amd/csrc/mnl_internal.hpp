@@ -213,15 +213,19 @@ struct FusedArgs {
   int ngen_e, ngen_ne;          // leading items of chunk 0 (the early launch of multi-rank steps)
   int gbeg, gend, ctr_line;     // set per launch by k_fused: item range and counter line
   unsigned long long cbase;     // counter value at launch start (counters are never reset)
-  int ngrp;                     // lean work queues (1 or 8: one per XCD group, blockIdx % 8)
+  int ngrp;                     // work queues (1 or 8: one per XCD group, blockIdx % 8)
+  int ngrp_gen;                 // the same for the general kernels (k_fused copies it to ngrp)
   unsigned long long cbg[8];    // lean queue g: counter line g's value at launch start
-  unsigned long long *ctr;      // 12 work-queue counters (128 B apart); see cbase
+  unsigned long long *ctr;      // FUSED_NCTR work-queue counters (128 B apart); see cbase
 };
 // which: 0 = lean tiles, 1 = all general tiles, 2 = general tiles of chunk 0
 // only (early launch), 3 = the other general tiles.  Every launch reads old /
 // writes new buffers only, on disjoint points, so any order is valid.
-// bases[12]: host copy of each counter line's value, advanced by every launch
+// bases[FUSED_NCTR]: host copy of each counter line's value, advanced by every launch
 // (items + workgroups), so no counter reset (memset launch) is needed per step
+// counter lines: 0-7 lean queues, 8-11 general (wide/narrow x all/early, one
+// queue), FUSED_GLINE0 + (line - 8) * 8 + g: general line split per XCD group g
+constexpr int FUSED_GLINE0 = 16, FUSED_NCTR = 48;
 int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bases);
 int k_cu_count();
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],

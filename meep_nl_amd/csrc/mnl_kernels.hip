@@ -1405,12 +1405,19 @@ __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel
   __shared__ int s_item;
   if (UMODE == 2)
     for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) sU[i >> 8][i & 255] = a.utab[i];
-  const int base = a.gbeg, n = a.gend - a.gbeg;
-  unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
+  // ngrp > 1: the workgroups sharing an XCD (blockIdx % ngrp) take a contiguous
+  // share of the (chunk-major) item list from their own counter line
+  const int grp = a.ngrp > 1 ? (int)(blockIdx.x % a.ngrp) : 0;
+  const int ntot = a.gend - a.gbeg;
+  const int base = a.gbeg + (int)((long long)ntot * grp / a.ngrp);
+  const int n = a.gbeg + (int)((long long)ntot * (grp + 1) / a.ngrp) - base;
+  unsigned long long *ctr =
+      a.ctr + 16 * (a.ngrp > 1 ? FUSED_GLINE0 + (a.ctr_line - 8) * 8 + grp : a.ctr_line);
+  const unsigned long long cb = a.ngrp > 1 ? a.cbg[grp] : a.cbase;
   const int *yb = TX == 64 ? a.gyb : a.nyb;
   for (;;) {
     if (threadIdx.x == 0) {
-      const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
+      const unsigned long long v = atomicAdd(ctr, 1ULL) - cb;
       s_item = (long long)v < n ? a.gitems[base + v] : -1;
     }
     __syncthreads();  // also separates LDS use of consecutive items
@@ -1813,17 +1820,33 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
     long long cus = fused_grid_blocks(1);
     if (a.wg_limit > 0 && cus > a.wg_limit) cus = a.wg_limit;
     FusedArgs g = a;
+    // set up one launch over items [ib, ie) on counter line ln (grouped per XCD
+    // when there are enough workgroups and items)
+    auto setup = [&](int ib, int ie, int ln, unsigned nblk) {
+      g.gbeg = ib, g.gend = ie, g.ctr_line = ln, g.cbase = bases[ln];
+      const long long n = ie - ib;
+      g.ngrp = (a.ngrp_gen > 1 && nblk >= (unsigned)a.ngrp_gen && n >= 4LL * a.ngrp_gen) ? a.ngrp_gen : 1;
+      if (g.ngrp == 1) {
+        bases[ln] += (unsigned long long)n + nblk;
+        return;
+      }
+      for (int q = 0; q < g.ngrp; q++) {
+        const int L = FUSED_GLINE0 + (ln - 8) * 8 + q;
+        g.cbg[q] = bases[L];
+        const long long items = n * (q + 1) / g.ngrp - n * q / g.ngrp;
+        const long long blocks = ((long long)nblk - q + g.ngrp - 1) / g.ngrp;
+        bases[L] += (unsigned long long)(items + blocks);
+      }
+    };
     if (we > wb) {
-      g.gbeg = wb, g.gend = we, g.ctr_line = line, g.cbase = bases[line];
       const dim3 gr((unsigned)std::min<long long>(cus, we - wb)), b(64 * GenShape<64>::WAVES);
+      setup(wb, we, line, gr.x);
       launch_general<64>(g, um, gr, b, s);
-      bases[line] += (unsigned long long)(we - wb) + gr.x;
     }
     if (ne > nb_) {
-      g.gbeg = nb_, g.gend = ne, g.ctr_line = line + 1, g.cbase = bases[line + 1];
       const dim3 gr((unsigned)std::min<long long>(cus, ne - nb_)), b(64 * GenShape<16>::WAVES);
+      setup(nb_, ne, line + 1, gr.x);
       launch_general<16>(g, um, gr, b, s);
-      bases[line + 1] += (unsigned long long)(ne - nb_) + gr.x;
     }
     return hipPeekAtLastError() == hipSuccess ? 0 : 9;
   }
