@@ -78,6 +78,12 @@ int mnl_structure_set_chi3(mnl_structure *s, int comp, const double *host);
 int mnl_structure_add_lorentzian(mnl_structure *s, double omega0, double gamma, int drude,
                                  const double *sigma_x, const double *sigma_y,
                                  const double *sigma_z);
+/* Nonlinear E update: 0 = the fork (chi2 through Newton-Raphson where the
+ * 3x3 chi1inv is present, chi3 inert; default), 1 = upstream Meep (chi2/chi3
+ * through the Pade approximant calc_nonlinear_u, src/step_generic.cpp:546-553,
+ * on every E point including PML; diagonal chi1inv only).  Pinned by the
+ * reference's python/tests/test_3rd_harm_1d.py golden harmonics. */
+int mnl_structure_set_nonlinear_mode(mnl_structure *s, int mode);
 /* Fill chi1inv/chi2/Lorentz-sigma of axis-aligned boxes on the device (fast
  * setup for large grids; same values as passing 1/eps(loc) arrays with
  * eps_averaging=False).  box = {xmin,xmax,ymin,ymax,zmin,zmax} in length

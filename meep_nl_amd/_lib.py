@@ -28,6 +28,7 @@ _SIGS = {
     "mnl_structure_set_chi3": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_add_lorentzian": (c_int, [c_void, c_double, c_double, c_int, dptr, dptr, dptr]),
     "mnl_structure_set_box": (c_int, [c_void, c_int, c_int, dptr, c_double]),
+    "mnl_structure_set_nonlinear_mode": (c_int, [c_void, c_int]),
     "mnl_fields_create": (c_void, [c_void, c_int]),
     "mnl_fields_create_dist": (c_void, [c_void, c_int, c_int, c_int, ctypes.c_char_p]),
     "mnl_comm_unique_id": (c_int, [ctypes.c_char_p]),

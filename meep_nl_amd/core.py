@@ -133,6 +133,12 @@ class Structure:
         b = np.ascontiguousarray(box, dtype=np.float64)
         check(lib().mnl_structure_set_box(self.h, kind, index, ptr(b), float(value)))
 
+    def set_nonlinear_mode(self, mode):
+        """'fork' (default: chi2 through Newton-Raphson, chi3 inert) or 'upstream'
+        (upstream Meep's Pade chi2/chi3 update, src/step_generic.cpp:546-553)."""
+        m = {"fork": 0, "upstream": 1}[mode] if isinstance(mode, str) else int(mode)
+        check(lib().mnl_structure_set_nonlinear_mode(self.h, m))
+
 
 def _src_last_time(kind, params):
     """src_time::last_time(): gaussian float(peak_time + cutoff) with the cutoff

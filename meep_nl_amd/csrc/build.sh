@@ -13,6 +13,9 @@ hipcc --offload-arch=$ARCH -O3 -ffp-contract=off -fPIC -std=c++17 -Wall \
 CXXF="-O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$ROCM/include"
 g++ $CXXF -c "$HERE/mnl_host.cpp" -o "$TMP/mnl_host.o"
 g++ $CXXF -c "$HERE/mnl_comm.cpp" -o "$TMP/mnl_comm.o"
-hipcc --offload-arch=$ARCH -shared -fPIC -o "$OUT" "$TMP/mnl_kernels.o" "$TMP/mnl_host.o" \
-  "$TMP/mnl_comm.o" -L$ROCM/lib -lrccl -Wl,-rpath,$ROCM/lib
+# Link with g++ so the host's complex arithmetic (__muldc3 / __divdc3 of
+# std::complex) comes from libgcc as in the reference (and the oracle), not
+# from clang's compiler-rt, whose complex division rounds differently.
+g++ -shared -fPIC -o "$OUT" "$TMP/mnl_kernels.o" "$TMP/mnl_host.o" "$TMP/mnl_comm.o" \
+  -L$ROCM/lib -lamdhip64 -lrccl -Wl,-rpath,$ROCM/lib
 echo "built $OUT"

@@ -131,6 +131,7 @@ struct mnl_structure {
   std::vector<Lorentz> lor;
   std::vector<BoxSpec> boxes;
   size_t ntot;
+  int nl_mode = 0;  // 0: the fork (NR chi2, inert chi3); 1: upstream Meep (Pade chi2/chi3)
 
   int shift(int c, int d) const {
     if (!has[d]) return 0;
@@ -242,6 +243,7 @@ struct mnl_fields {
   bool allow_fused = true;
   CurlPlan planB, planD;
   bool nr = false;
+  bool upnl = false;  // upstream chi2/chi3 update active (nl_mode 1 with nonzero chi)
   // sources
   std::vector<SrcTime> srcs;
   std::vector<SrcGroup> groups;
@@ -703,7 +705,20 @@ int setup_materials(mnl_fields *F) {
   DevFields &f = F->f;
   // Newton-Raphson needed? chi2 nontrivial and both off-diagonal rows present.
   F->nr = false;
-  for (int c = 0; c < 3; c++) {
+  F->upnl = false;
+  if (S.nl_mode == 1) {  // upstream Meep: Pade chi2/chi3 on every E point, no NR
+    for (int c = 0; c < 3; c++)
+      for (const auto *v : {&S.chi2[c], &S.chi3[c]})
+        if (!v->empty() && !all_eq(*v, 0.0)) F->upnl = true;
+    for (auto &b : S.boxes) F->upnl = F->upnl || ((b.kind == 1 || b.kind == 2) && b.value != 0.0);
+    for (int c = 0; c < 3 && F->upnl; c++)
+      for (int k = 1; k <= 2; k++) {
+        const auto &od = S.chi1inv[c][(c + k) % 3];
+        if (!od.empty() && !all_eq(od, 0.0))
+          return fail("upstream nonlinear mode: off-diagonal epsilon is not supported");
+      }
+  }
+  for (int c = 0; c < 3 && !F->upnl; c++) {
     if (S.chi2[c].empty() || all_eq(S.chi2[c], 0.0)) continue;
     int d1 = (c + 1) % 3, d2 = (c + 2) % 3;
     if (!S.chi1inv[c][d1].empty() && !all_eq(S.chi1inv[c][d1], 0.0) &&
@@ -742,6 +757,15 @@ int setup_materials(mnl_fields *F) {
       if (upload_canonical(F, p, S.chi2[c], c)) return -1;
       f.chi2[c] = p;
     }
+    if (F->upnl) {  // both arrays on every E component (zeros where absent)
+      const std::vector<double> *src[2] = {&S.chi2[c], &S.chi3[c]};
+      for (int k = 0; k < 2; k++) {
+        double *p;
+        if (dev_alloc(F, &p, F->nlocal)) return -1;
+        if (!src[k]->empty() && upload_canonical(F, p, *src[k], c)) return -1;
+        (k == 0 ? f.chi2[c] : f.chi3[c]) = p;
+      }
+    }
   }
   // offdiag presence per reference chunk (zone box)
   std::vector<uint8_t> oz(27, 0);
@@ -771,6 +795,7 @@ int setup_materials(mnl_fields *F) {
   HIPCHK(hipMemcpyAsync(doz, oz.data(), 27, hipMemcpyHostToDevice, F->stream));
   f.offd_zone = doz;
   f.nr_enabled = F->nr ? 1 : 0;
+  f.upnl = F->upnl ? 1 : 0;
   // Lorentzian susceptibilities: pol list = reverse add order
   // (src/anisotropic_averaging.cpp:368-369, src/fields.cpp:266-282)
   int nl = (int)S.lor.size();
@@ -807,6 +832,8 @@ int setup_materials(mnl_fields *F) {
         invert = 1;
       } else if (b.kind == 1)
         dst = const_cast<double *>(f.chi2[c]);
+      else if (b.kind == 2)
+        dst = const_cast<double *>(f.chi3[c]);  // upstream mode only (null otherwise)
       else if (b.kind == 3 && b.index < nl)
         dst = const_cast<double *>(f.pol[nl - 1 - b.index].sigma[c]);
       if (!dst) continue;
@@ -1862,7 +1889,7 @@ bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
 }
 
 bool fused_possible(mnl_fields *F) {
-  if (!F->allow_fused || F->S.dim != 3 || F->nr) return false;
+  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->upnl) return false;
   if (F->any_srcB || F->any_isrc || F->any_dsrc_w) return false;
   // a D source inside a polarization box would need E recomputed after it
   // (local check; fused_agreed makes the decision collective)
@@ -2375,18 +2402,18 @@ int step_batch(mnl_fields *F, int nsteps) {
         return fail("curl D launch failed");
       ev_end(k);
       // shell curl D; the shell E update rides along when it only reads its own D
-      const bool fuseE = !F->nr && f.npol == 0 && nI == 0 && !F->dsrc_in_shell;
+      const bool fuseE = !F->nr && !F->upnl && f.npol == 0 && nI == 0 && !F->dsrc_in_shell;
       k = ev_begin(TM_D);
       if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream, fuseE))
         return fail("curl D launch failed");
       ev_end(k);
       if (nD && k_source(T_D, g, f, sD, 0, F->stream)) return fail("source launch failed");
-      if (F->nr && F->nranks > 1) {
+      if ((F->nr || F->upnl) && F->nranks > 1) {
         if (exchange(F, 2)) return fail("D halo exchange failed");
       }
       // ---- E (+ Lorentzian P)
       k = ev_begin(TM_E);
-      bool fuse = !F->nr;
+      bool fuse = !F->nr && !F->upnl;  // neighbour reads of D - P: P after all of E
       if ((!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) ||
           (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream)))
         return fail("update E launch failed");
@@ -2610,6 +2637,12 @@ int mnl_structure_add_lorentzian(mnl_structure *s, double omega0, double gamma, 
   s->lor.push_back(std::move(L));
   return 0;
 }
+int mnl_structure_set_nonlinear_mode(mnl_structure *s, int mode) {
+  if (!s || mode < 0 || mode > 1) return fail("nonlinear mode must be 0 (fork) or 1 (upstream)");
+  s->nl_mode = mode;
+  return 0;
+}
+
 int mnl_structure_set_box(mnl_structure *s, int kind, int index, const double box[6],
                           double value) {
   if (!s || kind < 0 || kind > 3) return fail("bad box kind");

@@ -89,6 +89,8 @@ struct DevFields {
   const double *inveps[3];   // diagonal chi1inv of E comps (null = trivial)
   const double *offd[3][2];  // chi1inv[ec][cycle(d,1)], [cycle(d,2)] (null = absent)
   const double *chi2[3];
+  const double *chi3[3];     // upstream nonlinear mode only (the fork's chi3 is inert)
+  int upnl;                  // 1: upstream chi2/chi3 Pade update of E (calc_nonlinear_u)
   int npol;
   PolDev pol[MAX_POL];       // in reference pol-list order (reverse of add order)
   PmlDev pml;

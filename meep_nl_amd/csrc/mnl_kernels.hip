@@ -439,6 +439,15 @@ __device__ __forceinline__ double dmp_at(const DevFields &f, const ISrcDev &is, 
   return v;
 }
 
+// calc_nonlinear_u (src/step_generic.cpp:546-553): the Pade approximant of the
+// upstream Meep chi2/chi3 update
+__device__ __forceinline__ double calc_nonlinear_u(double Dsqr, double Di, double chi1inv,
+                                                   double chi2, double chi3) {
+  double c2 = Di * chi2 * (chi1inv * chi1inv);
+  double c3 = Dsqr * chi3 * (chi1inv * chi1inv * chi1inv);
+  return (1 + c2 + 2 * c3) / (1 + 2 * c2 + 3 * c3);
+}
+
 // ----------------------------------------------------------------- E from D
 // update_eh(E_stuff) -> step_update_EDHB (src/update_eh.cpp:67-283,
 // src/step_generic.cpp:576-906) + lorentzian update_P (src/susceptibility.cpp:
@@ -466,10 +475,32 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
       pml = pml_at(f, g, d, kw);
     }
     double wv;  // the W field read by update_pols (f_w if allocated, else E)
+    double unl = 0;  // upstream mode: (g*u) * calc_nonlinear_u(...) (step_generic.cpp:668-702,
+                     // 853-884 as the fork comments them out; u = 1 where trivial)
+    if (f.upnl) {
+      const int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
+      const long long s = g.sdir[d];
+      auto nsum = [&](int e) {
+        const long long se = g.sdir[e];
+        return dmp_at<ISRC>(f, is, step, e, i) + dmp_at<ISRC>(f, is, step, e, i + s) +
+               dmp_at<ISRC>(f, is, step, e, i - se) + dmp_at<ISRC>(f, is, step, e, i + (s - se));
+      };
+      const double us = u ? u[i] : 1.0;
+      double dsq = gs * gs;
+      const bool h1 = f.ecomp_present[d1] != 0, h2 = f.ecomp_present[d2] != 0;
+      if (h1 && h2) {
+        const double g1s = nsum(d1), g2s = nsum(d2);
+        dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
+      } else if (h1 || h2) {
+        const double g1s = nsum(h1 ? d1 : d2);
+        dsq = gs * gs + 0.0625 * (g1s * g1s);
+      }
+      unl = (gs * us) * calc_nonlinear_u(dsq, gs, us, f.chi2[d][i], f.chi3[d][i]);
+    }
     if (pml) {
       double fwprev = f.WE[d][i];
       double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
-      double fw = u ? (gs * u[i]) : gs;
+      double fw = f.upnl ? unl : (u ? (gs * u[i]) : gs);
       f.WE[d][i] = fw;
       En[i] = E[i] + ((kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev);
       wv = fw;
@@ -532,7 +563,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
           }
         }
       }
-      if (!done) En[i] = u ? (gs * u[i]) : gs;
+      if (!done) En[i] = f.upnl ? unl : (u ? (gs * u[i]) : gs);
       wv = En[i];
     }
     if (FUSEPOL) {

@@ -425,7 +425,7 @@ class Simulation:
     def __init__(self, cell_size, resolution, geometry=(), sources=(), boundary_layers=(),
                  default_material=Medium(), Courant=0.5, eps_averaging=True, dimensions=None,
                  force_complex_fields=False, k_point=False, symmetries=(), parallel=None,
-                 **kwargs):
+                 nonlinear_mode="fork", **kwargs):
         self.cell_size = Vector3(*cell_size)
         self.resolution = float(resolution)
         self.geometry = list(geometry)
@@ -442,6 +442,9 @@ class Simulation:
                 dimensions = 1
         self.dimensions = dimensions
         self.parallel = parallel
+        # "upstream": Meep's Pade chi2/chi3 E update instead of the fork's (an
+        # extension; the fork's behaviour is the default)
+        self.nonlinear_mode = nonlinear_mode
         self.fields = None
         self.structure = None
         self.dft_objects = []
@@ -471,6 +474,8 @@ class Simulation:
     def _init_structure(self):
         gv = self._create_grid_volume()
         s = core.Structure(gv, self.Courant)
+        if self.nonlinear_mode != "fork":
+            s.set_nonlinear_mode(self.nonlinear_mode)
         for layer in self.boundary_layers:
             if not isinstance(layer, PML):
                 raise NotImplementedError("only PML boundary layers are supported")

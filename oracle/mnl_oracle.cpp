@@ -374,6 +374,7 @@ struct orc_sim {
   double courant = 0.5, dt = 0.05;
   long long t = 0;
   bool finalized = false;
+  bool upstream_nl = false;  // upstream Meep chi2/chi3 (Pade) instead of the fork's NR / inert chi3
   // PML requests: [dir][side]
   double pml_thick[3][2] = {{0, 0}, {0, 0}, {0, 0}};
   double pml_R[3][2], pml_stretch[3][2];
@@ -883,6 +884,48 @@ void step_source(orc_sim *s, int ftype) {
   }
 }
 
+// calc_nonlinear_u, src/step_generic.cpp:546-553 (the Pade approximant of the
+// upstream chi2/chi3 update; the fork only keeps it in comments)
+inline realnum calc_nonlinear_u(realnum Dsqr, realnum Di, realnum chi1inv, realnum chi2,
+                                realnum chi3) {
+  realnum c2 = Di * chi2 * (chi1inv * chi1inv);
+  realnum c3 = Dsqr * chi3 * (chi1inv * chi1inv * chi1inv);
+  return (1 + c2 + 2 * c3) / (1 + 2 * c2 + 3 * c3);
+}
+
+// Upstream-mode E update with diagonal chi1inv and chi2/chi3: the branches the
+// fork comments out (src/step_generic.cpp:668-702 PML, 853-884 non-PML):
+// f = (g*u) * calc_nonlinear_u(g^2 + (1/16)(g1s^2 + g2s^2), g, u, chi2, chi3),
+// g1s/g2s the four-point sums of the other D components; u = 1 where chi1inv
+// is trivial (deallocated).
+void update_upstream_nl(const GV &g, realnum *f, int fc, const realnum *gg, const realnum *g1,
+                        const realnum *g2, const realnum *u, long sd, long s1, long s2,
+                        const realnum *chi2, const realnum *chi3, realnum *fw, int dsigw,
+                        const realnum *sigw, const realnum *kapw) {
+  loop_owned(g, fc, [&](long i, const int p[3]) {
+    realnum gs = gg[i];
+    realnum us = u ? u[i] : 1;
+    realnum dsq = gs * gs;
+    if (g1 && g2) {
+      realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
+      realnum g2s = g2[i] + g2[i + sd] + g2[i - s2] + g2[i + (sd - s2)];
+      dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
+    } else if (g1) {
+      realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
+      dsq = gs * gs + 0.0625 * (g1s * g1s);
+    }
+    realnum v = (gs * us) * calc_nonlinear_u(dsq, gs, us, chi2[i], chi3[i]);
+    if (dsigw != NO_DIR) {
+      int kw = p[dsigw] - g.io[dsigw];
+      realnum fwprev = fw[i], kapwkw = kapw[kw], sigwkw = sigw[kw];
+      fw[i] = v;
+      f[i] += (kapwkw + sigwkw) * fw[i] - (kapwkw - sigwkw) * fwprev;
+    } else {
+      f[i] = v;
+    }
+  });
+}
+
 // step_update_EDHB, src/step_generic.cpp:576-906 (fork version)
 void step_update_EDHB(orc_sim *s, const GV &g, realnum *f, int fc, const realnum *gg,
                       const realnum *g1, const realnum *g2, const realnum *u, const realnum *u1,
@@ -894,6 +937,10 @@ void step_update_EDHB(orc_sim *s, const GV &g, realnum *f, int fc, const realnum
     std::swap(g1, g2);
     std::swap(u1, u2);
     std::swap(s1, s2);
+  }
+  if (s->upstream_nl && chi3 && !u1 && !u2) {
+    update_upstream_nl(g, f, fc, gg, g1, g2, u, sd, s1, s2, chi2, chi3, fw, dsigw, sigw, kapw);
+    return;
   }
   if (dsigw != NO_DIR) {  // PML: every u/chi branch reduces to fw = g*u (or g)
     loop_owned(g, fc, [&](long i, const int p[3]) {
@@ -1316,6 +1363,11 @@ int check_comp(const orc_sim *s, int c) {
 extern "C" {
 
 const char *orc_last_error(void) { return g_err.c_str(); }
+
+int orc_set_upstream_nl(orc_sim *s, int on) {
+  s->upstream_nl = on != 0;
+  return 0;
+}
 
 int orc_set_threads(int n) {
 #ifdef _OPENMP

@@ -35,6 +35,9 @@ int orc_step(orc_sim *s, int nsteps);
 int orc_get_field(orc_sim *s, int comp, const double pos[3], double *out);
 int orc_copy_component(orc_sim *s, int comp, double *out, size_t n);
 int orc_set_threads(int nthreads);
+/* upstream Meep chi2/chi3 update (Pade, src/step_generic.cpp:546-553 and the
+ * branches the fork comments out) instead of the fork's NR / inert chi3 */
+int orc_set_upstream_nl(orc_sim *s, int on);
 long long orc_t(orc_sim *s);
 double orc_dt(orc_sim *s);
 size_t orc_ntot(orc_sim *s);

@@ -58,6 +58,7 @@ def lib():
         L.orc_nr_failures.restype = ctypes.c_longlong
         L.orc_nr_failures.argtypes = [c_void]
         L.orc_set_threads.argtypes = [c_int]
+        L.orc_set_upstream_nl.argtypes = [c_void, c_int]
         L.orc_add_dft_flux.argtypes = [c_void, c_int, dptr, dptr, c_int, c_int]
         L.orc_dft_flux.argtypes = [c_void, c_int, dptr]
         L.orc_dft_size.restype = ctypes.c_longlong
@@ -226,6 +227,11 @@ class Oracle:
 
     def nr_random_fallbacks(self):
         return lib().orc_nr_failures(self.h)
+
+    def set_upstream_nl(self, on=True):
+        """Upstream Meep chi2/chi3 (Pade approximant) instead of the fork's NR /
+        inert chi3."""
+        _chk(lib().orc_set_upstream_nl(self.h, int(on)))
 
     # ---- DFT flux (fields::add_dft_flux, src/dft.cpp:578-640)
     def add_dft_flux(self, regions, freqs, decimation=0):

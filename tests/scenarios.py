@@ -101,6 +101,9 @@ class ProductSim:
     def add_dft_flux(self, regions, freqs, decimation=0):
         return self._fields().add_dft_flux(regions, freqs, decimation)
 
+    def set_upstream_nl(self, on=True):
+        self.s.set_nonlinear_mode("upstream" if on else "fork")
+
     def flux(self, h):
         return self._fields().flux(h)
 
@@ -511,3 +514,70 @@ def sc_flux_1d(make, steps=1500, chi3=1e-2):
           o.add_dft_flux(flux_box_faces([0, 0, -8.5], [0, 0, -7.3], 3), fr, 0)]
     o.step(steps)
     return o, hs
+
+
+def third_harmonic_1d(make, upstream=True, decay=1e-6):
+    """python/tests/test_3rd_harm_1d.py on the scenario interface: returns (sim,
+    flux(fcen), flux(3 fcen)) after run(until_after_sources=
+    stop_when_fields_decayed(50, Ex, pt, decay)) replayed step by step."""
+    sz, fcen, dpml, k = 100, 1 / 3.0, 1.0, 1e-2
+    df = fcen / 20
+    o = vol(make, 1, [sz], 20, center_origin=True)
+    o.add_pml(dpml)
+    if upstream:
+        o.set_upstream_nl(True)
+    o.set_chi3(0, np.full(o.shape(), k))
+    w = 1 / df
+    o.add_gaussian_source(0, fcen, w, 0.0, 2 * w * 5.0, (0, 0, -0.5 * sz + dpml), 1.0)
+    zf = 0.5 * sz - dpml - 0.5
+    reg = [([0, 0, zf], [0, 0, zf], 2, 1.0)]
+    h1 = o.add_dft_flux(reg, [fcen], 1)
+    h3 = o.add_dft_flux(reg, [3 * fcen], 1)
+    st, et = 0.0, 2 * w * 5.0  # last_source_time (src/meep.hpp:1024)
+    peak, cut = 0.5 * (st + et), (et - st) * 0.5
+    while math.exp(-cut * cut / (2 * w * w)) < 1e-100:
+        cut *= 0.9
+    ts = float(np.float32(peak + float(np.float32(cut))))
+    clo = {"max_abs": 0, "cur_max": 0, "t0": 0}
+
+    def stop():  # python/simulation.py:5250-5271
+        v = o.get_field(0, (0, 0, zf))
+        clo["cur_max"] = max(clo["cur_max"], abs(v) * abs(v))
+        if o.round_time() <= 50 + clo["t0"]:
+            return False
+        old = clo["cur_max"]
+        clo["cur_max"] = 0
+        clo["t0"] = o.round_time()
+        clo["max_abs"] = max(clo["max_abs"], old)
+        return old <= clo["max_abs"] * decay
+
+    while not (stop() and o.round_time() >= ts):
+        o.step(1)
+    return o, o.flux(h1)[0], o.flux(h3)[0]
+
+
+def sc_upstream_nl_3d(make, steps=50, lorentz=True, isrc=True, chi2=True, pml=True,
+                      upstream=True):
+    """Upstream-mode chi2 + chi3 slab (diagonal eps 2.25) crossing the PML boundary,
+    a Lorentzian in part of it (D - P neighbour reads), an integrated source and a
+    current source, strong fields (amp 40)."""
+    o = vol(make, 3, [3.2, 3.2, 3.2], 10, center_origin=True)
+    if pml:
+        o.add_pml(0.8)
+    if upstream:
+        o.set_upstream_nl(True)
+    sig = []
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        inside = np.abs(z - 0.2) < 0.9
+        o.set_chi1inv(c, c, np.where(inside, 1 / 2.25, 1.0))
+        o.set_chi3(c, np.where(inside, 2e-2, 0.0))
+        if chi2:
+            o.set_chi2(c, np.where(inside & (x > -0.5), 3e-2, 0.0))
+        sig.append(np.where(inside & (y > 0.2), 0.4, 0.0))
+    if lorentz:
+        o.add_lorentzian(1.3, 0.08, sig)
+    o.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -0.3), 40.0)
+    o.add_gaussian_source(1, 0.35, 4.0, 0.0, 40.0, (-0.4, 0.25, 0.35), 25.0, is_integrated=isrc)
+    o.step(steps)
+    return o

@@ -180,3 +180,20 @@ def test_fused_lorentz_toggle():
         o.add_gaussian_source(4, 0.3, 3.0, 0.0, 30.0, (1.0, 0.3, 2.2), 0.8)
     _bitwise(sc_big_lorentz_3d(ProductSim, extra=add_h),
              sc_big_lorentz_3d(make_oracle, extra=add_h))
+
+
+@pytest.mark.parametrize("freq,width,end", [(0.35, 10.0, 40.0), (0.35, 4.0, 100.0), (0.27, 3.0, 30.0)])
+def test_source_values_bitwise(freq, width, end):
+    """Per-step source amplitudes are computed on the host with libgcc's complex
+    arithmetic (__divdc3 / __muldc3, like the reference and the oracle): the
+    library is linked with g++ so clang's compiler-rt versions, which round
+    1/(-2*pi*f*i) differently for some f, are not pulled in."""
+    from scenarios import vol
+    res = []
+    for make in (ProductSim, make_oracle):
+        o = vol(make, 3, [1.6, 1.6, 1.6], 10, center_origin=True)
+        o.add_gaussian_source(2, freq, width, 0.0, end, (0.05, 0.05, 0.05), 1.0)
+        o.add_continuous_source(0, freq * 1.1, 2.0, 0.0, 1e20, 3.0, (-0.25, 0.15, 0.05), 0.5)
+        o.step(6)
+        res.append(o)
+    _bitwise(*res)

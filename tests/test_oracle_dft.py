@@ -67,3 +67,13 @@ def test_flux_1d_plane_wave_direction():
     assert np.all(o.flux(hs[1])[:3] > 0)
     e = o.dft_data(hs[0], 0)
     assert e.shape == (2 * 4,) and np.any(e != 0)
+
+
+def test_third_harmonic_upstream_golden(golden):
+    """Upstream-mode chi3 + DFT flux reproduce the reference's published harmonics
+    (python/tests/test_3rd_harm_1d.py:53, tolerance 1e-7 as the test uses)."""
+    from scenarios import third_harmonic_1d
+    g = golden["upstream_third_harmonic_1d"]
+    o, f1, f3 = third_harmonic_1d(make_oracle)
+    assert abs(f1 - g["flux_fcen"]) <= g["rel_tol"] * abs(g["flux_fcen"])
+    assert abs(f3 - g["flux_3fcen"]) <= g["rel_tol"] * abs(g["flux_3fcen"])
