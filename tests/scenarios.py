@@ -581,3 +581,42 @@ def sc_upstream_nl_3d(make, steps=50, lorentz=True, isrc=True, chi2=True, pml=Tr
     o.add_gaussian_source(1, 0.35, 4.0, 0.0, 40.0, (-0.4, 0.25, 0.35), 25.0, is_integrated=isrc)
     o.step(steps)
     return o
+
+
+def harmonics_cpp(make, chi2, chi3, J, upstream=True):
+    """tests/harmonics.cpp:27-80 on the scenario interface: 1-D cell 110 @ res 20,
+    PML 5, chi2 / chi3 everywhere, integrated Ex source gaussian_src_time(1/3,
+    1/60) (C++ default: is_integrated) at z = -50, single-frequency DFT fluxes at
+    f, 2f, 3f at z = 49.5; stepped until time() >= last_source_time(), then in
+    50-unit rounds until the round's max |Ex| < 1e-6 of the overall max.
+    Returns (sim, A2, A3) = (flux(2f) / flux(f), flux(3f) / flux(f))."""
+    dpml, res, freq = 5.0, 20, 1.0 / 3.0
+    sz = 100 + 2 * dpml
+    o = vol(make, 1, [sz], res, center_origin=True)
+    o.add_pml(dpml)
+    if upstream:
+        o.set_upstream_nl(True)
+    o.set_chi2(0, np.full(o.shape(), chi2))
+    o.set_chi3(0, np.full(o.shape(), chi3))
+    w = 1.0 / (freq / 20)  # gaussian_src_time(f, fwidth, s = 5): peak = cutoff = 5 w
+    o.add_gaussian_source(0, freq, w, 0.0, 10 * w, (0, 0, -0.5 * sz + dpml), J, is_integrated=True)
+    zf = 0.5 * sz - dpml - 0.5
+    hs = [o.add_dft_flux([([0, 0, zf], [0, 0, zf], 2, 1.0)], [k * freq], 1) for k in (1, 2, 3)]
+    cut = 5 * w
+    while math.exp(-cut * cut / (2 * w * w)) < 1e-100:
+        cut *= 0.9
+    last = float(np.float32(5 * w + float(np.float32(cut))))
+    emax = 0.0
+    while o.t * o.dt < last:
+        emax = max(emax, abs(o.get_field(0, (0, 0, zf))))
+        o.step(1)
+    while True:
+        emaxcur, T = 0.0, o.t * o.dt + 50
+        while o.t * o.dt < T:
+            e = abs(o.get_field(0, (0, 0, zf)))
+            emax, emaxcur = max(emax, e), max(emaxcur, e)
+            o.step(1)
+        if emaxcur < 1e-6 * emax:
+            break
+    f1, f2, f3 = (o.flux(h)[0] for h in hs)
+    return o, f2 / f1, f3 / f1

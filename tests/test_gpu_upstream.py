@@ -69,3 +69,20 @@ def test_upstream_3d_bitwise():
 @pytest.mark.parametrize("G", [GroupSim, GroupSim3])
 def test_upstream_3d_slabs(G):
     _bitwise(sc_upstream_nl_3d(G), sc_upstream_nl_3d(make_oracle))
+
+
+def test_harmonics_cpp_golden_and_scaling(golden):
+    """tests/harmonics.cpp on the GPU: the known 2nd/3rd harmonic ratios (rel 1e-5),
+    bitwise equal to the oracle, and the test's scaling checks (doubling chi2 and
+    chi3 -> 4x both ratios; doubling J -> 4x / 16x; within 1 %)."""
+    from scenarios import harmonics_cpp
+    g = golden["upstream_harmonics_cpp"]
+    p, a2, a3 = harmonics_cpp(ProductSim, 0.27e-4, 1e-4, 1.0)
+    assert abs(a2 - g["A2"]) <= g["rel_tol"] * g["A2"]
+    assert abs(a3 - g["A3"]) <= g["rel_tol"] * g["A3"]
+    o, b2, b3 = harmonics_cpp(make_oracle, 0.27e-4, 1e-4, 1.0)
+    assert (a2, a3) == (b2, b3) and p.t == o.t
+    _, c2, c3 = harmonics_cpp(ProductSim, 0.54e-4, 2e-4, 1.0)
+    assert abs(c2 / a2 - 4.0) <= 0.04 and abs(c3 / a3 - 4.0) <= 0.04
+    _, j2, j3 = harmonics_cpp(ProductSim, 0.27e-4, 1e-4, 2.0)
+    assert abs(j2 / a2 - 4.0) <= 0.04 and abs(j3 / a3 - 16.0) <= 0.16

@@ -77,3 +77,13 @@ def test_third_harmonic_upstream_golden(golden):
     o, f1, f3 = third_harmonic_1d(make_oracle)
     assert abs(f1 - g["flux_fcen"]) <= g["rel_tol"] * abs(g["flux_fcen"])
     assert abs(f3 - g["flux_3fcen"]) <= g["rel_tol"] * abs(g["flux_3fcen"])
+
+
+def test_harmonics_cpp_upstream_golden(golden):
+    """tests/harmonics.cpp:114-122: 2nd / 3rd harmonic ratios of the upstream chi2 /
+    chi3 update measured through single-frequency DFT fluxes (rel 1e-5)."""
+    from scenarios import harmonics_cpp
+    g = golden["upstream_harmonics_cpp"]
+    _, a2, a3 = harmonics_cpp(make_oracle, 0.27e-4, 1e-4, 1.0)
+    assert abs(a2 - g["A2"]) <= g["rel_tol"] * g["A2"]
+    assert abs(a3 - g["A3"]) <= g["rel_tol"] * g["A3"]
