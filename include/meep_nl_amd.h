@@ -162,7 +162,9 @@ int mnl_fields_traffic_model(mnl_fields *f, double *bytes_per_cell_step, double 
  * magnetic or integrated sources).  Results are identical either way. */
 int mnl_fields_set_fused(mnl_fields *f, int allow);
 /* bit 0: the last step ran the fused interior kernel; bit 1: it read chi1inv
- * through the palette (DESIGN.md "chi1inv palette"). */
+ * through the palette (DESIGN.md "chi1inv palette"); bit 2: field arrays are
+ * requested physically contiguous; bits 8-15: how many such requests the
+ * driver could not satisfy (plain allocations instead). */
 int mnl_fields_mode(mnl_fields *f, int *fused);
 /* Enable HIP-event timing around every sub-step kernel group (on the stream
  * the kernels run on) and reset the accumulated timers. */

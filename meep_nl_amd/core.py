@@ -282,6 +282,12 @@ class Fields:
         check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
         return bool(v.value & 2)
 
+    def alloc_info(self):
+        """(contiguous field allocations requested, requests that fell back)."""
+        v = ctypes.c_int()
+        check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
+        return bool(v.value & 4), (v.value >> 8) & 255
+
     def set_fused(self, allow=True):
         check(lib().mnl_fields_set_fused(self.h, int(allow)))
 

@@ -234,6 +234,7 @@ struct mnl_fields {
   size_t arena_cap = 0, arena_used = 0, arena_gap = 0;
   int arena_req = 0;               // MNL_ARENA: field arrays to reserve (0: off)
   bool contig = false;             // MNL_CONTIG: physically contiguous field allocations
+  int contig_fallbacks = 0;        // contiguous requests the driver could not satisfy
   bool palette_tried = false;
   bool dsrc_in_shell = false;  // a D source point lies outside the interior box
   bool any_srcB = false, any_isrc = false;  // anywhere in the cell (all ranks agree)
@@ -324,7 +325,10 @@ int dev_alloc(mnl_fields *F, T **p, size_t n, bool zero = true) {
   hipError_t e = hipErrorUnknown;
   if (F->contig && bytes >= (size_t(64) << 20)) {
     e = hipExtMallocWithFlags(&q, nb, hipDeviceMallocContiguous);
-    if (e != hipSuccess) (void)hipGetLastError();
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      F->contig_fallbacks++;
+    }
   }
   if (e != hipSuccess) e = hipMalloc(&q, nb);
   if (e != hipSuccess) return fail(std::string("hipMalloc failed: ") + hipGetErrorString(e));
@@ -2946,7 +2950,8 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
 
 int mnl_fields_mode(mnl_fields *F, int *fused) {
   if (!F) return fail("null fields");
-  *fused = (F->fused ? 1 : 0) | (F->fused && F->d_uidx ? 2 : 0);
+  *fused = (F->fused ? 1 : 0) | (F->fused && F->d_uidx ? 2 : 0) | (F->contig ? 4 : 0) |
+           (std::min(F->contig_fallbacks, 255) << 8);
   return 0;
 }
 

@@ -17,4 +17,4 @@ for seg in range(6):
     t0 = time.perf_counter()
     f.step(30)
     out.append((time.perf_counter() - t0) / 30 * 1e3)
-print("segments ms/step:", " ".join(f"{v:.3f}" for v in out))
+print("segments ms/step:", " ".join(f"{v:.3f}" for v in out), "alloc", f.alloc_info())
