@@ -72,6 +72,14 @@ int mnl_structure_set_chi1inv(mnl_structure *s, int comp, int dir, const double 
  * inert in the fork (src/step_generic.cpp:829-886) and only recorded. */
 int mnl_structure_set_chi2(mnl_structure *s, int comp, const double *host);
 int mnl_structure_set_chi3(mnl_structure *s, int comp, const double *host);
+/* structure::set_conductivity(c, C) (src/structure.cpp:425-437, chunk part
+ * 868-905): conductivity of D or B component comp (an E / H component names
+ * its D / B array; E values are multiplied by the diagonal chi1inv set so
+ * far, as the reference does).  Enters step_curl's conductivity branches
+ * (src/step_generic.cpp:89-229) with cndinv = 1/(1 + cnd dt/2)
+ * (src/structure.cpp:693-707) and scales current sources by cndinv
+ * (src/step.cpp:300-309).  NULL resets to zero. */
+int mnl_structure_set_conductivity(mnl_structure *s, int comp, const double *host);
 /* structure::add_susceptibility(sigma, E_stuff, lorentzian_susceptibility(
  * omega0, gamma, drude)) -- src/anisotropic_averaging.cpp:300-372, isotropic
  * (diagonal sigma per E component; NULL = 0). */

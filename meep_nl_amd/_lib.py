@@ -26,6 +26,7 @@ _SIGS = {
     "mnl_structure_set_chi1inv": (c_int, [c_void, c_int, c_int, dptr]),
     "mnl_structure_set_chi2": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_set_chi3": (c_int, [c_void, c_int, dptr]),
+    "mnl_structure_set_conductivity": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_add_lorentzian": (c_int, [c_void, c_double, c_double, c_int, dptr, dptr, dptr]),
     "mnl_structure_set_box": (c_int, [c_void, c_int, c_int, dptr, c_double]),
     "mnl_structure_set_nonlinear_mode": (c_int, [c_void, c_int]),

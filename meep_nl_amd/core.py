@@ -122,6 +122,13 @@ class Structure:
     def set_chi3(self, comp, arr):
         check(lib().mnl_structure_set_chi3(self.h, comp, ptr(self._arr(arr))))
 
+    def set_conductivity(self, comp, arr):
+        """structure::set_conductivity(c, C) (src/structure.cpp:868-905): D or B
+        component (E / H name their D / B array; E values are multiplied by the
+        diagonal chi1inv set so far).  None resets to zero."""
+        a = None if arr is None else self._arr(arr)
+        check(lib().mnl_structure_set_conductivity(self.h, comp, None if a is None else ptr(a)))
+
     def add_lorentzian(self, omega0, gamma, sigmas, drude=False):
         s = [None if v is None else self._arr(v) for v in sigmas]
         check(lib().mnl_structure_add_lorentzian(self.h, omega0, gamma, int(drude),

@@ -128,6 +128,7 @@ struct mnl_structure {
   double pml_R[3][2], pml_stretch[3][2];
   std::vector<double> chi1inv[3][3];  // [E comp][dir], canonical
   std::vector<double> chi2[3], chi3[3];
+  std::vector<double> cond[2][3];     // conductivity of [B, D][dir], canonical (empty = 0)
   std::vector<Lorentz> lor;
   std::vector<BoxSpec> boxes;
   size_t ntot;
@@ -704,6 +705,55 @@ bool nontrivial_in_zone(const mnl_structure &S, const std::vector<double> &arr, 
   return false;
 }
 
+std::vector<ZoneIv> zone_ivs_or_one(const mnl_structure &S, int d) {
+  if (S.has[d]) return zone_intervals(S, d);
+  return {{0, 0, 1}};
+}
+
+// Conductivity of the D and B components: cnd and cndinv = 1/(1 + cnd*dt*0.5)
+// (structure_chunk::update_condinv, src/structure.cpp:693-707) where nonzero
+// anywhere; f_cond where a PML lies along dsig = cycle(d, 1); per reference
+// chunk, whether its conductivity array survives the trivial test
+// (src/structure.cpp:898-901) -- that selects the f_cond branch of step_curl.
+int setup_conductivity(mnl_fields *F) {
+  const mnl_structure &S = F->S;
+  DevFields &f = F->f;
+  std::vector<uint8_t> cz(27, 0);
+  bool any = false;
+  for (int t = 0; t < 2; t++)
+    for (int d = 0; d < 3; d++) {
+      const int comp = 3 * (t ? T_D : T_B) + d;
+      const auto &cv = S.cond[t][d];
+      if (!has_field(S, comp) || cv.empty() || all_eq(cv, 0.0)) continue;
+      any = true;
+      std::vector<double> inv(cv.size());
+      for (size_t i = 0; i < cv.size(); i++) inv[i] = 1 / (1 + cv[i] * F->dt * 0.5);
+      double *pc, *pi;
+      if (dev_alloc(F, &pc, F->nlocal) || dev_alloc(F, &pi, F->nlocal)) return -1;
+      if (upload_canonical(F, pc, cv, comp) || upload_canonical(F, pi, inv, comp)) return -1;
+      f.cnd[t][d] = pc;
+      f.cndinv[t][d] = pi;
+      const int dsig = (d + 1) % 3;
+      if (S.has[dsig] && F->pml_any[dsig] && dev_alloc(F, &f.fcnd[t][d], F->nlocal)) return -1;
+      auto ivx = zone_ivs_or_one(S, 0), ivy = zone_ivs_or_one(S, 1), ivz = zone_ivs_or_one(S, 2);
+      for (auto &zx : ivx)
+        for (auto &zy : ivy)
+          for (auto &zz : ivz) {
+            const ZoneIv *zv[3] = {&zx, &zy, &zz};
+            if (nontrivial_in_zone(S, cv, comp, zv, 0.0))
+              cz[zx.zone * 9 + zy.zone * 3 + zz.zone] |= 1 << (3 * t + d);
+          }
+    }
+  f.cnd_dt2 = F->dt * 0.5;
+  if (!any) return 0;
+  uint8_t *dcz;
+  if (dev_alloc(F, &dcz, 27)) return -1;
+  HIPCHK(hipMemcpyAsync(dcz, cz.data(), 27, hipMemcpyHostToDevice, F->stream));
+  HIPCHK(hipStreamSynchronize(F->stream));
+  f.cnd_zone = dcz;
+  return 0;
+}
+
 int setup_materials(mnl_fields *F) {
   const mnl_structure &S = F->S;
   DevFields &f = F->f;
@@ -798,6 +848,7 @@ int setup_materials(mnl_fields *F) {
   if (dev_alloc(F, &doz, 27)) return -1;
   HIPCHK(hipMemcpyAsync(doz, oz.data(), 27, hipMemcpyHostToDevice, F->stream));
   f.offd_zone = doz;
+  if (setup_conductivity(F)) return -1;
   f.nr_enabled = F->nr ? 1 : 0;
   f.upnl = F->upnl ? 1 : 0;
   // Lorentzian susceptibilities: pol list = reverse add order
@@ -1896,6 +1947,9 @@ bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
 
 bool fused_possible(mnl_fields *F) {
   if (!F->allow_fused || F->S.dim != 3 || F->nr || F->upnl) return false;
+  for (int t = 0; t < 2; t++)
+    for (int d = 0; d < 3; d++)
+      if (F->f.cnd[t][d]) return false;
   if (F->any_srcB || F->any_isrc || F->any_dsrc_w) return false;
   // a D source inside a polarization box would need E recomputed after it
   // (local check; fused_agreed makes the decision collective)
@@ -2621,6 +2675,22 @@ int mnl_structure_set_chi2(mnl_structure *s, int comp, const double *host) {
   s->chi2[comp].assign(host, host + s->ntot);
   return 0;
 }
+int mnl_structure_set_conductivity(mnl_structure *s, int comp, const double *host) {
+  // structure_chunk::set_conductivity (src/structure.cpp:868-905): E/H name the
+  // D/B array; an E value is multiplied by the current diagonal chi1inv
+  if (!s || comp < 0 || comp >= MNL_NUM_COMPONENTS) return fail("invalid component for conductivity");
+  const int t = ctype(comp), d = cdir(comp), tb = (t == T_D || t == T_E) ? 1 : 0;
+  auto &dst = s->cond[tb][d];
+  if (!host) {
+    dst.clear();
+    return 0;
+  }
+  dst.assign(host, host + s->ntot);
+  if (t == T_E && !s->chi1inv[d][d].empty())
+    for (size_t i = 0; i < s->ntot; i++) dst[i] = host[i] * s->chi1inv[d][d][i];
+  return 0;
+}
+
 int mnl_structure_set_chi3(mnl_structure *s, int comp, const double *host) {
   if (!s || comp < MNL_EX || comp > MNL_EZ) return fail("chi3: E components only");
   s->chi3[comp].assign(host, host + s->ntot);  // inert in the fork
@@ -3032,6 +3102,9 @@ int mnl_fields_traffic_model(mnl_fields *F, double *bpc, double *cells) {
     for (int k = 0; k < F->f.npol; k++)
       for (int d = 0; d < 3; d++)
         if (F->f.pol[k].P[d]) b += 8.0 * 5;
+    for (int t = 0; t < 2; t++)  // cnd and cndinv read per conductive component
+      for (int d = 0; d < 3; d++)
+        if (F->f.cnd[t][d]) b += 8.0 * 2;
   }
   *bpc = b;
   double c = 1;

@@ -106,6 +106,16 @@ struct DevFields {
   // wherever it is owned and not in a PML chunk along its own direction
   int fused;
   Box fG;
+  // conductivity (structure_chunk::conductivity/condinv of the D and B
+  // components, src/structure.cpp:693-707, 868-905), [0] = B, [1] = D; null =
+  // zero everywhere.  fcnd: f_cond, the auxiliary field of PML chunks along
+  // dsig with conductivity (src/step_db.cpp:67-70).  cnd_zone: per zone box,
+  // bit 3*t+d set if conductivity[t][d] is allocated in that chunk.
+  const double *cnd[2][3];
+  const double *cndinv[2][3];
+  double *fcnd[2][3];
+  const uint8_t *cnd_zone;
+  double cnd_dt2;            // dt * 0.5 (src/step_generic.cpp:92)
 };
 
 // Point sources in rank-local linear indices.

@@ -111,8 +111,23 @@ __device__ __forceinline__ bool e_implicit(const DevFields &f, const DevGrid &g,
   return owned(g, T_E, c, p) && !pml_at(f, g, c, qcoord(g, p, T_E, c, c));
 }
 
+// conductivity allocated in the reference chunk that owns point p (zone box)
+__device__ __forceinline__ bool cnd_in_chunk(const DevFields &f, const DevGrid &g, const Pt &p,
+                                             int FT, int d) {
+  int zb = 0;
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    const int z = g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, FT, d, e)] : 1;  // absent: middle
+    zb = zb * 3 + z;
+  }
+  return (f.cnd_zone[zb] >> (3 * (FT == T_D) + d)) & 1;
+}
+
 // Apply one curl update with the per-point PML branch selection of step_curl
-// (src/step_generic.cpp:84-252, cnd == NULL).
+// (src/step_generic.cpp:84-252).  With conductivity (cnd != null) the
+// cnd branches apply; where cnd == 0 they equal the cnd-free ones bit for bit
+// ((1 - 0)*f - x)*1), except the f_cond form of a PML chunk along dsig, which
+// is taken only where the chunk holds a conductivity array (cnd_in_chunk).
 template <int FT>
 __device__ __forceinline__ double curl_apply(const DevFields &f, const DevGrid &g, const Pt &p,
                                              int d, long long i, double T, double dtdx) {
@@ -121,29 +136,44 @@ __device__ __forceinline__ double curl_apply(const DevFields &f, const DevGrid &
   const int dsig = (d + 1) % 3, dsigu = (d + 2) % 3;
   const int k = qcoord(g, p, FT, d, dsig), ku = qcoord(g, p, FT, d, dsigu);
   const bool ps = pml_at(f, g, dsig, k), pu = pml_at(f, g, dsigu, ku);
+  const int t = FT == T_D;
+  const double *cnd = f.cnd[t][d], *cndinv = f.cndinv[t][d];
+  const double dt2 = f.cnd_dt2;
   double nv;
   if (!ps && !pu) {
-    nv = Fo[i] - dtdx * T;
+    nv = cnd ? ((1 - dt2 * cnd[i]) * Fo[i] - dtdx * T) * cndinv[i] : Fo[i] - dtdx * T;
   } else if (!ps) {
     const double *U = FT == T_B ? f.UB[d] : f.UD[d];
     double *Un = FT == T_B ? f.UBn[d] : f.UD[d];
     const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
     double fprev = U[i];
-    double fu = fprev - dtdx * T;
+    double fu = cnd ? ((1 - dt2 * cnd[i]) * fprev - dtdx * T) * cndinv[i] : fprev - dtdx * T;
     Un[i] = fu;
     nv = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
-  } else if (!pu) {
-    const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
-    nv = ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
   } else {
-    const double *U = FT == T_B ? f.UB[d] : f.UD[d];
-    double *Un = FT == T_B ? f.UBn[d] : f.UD[d];
     const double *sig = f.pml.sig[dsig], *kap = f.pml.kap[dsig], *siginv = f.pml.siginv[dsig];
-    const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
-    double fprev = U[i];
-    double fu = ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
-    Un[i] = fu;
-    nv = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
+    const bool fc = cnd && cnd_in_chunk(f, g, p, FT, d);
+    double x = 0;  // the f_cond difference (f_cond chunks only)
+    if (fc) {
+      double *FC = f.fcnd[t][d];
+      const double fcnd_prev = FC[i];
+      const double fcn = ((1 - dt2 * cnd[i]) * fcnd_prev - dtdx * T) * cndinv[i];
+      FC[i] = fcn;
+      x = fcn - fcnd_prev;
+    }
+    if (!pu) {
+      nv = fc ? ((kap[k] - sig[k]) * Fo[i] + x) * siginv[k]
+              : ((kap[k] - sig[k]) * Fo[i] - dtdx * T) * siginv[k];
+    } else {
+      const double *U = FT == T_B ? f.UB[d] : f.UD[d];
+      double *Un = FT == T_B ? f.UBn[d] : f.UD[d];
+      const double *sigu = f.pml.sig[dsigu], *kapu = f.pml.kap[dsigu], *siginvu = f.pml.siginv[dsigu];
+      double fprev = U[i];
+      double fu = fc ? ((kap[k] - sig[k]) * fprev + x) * siginv[k]
+                     : ((kap[k] - sig[k]) * fprev - dtdx * T) * siginv[k];
+      Un[i] = fu;
+      nv = siginvu[ku] * ((kapu[ku] - sigu[ku]) * Fo[i] + fu - fprev);
+    }
   }
   F[i] = nv;
   return nv;
@@ -185,7 +215,7 @@ __device__ __forceinline__ void fused_point_update(const DevFields &f, const Dev
 
 // ----------------------------------------------------------------- curl B / D
 // fields_chunk::step_db -> step_curl (src/step_db.cpp:44-146,
-// src/step_generic.cpp:69-253, conductivity-free branches).  Component d of
+// src/step_generic.cpp:69-253, conductivity as in curl_apply).  Component d of
 // B (D): g1 = E (H) comp (d+2)%3 along dir (d+1)%3, g2 = comp (d+1)%3 along
 // dir (d+2)%3; D uses negated strides (src/step_db.cpp:81-84).
 template <int FT, bool SHELL, bool FUSEUP>
@@ -250,7 +280,11 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
     if (!SHELL) {
       const double *Fo = FT == T_B ? f.B[d] : f.D[d];
       double *F = FT == T_B ? f.Bn[d] : f.Dn[d];
-      F[i] = Fo[i] - dtdx * T;
+      const double *cnd = f.cnd[FT == T_D][d];
+      if (cnd)  // src/step_generic.cpp:91-103
+        F[i] = ((1 - f.cnd_dt2 * cnd[i]) * Fo[i] - dtdx * T) * f.cndinv[FT == T_D][d][i];
+      else
+        F[i] = Fo[i] - dtdx * T;
       continue;
     }
     const double nv = curl_apply<FT>(f, g, p, d, i, T, dtdx);
@@ -606,15 +640,21 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, BoxL
 }
 
 // ----------------------------------------------------------------- sources
-// fields_chunk::step_source (src/step.cpp:296-319): f -= real(amp*J*dt),
-// applied in source-list order by a single lane (exact sequential semantics).
+// fields_chunk::step_source (src/step.cpp:296-319): f -= real(amp*J*dt), times
+// cndinv with conductivity (real((A*dt)*cndinv) = real(A*dt)*cndinv), applied
+// in source-list order by a single lane (exact sequential semantics).
 struct Ptr3 {
   double *p[3];
+  const double *ci[3];
 };
 __global__ void source_kernel(Ptr3 pt, SrcDev s, int step) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   const double *v = s.val + (long long)step * s.n;
-  for (int k = 0; k < s.n; k++) pt.p[s.comp[k]][s.idx[k]] -= v[k];
+  for (int k = 0; k < s.n; k++) {
+    const int c = s.comp[k];
+    const long long i = s.idx[k];
+    pt.p[c][i] -= pt.ci[c] ? v[k] * pt.ci[c][i] : v[k];
+  }
 }
 
 __global__ void fill_kernel(double *p, double v, size_t n) {
@@ -807,7 +847,10 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
   (void)g;
   if (s.n == 0) return 0;
   Ptr3 pt;
-  for (int d = 0; d < 3; d++) pt.p[d] = ft == T_D ? f.Dn[d] : f.Bn[d];
+  for (int d = 0; d < 3; d++) {
+    pt.p[d] = ft == T_D ? f.Dn[d] : f.Bn[d];
+    pt.ci[d] = f.cndinv[ft == T_D][d];
+  }
   source_kernel<<<1, 64, 0, (hipStream_t)stream>>>(pt, s, step);
   return rc();
 }

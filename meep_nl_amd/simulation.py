@@ -82,7 +82,9 @@ class DrudeSusceptibility(LorentzianSusceptibility):
 
 class Medium:
     def __init__(self, epsilon=1.0, epsilon_diag=None, epsilon_offdiag=None, E_chi2=0.0,
-                 E_chi3=0.0, chi2=None, chi3=None, E_susceptibilities=(), index=None, mu=1.0):
+                 E_chi3=0.0, chi2=None, chi3=None, E_susceptibilities=(), index=None, mu=1.0,
+                 D_conductivity=None, B_conductivity=None, D_conductivity_diag=None,
+                 B_conductivity_diag=None):
         if index is not None:
             epsilon = index * index
         self.epsilon_diag = Vector3(*(epsilon_diag if epsilon_diag is not None else
@@ -92,6 +94,11 @@ class Medium:
         self.E_chi2 = float(chi2 if chi2 is not None else E_chi2)
         self.E_chi3 = float(chi3 if chi3 is not None else E_chi3)
         self.E_susceptibilities = list(E_susceptibilities)
+        # python/geom.py Medium: a scalar *_conductivity sets the whole diagonal
+        self.D_conductivity_diag = Vector3(*(D_conductivity_diag if D_conductivity_diag is not None
+                                             else (D_conductivity or 0.0,) * 3))
+        self.B_conductivity_diag = Vector3(*(B_conductivity_diag if B_conductivity_diag is not None
+                                             else (B_conductivity or 0.0,) * 3))
         if mu != 1.0:
             raise NotImplementedError("magnetic materials (mu != 1) are outside the hot-path scope")
 
@@ -532,6 +539,17 @@ class Simulation:
                 sus_sig[key][d] = table(sig)
         for key in sus_keys:
             s.add_lorentzian(key[0], key[1], sus_sig[key], drude=key[2])
+        # structure::set_materials -> set_conductivity(c, mat) for the D and B
+        # components with nonzero conductivity (src/structure.cpp:378-380, 868-905),
+        # sampled at each component's own Yee points
+        for attr, base in (("D_conductivity_diag", Dx), ("B_conductivity_diag", Bx)):
+            if not any(getattr(m, attr) != Vector3() for m in media):
+                continue
+            for d in ((0,) if base == Dx else (1,)) if self.dimensions == 1 else (0, 1, 2):
+                c = base + d
+                which, mats = self._materials_at(gv, c)
+                s.set_conductivity(c, np.array([getattr(m, attr)[d] for m in mats],
+                                               dtype=np.float64)[which])
         self.structure = s
         return s
 

@@ -11,7 +11,9 @@
 //     (src/structure.cpp:118-137, 509-523) with per-chunk sigma/kappa
 //     profiles (src/structure.cpp:657-691) -- the region-dependent
 //     arithmetic (PML formula with sigma=0 vs plain formula) follows.
-//   * step_curl (src/step_generic.cpp:69-253, conductivity-free branches),
+//   * step_curl (src/step_generic.cpp:69-253, with the conductivity
+//     branches; per-chunk trivial conductivity arrays, src/structure.cpp:
+//     693-707, 868-905),
 //     step_update_EDHB (src/step_generic.cpp:576-906) with the fork's
 //     diagonal-only epsilon^-1, inert chi3 and the chi2 Newton-Raphson branch
 //     (src/step_generic.cpp:730-816, src/newton_raphson.cpp:93-359).
@@ -26,7 +28,7 @@
 //     (src/vec.cpp:528-621, src/monitor.cpp:127-160).
 //
 // Not restated (out of the configs' scope): cylindrical coordinates, Bloch
-// phases / periodic boundaries, symmetries, conductivity, magnetic
+// phases / periodic boundaries, symmetries, magnetic
 // materials, anisotropic Lorentzian, subpixel averaging, DFT/flux.
 //
 // Parity is pinned against the reference's own golden values
@@ -345,6 +347,8 @@ struct Chunk {
   bool h_alias[3] = {true, true, true};  // H aliases B (src/fields.cpp:493-517)
   std::vector<realnum> fu[NCOMP], fw[NCOMP], fmp[NCOMP];
   std::vector<realnum> chi1inv[NCOMP][3], chi2[NCOMP], chi3[NCOMP];
+  // structure_chunk::conductivity[c][d_c] / condinv of D and B comps, f_cond
+  std::vector<realnum> cond[NCOMP], condinv[NCOMP], fcond[NCOMP];
   std::vector<std::vector<realnum>> psigma;  // per susceptibility: [3 E comps] flattened
   std::vector<std::vector<realnum> *> dummy;
   std::vector<PolData> pol;
@@ -385,6 +389,7 @@ struct orc_sim {
   bool have_plus[NCOMP], have_minus[NCOMP];
   // global material inputs (canonical layout), kept until finalize
   std::vector<realnum> g_chi1inv[NCOMP][3], g_chi2[NCOMP], g_chi3[NCOMP];
+  std::vector<realnum> g_cond[NCOMP];  // D / B comps
   std::vector<Lorentz> lor;
   std::vector<std::vector<realnum>> g_lsig[3];  // per E-comp dir: per susceptibility
   std::vector<SrcTime> srcs;
@@ -665,6 +670,19 @@ void finalize(orc_sim *s) {
         }
       }
     }
+    // conductivity (src/structure.cpp:868-905): trivial chunk arrays are
+    // deleted; condinv = 1/(1 + cnd*dt*0.5) (update_condinv, 693-707)
+    for (int c = 0; c < NCOMP; c++) {
+      if (s->g_cond[c].empty() || !G.has_field(c)) continue;
+      scatter_to_chunk(G, ch, c, s->g_cond[c], ch.cond[c]);
+      if (all_equal(ch.cond[c], 0.0)) {
+        ch.cond[c].clear();
+        continue;
+      }
+      ch.condinv[c].resize(ch.cond[c].size());
+      for (size_t i = 0; i < ch.cond[c].size(); i++)
+        ch.condinv[c][i] = 1 / (1 + ch.cond[c][i] * s->dt * 0.5);
+    }
     // susceptibilities: chiP list is prepended (anisotropic_averaging.cpp:368-369),
     // so the pol list order is the reverse of the add order.
     size_t nl = s->lor.size();
@@ -785,11 +803,12 @@ void step_boundaries_P(orc_sim *s) {  // PE_stuff
 }
 
 // ---------------------------------------------------------------- step_curl
-// src/step_generic.cpp:69-253 (cnd == NULL branches).
+// src/step_generic.cpp:69-253.
 void step_curl(const GV &g, int c, realnum *f, const realnum *g1, const realnum *g2, long s1,
                long s2, realnum dtdx, int dsig, const realnum *sig, const realnum *kap,
                const realnum *siginv, realnum *fu, int dsigu, const realnum *sigu,
-               const realnum *kapu, const realnum *siginvu) {
+               const realnum *kapu, const realnum *siginvu, realnum dt, const realnum *cnd,
+               const realnum *cndinv, realnum *fcnd) {
   if (!g1) {
     std::swap(g1, g2);
     std::swap(s1, s2);
@@ -799,14 +818,23 @@ void step_curl(const GV &g, int c, realnum *f, const realnum *g1, const realnum 
     return g2 ? g1[i + s1] - g1[i] + g2[i] - g2[i + s2] : g1[i + s1] - g1[i];
   };
   auto kidx = [&](int dsg, const int p[3]) { return p[dsg] - g.io[dsg]; };  // KSTRIDE_DEF/KDEF
+  const realnum dt2 = dt * 0.5;
   if (dsig == NO_DIR) {
     if (dsigu == NO_DIR) {
-      loop_owned(g, c, [&](long i, const int *) { f[i] -= dtdx * curl(i); });
+      if (cnd)  // 91-103
+        loop_owned(g, c, [&](long i, const int *) {
+          f[i] = ((1 - dt2 * cnd[i]) * f[i] - dtdx * curl(i)) * cndinv[i];
+        });
+      else
+        loop_owned(g, c, [&](long i, const int *) { f[i] -= dtdx * curl(i); });
     } else {
       loop_owned(g, c, [&](long i, const int p[3]) {
         int ku = kidx(dsigu, p);
         realnum fprev = fu[i];
-        fu[i] -= dtdx * curl(i);
+        if (cnd)  // 118-137
+          fu[i] = ((1 - dt2 * cnd[i]) * fprev - dtdx * curl(i)) * cndinv[i];
+        else
+          fu[i] -= dtdx * curl(i);
         f[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * f[i] + fu[i] - fprev);
       });
     }
@@ -814,13 +842,25 @@ void step_curl(const GV &g, int c, realnum *f, const realnum *g1, const realnum 
     if (dsigu == NO_DIR) {
       loop_owned(g, c, [&](long i, const int p[3]) {
         int k = kidx(dsig, p);
-        f[i] = ((kap[k] - sig[k]) * f[i] - dtdx * curl(i)) * siginv[k];
+        if (cnd) {  // 162-181
+          realnum fcnd_prev = fcnd[i];
+          fcnd[i] = ((1 - dt2 * cnd[i]) * fcnd[i] - dtdx * curl(i)) * cndinv[i];
+          f[i] = ((kap[k] - sig[k]) * f[i] + (fcnd[i] - fcnd_prev)) * siginv[k];
+        } else {
+          f[i] = ((kap[k] - sig[k]) * f[i] - dtdx * curl(i)) * siginv[k];
+        }
       });
     } else {
       loop_owned(g, c, [&](long i, const int p[3]) {
         int k = kidx(dsig, p), ku = kidx(dsigu, p);
         realnum fprev = fu[i];
-        fu[i] = ((kap[k] - sig[k]) * fu[i] - dtdx * curl(i)) * siginv[k];
+        if (cnd) {  // 201-228 (the most general case)
+          realnum fcnd_prev = fcnd[i];
+          fcnd[i] = ((1 - dt2 * cnd[i]) * fcnd[i] - dtdx * curl(i)) * cndinv[i];
+          fu[i] = ((kap[k] - sig[k]) * fu[i] + (fcnd[i] - fcnd_prev)) * siginv[k];
+        } else {
+          fu[i] = ((kap[k] - sig[k]) * fu[i] - dtdx * curl(i)) * siginv[k];
+        }
         f[i] = siginvu[ku] * ((kapu[ku] - sigu[ku]) * f[i] + fu[i] - fprev);
       });
     }
@@ -848,6 +888,9 @@ void step_db(orc_sim *s, int ftype) {
       const realnum *f_m = hm ? ch.F(s->minus_c[cc]) : nullptr;
       if (hp && !s->allocated[s->plus_c[cc]]) f_p = nullptr;
       if (hm && !s->allocated[s->minus_c[cc]]) f_m = nullptr;
+      const realnum *cnd = ch.cond[cc].empty() ? nullptr : ch.cond[cc].data();
+      if (dsig != NO_DIR && cnd && ch.fcond[cc].empty())  // step_db.cpp:67-70
+        ch.fcond[cc].assign(g.ntot, 0.0);
       if (dsigu != NO_DIR && ch.fu[cc].empty()) ch.fu[cc] = ch.f[cc];  // memcpy of f
       if (ftype == T_D) {
         stride_p = -stride_p;
@@ -861,12 +904,14 @@ void step_db(orc_sim *s, int ftype) {
                 ch.fu[cc].empty() ? nullptr : ch.fu[cc].data(), dsigu,
                 dsigu == NO_DIR ? nullptr : ch.sig[dsigu].data(),
                 dsigu == NO_DIR ? nullptr : ch.kap[dsigu].data(),
-                dsigu == NO_DIR ? nullptr : ch.siginv[dsigu].data());
+                dsigu == NO_DIR ? nullptr : ch.siginv[dsigu].data(), s->dt, cnd,
+                cnd ? ch.condinv[cc].data() : nullptr,
+                ch.fcond[cc].empty() ? nullptr : ch.fcond[cc].data());
     }
   }
 }
 
-// fields_chunk::step_source, src/step.cpp:296-319 (no conductivity)
+// fields_chunk::step_source, src/step.cpp:296-319
 void step_source(orc_sim *s, int ftype) {
   for (auto &ch : s->chunks) {
     auto &list = ftype == T_D ? ch.srcD : ch.srcB;
@@ -876,9 +921,12 @@ void step_source(orc_sim *s, int ftype) {
       int c = tcomp(ftype, cdir(sv.c));
       realnum *f = ch.f[c].empty() ? nullptr : ch.f[c].data();
       if (!f) continue;
+      const realnum *cndinv = ch.condinv[c].empty() ? nullptr : ch.condinv[c].data();
       for (size_t j = 0; j < sv.idx.size(); j++) {
-        const cplx A = (sv.amp[j] * st.current_current) * s->dt;
-        f[sv.idx[j]] -= real(A);
+        const long i = sv.idx[j];
+        const cplx A = cndinv ? (sv.amp[j] * st.current_current) * s->dt * double(cndinv[i])
+                              : (sv.amp[j] * st.current_current) * s->dt;
+        f[i] -= real(A);
       }
     }
   }
@@ -1436,6 +1484,22 @@ int orc_set_chi2(orc_sim *s, int comp, const double *arr) {
   if (s->finalized) return set_err("structure already finalized");
   if (comp < Ex || comp > Ez) return set_err("chi2: E components only");
   s->g_chi2[comp].assign(arr, arr + s->gv.ntot);
+  return 0;
+}
+// structure::set_conductivity (src/structure.cpp:425-437, 868-905): E / H name
+// the D / B array, E values multiplied by the diagonal chi1inv set so far
+int orc_set_conductivity(orc_sim *s, int comp, const double *arr) {
+  if (s->finalized) return set_err("structure already finalized");
+  if (comp < 0 || comp >= NCOMP) return set_err("invalid component for conductivity");
+  const int t = comp / 3, d = comp % 3;
+  const int cc = (t == T_E || t == T_D) ? tcomp(T_D, d) : tcomp(T_B, d);
+  if (!arr) {
+    s->g_cond[cc].clear();
+    return 0;
+  }
+  s->g_cond[cc].assign(arr, arr + s->gv.ntot);
+  if (t == T_E && !s->g_chi1inv[comp][d].empty())
+    for (size_t i = 0; i < s->gv.ntot; i++) s->g_cond[cc][i] = arr[i] * s->g_chi1inv[comp][d][i];
   return 0;
 }
 int orc_set_chi3(orc_sim *s, int comp, const double *arr) {

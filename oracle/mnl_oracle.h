@@ -26,6 +26,8 @@ int orc_add_pml(orc_sim *s, int dir, int side, double thickness, double R, doubl
 int orc_set_chi1inv(orc_sim *s, int comp, int dir, const double *arr);
 int orc_set_chi2(orc_sim *s, int comp, const double *arr);
 int orc_set_chi3(orc_sim *s, int comp, const double *arr);
+/* structure::set_conductivity (src/structure.cpp:868-905); D/B (or E/H) comp */
+int orc_set_conductivity(orc_sim *s, int comp, const double *arr);
 int orc_add_lorentzian(orc_sim *s, double omega0, double gamma, int drude, const double *sx,
                        const double *sy, const double *sz);
 int orc_add_point_source(orc_sim *s, int comp, int kind, const double *params, int nparams,

@@ -42,6 +42,7 @@ def lib():
         L.orc_set_chi1inv.argtypes = [c_void, c_int, c_int, dptr]
         L.orc_set_chi2.argtypes = [c_void, c_int, dptr]
         L.orc_set_chi3.argtypes = [c_void, c_int, dptr]
+        L.orc_set_conductivity.argtypes = [c_void, c_int, dptr]
         L.orc_add_lorentzian.argtypes = [c_void, c_double, c_double, c_int, dptr, dptr, dptr]
         L.orc_add_point_source.argtypes = [c_void, c_int, c_int, dptr, c_int, dptr, c_double,
                                            c_double, c_int]
@@ -156,6 +157,12 @@ class Oracle:
     def set_chi3(self, comp, arr):
         arr = np.ascontiguousarray(arr, dtype=np.float64).ravel()
         _chk(lib().orc_set_chi3(self.h, comp, _dp(arr)))
+
+    def set_conductivity(self, comp, arr):
+        """structure::set_conductivity (src/structure.cpp:868-905); D/B (or E/H)
+        component, None = zero."""
+        a = None if arr is None else np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        _chk(lib().orc_set_conductivity(self.h, comp, None if a is None else _dp(a)))
 
     def add_lorentzian(self, omega0, gamma, sigmas, drude=False):
         s = [None if v is None else np.ascontiguousarray(v, dtype=np.float64).ravel()

@@ -57,6 +57,9 @@ class ProductSim:
     def set_chi3(self, c, arr):
         self.s.set_chi3(c, arr)
 
+    def set_conductivity(self, c, arr):
+        self.s.set_conductivity(c, arr)
+
     def add_lorentzian(self, *a, **k):
         self.s.add_lorentzian(*a, **k)
 
@@ -620,3 +623,110 @@ def harmonics_cpp(make, chi2, chi3, J, upstream=True):
             break
     f1, f2, f3 = (o.flux(h)[0] for h in hs)
     return o, f2 / f1, f3 / f1
+
+
+# ------------------------------------------------------------- conductivity
+def sc_conductive_3d(make, steps=40, slabs_extra=None):
+    """D and B conductivity (step_curl's cnd branches, src/step_generic.cpp:89-229):
+    a conductive D slab x < 0.3 that reaches into the PML chunks on the low-x /
+    y / z sides (f_cond chunks) but not the high-x ones, B conductivity in an
+    interior box, a dielectric core, a current source inside the conductive
+    slab (cndinv scaling, src/step.cpp:300-309) and an integrated one outside."""
+    o = vol(make, 3, [3.2, 2.6, 3.0], 10, center_origin=True)
+    o.add_pml(0.7)
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        o.set_chi1inv(c, c, np.where((np.abs(y) < 0.4) & (np.abs(z) < 0.4), 1 / 4.0, 1.0))
+    for c in (6, 7, 8):  # Dx, Dy, Dz
+        x, y, z = o.coords(c)
+        o.set_conductivity(c, np.where(x < 0.3, 0.8 + 0.1 * (c - 6), 0.0))
+    for c in (9, 10):  # Bx, By
+        x, y, z = o.coords(c)
+        box = (np.abs(x - 0.5) < 0.3) & (np.abs(y) < 0.5) & (np.abs(z) < 0.5)
+        o.set_conductivity(c, np.where(box, 2.0, 0.0))
+    o.add_gaussian_source(2, 0.3, 4.0, 0.0, 40.0, (-0.45, 0.05, 0.05), 1.0)
+    o.add_gaussian_source(0, 0.25, 4.0, 0.0, 40.0, (0.75, -0.1, 0.2), 0.5, is_integrated=True)
+    o.add_gaussian_source(3, 0.3, 4.0, 0.0, 40.0, (0.55, 0.1, 0.0), 0.7)  # Hx in the B box
+    o.step(steps)
+    return o
+
+
+def pml1d_ft(make, res, sz, dpml, conductivity, freq=1.0, stretch=2.0, R=1e-15, max_steps=None):
+    """One structure of tests/pml.cpp:check_pml1d (75-114): 1-D cell sz, pml(dpml, R,
+    stretch), By conductivity everywhere, integrated Ex gaussian_src_time(freq,
+    freq/20) at -sz/2 + dpml_0 + 0.1 (dpml_0 = 1), and do_ft (49-73): the Fourier
+    transform of Ex at sz/2 - dpml_0 - 0.1 summed over every step until the fields
+    have decayed.  Returns (ft, steps)."""
+    o = make(1, [0, 0, int(sz * res + 0.5)], res, 0.5, [0, 0, -int(sz * res + 0.5)])
+    o.add_pml(dpml, R=R, mean_stretch=stretch)
+    o.set_conductivity(10, np.full(o.shape(), float(conductivity)))  # By
+    width = 1.0 / (freq / 20)
+    o.add_gaussian_source(0, freq, width, 0.0, 2 * width * 5.0, (0, 0, -0.5 * 3.0 + 1.0 + 0.1),
+                          1.0, is_integrated=True)
+    last = float(np.float32(width * 5.0 + width * 5.0))
+    pt = (0, 0, 0.5 * 3.0 - 1.0 - 0.1)
+    ft = 0j
+    emax = 0.0
+    n = 0
+
+    def sample():
+        nonlocal ft, emax
+        v = o.get_field(0, pt)
+        ft += v * complex(math.cos(2 * math.pi * freq * o.time()),
+                          math.sin(2 * math.pi * freq * o.time()))
+        return abs(v)
+
+    while o.time() < last:
+        emax = max(emax, sample())
+        o.step()
+        n += 1
+    while True:
+        emaxcur = 0.0
+        T = o.time() + 50
+        while o.time() < T:
+            e = sample()
+            emax = max(emax, e)
+            emaxcur = max(emaxcur, e)
+            o.step()
+            n += 1
+            if max_steps and n >= max_steps:
+                return ft, n
+        if emaxcur < 1e-6 * emax:
+            break
+        if T > 500 and emaxcur > 1e-2 * emax:
+            raise RuntimeError("meep: fields do not seem to be decaying")
+    return ft, n
+
+
+def check_pml1d(make, conductivity=10.0, nres=8):
+    """tests/pml.cpp:check_pml1d (75-114, run by main at 323 with conductivity 10):
+    the reflection |ft - ft2|^2/|ft2|^2 against a cell with twice the PML must fall
+    at least as fast as ((res-10)/res)^8 * 1.1 from one resolution to the next.
+    Returns the list of (res, refl) and whether the reference's check passes."""
+    dpml = 1.0
+    sz, sz2 = 1.0 + 2 * dpml, 1.0 + 2 * dpml * 2
+    out, ok, prev = [], True, 0.0
+    for i in range(nres):
+        res = 10.0 + 10.0 * i
+        ft, _ = pml1d_ft(make, res, sz, dpml, conductivity)
+        ft2, _ = pml1d_ft(make, res, sz2, 2 * dpml, conductivity)
+        refl = abs(ft - ft2) ** 2 / abs(ft2) ** 2
+        out.append((res, refl))
+        if i > 0 and refl > prev * ((res - 10) / res) ** 8 * 1.1:
+            ok = False
+        prev = refl
+    return out, ok
+
+
+def sc_conductive_2d(make, steps=80):
+    """2-D TE + TM with conductivity on every D / B component across a one-sided PML."""
+    o = vol(make, 2, [2.3, 1.9], 10)
+    o.add_pml(0.5, dirs=(0,), sides=(1,))
+    o.add_pml(0.4, dirs=(1,), sides=(0,))
+    for c in range(6, 12):
+        x, y = o.coords(c)
+        o.set_conductivity(c, np.where(x > 1.0, 0.3 + 0.05 * c, 0.0))
+    o.add_gaussian_source(5, 0.4, 3.0, 0.0, 30.0, (1.03, 0.77), 2.0)
+    o.add_gaussian_source(2, 0.35, 3.0, 0.0, 30.0, (1.4, 1.1), 1.0)
+    o.step(steps)
+    return o
