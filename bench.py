@@ -48,6 +48,10 @@ def parse():
 
 
 def build_fields(args, rank, world, local_rank, nid):
+    # MNL_BENCH_DEVICE pins every rank to one device (rehearsing the RCCL path
+    # with several ranks on a one-GPU box); default: one GPU per local rank
+    if os.environ.get("MNL_BENCH_DEVICE"):
+        local_rank = int(os.environ["MNL_BENCH_DEVICE"])
     from meep_nl_amd import core
     res = 10.0
     n = [args.size, args.size, args.size * world]

@@ -186,6 +186,20 @@ int mnl_fields_set_profiling(mnl_fields *f, int on);
 int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch);
 
+/* ---- checkpoint (src/fields_dump.cpp, src/structure_dump.cpp) -----------
+ * fields::dump / fields::load (src/fields_dump.cpp:108-145, 232-270): t and
+ * every per-point state array of the rank (f, f_u, f_w, f_cond, and also the
+ * polarizations and DFT accumulators), flat binary, not HDF5 (no HDF5 in this
+ * build).  Distributed fields write one file per rank (filename.rank<r>).
+ * load() needs fields built the same way (same structure, decomposition,
+ * sources, flux objects) and resumes bit for bit.  structure dump/load
+ * (structure::dump / load, src/structure_dump.cpp) save the host-side
+ * material description; load before creating fields. */
+int mnl_fields_dump(mnl_fields *f, const char *filename);
+int mnl_fields_load(mnl_fields *f, const char *filename);
+int mnl_structure_dump(mnl_structure *s, const char *filename);
+int mnl_structure_load(mnl_structure *s, const char *filename);
+
 /* ---- DFT flux (src/dft.cpp; meep.hpp dft_flux) --------------------------
  * fields::add_dft_flux (src/dft.cpp:578-640) for a volume_list: regions =
  * nreg x {min x,y,z, max x,y,z, direction (0..2), weight}, nfreq frequencies

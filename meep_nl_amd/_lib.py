@@ -27,6 +27,10 @@ _SIGS = {
     "mnl_structure_set_chi2": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_set_chi3": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_set_conductivity": (c_int, [c_void, c_int, dptr]),
+    "mnl_fields_dump": (c_int, [c_void, ctypes.c_char_p]),
+    "mnl_fields_load": (c_int, [c_void, ctypes.c_char_p]),
+    "mnl_structure_dump": (c_int, [c_void, ctypes.c_char_p]),
+    "mnl_structure_load": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_add_lorentzian": (c_int, [c_void, c_double, c_double, c_int, dptr, dptr, dptr]),
     "mnl_structure_set_box": (c_int, [c_void, c_int, c_int, dptr, c_double]),
     "mnl_structure_set_nonlinear_mode": (c_int, [c_void, c_int]),

@@ -10,6 +10,7 @@ Arrays use the reference's own per-chunk layout for the whole cell
 ((n+1) points per present direction, Z fastest; src/vec.cpp:482-494).
 """
 import ctypes
+import os
 import math
 
 import numpy as np
@@ -128,6 +129,16 @@ class Structure:
         diagonal chi1inv set so far).  None resets to zero."""
         a = None if arr is None else self._arr(arr)
         check(lib().mnl_structure_set_conductivity(self.h, comp, None if a is None else ptr(a)))
+
+    def dump(self, fname):
+        """structure::dump (src/structure_dump.cpp): the host-side material
+        description (flat binary, not HDF5)."""
+        check(lib().mnl_structure_dump(self.h, os.fsencode(fname)))
+
+    def load(self, fname):
+        """structure::load: replace the materials / PML / susceptibilities by a
+        dumped description of the same grid volume (before creating fields)."""
+        check(lib().mnl_structure_load(self.h, os.fsencode(fname)))
 
     def add_lorentzian(self, omega0, gamma, sigmas, drude=False):
         s = [None if v is None else self._arr(v) for v in sigmas]
@@ -317,6 +328,16 @@ class Fields:
 
 
     # -- DFT flux (fields::add_dft_flux, src/dft.cpp:578-640; dft_flux, src/dft.cpp:482-547)
+    def dump(self, fname):
+        """fields::dump (src/fields_dump.cpp:108-145): t and every per-point state
+        array (one file per rank: fname.rank<r> when distributed)."""
+        check(lib().mnl_fields_dump(self.h, os.fsencode(fname)))
+
+    def load(self, fname):
+        """fields::load (src/fields_dump.cpp:232-270) into fields built the same
+        way (structure, sources, flux objects); resumes bit for bit."""
+        check(lib().mnl_fields_load(self.h, os.fsencode(fname)))
+
     def add_dft_flux(self, regions, freqs, decimation=0):
         """regions: [(min xyz, max xyz, direction, weight)]; returns a handle.
         The DFT is accumulated on the GPU after every decimated step."""

@@ -2545,6 +2545,248 @@ int finalize_fields(mnl_fields *F) {
   return 0;
 }
 
+// ------------------------------------------------------------- checkpoint
+// fields::dump / fields::load (src/fields_dump.cpp:108-145, 232-270) and
+// structure::dump / load (src/structure_dump.cpp).  The reference writes HDF5
+// (absent from this image); here a flat binary file per rank: a header (grid,
+// decomposition, t) and every per-point state array of the rank -- the
+// reference's f, f_u, f_w, f_cond plus the polarizations P / P_prev, which it
+// does not save, and the DFT accumulators -- raw in the rank-local device
+// layout, so a load into fields built the same way resumes bit for bit.
+constexpr char CK_MAGIC[8] = {'M', 'N', 'L', 'F', 'L', 'D', '0', '1'};
+constexpr char CS_MAGIC[8] = {'M', 'N', 'L', 'S', 'T', 'R', '0', '1'};
+
+struct CkEntry {
+  int kind, a, b;
+  double *p;
+  size_t n;
+};
+
+std::vector<CkEntry> ckpt_entries(mnl_fields *F) {
+  DevFields &f = F->f;
+  std::vector<CkEntry> v;
+  auto add = [&](int kind, int a, int b, double *p, size_t n) {
+    if (p) v.push_back({kind, a, b, p, n});
+  };
+  const size_t n = F->nlocal;
+  for (int d = 0; d < 3; d++) {
+    add(0, d, 0, f.E[d], n);
+    add(1, d, 0, f.D[d], n);
+    add(2, d, 0, f.B[d], n);
+    add(3, d, 0, f.H[d], n);
+    add(4, d, 0, f.UB[d], n);
+    add(5, d, 0, f.UD[d], n);
+    add(6, d, 0, f.WE[d], n);
+    add(7, d, 0, f.WH[d], n);
+  }
+  for (int t = 0; t < 2; t++)
+    for (int d = 0; d < 3; d++) add(8, t, d, f.fcnd[t][d], n);
+  for (int k = 0; k < f.npol; k++)
+    for (int d = 0; d < 3; d++) {
+      add(9, k, d, f.pol[k].P[d], n);
+      add(10, k, d, f.pol[k].Pp[d], n);
+    }
+  for (size_t h = 0; h < F->dfts.size(); h++) {
+    DftFluxH &o = *F->dfts[h];
+    add(11, (int)h, o.nfreq, o.d_dft, 2 * ((o.npts + 63) & ~size_t(63)) * o.nfreq);
+  }
+  return v;
+}
+
+struct CkHeader {
+  char magic[8];
+  int32_t dim, n[3], io[3], nranks, rank, nentries;
+  uint64_t nlocal;
+  int64_t t;
+};
+
+CkHeader ckpt_header(mnl_fields *F, int nentries) {
+  CkHeader h{};
+  memcpy(h.magic, CK_MAGIC, 8);
+  h.dim = F->S.dim;
+  for (int d = 0; d < 3; d++) h.n[d] = F->S.n[d], h.io[d] = F->S.io[d];
+  h.nranks = F->nranks;
+  h.rank = F->rank;
+  h.nentries = nentries;
+  h.nlocal = F->nlocal;
+  h.t = F->t;
+  return h;
+}
+
+// a consistent unfused state: implicit E and the W aux fields materialised,
+// buffered DFT updates accumulated
+int ckpt_quiesce(mnl_fields *F) {
+  if (set_fused(F, false)) return -1;
+  for (auto &op : F->dfts)
+    if (dft_flush(F, *op)) return -1;
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+int fields_dump(mnl_fields *F, const char *path) {
+  if (ckpt_quiesce(F)) return -1;
+  auto es = ckpt_entries(F);
+  FILE *fp = fopen(path, "wb");
+  if (!fp) return fail(std::string("cannot create fields output file ") + path);
+  std::unique_ptr<FILE, int (*)(FILE *)> guard(fp, fclose);
+  CkHeader h = ckpt_header(F, (int)es.size());
+  if (fwrite(&h, sizeof h, 1, fp) != 1) return fail("write error");
+  std::vector<double> buf;
+  for (auto &e : es) {
+    int32_t id[3] = {e.kind, e.a, e.b};
+    uint64_t n = e.n;
+    buf.resize(e.n);
+    HIPCHK(hipMemcpy(buf.data(), e.p, e.n * 8, hipMemcpyDeviceToHost));
+    if (fwrite(id, sizeof id, 1, fp) != 1 || fwrite(&n, 8, 1, fp) != 1 ||
+        fwrite(buf.data(), 8, e.n, fp) != e.n)
+      return fail("write error");
+  }
+  return 0;
+}
+
+int fields_load(mnl_fields *F, const char *path) {
+  if (F->src_dirty && build_source_lists(F)) return -1;
+  if (ckpt_quiesce(F)) return -1;
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return fail(std::string("cannot open fields file ") + path);
+  std::unique_ptr<FILE, int (*)(FILE *)> guard(fp, fclose);
+  CkHeader h{};
+  if (fread(&h, sizeof h, 1, fp) != 1 || memcmp(h.magic, CK_MAGIC, 8))
+    return fail("not a fields checkpoint file");
+  auto es = ckpt_entries(F);
+  CkHeader me = ckpt_header(F, (int)es.size());
+  if (h.dim != me.dim || memcmp(h.n, me.n, sizeof h.n) || memcmp(h.io, me.io, sizeof h.io) ||
+      h.nranks != me.nranks || h.rank != me.rank || h.nlocal != me.nlocal)
+    return fail("fields file has a different grid or chunk layout");
+  // every field-state array must match; DFT accumulators are loaded into the
+  // flux objects that exist (same creation order), extra ones are skipped
+  size_t nfield = 0, matched = 0;
+  for (auto &e : es) nfield += e.kind != 11;
+  std::vector<double> buf;
+  for (int k = 0; k < h.nentries; k++) {
+    int32_t id[3];
+    uint64_t n;
+    if (fread(id, sizeof id, 1, fp) != 1 || fread(&n, 8, 1, fp) != 1) return fail("read error");
+    const CkEntry *dst = nullptr;
+    for (auto &e : es)
+      if (e.kind == id[0] && e.a == id[1] && e.b == id[2]) dst = &e;
+    if (!dst && id[0] != 11)
+      return fail("fields file does not match these fields (allocated arrays differ)");
+    if (dst && dst->n != n) return fail("fields file does not match these fields (array sizes differ)");
+    buf.resize(n);
+    if (fread(buf.data(), 8, n, fp) != n) return fail("read error (truncated file)");
+    if (!dst) continue;
+    HIPCHK(hipMemcpy(dst->p, buf.data(), n * 8, hipMemcpyHostToDevice));
+    matched += dst->kind != 11;
+  }
+  if (matched != nfield) return fail("fields file does not match these fields (allocated arrays differ)");
+  F->t = h.t;
+  return 0;
+}
+
+template <class T>
+void put(std::string &o, const T &v) {
+  o.append(reinterpret_cast<const char *>(&v), sizeof v);
+}
+void put_vec(std::string &o, const std::vector<double> &v) {
+  put(o, (uint64_t)v.size());
+  o.append(reinterpret_cast<const char *>(v.data()), v.size() * 8);
+}
+struct Rd {
+  const std::string &s;
+  size_t i = 0;
+  bool ok = true;
+  template <class T>
+  void get(T &v) {
+    if (i + sizeof v > s.size()) {
+      ok = false;
+      return;
+    }
+    memcpy(&v, s.data() + i, sizeof v);
+    i += sizeof v;
+  }
+  void get_vec(std::vector<double> &v) {
+    uint64_t n = 0;
+    get(n);
+    if (!ok || i + n * 8 > s.size()) {
+      ok = false;
+      return;
+    }
+    v.resize(n);
+    memcpy(v.data(), s.data() + i, n * 8);
+    i += n * 8;
+  }
+};
+
+int structure_dump(const mnl_structure *S, const char *path) {
+  std::string o(CS_MAGIC, 8);
+  put(o, S->dim);
+  for (int d = 0; d < 3; d++) put(o, S->n[d]), put(o, S->io[d]);
+  put(o, S->a), put(o, S->courant), put(o, S->nl_mode);
+  for (int d = 0; d < 3; d++)
+    for (int e = 0; e < 2; e++) put(o, S->pml_thick[d][e]), put(o, S->pml_R[d][e]), put(o, S->pml_stretch[d][e]);
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) put_vec(o, S->chi1inv[c][d]);
+  for (int c = 0; c < 3; c++) put_vec(o, S->chi2[c]), put_vec(o, S->chi3[c]);
+  for (int t = 0; t < 2; t++)
+    for (int d = 0; d < 3; d++) put_vec(o, S->cond[t][d]);
+  put(o, (uint64_t)S->lor.size());
+  for (auto &L : S->lor) {
+    put(o, L.omega0), put(o, L.gamma), put(o, L.drude);
+    for (int d = 0; d < 3; d++) put_vec(o, L.sigma[d]);
+  }
+  put(o, (uint64_t)S->boxes.size());
+  for (auto &b : S->boxes) put(o, b);
+  FILE *fp = fopen(path, "wb");
+  if (!fp) return fail(std::string("cannot create structure output file ") + path);
+  size_t w = fwrite(o.data(), 1, o.size(), fp);
+  fclose(fp);
+  return w == o.size() ? 0 : fail("write error");
+}
+
+int structure_load(mnl_structure *S, const char *path) {
+  FILE *fp = fopen(path, "rb");
+  if (!fp) return fail(std::string("cannot open structure file ") + path);
+  std::string s;
+  char buf[1 << 16];
+  size_t r;
+  while ((r = fread(buf, 1, sizeof buf, fp)) > 0) s.append(buf, r);
+  fclose(fp);
+  if (s.size() < 8 || memcmp(s.data(), CS_MAGIC, 8)) return fail("not a structure file");
+  Rd in{s, 8};
+  int dim = 0, n[3] = {0, 0, 0}, io[3] = {0, 0, 0};
+  in.get(dim);
+  for (int d = 0; d < 3; d++) in.get(n[d]), in.get(io[d]);
+  double a = 0, courant = 0;
+  in.get(a), in.get(courant);
+  if (!in.ok || dim != S->dim || memcmp(n, S->n, sizeof n) || memcmp(io, S->io, sizeof io) ||
+      a != S->a || courant != S->courant)
+    return fail("structure file has a different grid volume");
+  mnl_structure T = *S;
+  in.get(T.nl_mode);
+  for (int d = 0; d < 3; d++)
+    for (int e = 0; e < 2; e++) in.get(T.pml_thick[d][e]), in.get(T.pml_R[d][e]), in.get(T.pml_stretch[d][e]);
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) in.get_vec(T.chi1inv[c][d]);
+  for (int c = 0; c < 3; c++) in.get_vec(T.chi2[c]), in.get_vec(T.chi3[c]);
+  for (int t = 0; t < 2; t++)
+    for (int d = 0; d < 3; d++) in.get_vec(T.cond[t][d]);
+  uint64_t nl = 0;
+  in.get(nl);
+  T.lor.assign(in.ok && nl < 1024 ? nl : 0, Lorentz{});
+  for (auto &L : T.lor) {
+    in.get(L.omega0), in.get(L.gamma), in.get(L.drude);
+    for (int d = 0; d < 3; d++) in.get_vec(L.sigma[d]);
+  }
+  uint64_t nb = 0;
+  in.get(nb);
+  T.boxes.assign(in.ok && nb < (1u << 20) ? nb : 0, BoxSpec{});
+  for (auto &b : T.boxes) in.get(b);
+  if (!in.ok || in.i != s.size()) return fail("structure file is truncated or corrupt");
+  *S = std::move(T);
+  return 0;
+}
+
 mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, const void *id,
                           LocalHub *hub = nullptr) {
   if (!s) {
@@ -2832,6 +3074,32 @@ int mnl_fields_step(mnl_fields *F, int nsteps) {
   if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
   if (step_batch(F, nsteps)) return -1;
   return nan_check(F);
+}
+
+int mnl_fields_dump(mnl_fields *F, const char *filename) {
+  if (!F || !filename) return fail("null argument");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  std::string p = filename;
+  if (F->nranks > 1) p += ".rank" + std::to_string(F->rank);
+  return fields_dump(F, p.c_str());
+}
+
+int mnl_fields_load(mnl_fields *F, const char *filename) {
+  if (!F || !filename) return fail("null argument");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  std::string p = filename;
+  if (F->nranks > 1) p += ".rank" + std::to_string(F->rank);
+  return fields_load(F, p.c_str());
+}
+
+int mnl_structure_dump(mnl_structure *s, const char *filename) {
+  if (!s || !filename) return fail("null argument");
+  return structure_dump(s, filename);
+}
+
+int mnl_structure_load(mnl_structure *s, const char *filename) {
+  if (!s || !filename) return fail("null argument");
+  return structure_load(s, filename);
 }
 
 int mnl_fields_time(mnl_fields *F, long long *t, double *dt) {

@@ -567,6 +567,8 @@ class Simulation:
             self.fields = core.Fields(self.structure)
         for src in self.sources:
             src.add_source(self.fields)
+        if getattr(self, "load_fields_file", None):  # delayed load (python/simulation.py:2509-2510)
+            self.load_fields(self.load_fields_file)
 
     # -- time
     def meep_time(self):
@@ -649,6 +651,61 @@ class Simulation:
         flux._create()
         self.dft_objects.append(flux)
         return flux
+
+    # -- checkpoint (python/simulation.py:2293-2450); flat binary files, not HDF5
+    def _load_dump_dirname(self, dirname, single_parallel_file=True):
+        if single_parallel_file:
+            return dirname
+        ctx = _dist_context() if self.parallel is not False else None
+        return os.path.join(dirname, "rank%02d" % (ctx[0] if ctx else 0))
+
+    def dump_structure(self, fname, single_parallel_file=True):
+        if self.structure is None:
+            raise ValueError("Structure must be initialized before calling dump_structure")
+        self.structure.dump(fname)
+
+    def load_structure(self, fname, single_parallel_file=True):
+        if self.structure is None:
+            raise ValueError("Structure must be initialized before loading structure from file "
+                             "'%s'" % fname)
+        if self.fields is not None:
+            raise ValueError("load_structure must be called before the fields are created")
+        self.structure.load(fname)
+
+    def dump_fields(self, fname, single_parallel_file=True):
+        if self.fields is None:
+            raise ValueError("Fields must be initialized before calling dump_fields")
+        self.fields.dump(fname)
+
+    def load_fields(self, fname, single_parallel_file=True):
+        if self.fields is None:
+            raise ValueError("Fields must be initialized before loading fields from file '%s'"
+                             % fname)
+        self.fields.load(fname)
+
+    def dump(self, dirname, dump_structure=True, dump_fields=True, single_parallel_file=True):
+        d = self._load_dump_dirname(dirname, single_parallel_file)
+        os.makedirs(d, exist_ok=True)
+        if dump_structure:
+            self.dump_structure(os.path.join(d, "structure.mnl"))
+        if dump_fields:
+            self.dump_fields(os.path.join(d, "fields.mnl"))
+
+    def load(self, dirname, load_structure=True, load_fields=True, single_parallel_file=True):
+        """Call right after creating the Simulation, before init_sim (as the
+        reference): the structure is loaded when it is built, the fields after
+        the sources are added."""
+        d = self._load_dump_dirname(dirname, single_parallel_file)
+        if load_structure:
+            if self.structure is None:
+                self._init_structure()
+            self.load_structure(os.path.join(d, "structure.mnl"))
+        if load_fields:
+            f = os.path.join(d, "fields.mnl")
+            if self.fields is not None:
+                self.load_fields(f)
+            else:
+                self.load_fields_file = f
 
     # -- monitors
     def get_field_point(self, c, pt):

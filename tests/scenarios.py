@@ -116,6 +116,12 @@ class ProductSim:
     def dft_decimation(self, h):
         return self._fields().dft_decimation(h)
 
+    def dump(self, path):
+        self._fields().dump(path)
+
+    def load(self, path):
+        self._fields().load(path)
+
 
 class GroupSim(ProductSim):
     """nranks z-slabs (y-slabs in 2-D) of one grid on one GPU, one host thread per
@@ -203,6 +209,15 @@ class GroupSim(ProductSim):
     def dft_data(self, h, which):
         # each point is accumulated by the rank that owns it, the others hold 0
         return sum(f.dft_data(h, which) for f in self._all())
+
+
+    def dump(self, path):
+        self._all()
+        self._par(lambda f: f.dump(path))
+
+    def load(self, path):
+        self._all()
+        self._par(lambda f: f.load(path))
 
 
 class GroupSim3(GroupSim):
