@@ -86,6 +86,14 @@ int mnl_structure_set_conductivity(mnl_structure *s, int comp, const double *hos
 int mnl_structure_add_lorentzian(mnl_structure *s, double omega0, double gamma, int drude,
                                  const double *sigma_x, const double *sigma_y,
                                  const double *sigma_z);
+/* add_susceptibility with a sigma tensor (src/anisotropic_averaging.cpp:
+ * 300-372): sigma[3*c + d] = row of E component c, column d (NULL = 0), at
+ * c's Yee points -- the reference samples the off-diagonal entries half a pixel
+ * back along c (334-341), the caller does the same.  Off-diagonal entries
+ * enter update_P's 2x2 / 3x3 branches (src/susceptibility.cpp:185-250) per
+ * reference chunk. */
+int mnl_structure_add_lorentzian_tensor(mnl_structure *s, double omega0, double gamma, int drude,
+                                        const double *const sigma[9]);
 /* Nonlinear E update: 0 = the fork (chi2 through Newton-Raphson where the
  * 3x3 chi1inv is present, chi3 inert; default), 1 = upstream Meep (chi2/chi3
  * through the Pade approximant calc_nonlinear_u, src/step_generic.cpp:546-553,

@@ -27,6 +27,8 @@ _SIGS = {
     "mnl_structure_set_chi2": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_set_chi3": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_set_conductivity": (c_int, [c_void, c_int, dptr]),
+    "mnl_structure_add_lorentzian_tensor": (c_int, [c_void, ctypes.c_double, ctypes.c_double,
+                                                    c_int, ctypes.POINTER(dptr)]),
     "mnl_fields_dump": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_fields_load": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_dump": (c_int, [c_void, ctypes.c_char_p]),

@@ -16,7 +16,7 @@ import math
 import numpy as np
 
 from . import _lib
-from ._lib import check, lib, ptr
+from ._lib import check, dptr, lib, ptr
 
 Ex, Ey, Ez, Hx, Hy, Hz, Dx, Dy, Dz, Bx, By, Bz = range(12)
 X, Y, Z = 0, 1, 2
@@ -146,6 +146,16 @@ class Structure:
                                                  *[ptr(v) for v in s]))
         self._nsus += 1
         return self._nsus - 1
+
+    def add_lorentzian_tensor(self, omega0, gamma, sigma, drude=False):
+        """add_susceptibility with a sigma tensor (src/anisotropic_averaging.cpp:
+        300-372): sigma[c][d] (3x3 nested, None = 0) per E component row c at c's
+        Yee points; off-diagonal entries sampled half a pixel back along c."""
+        arrs = [None if sigma[c][d] is None else self._arr(sigma[c][d])
+                for c in range(3) for d in range(3)]
+        ptrs = (dptr * 9)(*[ptr(a) if a is not None else None for a in arrs])
+        check(lib().mnl_structure_add_lorentzian_tensor(self.h, float(omega0), float(gamma),
+                                                         int(drude), ptrs))
 
     def set_box(self, kind, box, value, index=0):
         b = np.ascontiguousarray(box, dtype=np.float64)

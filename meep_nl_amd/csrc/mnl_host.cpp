@@ -107,6 +107,13 @@ struct Lorentz {
   double omega0, gamma;
   int drude;
   std::vector<double> sigma[3];  // canonical arrays (empty = 0)
+  std::vector<double> off[3][3];  // off-diagonal sigma[c][d], d != c (empty = 0)
+  bool aniso() const {
+    for (int c = 0; c < 3; c++)
+      for (int d = 0; d < 3; d++)
+        if (!off[c][d].empty()) return true;
+    return false;
+  }
 };
 
 struct BoxSpec {
@@ -872,6 +879,39 @@ int setup_materials(mnl_fields *F) {
       if (dev_alloc(F, &p, F->nlocal)) return -1;
       if (upload_canonical(F, p, L.sigma[d], d)) return -1;
       pd.sigma[d] = p;
+    }
+    if (L.aniso()) {  // off-diagonal sigma + per-chunk array presence (zone boxes)
+      f.aniso = 1;
+      for (int c = 0; c < 3; c++)
+        for (int d = 0; d < 3; d++) {
+          if (L.off[c][d].empty() || !has_field(S, c)) continue;
+          double *p;
+          if (dev_alloc(F, &p, F->nlocal)) return -1;
+          if (upload_canonical(F, p, L.off[c][d], c)) return -1;
+          pd.soff[c][d] = p;
+        }
+      std::vector<uint16_t> zb(27, 0);
+      auto ivx = zone_ivs_or_one(S, 0), ivy = zone_ivs_or_one(S, 1), ivz = zone_ivs_or_one(S, 2);
+      for (auto &zx : ivx)
+        for (auto &zy : ivy)
+          for (auto &zz : ivz) {
+            const ZoneIv *zv[3] = {&zx, &zy, &zz};
+            uint16_t &m = zb[zx.zone * 9 + zy.zone * 3 + zz.zone];
+            for (int c = 0; c < 3; c++) {
+              bool row = !L.sigma[c].empty() && nontrivial_in_zone(S, L.sigma[c], c, zv, 0.0);
+              for (int d = 0; d < 3; d++)
+                if (d != c && !L.off[c][d].empty() && nontrivial_in_zone(S, L.off[c][d], c, zv, 0.0)) {
+                  m |= 1 << (3 * c + d);
+                  row = true;
+                }
+              if (row) m |= 1 << (4 * c);
+            }
+          }
+      uint16_t *dz;
+      if (dev_alloc(F, &dz, 27)) return -1;
+      HIPCHK(hipMemcpyAsync(dz, zb.data(), 27 * sizeof(uint16_t), hipMemcpyHostToDevice, F->stream));
+      HIPCHK(hipStreamSynchronize(F->stream));
+      pd.zbits = dz;
     }
     (void)box_sig;
   }
@@ -1696,6 +1736,11 @@ int exchange(mnl_fields *F, int kind, hipStream_t st = nullptr) {
         items.push_back({F->f.Bn[c], false});
         if (F->f.H[c]) items.push_back({F->f.Hn[c], false});
       }
+    } else if (kind == 4) {  // W of E (E, and f_w where allocated): the one ghost plane
+      if (F->f.E[c] && F->allocated[c]) {
+        items.push_back({F->f.E[c], c != sd});
+        if (F->f.WE[c]) items.push_back({F->f.WE[c], c != sd});
+      }
     } else if (kind == 3) {  // DFT: H comps unshifted along the slab axis, low ghost
       if (c == sd && F->allocated[3 * T_H + c]) {
         items.push_back({F->f.B[c], true});
@@ -1946,7 +1991,7 @@ bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
 }
 
 bool fused_possible(mnl_fields *F) {
-  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->upnl) return false;
+  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->upnl || F->f.aniso) return false;
   for (int t = 0; t < 2; t++)
     for (int d = 0; d < 3; d++)
       if (F->f.cnd[t][d]) return false;
@@ -2473,15 +2518,21 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       // ---- E (+ Lorentzian P)
       k = ev_begin(TM_E);
-      bool fuse = !F->nr && !F->upnl;  // neighbour reads of D - P: P after all of E
+      // neighbour reads of D - P (NR, upstream chi) or of W (anisotropic sigma):
+      // P after all of E
+      bool fuse = !F->nr && !F->upnl && !f.aniso;
       if ((!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) ||
           (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream)))
         return fail("update E launch failed");
+      if (f.aniso && k_aniso_wall(g, f, 0, F->stream)) return fail("wall W launch failed");
+      if (f.aniso && F->nranks > 1 && exchange(F, 4))  // WE_stuff ghosts (step.cpp:111-114)
+        return fail("W halo exchange failed");
       if (!fuse && f.npol) {
         if (k_update_pols(F->interior, nullptr, g, f, F->stream) ||
             k_update_pols(F->interior, sl, g, f, F->stream))
           return fail("pols launch failed");
       }
+      if (f.aniso && k_aniso_wall(g, f, 1, F->stream)) return fail("wall W launch failed");
       ev_end(k);
       if (F->fused)
         for (int d = 0; d < 3; d++) {
@@ -2734,6 +2785,8 @@ int structure_dump(const mnl_structure *S, const char *path) {
   for (auto &L : S->lor) {
     put(o, L.omega0), put(o, L.gamma), put(o, L.drude);
     for (int d = 0; d < 3; d++) put_vec(o, L.sigma[d]);
+    for (int c = 0; c < 3; c++)
+      for (int d = 0; d < 3; d++) put_vec(o, L.off[c][d]);
   }
   put(o, (uint64_t)S->boxes.size());
   for (auto &b : S->boxes) put(o, b);
@@ -2777,6 +2830,8 @@ int structure_load(mnl_structure *S, const char *path) {
   for (auto &L : T.lor) {
     in.get(L.omega0), in.get(L.gamma), in.get(L.drude);
     for (int d = 0; d < 3; d++) in.get_vec(L.sigma[d]);
+    for (int c = 0; c < 3; c++)
+      for (int d = 0; d < 3; d++) in.get_vec(L.off[c][d]);
   }
   uint64_t nb = 0;
   in.get(nb);
@@ -2940,17 +2995,25 @@ int mnl_structure_set_chi3(mnl_structure *s, int comp, const double *host) {
 }
 int mnl_structure_add_lorentzian(mnl_structure *s, double omega0, double gamma, int drude,
                                  const double *sx, const double *sy, const double *sz) {
-  if (!s) return fail("null structure");
+  const double *sig[9] = {sx, nullptr, nullptr, nullptr, sy, nullptr, nullptr, nullptr, sz};
+  return mnl_structure_add_lorentzian_tensor(s, omega0, gamma, drude, sig);
+}
+
+int mnl_structure_add_lorentzian_tensor(mnl_structure *s, double omega0, double gamma, int drude,
+                                        const double *const sigma[9]) {
+  if (!s || !sigma) return fail("null argument");
   if ((int)s->lor.size() >= MAX_POL) return fail("too many susceptibilities (max 4)");
   Lorentz L;
   L.omega0 = omega0;
   L.gamma = gamma;
   L.drude = drude;
-  const double *sv[3] = {sx, sy, sz};
-  for (int d = 0; d < 3; d++)
-    if (sv[d]) {
-      L.sigma[d].assign(sv[d], sv[d] + s->ntot);
-      if (all_eq(L.sigma[d], 0.0)) L.sigma[d].clear();
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) {
+      const double *v = sigma[3 * c + d];
+      if (!v) continue;
+      auto &dst = d == c ? L.sigma[c] : L.off[c][d];
+      dst.assign(v, v + s->ntot);
+      if (all_eq(dst, 0.0)) dst.clear();
     }
   s->lor.push_back(std::move(L));
   return 0;

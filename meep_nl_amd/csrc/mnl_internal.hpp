@@ -70,6 +70,12 @@ struct PolDev {
   double *P[3];
   double *Pp[3];
   const double *sigma[3];
+  // anisotropic sigma (src/susceptibility.cpp:227-250): off-diagonal sigma[c][d]
+  // (null = zero everywhere) and, per zone box, which arrays the reference
+  // chunk holds: bit 3c+d (d != c: off-diagonal nontrivial there; d == c: the
+  // diagonal array kept, i.e. some entry of row c nontrivial there)
+  const double *soff[3][3];
+  const uint16_t *zbits;
   // box (local indices per direction) holding every point with sigma != 0; outside
   // it P and Pprev stay 0 (update_P with sigma = 0 from 0), so the E update
   // neither reads nor writes them there
@@ -116,6 +122,7 @@ struct DevFields {
   double *fcnd[2][3];
   const uint8_t *cnd_zone;
   double cnd_dt2;            // dt * 0.5 (src/step_generic.cpp:92)
+  int aniso;                 // some susceptibility has off-diagonal sigma
 };
 
 // Point sources in rank-local linear indices.
@@ -158,6 +165,7 @@ int k_update_e(const Box &in, const BoxList *shell, const DevGrid &g, const DevF
                const ISrcDev &is, int step, bool fuse_pols, void *stream);
 int k_update_pols(const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
                   void *stream);
+int k_aniso_wall(const DevGrid &g, const DevFields &f, int zero, void *stream);
 int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int step,
              void *stream);
 // Fused step (DESIGN.md "Fused step"): one pass per fields::step() over box G

@@ -639,6 +639,140 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, BoxL
   }
 }
 
+// lorentzian update_P with off-diagonal sigma (src/susceptibility.cpp:188-262):
+// per point the branch of its reference chunk (3x3 / 2x2 / isotropic, from the
+// arrays that chunk holds), the off-diagonal partners W averaged by OFFDIAG
+// (185-186).  W of a component = f_w where its chunk has PML along its own
+// direction, f elsewhere (update_pols.cpp:44); neighbours read the owner's W,
+// as the WE_stuff ghost exchange (boundaries.cpp:407-408, 508-525) provides.
+// Owned by the reference's chunk although the kernels never update it: the high
+// metallic wall plane of a component unshifted along the wall normal
+// (little_owned_corner0..big_corner includes it, src/meep/vec.hpp:1102-1104;
+// zero_metal zeroes f there only in step_boundaries, src/boundaries.cpp:304-339).
+// glob: the whole-cell owned ranges (a neighbour rank's plane counts as owned)
+__device__ __forceinline__ bool on_wall(const DevGrid &g, int c, const Pt &p, bool glob = false) {
+  bool wall = false;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    const bool sh = d == c;
+    if (!sh && g.wall[d] && p.j[d] + g.off[d] == g.nglob[d]) {
+      wall = true;
+      continue;
+    }
+    if (glob) {
+      const int jg = p.j[d] + g.off[d];
+      if (jg < (sh ? 0 : 1) || jg > g.nglob[d] - 1) return false;
+    } else {
+      const int lo = sh ? g.owned_lo_sh[d] : g.owned_lo_un[d];
+      const int hi = sh ? g.owned_hi_sh[d] : g.owned_hi_un[d];
+      if (p.j[d] < lo || p.j[d] > hi) return false;
+    }
+  }
+  return wall;
+}
+
+__device__ __forceinline__ int zone_box(const DevFields &f, const DevGrid &g, const Pt &p, int c) {
+  int zb = 0;
+#pragma unroll
+  for (int e = 0; e < 3; e++) zb = zb * 3 + (g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, c, e)] : 1);
+  return zb;
+}
+
+// W of E component c at point q (linear index n) as read by a point of
+// reference chunk zb: f_w where q's chunk has PML along c, f elsewhere
+// (update_pols.cpp:44).  Ghosts hold the owner's W (WE_stuff exchange), except
+// on the metallic wall planes, which are never connected (boundaries.cpp:
+// 347-460): there only the owning chunk sees its transient value, others 0.
+__device__ __forceinline__ double w_at(const DevFields &f, const DevGrid &g, const Pt &q, int c,
+                                       long long n, int zb) {
+  if (on_wall(g, c, q, true) && zone_box(f, g, q, c) != zb) return 0.0;
+  return pml_at(f, g, c, qcoord(g, q, T_E, c, c)) ? f.WE[c][n] : f.En[c][n];
+}
+
+// Between update_eh(E) and step_boundaries(E) the reference's wall-plane E (and
+// f_w) hold u*(D - sum P) with D = 0 there, and update_pols reads them through
+// OFFDIAG.  zero = 0: write that transient W; zero = 1: E back to 0 afterwards.
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void aniso_wall_kernel(Box b, DevGrid g, DevFields f,
+                                                                     int zero) {
+  Pt p;
+  if (!make_pt(b, g, p)) return;
+  const long long i = p.idx;
+  for (int c = 0; c < 3; c++) {
+    if (!f.ecomp_present[c] || !on_wall(g, c, p)) continue;
+    if (zero) {
+      f.En[c][i] = 0;
+      continue;
+    }
+    double v = f.Dn[c][i];
+    for (int k = 0; k < f.npol; k++)
+      if (f.pol[k].P[c]) v -= f.pol[k].P[c][i];
+    const double w = f.inveps[c] ? v * f.inveps[c][i] : v;
+    if (pml_at(f, g, c, qcoord(g, p, T_E, c, c)))
+      f.WE[c][i] = w;
+    else
+      f.En[c][i] = w;
+  }
+}
+
+template <bool SHELL>
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_aniso_kernel(Box b, BoxList bl,
+                                                                            DevGrid g, DevFields f) {
+  Pt p;
+  if (!map_pt<SHELL>(b, bl, g, p)) return;
+  const long long i = p.idx;
+  for (int d = 0; d < 3; d++) {
+    if (!f.ecomp_present[d] || !(owned(g, T_E, d, p) || on_wall(g, d, p))) continue;
+    const int zb = zone_box(f, g, p, d);
+    const double wv = w_at(f, g, p, d, i, zb);
+    const long long is = g.sdir[d];
+    Pt pu = p;  // the point i + s (one step along d)
+    if (g.ax[d] >= 0) pu.j[d] += 1;
+    for (int k = 0; k < f.npol; k++) {
+      const PolDev &pd = f.pol[k];
+      if (!pd.P[d] || !pd.sigma[d]) continue;
+      const unsigned zbits = pd.zbits ? pd.zbits[zb] : (1u << (4 * d));
+      if (!((zbits >> (4 * d)) & 1)) continue;  // row trivial in this chunk
+      int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
+      const double *s1 = f.ecomp_present[d1] && ((zbits >> (3 * d + d1)) & 1) ? pd.soff[d][d1] : nullptr;
+      const double *s2 = f.ecomp_present[d2] && ((zbits >> (3 * d + d2)) & 1) ? pd.soff[d][d2] : nullptr;
+      if (s2 && !s1) {
+        const int t = d1;
+        d1 = d2;
+        d2 = t;
+        s1 = s2;
+        s2 = nullptr;
+      }
+      const double *s = pd.sigma[d];
+      double *P = pd.P[d], *Pp = pd.Pp[d];
+      // OFFDIAG(u, g, sx, s) = 0.25*((g[i] + g[i-sx])*u[i] + (g[i+s] + g[(i+s)-sx])*u[i+s])
+      auto offd = [&](const double *u, int dd) -> double {
+        const long long sx = g.sdir[dd];
+        Pt pm = p, pum = pu;
+        if (g.ax[dd] >= 0) pm.j[dd] -= 1, pum.j[dd] -= 1;
+        const double g0 = w_at(f, g, p, dd, i, zb), g1 = w_at(f, g, pm, dd, i - sx, zb);
+        const double g2 = w_at(f, g, pu, dd, i + is, zb), g3 = w_at(f, g, pum, dd, (i + is) - sx, zb);
+        return 0.25 * ((g0 + g1) * u[i] + (g2 + g3) * u[i + is]);
+      };
+      if (s1) {
+        if (s[i] == 0) continue;  // the PR #666 guard of the anisotropic branches
+        double x = s[i] * wv + offd(s1, d1);
+        if (s2) x = x + offd(s2, d2);
+        const double pcur = P[i];
+        P[i] = pd.gamma1inv * (pcur * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * Pp[i] +
+                               pd.omega0dtsqr * x);
+        Pp[i] = pcur;
+      } else {
+        if (!in_box(pd.nz, p)) continue;
+        const double pcur = P[i];
+        P[i] = pd.gamma1inv * (pcur * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * Pp[i] +
+                               pd.omega0dtsqr * (s[i] * wv));
+        Pp[i] = pcur;
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------- sources
 // fields_chunk::step_source (src/step.cpp:296-319): f -= real(amp*J*dt), times
 // cndinv with conductivity (real((A*dt)*cndinv) = real(A*dt)*cndinv), applied
@@ -834,11 +968,24 @@ int k_update_pols(const Box &in, const BoxList *sh, const DevGrid &g, const DevF
   BoxList none{};
   if (!sh) {
     if (empty(in)) return 0;
-    update_pols_kernel<false><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(in, none, g, f);
+    if (f.aniso)
+      update_pols_aniso_kernel<false><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(in, none, g, f);
+    else
+      update_pols_kernel<false><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(in, none, g, f);
   } else {
     if (sh->n == 0 || sh->start[sh->n] == 0) return 0;
-    update_pols_kernel<true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f);
+    if (f.aniso)
+      update_pols_aniso_kernel<true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f);
+    else
+      update_pols_kernel<true><<<lin_grid(*sh), 256, 0, s>>>(in, *sh, g, f);
   }
+  return rc();
+}
+
+int k_aniso_wall(const DevGrid &g, const DevFields &f, int zero, void *stream) {
+  Box all;
+  for (int a = 0; a < 3; a++) all.lo[a] = 0, all.hi[a] = g.N[a] - 1;
+  aniso_wall_kernel<<<grid_for(all), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(all, g, f, zero);
   return rc();
 }
 

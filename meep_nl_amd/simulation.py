@@ -66,11 +66,19 @@ class LorentzianSusceptibility:
 
     drude = False
 
-    def __init__(self, frequency=0.0, gamma=0.0, sigma=1.0, sigma_diag=None):
+    def __init__(self, frequency=0.0, gamma=0.0, sigma=1.0, sigma_diag=None, sigma_offdiag=None):
         self.frequency = float(frequency)
         self.gamma = float(gamma)
         sd = sigma_diag if sigma_diag is not None else Vector3(sigma, sigma, sigma)
         self.sigma_diag = Vector3(*sd)
+        # (xy, xz, yz) of the symmetric sigma tensor (python/geom.py:717-737)
+        self.sigma_offdiag = Vector3(*(sigma_offdiag if sigma_offdiag is not None else (0, 0, 0)))
+
+    def sigma_row(self, c):
+        """Row c of the sigma tensor [[a, u, v], [u, b, w], [v, w, c]]."""
+        dg, od = self.sigma_diag, self.sigma_offdiag
+        t = [[dg.x, od.x, od.y], [od.x, dg.y, od.z], [od.y, od.z, dg.z]]
+        return t[c]
 
     def key(self):
         return (self.frequency, self.gamma, self.drude)
@@ -463,14 +471,15 @@ class Simulation:
                                                      else [sz.x, sz.y, sz.z])
         return core.GridVolume.vol(self.dimensions, sizes, self.resolution, center_origin=True)
 
-    def _materials_at(self, gv, c):
-        """Per-point material of E component c (no subpixel averaging)."""
+    def _materials_at(self, gv, c, offset=(0.0, 0.0, 0.0)):
+        """Per-point material of component c (no subpixel averaging), optionally at
+        the Yee points shifted by `offset`."""
         pts = gv.coords(c)
         full = [np.zeros(gv.shape()) for _ in range(3)]
         k = 0
         for d in range(3):
             if gv.has[d]:
-                full[d] = pts[k]
+                full[d] = pts[k] + offset[d]
                 k += 1
         idx = np.full(gv.shape(), -1, dtype=np.int32)
         for i, g in enumerate(self.geometry):
@@ -504,7 +513,7 @@ class Simulation:
                 if su.key() not in sus_keys:
                     sus_keys.append(su.key())
         comps = (Ex,) if self.dimensions == 1 else (Ex, Ey, Ez)
-        sus_sig = {k: [None, None, None] for k in sus_keys}
+        sus_sig = {k: [[None] * 3 for _ in range(3)] for k in sus_keys}
         for c in comps:
             d = c % 3
             which, mats = self._materials_at(gv, c)
@@ -531,14 +540,25 @@ class Simulation:
             if need_chi2:
                 s.set_chi2(c, table(lambda m: m.E_chi2))
             for key in sus_keys:
-                def sig(m, key=key):
+                def sig(m, key=key, row=d, col=d):
                     for su in m.E_susceptibilities:
                         if su.key() == key:
-                            return su.sigma_diag[d]
+                            return su.sigma_row(row)[col]
                     return 0.0
-                sus_sig[key][d] = table(sig)
+                sus_sig[key][d][d] = table(sig)
+                if any(su.sigma_offdiag != Vector3() for m in mats for su in m.E_susceptibilities
+                       if su.key() == key):
+                    # off-diagonal entries sampled half a pixel back along d
+                    # (src/anisotropic_averaging.cpp:334-341)
+                    h = [0.0, 0.0, 0.0]
+                    h[d] = -0.5 / self.resolution
+                    which_o, mats_o = self._materials_at(gv, c, offset=h)
+                    for col in range(3):
+                        if col != d and self.dimensions != 1:
+                            sus_sig[key][d][col] = np.array(
+                                [sig(m, col=col) for m in mats_o], dtype=np.float64)[which_o]
         for key in sus_keys:
-            s.add_lorentzian(key[0], key[1], sus_sig[key], drude=key[2])
+            s.add_lorentzian_tensor(key[0], key[1], sus_sig[key], drude=key[2])
         # structure::set_materials -> set_conductivity(c, mat) for the D and B
         # components with nonzero conductivity (src/structure.cpp:378-380, 868-905),
         # sampled at each component's own Yee points

@@ -350,6 +350,9 @@ struct Chunk {
   // structure_chunk::conductivity[c][d_c] / condinv of D and B comps, f_cond
   std::vector<realnum> cond[NCOMP], condinv[NCOMP], fcond[NCOMP];
   std::vector<std::vector<realnum>> psigma;  // per susceptibility: [3 E comps] flattened
+  // off-diagonal sigma[c][d] (d != c) per susceptibility: [k*9 + 3*c + d]; empty =
+  // trivial in this chunk (anisotropic_averaging.cpp:351-357)
+  std::vector<std::vector<realnum>> psoff;
   std::vector<std::vector<realnum> *> dummy;
   std::vector<PolData> pol;
   std::vector<SrcVol> srcD, srcB;
@@ -364,6 +367,7 @@ struct Lorentz {
   double omega0, gamma;
   bool drude;
   bool nontrivial[3];
+  bool nt_off[3][3] = {};  // global (and_to_all) off-diagonal flags, structure.cpp:491-506
 };
 
 }  // namespace
@@ -392,6 +396,7 @@ struct orc_sim {
   std::vector<realnum> g_cond[NCOMP];  // D / B comps
   std::vector<Lorentz> lor;
   std::vector<std::vector<realnum>> g_lsig[3];  // per E-comp dir: per susceptibility
+  std::vector<std::vector<realnum>> g_lsig_off[3][3];  // [c][d], d != c: per susceptibility
   std::vector<SrcTime> srcs;
   // connections: per chunk, per field type, list of (dst index, src chunk, src index, comp)
   struct Conn {
@@ -687,14 +692,30 @@ void finalize(orc_sim *s) {
     // so the pol list order is the reverse of the add order.
     size_t nl = s->lor.size();
     ch.psigma.assign(nl * 3, std::vector<realnum>());
+    ch.psoff.assign(nl * 9, std::vector<realnum>());
     ch.pol.assign(nl, PolData());
     for (size_t k = 0; k < nl; k++) {
       size_t src = nl - 1 - k;  // pol index k <- susceptibility added at position src
       for (int c = Ex; c <= Ez; c++) {
-        if (!G.has_field(c) || s->g_lsig[c][src].empty()) continue;
+        if (!G.has_field(c)) continue;
+        // anisotropic_averaging.cpp:317-362: trivial off-diagonal arrays are
+        // deleted per chunk, the diagonal one only if the whole row is trivial
+        bool row = false;
+        for (int d = 0; d < 3; d++) {
+          if (d == c || s->g_lsig_off[c][d][src].empty()) continue;
+          std::vector<realnum> v;
+          scatter_to_chunk(G, ch, c, s->g_lsig_off[c][d][src], v);
+          if (!all_equal(v, 0.0)) {
+            ch.psoff[k * 9 + 3 * c + d] = std::move(v);
+            row = true;
+          }
+        }
         std::vector<realnum> v;
-        scatter_to_chunk(G, ch, c, s->g_lsig[c][src], v);
-        if (!all_equal(v, 0.0)) ch.psigma[k * 3 + c] = std::move(v);
+        if (!s->g_lsig[c][src].empty())
+          scatter_to_chunk(G, ch, c, s->g_lsig[c][src], v);
+        else if (row)
+          v.assign(ch.gv.ntot, 0.0);
+        if (!v.empty() && (row || !all_equal(v, 0.0))) ch.psigma[k * 3 + c] = std::move(v);
       }
     }
   }
@@ -782,6 +803,26 @@ void step_boundaries(orc_sim *s, int ftype) {  // src/step.cpp:226-288
       if (ctype(cn.c) != ftype) continue;
       realnum *dst = ch.F(cn.c);
       realnum *src = s->chunks[cn.jc].F(cn.c);
+      if (dst && src) dst[cn.dst] = src[cn.src];
+    }
+  }
+}
+
+bool needs_W_notowned(const orc_sim *s, int c);
+// WE_stuff ghosts (boundaries.cpp:407-408, 508-525): where a W is read off the
+// diagonal, every ghost of (f_w or f) takes the owner's (f_w or f)
+void step_boundaries_W(orc_sim *s) {
+  if (!s->conn_valid) connect_chunks(s);
+  bool need[3];
+  for (int d = 0; d < 3; d++) need[d] = s->allocated[tcomp(T_E, d)] && needs_W_notowned(s, tcomp(T_E, d));
+  if (!need[0] && !need[1] && !need[2]) return;
+  for (size_t i = 0; i < s->chunks.size(); i++) {
+    Chunk &ch = s->chunks[i];
+    for (const auto &cn : s->conn[i]) {
+      if (ctype(cn.c) != T_E || !need[cdir(cn.c)]) continue;
+      Chunk &o = s->chunks[cn.jc];
+      realnum *dst = !ch.fw[cn.c].empty() ? ch.fw[cn.c].data() : ch.F(cn.c);
+      const realnum *src = !o.fw[cn.c].empty() ? o.fw[cn.c].data() : o.F(cn.c);
       if (dst && src) dst[cn.dst] = src[cn.src];
     }
   }
@@ -1047,9 +1088,29 @@ void step_update_EDHB(orc_sim *s, const GV &g, realnum *f, int fc, const realnum
   }
 }
 
-bool pol_needs_P(orc_sim *s, int c) {  // susceptibility.cpp:76-82 (global trivial flags)
+// susceptibility::needs_P (susceptibility.cpp:76-82, global trivial flags): some
+// sigma[c][d] nontrivial whose W (E component d) exists
+bool lor_needs_P(const orc_sim *s, const Lorentz &L, int c) {
+  for (int d = 0; d < 3; d++) {
+    const bool nt = d == cdir(c) ? L.nontrivial[d] : L.nt_off[cdir(c)][d];
+    if (nt && s->allocated[tcomp(T_E, d)]) return true;
+  }
+  return false;
+}
+bool pol_needs_P(orc_sim *s, int c) {
   for (auto &L : s->lor)
-    if (L.nontrivial[cdir(c)]) return true;
+    if (lor_needs_P(s, L, c)) return true;
+  return false;
+}
+// susceptibility::needs_W_notowned (susceptibility.cpp:88-96): W of E comp c is
+// read off-diagonally by another component's P update
+bool needs_W_notowned(const orc_sim *s, int c) {
+  for (auto &L : s->lor)
+    for (int d = 0; d < 3; d++) {
+      if (d == cdir(c)) continue;
+      const int cP = tcomp(T_E, d);
+      if (lor_needs_P(s, L, cP) && L.nt_off[d][cdir(c)]) return true;
+    }
   return false;
 }
 
@@ -1149,7 +1210,7 @@ void update_pols(orc_sim *s) {
       const Lorentz &L = s->lor[s->lor.size() - 1 - k];
       if (!pd.allocated) {
         for (int d = 0; d < 3; d++)
-          if (s->allocated[tcomp(T_E, d)] && L.nontrivial[d]) {
+          if (s->allocated[tcomp(T_E, d)] && lor_needs_P(s, L, tcomp(T_E, d))) {
             pd.P[d].assign(g.ntot, 0.0);
             pd.Pp[d].assign(g.ntot, 0.0);
           }
@@ -1160,20 +1221,65 @@ void update_pols(orc_sim *s) {
       const realnum omega0dtsqr = omega2pi * omega2pi * s->dt * s->dt;
       const realnum gamma1inv = 1 / (1 + g2pi * s->dt / 2), gamma1 = (1 - g2pi * s->dt / 2);
       const realnum omega0dtsqr_denom = L.drude ? 0 : omega0dtsqr;
+      auto W = [&](int cc) -> const realnum * {  // update_pols.cpp:44
+        if (!s->allocated[cc]) return nullptr;
+        return !ch.fw[cc].empty() ? ch.fw[cc].data() : ch.F(cc);
+      };
       for (int d = 0; d < 3; d++) {
         if (pd.P[d].empty()) continue;
         int c = tcomp(T_E, d);
-        const realnum *w = !ch.fw[c].empty() ? ch.fw[c].data() : ch.F(c);
+        const realnum *w = W(c);
         const std::vector<realnum> &sv = ch.psigma[k * 3 + d];
         if (!w || sv.empty()) continue;
         const realnum *sg = sv.data();
         realnum *p = pd.P[d].data(), *pp = pd.Pp[d].data();
-        loop_owned(g, c, [&](long i, const int *) {
-          realnum pcur = p[i];
-          p[i] = gamma1inv *
-                 (pcur * (2 - omega0dtsqr_denom) - gamma1 * pp[i] + omega0dtsqr * (sg[i] * w[i]));
-          pp[i] = pcur;
-        });
+        // susceptibility.cpp:206-226: off-diagonal partners
+        const long is = g.s[d];
+        int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
+        long is1 = g.s[d1], is2 = g.s[d2];
+        const realnum *w1 = W(tcomp(T_E, d1)), *w2 = W(tcomp(T_E, d2));
+        auto off = [&](int dd) -> const realnum * {
+          const auto &v = ch.psoff[k * 9 + 3 * d + dd];
+          return v.empty() ? nullptr : v.data();
+        };
+        const realnum *s1 = w1 ? off(d1) : nullptr, *s2 = w2 ? off(d2) : nullptr;
+        if (s2 && !s1) {
+          std::swap(d1, d2);
+          std::swap(is1, is2);
+          std::swap(w1, w2);
+          std::swap(s1, s2);
+        }
+        // OFFDIAG(u, g, sx, s), susceptibility.cpp:185-186
+        auto OFFD = [&](const realnum *u, const realnum *gg, long sx, long i) -> realnum {
+          return 0.25 * ((gg[i] + gg[i - sx]) * u[i] + (gg[i + is] + gg[(i + is) - sx]) * u[i + is]);
+        };
+        if (s1 && s2) {  // 3x3 (227-240)
+          loop_owned(g, c, [&](long i, const int *) {
+            if (sg[i] != 0) {
+              realnum pcur = p[i];
+              p[i] = gamma1inv * (pcur * (2 - omega0dtsqr_denom) - gamma1 * pp[i] +
+                                  omega0dtsqr * (sg[i] * w[i] + OFFD(s1, w1, is1, i) +
+                                                 OFFD(s2, w2, is2, i)));
+              pp[i] = pcur;
+            }
+          });
+        } else if (s1) {  // 2x2 (241-250)
+          loop_owned(g, c, [&](long i, const int *) {
+            if (sg[i] != 0) {
+              realnum pcur = p[i];
+              p[i] = gamma1inv * (pcur * (2 - omega0dtsqr_denom) - gamma1 * pp[i] +
+                                  omega0dtsqr * (sg[i] * w[i] + OFFD(s1, w1, is1, i)));
+              pp[i] = pcur;
+            }
+          });
+        } else {  // isotropic (251-258)
+          loop_owned(g, c, [&](long i, const int *) {
+            realnum pcur = p[i];
+            p[i] = gamma1inv *
+                   (pcur * (2 - omega0dtsqr_denom) - gamma1 * pp[i] + omega0dtsqr * (sg[i] * w[i]));
+            pp[i] = pcur;
+          });
+        }
       }
     }
   }
@@ -1198,6 +1304,7 @@ void step_once(orc_sim *s) {  // fields::step, src/step.cpp:35-140
   step_boundaries(s, T_D);
   calc_sources(s, time + s->dt);
   update_eh(s, T_E);
+  step_boundaries_W(s);
   update_pols(s);
   step_boundaries_P(s);
   step_boundaries(s, T_E);
@@ -1510,12 +1617,34 @@ int orc_set_chi3(orc_sim *s, int comp, const double *arr) {
 }
 int orc_add_lorentzian(orc_sim *s, double omega0, double gamma, int drude, const double *sx,
                        const double *sy, const double *sz) {
+  const double *sig[9] = {sx, nullptr, nullptr, nullptr, sy, nullptr, nullptr, nullptr, sz};
+  return orc_add_lorentzian_tensor(s, omega0, gamma, drude, sig);
+}
+
+// structure::add_susceptibility with a sigma tensor (anisotropic_averaging.cpp:
+// 300-372): sig[3*c + d] = row of E comp c, column d, at c's Yee points (the
+// caller samples the off-diagonal entries half a pixel back along c, 334-341)
+int orc_add_lorentzian_tensor(orc_sim *s, double omega0, double gamma, int drude,
+                              const double *const sig[9]) {
   if (s->finalized) return set_err("structure already finalized");
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) {
+      if (d == c) continue;
+      std::vector<realnum> v;
+      bool nt = false;
+      if (sig[3 * c + d] && s->gv.has_field(tcomp(T_E, c))) {
+        v.assign(sig[3 * c + d], sig[3 * c + d] + s->gv.ntot);
+        nt = !all_equal(v, 0.0);
+      }
+      s->g_lsig_off[c][d].push_back(nt ? std::move(v) : std::vector<realnum>());
+    }
+  const double *sv[3] = {sig[0], sig[4], sig[8]};
   Lorentz L;
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) L.nt_off[c][d] = d != c && !s->g_lsig_off[c][d].back().empty();
   L.omega0 = omega0;
   L.gamma = gamma;
   L.drude = drude != 0;
-  const double *sv[3] = {sx, sy, sz};
   for (int d = 0; d < 3; d++) {
     std::vector<realnum> v;
     L.nontrivial[d] = false;

@@ -30,6 +30,9 @@ int orc_set_chi3(orc_sim *s, int comp, const double *arr);
 int orc_set_conductivity(orc_sim *s, int comp, const double *arr);
 int orc_add_lorentzian(orc_sim *s, double omega0, double gamma, int drude, const double *sx,
                        const double *sy, const double *sz);
+/* sigma tensor: sig[3*c + d] (row of E comp c, column d; NULL = 0) */
+int orc_add_lorentzian_tensor(orc_sim *s, double omega0, double gamma, int drude,
+                              const double *const sig[9]);
 int orc_add_point_source(orc_sim *s, int comp, int kind, const double *params, int nparams,
                          const double pos[3], double amp_re, double amp_im, int is_integrated);
 int orc_require_component(orc_sim *s, int comp);

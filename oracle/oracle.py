@@ -43,6 +43,8 @@ def lib():
         L.orc_set_chi2.argtypes = [c_void, c_int, dptr]
         L.orc_set_chi3.argtypes = [c_void, c_int, dptr]
         L.orc_set_conductivity.argtypes = [c_void, c_int, dptr]
+        L.orc_add_lorentzian_tensor.argtypes = [c_void, ctypes.c_double, ctypes.c_double, c_int,
+                                                ctypes.POINTER(dptr)]
         L.orc_add_lorentzian.argtypes = [c_void, c_double, c_double, c_int, dptr, dptr, dptr]
         L.orc_add_point_source.argtypes = [c_void, c_int, c_int, dptr, c_int, dptr, c_double,
                                            c_double, c_int]
@@ -163,6 +165,13 @@ class Oracle:
         component, None = zero."""
         a = None if arr is None else np.ascontiguousarray(arr, dtype=np.float64).ravel()
         _chk(lib().orc_set_conductivity(self.h, comp, None if a is None else _dp(a)))
+
+    def add_lorentzian_tensor(self, omega0, gamma, sigma, drude=False):
+        arrs = [None if sigma[c][d] is None else
+                np.ascontiguousarray(sigma[c][d], dtype=np.float64).ravel()
+                for c in range(3) for d in range(3)]
+        ptrs = (ctypes.POINTER(ctypes.c_double) * 9)(*[_dp(a) if a is not None else None for a in arrs])
+        _chk(lib().orc_add_lorentzian_tensor(self.h, omega0, gamma, int(drude), ptrs))
 
     def add_lorentzian(self, omega0, gamma, sigmas, drude=False):
         s = [None if v is None else np.ascontiguousarray(v, dtype=np.float64).ravel()

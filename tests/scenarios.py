@@ -60,6 +60,9 @@ class ProductSim:
     def set_conductivity(self, c, arr):
         self.s.set_conductivity(c, arr)
 
+    def add_lorentzian_tensor(self, *a, **k):
+        self.s.add_lorentzian_tensor(*a, **k)
+
     def add_lorentzian(self, *a, **k):
         self.s.add_lorentzian(*a, **k)
 
@@ -743,5 +746,43 @@ def sc_conductive_2d(make, steps=80):
         o.set_conductivity(c, np.where(x > 1.0, 0.3 + 0.05 * c, 0.0))
     o.add_gaussian_source(5, 0.4, 3.0, 0.0, 30.0, (1.03, 0.77), 2.0)
     o.add_gaussian_source(2, 0.35, 3.0, 0.0, 30.0, (1.4, 1.1), 1.0)
+    o.step(steps)
+    return o
+
+
+# ------------------------------------------------- anisotropic Lorentzian
+def sc_aniso_lorentz_3d(make, steps=40, full=True):
+    """Anisotropic Lorentzian sigma (update_P's 3x3 / 2x2 branches and OFFDIAG
+    averaging, src/susceptibility.cpp:185-250): a slab with a full symmetric
+    tensor crossing into the PML chunks (f_w as W), a second susceptibility with
+    only an xy term in a box (2x2 branch; isotropic chunks elsewhere), eps."""
+    o = vol(make, 3, [3.2, 2.8, 3.0], 10, center_origin=True)
+    o.add_pml(0.7)
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        o.set_chi1inv(c, c, np.where(np.abs(z) < 0.6, 1 / 2.25, 1.0))
+    diag = (0.5, 0.4, 0.3)
+    off = {(0, 1): 0.12, (0, 2): 0.07, (1, 2): 0.05} if full else {(0, 1): 0.12}
+    sig = [[None] * 3 for _ in range(3)]
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        sig[c][c] = np.where(np.abs(z) < 0.6, diag[c], 0.0)
+        h = 0.5 / 10  # off-diagonal entries half a pixel back along c
+        xs, ys, zs = x - h * (c == 0), y - h * (c == 1), z - h * (c == 2)
+        for (a, b), v in off.items():
+            for (r, col) in ((a, b), (b, a)):
+                if r == c:
+                    sig[c][col] = np.where(np.abs(zs) < 0.6, v, 0.0)
+    o.add_lorentzian_tensor(1.1, 0.05, sig)
+    sig2 = [[None] * 3 for _ in range(3)]
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        box = (np.abs(x - 0.3) < 0.5) & (np.abs(y) < 0.4) & (z > 0.7) & (z < 1.2)
+        sig2[c][c] = np.where(box, 0.3, 0.0)
+        if c in (0, 1):
+            sig2[c][1 - c] = np.where(box, 0.1, 0.0)
+    o.add_lorentzian_tensor(0.8, 0.1, sig2)
+    o.add_gaussian_source(0, 0.3, 4.0, 0.0, 40.0, (0.05, 0.05, -0.2), 10.0)
+    o.add_gaussian_source(1, 0.35, 4.0, 0.0, 40.0, (0.4, -0.1, 0.9), 5.0)
     o.step(steps)
     return o
