@@ -30,6 +30,8 @@ _SIGS = {
     "mnl_structure_add_lorentzian_tensor": (c_int, [c_void, ctypes.c_double, ctypes.c_double,
                                                     c_int, ctypes.POINTER(dptr)]),
     "mnl_fields_dump": (c_int, [c_void, ctypes.c_char_p]),
+    "mnl_fields_array_slice": (c_int, [c_void, c_int, dptr, dptr, ctypes.POINTER(c_int),
+                                       ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]),
     "mnl_fields_load": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_dump": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_load": (c_int, [c_void, ctypes.c_char_p]),

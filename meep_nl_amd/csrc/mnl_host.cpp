@@ -2842,6 +2842,160 @@ int structure_load(mnl_structure *S, const char *path) {
   return 0;
 }
 
+// ------------------------------------------------------------- array slices
+// fields::get_array_slice(volume, c) for real fields without symmetry
+// (src/array_slice.cpp:251-433, 447-507, 525-601, 611-704): loop_in_chunks over
+// the Centered grid in the reference's chunks, each point the average of the
+// component's four Yee neighbours (yee2cent_offsets, src/vec.cpp:333-344)
+// times the interpolation weights of the empty dimensions only
+// (IVEC_LOOP_WEIGHT with s0i..e1i, src/meep/vec.hpp:372-383), then the empty
+// dimensions collapsed by summation (collapse_array, snap = false).  Host-side
+// from the whole-cell component array, as the reference's CPU loop.
+inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) {
+  return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
+}
+
+int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3], int *rank,
+                long long dims[3], double *out, long long nout) {
+  const mnl_structure &S = F->S;
+  if (F->nranks > 1) return fail("array slices of distributed fields are not supported");
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    is[d] = 1 + 2 * int(floor(vmin[d] * S.a - .5));
+    ie[d] = 1 + 2 * int(ceil(vmax[d] * S.a - .5));
+  }
+  double s0[3], s1[3], e0[3], e1[3];
+  dft_boundary_weights(S, vmin, vmax, is, ie, s0, e0, s1, e1);
+  struct Lp {
+    int is[3], ie[3];
+    double s0[3], s1[3], e0[3], e1[3];
+  };
+  std::vector<Lp> loops;
+  for (auto &ch : reference_chunks(S)) {
+    Lp L;
+    bool emp = false;
+    for (int d = 0; d < 3; d++) {
+      L.s0[d] = L.s1[d] = L.e0[d] = L.e1[d] = 1.0;
+      if (!S.has[d]) {
+        L.is[d] = L.ie[d] = 0;
+        continue;
+      }
+      const int uoc = S.io[d] + 1, coc = ch[d] + 1, cbo = ch[d] + 2 * ch[3 + d] - 1;
+      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
+      L.is[d] = std::max(is[d], iscoS);
+      L.ie[d] = std::min(ie[d], iecoS);
+      if (L.is[d] > L.ie[d]) emp = true;
+    }
+    if (emp) continue;
+    for (int d = 0; d < 3; d++) {  // per-chunk weights (loop_in_chunks.cpp:430-470)
+      if (!S.has[d]) continue;
+      if (L.is[d] == is[d]) {
+        L.s0[d] = s0[d];
+        L.s1[d] = s1[d];
+      } else if (L.is[d] == is[d] + 2) {
+        L.s0[d] = s1[d];
+      }
+      if (L.ie[d] == ie[d]) {
+        L.e0[d] = e0[d];
+        L.e1[d] = e1[d];
+      } else if (L.ie[d] == ie[d] - 2) {
+        L.e0[d] = e1[d];
+      }
+      if (L.ie[d] == L.is[d]) {
+        double w = std::min(L.s0[d], L.e0[d]);
+        L.s0[d] = L.e0[d] = L.s1[d] = L.e1[d] = w;
+      } else if (L.ie[d] == L.is[d] + 2) {
+        double w = std::min(L.s0[d], L.e1[d]);
+        L.s0[d] = w, L.e1[d] = w;
+        w = std::min(L.s1[d], L.e0[d]);
+        L.s1[d] = w, L.e0[d] = w;
+      } else if (L.ie[d] == L.is[d] + 4) {
+        double w = std::min(L.s1[d], L.e1[d]);
+        L.s1[d] = w, L.e1[d] = w;
+      }
+    }
+    loops.push_back(L);
+  }
+  // get_array_slice_dimensions: corners over all chunks, directions with n > 1
+  int mn[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, mx[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  for (auto &L : loops)
+    for (int d = 0; d < 3; d++) mn[d] = std::min(mn[d], L.is[d]), mx[d] = std::max(mx[d], L.ie[d]);
+  int r = 0, ds[3] = {0, 0, 0};
+  long long full[3] = {1, 1, 1};
+  if (!loops.empty())
+    for (int d = 0; d < 3; d++) {
+      if (!S.has[d]) continue;
+      long long n = (mx[d] - mn[d]) / 2 + 1;
+      if (n > 1) ds[r] = d, full[r++] = n;
+    }
+  int rr = 0;
+  long long rd[3] = {1, 1, 1};
+  for (int k = 0; k < r; k++)
+    if (vmax[ds[k]] - vmin[ds[k]] != 0.0) rd[rr++] = full[k];
+  *rank = rr;
+  for (int k = 0; k < 3; k++) dims[k] = k < rr ? rd[k] : 1;
+  if (!out) return 0;
+  long long rs[3] = {0, 0, 0}, nred = 1;
+  for (int k = r - 1; k >= 0; k--)
+    if (vmax[ds[k]] - vmin[ds[k]] != 0.0) rs[k] = nred, nred *= full[k];
+  if (nout < nred) return fail("output buffer too small");
+  for (long long k = 0; k < nred; k++) out[k] = 0.0;
+  if (loops.empty()) return 0;
+  std::vector<double> f(S.ntot);
+  if (mnl_fields_copy_component(F, c, f.data(), f.size())) return -1;
+  long long o1 = 0, o2 = 0;
+  for (int d = 0; d < 3; d++)
+    if (S.has[d] && !S.shift(c, d)) {
+      if (o1)
+        o2 = S.cstride(d);
+      else
+        o1 = S.cstride(d);
+    }
+  long long ntot = 1;
+  for (int k = 0; k < r; k++) ntot *= full[k];
+  std::vector<double> arr(ntot, 0.0);
+  bool empty_dim[3];
+  for (int d = 0; d < 3; d++) empty_dim[d] = S.has[d] && vmax[d] - vmin[d] == 0.0;
+  const int yd[3] = {S.dim == 2 ? 2 : 0, S.dim == 2 ? 0 : 1, S.dim == 2 ? 1 : 2};
+  for (auto &L : loops) {
+    int n[3];
+    for (int k = 0; k < 3; k++) n[k] = S.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
+    for (int i1 = 0; i1 < n[0]; i1++)
+      for (int i2 = 0; i2 < n[1]; i2++)
+        for (int i3 = 0; i3 < n[2]; i3++) {
+          const int ii[3] = {i1, i2, i3};
+          int p[3] = {0, 0, 0};
+          for (int k = 0; k < 3; k++)
+            if (S.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
+          double w[3];
+          for (int k = 0; k < 3; k++) {
+            const int d = yd[k];
+            w[k] = empty_dim[d] ? loop_w1(L.s0[d], L.s1[d], L.e0[d], L.e1[d], ii[k], n[k])
+                                : loop_w1(1.0, 1.0, 1.0, 1.0, ii[k], n[k]);
+          }
+          const double wt = w[2] * (w[1] * (1.0 * w[0]));
+          long long idx = 0;
+          for (int d = 0; d < 3; d++)
+            if (S.has[d]) idx += (long long)((p[d] - S.io[d]) / 2) * S.cstride(d);
+          const double avg = 0.25 * (f[idx] + f[idx + o1] + f[idx + o2] + f[idx + o1 + o2]);
+          const cplx v = wt * cplx(avg, 0.0) * cplx(1.0, 0.0);
+          long long oi = 0;
+          for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
+          arr[oi] = real(v);
+        }
+  }
+  for (long long q = 0; q < ntot; q++) {  // collapse_array: in full-index order
+    long long t = q, ri = 0;
+    for (int k = r - 1; k >= 0; k--) {
+      ri += (t % full[k]) * rs[k];
+      t /= full[k];
+    }
+    out[ri] += arr[q];
+  }
+  return 0;
+}
+
 mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, const void *id,
                           LocalHub *hub = nullptr) {
   if (!s) {
@@ -3137,6 +3291,12 @@ int mnl_fields_step(mnl_fields *F, int nsteps) {
   if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
   if (step_batch(F, nsteps)) return -1;
   return nan_check(F);
+}
+
+int mnl_fields_array_slice(mnl_fields *F, int comp, const double vmin[3], const double vmax[3],
+                           int *rank, long long dims[3], double *out, long long nout) {
+  if (!F || check_comp(comp) || !vmin || !vmax || !rank || !dims) return fail("bad argument");
+  return array_slice(F, comp, vmin, vmax, rank, dims, out, nout);
 }
 
 int mnl_fields_dump(mnl_fields *F, const char *filename) {

@@ -732,6 +732,31 @@ class Simulation:
         self.init_sim()
         return self.fields.get_field(c, tuple(pt))
 
-    def get_array(self, component=Ez):
+    def get_array(self, component=Ez, vol=None, center=None, size=None, cmplx=None, arr=None,
+                  frequency=0, snap=False):
+        """Simulation.get_array (python/simulation.py:3872-3990) ->
+        fields::get_array_slice over the volume (default: the whole cell) on the
+        Centered grid, empty dimensions interpolated and collapsed.  Real fields
+        only; snap=True is not supported."""
+        self.init_sim()
+        if snap or cmplx or frequency:
+            raise NotImplementedError("get_array: snap / complex / frequency-dependent slices")
+        if vol is not None:
+            center, size = vol.center, vol.size
+        center = Vector3(*(center if center is not None else Vector3()))
+        size = Vector3(*(size if size is not None else self.cell_size))
+        lo, hi = [0.0] * 3, [0.0] * 3
+        dirs = (2,) if self.dimensions == 1 else ((0, 1) if self.dimensions == 2 else (0, 1, 2))
+        for d in dirs:
+            lo[d] = center[d] - 0.5 * size[d]
+            hi[d] = center[d] + 0.5 * size[d]
+        out = self.fields.get_array_slice(component, lo, hi)
+        if arr is not None:
+            arr[...] = out
+            return arr
+        return out
+
+    def get_component_array(self, component=Ez):
+        """The raw whole-cell array of a component (Yee layout, ghosts 0)."""
         self.init_sim()
         return self.fields.get_array(component)

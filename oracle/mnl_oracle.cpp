@@ -2059,3 +2059,175 @@ size_t orc_ntot(orc_sim *s) { return s->gv.ntot; }
 long long orc_nr_failures(orc_sim *s) { return s->nr_random; }
 
 }  // extern "C"
+
+namespace {
+// ---------------------------------------------------------------- array slices
+// fields::get_array_slice_dimensions / get_array_slice for one component,
+// real fields, no symmetry (src/array_slice.cpp:251-433, 447-507, 525-601,
+// 611-704): loop_in_chunks over the Centered grid, each point the average of
+// the component's four Yee neighbours (yee2cent_offsets, src/vec.cpp:333-344)
+// times the interpolation weights of the empty dimensions only, then the
+// empty dimensions collapsed by summation (snap = false).
+struct SliceLoop {
+  int ci, is[3], ie[3];
+  double s0[3], s1[3], e0[3], e1[3];
+};
+
+std::vector<SliceLoop> slice_loops(orc_sim *s, const double wmin[3], const double wmax[3]) {
+  const GV &G = s->gv;
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!G.has[d]) continue;
+    is[d] = 1 + 2 * int(floor(wmin[d] * G.a - .5));
+    ie[d] = 1 + 2 * int(ceil(wmax[d] * G.a - .5));
+  }
+  double s0[3], s1[3], e0[3], e1[3];
+  boundary_weights(G, wmin, wmax, is, ie, s0, e0, s1, e1);
+  std::vector<SliceLoop> out;
+  for (size_t ci = 0; ci < s->chunks.size(); ci++) {
+    const GV &g = s->chunks[ci].gv;
+    SliceLoop L;
+    L.ci = (int)ci;
+    bool empty = false;
+    for (int d = 0; d < 3; d++) {
+      L.s0[d] = L.s1[d] = L.e0[d] = L.e1[d] = 1.0;
+      if (!G.has[d]) {
+        L.is[d] = L.ie[d] = 0;
+        continue;
+      }
+      const int uoc = G.io[d] + 1, coc = g.io[d] + 1, cbo = g.big(d) - 1;
+      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
+      L.is[d] = std::max(is[d], iscoS);
+      L.ie[d] = std::min(ie[d], iecoS);
+      if (L.is[d] > L.ie[d]) empty = true;
+    }
+    if (empty) continue;
+    for (int d = 0; d < 3; d++) {
+      if (!G.has[d]) continue;
+      if (L.is[d] == is[d]) {
+        L.s0[d] = s0[d];
+        L.s1[d] = s1[d];
+      } else if (L.is[d] == is[d] + 2) {
+        L.s0[d] = s1[d];
+      }
+      if (L.ie[d] == ie[d]) {
+        L.e0[d] = e0[d];
+        L.e1[d] = e1[d];
+      } else if (L.ie[d] == ie[d] - 2) {
+        L.e0[d] = e1[d];
+      }
+      if (L.ie[d] == L.is[d]) {
+        double w = std::min(L.s0[d], L.e0[d]);
+        L.s0[d] = L.e0[d] = L.s1[d] = L.e1[d] = w;
+      } else if (L.ie[d] == L.is[d] + 2) {
+        double w = std::min(L.s0[d], L.e1[d]);
+        L.s0[d] = w, L.e1[d] = w;
+        w = std::min(L.s1[d], L.e0[d]);
+        L.s1[d] = w, L.e0[d] = w;
+      } else if (L.ie[d] == L.is[d] + 4) {
+        double w = std::min(L.s1[d], L.e1[d]);
+        L.s1[d] = w, L.e1[d] = w;
+      }
+    }
+    out.push_back(L);
+  }
+  return out;
+}
+
+inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) {  // vec.hpp:372-378
+  return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
+}
+
+}  // namespace
+
+extern "C" {
+int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3], int *rank,
+                    long long dims[3], double *out, long long nout) {
+  finalize(s);
+  const GV &G = s->gv;
+  auto loops = slice_loops(s, vmin, vmax);
+  int mn[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, mx[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  for (auto &L : loops)
+    for (int d = 0; d < 3; d++) mn[d] = std::min(mn[d], L.is[d]), mx[d] = std::max(mx[d], L.ie[d]);
+  int r = 0, ds[3];
+  long long full[3] = {1, 1, 1};
+  if (!loops.empty())
+    for (int d = 0; d < 3; d++) {
+      if (!G.has[d]) continue;
+      long long n = (mx[d] - mn[d]) / 2 + 1;
+      if (n > 1) ds[r] = d, full[r++] = n;
+    }
+  // collapsed dimensions (empty in the volume)
+  int rr = 0;
+  long long rd[3] = {1, 1, 1};
+  for (int k = 0; k < r; k++)
+    if (vmax[ds[k]] - vmin[ds[k]] != 0.0) rd[rr++] = full[k];
+  *rank = rr;
+  for (int k = 0; k < 3; k++) dims[k] = k < rr ? rd[k] : 1;
+  if (!out) return 0;
+  long long ntot = 1;
+  for (int k = 0; k < r; k++) ntot *= full[k];
+  std::vector<double> arr(loops.empty() ? 0 : ntot, 0.0);
+  bool empty_dim[3];
+  for (int d = 0; d < 3; d++) empty_dim[d] = G.has[d] && vmax[d] - vmin[d] == 0.0;
+  const int yd[3] = {G.dim == 2 ? 2 : 0, G.dim == 2 ? 0 : 1, G.dim == 2 ? 1 : 2};
+  for (auto &L : loops) {
+    Chunk &ch = s->chunks[L.ci];
+    const GV &g = ch.gv;
+    const realnum *f = ch.F(c);
+    long o1 = 0, o2 = 0;
+    for (int d = 0; d < 3; d++)
+      if (G.has[d] && !G.shift(c, d)) {
+        if (o1)
+          o2 = g.s[d];
+        else
+          o1 = g.s[d];
+      }
+    int n[3];
+    for (int k = 0; k < 3; k++) n[k] = G.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
+    for (int i1 = 0; i1 < n[0]; i1++)
+      for (int i2 = 0; i2 < n[1]; i2++)
+        for (int i3 = 0; i3 < n[2]; i3++) {
+          const int ii[3] = {i1, i2, i3};
+          int p[3] = {0, 0, 0};
+          for (int k = 0; k < 3; k++)
+            if (G.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
+          double w[3];
+          for (int k = 0; k < 3; k++) {
+            const int d = yd[k];
+            w[k] = empty_dim[d] ? loop_w1(L.s0[d], L.s1[d], L.e0[d], L.e1[d], ii[k], n[k])
+                                : loop_w1(1.0, 1.0, 1.0, 1.0, ii[k], n[k]);
+          }
+          const double wt = w[2] * (w[1] * (1.0 * w[0]));
+          long idx = 0;  // LOOP_OVER_IVECS index of the centered point in the chunk
+          for (int d = 0; d < 3; d++)
+            if (G.has[d]) idx += long((p[d] - g.io[d]) / 2) * g.s[d];
+          double avg = 0;
+          if (f) avg = 0.25 * (f[idx] + f[idx + o1] + f[idx + o2] + f[idx + o1 + o2]);
+          const cplx v = wt * cplx(avg, 0.0) * cplx(1.0, 0.0);
+          long long oi = 0;
+          for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
+          arr[oi] = real(v);
+        }
+  }
+  // collapse_array (array_slice.cpp:554-601): sum over the empty dimensions
+  long long rs[3] = {0, 0, 0}, acc = 1;
+  for (int k = r - 1; k >= 0; k--)
+    if (vmax[ds[k]] - vmin[ds[k]] != 0.0) rs[k] = acc, acc *= full[k];
+  long long nred = acc;
+  if (nout < nred) return set_err("output buffer too small");
+  for (long long k = 0; k < nred; k++) out[k] = 0.0;
+  if (arr.empty()) return 0;
+  long long m[3] = {0, 0, 0};
+  for (long long q = 0; q < ntot; q++) {
+    long long t = q, rem[3] = {0, 0, 0};
+    for (int k = r - 1; k >= 0; k--) rem[k] = t % full[k], t /= full[k];
+    long long ri = 0;
+    for (int k = 0; k < r; k++) ri += rem[k] * rs[k];
+    out[ri] += arr[q];
+  }
+  (void)m;
+  return 0;
+}
+
+}  // extern "C"

@@ -89,4 +89,4 @@ def test_simulation_dump_load(tmp_path):
     s2.run(until=1.5)
     assert s1.round_time() == s2.round_time()
     for c in (mp.Ex, mp.Ez, mp.Hy):
-        assert np.array_equal(s1.get_array(c), s2.get_array(c))
+        assert np.array_equal(s1.get_component_array(c), s2.get_component_array(c))
