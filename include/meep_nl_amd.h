@@ -35,7 +35,9 @@ enum {
 };
 enum { MNL_X = 0, MNL_Y = 1, MNL_Z = 2 };
 enum { MNL_LOW = 0, MNL_HIGH = 1 };
-enum { MNL_SRC_GAUSSIAN = 0, MNL_SRC_CONTINUOUS = 1 };
+enum { MNL_SRC_GAUSSIAN = 0, MNL_SRC_CONTINUOUS = 1, MNL_SRC_CUSTOM = 2 };
+/* custom_src_time callback: writes the complex dipole f(t) (src/meep.hpp:1059-1092) */
+typedef void (*mnl_src_func)(double t, void *data, double *re, double *im);
 
 typedef struct mnl_structure mnl_structure;
 typedef struct mnl_fields mnl_fields;
@@ -143,6 +145,14 @@ void mnl_fields_destroy(mnl_fields *f);
 int mnl_fields_add_point_source(mnl_fields *f, int comp, int kind, const double *params,
                                 int nparams, const double pos[3], double amp_re, double amp_im,
                                 int is_integrated);
+/* add_point_source with custom_src_time(func, data, start, end) (src/meep.hpp:
+ * 1059-1092; Python CustomSource, python/source.py:338-400): dipole(t) =
+ * func(t) for float(t) in [float(start), float(end)], else 0; current = dipole
+ * unless is_integrated (then the finite difference of the dipole).  func is
+ * called on the host thread that steps the fields. */
+int mnl_fields_add_custom_point_source(mnl_fields *f, int comp, mnl_src_func func, void *data,
+                                       double start_time, double end_time, const double pos[3],
+                                       double amp_re, double amp_im, int is_integrated);
 /* fields::require_component (src/fields.cpp:566-586). */
 int mnl_fields_require_component(mnl_fields *f, int comp);
 /* fields::step() x nsteps (src/step.cpp:35-140).  Collective for

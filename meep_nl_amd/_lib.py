@@ -13,6 +13,8 @@ _LIB = None
 
 c_int, c_double, c_void, c_size = ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
 dptr = ctypes.POINTER(ctypes.c_double)
+# custom_src_time callback (include/meep_nl_amd.h mnl_src_func)
+SRC_FUNC = ctypes.CFUNCTYPE(None, ctypes.c_double, ctypes.c_void_p, dptr, dptr)
 iptr = ctypes.POINTER(ctypes.c_int)
 llptr = ctypes.POINTER(ctypes.c_longlong)
 
@@ -29,6 +31,9 @@ _SIGS = {
     "mnl_structure_set_conductivity": (c_int, [c_void, c_int, dptr]),
     "mnl_structure_add_lorentzian_tensor": (c_int, [c_void, ctypes.c_double, ctypes.c_double,
                                                     c_int, ctypes.POINTER(dptr)]),
+    "mnl_fields_add_custom_point_source": (c_int, [c_void, c_int, SRC_FUNC, ctypes.c_void_p,
+                                                   ctypes.c_double, ctypes.c_double, dptr,
+                                                   ctypes.c_double, ctypes.c_double, c_int]),
     "mnl_fields_dump": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_fields_array_slice": (c_int, [c_void, c_int, dptr, dptr, ctypes.POINTER(c_int),
                                        ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]),

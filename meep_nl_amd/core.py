@@ -214,6 +214,26 @@ class Fields:
         self._last_times = getattr(self, "_last_times", [])
         self._last_times.append(_src_last_time(kind, list(params)))
 
+    def add_custom_source(self, comp, func, start, end, pos, amp=1.0, is_integrated=False):
+        """custom_src_time(func, data, start, end) (src/meep.hpp:1059-1092): func(t) ->
+        complex dipole, called on the host at every step.  One callback per Python
+        function, so sources sharing a function merge as in custom_src_time::is_equal."""
+        cbs = self.__dict__.setdefault("_custom_cbs", {})
+        if id(func) not in cbs:
+            def _cb(t, _data, re, im, func=func):
+                v = complex(func(t))
+                re[0] = v.real
+                im[0] = v.imag
+            cbs[id(func)] = (func, _lib.SRC_FUNC(_cb))
+        cf = cbs[id(func)][1]
+        pos = np.ascontiguousarray(list(pos) + [0.0] * (3 - len(pos)), dtype=np.float64)
+        amp = complex(amp)
+        check(lib().mnl_fields_add_custom_point_source(self.h, comp, cf, None, float(start),
+                                                       float(end), ptr(pos), amp.real, amp.imag,
+                                                       int(is_integrated)))
+        self._last_times = getattr(self, "_last_times", [])
+        self._last_times.append(float(np.float32(end)))
+
     def add_gaussian_source(self, comp, freq, width, start, end, pos, amp=1.0,
                             is_integrated=False):
         """gaussian_src_time(f, w, start, end) (src/sources.cpp:85-96)."""

@@ -63,8 +63,17 @@ struct SrcTime {
   double cwidth = 0, start_time = 0, end_time = 0, slowness = 3;
   double cur_time = NAN;
   cplx cur_dipole, cur_current;
+  mnl_src_func func = nullptr;  // kind 2: custom_src_time (src/meep.hpp:1059-1092)
+  void *fdata = nullptr;
 
   cplx dipole(double time) const {
+    if (kind == 2) {
+      const float rtime = float(time);
+      if (!(rtime >= start_time && rtime <= end_time)) return 0.0;
+      double re = 0, im = 0;
+      func(time, fdata, &re, &im);
+      return cplx(re, im);
+    }
     if (kind == 0) {
       double tt = time - peak_time;
       if (float(fabs(tt)) > cutoff) return 0.0;
@@ -83,7 +92,9 @@ struct SrcTime {
   void update(double time, double dt) {  // src_time::update, src/meep.hpp:972-978
     if (time != cur_time) {
       cur_dipole = dipole(time);
-      cur_current = (dipole(time + dt) - dipole(time)) / dt;
+      // custom_src_time::current: the dipole itself unless integrated
+      cur_current = (kind == 2 && !is_integrated) ? dipole(time)
+                                                 : (dipole(time + dt) - dipole(time)) / dt;
       cur_time = time;
     }
   }
@@ -91,7 +102,7 @@ struct SrcTime {
     return kind == o.kind && is_integrated == o.is_integrated && freq == o.freq &&
            width == o.width && peak_time == o.peak_time && cutoff == o.cutoff &&
            cfreq == o.cfreq && cwidth == o.cwidth && start_time == o.start_time &&
-           end_time == o.end_time && slowness == o.slowness;
+           end_time == o.end_time && slowness == o.slowness && func == o.func && fdata == o.fdata;
   }
 };
 
@@ -3050,6 +3061,55 @@ int check_comp(int c) {
   return 0;
 }
 
+int add_point_source_any(mnl_fields *F, int comp, int kind, const double *p, int np,
+                         mnl_src_func func, void *fdata, const double pos[3], double amp_re,
+                         double amp_im, int is_integrated) {
+  if (!F || check_comp(comp)) return -1;
+  if (!(ctype(comp) == T_E || ctype(comp) == T_H)) return fail("sources must be E or H components");
+  if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  SrcTime st;
+  if (kind == MNL_SRC_GAUSSIAN) {
+    if (np < 4) return fail("gaussian source needs 4 parameters");
+    // gaussian_src_time(f, w, st, et) (src/sources.cpp:85-96)
+    st.kind = 0;
+    st.freq = p[0];
+    st.width = p[1];
+    st.peak_time = 0.5 * (p[2] + p[3]);
+    st.cutoff = (p[3] - p[2]) * 0.5;
+    while (exp(-st.cutoff * st.cutoff / (2 * st.width * st.width)) < 1e-100) st.cutoff *= 0.9;
+    st.cutoff = float(st.cutoff);
+  } else if (kind == MNL_SRC_CONTINUOUS) {
+    if (np < 6) return fail("continuous source needs 6 parameters");
+    st.kind = 1;
+    st.cfreq = cplx(p[0], p[1]);
+    st.cwidth = p[2];
+    st.start_time = float(p[3]);
+    st.end_time = float(p[4]);
+    st.slowness = p[5];
+  } else if (kind == MNL_SRC_CUSTOM) {  // custom_src_time(func, data, st, et)
+    st.kind = 2;
+    st.func = func;
+    st.fdata = fdata;
+    st.start_time = float(p[0]);
+    st.end_time = float(p[1]);
+  } else
+    return fail("unknown source kind");
+  st.is_integrated = is_integrated != 0;
+  int idx = -1;
+  for (size_t i = 0; i < F->srcs.size(); i++)
+    if (F->srcs[i].same(st)) idx = (int)i;
+  if (idx < 0) {
+    F->srcs.push_back(st);
+    idx = (int)F->srcs.size() - 1;
+  }
+  if (require_component(F, comp)) return -1;
+  double pp[3] = {pos[0], pos[1], pos[2]};
+  if (F->S.dim == 1) pp[0] = pp[1] = 0;
+  if (F->S.dim == 2) pp[2] = 0;
+  return add_point_source(F, comp, idx, pp, cplx(amp_re, amp_im));
+}
+
 }  // namespace
 
 // =============================================================== C ABI
@@ -3238,45 +3298,19 @@ void mnl_fields_destroy(mnl_fields *f) { delete f; }
 int mnl_fields_add_point_source(mnl_fields *F, int comp, int kind, const double *p, int np,
                                 const double pos[3], double amp_re, double amp_im,
                                 int is_integrated) {
-  if (!F || check_comp(comp)) return -1;
-  if (!(ctype(comp) == T_E || ctype(comp) == T_H)) return fail("sources must be E or H components");
-  if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
-  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
-  SrcTime st;
-  if (kind == MNL_SRC_GAUSSIAN) {
-    if (np < 4) return fail("gaussian source needs 4 parameters");
-    // gaussian_src_time(f, w, st, et) (src/sources.cpp:85-96)
-    st.kind = 0;
-    st.freq = p[0];
-    st.width = p[1];
-    st.peak_time = 0.5 * (p[2] + p[3]);
-    st.cutoff = (p[3] - p[2]) * 0.5;
-    while (exp(-st.cutoff * st.cutoff / (2 * st.width * st.width)) < 1e-100) st.cutoff *= 0.9;
-    st.cutoff = float(st.cutoff);
-  } else if (kind == MNL_SRC_CONTINUOUS) {
-    if (np < 6) return fail("continuous source needs 6 parameters");
-    st.kind = 1;
-    st.cfreq = cplx(p[0], p[1]);
-    st.cwidth = p[2];
-    st.start_time = float(p[3]);
-    st.end_time = float(p[4]);
-    st.slowness = p[5];
-  } else
-    return fail("unknown source kind");
-  st.is_integrated = is_integrated != 0;
-  int idx = -1;
-  for (size_t i = 0; i < F->srcs.size(); i++)
-    if (F->srcs[i].same(st)) idx = (int)i;
-  if (idx < 0) {
-    F->srcs.push_back(st);
-    idx = (int)F->srcs.size() - 1;
-  }
-  if (require_component(F, comp)) return -1;
-  double pp[3] = {pos[0], pos[1], pos[2]};
-  if (F->S.dim == 1) pp[0] = pp[1] = 0;
-  if (F->S.dim == 2) pp[2] = 0;
-  return add_point_source(F, comp, idx, pp, cplx(amp_re, amp_im));
+  return add_point_source_any(F, comp, kind, p, np, nullptr, nullptr, pos, amp_re, amp_im,
+                              is_integrated);
 }
+
+int mnl_fields_add_custom_point_source(mnl_fields *F, int comp, mnl_src_func func, void *data,
+                                       double start_time, double end_time, const double pos[3],
+                                       double amp_re, double amp_im, int is_integrated) {
+  if (!func) return fail("custom source needs a function");
+  const double p[2] = {start_time, end_time};
+  return add_point_source_any(F, comp, MNL_SRC_CUSTOM, p, 2, func, data, pos, amp_re, amp_im,
+                              is_integrated);
+}
+
 
 int mnl_fields_require_component(mnl_fields *F, int comp) {
   if (!F || check_comp(comp)) return -1;

@@ -176,6 +176,19 @@ class ContinuousSource(SourceTime):
         return 1, [f.real, f.imag, self.width, self.start_time, self.end_time, self.slowness]
 
 
+class CustomSource(SourceTime):
+    """python/source.py:338-400 -> custom_src_time(src_func, start, end, f, fw):
+    src_func(t) is the (complex) dipole, or the current if not is_integrated."""
+
+    def __init__(self, src_func, start_time=-1.0e20, end_time=1.0e20, is_integrated=False,
+                 center_frequency=0, fwidth=0):
+        self.src_func = src_func
+        self.start_time, self.end_time = start_time, end_time
+        self.is_integrated = is_integrated
+        self.center_frequency, self.fwidth = center_frequency, fwidth
+        self.frequency = center_frequency
+
+
 class Source:
     def __init__(self, src, component, center=None, volume=None, size=Vector3(), amplitude=1.0,
                  amp_func=None):
@@ -190,6 +203,11 @@ class Source:
             raise NotImplementedError("only point sources (size 0, no amp_func) are in scope")
 
     def add_source(self, fields):  # python/source.py:132-158
+        if isinstance(self.src, CustomSource):
+            fields.add_custom_source(self.component, self.src.src_func, self.src.start_time,
+                                     self.src.end_time, tuple(self.center), self.amplitude,
+                                     self.src.is_integrated)
+            return
         kind, p = self.src.params()
         fields.add_point_source(self.component, kind, p, tuple(self.center), self.amplitude,
                                 self.src.is_integrated)

@@ -150,6 +150,9 @@ struct SrcTime {
   // cache (src/meep.hpp:970-979)
   double current_time = NAN;
   cplx current_dipole, current_current;
+  // kind 2: custom_src_time (src/meep.hpp:1059-1092)
+  void (*func)(double, void *, double *, double *) = nullptr;
+  void *fdata = nullptr;
 
   static SrcTime gaussian(double f, double w, double st, double et) {  // sources.cpp:85-96
     SrcTime s;
@@ -173,6 +176,13 @@ struct SrcTime {
     return s;
   }
   cplx dipole(double time) const {
+    if (kind == 2) {  // custom_src_time::dipole, meep.hpp:1072-1078
+      float rtime = float(time);
+      if (!(rtime >= start_time && rtime <= end_time)) return 0.0;
+      double re = 0, im = 0;
+      func(time, fdata, &re, &im);
+      return cplx(re, im);
+    }
     if (kind == 0) {  // sources.cpp:98-110
       double tt = time - peak_time;
       if (float(fabs(tt)) > cutoff) return 0.0;
@@ -189,7 +199,10 @@ struct SrcTime {
     return exp(cplx(0, -1.0) * (2 * pi) * cfreq * time) * amp * (1.0 + tanh(ts)) *
            (1.0 + tanh(te)) * 0.25;
   }
-  cplx current(double time, double dt) const { return (dipole(time + dt) - dipole(time)) / dt; }
+  cplx current(double time, double dt) const {  // custom: meep.hpp:1066-1071
+    if (kind == 2 && !is_integrated) return dipole(time);
+    return (dipole(time + dt) - dipole(time)) / dt;
+  }
   void update(double time, double dt) {  // meep.hpp:972-978
     if (time != current_time) {
       current_dipole = dipole(time);
@@ -398,6 +411,8 @@ struct orc_sim {
   std::vector<std::vector<realnum>> g_lsig[3];  // per E-comp dir: per susceptibility
   std::vector<std::vector<realnum>> g_lsig_off[3][3];  // [c][d], d != c: per susceptibility
   std::vector<SrcTime> srcs;
+  void (*pending_func)(double, void *, double *, double *) = nullptr;  // custom source being added
+  void *pending_fdata = nullptr;
   // connections: per chunk, per field type, list of (dst index, src chunk, src index, comp)
   struct Conn {
     int c;
@@ -1665,6 +1680,20 @@ int orc_require_component(orc_sim *s, int comp) {
   return 0;
 }
 
+int orc_add_custom_point_source(orc_sim *s, int comp,
+                                void (*func)(double, void *, double *, double *), void *data,
+                                double start_time, double end_time, const double pos[3],
+                                double amp_re, double amp_im, int is_integrated) {
+  if (!func) return set_err("custom source needs a function");
+  const double p[2] = {start_time, end_time};
+  s->pending_func = func;
+  s->pending_fdata = data;
+  int rc = orc_add_point_source(s, comp, 2, p, 2, pos, amp_re, amp_im, is_integrated);
+  s->pending_func = nullptr;
+  s->pending_fdata = nullptr;
+  return rc;
+}
+
 int orc_add_point_source(orc_sim *s, int comp, int kind, const double *p, int np,
                          const double pos[3], double amp_re, double amp_im, int is_integrated) {
   if (check_comp(s, comp)) return -1;
@@ -1677,6 +1706,12 @@ int orc_add_point_source(orc_sim *s, int comp, int kind, const double *p, int np
   } else if (kind == 1) {
     if (np < 6) return set_err("continuous source needs 6 parameters");
     st = SrcTime::continuous(cplx(p[0], p[1]), p[2], p[3], p[4], p[5]);
+  } else if (kind == 2 && s->pending_func) {
+    st.kind = 2;
+    st.func = s->pending_func;
+    st.fdata = s->pending_fdata;
+    st.start_time = float(p[0]);
+    st.end_time = float(p[1]);
   } else
     return set_err("unknown source kind");
   st.is_integrated = is_integrated != 0;
@@ -1686,7 +1721,8 @@ int orc_add_point_source(orc_sim *s, int comp, int kind, const double *p, int np
     if (o.kind == st.kind && o.is_integrated == st.is_integrated && o.freq == st.freq &&
         o.width == st.width && o.peak_time == st.peak_time && o.cutoff == st.cutoff &&
         o.cfreq == st.cfreq && o.cwidth == st.cwidth && o.start_time == st.start_time &&
-        o.end_time == st.end_time && o.slowness == st.slowness)
+        o.end_time == st.end_time && o.slowness == st.slowness && o.func == st.func &&
+        o.fdata == st.fdata)
       idx = int(i);
   }
   if (idx < 0) {

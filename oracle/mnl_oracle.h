@@ -35,6 +35,10 @@ int orc_add_lorentzian_tensor(orc_sim *s, double omega0, double gamma, int drude
                               const double *const sig[9]);
 int orc_add_point_source(orc_sim *s, int comp, int kind, const double *params, int nparams,
                          const double pos[3], double amp_re, double amp_im, int is_integrated);
+int orc_add_custom_point_source(orc_sim *s, int comp,
+                                void (*func)(double, void *, double *, double *), void *data,
+                                double start_time, double end_time, const double pos[3],
+                                double amp_re, double amp_im, int is_integrated);
 int orc_require_component(orc_sim *s, int comp);
 int orc_step(orc_sim *s, int nsteps);
 int orc_get_field(orc_sim *s, int comp, const double pos[3], double *out);

@@ -43,6 +43,9 @@ def lib():
         L.orc_set_chi2.argtypes = [c_void, c_int, dptr]
         L.orc_set_chi3.argtypes = [c_void, c_int, dptr]
         L.orc_set_conductivity.argtypes = [c_void, c_int, dptr]
+        L.orc_add_custom_point_source.argtypes = [c_void, c_int, SRC_FUNC, ctypes.c_void_p,
+                                                  ctypes.c_double, ctypes.c_double, dptr,
+                                                  ctypes.c_double, ctypes.c_double, c_int]
         L.orc_array_slice.argtypes = [c_void, c_int, dptr, dptr, ctypes.POINTER(c_int),
                                       ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]
         L.orc_add_lorentzian_tensor.argtypes = [c_void, ctypes.c_double, ctypes.c_double, c_int,
@@ -72,6 +75,10 @@ def lib():
         L.orc_dft_decimation.argtypes = [c_void, c_int]
         _LIB = L
     return _LIB
+
+
+SRC_FUNC = ctypes.CFUNCTYPE(None, ctypes.c_double, ctypes.c_void_p,
+                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double))
 
 
 def _chk(rc):
@@ -188,6 +195,20 @@ class Oracle:
         _chk(lib().orc_array_slice(self.h, comp, _dp(lo), _dp(hi), ctypes.byref(rank), dims,
                                    _dp(out), out.size))
         return out.reshape(shape) if shape else out[0]
+
+    def add_custom_source(self, comp, func, start, end, pos, amp=1.0, is_integrated=False):
+        cbs = self.__dict__.setdefault("_custom_cbs", {})
+        if id(func) not in cbs:
+            def _cb(t, _data, re, im, func=func):
+                v = complex(func(t))
+                re[0] = v.real
+                im[0] = v.imag
+            cbs[id(func)] = (func, SRC_FUNC(_cb))
+        p = np.ascontiguousarray(list(pos) + [0.0] * (3 - len(pos)), dtype=np.float64)
+        a = complex(amp)
+        _chk(lib().orc_add_custom_point_source(self.h, comp, cbs[id(func)][1], None, float(start),
+                                               float(end), _dp(p), a.real, a.imag,
+                                               int(is_integrated)))
 
     def add_lorentzian(self, omega0, gamma, sigmas, drude=False):
         s = [None if v is None else np.ascontiguousarray(v, dtype=np.float64).ravel()

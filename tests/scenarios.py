@@ -72,6 +72,9 @@ class ProductSim:
     def add_continuous_source(self, *a, **k):
         self._fields().add_continuous_source(*a, **k)
 
+    def add_custom_source(self, *a, **k):
+        self._fields().add_custom_source(*a, **k)
+
     def legacy_point_source(self, *a, **k):
         self._fields().legacy_point_source(*a, **k)
 
@@ -178,6 +181,10 @@ class GroupSim(ProductSim):
     def legacy_point_source(self, *a, **k):
         for f in self._all():
             f.legacy_point_source(*a, **k)
+
+    def add_custom_source(self, *a, **k):  # every rank adds every source (SPMD)
+        for f in self._all():
+            f.add_custom_source(*a, **k)
 
     def require_component(self, c):
         for f in self._all():
@@ -784,5 +791,28 @@ def sc_aniso_lorentz_3d(make, steps=40, full=True):
     o.add_lorentzian_tensor(0.8, 0.1, sig2)
     o.add_gaussian_source(0, 0.3, 4.0, 0.0, 40.0, (0.05, 0.05, -0.2), 10.0)
     o.add_gaussian_source(1, 0.35, 4.0, 0.0, 40.0, (0.4, -0.1, 0.9), 5.0)
+    o.step(steps)
+    return o
+
+
+# --------------------------------------------------------- custom sources
+def _chirp(t):
+    return complex(math.exp(-((t - 4.0) / 1.5) ** 2) * math.cos(2 * math.pi * 0.3 * t * (1 + 0.05 * t)),
+                   0.1 * math.sin(0.7 * t))
+
+
+def sc_custom_source_3d(make, steps=50):
+    """custom_src_time (src/meep.hpp:1059-1092): a chirped current source, the same
+    function again at another point (merged src_time), an integrated custom
+    source, with PML and a dielectric core."""
+    o = vol(make, 3, [3.0, 2.6, 2.2], 10, center_origin=True)
+    o.add_pml(0.6)
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        o.set_chi1inv(c, c, np.where(np.abs(y) < 0.4, 0.25, 1.0))
+    o.add_custom_source(2, _chirp, 0.0, 9.0, (0.05, 0.02, 0.01), 1.0)
+    o.add_custom_source(2, _chirp, 0.0, 9.0, (-0.43, 0.31, 0.2), complex(0.3, 0.4))
+    o.add_custom_source(0, lambda t: math.sin(0.9 * t) * math.exp(-0.1 * t), 0.5, 7.3,
+                        (0.2, -0.3, -0.1), 0.8, is_integrated=True)
     o.step(steps)
     return o

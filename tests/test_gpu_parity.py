@@ -103,7 +103,7 @@ def test_simulation_api_matches_core():
     p = ProductSim(2, [20, 20, 0], 10, 0.5, [-20, -20, 0])
     p.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0, 0), 1.0)
     p.step(sim.timestep)
-    np.testing.assert_array_equal(sim.get_array(mp.Ez), p.get_array(2))
+    np.testing.assert_array_equal(sim.get_component_array(mp.Ez), p.get_array(2))
     assert sim.meep_time() == pytest.approx(sim.timestep * 0.05)
 
 
