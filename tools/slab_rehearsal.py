@@ -6,7 +6,9 @@ with device copies instead of xGMI).  All slabs share one GPU, so the ideal is
 the same cells*steps/s as the single slab; the gap is the overhead of the
 multi-rank step (split kernels, chunk 0 on the side stream, top-plane shell
 kernels, exchanges) that each GPU pays at N > 1.
-  python tools/slab_rehearsal.py [P ...]"""
+  python tools/slab_rehearsal.py [--weak] [P ...]
+--weak: every slab keeps a full 512^3 (global 512x512x512P, as bench.py --gpus P);
+the ideal is then P times the single-slab step time."""
 import os
 import sys
 import threading
@@ -17,8 +19,11 @@ sys.path.insert(0, ROOT)
 from meep_nl_amd import core  # noqa: E402
 
 
+WEAK = "--weak" in sys.argv
+
+
 def build(nr, hub=None, rank=0):
-    n = [512, 512, 512]
+    n = [512, 512, 512 * (nr if WEAK else 1)]
     io = [-v for v in n]
     gv = core.GridVolume(3, n, 10.0, io)
     s = core.Structure(gv, 0.5)
@@ -49,12 +54,12 @@ def run(P, steps=40, warm=6):
     par(steps)
     el = time.perf_counter() - t0
     fused = all(f.fused_active() for f in fs)
-    cells = 512.0 ** 3
+    cells = 512.0 ** 3 * (P if WEAK else 1)
     print(f"slabs {P}: {el / steps * 1e3:.3f} ms/step, {cells * steps / el / 1e6:.0f} Mcells*steps/s,"
           f" fused={fused}", flush=True)
     del fs
 
 
 if __name__ == "__main__":
-    for P in [int(a) for a in sys.argv[1:]] or [1, 2, 4]:
+    for P in [int(a) for a in sys.argv[1:] if a != "--weak"] or [1, 2, 4]:
         run(P)
