@@ -176,7 +176,8 @@ int mnl_fields_copy_component(mnl_fields *f, int comp, double *host, size_t n);
  * points of the volume [vmin, vmax] (average of its Yee neighbours), empty
  * dimensions interpolated and collapsed (snap = false).  *rank / dims[3]: the
  * kept directions in X,Y,Z order; out (nout doubles, row-major) may be NULL to
- * query the size.  Single-rank fields only. */
+ * query the size.  Collective for distributed fields (every rank gets the
+ * whole slice). */
 int mnl_fields_array_slice(mnl_fields *f, int comp, const double vmin[3], const double vmax[3],
                            int *rank, long long dims[3], double *out, long long nout);
 /* Number of entries of the whole-cell array of comp. */

@@ -142,7 +142,7 @@ int Comm::recv(double *buf, size_t n, int peer, void *stream) {
 }
 
 int Comm::allreduce_sum(double *host, int n, void *stream) {
-  if (n > 64) return -1;
+  if (n < 0) return -1;
   if (hub_) {
     LocalHub &H = *hub_;
     H.red[rank].assign(host, host + n);
@@ -156,6 +156,13 @@ int Comm::allreduce_sum(double *host, int n, void *stream) {
     return 0;
   }
   hipStream_t s = (hipStream_t)stream;
+  if ((size_t)n > dcap_) {  // grow the device staging buffer (64 doubles at init)
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    if (dscratch_) (void)hipFree(dscratch_);
+    dscratch_ = nullptr;
+    if (hipMalloc(&dscratch_, (size_t)n * sizeof(double)) != hipSuccess) return -1;
+    dcap_ = (size_t)n;
+  }
   if (hipMemcpyAsync(dscratch_, host, n * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
     return -1;
   if (ncclAllReduce(dscratch_, dscratch_, n, ncclDouble, ncclSum, (ncclComm_t)comm_, s) !=

@@ -22,7 +22,7 @@ class Comm {
   int group_end(void *stream);
   int send(const double *buf, size_t n, int peer, void *stream);
   int recv(double *buf, size_t n, int peer, void *stream);
-  // in-place sum over ranks of n host doubles (small; used by get_field)
+  // in-place sum over ranks of n host doubles (get_field, fluxes, array slices)
   int allreduce_sum(double *host, int n, void *stream);
   ~Comm();
   int rank = 0, nranks = 1;
@@ -30,6 +30,7 @@ class Comm {
  private:
   void *comm_ = nullptr;
   double *dscratch_ = nullptr;
+  size_t dcap_ = 64;
   LocalHub *hub_ = nullptr;
   struct Op {
     double *dst;

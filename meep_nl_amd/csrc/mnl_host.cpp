@@ -2869,7 +2869,6 @@ inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) 
 int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3], int *rank,
                 long long dims[3], double *out, long long nout) {
   const mnl_structure &S = F->S;
-  if (F->nranks > 1) return fail("array slices of distributed fields are not supported");
   int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
   for (int d = 0; d < 3; d++) {
     if (!S.has[d]) continue;
@@ -2955,6 +2954,11 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   if (loops.empty()) return 0;
   std::vector<double> f(S.ntot);
   if (mnl_fields_copy_component(F, c, f.data(), f.size())) return -1;
+  // distributed: every rank holds only its own entries (others 0); the four
+  // Yee values of each point are summed over ranks separately -- each has one
+  // owner, so the sums are exact -- and every rank then forms the same average
+  const bool dist = F->nranks > 1;
+  std::vector<double> v4;
   long long o1 = 0, o2 = 0;
   for (int d = 0; d < 3; d++)
     if (S.has[d] && !S.shift(c, d)) {
@@ -2969,16 +2973,34 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   bool empty_dim[3];
   for (int d = 0; d < 3; d++) empty_dim[d] = S.has[d] && vmax[d] - vmin[d] == 0.0;
   const int yd[3] = {S.dim == 2 ? 2 : 0, S.dim == 2 ? 0 : 1, S.dim == 2 ? 1 : 2};
+  for (int pass = dist ? 0 : 1; pass < 2; pass++) {
+  if (pass == 1 && dist) {  // exact gather of the four values per point
+    for (size_t q = 0; q < v4.size(); q += 1 << 20) {
+      const int n = (int)std::min<size_t>(1 << 20, v4.size() - q);
+      if (F->comm->allreduce_sum(v4.data() + q, n, F->stream)) return fail("slice allreduce failed");
+    }
+  }
+  size_t pi = 0;  // point ordinal over all chunk loops
   for (auto &L : loops) {
     int n[3];
     for (int k = 0; k < 3; k++) n[k] = S.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
     for (int i1 = 0; i1 < n[0]; i1++)
       for (int i2 = 0; i2 < n[1]; i2++)
-        for (int i3 = 0; i3 < n[2]; i3++) {
+        for (int i3 = 0; i3 < n[2]; i3++, pi++) {
           const int ii[3] = {i1, i2, i3};
           int p[3] = {0, 0, 0};
           for (int k = 0; k < 3; k++)
             if (S.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
+          if (pass == 0) {  // distributed, first pass: the four owned values
+            long long idx = 0;
+            for (int d = 0; d < 3; d++)
+              if (S.has[d]) idx += (long long)((p[d] - S.io[d]) / 2) * S.cstride(d);
+            v4.push_back(f[idx]);
+            v4.push_back(f[idx + o1]);
+            v4.push_back(f[idx + o2]);
+            v4.push_back(f[idx + o1 + o2]);
+            continue;
+          }
           double w[3];
           for (int k = 0; k < 3; k++) {
             const int d = yd[k];
@@ -2989,12 +3011,15 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
           long long idx = 0;
           for (int d = 0; d < 3; d++)
             if (S.has[d]) idx += (long long)((p[d] - S.io[d]) / 2) * S.cstride(d);
-          const double avg = 0.25 * (f[idx] + f[idx + o1] + f[idx + o2] + f[idx + o1 + o2]);
+          const double avg =
+              dist ? 0.25 * (v4[4 * pi] + v4[4 * pi + 1] + v4[4 * pi + 2] + v4[4 * pi + 3])
+                   : 0.25 * (f[idx] + f[idx + o1] + f[idx + o2] + f[idx + o1 + o2]);
           const cplx v = wt * cplx(avg, 0.0) * cplx(1.0, 0.0);
           long long oi = 0;
           for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
           arr[oi] = real(v);
         }
+  }
   }
   for (long long q = 0; q < ntot; q++) {  // collapse_array: in full-index order
     long long t = q, ri = 0;

@@ -125,6 +125,9 @@ class ProductSim:
     def dump(self, path):
         self._fields().dump(path)
 
+    def get_array_slice(self, c, lo, hi):
+        return self._fields().get_array_slice(c, lo, hi)
+
     def load(self, path):
         self._fields().load(path)
 
@@ -181,6 +184,12 @@ class GroupSim(ProductSim):
     def legacy_point_source(self, *a, **k):
         for f in self._all():
             f.legacy_point_source(*a, **k)
+
+    def get_array_slice(self, c, lo, hi):  # collective: every rank gets the slice
+        out = self._par(lambda f: f.get_array_slice(c, lo, hi))
+        for o in out[1:]:
+            assert np.array_equal(o, out[0])
+        return out[0]
 
     def add_custom_source(self, *a, **k):  # every rank adds every source (SPMD)
         for f in self._all():

@@ -6,7 +6,8 @@ Simulation.get_array on top of it."""
 import numpy as np
 import pytest
 
-from scenarios import ProductSim, make_oracle, sc_cfg1, sc_te_magnetic_2d, sc_vacuum_pml_3d
+from scenarios import (GroupSim, GroupSim3, ProductSim, make_oracle, sc_cfg1, sc_te_magnetic_2d,
+                       sc_vacuum_pml_3d)
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
@@ -21,7 +22,7 @@ VOL3 = [([-1.6, -1.6, 0.12], [1.6, 1.6, 0.12]), ([-1.2, -0.65, -1.0], [0.9, 0.45
 def _same(p, o, comps, vols):
     for c in comps:
         for lo, hi in vols:
-            a, b = p._fields().get_array_slice(c, lo, hi), o.get_array_slice(c, lo, hi)
+            a, b = p.get_array_slice(c, lo, hi), o.get_array_slice(c, lo, hi)
             assert np.shape(a) == np.shape(b), (c, lo, hi)
             assert np.array_equal(a, b), (c, lo, hi, float(np.max(np.abs(np.asarray(a) - b))))
 
@@ -32,9 +33,16 @@ def test_slices_2d():
     _same(sc_te_magnetic_2d(ProductSim), sc_te_magnetic_2d(make_oracle), (0, 1, 5), te)
 
 
-def test_slices_3d():
-    _same(sc_vacuum_pml_3d(ProductSim, steps=40), sc_vacuum_pml_3d(make_oracle, steps=40),
+@pytest.mark.parametrize("G", [ProductSim, GroupSim, GroupSim3])
+def test_slices_3d(G):
+    """GroupSim / GroupSim3: distributed fields (2 / 3 z-slabs), the four Yee values
+    of each point gathered exactly over the slabs."""
+    _same(sc_vacuum_pml_3d(G, steps=40), sc_vacuum_pml_3d(make_oracle, steps=40),
           (0, 2, 3, 5, 7), VOL3)
+
+
+def test_slices_2d_slabs():
+    _same(sc_cfg1(GroupSim3, steps=120), sc_cfg1(make_oracle, steps=120), (2, 3, 4, 8), VOL2)
 
 
 def test_simulation_get_array():
