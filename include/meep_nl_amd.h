@@ -174,12 +174,13 @@ int mnl_fields_copy_component(mnl_fields *f, int comp, double *host, size_t n);
 /* fields::get_array_slice(volume, c) (src/array_slice.cpp:611-704, with
  * get_array_slice_dimensions 447-507): the component on the Centered grid
  * points of the volume [vmin, vmax] (average of its Yee neighbours), empty
- * dimensions interpolated and collapsed (snap = false).  *rank / dims[3]: the
+ * dimensions interpolated and collapsed (snap = 0) or snapped to the
+ * nearest grid point (snap = 1, src/loop_in_chunks.cpp:275-287).  *rank / dims[3]: the
  * kept directions in X,Y,Z order; out (nout doubles, row-major) may be NULL to
  * query the size.  Collective for distributed fields (every rank gets the
  * whole slice). */
 int mnl_fields_array_slice(mnl_fields *f, int comp, const double vmin[3], const double vmax[3],
-                           int *rank, long long dims[3], double *out, long long nout);
+                           int snap, int *rank, long long dims[3], double *out, long long nout);
 /* Number of entries of the whole-cell array of comp. */
 size_t mnl_fields_ntot(mnl_fields *f);
 /* Per-sub-step GPU time in ms accumulated since creation (time_sink

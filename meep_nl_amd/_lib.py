@@ -35,7 +35,7 @@ _SIGS = {
                                                    ctypes.c_double, ctypes.c_double, dptr,
                                                    ctypes.c_double, ctypes.c_double, c_int]),
     "mnl_fields_dump": (c_int, [c_void, ctypes.c_char_p]),
-    "mnl_fields_array_slice": (c_int, [c_void, c_int, dptr, dptr, ctypes.POINTER(c_int),
+    "mnl_fields_array_slice": (c_int, [c_void, c_int, dptr, dptr, c_int, ctypes.POINTER(c_int),
                                        ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]),
     "mnl_fields_load": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_dump": (c_int, [c_void, ctypes.c_char_p]),

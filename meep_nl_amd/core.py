@@ -304,7 +304,7 @@ class Fields:
         check(lib().mnl_fields_copy_component(self.h, comp, ptr(out), nt))
         return out.reshape(self.gv.shape())
 
-    def get_array_slice(self, comp, vmin, vmax):
+    def get_array_slice(self, comp, vmin, vmax, snap=False):
         """fields::get_array_slice(volume, c) (src/array_slice.cpp:611-704) over
         [vmin, vmax] (3 coordinates): Centered-grid values, empty dimensions
         interpolated and collapsed; shape = kept directions in X, Y, Z order."""
@@ -312,12 +312,12 @@ class Fields:
         hi = np.ascontiguousarray(vmax, dtype=np.float64)
         rank = ctypes.c_int(0)
         dims = (ctypes.c_longlong * 3)()
-        check(lib().mnl_fields_array_slice(self.h, comp, ptr(lo), ptr(hi), ctypes.byref(rank), dims,
-                                           None, 0))
+        check(lib().mnl_fields_array_slice(self.h, comp, ptr(lo), ptr(hi), int(snap),
+                                           ctypes.byref(rank), dims, None, 0))
         shape = tuple(dims[k] for k in range(rank.value))
         out = np.zeros(int(np.prod(shape)) if shape else 1)
-        check(lib().mnl_fields_array_slice(self.h, comp, ptr(lo), ptr(hi), ctypes.byref(rank), dims,
-                                           ptr(out), out.size))
+        check(lib().mnl_fields_array_slice(self.h, comp, ptr(lo), ptr(hi), int(snap),
+                                           ctypes.byref(rank), dims, ptr(out), out.size))
         return out.reshape(shape) if shape else out[0]
 
     def center(self):

@@ -2866,8 +2866,8 @@ inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) 
   return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
 }
 
-int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3], int *rank,
-                long long dims[3], double *out, long long nout) {
+int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3], int snap,
+                int *rank, long long dims[3], double *out, long long nout) {
   const mnl_structure &S = F->S;
   int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
   for (int d = 0; d < 3; d++) {
@@ -2877,6 +2877,16 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   }
   double s0[3], s1[3], e0[3], e1[3];
   dft_boundary_weights(S, vmin, vmax, is, ie, s0, e0, s1, e1);
+  if (snap)  // snap_empty_dimensions (src/loop_in_chunks.cpp:275-287): nearest point, weight 1
+    for (int d = 0; d < 3; d++) {
+      if (!S.has[d] || vmin[d] != vmax[d] || ie[d] >= is[d] + 4) continue;
+      const double w0 = 1. - vmin[d] * S.a + 0.5 * is[d], w1 = 1. + vmax[d] * S.a - 0.5 * ie[d];
+      if (w0 > w1)
+        ie[d] = is[d];
+      else
+        is[d] = ie[d];
+      s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
+    }
   struct Lp {
     int is[3], ie[3];
     double s0[3], s1[3], e0[3], e1[3];
@@ -3353,9 +3363,9 @@ int mnl_fields_step(mnl_fields *F, int nsteps) {
 }
 
 int mnl_fields_array_slice(mnl_fields *F, int comp, const double vmin[3], const double vmax[3],
-                           int *rank, long long dims[3], double *out, long long nout) {
+                           int snap, int *rank, long long dims[3], double *out, long long nout) {
   if (!F || check_comp(comp) || !vmin || !vmax || !rank || !dims) return fail("bad argument");
-  return array_slice(F, comp, vmin, vmax, rank, dims, out, nout);
+  return array_slice(F, comp, vmin, vmax, snap, rank, dims, out, nout);
 }
 
 int mnl_fields_dump(mnl_fields *F, const char *filename) {

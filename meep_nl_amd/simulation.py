@@ -755,10 +755,10 @@ class Simulation:
         """Simulation.get_array (python/simulation.py:3872-3990) ->
         fields::get_array_slice over the volume (default: the whole cell) on the
         Centered grid, empty dimensions interpolated and collapsed.  Real fields
-        only; snap=True is not supported."""
+        only; snap=True snaps empty dimensions to the nearest grid point."""
         self.init_sim()
-        if snap or cmplx or frequency:
-            raise NotImplementedError("get_array: snap / complex / frequency-dependent slices")
+        if cmplx or frequency:
+            raise NotImplementedError("get_array: complex / frequency-dependent slices")
         if vol is not None:
             center, size = vol.center, vol.size
         center = Vector3(*(center if center is not None else Vector3()))
@@ -768,7 +768,7 @@ class Simulation:
         for d in dirs:
             lo[d] = center[d] - 0.5 * size[d]
             hi[d] = center[d] + 0.5 * size[d]
-        out = self.fields.get_array_slice(component, lo, hi)
+        out = self.fields.get_array_slice(component, lo, hi, snap)
         if arr is not None:
             arr[...] = out
             return arr

@@ -2109,7 +2109,8 @@ struct SliceLoop {
   double s0[3], s1[3], e0[3], e1[3];
 };
 
-std::vector<SliceLoop> slice_loops(orc_sim *s, const double wmin[3], const double wmax[3]) {
+std::vector<SliceLoop> slice_loops(orc_sim *s, const double wmin[3], const double wmax[3],
+                                   bool snap) {
   const GV &G = s->gv;
   int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
   for (int d = 0; d < 3; d++) {
@@ -2119,6 +2120,17 @@ std::vector<SliceLoop> slice_loops(orc_sim *s, const double wmin[3], const doubl
   }
   double s0[3], s1[3], e0[3], e1[3];
   boundary_weights(G, wmin, wmax, is, ie, s0, e0, s1, e1);
+  if (snap)  // compute_boundary_weights, snap_empty_dimensions (loop_in_chunks.cpp:275-287)
+    for (int d = 0; d < 3; d++) {
+      if (!G.has[d] || wmin[d] != wmax[d] || ie[d] >= is[d] + 2 * 2) continue;
+      double w0 = 1. - wmin[d] * G.a + 0.5 * is[d];
+      double w1 = 1. + wmax[d] * G.a - 0.5 * ie[d];
+      if (w0 > w1)
+        ie[d] = is[d];
+      else
+        is[d] = ie[d];
+      s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
+    }
   std::vector<SliceLoop> out;
   for (size_t ci = 0; ci < s->chunks.size(); ci++) {
     const GV &g = s->chunks[ci].gv;
@@ -2177,11 +2189,11 @@ inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) 
 }  // namespace
 
 extern "C" {
-int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3], int *rank,
-                    long long dims[3], double *out, long long nout) {
+int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3], int snap,
+                    int *rank, long long dims[3], double *out, long long nout) {
   finalize(s);
   const GV &G = s->gv;
-  auto loops = slice_loops(s, vmin, vmax);
+  auto loops = slice_loops(s, vmin, vmax, snap != 0);
   int mn[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, mx[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
   for (auto &L : loops)
     for (int d = 0; d < 3; d++) mn[d] = std::min(mn[d], L.is[d]), mx[d] = std::max(mx[d], L.ie[d]);

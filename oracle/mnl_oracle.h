@@ -50,8 +50,8 @@ int orc_set_upstream_nl(orc_sim *s, int on);
 /* fields::get_array_slice(volume, c) (src/array_slice.cpp): *rank and the
  * collapsed dims[3]; out (nout doubles, row-major over the kept directions
  * in X,Y,Z order) may be NULL to query the size only. */
-int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3], int *rank,
-                    long long dims[3], double *out, long long nout);
+int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3], int snap,
+                    int *rank, long long dims[3], double *out, long long nout);
 long long orc_t(orc_sim *s);
 double orc_dt(orc_sim *s);
 size_t orc_ntot(orc_sim *s);

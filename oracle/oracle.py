@@ -46,7 +46,7 @@ def lib():
         L.orc_add_custom_point_source.argtypes = [c_void, c_int, SRC_FUNC, ctypes.c_void_p,
                                                   ctypes.c_double, ctypes.c_double, dptr,
                                                   ctypes.c_double, ctypes.c_double, c_int]
-        L.orc_array_slice.argtypes = [c_void, c_int, dptr, dptr, ctypes.POINTER(c_int),
+        L.orc_array_slice.argtypes = [c_void, c_int, dptr, dptr, c_int, ctypes.POINTER(c_int),
                                       ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]
         L.orc_add_lorentzian_tensor.argtypes = [c_void, ctypes.c_double, ctypes.c_double, c_int,
                                                 ctypes.POINTER(dptr)]
@@ -182,18 +182,19 @@ class Oracle:
         ptrs = (ctypes.POINTER(ctypes.c_double) * 9)(*[_dp(a) if a is not None else None for a in arrs])
         _chk(lib().orc_add_lorentzian_tensor(self.h, omega0, gamma, int(drude), ptrs))
 
-    def get_array_slice(self, comp, vmin, vmax):
+    def get_array_slice(self, comp, vmin, vmax, snap=False):
         """fields::get_array_slice over the volume [vmin, vmax] (3 coordinates, unused
         ones ignored); shape = the kept (non-empty) directions in X, Y, Z order."""
         lo = np.ascontiguousarray(vmin, dtype=np.float64)
         hi = np.ascontiguousarray(vmax, dtype=np.float64)
         rank = ctypes.c_int(0)
         dims = (ctypes.c_longlong * 3)()
-        _chk(lib().orc_array_slice(self.h, comp, _dp(lo), _dp(hi), ctypes.byref(rank), dims, None, 0))
+        _chk(lib().orc_array_slice(self.h, comp, _dp(lo), _dp(hi), int(snap), ctypes.byref(rank), dims,
+                                   None, 0))
         shape = tuple(dims[k] for k in range(rank.value))
         out = np.zeros(int(np.prod(shape)) if shape else 1)
-        _chk(lib().orc_array_slice(self.h, comp, _dp(lo), _dp(hi), ctypes.byref(rank), dims,
-                                   _dp(out), out.size))
+        _chk(lib().orc_array_slice(self.h, comp, _dp(lo), _dp(hi), int(snap), ctypes.byref(rank),
+                                   dims, _dp(out), out.size))
         return out.reshape(shape) if shape else out[0]
 
     def add_custom_source(self, comp, func, start, end, pos, amp=1.0, is_integrated=False):

@@ -125,8 +125,8 @@ class ProductSim:
     def dump(self, path):
         self._fields().dump(path)
 
-    def get_array_slice(self, c, lo, hi):
-        return self._fields().get_array_slice(c, lo, hi)
+    def get_array_slice(self, c, lo, hi, snap=False):
+        return self._fields().get_array_slice(c, lo, hi, snap)
 
     def load(self, path):
         self._fields().load(path)
@@ -185,8 +185,8 @@ class GroupSim(ProductSim):
         for f in self._all():
             f.legacy_point_source(*a, **k)
 
-    def get_array_slice(self, c, lo, hi):  # collective: every rank gets the slice
-        out = self._par(lambda f: f.get_array_slice(c, lo, hi))
+    def get_array_slice(self, c, lo, hi, snap=False):  # collective: every rank gets the slice
+        out = self._par(lambda f: f.get_array_slice(c, lo, hi, snap))
         for o in out[1:]:
             assert np.array_equal(o, out[0])
         return out[0]

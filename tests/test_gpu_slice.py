@@ -22,9 +22,11 @@ VOL3 = [([-1.6, -1.6, 0.12], [1.6, 1.6, 0.12]), ([-1.2, -0.65, -1.0], [0.9, 0.45
 def _same(p, o, comps, vols):
     for c in comps:
         for lo, hi in vols:
-            a, b = p.get_array_slice(c, lo, hi), o.get_array_slice(c, lo, hi)
-            assert np.shape(a) == np.shape(b), (c, lo, hi)
-            assert np.array_equal(a, b), (c, lo, hi, float(np.max(np.abs(np.asarray(a) - b))))
+            for snap in (False, True):
+                a, b = p.get_array_slice(c, lo, hi, snap), o.get_array_slice(c, lo, hi, snap)
+                assert np.shape(a) == np.shape(b), (c, lo, hi, snap)
+                assert np.array_equal(a, b), (c, lo, hi, snap,
+                                              float(np.max(np.abs(np.asarray(a) - b))))
 
 
 def test_slices_2d():

@@ -38,3 +38,13 @@ def test_3d_slices_shapes_and_chunks():
     assert box.ndim == 3 and np.isfinite(box).all() and np.abs(box).max() > 0
     pt = o.get_array_slice(2, [0.05, 0.05, 0.05], [0.05, 0.05, 0.05])
     assert np.ndim(pt) == 0
+
+
+def test_snap_picks_nearest_plane():
+    """snap_empty_dimensions (loop_in_chunks.cpp:275-287): y = 0.33 snaps to the
+    centered plane y = 0.35 (the nearer one), unweighted."""
+    o = sc_cfg1(make_oracle, steps=120)
+    b = o.get_array_slice(2, [-10, 0.35, 0], [10, 0.35, 0])
+    s = o.get_array_slice(2, [-10, 0.33, 0], [10, 0.33, 0], snap=True)
+    assert s.shape == (200,)
+    np.testing.assert_array_equal(s, b)
