@@ -48,10 +48,6 @@ def parse():
 
 
 def build_fields(args, rank, world, local_rank, nid):
-    # MNL_BENCH_DEVICE pins every rank to one device (rehearsing the RCCL path
-    # with several ranks on a one-GPU box); default: one GPU per local rank
-    if os.environ.get("MNL_BENCH_DEVICE"):
-        local_rank = int(os.environ["MNL_BENCH_DEVICE"])
     from meep_nl_amd import core
     res = 10.0
     n = [args.size, args.size, args.size * world]
@@ -109,26 +105,68 @@ def cpu_baseline(args):
                       f"+PML(1.0), {steps} steps in {el:.1f} s, OpenMP {threads} threads"}
 
 
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run
+    as CHILD processes (this process never touches the GPU) and exit with their
+    status."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def pick_transport(world, local_rank):
+    """RCCL over xGMI when every local rank has its own GPU; the IPC transport when
+    ranks must share one (a one-GPU rehearsal of the multi-process path).
+    Returns (transport, device)."""
+    from meep_nl_amd import core
+    ndev = core.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    forced = os.environ.get("MNL_BENCH_DEVICE")
+    device = int(forced) if forced else local_rank % max(ndev, 1)
+    tr = os.environ.get("MNL_COMM")
+    if not tr:
+        tr = "ipc" if (forced or ndev < local_world) else "rccl"
+    if tr not in ("ipc", "rccl"):
+        raise SystemExit(f"MNL_COMM must be ipc or rccl, not {tr!r}")
+    return tr, device
+
+
 def main():
     args = parse()
     if args.workload == "vacuum":
         args.vacuum = True
     if args.workload is None:
         args.workload = "vacuum" if args.vacuum else "waveguide"
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}\n")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     nid = None
+    transport, device = "single", local_rank
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from meep_nl_amd import core
-        obj = [core.unique_id() if rank == 0 else None]
+        transport, device = pick_transport(world, local_rank)
+        obj = [core.comm_id(world, transport) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nid = obj[0]
-    gv, s, f = build_fields(args, rank, world, local_rank, nid)
+    elif os.environ.get("MNL_BENCH_DEVICE"):
+        device = int(os.environ["MNL_BENCH_DEVICE"])
+    gv, s, f = build_fields(args, rank, world, device, nid)
     if args.flux:  # SURVEY.md 8(f) row 1: on-device DFT flux monitors
         hx = 0.5 * gv.n[0] / 10.0
         hy, hz = 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
@@ -228,6 +266,7 @@ def main():
                         (", Ez Gaussian current at (0.05,0.05,0.05)"
                          if args.workload != "kerr" else ""),
             "grid": list(gv.n), "per_gpu_cells": args.size ** 3, "parallelism": f"z-slab x{world}",
+            "transport": f.transport(),
             "flux_planes": args.flux, "flux_nfreq": args.nfreq if args.flux else 0,
             "model_bytes_per_cell_step": bpc},
         "roofline": roof,

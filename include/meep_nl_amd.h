@@ -122,6 +122,27 @@ mnl_fields *mnl_fields_create(mnl_structure *s, int device);
 mnl_fields *mnl_fields_create_dist(mnl_structure *s, int device, int rank, int nranks,
                                    const void *nccl_id);
 int mnl_comm_unique_id(void *out128);
+/* IPC transport id (one process per slab, several processes sharing one GPU --
+ * RCCL refuses duplicate devices): creates a POSIX shared-memory control block
+ * for `nranks` ranks and writes its 128-byte id; pass it to
+ * mnl_fields_create_dist in place of the RCCL id.  Replaces the reference's
+ * comms_manager (src/mympi.cpp:87-151) with a process-shared barrier plus
+ * IPC-exported device staging buffers. */
+int mnl_comm_ipc_id(void *out128, int nranks);
+/* Remove the shared-memory name of an IPC id that will not be used (the first
+ * init on rank 0 removes it otherwise; mapped segments stay valid). */
+int mnl_comm_ipc_unlink(const void *id128);
+/* Host-only collective over a fresh IPC group (no GPU call): every rank passes
+ * the same id; on return host[0..n) holds the rank-order sum over ranks and the
+ * return value is 0 on every rank, or -1 on every rank if any rank passed
+ * ok = 0 (the status agreement the data collectives use before they start). */
+int mnl_comm_ipc_reduce(const void *id128, int rank, int nranks, double *host, int n, int ok);
+/* Transport of a fields object: "single", "rccl", "ipc" or "local". */
+const char *mnl_fields_transport(mnl_fields *f);
+/* One-rank RCCL self test on `device`: grouped ncclSend/ncclRecv to self of n
+ * doubles plus an ncclAllReduce, through the same Comm wrappers the slab
+ * exchange uses.  Returns 0 when the data arrived intact. */
+int mnl_comm_rccl_selftest(int device, int n);
 /* Cells [lo, hi) of the slab axis owned by `rank` (host-only helper). */
 int mnl_slab_range(int ncell, int rank, int nranks, int *lo, int *hi);
 /* Several slabs of one grid in ONE process on one device (one host thread per

@@ -46,6 +46,11 @@ _SIGS = {
     "mnl_fields_create": (c_void, [c_void, c_int]),
     "mnl_fields_create_dist": (c_void, [c_void, c_int, c_int, c_int, ctypes.c_char_p]),
     "mnl_comm_unique_id": (c_int, [ctypes.c_char_p]),
+    "mnl_comm_ipc_id": (c_int, [ctypes.c_char_p, c_int]),
+    "mnl_fields_transport": (ctypes.c_char_p, [c_void]),
+    "mnl_comm_ipc_unlink": (c_int, [ctypes.c_char_p]),
+    "mnl_comm_ipc_reduce": (c_int, [ctypes.c_char_p, c_int, c_int, dptr, c_int, c_int]),
+    "mnl_comm_rccl_selftest": (c_int, [c_int, c_int]),
     "mnl_slab_range": (c_int, [c_int, c_int, c_int, iptr, iptr]),
     "mnl_local_hub_create": (c_void, [c_int]),
     "mnl_local_hub_destroy": (None, [c_void]),

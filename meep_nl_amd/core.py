@@ -335,6 +335,10 @@ class Fields:
         check(lib().mnl_fields_nr_fallbacks(self.h, ctypes.byref(v)))
         return v.value
 
+    def transport(self):
+        """'single', 'rccl', 'ipc' or 'local' (how ghost planes travel)."""
+        return lib().mnl_fields_transport(self.h).decode()
+
     def fused_active(self):
         v = ctypes.c_int()
         check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
@@ -448,9 +452,29 @@ def slab_range(ncell, rank, nranks):
 
 
 def unique_id():
+    """128-byte RCCL unique id (rank 0; broadcast it to the other ranks)."""
     buf = ctypes.create_string_buffer(128)
     check(lib().mnl_comm_unique_id(buf))
     return buf.raw
 
 
-__all__ = ["GridVolume", "Structure", "Fields", "device_count", "unique_id", "math"]
+def ipc_id(nranks):
+    """128-byte id of the IPC transport (ranks sharing one GPU): creates the
+    shared-memory control block; pass it as nccl_id to every rank's Fields."""
+    buf = ctypes.create_string_buffer(128)
+    check(lib().mnl_comm_ipc_id(buf, int(nranks)))
+    return buf.raw
+
+
+def comm_id(nranks, transport):
+    """Rank-0 side of communicator setup: 'rccl' or 'ipc'."""
+    return ipc_id(nranks) if transport == "ipc" else unique_id()
+
+
+def rccl_selftest(device=0, n=4096):
+    """One-rank RCCL send/recv-to-self + allreduce through the slab Comm wrappers."""
+    check(lib().mnl_comm_rccl_selftest(int(device), int(n)))
+
+
+__all__ = ["GridVolume", "Structure", "Fields", "device_count", "unique_id", "ipc_id", "comm_id",
+           "math"]

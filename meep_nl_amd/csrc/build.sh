@@ -17,5 +17,5 @@ g++ $CXXF -c "$HERE/mnl_comm.cpp" -o "$TMP/mnl_comm.o"
 # std::complex) comes from libgcc as in the reference (and the oracle), not
 # from clang's compiler-rt, whose complex division rounds differently.
 g++ -shared -fPIC -o "$OUT" "$TMP/mnl_kernels.o" "$TMP/mnl_host.o" "$TMP/mnl_comm.o" \
-  -L$ROCM/lib -lamdhip64 -lrccl -Wl,-rpath,$ROCM/lib
+  -L$ROCM/lib -lamdhip64 -lrccl -lrt -Wl,-rpath,$ROCM/lib
 echo "built $OUT"

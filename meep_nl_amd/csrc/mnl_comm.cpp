@@ -1,12 +1,23 @@
-// mnl_comm.cpp -- RCCL and in-process implementations of mnl::Comm.
+// mnl_comm.cpp -- RCCL, IPC (processes sharing a GPU) and in-process
+// implementations of mnl::Comm.
 #include "mnl_comm.hpp"
 
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <fcntl.h>
 #include <mutex>
+#include <sched.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
 
 namespace mnl {
 
@@ -48,6 +59,181 @@ struct LocalHub {
 LocalHub *local_hub_create(int nranks) { return new LocalHub(nranks); }
 void local_hub_destroy(LocalHub *h) { delete h; }
 
+// ------------------------------------------------------------------ IPC mode
+// One shared-memory segment per job (created by ipc_id on one rank, name passed
+// to the others in the 128-byte id).  Each rank owns a slot: the IPC handle of
+// its staging buffer (+ a generation bumped when it grows), the posts of its
+// current exchange group and a reduction buffer.
+static const char IPC_MAGIC[8] = {'M', 'N', 'L', 'I', 'P', 'C', '1', 0};
+constexpr int IPC_MAXR = 16, IPC_MAXPOST = 96, IPC_RED = 8192;
+
+struct IpcPost {
+  int dst;
+  int pad;
+  uint64_t off, n;  // doubles
+};
+struct IpcSlot {
+  hipIpcMemHandle_t h;
+  uint64_t gen;
+  int nposts;
+  int pad;
+  IpcPost posts[IPC_MAXPOST];
+  double red[IPC_RED];
+};
+struct IpcCtl {
+  std::atomic<int> arrived;
+  std::atomic<int> gen;
+  std::atomic<int> abort;
+  std::atomic<int> nranks;
+  IpcSlot slot[IPC_MAXR];
+};
+static_assert(std::atomic<int>::is_always_lock_free, "process-shared atomics need lock-free int");
+
+bool Comm::is_ipc_id(const void *id128) {
+  return id128 && memcmp(id128, IPC_MAGIC, sizeof(IPC_MAGIC)) == 0;
+}
+
+int Comm::ipc_id(void *out128, int nranks) {
+  if (nranks < 1 || nranks > IPC_MAXR) return -1;
+  static std::atomic<int> counter{0};
+  char name[96];
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  snprintf(name, sizeof(name), "/mnl_ipc_%d_%d_%lx", (int)getpid(), counter++,
+           (unsigned long)(ts.tv_nsec ^ (ts.tv_sec << 20)));
+  int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+  if (fd < 0) return -1;
+  if (ftruncate(fd, sizeof(IpcCtl)) != 0) {
+    close(fd);
+    shm_unlink(name);
+    return -1;
+  }
+  close(fd);  // zero-filled by ftruncate: counters 0, nranks 0 (set by the first rank)
+  memset(out128, 0, 128);
+  memcpy(out128, IPC_MAGIC, sizeof(IPC_MAGIC));
+  strncpy((char *)out128 + 8, name, 119);
+  return 0;
+}
+
+int Comm::ipc_unlink(const void *id128) {
+  if (!is_ipc_id(id128)) return -1;
+  char name[128];
+  memcpy(name, (const char *)id128 + 8, 120);
+  name[119] = 0;
+  return shm_unlink(name) == 0 ? 0 : -1;
+}
+
+int Comm::init_ipc(const void *id128) {
+  if (nranks > IPC_MAXR) return -1;
+  char name[128];
+  memcpy(name, (const char *)id128 + 8, 120);
+  name[119] = 0;
+  int fd = shm_open(name, O_RDWR, 0600);
+  if (fd < 0) return -1;
+  void *p = mmap(nullptr, sizeof(IpcCtl), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return -1;
+  ipc_ = (IpcCtl *)p;
+  int expect = 0;
+  if (!ipc_->nranks.compare_exchange_strong(expect, nranks) && expect != nranks) return -1;
+  if (const char *t = getenv("MNL_IPC_TIMEOUT")) ipc_timeout_s_ = std::max(1.0, atof(t));
+  peer_base_.assign(nranks, nullptr);
+  peer_gen_.assign(nranks, 0);
+  if (ipc_barrier()) return -1;
+  if (rank == 0) shm_unlink(name);  // every rank has it mapped: nothing leaks in /dev/shm
+  return 0;
+}
+
+void Comm::ipc_abort() {
+  if (ipc_) ipc_->abort.store(1, std::memory_order_release);
+}
+
+int Comm::ipc_barrier() {
+  IpcCtl &C = *ipc_;
+  if (C.abort.load(std::memory_order_acquire)) return -1;
+  const int g = C.gen.load(std::memory_order_acquire);
+  if (C.arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == nranks) {
+    C.arrived.store(0, std::memory_order_relaxed);
+    C.gen.fetch_add(1, std::memory_order_release);
+    return 0;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  long spins = 0;
+  while (C.gen.load(std::memory_order_acquire) == g) {
+    if (C.abort.load(std::memory_order_acquire)) return -1;
+    if (++spins > 2000) {
+      struct timespec d = {0, 20000};
+      nanosleep(&d, nullptr);
+      if ((spins & 1023) == 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+              ipc_timeout_s_) {
+        ipc_abort();  // a peer died or diverged: fail every rank instead of hanging
+        return -1;
+      }
+    } else {
+      sched_yield();
+    }
+  }
+  return 0;
+}
+
+int Comm::ipc_group_end(void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  IpcSlot &me = ipc_->slot[rank];
+  auto bail = [&]() {
+    ipc_abort();
+    return -1;
+  };
+  size_t total = 0;
+  for (auto &o : sends_) total += o.n;
+  if ((int)sends_.size() > IPC_MAXPOST) return bail();
+  if (total > stage_cap_) {  // peers finished reading the old buffer (last group's barrier)
+    if (hipStreamSynchronize(s) != hipSuccess) return bail();
+    if (stage_) (void)hipFree(stage_);
+    stage_ = nullptr;
+    size_t cap = std::max<size_t>(total + total / 4, 1 << 16);
+    if (hipMalloc(&stage_, cap * sizeof(double)) != hipSuccess) return bail();
+    if (hipIpcGetMemHandle(&me.h, stage_) != hipSuccess) return bail();
+    stage_cap_ = cap;
+    me.gen++;
+  }
+  size_t off = 0;
+  me.nposts = 0;
+  for (auto &o : sends_) {
+    if (o.n && hipMemcpyAsync(stage_ + off, o.src, o.n * sizeof(double), hipMemcpyDeviceToDevice,
+                              s) != hipSuccess)
+      return bail();
+    me.posts[me.nposts++] = {o.peer, 0, off, o.n};
+    off += o.n;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return bail();  // staged data is complete
+  if (ipc_barrier()) return -1;
+  std::vector<int> seen(nranks, 0);
+  for (auto &r : recvs_) {
+    const IpcSlot &ps = ipc_->slot[r.peer];
+    int k = seen[r.peer]++, cnt = 0;
+    const IpcPost *hit = nullptr;
+    for (int i = 0; i < ps.nposts; i++)
+      if (ps.posts[i].dst == rank && cnt++ == k) hit = &ps.posts[i];
+    if (!hit || hit->n != r.n) return bail();
+    if (peer_gen_[r.peer] != ps.gen) {  // (re)map the peer's staging buffer
+      if (peer_base_[r.peer]) (void)hipIpcCloseMemHandle(peer_base_[r.peer]);
+      peer_base_[r.peer] = nullptr;
+      void *p = nullptr;
+      if (hipIpcOpenMemHandle(&p, ps.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+        return bail();
+      peer_base_[r.peer] = (double *)p;
+      peer_gen_[r.peer] = ps.gen;
+    }
+    if (r.n && hipMemcpyAsync(r.dst, peer_base_[r.peer] + hit->off, r.n * sizeof(double),
+                              hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return bail();
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return bail();
+  return ipc_barrier();  // our staging buffer may be rewritten only after every peer copied
+}
+
+// ------------------------------------------------------------------ common
 int Comm::unique_id(void *out128) {
   ncclUniqueId id;
   if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
@@ -59,6 +245,8 @@ int Comm::unique_id(void *out128) {
 int Comm::init(int r, int n, const void *id128) {
   rank = r;
   nranks = n;
+  if (!id128) return -1;
+  if (is_ipc_id(id128)) return init_ipc(id128);
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
   ncclComm_t c;
@@ -84,7 +272,7 @@ int Comm::init_local(int r, int n, LocalHub *hub) {
 }
 
 int Comm::group_start() {
-  if (hub_) {
+  if (hub_ || ipc_) {
     sends_.clear();
     recvs_.clear();
     return 0;
@@ -93,6 +281,7 @@ int Comm::group_start() {
 }
 
 int Comm::group_end(void *stream) {
+  if (ipc_) return ipc_group_end(stream);
   if (!hub_) return ncclGroupEnd() == ncclSuccess ? 0 : -1;
   hipStream_t s = (hipStream_t)stream;
   LocalHub &H = *hub_;
@@ -123,7 +312,7 @@ int Comm::group_end(void *stream) {
 }
 
 int Comm::send(const double *buf, size_t n, int peer, void *stream) {
-  if (hub_) {
+  if (hub_ || ipc_) {
     sends_.push_back({nullptr, buf, n, peer});
     return 0;
   }
@@ -132,7 +321,7 @@ int Comm::send(const double *buf, size_t n, int peer, void *stream) {
              : -1;
 }
 int Comm::recv(double *buf, size_t n, int peer, void *stream) {
-  if (hub_) {
+  if (hub_ || ipc_) {
     recvs_.push_back({buf, nullptr, n, peer});
     return 0;
   }
@@ -155,6 +344,20 @@ int Comm::allreduce_sum(double *host, int n, void *stream) {
     H.barrier();
     return 0;
   }
+  if (ipc_) {  // same rank-order sum as the in-process hub, in chunks of the slot buffer
+    for (int q = 0; q < n; q += IPC_RED) {
+      const int m = std::min(IPC_RED, n - q);
+      memcpy(ipc_->slot[rank].red, host + q, m * sizeof(double));
+      if (ipc_barrier()) return -1;
+      for (int i = 0; i < m; i++) {
+        double acc = 0.0;
+        for (int r = 0; r < nranks; r++) acc += ipc_->slot[r].red[i];
+        host[q + i] = acc;
+      }
+      if (ipc_barrier()) return -1;
+    }
+    return 0;
+  }
   hipStream_t s = (hipStream_t)stream;
   if ((size_t)n > dcap_) {  // grow the device staging buffer (64 doubles at init)
     if (hipStreamSynchronize(s) != hipSuccess) return -1;
@@ -173,9 +376,19 @@ int Comm::allreduce_sum(double *host, int n, void *stream) {
   return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
 }
 
+int Comm::agree_ok(bool ok, void *stream) {
+  double v = ok ? 0.0 : 1.0;
+  if (allreduce_sum(&v, 1, stream)) return -1;
+  return v == 0.0 ? 0 : -1;
+}
+
 Comm::~Comm() {
   if (comm_) ncclCommDestroy((ncclComm_t)comm_);
   if (dscratch_) hipFree(dscratch_);
+  for (auto p : peer_base_)
+    if (p) (void)hipIpcCloseMemHandle(p);
+  if (stage_) (void)hipFree(stage_);
+  if (ipc_) munmap(ipc_, sizeof(IpcCtl));
   // events belong to the hub (it may be destroyed before or after us)
 }
 

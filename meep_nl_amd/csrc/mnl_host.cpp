@@ -270,6 +270,7 @@ struct mnl_fields {
   bool src_dirty = true;
   std::vector<long long> srcB_idx, srcD_idx, isrc_idx;  // local linear indices
   std::vector<int> srcB_comp, srcD_comp, isrc_comp;
+  std::vector<unsigned char> isrc_zone;  // owning reference chunk (zone box) per isrc point
   std::vector<std::pair<int, int>> srcB_ref, srcD_ref, isrc_ref;  // (group, point)
   long long *d_srcB_idx = nullptr, *d_srcD_idx = nullptr;
   int *d_srcB_comp = nullptr, *d_srcD_comp = nullptr;
@@ -1135,6 +1136,20 @@ long long local_index(const mnl_fields *F, int c, const int jg[3], bool include_
   return li;
 }
 
+// local linear index of a global point anywhere in this rank's arrays (ghost
+// planes included), or -1
+long long local_index_ghost(const mnl_fields *F, const int jg[3]) {
+  const DevGrid &g = F->g;
+  long long li = 0;
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    int j = jg[d] - g.off[d];
+    if (j < 0 || j >= g.N[g.ax[d]]) return -1;
+    li += (long long)j * g.st[g.ax[d]];
+  }
+  return li;
+}
+
 int build_source_lists(mnl_fields *F) {
   // whole-cell facts (the same on every rank): what keeps the step unfused
   F->any_srcB = F->any_isrc = F->any_dsrc_w = false;
@@ -1152,6 +1167,7 @@ int build_source_lists(mnl_fields *F) {
   F->srcB_idx.clear(), F->srcD_idx.clear(), F->isrc_idx.clear();
   F->srcB_comp.clear(), F->srcD_comp.clear(), F->isrc_comp.clear();
   F->srcB_ref.clear(), F->srcD_ref.clear(), F->isrc_ref.clear();
+  F->isrc_zone.clear();
   for (size_t gi = 0; gi < F->groups.size(); gi++) {
     const SrcGroup &G = F->groups[gi];
     const SrcTime &st = F->srcs[G.st];
@@ -1161,12 +1177,31 @@ int build_source_lists(mnl_fields *F) {
       const int *jg = &G.jglob[3 * j];
       int tgt = mag ? 3 * T_B + cdir(c) : 3 * T_D + cdir(c);
       long long li = local_index(F, tgt, jg, false);
-      if (li < 0) continue;
       if (st.is_integrated && !mag) {
+        // integrated dipoles are read (never written): keep the rank's ghost copies
+        // too, so a slab seam sees what one GPU sees; the zone box restricts the
+        // subtraction to readers in the owning reference chunk
+        if (li < 0 && F->nranks > 1) {
+          bool wall = false;  // high PEC wall of an unshifted direction: nobody owns it
+          for (int d = 0; d < 3; d++)
+            if (F->g.ax[d] >= 0 && !F->S.shift(tgt, d) && jg[d] == F->g.nglob[d]) wall = true;
+          if (!wall) li = local_index_ghost(F, jg);
+        }
+        if (li < 0) continue;
+        int zb = 0;
+        for (int d = 0; d < 3; d++) {
+          int z = 1;
+          if (F->S.has[d]) z = F->h_zone[d][2 * jg[d] + F->S.shift(tgt, d)];
+          zb = zb * 3 + z;
+        }
         F->isrc_idx.push_back(li);
         F->isrc_comp.push_back(cdir(c));
+        F->isrc_zone.push_back((unsigned char)zb);
         F->isrc_ref.push_back({(int)gi, (int)j});
-      } else if (!st.is_integrated) {
+        continue;
+      }
+      if (li < 0) continue;
+      if (!st.is_integrated) {
         auto &I = mag ? F->srcB_idx : F->srcD_idx;
         auto &C = mag ? F->srcB_comp : F->srcD_comp;
         auto &R = mag ? F->srcB_ref : F->srcD_ref;
@@ -2438,7 +2473,8 @@ int step_batch(mnl_fields *F, int nsteps) {
       SrcDev sD{(int)nD, F->d_srcD_idx, F->d_srcD_comp, F->d_vals + nB};
       ISrcDev is;
       is.n = (int)nI;
-      for (size_t k = 0; k < nI; k++) is.idx[k] = F->isrc_idx[k], is.comp[k] = F->isrc_comp[k];
+      for (size_t k = 0; k < nI; k++)
+        is.idx[k] = F->isrc_idx[k], is.comp[k] = F->isrc_comp[k], is.zone[k] = F->isrc_zone[k];
       is.val = F->d_vals + nB + nD;
       // per-step tables are strided by `per`: encode via pointer offset + stride trick
       // (kernels index val[step*n + k]; use a dedicated stride by shifting base per step)
@@ -3074,7 +3110,9 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (nranks > 1) {
     F->comm.reset(new Comm());
     if (hub ? F->comm->init_local(rank, nranks, hub) : F->comm->init(rank, nranks, id)) {
-      fail(hub ? "local slab group init failed" : "RCCL communicator init failed");
+      fail(hub ? "local slab group init failed"
+               : Comm::is_ipc_id(id) ? "IPC slab group init failed (shared-memory id)"
+                                     : "RCCL communicator init failed");
       return nullptr;
     }
   }
@@ -3327,6 +3365,60 @@ int mnl_slab_range(int ncell, int rank, int nranks, int *lo, int *hi) {
   return 0;
 }
 int mnl_comm_unique_id(void *out128) { return Comm::unique_id(out128) ? fail("ncclGetUniqueId failed") : 0; }
+int mnl_comm_ipc_id(void *out128, int nranks) {
+  if (!out128) return fail("null id buffer");
+  return Comm::ipc_id(out128, nranks) ? fail("cannot create the IPC shared-memory segment") : 0;
+}
+int mnl_comm_ipc_unlink(const void *id128) {
+  return Comm::ipc_unlink(id128) ? fail("no such IPC shared-memory segment") : 0;
+}
+int mnl_comm_ipc_reduce(const void *id128, int rank, int nranks, double *host, int n, int ok) {
+  if (!Comm::is_ipc_id(id128) || nranks < 1 || rank < 0 || rank >= nranks || n < 0)
+    return fail("bad IPC id / rank / size");
+  Comm cm;
+  if (cm.init(rank, nranks, id128)) return fail("IPC slab group init failed (shared-memory id)");
+  if (cm.agree_ok(ok != 0, nullptr)) return fail("a rank reported failure");
+  if (cm.allreduce_sum(host, n, nullptr)) return fail("IPC allreduce failed");
+  return 0;
+}
+const char *mnl_fields_transport(mnl_fields *f) {
+  if (!f) return "";
+  return f->comm ? f->comm->transport() : "single";
+}
+int mnl_comm_rccl_selftest(int device, int n) {
+  if (n < 1) return fail("selftest needs n >= 1");
+  if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
+  char id[128];
+  if (Comm::unique_id(id)) return fail("ncclGetUniqueId failed");
+  Comm cm;
+  if (cm.init(0, 1, id)) return fail("RCCL communicator init failed");
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+  std::vector<double> h(n), back(n);
+  for (int i = 0; i < n; i++) h[i] = 0.5 * i - 3.25;
+  double *a = nullptr, *b = nullptr;
+  int rc = 0;
+  if (hipMalloc(&a, n * sizeof(double)) != hipSuccess ||
+      hipMalloc(&b, n * sizeof(double)) != hipSuccess)
+    rc = fail("hipMalloc failed");
+  if (!rc && hipMemcpy(a, h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail("upload failed");
+  if (!rc && (cm.group_start() || cm.send(a, n, 0, s) || cm.recv(b, n, 0, s) || cm.group_end(s)))
+    rc = fail("grouped send/recv failed");
+  if (!rc && (hipStreamSynchronize(s) != hipSuccess ||
+              hipMemcpy(back.data(), b, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
+    rc = fail("download failed");
+  if (!rc && memcmp(back.data(), h.data(), n * sizeof(double)) != 0)
+    rc = fail("send/recv data mismatch");
+  std::vector<double> red(h);
+  if (!rc && cm.allreduce_sum(red.data(), n, s)) rc = fail("allreduce failed");
+  if (!rc && memcmp(red.data(), h.data(), n * sizeof(double)) != 0)
+    rc = fail("allreduce data mismatch");
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  (void)hipStreamDestroy(s);
+  return rc;
+}
 
 void mnl_fields_destroy(mnl_fields *f) { delete f; }
 

@@ -137,6 +137,10 @@ struct ISrcDev {             // integrated sources, read by the E kernel
   int n;
   long long idx[MAX_ISRC];
   int comp[MAX_ISRC];
+  // reference chunk (zone box zx*9+zy*3+zz) owning the point: only that chunk's
+  // f_minus_p has the dipole subtracted (src/update_eh.cpp:136-146 loops over the
+  // chunk's own src_vols); another chunk reading it as a ghost sees D - P only
+  unsigned char zone[MAX_ISRC];
   const double *val;         // [step][n] dipole value real(amp*dipole(t+dt))
 };
 

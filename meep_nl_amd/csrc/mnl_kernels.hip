@@ -460,15 +460,19 @@ __device__ __forceinline__ double dmp_own(const DevFields &f, const ISrcDev &is,
   return v;
 }
 
+// f_minus_p of component c at a neighbour n as the reader's reference chunk
+// (zone box rz) holds it: integrated dipoles are subtracted only at points that
+// chunk owns (the oracle's per-chunk fmp; DESIGN.md "Integrated sources on seams")
 template <bool ISRC>
 __device__ __forceinline__ double dmp_at(const DevFields &f, const ISrcDev &is, int step, int c,
-                                         long long n) {
+                                         long long n, int rz) {
   double v = f.Dn[c][n];
   for (int k = 0; k < f.npol; k++)
     if (f.pol[k].P[c]) v -= f.pol[k].P[c][n];
   if (ISRC) {
     for (int k = 0; k < is.n; k++)
-      if (is.comp[k] == c && is.idx[k] == n) v -= is.val[(long long)step * is.n + k];
+      if (is.comp[k] == c && is.idx[k] == n && is.zone[k] == rz)
+        v -= is.val[(long long)step * is.n + k];
   }
   return v;
 }
@@ -499,6 +503,14 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
     if (!f.ecomp_present[d]) continue;
     if (!owned(g, T_E, d, p)) continue;
     const double gs = dmp_own<ISRC>(f, is, step, d, i, pm);
+    // reference chunk of this voxel (zone box; interior kernels: 13 = interior chunk)
+    int rz = 13;
+    if (SHELL && (NR || ISRC)) {
+      int z3[3];
+#pragma unroll
+      for (int e = 0; e < 3; e++) z3[e] = g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, d, e)] : 1;
+      rz = z3[0] * 9 + z3[1] * 3 + z3[2];
+    }
     const double *u = f.inveps[d];
     const double *E = f.E[d];
     double *En = f.En[d];
@@ -516,8 +528,9 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
       const long long s = g.sdir[d];
       auto nsum = [&](int e) {
         const long long se = g.sdir[e];
-        return dmp_at<ISRC>(f, is, step, e, i) + dmp_at<ISRC>(f, is, step, e, i + s) +
-               dmp_at<ISRC>(f, is, step, e, i - se) + dmp_at<ISRC>(f, is, step, e, i + (s - se));
+        return dmp_at<ISRC>(f, is, step, e, i, rz) + dmp_at<ISRC>(f, is, step, e, i + s, rz) +
+               dmp_at<ISRC>(f, is, step, e, i - se, rz) +
+               dmp_at<ISRC>(f, is, step, e, i + (s - se), rz);
       };
       const double us = u ? u[i] : 1.0;
       double dsq = gs * gs;
@@ -542,13 +555,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
       bool done = false;
       if (NR) {
         // 3x3 chi1inv + chi2 branch (src/step_generic.cpp:730-816)
-        int zb = 13;
-        if (SHELL) {
-          int z3[3];
-#pragma unroll
-          for (int e = 0; e < 3; e++) z3[e] = g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, d, e)] : 1;
-          zb = z3[0] * 9 + z3[1] * 3 + z3[2];
-        }
+        const int zb = rz;
         const int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
         const bool have_off =
             ((f.offd_zone[zb] >> (3 * d)) & 3) == 3 && f.chi2[d] && f.ecomp_present[d1] &&
@@ -559,13 +566,15 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
           int zc = (u[i] == 0) + (u1[i] == 0) + (u2[i] == 0);
           if (!(chi2new == 0 || zc > 1)) {
             const long long s = g.sdir[d], s1 = g.sdir[d1], s2 = g.sdir[d2];
-            double gs_2 = (dmp_at<ISRC>(f, is, step, d1, i) + dmp_at<ISRC>(f, is, step, d1, i + s) +
-                           dmp_at<ISRC>(f, is, step, d1, i - s1) +
-                           dmp_at<ISRC>(f, is, step, d1, i + (s - s1))) *
+            double gs_2 = (dmp_at<ISRC>(f, is, step, d1, i, rz) +
+                           dmp_at<ISRC>(f, is, step, d1, i + s, rz) +
+                           dmp_at<ISRC>(f, is, step, d1, i - s1, rz) +
+                           dmp_at<ISRC>(f, is, step, d1, i + (s - s1), rz)) *
                           0.25;
-            double gs_3 = (dmp_at<ISRC>(f, is, step, d2, i) + dmp_at<ISRC>(f, is, step, d2, i + s) +
-                           dmp_at<ISRC>(f, is, step, d2, i - s2) +
-                           dmp_at<ISRC>(f, is, step, d2, i + (s - s2))) *
+            double gs_3 = (dmp_at<ISRC>(f, is, step, d2, i, rz) +
+                           dmp_at<ISRC>(f, is, step, d2, i + s, rz) +
+                           dmp_at<ISRC>(f, is, step, d2, i - s2, rz) +
+                           dmp_at<ISRC>(f, is, step, d2, i + (s - s2), rz)) *
                           0.25;
             double us = 1 / u[i];
             double us_2 = us, us_3 = us;

@@ -372,6 +372,31 @@ def sc_nr_pml_dispersive(make, steps=30):
     return o
 
 
+def sc_nr_isrc_seam(make, steps=30):
+    """chi2 Newton-Raphson voxels on both sides of a reference chunk seam (the low-z
+    PML boundary, z = -0.6) with integrated sources ON the seam: Ex exactly at the
+    seam point (owned by the PML chunk) and Ez between the seam's two neighbours.
+    The reference subtracts an integrated dipole only in its owner chunk's
+    f_minus_p (src/update_eh.cpp:136-146); the NR 4-point averages of the other
+    chunk read the ghost D - P without it (src/step_generic.cpp:740-743)."""
+    o = vol(make, 3, [2.6, 2.6, 2.6], 10, center_origin=True)
+    o.add_pml(0.6)
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        inside = (np.abs(x) < 0.5) & (np.abs(y) < 0.5) & (z > -0.95) & (z < 0.3)
+        for d in range(3):
+            if d == c:
+                o.set_chi1inv(c, d, np.where(inside, 0.25, 1.0))
+            else:
+                o.set_chi1inv(c, d, np.where(inside, 1e-3, 0.0))
+        o.set_chi2(c, np.where(inside, 0.5, 0.0))
+    o.legacy_point_source(0, 0.5, 0.5, 0.0, 3.0, (0.05, 0.05, -0.6), 5.0)
+    o.legacy_point_source(2, 0.45, 0.5, 0.0, 3.0, (0.0, 0.0, -0.57), 4.0)
+    o.legacy_point_source(1, 0.4, 0.5, 0.0, 3.0, (-0.03, 0.02, -0.61), 3.0)
+    o.step(steps)
+    return o
+
+
 def sc_known_metallic_3d(make):
     o = vol(make, 3, [1, 1, 1], 10)
     o.legacy_point_source(2, 0.2, 3.0, 0.0, 2.0, o.center(), complex(0, -2 * math.pi * 0.2))

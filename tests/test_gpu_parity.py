@@ -66,6 +66,16 @@ def test_nr_pml_dispersive():
     _bitwise(sc_nr_pml_dispersive(ProductSim), sc_nr_pml_dispersive(make_oracle))
 
 
+def test_nr_integrated_source_on_chunk_seam():
+    """Integrated sources on a reference chunk seam next to chi2 NR voxels: the
+    dipole is subtracted only by readers in the owning chunk (the reference's
+    per-chunk f_minus_p, src/update_eh.cpp:136-146)."""
+    from scenarios import sc_nr_isrc_seam
+    p = sc_nr_isrc_seam(ProductSim)
+    assert p.nr_random_fallbacks() == 0
+    _bitwise(p, sc_nr_isrc_seam(make_oracle))
+
+
 def test_known_results(golden):
     kr = golden["known_results"]
     p = sc_known_metallic_3d(ProductSim)

@@ -31,6 +31,15 @@ def test_slabs_nr_dispersive():
     _bitwise(sc_nr_pml_dispersive(GroupSim3), sc_nr_pml_dispersive(make_oracle))
 
 
+@pytest.mark.parametrize("G", [GroupSim, GroupSim3])
+def test_slabs_nr_integrated_seams(G):
+    """Integrated sources on a reference chunk seam AND (2 slabs) next to the slab
+    seam at z = 0: ghost copies of the dipole points follow the owner-chunk rule."""
+    from scenarios import sc_nr_isrc_seam
+    _bitwise(sc_nr_isrc_seam(G), sc_nr_isrc_seam(make_oracle))
+    _bitwise(sc_nr_pml_dispersive(G), sc_nr_pml_dispersive(make_oracle))
+
+
 def test_slabs_multi_source():
     _bitwise(sc_multi_source_3d(GroupSim3), sc_multi_source_3d(make_oracle))
 
