@@ -121,23 +121,6 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
-def pick_transport(world, local_rank):
-    """RCCL over xGMI when every local rank has its own GPU; the IPC transport when
-    ranks must share one (a one-GPU rehearsal of the multi-process path).
-    Returns (transport, device)."""
-    from meep_nl_amd import core
-    ndev = core.device_count()
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    forced = os.environ.get("MNL_BENCH_DEVICE")
-    device = int(forced) if forced else local_rank % max(ndev, 1)
-    tr = os.environ.get("MNL_COMM")
-    if not tr:
-        tr = "ipc" if (forced or ndev < local_world) else "rccl"
-    if tr not in ("ipc", "rccl"):
-        raise SystemExit(f"MNL_COMM must be ipc or rccl, not {tr!r}")
-    return tr, device
-
-
 def main():
     args = parse()
     if args.workload == "vacuum":
@@ -160,7 +143,7 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from meep_nl_amd import core
-        transport, device = pick_transport(world, local_rank)
+        transport, device = core.pick_transport(world, local_rank)
         obj = [core.comm_id(world, transport) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nid = obj[0]

@@ -178,8 +178,16 @@ int mnl_fields_add_custom_point_source(mnl_fields *f, int comp, mnl_src_func fun
 int mnl_fields_require_component(mnl_fields *f, int comp);
 /* fields::step() x nsteps (src/step.cpp:35-140).  Collective for
  * distributed fields.  NaN/Inf check of the D energy density at the cell
- * centre (src/step.cpp:138-139) runs once per call. */
+ * centre (src/step.cpp:138-139) every `every` steps (default 100, and after the
+ * last step): fails with "meep: simulation fields are NaN or Inf". */
 int mnl_fields_step(mnl_fields *f, int nsteps);
+int mnl_fields_set_nan_check(mnl_fields *f, int every);
+/* fields::initialize_field(c, func) (src/initialize.cpp:135-161) with the
+ * function evaluated by the caller: host = real part of func at every point of
+ * component c in the whole-cell layout (n >= cell size).  Adds it to the
+ * field, zeroes the metallic walls, exchanges ghosts; for D / B components also
+ * updates E / H from them, as the reference does.  Collective. */
+int mnl_fields_initialize_field(mnl_fields *f, int comp, const double *host, size_t n);
 /* t (timesteps) and dt; time() = t*dt, round_time() = float(t*dt)
  * (src/meep.hpp:1891-1892). */
 int mnl_fields_time(mnl_fields *f, long long *t, double *dt);

@@ -261,6 +261,20 @@ class Fields:
     def require_component(self, comp):
         check(lib().mnl_fields_require_component(self.h, comp))
 
+    def initialize_field(self, comp, values):
+        """fields::initialize_field(c, func) (src/initialize.cpp:135-161): values is
+        the whole-cell array of func at the points of comp (real part used), or a
+        callable f(*coords) vectorised over the coordinate arrays of comp."""
+        if callable(values):
+            values = values(*self.gv.coords(comp))
+        v = np.ascontiguousarray(np.real(np.broadcast_to(values, self.gv.shape())),
+                                 dtype=np.float64).ravel()
+        check(lib().mnl_fields_initialize_field(self.h, comp, ptr(v), v.size))
+
+    def set_nan_check(self, every):
+        """NaN / Inf guard cadence in steps (src/step.cpp:138-139 checks every step)."""
+        check(lib().mnl_fields_set_nan_check(self.h, int(every)))
+
     def last_source_time(self):
         """fields::last_source_time (src/bands.cpp:35-41): latest src_time::last_time()."""
         return max([0.0] + getattr(self, "_last_times", []))
@@ -464,6 +478,23 @@ def ipc_id(nranks):
     buf = ctypes.create_string_buffer(128)
     check(lib().mnl_comm_ipc_id(buf, int(nranks)))
     return buf.raw
+
+
+def pick_transport(world, local_rank):
+    """Transport and device of one rank: RCCL over xGMI when every local rank has
+    its own GPU, the IPC transport when ranks must share one.  Overrides:
+    MNL_COMM=rccl|ipc, MNL_BENCH_DEVICE=<device for every rank>.
+    Returns (transport, device)."""
+    ndev = device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    forced = os.environ.get("MNL_BENCH_DEVICE")
+    device = int(forced) if forced else local_rank % max(ndev, 1)
+    tr = os.environ.get("MNL_COMM")
+    if not tr:
+        tr = "ipc" if (forced or ndev < local_world) else "rccl"
+    if tr not in ("ipc", "rccl"):
+        raise ValueError(f"MNL_COMM must be ipc or rccl, not {tr!r}")
+    return tr, device
 
 
 def comm_id(nranks, transport):

@@ -261,6 +261,15 @@ struct mnl_fields {
   unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedG (null: f64 chi1inv)
   double *d_utab = nullptr;    // 3 x 256 palette values
   bool allow_fused = true;
+  // the reference allocates H (as a copy of B) and the W auxiliary fields (as a
+  // copy of E / H) on the first update_eh (src/update_eh.cpp:204-216); the first
+  // step runs unfused and performs those copies at the same points of the step
+  bool e_first_done = false, h_first_done = false;
+  bool u_first_done[2] = {false, false};  // f_u of B / D: a copy of f on the first step_db
+                                          // (src/step_db.cpp:71-75)
+  bool first_step_mode = false;
+  bool force_unfused_next = false;  // E / H set directly (initialize_field): E != chi1inv D
+  int nan_every = 100;              // NaN guard cadence inside a batch (src/step.cpp:138-139)
   CurlPlan planB, planD;
   bool nr = false;
   bool upnl = false;  // upstream chi2/chi3 update active (nl_mode 1 with nonzero chi)
@@ -2359,6 +2368,42 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
   return 0;
 }
 
+// first update_eh(H_stuff): H = copy of B and f_w = copy of H where they are
+// separate (src/update_eh.cpp:204-216)
+int h_lazy_copy(mnl_fields *F) {
+  DevFields &f = F->f;
+  for (int d = 0; d < 3; d++) {
+    if (!f.H[d] || !f.Bn[d]) continue;
+    if (k_copy(f.H[d], f.Bn[d], (long long)F->nlocal, F->stream)) return fail("copy launch failed");
+    if (f.WH[d] && k_copy(f.WH[d], f.Bn[d], (long long)F->nlocal, F->stream))
+      return fail("copy launch failed");
+  }
+  F->h_first_done = true;
+  return 0;
+}
+// first step_db(B_stuff / D_stuff): f_u = copy of f where a PML lies along
+// dsigu (src/step_db.cpp:71-75)
+int u_lazy_copy(mnl_fields *F, int which) {
+  DevFields &f = F->f;
+  for (int d = 0; d < 3; d++) {
+    double *u = which == 0 ? f.UB[d] : f.UD[d];
+    const double *src = which == 0 ? f.B[d] : f.D[d];
+    if (u && src && k_copy(u, src, (long long)F->nlocal, F->stream)) return fail("copy launch failed");
+  }
+  F->u_first_done[which] = true;
+  return 0;
+}
+// first update_eh(E_stuff): f_w = copy of E (src/update_eh.cpp:212-216)
+int e_lazy_copy(mnl_fields *F) {
+  DevFields &f = F->f;
+  for (int d = 0; d < 3; d++)
+    if (f.WE[d] && f.E[d] &&
+        k_copy(f.WE[d], f.E[d], (long long)F->nlocal, F->stream))
+      return fail("copy launch failed");
+  F->e_first_done = true;
+  return 0;
+}
+
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
   if (set_fused(F, fused_agreed(F))) return -1;
@@ -2486,6 +2531,7 @@ int step_batch(mnl_fields *F, int nsteps) {
         continue;
       }
       // ---- B: halo of E (low ghost), curl, sources
+      if (!F->u_first_done[0] && u_lazy_copy(F, 0)) return -1;
       if (F->nranks > 1) {
         int k = ev_begin(TM_HALO);
         if (exchange(F, 0)) return fail("E halo exchange failed");
@@ -2531,13 +2577,14 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       ev_end(k);
       // shell curl B; the PML H update rides along when no B source sits between
-      const bool fuseH = nB == 0;
+      const bool fuseH = nB == 0 && !F->first_step_mode;
       k = ev_begin(TM_B);
       if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream, fuseH))
         return fail("curl B launch failed");
       ev_end(k);
       if (nB && k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
       // ---- H
+      if (!F->h_first_done && h_lazy_copy(F)) return -1;
       k = ev_begin(TM_H);
       bool anyH = false;
       for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
@@ -2549,12 +2596,14 @@ int step_batch(mnl_fields *F, int nsteps) {
         ev_end(kk);
       }
       // ---- D
+      if (!F->u_first_done[1] && u_lazy_copy(F, 1)) return -1;
       k = ev_begin(TM_DINT);
       if (!F->fused && k_curl(T_D, F->interior, nullptr, g, f, F->planD, F->S.courant, F->stream))
         return fail("curl D launch failed");
       ev_end(k);
       // shell curl D; the shell E update rides along when it only reads its own D
-      const bool fuseE = !F->nr && !F->upnl && f.npol == 0 && nI == 0 && !F->dsrc_in_shell;
+      const bool fuseE = !F->nr && !F->upnl && f.npol == 0 && nI == 0 && !F->dsrc_in_shell &&
+                         !F->first_step_mode;
       k = ev_begin(TM_D);
       if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream, fuseE))
         return fail("curl D launch failed");
@@ -2564,6 +2613,7 @@ int step_batch(mnl_fields *F, int nsteps) {
         if (exchange(F, 2)) return fail("D halo exchange failed");
       }
       // ---- E (+ Lorentzian P)
+      if (!F->e_first_done && e_lazy_copy(F)) return -1;
       k = ev_begin(TM_E);
       // neighbour reads of D - P (NR, upstream chi) or of W (anisotropic sigma):
       // P after all of E
@@ -2779,6 +2829,10 @@ int fields_load(mnl_fields *F, const char *path) {
   }
   if (matched != nfield) return fail("fields file does not match these fields (allocated arrays differ)");
   F->t = h.t;
+  // the loaded state comes from fields that were stepped: H and the W fields are
+  // already separate (a dump taken before the first step holds zeros in them)
+  F->e_first_done = F->h_first_done = true;
+  F->u_first_done[0] = F->u_first_done[1] = true;
   return 0;
 }
 
@@ -3078,6 +3132,92 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   return 0;
 }
 
+// fields::step() n times: the NaN guard (src/step.cpp:138-139) every nan_every
+// steps; the first step after construction (or after E / H were set directly)
+// runs unfused (see e_first_done)
+int fields_step(mnl_fields *F, int nsteps) {
+  while (nsteps > 0) {
+    int m;
+    if (!F->e_first_done || !F->h_first_done || !F->u_first_done[0] || !F->u_first_done[1] ||
+        F->force_unfused_next) {
+      const bool saved = F->allow_fused;
+      F->allow_fused = false;
+      F->first_step_mode = true;
+      const int r = step_batch(F, 1);
+      F->allow_fused = saved;
+      F->first_step_mode = false;
+      if (r) return -1;
+      F->force_unfused_next = false;
+      m = 1;
+    } else {
+      m = std::min(nsteps, F->nan_every);
+      if (step_batch(F, m)) return -1;
+    }
+    nsteps -= m;
+    if (nan_check(F)) return -1;
+  }
+  return 0;
+}
+
+// fields::initialize_field(c, func) (src/initialize.cpp:135-148) with the
+// function's values given as a whole-cell host array (canonical layout, real
+// part): add, step_boundaries(type(c)); for D / B also update_eh(E / H) and
+// step_boundaries of that type.  Integrated-source dipoles are not subtracted
+// in that E update (DESIGN.md "initialize_field").
+int initialize_field(mnl_fields *F, int c, const double *host) {
+  if (require_component(F, c)) return -1;
+  if (F->fused && set_fused(F, false)) return -1;
+  const int t = ctype(c), d = cdir(c);
+  DevFields &f = F->f;
+  size_t nt = F->S.ntot;
+  if (F->scratch_cap < nt) {
+    HIPCHK(hipStreamSynchronize(F->stream));
+    if (F->d_scratch) hipFree(F->d_scratch);
+    F->d_scratch = nullptr;
+    HIPCHK(hipMalloc(&F->d_scratch, nt * sizeof(double)));
+    F->scratch_cap = nt;
+  }
+  HIPCHK(hipMemcpyAsync(F->d_scratch, host, nt * sizeof(double), hipMemcpyHostToDevice, F->stream));
+  double *dst = nullptr, *alt = nullptr;
+  switch (t) {
+    case T_E: dst = f.E[d]; break;
+    case T_D: dst = f.D[d]; break;
+    case T_B: dst = f.B[d]; break;
+    case T_H:  // H == B until the first H update separates it (PML chunks only)
+      dst = f.B[d];
+      if (F->h_first_done && f.H[d]) dst = f.H[d], alt = f.B[d];
+      break;
+  }
+  if (!dst) return fail("initialize_field: component not allocated");
+  if (k_init_add(dst, alt, F->d_scratch, F->g, f, t, d, F->stream))
+    return fail("initialize_field kernel launch failed");
+  if (F->nranks > 1) {
+    const int kind = t == T_E ? 0 : t == T_D ? 2 : 1;
+    if (exchange(F, kind)) return fail("initialize_field halo exchange failed");
+  }
+  ISrcDev is;
+  is.n = 0;
+  is.val = nullptr;
+  if (t == T_D) {  // update_eh(E_stuff); step_boundaries(E_stuff)
+    if (!F->e_first_done && e_lazy_copy(F)) return -1;
+    if (k_update_e(F->interior, nullptr, F->g, f, is, 0, false, F->stream) ||
+        k_update_e(F->interior, &F->shell_list, F->g, f, is, 0, false, F->stream))
+      return fail("update E launch failed");
+    if (F->nranks > 1 && exchange(F, 0)) return fail("E halo exchange failed");
+  } else if (t == T_B) {  // update_eh(H_stuff); step_boundaries(H_stuff)
+    if (!F->h_first_done && h_lazy_copy(F)) return -1;
+    bool anyH = false;
+    for (int e = 0; e < 3; e++) anyH = anyH || f.H[e];
+    if (anyH && k_update_h(F->shell_list, F->g, f, F->stream))
+      return fail("update H launch failed");
+    if (F->nranks > 1 && exchange(F, 1)) return fail("H halo exchange failed");
+  } else {
+    F->force_unfused_next = true;  // E (or H) differs from what D (B) implies
+  }
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
 mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, const void *id,
                           LocalHub *hub = nullptr) {
   if (!s) {
@@ -3120,6 +3260,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *bp = getenv("MNL_FUSED_BPC")) F->fused_bpc = std::max(1, atoi(bp));
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
+  if (const char *ne = getenv("MNL_NAN_EVERY")) F->nan_every = std::max(1, atoi(ne));
   if (const char *gc = getenv("MNL_GEN_CUS")) F->gen_cus = std::max(0, atoi(gc));
   if (const char *sg = getenv("MNL_STAGGER")) F->stagger = std::max(0, atoi(sg)) / 128 * 128;
   if (const char *ar = getenv("MNL_ARENA")) F->arena_req = std::max(0, atoi(ar));
@@ -3450,8 +3591,21 @@ int mnl_fields_step(mnl_fields *F, int nsteps) {
   if (!F) return fail("null fields");
   if (nsteps <= 0) return 0;
   if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
-  if (step_batch(F, nsteps)) return -1;
-  return nan_check(F);
+  return fields_step(F, nsteps);
+}
+
+int mnl_fields_initialize_field(mnl_fields *F, int comp, const double *host, size_t n) {
+  if (!F || check_comp(comp) || !host) return fail("bad argument");
+  if (n < F->S.ntot) return fail("initialize_field: array smaller than the cell");
+  if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  return initialize_field(F, comp, host);
+}
+
+int mnl_fields_set_nan_check(mnl_fields *F, int every) {
+  if (!F || every < 1) return fail("NaN check cadence must be >= 1 step");
+  F->nan_every = every;
+  return 0;
 }
 
 int mnl_fields_array_slice(mnl_fields *F, int comp, const double vmin[3], const double vmax[3],

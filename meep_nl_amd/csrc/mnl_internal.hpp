@@ -267,6 +267,9 @@ int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunk
                  long long npts, const DevGrid &g, const DevFields &f, void *stream);
 int k_dft_accum(const int *pj, const int *pch, double *dft, const double *fr, int n,
                 const double *ph, long long rstride, int nfreq, long long npts, void *stream);
+int k_init_add(double *dst, double *alt, const double *src, const DevGrid &g, const DevFields &f,
+               int comp_type, int comp_dir, void *stream);
+int k_copy(double *dst, const double *src, long long n, void *stream);
 int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_type,
                      int comp_dir, int zlo_glob, void *stream);
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,

@@ -2318,6 +2318,59 @@ int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_
   return rc();
 }
 
+// fields::initialize_field (src/initialize.cpp:135-161): every point of the
+// rank's array (ghost planes included: LOOP_OVER_VOL covers each chunk's whole
+// array) gets += v; then zero_metal (src/boundaries.cpp:304-339) zeroes the owned
+// points on the metallic high wall of each unshifted direction.  alt != null (H
+// after its lazy allocation): the H array holds the value only where H is
+// separate (PML chunk along c, src/update_eh.cpp:204-209), elsewhere H == B.
+__global__ void init_add_kernel(double *dst, double *alt, const double *src, DevGrid g,
+                                DevFields f, int type, int c, long long cs0, long long cs1,
+                                long long cs2) {
+  int i0 = blockIdx.x * MNL_BX + threadIdx.x;
+  int i1 = blockIdx.y * MNL_BY + threadIdx.y;
+  int i2 = blockIdx.z;
+  if (i0 >= g.N[0] || i1 >= g.N[1]) return;
+  int ii[3] = {i0, i1, i2};
+  Pt p;
+  long long cidx = 0;
+  const long long cs[3] = {cs0, cs1, cs2};
+  bool wall = false;
+  for (int d = 0; d < 3; d++) {
+    p.j[d] = g.ax[d] >= 0 ? ii[g.ax[d]] : 0;
+    if (g.ax[d] < 0) continue;
+    cidx += (long long)(p.j[d] + g.off[d]) * cs[d];
+    if (!shift_of(type, c, d) && p.j[d] + g.off[d] == g.nglob[d]) wall = true;
+  }
+  double *t = dst;
+  if (alt && !pml_at(f, g, c, qcoord(g, p, type, c, c))) t = alt;
+  const long long li = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
+  t[li] = wall ? 0.0 : t[li] + src[cidx];
+}
+
+// lazy allocation on the first update_eh (src/update_eh.cpp:204-216): H starts
+// as a copy of B, and the W auxiliary field as a copy of the field it shadows
+__global__ void copy_kernel(double *dst, const double *src, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+int k_copy(double *dst, const double *src, long long n, void *stream) {
+  if (n <= 0) return 0;
+  copy_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(dst, src, n);
+  return rc();
+}
+
+int k_init_add(double *dst, double *alt, const double *src, const DevGrid &g, const DevFields &f,
+               int comp_type, int comp_dir, void *stream) {
+  long long cs[3];
+  canon_strides(g, cs);
+  dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
+  init_add_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(
+      dst, alt, src, g, f, comp_type, comp_dir, cs[0], cs[1], cs[2]);
+  return rc();
+}
+
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
                    int comp_type, int comp_dir, const DevFields &f, const Box *fusedF,
                    const double *dsrc, const double *usrc, void *stream) {

@@ -439,8 +439,10 @@ def stop_after_walltime(t):
 
 # ---------------------------------------------------------------- distributed
 def _dist_context():
-    """(rank, world, local_rank, nccl_id) when launched one process per GPU by
-    torch.distributed.run, else None."""
+    """(rank, world, device, comm_id) when launched one process per GPU by
+    torch.distributed.run, else None.  The transport is RCCL when every local
+    rank has its own GPU, the IPC transport when ranks share one
+    (core.pick_transport)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return None
@@ -448,9 +450,17 @@ def _dist_context():
     if not dist.is_initialized():
         dist.init_process_group("gloo")
     rank = dist.get_rank()
-    obj = [core.unique_id() if rank == 0 else None]
+    transport, device = core.pick_transport(world, int(os.environ.get("LOCAL_RANK", rank)))
+    obj = [core.comm_id(world, transport) if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
-    return rank, world, int(os.environ.get("LOCAL_RANK", rank)), obj[0]
+    return rank, world, device, obj[0]
+
+
+def _dist_barrier():
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.barrier()
 
 
 # ---------------------------------------------------------------- Simulation
@@ -608,6 +618,23 @@ class Simulation:
         if getattr(self, "load_fields_file", None):  # delayed load (python/simulation.py:2509-2510)
             self.load_fields(self.load_fields_file)
 
+    def initialize_field(self, cmpnt=None, amp_func=None):
+        """Simulation.initialize_field (python/simulation.py:2520-2532) ->
+        fields::initialize_field (src/initialize.cpp:135-161): amp_func(Vector3)
+        -> complex at every point of the component (real part kept)."""
+        self.init_sim()
+        gv = self.fields.gv
+        pts = [p.ravel() for p in gv.coords(cmpnt)]
+        full = [np.zeros(pts[0].size) for _ in range(3)]
+        k = 0
+        for d in range(3):
+            if gv.has[d]:
+                full[d] = pts[k]
+                k += 1
+        vals = np.array([complex(amp_func(Vector3(x, y, z))).real
+                         for x, y, z in zip(*full)], dtype=np.float64)
+        self.fields.initialize_field(cmpnt, vals.reshape(gv.shape()))
+
     # -- time
     def meep_time(self):
         self.init_sim()
@@ -725,7 +752,14 @@ class Simulation:
         d = self._load_dump_dirname(dirname, single_parallel_file)
         os.makedirs(d, exist_ok=True)
         if dump_structure:
-            self.dump_structure(os.path.join(d, "structure.mnl"))
+            # the structure description is global: with a single parallel file only
+            # the master writes it (structure::dump, src/structure_dump.cpp), and no
+            # rank returns before it is complete
+            rank = self.fields.rank if self.fields is not None else 0
+            if not single_parallel_file or rank == 0:
+                self.dump_structure(os.path.join(d, "structure.mnl"))
+            if single_parallel_file:
+                _dist_barrier()
         if dump_fields:
             self.dump_fields(os.path.join(d, "fields.mnl"))
 

@@ -1680,6 +1680,42 @@ int orc_require_component(orc_sim *s, int comp) {
   return 0;
 }
 
+// fields::initialize_field (src/initialize.cpp:135-161): func's values given as a
+// whole-cell array; every point of each chunk's array (LOOP_OVER_VOL: ghosts
+// included) gets += value, then step_boundaries(type) and, for D / B, update_eh
+// of E / H and step_boundaries of that type.
+int orc_initialize_field(orc_sim *s, int comp, const double *vals) {
+  if (check_comp(s, comp)) return -1;
+  finalize(s);
+  require_component(s, comp);
+  const GV &G = s->gv;
+  for (auto &ch : s->chunks) {
+    realnum *f = s->allocated[comp] ? ch.F(comp) : nullptr;
+    if (!f) continue;
+    const GV &g = ch.gv;
+    int lo[3], hi[3];
+    for (int d = 0; d < 3; d++) {
+      lo[d] = g.has[d] ? g.io[d] + g.shift(comp, d) : 0;
+      hi[d] = g.has[d] ? g.big(d) + g.shift(comp, d) : 0;
+    }
+    int p[3];
+    for (p[0] = lo[0]; p[0] <= hi[0]; p[0] += 2)
+      for (p[1] = lo[1]; p[1] <= hi[1]; p[1] += 2)
+        for (p[2] = lo[2]; p[2] <= hi[2]; p[2] += 2) f[g.index(comp, p)] += vals[G.index(comp, p)];
+  }
+  const int t = ctype(comp);
+  step_boundaries(s, t);
+  if (t == T_D) {
+    update_eh(s, T_E);
+    step_boundaries(s, T_E);
+  }
+  if (t == T_B) {
+    update_eh(s, T_H);
+    step_boundaries(s, T_H);
+  }
+  return 0;
+}
+
 int orc_add_custom_point_source(orc_sim *s, int comp,
                                 void (*func)(double, void *, double *, double *), void *data,
                                 double start_time, double end_time, const double pos[3],

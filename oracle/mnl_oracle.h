@@ -40,6 +40,9 @@ int orc_add_custom_point_source(orc_sim *s, int comp,
                                 double start_time, double end_time, const double pos[3],
                                 double amp_re, double amp_im, int is_integrated);
 int orc_require_component(orc_sim *s, int comp);
+/* fields::initialize_field (src/initialize.cpp:135-161), func's real values as a
+ * whole-cell array */
+int orc_initialize_field(orc_sim *s, int comp, const double *vals);
 int orc_step(orc_sim *s, int nsteps);
 int orc_get_field(orc_sim *s, int comp, const double pos[3], double *out);
 int orc_copy_component(orc_sim *s, int comp, double *out, size_t n);

@@ -54,6 +54,7 @@ def lib():
         L.orc_add_point_source.argtypes = [c_void, c_int, c_int, dptr, c_int, dptr, c_double,
                                            c_double, c_int]
         L.orc_require_component.argtypes = [c_void, c_int]
+        L.orc_initialize_field.argtypes = [c_void, c_int, dptr]
         L.orc_step.argtypes = [c_void, c_int]
         L.orc_get_field.argtypes = [c_void, c_int, dptr, dptr]
         L.orc_copy_component.argtypes = [c_void, c_int, dptr, ctypes.c_size_t]
@@ -249,6 +250,15 @@ class Oracle:
 
     def require_component(self, comp):
         _chk(lib().orc_require_component(self.h, comp))
+
+    def initialize_field(self, comp, values):
+        """fields::initialize_field (src/initialize.cpp:135-161); values: whole-cell
+        array (or callable over coords(comp)), real part."""
+        if callable(values):
+            values = values(*self.coords(comp))
+        v = np.ascontiguousarray(np.real(np.broadcast_to(values, self.shape())),
+                                 dtype=np.float64).ravel()
+        _chk(lib().orc_initialize_field(self.h, comp, _dp(v)))
 
     def step(self, n=1):
         _chk(lib().orc_step(self.h, int(n)))

@@ -81,6 +81,9 @@ class ProductSim:
     def require_component(self, c):
         self._fields().require_component(c)
 
+    def initialize_field(self, c, values):
+        self._fields().initialize_field(c, values)
+
     def step(self, n=1):
         self._fields().step(n)
 
@@ -198,6 +201,10 @@ class GroupSim(ProductSim):
     def require_component(self, c):
         for f in self._all():
             f.require_component(c)
+
+    def initialize_field(self, c, values):  # collective (ghost exchange)
+        self._all()
+        self._par(lambda f: f.initialize_field(c, values))
 
     def step(self, n=1):
         self._all()
@@ -393,6 +400,46 @@ def sc_nr_isrc_seam(make, steps=30):
     o.legacy_point_source(0, 0.5, 0.5, 0.0, 3.0, (0.05, 0.05, -0.6), 5.0)
     o.legacy_point_source(2, 0.45, 0.5, 0.0, 3.0, (0.0, 0.0, -0.57), 4.0)
     o.legacy_point_source(1, 0.4, 0.5, 0.0, 3.0, (-0.03, 0.02, -0.61), 3.0)
+    o.step(steps)
+    return o
+
+
+def random_init(o, comps, seed=7, scale=1.0):
+    """Seeded random initial fields through initialize_field (src/initialize.cpp:
+    135-161) -- every tile, z chunk, PML region and wall of the grid carries data
+    from the first step on."""
+    for c in comps:
+        rng = np.random.default_rng(seed + 31 * c)
+        o.initialize_field(c, scale * rng.standard_normal(o.shape()))
+
+
+def sc_random_fields(make, sizes=(3.2, 3.2, 3.2), steps=12, dpml=1.0, eps=None, comps=(6, 7, 8, 9, 10, 11),
+                     kerr_lorentz=False, source=True):
+    """Random D and B everywhere (then E, H from them as the reference's
+    initialize_field does), optional dielectric core or Kerr + Lorentzian slab,
+    PML, a Gaussian source; stepped."""
+    o = vol(make, 3, list(sizes), 10, center_origin=True)
+    if dpml:
+        o.add_pml(dpml)
+    if kerr_lorentz:  # BASELINE configs[3]: |z| < 2 eps 2.25, chi3 1e-2, Lorentzian(1.1, 0.05, 0.5)
+        sig = []
+        for c in E_COMPS:
+            x, y, z = o.coords(c)
+            inside = np.abs(z) < 2.0
+            o.set_chi1inv(c, c, np.where(inside, 1 / 2.25, 1.0))
+            o.set_chi3(c, np.where(inside, 1e-2, 0.0))
+            sig.append(np.where(inside, 0.5, 0.0))
+        o.add_lorentzian(1.1, 0.05, sig)
+    elif eps:
+        for c in E_COMPS:
+            x, y, z = o.coords(c)
+            o.set_chi1inv(c, c, np.where((np.abs(y) < 0.5) & (np.abs(z) < 0.5), 1.0 / eps, 1.0))
+    if source:
+        if kerr_lorentz:
+            o.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -3.0), 50.0)
+        else:
+            o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    random_init(o, comps)
     o.step(steps)
     return o
 
