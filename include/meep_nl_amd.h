@@ -182,6 +182,16 @@ int mnl_fields_require_component(mnl_fields *f, int comp);
  * last step): fails with "meep: simulation fields are NaN or Inf". */
 int mnl_fields_step(mnl_fields *f, int nsteps);
 int mnl_fields_set_nan_check(mnl_fields *f, int every);
+/* Field energy over the box [vmin, vmax] (NULL, NULL: the whole cell,
+ * user_volume.surroundings()), src/energy_and_flux.cpp:48-178:
+ * which 0 = electric_energy_in_box (sum over E comps of 1/2 integral E.D),
+ * 1 = magnetic_energy_in_box (1/2 integral H.B with the current B, H),
+ * 2 = field_energy_in_box (electric + magnetic of B, H synchronized to E's
+ * time: one extra B half step averaged in and restored).  Integration on each
+ * component's Yee grid with loop_in_chunks weights; device reduction
+ * (compensated), per reference chunk.  Collective. */
+int mnl_fields_energy_in_box(mnl_fields *f, int which, const double vmin[3], const double vmax[3],
+                             double *out);
 /* fields::initialize_field(c, func) (src/initialize.cpp:135-161) with the
  * function evaluated by the caller: host = real part of func at every point of
  * component c in the whole-cell layout (n >= cell size).  Adds it to the

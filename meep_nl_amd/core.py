@@ -305,6 +305,31 @@ class Fields:
         t, dt = self._time()
         return float(np.float32(t * dt))
 
+    # -- energy (src/energy_and_flux.cpp:48-178)
+    def _energy(self, which, vmin=None, vmax=None):
+        out = ctypes.c_double()
+        lo = None if vmin is None else np.ascontiguousarray(vmin, dtype=np.float64)
+        hi = None if vmax is None else np.ascontiguousarray(vmax, dtype=np.float64)
+        check(lib().mnl_fields_energy_in_box(self.h, which, ptr(lo), ptr(hi), ctypes.byref(out)))
+        return out.value
+
+    def electric_energy_in_box(self, vmin=None, vmax=None):
+        """fields::electric_energy_in_box: sum over E comps of (1/2) integral E.D."""
+        return self._energy(0, vmin, vmax)
+
+    def magnetic_energy_in_box(self, vmin=None, vmax=None):
+        """fields::magnetic_energy_in_box with the current (unsynchronized) B, H."""
+        return self._energy(1, vmin, vmax)
+
+    def field_energy_in_box(self, vmin=None, vmax=None):
+        """fields::field_energy_in_box: electric + magnetic energy of B / H
+        synchronized to E's time (synchronize_magnetic_fields)."""
+        return self._energy(2, vmin, vmax)
+
+    def field_energy(self):
+        """fields::field_energy (src/energy_and_flux.cpp:48): the whole cell."""
+        return self._energy(2)
+
     # -- monitors
     def get_field(self, comp, pos):
         pos = np.ascontiguousarray(list(pos) + [0.0] * (3 - len(pos)), dtype=np.float64)

@@ -412,8 +412,15 @@ int build_pml_tables(mnl_fields *F) {
       if (z.zone == 0) nlo = 1;
       if (z.zone == 2) nhi = 1;
     }
-    if ((nlo || nhi) && ivs.size() < size_t(1 + nlo + nhi))
-      return fail("PML layers overlap (2*int(thickness*a+1.5) > cells along a direction)");
+    {  // PML chunks may touch (no interior chunk along d) but not overlap
+      int lo_end = -1, hi_start = INT32_MAX;
+      for (auto &z : ivs) {
+        if (z.zone == 0) lo_end = z.c1;
+        if (z.zone == 2) hi_start = z.c0;
+      }
+      if (nlo && nhi && lo_end > hi_start)
+        return fail("PML layers overlap (2*int(thickness*a+1.5) > cells along a direction)");
+    }
     for (auto &z : ivs) {
       // chunk-local profile, chunk io_c = io + c0, n_c = (c1-c0)/2
       int io_c = S.io[d] + z.c0, big_c = S.io[d] + z.c1;
@@ -3132,6 +3139,269 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   return 0;
 }
 
+// ------------------------------------------------------------- field energy
+// loop_in_chunks(where, cgrid = component c) (src/loop_in_chunks.cpp:325-520,
+// no symmetry / Bloch): the reference chunks' boxes on c's Yee grid with their
+// boundary weights, restricted to the points this rank owns; weights tabulated
+// per device axis into wtab.
+std::vector<EBox> energy_boxes(mnl_fields *F, int c, const double wmin[3], const double wmax[3],
+                               std::vector<double> &wtab) {
+  const mnl_structure &S = F->S;
+  const DevGrid &g = F->g;
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    const int iyc = 1 - S.shift(c, d);        // iyee_shift(Centered) - iyee_shift(c)
+    const double yc = iyc * (0.5 / S.a);      // yee_shift(Centered) - yee_shift(c)
+    is[d] = 1 + 2 * int(floor((wmin[d] + yc) * S.a - .5)) - iyc;  // vec2diel_floor - iyee_c
+    ie[d] = 1 + 2 * int(ceil((wmax[d] + yc) * S.a - .5)) - iyc;
+  }
+  double s0[3], s1[3], e0[3], e1[3];
+  dft_boundary_weights(S, wmin, wmax, is, ie, s0, e0, s1, e1);
+  double dV0 = 1.0;
+  for (int d = 0; d < 3; d++)
+    if (S.has[d] && wmax[d] - wmin[d] > 0.0) dV0 *= 1.0 / S.a;
+  int yd[3];
+  if (S.dim == 2)
+    yd[0] = 2, yd[1] = 0, yd[2] = 1;
+  else
+    yd[0] = 0, yd[1] = 1, yd[2] = 2;
+  std::vector<EBox> out;
+  for (auto &ch : reference_chunks(S)) {
+    int isc[3], iec[3];
+    double s0c[3], s1c[3], e0c[3], e1c[3];
+    bool emp = false;
+    for (int d = 0; d < 3; d++) {
+      s0c[d] = s1c[d] = e0c[d] = e1c[d] = 1.0;
+      if (!S.has[d]) {
+        isc[d] = iec[d] = 0;
+        continue;
+      }
+      const int sh = S.shift(c, d);
+      const int uoc = S.io[d] + 2 - sh, coc = ch[d] + 2 - sh, cbo = ch[d] + 2 * ch[3 + d] - sh;
+      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
+      isc[d] = std::max(is[d], iscoS);
+      iec[d] = std::min(ie[d], iecoS);
+      if (isc[d] > iec[d]) emp = true;
+    }
+    if (emp) continue;
+    for (int d = 0; d < 3; d++) {
+      if (!S.has[d]) continue;
+      if (isc[d] == is[d]) {
+        s0c[d] = s0[d];
+        s1c[d] = s1[d];
+      } else if (isc[d] == is[d] + 2) {
+        s0c[d] = s1[d];
+      }
+      if (iec[d] == ie[d]) {
+        e0c[d] = e0[d];
+        e1c[d] = e1[d];
+      } else if (iec[d] == ie[d] - 2) {
+        e0c[d] = e1[d];
+      }
+      if (iec[d] == isc[d]) {
+        double w = std::min(s0c[d], e0c[d]);
+        s0c[d] = e0c[d] = s1c[d] = e1c[d] = w;
+      } else if (iec[d] == isc[d] + 2) {
+        double w = std::min(s0c[d], e1c[d]);
+        s0c[d] = w, e1c[d] = w;
+        w = std::min(s1c[d], e0c[d]);
+        s1c[d] = w, e0c[d] = w;
+      } else if (iec[d] == isc[d] + 4) {
+        double w = std::min(s1c[d], e1c[d]);
+        s1c[d] = w, e1c[d] = w;
+      }
+    }
+    EBox b;
+    bool none = false;
+    for (int k = 0; k < 3; k++) b.dlo[k] = 0, b.dn[k] = 1, b.wofs[k] = 0, b.yd[k] = yd[k];
+    b.dV0 = dV0 + 0.0 * 0;  // dV0 + dV1 * loop_i2 with dV1 = 0
+    for (int d = 0; d < 3; d++) {
+      if (!S.has[d]) continue;
+      const int ax = g.ax[d], sh = S.shift(c, d);
+      const long nl = (iec[d] - isc[d]) / 2 + 1;           // chunk loop count
+      const int j0 = (isc[d] - S.io[d] - sh) / 2 - g.off[d];  // local index of loop point 0
+      const int lo_own = sh ? g.owned_lo_sh[d] : g.owned_lo_un[d];
+      const int hi_own = sh ? g.owned_hi_sh[d] : g.owned_hi_un[d];
+      int a = std::max(0, lo_own - j0), z = std::min<long>(nl - 1, hi_own - j0);
+      if (z < a) {
+        none = true;
+        break;
+      }
+      b.dlo[ax] = j0 + a;
+      b.dn[ax] = z - a + 1;
+      b.wofs[ax] = (long long)wtab.size();
+      for (long i = a; i <= z; i++) {
+        double w = 1.0;
+        if (!(i > 1 && i < nl - 2))
+          w = i == 0 ? s0c[d] : (i == 1 ? s1c[d] : i == nl - 1 ? e0c[d] : (i == nl - 2 ? e1c[d] : 1.0));
+        wtab.push_back(w);
+      }
+    }
+    if (!none) out.push_back(b);
+    else out.push_back(EBox{{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {yd[0], yd[1], yd[2]}, dV0});
+  }
+  return out;
+}
+
+// real(integrate(2, {A, B}, dot_integrand, where)) over component c's grid:
+// per reference chunk a device sum (rounded to double, as the reference adds
+// each chunk's long-double sum into a complex<double>), chunks added in order,
+// then summed over ranks (sum_to_all)
+int integrate_pair(mnl_fields *F, int c, const double *A, const double *Asep, const double *Bv,
+                   const double wmin[3], const double wmax[3], double *out) {
+  std::vector<double> wtab;
+  auto boxes = energy_boxes(F, c, wmin, wmax, wtab);
+  const int NB = 256;
+  double *dw = nullptr, *dp = nullptr;
+  HIPCHK(hipMalloc(&dw, std::max<size_t>(wtab.size(), 1) * 8));
+  HIPCHK(hipMalloc(&dp, 2 * NB * 8));
+  std::unique_ptr<void, void (*)(void *)> g1(dw, [](void *p) { (void)hipFree(p); });
+  std::unique_ptr<void, void (*)(void *)> g2(dp, [](void *p) { (void)hipFree(p); });
+  if (!wtab.empty())
+    HIPCHK(hipMemcpyAsync(dw, wtab.data(), wtab.size() * 8, hipMemcpyHostToDevice, F->stream));
+  std::vector<double> chunk(boxes.size(), 0.0), part(2 * NB);
+  for (size_t k = 0; k < boxes.size(); k++) {
+    const EBox &b = boxes[k];
+    const long long n = (long long)b.dn[0] * b.dn[1] * b.dn[2];
+    if (n == 0 || !A || !Bv) continue;
+    const int nb = (int)std::min<long long>(NB, (n + 255) / 256);
+    if (k_energy(A, Asep, Bv, F->g, F->f, ctype(c), cdir(c), b, dw, dp, nb, F->stream))
+      return fail("energy kernel launch failed");
+    HIPCHK(hipMemcpyAsync(part.data(), dp, 2 * nb * 8, hipMemcpyDeviceToHost, F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+    long double acc = 0.0L;
+    for (int i = 0; i < nb; i++) acc += (long double)part[2 * i] + (long double)part[2 * i + 1];
+    chunk[k] = (double)acc;
+  }
+  if (F->nranks > 1) {
+    if (F->comm->agree_ok(true, F->stream)) return fail("energy: a rank failed");
+    if (F->comm->allreduce_sum(chunk.data(), (int)chunk.size(), F->stream))
+      return fail("energy allreduce failed");
+  }
+  double sum = 0.0;
+  for (double v : chunk) sum += v;
+  *out = sum;
+  return 0;
+}
+
+// fields::field_energy_in_box(c, where) for every E (or H) component, summed
+// in long double (electric_energy_in_box / magnetic_energy_in_box,
+// src/energy_and_flux.cpp:85-95)
+int energy_of_type(mnl_fields *F, int t, const double wmin[3], const double wmax[3], double *out) {
+  long double sum = 0.0L;
+  const DevFields &f = F->f;
+  for (int d = 0; d < 3; d++) {
+    const int c = 3 * t + d;
+    if (!has_field(F->S, c)) continue;
+    double v = 0.0;
+    if (t == T_E) {
+      if (!F->allocated[c] || !F->allocated[3 * T_D + d]) continue;
+      if (integrate_pair(F, c, f.E[d], nullptr, f.D[d], wmin, wmax, &v)) return -1;
+    } else {
+      if (!F->allocated[3 * T_B + d]) continue;
+      const double *hsep = (F->h_first_done && f.H[d]) ? f.H[d] : nullptr;
+      if (integrate_pair(F, c, f.B[d], hsep, f.B[d], wmin, wmax, &v)) return -1;
+    }
+    sum += v * 0.5;
+  }
+  *out = (double)sum;
+  return 0;
+}
+
+// synchronize_magnetic_fields (src/energy_and_flux.cpp:146-167): back up B / H
+// (and f_u, f_w, f_cond where they exist), take one B half step (step_db(B),
+// B sources at time(), step_boundaries, update_eh(H)), average B and H with the
+// backups; restore_magnetic_fields (169-178) copies the backups back.
+struct MagBackup {
+  std::vector<std::pair<double *, double *>> items;  // (field array, backup)
+  std::vector<std::pair<double *, double *>> avg;    // averaged with backup
+  ~MagBackup() {
+    for (auto &it : items) (void)hipFree(it.second);
+  }
+};
+
+int sync_magnetic(mnl_fields *F, MagBackup &bk) {
+  if (F->src_dirty && build_source_lists(F)) return -1;
+  if (F->fused && set_fused(F, false)) return -1;
+  DevFields &f = F->f;
+  const size_t n = F->nlocal;
+  auto save = [&](double *p, bool average) -> int {
+    if (!p) return 0;
+    double *b = nullptr;
+    HIPCHK(hipMalloc(&b, n * 8));
+    HIPCHK(hipMemcpyAsync(b, p, n * 8, hipMemcpyDeviceToDevice, F->stream));
+    bk.items.push_back({p, b});
+    if (average) bk.avg.push_back({p, b});
+    return 0;
+  };
+  const bool have_u = F->u_first_done[0], have_h = F->h_first_done;
+  for (int d = 0; d < 3; d++) {
+    if (!F->allocated[3 * T_B + d]) continue;
+    if (save(f.B[d], true)) return -1;
+    if (have_u && (save(f.UB[d], false) || save(f.fcnd[0][d], false))) return -1;
+    if (have_h && (save(f.H[d], true) || save(f.WH[d], false))) return -1;
+  }
+  // one B step at time(): step_db(B) + step_source(B) + step_boundaries(B) +
+  // update_eh(H) + step_boundaries(H)
+  if (F->nranks > 1 && exchange(F, 0)) return fail("E halo exchange failed");
+  if (!F->u_first_done[0] && u_lazy_copy(F, 0)) return -1;
+  const DevGrid &g = F->g;
+  if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream) ||
+      k_curl(T_B, F->interior, &F->shell_list, g, f, F->planB, F->S.courant, F->stream, false))
+    return fail("curl B launch failed");
+  const size_t nB = F->srcB_idx.size();
+  if (nB) {
+    const double dt = F->dt, time = F->t * dt;
+    for (auto &st : F->srcs) st.update(time, dt);
+    std::vector<double> vB(nB);
+    for (size_t k = 0; k < nB; k++) {
+      const SrcGroup &G = F->groups[F->srcB_ref[k].first];
+      vB[k] = real((G.amp[F->srcB_ref[k].second] * F->srcs[G.st].cur_current) * dt);
+    }
+    double *dv = nullptr;
+    HIPCHK(hipMalloc(&dv, nB * 8));
+    std::unique_ptr<void, void (*)(void *)> gv(dv, [](void *p) { (void)hipFree(p); });
+    HIPCHK(hipMemcpyAsync(dv, vB.data(), nB * 8, hipMemcpyHostToDevice, F->stream));
+    SrcDev sB{(int)nB, F->d_srcB_idx, F->d_srcB_comp, dv};
+    if (k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
+    HIPCHK(hipStreamSynchronize(F->stream));
+  }
+  if (!F->h_first_done && h_lazy_copy(F)) return -1;
+  bool anyH = false;
+  for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
+  if (anyH && k_update_h(F->shell_list, g, f, F->stream)) return fail("update H launch failed");
+  if (F->nranks > 1 && exchange(F, 1)) return fail("H halo exchange failed");
+  for (auto &a : bk.avg)
+    if (k_average(a.first, a.second, (long long)n, F->stream)) return fail("average launch failed");
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+int restore_magnetic(mnl_fields *F, MagBackup &bk) {
+  for (auto &it : bk.items)
+    HIPCHK(hipMemcpyAsync(it.first, it.second, F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+// which: 0 electric_energy_in_box, 1 magnetic_energy_in_box (current B / H),
+// 2 field_energy_in_box (electric + magnetic of the synchronized B / H)
+int energy_in_box(mnl_fields *F, int which, const double wmin[3], const double wmax[3],
+                  double *out) {
+  if (F->fused && set_fused(F, false)) return -1;  // materialise implicit E
+  if (which == 0) return energy_of_type(F, T_E, wmin, wmax, out);
+  if (which == 1) return energy_of_type(F, T_H, wmin, wmax, out);
+  MagBackup bk;
+  double mag = 0.0, el = 0.0;
+  if (sync_magnetic(F, bk)) return -1;
+  const int r = energy_of_type(F, T_H, wmin, wmax, &mag);
+  if (restore_magnetic(F, bk) || r) return -1;
+  if (energy_of_type(F, T_E, wmin, wmax, &el)) return -1;
+  *out = el + mag;
+  return 0;
+}
+
 // fields::step() n times: the NaN guard (src/step.cpp:138-139) every nan_every
 // steps; the first step after construction (or after E / H were set directly)
 // runs unfused (see e_first_done)
@@ -3600,6 +3870,19 @@ int mnl_fields_initialize_field(mnl_fields *F, int comp, const double *host, siz
   if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
   if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
   return initialize_field(F, comp, host);
+}
+
+int mnl_fields_energy_in_box(mnl_fields *F, int which, const double vmin[3], const double vmax[3],
+                             double *out) {
+  if (!F || !out || which < 0 || which > 2) return fail("bad argument");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  double lo[3], hi[3];
+  const mnl_structure &S = F->S;
+  for (int d = 0; d < 3; d++) {  // NULL: the whole cell (user_volume.surroundings())
+    lo[d] = S.has[d] ? (vmin ? vmin[d] : S.io[d] * (0.5 / S.a)) : 0.0;
+    hi[d] = S.has[d] ? (vmax ? vmax[d] : (S.io[d] + 2 * S.n[d]) * (0.5 / S.a)) : 0.0;
+  }
+  return energy_in_box(F, which, lo, hi, out);
 }
 
 int mnl_fields_set_nan_check(mnl_fields *F, int every) {

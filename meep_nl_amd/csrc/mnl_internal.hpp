@@ -125,6 +125,17 @@ struct DevFields {
   int aniso;                 // some susceptibility has off-diagonal sigma
 };
 
+// One reference chunk's integration box on a component grid (field energy):
+// device-axis start / count on this rank, per-axis weight-table offsets, the
+// yucky direction order of IVEC_LOOP_WEIGHT, and dV0.
+struct EBox {
+  int dlo[3];
+  int dn[3];
+  long long wofs[3];
+  int yd[3];
+  double dV0;
+};
+
 // Point sources in rank-local linear indices.
 struct SrcDev {
   int n;
@@ -270,6 +281,10 @@ int k_dft_accum(const int *pj, const int *pch, double *dft, const double *fr, in
 int k_init_add(double *dst, double *alt, const double *src, const DevGrid &g, const DevFields &f,
                int comp_type, int comp_dir, void *stream);
 int k_copy(double *dst, const double *src, long long n, void *stream);
+int k_average(double *f, const double *bk, long long n, void *stream);
+int k_energy(const double *A, const double *Asep, const double *Bv, const DevGrid &g,
+             const DevFields &f, int type, int c, const EBox &box, const double *wt,
+             double *partial, int nblocks, void *stream);
 int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_type,
                      int comp_dir, int zlo_glob, void *stream);
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,

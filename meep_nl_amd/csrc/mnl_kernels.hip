@@ -2348,6 +2348,93 @@ __global__ void init_add_kernel(double *dst, double *alt, const double *src, Dev
   t[li] = wall ? 0.0 : t[li] + src[cidx];
 }
 
+// ------------------------------------------------------------- energy
+// fields::field_energy_in_box(c, where) (src/energy_and_flux.cpp:67-83) ->
+// integrate(2, {Ec, Dc} or {Hc, Bc}) on c's own Yee grid (src/integrate.cpp:
+// 46-129): per point fv = 0.25 * (((f + f) + f) + f) of each field (offsets 0
+// on a component grid), term = (fv0 * fv1) * IVEC_LOOP_WEIGHT.  One launch per
+// reference chunk box; every thread accumulates its terms with TwoSum
+// compensation, the workgroup combines (s, c) pairs in LDS and writes one pair.
+__device__ __forceinline__ void two_sum(double a, double b, double &s, double &e) {
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+
+__global__ __launch_bounds__(256) void energy_kernel(const double *A, const double *Asep,
+                                                     const double *Bv, DevGrid g, DevFields f,
+                                                     int type, int c, EBox box, const double *wt,
+                                                     double *partial) {
+  __shared__ double ls[256], lc[256];
+  const long long n0 = box.dn[0], n1 = box.dn[1], n2 = box.dn[2];
+  const long long ntot = n0 * n1 * n2;
+  double s = 0.0, comp = 0.0;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < ntot;
+       q += (long long)gridDim.x * 256) {
+    const long long a0 = q % n0, r = q / n0, a1 = r % n1, a2 = r / n1;
+    const long long ia[3] = {a0, a1, a2};
+    Pt p;
+    long long li = 0;
+    double w[3];
+    for (int d = 0; d < 3; d++) {
+      const int ax = g.ax[d];
+      w[d] = 1.0;
+      p.j[d] = 0;
+      if (ax < 0) continue;
+      p.j[d] = box.dlo[ax] + (int)ia[ax];
+      li += (long long)p.j[d] * g.st[ax];
+      w[d] = wt[box.wofs[ax] + ia[ax]];
+    }
+    // IVEC_LOOP_WEIGHT order: W(yd[2]) * (W(yd[1]) * (dV * W(yd[0])))
+    const double wgt = w[box.yd[2]] * (w[box.yd[1]] * (box.dV0 * w[box.yd[0]]));
+    const double *src = A;
+    if (Asep && pml_at(f, g, c, qcoord(g, p, type, c, c))) src = Asep;  // H separate here
+    const double x = src[li], y = Bv[li];
+    const double xv = 0.25 * (((x + x) + x) + x), yv = 0.25 * (((y + y) + y) + y);
+    const double t = (xv * yv) * wgt;
+    double ns, e;
+    two_sum(s, t, ns, e);
+    s = ns;
+    comp += e;
+  }
+  ls[threadIdx.x] = s;
+  lc[threadIdx.x] = comp;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) {
+      double ns, e;
+      two_sum(ls[threadIdx.x], ls[threadIdx.x + k], ns, e);
+      ls[threadIdx.x] = ns;
+      lc[threadIdx.x] = lc[threadIdx.x] + lc[threadIdx.x + k] + e;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = ls[0];
+    partial[2 * blockIdx.x + 1] = lc[0];
+  }
+}
+
+int k_energy(const double *A, const double *Asep, const double *Bv, const DevGrid &g,
+             const DevFields &f, int type, int c, const EBox &box, const double *wt,
+             double *partial, int nblocks, void *stream) {
+  energy_kernel<<<nblocks, 256, 0, (hipStream_t)stream>>>(A, Asep, Bv, g, f, type, c, box, wt,
+                                                          partial);
+  return rc();
+}
+
+// average_with_backup (src/energy_and_flux.cpp:136-144): f = 0.5 * (f + backup)
+__global__ void average_kernel(double *f, const double *bk, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = 0.5 * (f[i] + bk[i]);
+}
+
+int k_average(double *f, const double *bk, long long n, void *stream) {
+  if (n <= 0) return 0;
+  average_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(f, bk, n);
+  return rc();
+}
+
 // lazy allocation on the first update_eh (src/update_eh.cpp:204-216): H starts
 // as a copy of B, and the W auxiliary field as a copy of the field it shadows
 __global__ void copy_kernel(double *dst, const double *src, long long n) {

@@ -2222,9 +2222,200 @@ inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) 
   return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
 }
 
+// ---------------------------------------------------------------- field energy
+// loop_in_chunks(where, cgrid = c) (src/loop_in_chunks.cpp:325-520) restricted
+// to Cartesian grids without symmetry / Bloch, on component c's Yee grid.
+std::vector<SliceLoop> energy_loops(orc_sim *s, int c, const double wmin[3], const double wmax[3]) {
+  const GV &G = s->gv;
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!G.has[d]) continue;
+    const int iyc = 1 - G.shift(c, d);      // iyee_shift(Centered) - iyee_shift(c)
+    const double yc = iyc * (0.5 / G.a);    // wherec = where + yee_c
+    is[d] = 1 + 2 * int(floor((wmin[d] + yc) * G.a - .5)) - iyc;
+    ie[d] = 1 + 2 * int(ceil((wmax[d] + yc) * G.a - .5)) - iyc;
+  }
+  double s0[3], s1[3], e0[3], e1[3];
+  boundary_weights(G, wmin, wmax, is, ie, s0, e0, s1, e1);
+  std::vector<SliceLoop> out;
+  for (size_t ci = 0; ci < s->chunks.size(); ci++) {
+    const GV &g = s->chunks[ci].gv;
+    SliceLoop L;
+    L.ci = (int)ci;
+    bool empty = false;
+    for (int d = 0; d < 3; d++) {
+      L.s0[d] = L.s1[d] = L.e0[d] = L.e1[d] = 1.0;
+      if (!G.has[d]) {
+        L.is[d] = L.ie[d] = 0;
+        continue;
+      }
+      // little_owned_corner(c) = little + 2 - iyee_shift(c), big_owned_corner(c) =
+      // big - iyee_shift(c) (src/meep/vec.hpp:1102-1107)
+      const int sh = G.shift(c, d);
+      const int uoc = G.io[d] + 2 - sh, coc = g.io[d] + 2 - sh, cbo = g.big(d) - sh;
+      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
+      L.is[d] = std::max(is[d], iscoS);
+      L.ie[d] = std::min(ie[d], iecoS);
+      if (L.is[d] > L.ie[d]) empty = true;
+    }
+    if (empty) continue;
+    for (int d = 0; d < 3; d++) {
+      if (!G.has[d]) continue;
+      if (L.is[d] == is[d]) {
+        L.s0[d] = s0[d];
+        L.s1[d] = s1[d];
+      } else if (L.is[d] == is[d] + 2) {
+        L.s0[d] = s1[d];
+      }
+      if (L.ie[d] == ie[d]) {
+        L.e0[d] = e0[d];
+        L.e1[d] = e1[d];
+      } else if (L.ie[d] == ie[d] - 2) {
+        L.e0[d] = e1[d];
+      }
+      if (L.ie[d] == L.is[d]) {
+        double w = std::min(L.s0[d], L.e0[d]);
+        L.s0[d] = L.e0[d] = L.s1[d] = L.e1[d] = w;
+      } else if (L.ie[d] == L.is[d] + 2) {
+        double w = std::min(L.s0[d], L.e1[d]);
+        L.s0[d] = w, L.e1[d] = w;
+        w = std::min(L.s1[d], L.e0[d]);
+        L.s1[d] = w, L.e0[d] = w;
+      } else if (L.ie[d] == L.is[d] + 4) {
+        double w = std::min(L.s1[d], L.e1[d]);
+        L.s1[d] = w, L.e1[d] = w;
+      }
+    }
+    out.push_back(L);
+  }
+  return out;
+}
+
+// real(integrate(2, {c0, c1}, dot_integrand, 0, where)) on c0's grid
+// (src/integrate.cpp:46-201): complex<long double> sum per chunk, added into a
+// complex<double> chunk by chunk.
+double integrate_dot(orc_sim *s, int c0, int c1, const double wmin[3], const double wmax[3]) {
+  const GV &G = s->gv;
+  double dV0 = 1.0;
+  for (int d = 0; d < 3; d++)
+    if (G.has[d] && wmax[d] - wmin[d] > 0.0) dV0 *= G.inva;
+  const int yd[3] = {G.dim == 2 ? 2 : 0, G.dim == 2 ? 0 : 1, G.dim == 2 ? 1 : 2};
+  cplx total = 0.0;
+  for (auto &L : energy_loops(s, c0, wmin, wmax)) {
+    Chunk &ch = s->chunks[L.ci];
+    const GV &g = ch.gv;
+    const realnum *f0 = s->allocated[c0] ? ch.F(c0) : nullptr;
+    const realnum *f1 = s->allocated[c1] ? ch.F(c1) : nullptr;
+    int n[3];
+    for (int k = 0; k < 3; k++) n[k] = G.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
+    std::complex<long double> sum = 0.0;
+    for (int i1 = 0; i1 < n[0]; i1++)
+      for (int i2 = 0; i2 < n[1]; i2++)
+        for (int i3 = 0; i3 < n[2]; i3++) {
+          const int ii[3] = {i1, i2, i3};
+          int p[3] = {0, 0, 0};
+          for (int k = 0; k < 3; k++)
+            if (G.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
+          const long idx = g.index(c0, p);
+          double fv[2];
+          const realnum *fs[2] = {f0, f1};
+          for (int q = 0; q < 2; q++) {
+            const realnum *fp = fs[q];
+            fv[q] = fp ? 0.25 * (fp[idx] + fp[idx + 0] + fp[idx + 0] + fp[idx + 0 + 0]) : 0.0;
+          }
+          const cplx v0 = cplx(fv[0], 0.0) * cplx(1.0, 0.0), v1 = cplx(fv[1], 0.0) * cplx(1.0, 0.0);
+          const cplx integrand = real(conj(v0) * v1);
+          double w[3];
+          for (int k = 0; k < 3; k++) {
+            const int d = yd[k];
+            w[k] = loop_w1(L.s0[d], L.s1[d], L.e0[d], L.e1[d], ii[k], n[k]);
+          }
+          const double wt = w[2] * (w[1] * ((dV0 + 0.0 * i2) * w[0]));
+          sum += integrand * wt;
+        }
+    total += sum;
+  }
+  return real(total);
+}
+
+// fields::field_energy_in_box(c, where) (src/energy_and_flux.cpp:67-83)
+double energy_c(orc_sim *s, int c, const double wmin[3], const double wmax[3]) {
+  const int d = cdir(c);
+  if (ctype(c) == T_E || ctype(c) == T_D) return integrate_dot(s, tcomp(T_E, d), tcomp(T_D, d), wmin, wmax) * 0.5;
+  return integrate_dot(s, tcomp(T_H, d), tcomp(T_B, d), wmin, wmax) * 0.5;
+}
+
+double energy_type(orc_sim *s, int t, const double wmin[3], const double wmax[3]) {
+  long double sum = 0.0;  // FOR_ELECTRIC_COMPONENTS / FOR_MAGNETIC_COMPONENTS
+  for (int d = 0; d < 3; d++) sum += energy_c(s, tcomp(t, d), wmin, wmax);
+  return (double)sum;
+}
+
+struct ChunkBackup {
+  std::vector<realnum> *dst;
+  std::vector<realnum> copy;
+  bool average;
+};
+
+// synchronize_magnetic_fields (src/energy_and_flux.cpp:146-167): backup_component
+// of every B and H (f, f_u, f_w, f_cond where they exist; H only when not
+// aliased to B), one B step, average f with the backups
+std::vector<ChunkBackup> sync_magnetic(orc_sim *s) {
+  std::vector<ChunkBackup> bk;
+  for (auto &ch : s->chunks)
+    for (int t : {T_B, T_H})
+      for (int d = 0; d < 3; d++) {
+        const int c = tcomp(t, d);
+        if (t == T_H && ch.h_alias[d]) continue;  // H == B: nothing of its own
+        if (ch.f[c].empty()) continue;
+        bk.push_back({&ch.f[c], ch.f[c], true});
+        for (auto *v : {&ch.fu[c], &ch.fw[c], &ch.fcond[c]})
+          if (!v->empty()) bk.push_back({v, *v, false});
+      }
+  const double time = s->t * s->dt;
+  calc_sources(s, time);
+  step_db(s, T_B);
+  step_source(s, T_B);
+  step_boundaries(s, T_B);
+  calc_sources(s, time + 0.5 * s->dt);
+  update_eh(s, T_H);
+  step_boundaries(s, T_H);
+  for (auto &b : bk)
+    if (b.average)
+      for (size_t i = 0; i < b.copy.size(); i++) (*b.dst)[i] = 0.5 * ((*b.dst)[i] + b.copy[i]);
+  return bk;
+}
+
+void restore_magnetic(std::vector<ChunkBackup> &bk) {  // src/energy_and_flux.cpp:169-178
+  for (auto &b : bk)
+    if (b.dst->size() == b.copy.size()) *b.dst = b.copy;
+}
+
 }  // namespace
 
 extern "C" {
+int orc_energy_in_box(orc_sim *s, int which, const double vmin[3], const double vmax[3],
+                      double *out) {
+  finalize(s);
+  const GV &G = s->gv;
+  double lo[3], hi[3];
+  for (int d = 0; d < 3; d++) {  // NULL: gv.surroundings()
+    lo[d] = G.has[d] ? (vmin ? vmin[d] : G.io[d] * (0.5 * G.inva)) : 0.0;
+    hi[d] = G.has[d] ? (vmax ? vmax[d] : (G.io[d] + 2 * G.n[d]) * (0.5 * G.inva)) : 0.0;
+  }
+  if (which == 0) {
+    *out = energy_type(s, T_E, lo, hi);
+  } else if (which == 1) {
+    *out = energy_type(s, T_H, lo, hi);
+  } else {
+    auto bk = sync_magnetic(s);
+    const double mag = energy_type(s, T_H, lo, hi);
+    restore_magnetic(bk);
+    *out = energy_type(s, T_E, lo, hi) + mag;
+  }
+  return 0;
+}
+
 int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3], int snap,
                     int *rank, long long dims[3], double *out, long long nout) {
   finalize(s);

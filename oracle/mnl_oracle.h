@@ -55,6 +55,11 @@ int orc_set_upstream_nl(orc_sim *s, int on);
  * in X,Y,Z order) may be NULL to query the size only. */
 int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3], int snap,
                     int *rank, long long dims[3], double *out, long long nout);
+/* fields::electric_energy_in_box (which 0), magnetic_energy_in_box (1),
+ * field_energy_in_box (2, synchronized B / H) over [vmin, vmax] (NULL: the
+ * whole cell), src/energy_and_flux.cpp:48-178 */
+int orc_energy_in_box(orc_sim *s, int which, const double vmin[3], const double vmax[3],
+                      double *out);
 long long orc_t(orc_sim *s);
 double orc_dt(orc_sim *s);
 size_t orc_ntot(orc_sim *s);

@@ -55,6 +55,7 @@ def lib():
                                            c_double, c_int]
         L.orc_require_component.argtypes = [c_void, c_int]
         L.orc_initialize_field.argtypes = [c_void, c_int, dptr]
+        L.orc_energy_in_box.argtypes = [c_void, c_int, dptr, dptr, dptr]
         L.orc_step.argtypes = [c_void, c_int]
         L.orc_get_field.argtypes = [c_void, c_int, dptr, dptr]
         L.orc_copy_component.argtypes = [c_void, c_int, dptr, ctypes.c_size_t]
@@ -262,6 +263,26 @@ class Oracle:
 
     def step(self, n=1):
         _chk(lib().orc_step(self.h, int(n)))
+
+    def _energy(self, which, vmin=None, vmax=None):
+        out = ctypes.c_double()
+        lo = None if vmin is None else np.ascontiguousarray(vmin, dtype=np.float64)
+        hi = None if vmax is None else np.ascontiguousarray(vmax, dtype=np.float64)
+        _chk(lib().orc_energy_in_box(self.h, which, _dp(lo), _dp(hi), ctypes.byref(out)))
+        return out.value
+
+    def electric_energy_in_box(self, vmin=None, vmax=None):
+        return self._energy(0, vmin, vmax)
+
+    def magnetic_energy_in_box(self, vmin=None, vmax=None):
+        return self._energy(1, vmin, vmax)
+
+    def field_energy_in_box(self, vmin=None, vmax=None):
+        return self._energy(2, vmin, vmax)
+
+    def field_energy(self):
+        """fields::field_energy (src/energy_and_flux.cpp:48): the whole cell."""
+        return self._energy(2)
 
     @property
     def t(self):

@@ -84,6 +84,18 @@ class ProductSim:
     def initialize_field(self, c, values):
         self._fields().initialize_field(c, values)
 
+    def field_energy(self):
+        return self._fields().field_energy()
+
+    def electric_energy_in_box(self, vmin=None, vmax=None):
+        return self._fields().electric_energy_in_box(vmin, vmax)
+
+    def magnetic_energy_in_box(self, vmin=None, vmax=None):
+        return self._fields().magnetic_energy_in_box(vmin, vmax)
+
+    def field_energy_in_box(self, vmin=None, vmax=None):
+        return self._fields().field_energy_in_box(vmin, vmax)
+
     def step(self, n=1):
         self._fields().step(n)
 
@@ -205,6 +217,24 @@ class GroupSim(ProductSim):
     def initialize_field(self, c, values):  # collective (ghost exchange)
         self._all()
         self._par(lambda f: f.initialize_field(c, values))
+
+    def _energy_all(self, name, *a):  # collective: every rank returns the summed energy
+        self._all()
+        vals = self._par(lambda f: getattr(f, name)(*a))
+        assert all(v == vals[0] for v in vals)
+        return vals[0]
+
+    def field_energy(self):
+        return self._energy_all("field_energy")
+
+    def electric_energy_in_box(self, vmin=None, vmax=None):
+        return self._energy_all("electric_energy_in_box", vmin, vmax)
+
+    def magnetic_energy_in_box(self, vmin=None, vmax=None):
+        return self._energy_all("magnetic_energy_in_box", vmin, vmax)
+
+    def field_energy_in_box(self, vmin=None, vmax=None):
+        return self._energy_all("field_energy_in_box", vmin, vmax)
 
     def step(self, n=1):
         self._all()
@@ -442,6 +472,69 @@ def sc_random_fields(make, sizes=(3.2, 3.2, 3.2), steps=12, dpml=1.0, eps=None, 
     random_init(o, comps)
     o.step(steps)
     return o
+
+
+def legacy_last_time(freq, width, peaktime, cutoff, a, dt, t=0, magnetic=False):
+    """last_source_time() of fields::add_point_source(c, freq, width, peaktime,
+    cutoff, ...) (src/sources.cpp:189-211 -> gaussian_src_time, src/meep.hpp:1024)."""
+    width = width / freq
+    cutoff = (1.0 / a) + cutoff * width
+    if peaktime <= 0.0:
+        peaktime = t * dt + cutoff
+    peaktime += (-dt * 0.5) if magnetic else dt
+    st, et = peaktime - cutoff, peaktime + cutoff
+    peak, cut = 0.5 * (st + et), (et - st) * 0.5
+    while math.exp(-cut * cut / (2 * width * width)) < 1e-100:
+        cut *= 0.9
+    return float(np.float32(peak + float(np.float32(cut))))
+
+
+def three_d_test_pml(make, energy_every=None):
+    """tests/three_d.cpp:163-194 (test_pml): vol3d(1.5, 1.0, 1.2) @ 10, pml(0.401),
+    vacuum, Ez point source (0.8, 0.6, 0, 4) at (0.751, 0.5, 0.601); after the
+    source, the field energy must fall below 4e-3 of its value within every 10
+    time units up to 31.  Returns (sim, last_energy, [(time, energy)])."""
+    o = make(3, [15, 10, 12], 10.0, 0.5, [0, 0, 0])
+    o.add_pml(0.401)
+    o.legacy_point_source(2, 0.8, 0.6, 0.0, 4.0, (0.751, 0.5, 0.601), 1.0)
+    ts = legacy_last_time(0.8, 0.6, 0.0, 4.0, 10.0, 0.05)
+    while o.time() < ts:
+        o.step()
+    last = o.field_energy()
+    out, check = [], 10.0
+    while o.time() < 3.1 * 10.0:
+        o.step()
+        if o.time() >= check:
+            out.append((o.time(), o.field_energy()))
+            check += 10.0
+    return o, last, out
+
+
+def three_d_test_pml_splitting(make):
+    """tests/three_d.cpp:196-224 (test_pml_splitting) on one side: vol3d(1.5, 1.0,
+    1.2) @ 10, pml(0.3), Ez point source (0.8, 1.6, 0, 4) at (1.099, 0.499, 0.501),
+    stepped to t = 31 with field_energy() whenever time() passes 10, 20, 30.
+    Returns (sim, [(step, energy)], [probe values])."""
+    o = make(3, [15, 10, 12], 10.0, 0.5, [0, 0, 0])
+    o.add_pml(0.3)
+    o.legacy_point_source(2, 0.8, 1.6, 0.0, 4.0, (1.099, 0.499, 0.501), 1.0)
+    nxt, en, probes = 10.0, [], []
+    pts = [(0.5, 0.01, 1.0), (0.46, 0.33, 0.33), (1.0, 1.0, 0.33), (1.3, 0.3, 0.15)]
+    while o.time() < 31.0:
+        o.step()
+        if o.t % 25 == 0:
+            probes.append([o.get_field(2, p) for p in pts])
+        if o.time() > nxt:
+            en.append((o.t, o.field_energy()))
+            nxt += 10.0
+    return o, en, probes
+
+
+def polariton_energy_1d(make):
+    """tests/known_results.cpp:145-155 (polariton_energy): the 1-D polariton of
+    sc_polariton_1d and its field_energy() at round_time 10 (golden 0.0863443)."""
+    o = sc_polariton_1d(make)
+    return o, o.field_energy()
 
 
 def sc_known_metallic_3d(make):
