@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X fields::step() hot path (BASELINE.json metric).
 
-Workload (weak scaling): BASELINE configs[2] -- 3-D dielectric waveguide
-(eps = 12 core |y|,|z| < 0.5 along x, eps_averaging=False) + PML(1.0) on all
-faces, resolution 10, fp64, real fields, Ez Gaussian current source
+Headline workload (weak scaling): BASELINE configs[2] -- 3-D dielectric
+waveguide (eps = 12 core |y|,|z| < 0.5 along x, eps_averaging=False) + PML(1.0)
+on all faces, resolution 10, fp64, real fields, Ez Gaussian current source
 (GaussianSource(0.15, fwidth=0.1)) at (0.05, 0.05, 0.05).  Each GPU owns a
 512^3-cell z-slab: the global grid is 512 x 512 x (512*N), so N=1 is exactly
 the 512^3 headline and per-GPU work is fixed as N grows.
@@ -11,12 +11,20 @@ the 512^3 headline and per-GPU work is fixed as N grows.
 A "step" is one fields::step() (src/step.cpp:35-140) over the whole grid.
 value = (all cells * K) / max-over-ranks wall time, in Mcells*steps/s.
 
+At N=1 the same JSON line also carries the other single-GPU BASELINE configs,
+measured in the same run ("configs"): C2 256^3 vacuum + PML, C4 256^3 Kerr +
+Lorentzian slab, and C4's chi(2) Newton-Raphson sub-variant (NR solves/s).
+
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size S] [--vacuum]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+--gpus N without a launcher starts N ranks under torch.distributed.run (child
+processes).  Ranks sharing a GPU (MNL_BENCH_DEVICE, or fewer GPUs than ranks)
+exchange ghost planes over the IPC transport, otherwise over RCCL.
 Prints ONE JSON line on rank 0 (with "roofline" and "cpu_baseline").
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -26,6 +34,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+WORKLOADS = {
+    "waveguide": "C3 3-D dielectric waveguide eps=12 core + PML(1.0)",
+    "vacuum": "C3-vacuum 3-D vacuum + PML(1.0)",
+    "c2": "C2 3-D vacuum box + PML(1.0), Ez Gaussian at (0.05,0.05,0.05)",
+    "kerr": "C4 3-D Kerr chi3 + Lorentzian slab |z|<2 + PML(1.0), Ex source at z=-3 amp 50",
+    "kerr_nr": "C4-NR: C4 + chi2 0.5 and chi1inv off-diagonal 1e-3 in the box |x|,|y|<3, "
+               "|z|<1.5 (Newton-Raphson E update)",
+}
+NR_BOX = (-3.0, 3.0, -3.0, 3.0, -1.5, 1.5)
 
 
 def parse():
@@ -35,9 +52,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=512, help="cells per side of each GPU's slab")
     ap.add_argument("--vacuum", action="store_true", help="north-star vacuum variant (no core)")
-    ap.add_argument("--workload", choices=["waveguide", "vacuum", "kerr"], default=None,
-                    help="kerr: BASELINE configs[3] (chi3 + Lorentzian slab, unfused path)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the C2 / C4 / C4-NR measurements (N=1)")
+    ap.add_argument("--extra-size", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--flux", type=int, default=0,
                     help="add N DFT flux planes (x-normal, whole cross-section; decimation 1)")
@@ -47,37 +66,146 @@ def parse():
     return ap.parse_args()
 
 
-def build_fields(args, rank, world, local_rank, nid):
+def build_fields(workload, size, rank, world, device, nid):
+    """Structure + fields of one workload on this rank (global grid
+    size x size x size*world, center_origin, res 10, Courant 0.5)."""
     from meep_nl_amd import core
-    res = 10.0
-    n = [args.size, args.size, args.size * world]
+    import numpy as np
+    n = [size, size, size * world]
     io = [-(v - (v & 1)) for v in n]  # center_origin()
-    gv = core.GridVolume(3, n, res, io)
+    gv = core.GridVolume(3, n, 10.0, io)
     s = core.Structure(gv, 0.5)
     s.add_pml(1.0)
-    if args.workload == "kerr":  # |z| < 2: eps 2.25, chi3 1e-2, Lorentzian(1.1, 0.05, 0.5)
-        big = 1e9
+    big = 1e9
+    if workload in ("kerr", "kerr_nr"):  # |z| < 2: eps 2.25, chi3 1e-2, Lorentzian(1.1, 0.05, 0.5)
         slab = [-big, big, -big, big, -2.0, 2.0]
         s.set_box(0, slab, 2.25)
         s.set_box(2, slab, 1e-2)
         k = s.add_lorentzian(1.1, 0.05, [None, None, None])
         s.set_box(3, slab, 0.5, index=k)
-        f = core.Fields(s, device=local_rank, rank=rank, nranks=world, nccl_id=nid)
+        if workload == "kerr_nr":  # chi2 + off-diagonal chi1inv rows: the NR branch
+            x0, x1, y0, y1, z0, z1 = NR_BOX
+            s.set_box(1, list(NR_BOX), 0.5)
+            for c in range(3):
+                x, y, z = gv.coords(c)
+                inside = (x > x0) & (x < x1) & (y > y0) & (y < y1) & (z > z0) & (z < z1)
+                off = np.where(inside, 1e-3, 0.0)
+                del x, y, z, inside
+                for d in range(3):
+                    if d != c:
+                        s.set_chi1inv(c, d, off)
+                del off
+        f = core.Fields(s, device=device, rank=rank, nranks=world, nccl_id=nid)
         f.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -3.0), 50.0,
                               is_integrated=False)
         return gv, s, f
-    if not args.vacuum:
-        big = 1e9
+    if workload == "waveguide":
         s.set_box(0, [-big, big, -0.5 + 1e-12, 0.5 - 1e-12, -0.5 + 1e-12, 0.5 - 1e-12], 12.0)
-    f = core.Fields(s, device=local_rank, rank=rank, nranks=world, nccl_id=nid)
+    f = core.Fields(s, device=device, rank=rank, nranks=world, nccl_id=nid)
     f.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0,
                           is_integrated=False)
     return gv, s, f
 
 
+def nr_voxels(gv):
+    """E points on which the NR branch runs: every E component point inside the
+    chi2 / off-diagonal box (non-PML, all three rows present there)."""
+    import numpy as np
+    x0, x1, y0, y1, z0, z1 = NR_BOX
+    lo, hi = (x0, y0, z0), (x1, y1, z1)
+    n = 0
+    for c in range(3):
+        m = 1
+        for d in range(3):
+            j = np.arange(gv.n[d] + 1)
+            ax = (gv.io[d] + 2 * j + gv.shift(c, d)) * (0.5 / gv.a)
+            m *= int(np.sum((ax > lo[d]) & (ax < hi[d])))
+        n += m
+    return n
+
+
+def roofline(f, kind=0):
+    """Roofline object of the dominant kernel: algorithmic bytes per launch over
+    its average duration from HIP events on its own stream."""
+    n_launch, k_ms, k_bytes = f.kernel_stats(kind)
+    avg_ms = k_ms / max(n_launch, 1)
+    achieved = k_bytes / (avg_ms * 1e-3) / 1e9 if n_launch and avg_ms > 0 else 0.0
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": (("fused_kernel + fused_general_kernel concurrently (whole step, one pass)"
+                        if f.kernel_stats(2)[0] == 0 else
+                        "fused_kernel (lean tiles: curl B + curl D + E=chi1inv*D, one pass)")
+                       if f.fused_active() else "curl_kernel<B, interior> (step_db(B_stuff))"),
+            "bytes_per_launch": k_bytes, "avg_launch_ms": round(avg_ms, 4),
+            "launches": n_launch}
+    if f.fused_active():  # the PML / boundary tiles run in the second fused kernel
+        g_n, g_ms, g_bytes = f.kernel_stats(2)
+        if g_n:
+            g_avg = g_ms / g_n
+            roof["general_kernel"] = {
+                "kernel": "fused_general_kernel (PML / boundary tiles, same pass)",
+                "bytes_per_launch": g_bytes, "avg_launch_ms": round(g_avg, 4),
+                "achieved": round(g_bytes / (g_avg * 1e-3) / 1e9, 1)}
+    return roof
+
+
+def pmc_traffic(size, vacuum):
+    """HBM bytes per launch of the lean kernel from the committed PMC profile of
+    THIS kernel source (profiles/pmc_traffic.json), else None."""
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(tpath):
+        return None
+    try:
+        import hashlib
+        with open(tpath) as fh:
+            tj = json.load(fh)
+        with open(os.path.join(ROOT, "meep_nl_amd", "csrc", "mnl_kernels.hip"), "rb") as fh:
+            khash = hashlib.sha256(fh.read()).hexdigest()[:16]
+        if (tj.get("size") == size and tj.get("vacuum", False) == vacuum
+                and tj.get("kernels_hash") == khash):
+            return round(tj["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+    return None
+
+
+def measure_extra(workload, size, steps, warmup):
+    """One single-GPU BASELINE config in the same process: warm-up, K timed
+    steps (stream-synchronized), its own roofline."""
+    dev = int(os.environ.get("MNL_BENCH_DEVICE", "0"))
+    gv, s, f = build_fields(workload, size, 0, 1, dev, None)
+    f.step(warmup)
+    f.set_profiling(True)
+    t0 = time.perf_counter()
+    f.step(steps)
+    el = time.perf_counter() - t0
+    cells = float(size) ** 3
+    bpc, _ = f.traffic_model()
+    out = {"workload": WORKLOADS[workload] + f", {size}^3 cells, res 10, real fields, fp64",
+           "value": round(cells * steps / el / 1e6, 1), "unit": "Mcells*steps/s",
+           "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+           "fused": f.fused_active(), "model_bytes_per_cell_step": round(bpc, 2),
+           "model_fraction_of_peak": round(bpc * cells / (el / steps) / 1e9 / HBM_PEAK_GBS, 4),
+           "roofline": roofline(f)}
+    if workload == "kerr_nr":
+        nv = nr_voxels(gv)
+        e_n, e_ms, _ = f.kernel_stats(4)
+        out["nr"] = {"metric": "chi(2) Newton-Raphson solves/s", "nr_voxels_per_step": nv,
+                     "solves_per_s_whole_step": round(nv * steps / el, 1),
+                     "solves_per_s_e_update": round(nv * e_n / (e_ms * 1e-3), 1) if e_ms else None,
+                     "e_update_ms_per_step": round(e_ms / max(e_n, 1), 4),
+                     "nr_random_fallbacks": f.nr_fallbacks(),
+                     "bound": "latency/compute (per-voxel 3x3 Newton iterations), not HBM"}
+    del f, s
+    gc.collect()
+    return out
+
+
 def cpu_baseline(args):
-    """Time the oracle (CPU restatement, oracle/) on a bounded sample of the same
-    workload on this host's cores."""
+    """Time the oracle (CPU restatement, oracle/) on a bounded sample of the
+    headline workload on this host's cores: a 128^3 grid of the same waveguide
+    whose PML (0.15 -> 3 cells per face) keeps about the PML-cell fraction of
+    the 512^3 config (13.3 % vs 12.3 %)."""
     from oracle import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 64))
@@ -85,7 +213,7 @@ def cpu_baseline(args):
     import numpy as np
     L = 128
     o = orc.Oracle(3, [L, L, L], 10.0, 0.5, [-L, -L, -L])
-    o.add_pml(1.0)
+    o.add_pml(0.15)
     if not args.vacuum:
         for c in (0, 1, 2):
             x, y, z = o.coords(c)
@@ -100,9 +228,11 @@ def cpu_baseline(args):
         if el >= args.cpu_seconds or steps >= 400:
             break
     v = L ** 3 * steps / el / 1e6
+    pml_frac = 1 - ((L - 2 * 3) / L) ** 3
     return {"value": round(v, 2), "unit": "Mcells*steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ CPU restatement, {L}^3 {'vacuum' if args.vacuum else 'waveguide'}"
-                      f"+PML(1.0), {steps} steps in {el:.1f} s, OpenMP {threads} threads"}
+                      f" + PML(0.15) ({100 * pml_frac:.1f}% PML cells; the 512^3 config has "
+                      f"12.3%), {steps} steps in {el:.1f} s, OpenMP {threads} threads"}
 
 
 def launch_ranks(args):
@@ -137,7 +267,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     nid = None
-    transport, device = "single", local_rank
+    device = local_rank
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -149,7 +279,7 @@ def main():
         nid = obj[0]
     elif os.environ.get("MNL_BENCH_DEVICE"):
         device = int(os.environ["MNL_BENCH_DEVICE"])
-    gv, s, f = build_fields(args, rank, world, device, nid)
+    gv, s, f = build_fields(args.workload, args.size, rank, world, device, nid)
     if args.flux:  # on-device DFT flux monitors
         hx = 0.5 * gv.n[0] / 10.0
         hy, hz = 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
@@ -174,46 +304,11 @@ def main():
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    n_launch, k_ms, k_bytes = f.kernel_stats(0)
-    bpc, cells_local = f.traffic_model()
+    bpc, _ = f.traffic_model()
     total_cells = float(gv.n[0]) * gv.n[1] * gv.n[2]
     value = total_cells * args.steps / el / 1e6
-    if rank != 0:
-        if dist is not None:
-            dist.barrier()
-        return
-    avg_ms = k_ms / max(n_launch, 1)
-    achieved = k_bytes / (avg_ms * 1e-3) / 1e9 if n_launch else 0.0
-    traffic = None  # HBM bytes per launch from the committed PMC profile of THIS kernel source
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            import hashlib
-            with open(tpath) as fh:
-                tj = json.load(fh)
-            with open(os.path.join(ROOT, "meep_nl_amd", "csrc", "mnl_kernels.hip"), "rb") as fh:
-                khash = hashlib.sha256(fh.read()).hexdigest()[:16]
-            if (tj.get("size") == args.size and tj.get("vacuum", False) == args.vacuum
-                    and tj.get("kernels_hash") == khash):
-                traffic = round(tj["hbm_bytes_per_launch"])
-        except (OSError, ValueError, KeyError):
-            traffic = None
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": (("fused_kernel + fused_general_kernel concurrently (whole step, one pass)"
-                        if f.kernel_stats(2)[0] == 0 else
-                        "fused_kernel (lean tiles: curl B + curl D + E=chi1inv*D, one pass)")
-                       if f.fused_active() else "curl_kernel<B, interior> (step_db(B_stuff))"),
-            "bytes_per_launch": k_bytes, "avg_launch_ms": round(avg_ms, 4),
-            "launches": n_launch}
-    if f.fused_active():  # the PML / boundary tiles run in the second fused kernel
-        g_n, g_ms, g_bytes = f.kernel_stats(2)
-        if g_n:
-            g_avg = g_ms / g_n
-            roof["general_kernel"] = {
-                "kernel": "fused_general_kernel (PML / boundary tiles, same pass)",
-                "bytes_per_launch": g_bytes, "avg_launch_ms": round(g_avg, 4),
-                "achieved": round(g_bytes / (g_avg * 1e-3) / 1e9, 1)}
+    roof = roofline(f)
+    roof["traffic"] = pmc_traffic(args.size, args.vacuum) if f.fused_active() else None
     if args.flux:
         d_n, d_ms, d_bytes = f.kernel_stats(3)
         if d_n:
@@ -221,8 +316,24 @@ def main():
             roof["dft"] = {"kernel": f"dft_update_kernel x{args.flux} planes, {args.nfreq} freqs",
                            "bytes_per_step": d_bytes, "avg_step_ms": round(d_avg, 4),
                            "achieved": round(d_bytes / (d_avg * 1e-3) / 1e9, 1)}
+    transport = f.transport()
+    fused = f.fused_active()
+    del f, s
+    gc.collect()
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+    extra = None
+    if world == 1 and not args.no_extra and not args.flux:
+        extra = {}
+        for wl in ("c2", "kerr", "kerr_nr"):
+            try:
+                extra[wl] = measure_extra(wl, args.extra_size, 20, 5)
+            except Exception as e:  # an extra config must never hide the headline number
+                extra[wl] = {"error": str(e)}
     cpu = None
-    if world == 1 and not args.no_cpu and args.workload != "kerr" and not args.flux:
+    if world == 1 and not args.no_cpu and args.workload in ("waveguide", "vacuum") and not args.flux:
         try:
             cpu = cpu_baseline(args)
         except Exception as e:  # the baseline must never hide the GPU number
@@ -241,19 +352,19 @@ def main():
         "dtype": "f64",
         "data": "synthetic (Gaussian point source; fields start at zero)",
         "config": {
-            "workload": {"waveguide": "C3 3-D dielectric waveguide eps=12 core + PML(1.0)",
-                         "vacuum": "C3-vacuum 3-D vacuum + PML(1.0)",
-                         "kerr": "C4 3-D Kerr chi3 + Lorentzian slab |z|<2 + PML(1.0), "
-                                 "Ex source at z=-3"}[args.workload] +
+            "workload": WORKLOADS[args.workload] +
                         f", {args.size}x{args.size}x({args.size}*N) cells, res 10, real fields" +
                         (", Ez Gaussian current at (0.05,0.05,0.05)"
-                         if args.workload != "kerr" else ""),
+                         if args.workload in ("waveguide", "vacuum") else ""),
             "grid": list(gv.n), "per_gpu_cells": args.size ** 3, "parallelism": f"z-slab x{world}",
-            "transport": f.transport(),
+            "transport": transport, "fused": fused,
             "flux_planes": args.flux, "flux_nfreq": args.nfreq if args.flux else 0,
-            "model_bytes_per_cell_step": bpc},
+            "model_bytes_per_cell_step": bpc,
+            "model_fraction_of_peak": round(bpc * total_cells / world / (el / args.steps) / 1e9
+                                            / HBM_PEAK_GBS, 4)},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "configs": extra,
     }
     print(json.dumps(out))
     sys.stdout.flush()

@@ -249,7 +249,9 @@ int mnl_fields_set_profiling(mnl_fields *f, int on);
  * which = 0: fused step kernel (fused mode) or curl B = step_db(B_stuff);
  * which = 1: curl D = step_db(D_stuff) (unfused mode);
  * which = 2: general fused kernel (PML / boundary tiles);
- * which = 3: the DFT updates of one step (all flux objects). */
+ * which = 3: the DFT updates of one step (all flux objects);
+ * which = 4: the E update (update_eh(E_stuff): chi(2) Newton-Raphson,
+ *            Lorentzian P), unfused mode; bytes 0 (not HBM-bound). */
 int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch);
 

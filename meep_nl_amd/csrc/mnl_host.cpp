@@ -807,8 +807,12 @@ int setup_materials(mnl_fields *F) {
           return fail("upstream nonlinear mode: off-diagonal epsilon is not supported");
       }
   }
+  // chi2 nontrivial on component c: a host array or a chi2 box (rasterised below)
+  bool box_chi2 = false;
+  for (auto &b : S.boxes) box_chi2 = box_chi2 || (b.kind == 1 && b.value != 0.0);
+  auto chi2_nt = [&](int c) { return box_chi2 || (!S.chi2[c].empty() && !all_eq(S.chi2[c], 0.0)); };
   for (int c = 0; c < 3 && !F->upnl; c++) {
-    if (S.chi2[c].empty() || all_eq(S.chi2[c], 0.0)) continue;
+    if (!chi2_nt(c)) continue;
     int d1 = (c + 1) % 3, d2 = (c + 2) % 3;
     if (!S.chi1inv[c][d1].empty() && !all_eq(S.chi1inv[c][d1], 0.0) &&
         !S.chi1inv[c][d2].empty() && !all_eq(S.chi1inv[c][d2], 0.0))
@@ -840,10 +844,10 @@ int setup_materials(mnl_fields *F) {
         f.offd[c][k] = p;
       }
     }
-    if (F->nr && !S.chi2[c].empty() && !all_eq(S.chi2[c], 0.0)) {
+    if (F->nr && chi2_nt(c)) {
       double *p;
-      if (dev_alloc(F, &p, F->nlocal)) return -1;
-      if (upload_canonical(F, p, S.chi2[c], c)) return -1;
+      if (dev_alloc(F, &p, F->nlocal)) return -1;  // zeroed: boxes are filled in below
+      if (!S.chi2[c].empty() && upload_canonical(F, p, S.chi2[c], c)) return -1;
       f.chi2[c] = p;
     }
     if (F->upnl) {  // both arrays on every E component (zeros where absent)
@@ -4068,7 +4072,13 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
 
 int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch) {
-  if (!F || which < 0 || which > 3) return fail("bad kernel id");
+  if (!F || which < 0 || which > 4) return fail("bad kernel id");
+  if (which == 4) {  // E update (update_eh(E_stuff) incl. chi(2) Newton-Raphson, Lorentzian P)
+    *launches = F->timer_count[TM_E];
+    *total_ms = F->timer_ms[TM_E];
+    *bytes_per_launch = 0;
+    return 0;
+  }
   if (which == 3) {  // DFT updates of one step (all flux objects)
     *launches = F->timer_count[TM_DFT];
     *total_ms = F->timer_ms[TM_DFT] + F->timer_ms[TM_DFTF];

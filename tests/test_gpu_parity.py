@@ -76,6 +76,33 @@ def test_nr_integrated_source_on_chunk_seam():
     _bitwise(p, sc_nr_isrc_seam(make_oracle))
 
 
+def test_nr_chi2_from_boxes():
+    """chi2 given as a device-rasterised box (mnl_structure_set_box kind 1, the
+    bench's fast setup) enables the Newton-Raphson branch exactly as the same
+    chi2 given as an array (points with lo <= pos <= hi, no averaging)."""
+    box = (-0.5, 0.5, -0.45, 0.55, -0.5, 0.3)
+
+    def run(make, use_box):
+        o = make(3, [26, 26, 26], 10.0, 0.5, [-26, -26, -26])
+        o.add_pml(0.6)
+        for c in range(3):
+            x, y, z = o.coords(c)
+            inside = ((x >= box[0]) & (x <= box[1]) & (y >= box[2]) & (y <= box[3]) &
+                      (z >= box[4]) & (z <= box[5]))
+            for d in range(3):
+                o.set_chi1inv(c, d, np.where(inside, 0.25 if d == c else 1e-3, 1.0 if d == c else 0.0))
+            if not use_box:
+                o.set_chi2(c, np.where(inside, 0.5, 0.0))
+        if use_box:
+            o.s.set_box(1, list(box), 0.5)
+        o.legacy_point_source(2, 0.5, 0.5, 0.0, 3.0, (0.05, 0.05, 0.05), 5.0)
+        o.step(30)
+        return o
+    p = run(ProductSim, True)
+    assert not p._fields().fused_active()  # NR keeps the step unfused
+    _bitwise(p, run(make_oracle, False))
+
+
 def test_known_results(golden):
     kr = golden["known_results"]
     p = sc_known_metallic_3d(ProductSim)
