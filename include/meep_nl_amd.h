@@ -38,6 +38,9 @@ enum { MNL_LOW = 0, MNL_HIGH = 1 };
 enum { MNL_SRC_GAUSSIAN = 0, MNL_SRC_CONTINUOUS = 1, MNL_SRC_CUSTOM = 2 };
 /* custom_src_time callback: writes the complex dipole f(t) (src/meep.hpp:1059-1092) */
 typedef void (*mnl_src_func)(double t, void *data, double *re, double *im);
+/* amplitude function A(r) of a volume source: writes A at the position rel
+ * (relative to the volume centre; src/sources.cpp:262-271) */
+typedef void (*mnl_amp_func)(const double rel[3], void *data, double *re, double *im);
 
 typedef struct mnl_structure mnl_structure;
 typedef struct mnl_fields mnl_fields;
@@ -174,6 +177,23 @@ int mnl_fields_add_point_source(mnl_fields *f, int comp, int kind, const double 
 int mnl_fields_add_custom_point_source(mnl_fields *f, int comp, mnl_src_func func, void *data,
                                        double start_time, double end_time, const double pos[3],
                                        double amp_re, double amp_im, int is_integrated);
+/* fields::add_volume_source(c, src_time, volume(vmin, vmax), A, amp)
+ * (src/sources.cpp:455-494, src_vol_chunkloop 243-312): every owned point of
+ * component comp's grid in the volume gets the loop_in_chunks weight (linear
+ * interpolation at the faces, per reference chunk) times amp times A(r - centre)
+ * (afunc NULL: A = 1); zero-width directions scale amp by the resolution (J as
+ * a delta function); a volume up to one pixel wider than the cell is clamped,
+ * wider fails ("Source width > cell width").  kind / params as
+ * mnl_fields_add_point_source (not CUSTOM).  Integrated (dipole) sources are
+ * limited to 64 points per fields object. */
+int mnl_fields_add_volume_source(mnl_fields *f, int comp, int kind, const double *params, int np,
+                                 const double vmin[3], const double vmax[3], double amp_re,
+                                 double amp_im, int is_integrated, mnl_amp_func afunc,
+                                 void *adata);
+int mnl_fields_add_custom_volume_source(mnl_fields *f, int comp, mnl_src_func func, void *data,
+                                        double start_time, double end_time, const double vmin[3],
+                                        const double vmax[3], double amp_re, double amp_im,
+                                        int is_integrated, mnl_amp_func afunc, void *adata);
 /* fields::require_component (src/fields.cpp:566-586). */
 int mnl_fields_require_component(mnl_fields *f, int comp);
 /* fields::step() x nsteps (src/step.cpp:35-140).  Collective for

@@ -15,6 +15,8 @@ c_int, c_double, c_void, c_size = ctypes.c_int, ctypes.c_double, ctypes.c_void_p
 dptr = ctypes.POINTER(ctypes.c_double)
 # custom_src_time callback (include/meep_nl_amd.h mnl_src_func)
 SRC_FUNC = ctypes.CFUNCTYPE(None, ctypes.c_double, ctypes.c_void_p, dptr, dptr)
+# volume-source amplitude function A(r) (include/meep_nl_amd.h mnl_amp_func)
+AMP_FUNC = ctypes.CFUNCTYPE(None, dptr, ctypes.c_void_p, dptr, dptr)
 iptr = ctypes.POINTER(ctypes.c_int)
 llptr = ctypes.POINTER(ctypes.c_longlong)
 
@@ -34,6 +36,13 @@ _SIGS = {
     "mnl_fields_add_custom_point_source": (c_int, [c_void, c_int, SRC_FUNC, ctypes.c_void_p,
                                                    ctypes.c_double, ctypes.c_double, dptr,
                                                    ctypes.c_double, ctypes.c_double, c_int]),
+    "mnl_fields_add_volume_source": (c_int, [c_void, c_int, c_int, dptr, c_int, dptr, dptr,
+                                             ctypes.c_double, ctypes.c_double, c_int, AMP_FUNC,
+                                             ctypes.c_void_p]),
+    "mnl_fields_add_custom_volume_source": (c_int, [c_void, c_int, SRC_FUNC, ctypes.c_void_p,
+                                                    ctypes.c_double, ctypes.c_double, dptr, dptr,
+                                                    ctypes.c_double, ctypes.c_double, c_int,
+                                                    AMP_FUNC, ctypes.c_void_p]),
     "mnl_fields_dump": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_fields_array_slice": (c_int, [c_void, c_int, dptr, dptr, c_int, ctypes.POINTER(c_int),
                                        ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]),

@@ -234,6 +234,56 @@ class Fields:
         self._last_times = getattr(self, "_last_times", [])
         self._last_times.append(float(np.float32(end)))
 
+    def _amp_cb(self, amp_func):
+        """ctypes callback for a volume source's amplitude function A(r) (r relative
+        to the volume centre, 3 coordinates) -> complex; kept alive with the fields."""
+        if amp_func is None:
+            return _lib.AMP_FUNC()
+        def _cb(rel, _data, re, im, f=amp_func):
+            v = complex(f((rel[0], rel[1], rel[2])))
+            re[0] = v.real
+            im[0] = v.imag
+        cb = _lib.AMP_FUNC(_cb)
+        self.__dict__.setdefault("_amp_cbs", []).append(cb)
+        return cb
+
+    def add_volume_source(self, comp, kind, params, vmin, vmax, amp=1.0, is_integrated=False,
+                          amp_func=None):
+        """fields::add_volume_source(c, src, volume(vmin, vmax), A, amp)
+        (src/sources.cpp:455-494); amp_func(r) -> complex, r relative to the centre."""
+        p = np.ascontiguousarray(params, dtype=np.float64)
+        lo = np.ascontiguousarray(list(vmin) + [0.0] * (3 - len(vmin)), dtype=np.float64)
+        hi = np.ascontiguousarray(list(vmax) + [0.0] * (3 - len(vmax)), dtype=np.float64)
+        amp = complex(amp)
+        check(lib().mnl_fields_add_volume_source(self.h, comp, kind, ptr(p), len(p), ptr(lo),
+                                                 ptr(hi), amp.real, amp.imag, int(is_integrated),
+                                                 self._amp_cb(amp_func), None))
+        self._last_times = getattr(self, "_last_times", [])
+        self._last_times.append(_src_last_time(kind, list(params)))
+
+    def add_custom_volume_source(self, comp, func, start, end, vmin, vmax, amp=1.0,
+                                 is_integrated=False, amp_func=None):
+        cbs = self.__dict__.setdefault("_custom_cbs", {})
+        if id(func) not in cbs:
+            def _cb(t, _data, re, im, func=func):
+                v = complex(func(t))
+                re[0] = v.real
+                im[0] = v.imag
+            cbs[id(func)] = (func, _lib.SRC_FUNC(_cb))
+        lo = np.ascontiguousarray(list(vmin) + [0.0] * (3 - len(vmin)), dtype=np.float64)
+        hi = np.ascontiguousarray(list(vmax) + [0.0] * (3 - len(vmax)), dtype=np.float64)
+        amp = complex(amp)
+        check(lib().mnl_fields_add_custom_volume_source(
+            self.h, comp, cbs[id(func)][1], None, float(start), float(end), ptr(lo), ptr(hi),
+            amp.real, amp.imag, int(is_integrated), self._amp_cb(amp_func), None))
+        self._last_times = getattr(self, "_last_times", [])
+        self._last_times.append(float(np.float32(end)))
+
+    def add_gaussian_volume_source(self, comp, freq, width, start, end, vmin, vmax, amp=1.0,
+                                   is_integrated=False, amp_func=None):
+        self.add_volume_source(comp, 0, [freq, width, start, end], vmin, vmax, amp, is_integrated,
+                               amp_func)
+
     def add_gaussian_source(self, comp, freq, width, start, end, pos, amp=1.0,
                             is_integrated=False):
         """gaussian_src_time(f, w, start, end) (src/sources.cpp:85-96)."""

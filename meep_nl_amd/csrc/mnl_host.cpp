@@ -23,6 +23,7 @@
 #include <unordered_set>
 #include <string>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/meep_nl_amd.h"
@@ -281,8 +282,13 @@ struct mnl_fields {
   std::vector<int> srcB_comp, srcD_comp, isrc_comp;
   std::vector<unsigned char> isrc_zone;  // owning reference chunk (zone box) per isrc point
   std::vector<std::pair<int, int>> srcB_ref, srcD_ref, isrc_ref;  // (group, point)
+  // current sources per field type ([0] B, [1] D), in layer order (SrcDev)
+  std::vector<double> src_amp[2];
+  std::vector<int> src_gid[2], src_layer[2];
   long long *d_srcB_idx = nullptr, *d_srcD_idx = nullptr;
   int *d_srcB_comp = nullptr, *d_srcD_comp = nullptr;
+  double *d_src_amp[2] = {nullptr, nullptr};
+  int *d_src_gid[2] = {nullptr, nullptr};
   double *d_vals = nullptr;
   size_t d_vals_cap = 0;
   long long t = 0;
@@ -1024,109 +1030,165 @@ int upload_pml(mnl_fields *F) {
   return 0;
 }
 
+// ------------------------------------------------------------- loop_in_chunks
+void dft_boundary_weights(const mnl_structure &S, const double wmin[3], const double wmax[3],
+                          const int is[3], const int ie[3], double s0[3], double e0[3],
+                          double s1[3], double e1[3]);
+std::vector<std::array<int, 6>> reference_chunks(const mnl_structure &S);
+
+// One reference chunk's loop of fields::loop_in_chunks over [wmin, wmax] on
+// component c's Yee grid (src/loop_in_chunks.cpp:325-520; no symmetry, no
+// Bloch): half-coordinate range [isc, iec] and the boundary weights.
+struct CLoop {
+  int isc[3], iec[3];
+  double s0[3], s1[3], e0[3], e1[3];
+  double W(int d, long i) const {  // IVEC_LOOP_WEIGHT1x (src/meep/vec.hpp:372-378)
+    const long n = (iec[d] - isc[d]) / 2 + 1;
+    if (i > 1 && i < n - 2) return 1.0;
+    return i == 0 ? s0[d] : (i == 1 ? s1[d] : i == n - 1 ? e0[d] : (i == n - 2 ? e1[d] : 1.0));
+  }
+};
+
+std::vector<CLoop> chunk_loops(const mnl_structure &S, int c, const double wmin[3],
+                               const double wmax[3]) {
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    if (!S.has[d]) continue;
+    const int iyc = 1 - S.shift(c, d);    // iyee_shift(Centered) - iyee_shift(c)
+    const double yc = iyc * (0.5 / S.a);  // wherec = where + yee_c
+    is[d] = 1 + 2 * int(floor((wmin[d] + yc) * S.a - .5)) - iyc;  // vec2diel_floor - iyee_c
+    ie[d] = 1 + 2 * int(ceil((wmax[d] + yc) * S.a - .5)) - iyc;
+  }
+  double s0[3], s1[3], e0[3], e1[3];
+  dft_boundary_weights(S, wmin, wmax, is, ie, s0, e0, s1, e1);
+  std::vector<CLoop> out;
+  for (auto &ch : reference_chunks(S)) {
+    CLoop L;
+    bool emp = false;
+    for (int d = 0; d < 3; d++) {
+      L.s0[d] = L.s1[d] = L.e0[d] = L.e1[d] = 1.0;
+      if (!S.has[d]) {
+        L.isc[d] = L.iec[d] = 0;
+        continue;
+      }
+      // little_owned_corner(c) = little + 2 - iyee_shift(c), big_owned_corner(c) =
+      // big - iyee_shift(c) (src/meep/vec.hpp:1102-1107)
+      const int sh = S.shift(c, d);
+      const int uoc = S.io[d] + 2 - sh, coc = ch[d] + 2 - sh, cbo = ch[d] + 2 * ch[3 + d] - sh;
+      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
+      L.isc[d] = std::max(is[d], iscoS);
+      L.iec[d] = std::min(ie[d], iecoS);
+      if (L.isc[d] > L.iec[d]) emp = true;
+    }
+    if (emp) continue;
+    for (int d = 0; d < 3; d++) {
+      if (!S.has[d]) continue;
+      if (L.isc[d] == is[d]) {
+        L.s0[d] = s0[d];
+        L.s1[d] = s1[d];
+      } else if (L.isc[d] == is[d] + 2) {
+        L.s0[d] = s1[d];
+      }
+      if (L.iec[d] == ie[d]) {
+        L.e0[d] = e0[d];
+        L.e1[d] = e1[d];
+      } else if (L.iec[d] == ie[d] - 2) {
+        L.e0[d] = e1[d];
+      }
+      if (L.iec[d] == L.isc[d]) {
+        double w = std::min(L.s0[d], L.e0[d]);
+        L.s0[d] = L.e0[d] = L.s1[d] = L.e1[d] = w;
+      } else if (L.iec[d] == L.isc[d] + 2) {
+        double w = std::min(L.s0[d], L.e1[d]);
+        L.s0[d] = w, L.e1[d] = w;
+        w = std::min(L.s1[d], L.e0[d]);
+        L.s1[d] = w, L.e0[d] = w;
+      } else if (L.iec[d] == L.isc[d] + 4) {
+        double w = std::min(L.s1[d], L.e1[d]);
+        L.s1[d] = w, L.e1[d] = w;
+      }
+    }
+    out.push_back(L);
+  }
+  return out;
+}
+
 // ------------------------------------------------------------- sources
-// Point-source weights: loop_in_chunks for a zero-size volume
-// (src/loop_in_chunks.cpp:339-500, compute_boundary_weights 263-300) on the
-// whole cell (the chunk split of the reference gives the same weights).
-int add_point_source(mnl_fields *F, int c, int st, const double pos[3], cplx amp0) {
+// fields::add_volume_source(c, src, where, A, amp) (src/sources.cpp:455-494):
+// the source volume is clamped to the cell, delta-function directions scale
+// the amplitude by a, and src_vol_chunkloop (243-312) gives every owned point
+// of each reference chunk the amplitude IVEC_LOOP_WEIGHT * amp * A(loc -
+// center).  The points of all chunks form one group (src_vol list order).
+int add_volume_source(mnl_fields *F, int c, int st, const double wmin0[3], const double wmax0[3],
+                      cplx amp0, mnl_amp_func afunc, void *adata) {
   const mnl_structure &S = F->S;
+  double wmin[3], wmax[3];
+  for (int d = 0; d < 3; d++) {
+    wmin[d] = S.has[d] ? wmin0[d] : 0.0;
+    wmax[d] = S.has[d] ? wmax0[d] : 0.0;
+    if (wmax[d] < wmin[d]) return fail("source volume: max < min");
+    if (!S.has[d]) continue;
+    const double w = S.n[d] * (1.0 / S.a);  // user_volume width
+    const double wd = wmax[d] - wmin[d];
+    if (wd > w + 1.0 / S.a) {
+      const char *nm[3] = {"X", "Y", "Z"};
+      return fail(std::string("Source width > cell width in ") + nm[d] + " direction!");
+    } else if (wd > w) {  // less than a pixel too wide
+      const double dw = wd - w;
+      wmin[d] = wmin[d] - dw * 0.5;
+      wmax[d] = wmin[d] + w;
+    }
+  }
   cplx amp = amp0;
   for (int d = 0; d < 3; d++)
-    if (S.has[d]) amp *= S.a;  // src/sources.cpp:484-487
-  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
-  double s0[3], s1[3], e0[3], e1[3];
-  for (int d = 0; d < 3; d++) {
-    s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
-    if (!S.has[d]) continue;
-    int sh = S.shift(c, d);
-    int iyee_c = 1 - sh;
-    double yee_c = 1 * (0.5 * (1.0 / S.a)) - sh * (0.5 * (1.0 / S.a));
-    double P = pos[d] + yee_c;
-    is[d] = 1 + 2 * int(floor(P * S.a - .5)) - iyee_c;
-    ie[d] = 1 + 2 * int(ceil(P * S.a - .5)) - iyee_c;
-    double w0 = 1. - pos[d] * S.a + 0.5 * is[d];
-    double w1 = 1. + pos[d] * S.a - 0.5 * ie[d];
-    s0[d] = w0, s1[d] = w1, e0[d] = w1, e1[d] = w0;
-  }
-  int isc[3], iec[3];
-  double s0c[3], s1c[3], e0c[3], e1c[3];
-  for (int d = 0; d < 3; d++) {
-    s0c[d] = s1c[d] = e0c[d] = e1c[d] = 1.0;
-    if (!S.has[d]) {
-      isc[d] = iec[d] = 0;
-      continue;
-    }
-    int sh = S.shift(c, d);
-    int uoc = S.io[d] + 2 - sh, ubo = S.io[d] + 2 * S.n[d] - sh;
-    isc[d] = std::max(is[d], uoc);
-    iec[d] = std::min(ie[d], ubo);
-    if (isc[d] > iec[d]) return 0;  // outside the cell
-    if (isc[d] == is[d]) {
-      s0c[d] = s0[d];
-      s1c[d] = s1[d];
-    } else if (isc[d] == is[d] + 2) {
-      s0c[d] = s1[d];
-    }
-    if (iec[d] == ie[d]) {
-      e0c[d] = e0[d];
-      e1c[d] = e1[d];
-    } else if (iec[d] == ie[d] - 2) {
-      e0c[d] = e1[d];
-    }
-    if (iec[d] == isc[d]) {
-      double w = std::min(s0c[d], e0c[d]);
-      s0c[d] = e0c[d] = s1c[d] = e1c[d] = w;
-    } else if (iec[d] == isc[d] + 2) {
-      double w = std::min(s0c[d], e1c[d]);
-      s0c[d] = w, e1c[d] = w;
-      w = std::min(s1c[d], e0c[d]);
-      s1c[d] = w, e0c[d] = w;
-    } else if (iec[d] == isc[d] + 4) {
-      double w = std::min(s1c[d], e1c[d]);
-      s1c[d] = w, e1c[d] = w;
-    }
-  }
+    if (S.has[d] && wmax[d] - wmin[d] == 0.0) amp *= S.a;  // delta-function units
+  double center[3];
+  for (int d = 0; d < 3; d++) center[d] = (wmin[d] + wmax[d]) * 0.5;
   int yd[3];
   if (S.dim == 2)
     yd[0] = 2, yd[1] = 0, yd[2] = 1;
   else
     yd[0] = 0, yd[1] = 1, yd[2] = 2;
-  int ln[3];
-  for (int k = 0; k < 3; k++) ln[k] = S.has[yd[k]] ? (iec[yd[k]] - isc[yd[k]]) / 2 + 1 : 1;
-  auto W1 = [&](int k, int i) -> double {
-    int d = yd[k], n = ln[k];
-    if (i > 1 && i < n - 2) return 1.0;
-    if (i == 0) return s0c[d];
-    if (i == 1) return s1c[d];
-    if (i == n - 1) return e0c[d];
-    if (i == n - 2) return e1c[d];
-    return 1.0;
-  };
   SrcGroup grp;
   grp.comp = c;
   grp.st = st;
-  for (int i1 = 0; i1 < ln[0]; i1++)
-    for (int i2 = 0; i2 < ln[1]; i2++)
-      for (int i3 = 0; i3 < ln[2]; i3++) {
-        int p[3] = {0, 0, 0}, ii[3] = {i1, i2, i3};
-        for (int k = 0; k < 3; k++)
-          if (S.has[yd[k]]) p[yd[k]] = isc[yd[k]] + 2 * ii[k];
-        bool own = true;
-        int jg[3] = {0, 0, 0};
-        long long gi = 0;
-        for (int d = 0; d < 3; d++)
-          if (S.has[d]) {
-            int o = p[d] - S.io[d];
-            if (!(o > 0 && o <= 2 * S.n[d])) own = false;
-            jg[d] = (p[d] - S.io[d] - S.shift(c, d)) / 2;
-            gi += jg[d] * S.cstride(d);
+  for (const CLoop &L : chunk_loops(S, c, wmin, wmax)) {
+    long ln[3];
+    for (int k = 0; k < 3; k++) ln[k] = S.has[yd[k]] ? (L.iec[yd[k]] - L.isc[yd[k]]) / 2 + 1 : 1;
+    for (long i1 = 0; i1 < ln[0]; i1++)
+      for (long i2 = 0; i2 < ln[1]; i2++)
+        for (long i3 = 0; i3 < ln[2]; i3++) {
+          const long ii[3] = {i1, i2, i3};
+          int p[3] = {0, 0, 0};
+          for (int k = 0; k < 3; k++)
+            if (S.has[yd[k]]) p[yd[k]] = L.isc[yd[k]] + 2 * int(ii[k]);
+          bool own = true;
+          int jg[3] = {0, 0, 0};
+          long long gi = 0;
+          for (int d = 0; d < 3; d++)
+            if (S.has[d]) {
+              const int o = p[d] - S.io[d];
+              if (!(o > 0 && o <= 2 * S.n[d])) own = false;
+              jg[d] = (p[d] - S.io[d] - S.shift(c, d)) / 2;
+              gi += jg[d] * S.cstride(d);
+            }
+          if (!own) continue;
+          double w[3];
+          for (int k = 0; k < 3; k++) w[k] = L.W(yd[k], ii[k]);
+          const double wgt = w[2] * (w[1] * (1.0 * w[0]));
+          cplx A = 1.0;
+          if (afunc) {
+            double rel[3];
+            for (int d = 0; d < 3; d++) rel[d] = S.has[d] ? p[d] * (0.5 * (1.0 / S.a)) - center[d] : 0.0;
+            double re = 0, im = 0;
+            afunc(rel, adata, &re, &im);
+            A = cplx(re, im);
           }
-        if (!own) continue;
-        double wgt = (W1(2, i3) * (W1(1, i2) * ((1.0) * W1(0, i1))));
-        grp.amp.push_back(wgt * (amp * std::conj(cplx(1.0))) * cplx(1.0));
-        grp.gidx.push_back(gi);
-        for (int d = 0; d < 3; d++) grp.jglob.push_back(jg[d]);
-      }
+          grp.amp.push_back(wgt * (amp * std::conj(cplx(1.0))) * A);
+          grp.gidx.push_back(gi);
+          for (int d = 0; d < 3; d++) grp.jglob.push_back(jg[d]);
+        }
+  }
   if (grp.gidx.empty()) return 0;
   for (auto &o : F->groups)  // src_vol::combinable merge (src/fields.cpp:588-597)
     if (o.comp == grp.comp && o.st == grp.st && o.gidx == grp.gidx) {
@@ -1233,18 +1295,74 @@ int build_source_lists(mnl_fields *F) {
   }
   if (F->isrc_idx.size() > (size_t)MAX_ISRC)
     return fail("too many integrated source points (max 64)");
-  auto up = [&](long long **dI, int **dC, const std::vector<long long> &I,
-                const std::vector<int> &C) -> int {
-    if (I.empty()) return 0;
-    if (dev_alloc(F, dI, I.size(), false) || dev_alloc(F, dC, C.size(), false)) return -1;
+  // layers: the k-th occurrence of a (component, point) goes to layer k, so a layer
+  // is applied in parallel and the layers in list order (step_source order)
+  for (int t = 0; t < 2; t++) {
+    auto &I = t ? F->srcD_idx : F->srcB_idx;
+    auto &C = t ? F->srcD_comp : F->srcB_comp;
+    auto &R = t ? F->srcD_ref : F->srcB_ref;
+    std::unordered_map<long long, int> seen;
+    std::vector<int> lay(I.size());
+    int nl = 0;
+    for (size_t k = 0; k < I.size(); k++) {
+      lay[k] = seen[I[k] * 3 + C[k]]++;
+      nl = std::max(nl, lay[k] + 1);
+    }
+    std::vector<size_t> ord(I.size());
+    for (size_t k = 0; k < ord.size(); k++) ord[k] = k;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return lay[a] < lay[b]; });
+    std::vector<long long> I2;
+    std::vector<int> C2;
+    std::vector<std::pair<int, int>> R2;
+    auto &A = F->src_amp[t];
+    auto &Gd = F->src_gid[t];
+    auto &L = F->src_layer[t];
+    A.clear(), Gd.clear(), L.assign(nl + 1, 0);
+    for (size_t k : ord) {
+      I2.push_back(I[k]);
+      C2.push_back(C[k]);
+      R2.push_back(R[k]);
+      const cplx a = F->groups[R[k].first].amp[R[k].second];
+      A.push_back(real(a));
+      A.push_back(imag(a));
+      Gd.push_back(R[k].first);
+      L[lay[k] + 1]++;
+    }
+    for (int l = 0; l < nl; l++) L[l + 1] += L[l];
+    I.swap(I2), C.swap(C2), R.swap(R2);
+    if (I.empty()) continue;
+    long long **dI = t ? &F->d_srcD_idx : &F->d_srcB_idx;
+    int **dC = t ? &F->d_srcD_comp : &F->d_srcB_comp;
+    if (dev_alloc(F, dI, I.size(), false) || dev_alloc(F, dC, C.size(), false) ||
+        dev_alloc(F, &F->d_src_amp[t], A.size(), false) ||
+        dev_alloc(F, &F->d_src_gid[t], Gd.size(), false))
+      return -1;
     HIPCHK(hipMemcpyAsync(*dI, I.data(), I.size() * 8, hipMemcpyHostToDevice, F->stream));
     HIPCHK(hipMemcpyAsync(*dC, C.data(), C.size() * 4, hipMemcpyHostToDevice, F->stream));
-    return 0;
-  };
-  if (up(&F->d_srcB_idx, &F->d_srcB_comp, F->srcB_idx, F->srcB_comp)) return -1;
-  if (up(&F->d_srcD_idx, &F->d_srcD_comp, F->srcD_idx, F->srcD_comp)) return -1;
+    HIPCHK(hipMemcpyAsync(F->d_src_amp[t], A.data(), A.size() * 8, hipMemcpyHostToDevice,
+                          F->stream));
+    HIPCHK(hipMemcpyAsync(F->d_src_gid[t], Gd.data(), Gd.size() * 4, hipMemcpyHostToDevice,
+                          F->stream));
+  }
+  HIPCHK(hipStreamSynchronize(F->stream));
   F->src_dirty = false;
   return 0;
+}
+
+// SrcDev of field type t (0 = B, 1 = D) reading the group currents at J
+SrcDev src_dev(mnl_fields *F, int t, const double *J) {
+  SrcDev s;
+  s.n = (int)(t ? F->srcD_idx.size() : F->srcB_idx.size());
+  s.idx = t ? F->d_srcD_idx : F->d_srcB_idx;
+  s.comp = t ? F->d_srcD_comp : F->d_srcB_comp;
+  s.amp = F->d_src_amp[t];
+  s.gid = F->d_src_gid[t];
+  s.J = J;
+  s.dt = F->dt;
+  s.nlayer = (int)F->src_layer[t].size() - 1;
+  s.layer = F->src_layer[t].data();
+  if (s.nlayer < 0) s.nlayer = 0;
+  return s;
 }
 
 // ------------------------------------------------------------- interpolation
@@ -2434,7 +2552,11 @@ int step_batch(mnl_fields *F, int nsteps) {
   const double dt = F->dt;
   // per-step source values, computed on the host exactly as the reference
   size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
-  size_t per = nB + nD + nI;
+  // per step: the current of every group at time (B) and time + dt/2 (D), complex,
+  // then the integrated dipoles real(amp * dipole(time + dt)) per point
+  const size_t ng = F->groups.size();
+  size_t per = (nB || nD ? 4 * ng : 0) + nI;
+  const size_t jofs = (nB || nD) ? 4 * ng : 0;
   const int CH = 1024;
   std::vector<EvPair> evs;
   size_t evi = 0;
@@ -2492,19 +2614,19 @@ int step_batch(mnl_fields *F, int nsteps) {
       for (int s = 0; s < ns; s++) {
         long long tt = F->t + s;
         double time = tt * dt;
-        double *vB = &vals[(size_t)s * per], *vD = vB + nB, *vI = vD + nD;
+        double *vB = &vals[(size_t)s * per], *vD = vB + 2 * ng, *vI = vB + jofs;
         for (auto &st : F->srcs) st.update(time, dt);  // calc_sources(time())
-        for (size_t k = 0; k < nB; k++) {
-          const SrcGroup &G = F->groups[F->srcB_ref[k].first];
-          const cplx A = (G.amp[F->srcB_ref[k].second] * F->srcs[G.st].cur_current) * dt;
-          vB[k] = real(A);
-        }
+        if (jofs)
+          for (size_t g = 0; g < ng; g++) {
+            const cplx J = F->srcs[F->groups[g].st].cur_current;
+            vB[2 * g] = real(J), vB[2 * g + 1] = imag(J);
+          }
         for (auto &st : F->srcs) st.update(time + 0.5 * dt, dt);
-        for (size_t k = 0; k < nD; k++) {
-          const SrcGroup &G = F->groups[F->srcD_ref[k].first];
-          const cplx A = (G.amp[F->srcD_ref[k].second] * F->srcs[G.st].cur_current) * dt;
-          vD[k] = real(A);
-        }
+        if (jofs)
+          for (size_t g = 0; g < ng; g++) {
+            const cplx J = F->srcs[F->groups[g].st].cur_current;
+            vD[2 * g] = real(J), vD[2 * g + 1] = imag(J);
+          }
         for (auto &st : F->srcs) st.update(time + dt, dt);
         for (size_t k = 0; k < nI; k++) {
           const SrcGroup &G = F->groups[F->isrc_ref[k].first];
@@ -2525,18 +2647,13 @@ int step_batch(mnl_fields *F, int nsteps) {
     for (int s = 0; s < ns; s++) {
       DevFields &f = F->f;
       const DevGrid &g = F->g;
-      SrcDev sB{(int)nB, F->d_srcB_idx, F->d_srcB_comp, F->d_vals};
-      SrcDev sD{(int)nD, F->d_srcD_idx, F->d_srcD_comp, F->d_vals + nB};
+      const double *vs = F->d_vals + (size_t)s * per;  // this step's table
+      const SrcDev sB = src_dev(F, 0, vs), sD = src_dev(F, 1, vs + 2 * ng);
       ISrcDev is;
       is.n = (int)nI;
       for (size_t k = 0; k < nI; k++)
         is.idx[k] = F->isrc_idx[k], is.comp[k] = F->isrc_comp[k], is.zone[k] = F->isrc_zone[k];
-      is.val = F->d_vals + nB + nD;
-      // per-step tables are strided by `per`: encode via pointer offset + stride trick
-      // (kernels index val[step*n + k]; use a dedicated stride by shifting base per step)
-      sB.val = F->d_vals + (size_t)s * per;
-      sD.val = F->d_vals + (size_t)s * per + nB;
-      is.val = F->d_vals + (size_t)s * per + nB + nD;
+      is.val = vs + jofs;  // kernels index val[step * n + k] with step 0
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
         continue;
@@ -3355,20 +3472,20 @@ int sync_magnetic(mnl_fields *F, MagBackup &bk) {
       k_curl(T_B, F->interior, &F->shell_list, g, f, F->planB, F->S.courant, F->stream, false))
     return fail("curl B launch failed");
   const size_t nB = F->srcB_idx.size();
-  if (nB) {
+  if (nB) {  // calc_sources(time()) + step_source(B_stuff)
     const double dt = F->dt, time = F->t * dt;
     for (auto &st : F->srcs) st.update(time, dt);
-    std::vector<double> vB(nB);
-    for (size_t k = 0; k < nB; k++) {
-      const SrcGroup &G = F->groups[F->srcB_ref[k].first];
-      vB[k] = real((G.amp[F->srcB_ref[k].second] * F->srcs[G.st].cur_current) * dt);
+    const size_t ng = F->groups.size();
+    std::vector<double> J(2 * ng);
+    for (size_t g2 = 0; g2 < ng; g2++) {
+      const cplx v = F->srcs[F->groups[g2].st].cur_current;
+      J[2 * g2] = real(v), J[2 * g2 + 1] = imag(v);
     }
     double *dv = nullptr;
-    HIPCHK(hipMalloc(&dv, nB * 8));
+    HIPCHK(hipMalloc(&dv, J.size() * 8));
     std::unique_ptr<void, void (*)(void *)> gv(dv, [](void *p) { (void)hipFree(p); });
-    HIPCHK(hipMemcpyAsync(dv, vB.data(), nB * 8, hipMemcpyHostToDevice, F->stream));
-    SrcDev sB{(int)nB, F->d_srcB_idx, F->d_srcB_comp, dv};
-    if (k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
+    HIPCHK(hipMemcpyAsync(dv, J.data(), J.size() * 8, hipMemcpyHostToDevice, F->stream));
+    if (k_source(T_B, g, f, src_dev(F, 0, dv), 0, F->stream)) return fail("source launch failed");
     HIPCHK(hipStreamSynchronize(F->stream));
   }
   if (!F->h_first_done && h_lazy_copy(F)) return -1;
@@ -3549,9 +3666,9 @@ int check_comp(int c) {
   return 0;
 }
 
-int add_point_source_any(mnl_fields *F, int comp, int kind, const double *p, int np,
-                         mnl_src_func func, void *fdata, const double pos[3], double amp_re,
-                         double amp_im, int is_integrated) {
+int add_source_any(mnl_fields *F, int comp, int kind, const double *p, int np, mnl_src_func func,
+                   void *fdata, const double vmin[3], const double vmax[3], double amp_re,
+                   double amp_im, int is_integrated, mnl_amp_func afunc, void *adata) {
   if (!F || check_comp(comp)) return -1;
   if (!(ctype(comp) == T_E || ctype(comp) == T_H)) return fail("sources must be E or H components");
   if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
@@ -3592,10 +3709,10 @@ int add_point_source_any(mnl_fields *F, int comp, int kind, const double *p, int
     idx = (int)F->srcs.size() - 1;
   }
   if (require_component(F, comp)) return -1;
-  double pp[3] = {pos[0], pos[1], pos[2]};
-  if (F->S.dim == 1) pp[0] = pp[1] = 0;
-  if (F->S.dim == 2) pp[2] = 0;
-  return add_point_source(F, comp, idx, pp, cplx(amp_re, amp_im));
+  double lo[3] = {vmin[0], vmin[1], vmin[2]}, hi[3] = {vmax[0], vmax[1], vmax[2]};
+  if (F->S.dim == 1) lo[0] = lo[1] = hi[0] = hi[1] = 0;
+  if (F->S.dim == 2) lo[2] = hi[2] = 0;
+  return add_volume_source(F, comp, idx, lo, hi, cplx(amp_re, amp_im), afunc, adata);
 }
 
 }  // namespace
@@ -3840,8 +3957,30 @@ void mnl_fields_destroy(mnl_fields *f) { delete f; }
 int mnl_fields_add_point_source(mnl_fields *F, int comp, int kind, const double *p, int np,
                                 const double pos[3], double amp_re, double amp_im,
                                 int is_integrated) {
-  return add_point_source_any(F, comp, kind, p, np, nullptr, nullptr, pos, amp_re, amp_im,
-                              is_integrated);
+  if (!pos) return fail("null position");
+  return add_source_any(F, comp, kind, p, np, nullptr, nullptr, pos, pos, amp_re, amp_im,
+                        is_integrated, nullptr, nullptr);
+}
+
+int mnl_fields_add_volume_source(mnl_fields *F, int comp, int kind, const double *p, int np,
+                                 const double vmin[3], const double vmax[3], double amp_re,
+                                 double amp_im, int is_integrated, mnl_amp_func afunc,
+                                 void *adata) {
+  if (!vmin || !vmax) return fail("null volume");
+  if (kind == MNL_SRC_CUSTOM) return fail("custom sources: use mnl_fields_add_custom_volume_source");
+  return add_source_any(F, comp, kind, p, np, nullptr, nullptr, vmin, vmax, amp_re, amp_im,
+                        is_integrated, afunc, adata);
+}
+
+int mnl_fields_add_custom_volume_source(mnl_fields *F, int comp, mnl_src_func func, void *data,
+                                        double start_time, double end_time, const double vmin[3],
+                                        const double vmax[3], double amp_re, double amp_im,
+                                        int is_integrated, mnl_amp_func afunc, void *adata) {
+  if (!func) return fail("custom source needs a function");
+  if (!vmin || !vmax) return fail("null volume");
+  const double p[2] = {start_time, end_time};
+  return add_source_any(F, comp, MNL_SRC_CUSTOM, p, 2, func, data, vmin, vmax, amp_re, amp_im,
+                        is_integrated, afunc, adata);
 }
 
 int mnl_fields_add_custom_point_source(mnl_fields *F, int comp, mnl_src_func func, void *data,
@@ -3849,8 +3988,9 @@ int mnl_fields_add_custom_point_source(mnl_fields *F, int comp, mnl_src_func fun
                                        double amp_re, double amp_im, int is_integrated) {
   if (!func) return fail("custom source needs a function");
   const double p[2] = {start_time, end_time};
-  return add_point_source_any(F, comp, MNL_SRC_CUSTOM, p, 2, func, data, pos, amp_re, amp_im,
-                              is_integrated);
+  if (!pos) return fail("null position");
+  return add_source_any(F, comp, MNL_SRC_CUSTOM, p, 2, func, data, pos, pos, amp_re, amp_im,
+                        is_integrated, nullptr, nullptr);
 }
 
 

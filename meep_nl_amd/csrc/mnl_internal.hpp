@@ -137,11 +137,22 @@ struct EBox {
 };
 
 // Point sources in rank-local linear indices.
+// Current sources (step_source, src/step.cpp:296-319) of one field type: per
+// point its rank-local index, direction, complex amplitude and src_vol group;
+// per step and group the src_time current (host, calc_sources).  The list is
+// split into layers in which every (comp, idx) occurs once, so a layer is
+// applied in parallel and the layers in list order (sequential semantics
+// where sources overlap).
 struct SrcDev {
   int n;
   const long long *idx;
   const int *comp;          // direction 0..2 of the D/B component
-  const double *val;        // [step][n] value subtracted this step
+  const double *amp;        // [2 n] amplitude (re, im)
+  const int *gid;           // [n] group (src_vol) index into the current table
+  const double *J;          // [2 ngroups] this step's current of every group
+  double dt;
+  int nlayer;
+  const int *layer;         // host array: layer start offsets [nlayer + 1]
 };
 
 struct ISrcDev {             // integrated sources, read by the E kernel

@@ -790,14 +790,19 @@ struct Ptr3 {
   double *p[3];
   const double *ci[3];
 };
-__global__ void source_kernel(Ptr3 pt, SrcDev s, int step) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  const double *v = s.val + (long long)step * s.n;
-  for (int k = 0; k < s.n; k++) {
-    const int c = s.comp[k];
-    const long long i = s.idx[k];
-    pt.p[c][i] -= pt.ci[c] ? v[k] * pt.ci[c][i] : v[k];
-  }
+// f[c][i] -= real((amp * current) * dt) [* cndinv[i]] for the points [k0, k1)
+// of one layer (src/step.cpp:296-319; complex products as std::complex<double>,
+// no contraction)
+__global__ void source_kernel(Ptr3 pt, SrcDev s, int k0, int k1) {
+  const int k = k0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (k >= k1) return;
+  const int c = s.comp[k];
+  const long long i = s.idx[k];
+  const int g = s.gid[k];
+  const double ar = s.amp[2 * k], ai = s.amp[2 * k + 1];
+  const double jr = s.J[2 * g], ji = s.J[2 * g + 1];
+  const double v = (ar * jr - ai * ji) * s.dt;
+  pt.p[c][i] -= pt.ci[c] ? v * pt.ci[c][i] : v;
 }
 
 __global__ void fill_kernel(double *p, double v, size_t n) {
@@ -1007,7 +1012,12 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
     pt.p[d] = ft == T_D ? f.Dn[d] : f.Bn[d];
     pt.ci[d] = f.cndinv[ft == T_D][d];
   }
-  source_kernel<<<1, 64, 0, (hipStream_t)stream>>>(pt, s, step);
+  (void)step;
+  for (int l = 0; l < s.nlayer; l++) {
+    const int k0 = s.layer[l], k1 = s.layer[l + 1];
+    if (k1 <= k0) continue;
+    source_kernel<<<(unsigned)((k1 - k0 + 255) / 256), 256, 0, (hipStream_t)stream>>>(pt, s, k0, k1);
+  }
   return rc();
 }
 

@@ -190,27 +190,81 @@ class CustomSource(SourceTime):
 
 
 class Source:
+    """python/source.py:22-158: a current source over the volume (center, size) --
+    a point, line, plane or box -- with an optional amplitude function
+    amp_func(Vector3 relative to the center) -> complex."""
+
     def __init__(self, src, component, center=None, volume=None, size=Vector3(), amplitude=1.0,
-                 amp_func=None):
+                 amp_func=None, amp_func_file=None, amp_data=None):
+        if center is None and volume is None:
+            raise ValueError("Source requires either center or volume")
         self.src = src
         self.component = component
         if volume is not None:
             center, size = volume.center, volume.size
-        self.center = Vector3(*(center if center is not None else (0, 0, 0)))
+        self.center = Vector3(*center)
         self.size = Vector3(*size)
         self.amplitude = complex(amplitude)
-        if amp_func is not None or any(v != 0 for v in self.size):
-            raise NotImplementedError("only point sources (size 0, no amp_func) are in scope")
+        self.amp_func = amp_func
+        self.amp_data = None if amp_data is None else np.asarray(amp_data, dtype=np.complex128)
+        if amp_func_file is not None:
+            raise NotImplementedError("amp_func_file (HDF5 amplitude profiles): no HDF5 in this "
+                                      "build; pass the array as amp_data")
 
-    def add_source(self, fields):  # python/source.py:132-158
+    def _amp_data_func(self):
+        """amp_file_func (src/sources.cpp:347-374): the array linearly interpolated
+        over the source volume (map_coordinates / linear_interpolate,
+        src/fields.cpp:767-825, mirror boundaries)."""
+        a = self.amp_data
+        while a.ndim < 3:
+            a = a[..., None]
+        nx, ny, nz = a.shape
+        re, im = np.ascontiguousarray(a.real).ravel(), np.ascontiguousarray(a.imag).ravel()
+        size = self.size
+
+        def mirror(i, n):
+            return 2 * n - 1 - i if i >= n else (-1 - i if i < 0 else i)
+
+        def coords(r, n):
+            r = -r if r < 0.0 else (1.0 - r if r > 1.0 else r)
+            i1 = mirror(int(r * n), n)
+            d = r * n - i1 - 0.5
+            i2 = mirror(i1 + 1 if d >= 0.0 else i1 - 1, n)
+            return i1, i2, abs(d)
+
+        def interp(data, rx, ry, rz):
+            x1, x2, dx = coords(rx, nx)
+            y1, y2, dy = coords(ry, ny)
+            z1, z2, dz = coords(rz, nz)
+
+            def D(x, y, z):
+                return data[(x * ny + y) * nz + z]
+            return (((D(x1, y1, z1) * (1.0 - dx) + D(x2, y1, z1) * dx) * (1.0 - dy) +
+                     (D(x1, y2, z1) * (1.0 - dx) + D(x2, y2, z1) * dx) * dy) * (1.0 - dz) +
+                    ((D(x1, y1, z2) * (1.0 - dx) + D(x2, y1, z2) * dx) * (1.0 - dy) +
+                     (D(x1, y2, z2) * (1.0 - dx) + D(x2, y2, z2) * dx) * dy) * dz)
+
+        def f(p):
+            r = [0.0 if size[d] == 0 else 0.5 + p[d] / size[d] for d in range(3)]
+            return complex(interp(re, *r), interp(im, *r))
+        return f
+
+    def add_source(self, fields):  # python/source.py:132-158 -> fields::add_volume_source
+        lo = tuple(c - 0.5 * s for c, s in zip(self.center, self.size))
+        hi = tuple(c + 0.5 * s for c, s in zip(self.center, self.size))
+        af = None
+        if self.amp_func is not None:
+            af = (lambda f: lambda r: f(Vector3(*r)))(self.amp_func)
+        elif self.amp_data is not None:
+            af = self._amp_data_func()
         if isinstance(self.src, CustomSource):
-            fields.add_custom_source(self.component, self.src.src_func, self.src.start_time,
-                                     self.src.end_time, tuple(self.center), self.amplitude,
-                                     self.src.is_integrated)
+            fields.add_custom_volume_source(self.component, self.src.src_func, self.src.start_time,
+                                            self.src.end_time, lo, hi, self.amplitude,
+                                            self.src.is_integrated, af)
             return
         kind, p = self.src.params()
-        fields.add_point_source(self.component, kind, p, tuple(self.center), self.amplitude,
-                                self.src.is_integrated)
+        fields.add_volume_source(self.component, kind, p, lo, hi, self.amplitude,
+                                 self.src.is_integrated, af)
 
 
 # ---------------------------------------------------------------- flux monitors

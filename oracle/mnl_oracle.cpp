@@ -1409,24 +1409,45 @@ realnum field_at(orc_sim *s, int c, const int p[3]) {  // fields::get_field(c, i
 
 // Point-source weights, loop_in_chunks for a zero-size volume
 // (src/loop_in_chunks.cpp:339-500, 263-300; src/sources.cpp:243-312).
-void add_point_source_impl(orc_sim *s, int c, int st, const double pos[3], cplx amp0) {
+void boundary_weights(const GV &G, const double wmin[3], const double wmax[3], const int is[3],
+                      const int ie[3], double s0[3], double e0[3], double s1[3], double e1[3]);
+typedef void (*orc_amp_func)(const double rel[3], void *data, double *re, double *im);
+
+// fields::add_volume_source(c, src, where, A, amp) (src/sources.cpp:455-494) and
+// src_vol_chunkloop (243-312): where clamped to the cell, delta-function
+// directions scale amp by a, loop_in_chunks on c's grid without symmetry, one
+// src_vol per chunk with IVEC_LOOP_WEIGHT * amp * A(loc - center) per owned point.
+int add_volume_source_impl(orc_sim *s, int c, int st, const double wmin0[3], const double wmax0[3],
+                           cplx amp0, orc_amp_func afunc, void *adata) {
   const GV &G = s->gv;
+  double wmin[3], wmax[3];
+  for (int d = 0; d < 3; d++) {
+    wmin[d] = G.has[d] ? wmin0[d] : 0.0;
+    wmax[d] = G.has[d] ? wmax0[d] : 0.0;
+    if (!G.has[d]) continue;
+    const double w = G.n[d] * G.inva, wd = wmax[d] - wmin[d];
+    if (wd > w + G.inva) return set_err("Source width > cell width");
+    if (wd > w) {
+      const double dw = wd - w;
+      wmin[d] = wmin[d] - dw * 0.5;
+      wmax[d] = wmin[d] + w;
+    }
+  }
   cplx amp = amp0;
   for (int d = 0; d < 3; d++)
-    if (G.has[d]) amp *= G.a;  // delta-function units (sources.cpp:484-487)
+    if (G.has[d] && wmax[d] - wmin[d] == 0.0) amp *= G.a;  // delta-function units
+  double center[3];
+  for (int d = 0; d < 3; d++) center[d] = (wmin[d] + wmax[d]) * 0.5;
   int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
-  double s0[3] = {1, 1, 1}, s1[3] = {1, 1, 1}, e0[3] = {1, 1, 1}, e1[3] = {1, 1, 1};
   for (int d = 0; d < 3; d++) {
     if (!G.has[d]) continue;
-    int iyee_c = 1 - G.shift(c, d);
-    double yee_c = 1 * (0.5 * G.inva) - G.shift(c, d) * (0.5 * G.inva);
-    double P = pos[d] + yee_c;
-    is[d] = 1 + 2 * int(floor(P * G.a - .5)) - iyee_c;
-    ie[d] = 1 + 2 * int(ceil(P * G.a - .5)) - iyee_c;
-    double w0 = 1. - pos[d] * G.a + 0.5 * is[d];
-    double w1 = 1. + pos[d] * G.a - 0.5 * ie[d];
-    s0[d] = w0, s1[d] = w1, e0[d] = w1, e1[d] = w0;  // point: "where.min == where.max"
+    const int iyee_c = 1 - G.shift(c, d);
+    const double yee_c = 1 * (0.5 * G.inva) - G.shift(c, d) * (0.5 * G.inva);
+    is[d] = 1 + 2 * int(floor((wmin[d] + yee_c) * G.a - .5)) - iyee_c;
+    ie[d] = 1 + 2 * int(ceil((wmax[d] + yee_c) * G.a - .5)) - iyee_c;
   }
+  double s0[3], s1[3], e0[3], e1[3];
+  boundary_weights(G, wmin, wmax, is, ie, s0, e0, s1, e1);
   for (size_t ci = 0; ci < s->chunks.size(); ci++) {
     Chunk &ch = s->chunks[ci];
     const GV &g = ch.gv;
@@ -1505,7 +1526,14 @@ void add_point_source_impl(orc_sim *s, int c, int st, const double pos[3], cplx 
             if (G.has[yd[k]]) p[yd[k]] = isc[yd[k]] + 2 * ii[k];
           if (!g.owns(p)) continue;
           double wgt = (W1(2, i3) * (W1(1, i2) * ((1.0) * W1(0, i1))));
-          cplx a = wgt * (amp * std::conj(cplx(1.0))) * cplx(1.0);
+          cplx A = 1.0;
+          if (afunc) {
+            double rel[3], re = 0, im = 0;
+            for (int d = 0; d < 3; d++) rel[d] = G.has[d] ? p[d] * (0.5 * G.inva) - center[d] : 0.0;
+            afunc(rel, adata, &re, &im);
+            A = cplx(re, im);
+          }
+          cplx a = wgt * (amp * std::conj(cplx(1.0))) * A;
           sv.idx.push_back(g.index(c, p));
           sv.amp.push_back(a);
         }
@@ -1519,6 +1547,11 @@ void add_point_source_impl(orc_sim *s, int c, int st, const double pos[3], cplx 
       }
     if (!merged) list.push_back(std::move(sv));
   }
+  return 0;
+}
+
+void add_point_source_impl(orc_sim *s, int c, int st, const double pos[3], cplx amp0) {
+  add_volume_source_impl(s, c, st, pos, pos, amp0, nullptr, nullptr);
 }
 
 int check_comp(const orc_sim *s, int c) {
@@ -1716,6 +1749,24 @@ int orc_initialize_field(orc_sim *s, int comp, const double *vals) {
   return 0;
 }
 
+int orc_add_custom_volume_source(orc_sim *s, int comp,
+                                 void (*func)(double, void *, double *, double *), void *data,
+                                 double start_time, double end_time, const double vmin[3],
+                                 const double vmax[3], double amp_re, double amp_im,
+                                 int is_integrated,
+                                 void (*afunc)(const double *, void *, double *, double *),
+                                 void *adata) {
+  if (!func) return set_err("custom source needs a function");
+  const double p[2] = {start_time, end_time};
+  s->pending_func = func;
+  s->pending_fdata = data;
+  int rc = orc_add_volume_source(s, comp, 2, p, 2, vmin, vmax, amp_re, amp_im, is_integrated,
+                                 afunc, adata);
+  s->pending_func = nullptr;
+  s->pending_fdata = nullptr;
+  return rc;
+}
+
 int orc_add_custom_point_source(orc_sim *s, int comp,
                                 void (*func)(double, void *, double *, double *), void *data,
                                 double start_time, double end_time, const double pos[3],
@@ -1732,6 +1783,14 @@ int orc_add_custom_point_source(orc_sim *s, int comp,
 
 int orc_add_point_source(orc_sim *s, int comp, int kind, const double *p, int np,
                          const double pos[3], double amp_re, double amp_im, int is_integrated) {
+  return orc_add_volume_source(s, comp, kind, p, np, pos, pos, amp_re, amp_im, is_integrated,
+                               nullptr, nullptr);
+}
+
+int orc_add_volume_source(orc_sim *s, int comp, int kind, const double *p, int np,
+                          const double vmin[3], const double vmax[3], double amp_re, double amp_im,
+                          int is_integrated,
+                          void (*afunc)(const double *, void *, double *, double *), void *adata) {
   if (check_comp(s, comp)) return -1;
   if (!(is_electric(comp) || is_magnetic(comp))) return set_err("sources must be E or H components");
   finalize(s);
@@ -1765,11 +1824,11 @@ int orc_add_point_source(orc_sim *s, int comp, int kind, const double *p, int np
     s->srcs.push_back(st);
     idx = int(s->srcs.size()) - 1;
   }
-  double ppos[3] = {pos[0], pos[1], pos[2]};
-  if (s->gv.dim == 1) ppos[0] = ppos[1] = 0;
-  if (s->gv.dim == 2) ppos[2] = 0;
+  double lo[3] = {vmin[0], vmin[1], vmin[2]}, hi[3] = {vmax[0], vmax[1], vmax[2]};
+  if (s->gv.dim == 1) lo[0] = lo[1] = hi[0] = hi[1] = 0;
+  if (s->gv.dim == 2) lo[2] = hi[2] = 0;
   require_component(s, comp);
-  add_point_source_impl(s, comp, idx, ppos, cplx(amp_re, amp_im));
+  if (add_volume_source_impl(s, comp, idx, lo, hi, cplx(amp_re, amp_im), afunc, adata)) return -1;
   s->conn_valid = false;
   return 0;
 }

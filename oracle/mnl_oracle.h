@@ -39,6 +39,19 @@ int orc_add_custom_point_source(orc_sim *s, int comp,
                                 void (*func)(double, void *, double *, double *), void *data,
                                 double start_time, double end_time, const double pos[3],
                                 double amp_re, double amp_im, int is_integrated);
+/* fields::add_volume_source(c, src, volume(vmin, vmax), A, amp) (src/sources.cpp:
+ * 455-494); afunc (NULL = 1) gets the position relative to the volume centre */
+int orc_add_volume_source(orc_sim *s, int comp, int kind, const double *params, int nparams,
+                          const double vmin[3], const double vmax[3], double amp_re, double amp_im,
+                          int is_integrated,
+                          void (*afunc)(const double *, void *, double *, double *), void *adata);
+int orc_add_custom_volume_source(orc_sim *s, int comp,
+                                 void (*func)(double, void *, double *, double *), void *data,
+                                 double start_time, double end_time, const double vmin[3],
+                                 const double vmax[3], double amp_re, double amp_im,
+                                 int is_integrated,
+                                 void (*afunc)(const double *, void *, double *, double *),
+                                 void *adata);
 int orc_require_component(orc_sim *s, int comp);
 /* fields::initialize_field (src/initialize.cpp:135-161), func's real values as a
  * whole-cell array */

@@ -54,6 +54,11 @@ def lib():
         L.orc_add_point_source.argtypes = [c_void, c_int, c_int, dptr, c_int, dptr, c_double,
                                            c_double, c_int]
         L.orc_require_component.argtypes = [c_void, c_int]
+        L.orc_add_volume_source.argtypes = [c_void, c_int, c_int, dptr, c_int, dptr, dptr,
+                                            c_double, c_double, c_int, AMP_FUNC, ctypes.c_void_p]
+        L.orc_add_custom_volume_source.argtypes = [c_void, c_int, SRC_FUNC, ctypes.c_void_p,
+                                                   c_double, c_double, dptr, dptr, c_double,
+                                                   c_double, c_int, AMP_FUNC, ctypes.c_void_p]
         L.orc_initialize_field.argtypes = [c_void, c_int, dptr]
         L.orc_energy_in_box.argtypes = [c_void, c_int, dptr, dptr, dptr]
         L.orc_step.argtypes = [c_void, c_int]
@@ -80,6 +85,8 @@ def lib():
 
 
 SRC_FUNC = ctypes.CFUNCTYPE(None, ctypes.c_double, ctypes.c_void_p,
+                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double))
+AMP_FUNC = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p,
                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double))
 
 
@@ -225,6 +232,49 @@ class Oracle:
         amp = complex(amp)
         _chk(lib().orc_add_point_source(self.h, comp, kind, _dp(p), len(p), _dp(pos), amp.real,
                                         amp.imag, int(is_integrated)))
+
+    def _amp_cb(self, amp_func):
+        if amp_func is None:
+            return AMP_FUNC()
+        def _cb(rel, _data, re, im, f=amp_func):
+            v = complex(f((rel[0], rel[1], rel[2])))
+            re[0] = v.real
+            im[0] = v.imag
+        cb = AMP_FUNC(_cb)
+        self.__dict__.setdefault("_amp_cbs", []).append(cb)
+        return cb
+
+    def add_volume_source(self, comp, kind, params, vmin, vmax, amp=1.0, is_integrated=False,
+                          amp_func=None):
+        """fields::add_volume_source (src/sources.cpp:455-494)."""
+        p = np.ascontiguousarray(params, dtype=np.float64)
+        lo = np.ascontiguousarray(list(vmin) + [0.0] * (3 - len(vmin)), dtype=np.float64)
+        hi = np.ascontiguousarray(list(vmax) + [0.0] * (3 - len(vmax)), dtype=np.float64)
+        a = complex(amp)
+        _chk(lib().orc_add_volume_source(self.h, comp, kind, _dp(p), len(p), _dp(lo), _dp(hi),
+                                         a.real, a.imag, int(is_integrated),
+                                         self._amp_cb(amp_func), None))
+
+    def add_custom_volume_source(self, comp, func, start, end, vmin, vmax, amp=1.0,
+                                 is_integrated=False, amp_func=None):
+        cbs = self.__dict__.setdefault("_custom_cbs", {})
+        if id(func) not in cbs:
+            def _cb(t, _data, re, im, func=func):
+                v = complex(func(t))
+                re[0] = v.real
+                im[0] = v.imag
+            cbs[id(func)] = (func, SRC_FUNC(_cb))
+        lo = np.ascontiguousarray(list(vmin) + [0.0] * (3 - len(vmin)), dtype=np.float64)
+        hi = np.ascontiguousarray(list(vmax) + [0.0] * (3 - len(vmax)), dtype=np.float64)
+        a = complex(amp)
+        _chk(lib().orc_add_custom_volume_source(self.h, comp, cbs[id(func)][1], None, float(start),
+                                                float(end), _dp(lo), _dp(hi), a.real, a.imag,
+                                                int(is_integrated), self._amp_cb(amp_func), None))
+
+    def add_gaussian_volume_source(self, comp, freq, width, start, end, vmin, vmax, amp=1.0,
+                                   is_integrated=False, amp_func=None):
+        self.add_volume_source(comp, 0, [freq, width, start, end], vmin, vmax, amp, is_integrated,
+                               amp_func)
 
     def add_gaussian_source(self, comp, freq, width, start, end, pos, amp=1.0,
                             is_integrated=False):

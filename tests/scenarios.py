@@ -72,6 +72,15 @@ class ProductSim:
     def add_continuous_source(self, *a, **k):
         self._fields().add_continuous_source(*a, **k)
 
+    def add_volume_source(self, *a, **k):
+        self._fields().add_volume_source(*a, **k)
+
+    def add_gaussian_volume_source(self, *a, **k):
+        self._fields().add_gaussian_volume_source(*a, **k)
+
+    def add_custom_volume_source(self, *a, **k):
+        self._fields().add_custom_volume_source(*a, **k)
+
     def add_custom_source(self, *a, **k):
         self._fields().add_custom_source(*a, **k)
 
@@ -195,6 +204,18 @@ class GroupSim(ProductSim):
     def add_continuous_source(self, *a, **k):
         for f in self._all():
             f.add_continuous_source(*a, **k)
+
+    def add_volume_source(self, *a, **k):
+        for f in self._all():
+            f.add_volume_source(*a, **k)
+
+    def add_gaussian_volume_source(self, *a, **k):
+        for f in self._all():
+            f.add_gaussian_volume_source(*a, **k)
+
+    def add_custom_volume_source(self, *a, **k):
+        for f in self._all():
+            f.add_custom_volume_source(*a, **k)
 
     def legacy_point_source(self, *a, **k):
         for f in self._all():

@@ -76,5 +76,11 @@ def test_simulation_setup_host_side(libpath):
         sources=[mp.Source(mp.GaussianSource(0.15, fwidth=0.1), mp.Ez, center=mp.Vector3())])
     s = sim._init_structure()
     assert s.gv.n == [16, 16, 16] and s.gv.io == [-16, -16, -16]
+    src = mp.Source(mp.GaussianSource(1.0, fwidth=1.0), mp.Ez, center=mp.Vector3(),
+                    size=mp.Vector3(1, 0, 0))  # line sources are in scope
+    assert src.size.x == 1
+    with pytest.raises(ValueError):
+        mp.Source(mp.GaussianSource(1.0, fwidth=1.0), mp.Ez)  # neither center nor volume
     with pytest.raises(NotImplementedError):
-        mp.Source(mp.GaussianSource(1.0, fwidth=1.0), mp.Ez, size=mp.Vector3(1, 0, 0))
+        mp.Source(mp.GaussianSource(1.0, fwidth=1.0), mp.Ez, center=mp.Vector3(),
+                  amp_func_file="x.h5:amp")
