@@ -9,6 +9,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmnl.so")
+if os.environ.get("MNL_LIB_VARIANT"):  # A/B experiments: meep_nl_amd/variants/<name>/libmnl.so
+    LIB_PATH = os.path.join(_HERE, "variants", os.environ["MNL_LIB_VARIANT"], "libmnl.so")
 _LIB = None
 
 c_int, c_double, c_void, c_size = ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t

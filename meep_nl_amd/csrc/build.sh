@@ -3,14 +3,14 @@
 # g++ for the host side (see mnl_host.cpp header for why).
 set -e
 HERE="$(cd "$(dirname "$0")" && pwd)"
-OUT="$HERE/../libmnl.so"
+OUT=${MNL_OUT:-"$HERE/../libmnl.so"}
 ROCM=${ROCM_PATH:-/opt/rocm}
-TMP="$HERE/_obj"
+TMP=${MNL_OBJ:-"$HERE/_obj"}
 mkdir -p "$TMP"
 ARCH=${MNL_ARCH:-gfx950}
-hipcc --offload-arch=$ARCH -O3 -ffp-contract=off -fPIC -std=c++17 -Wall \
+hipcc --offload-arch=$ARCH $MNL_KFLAGS -O3 -ffp-contract=off -fPIC -std=c++17 -Wall \
   -c "$HERE/mnl_kernels.hip" -o "$TMP/mnl_kernels.o"
-CXXF="-O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$ROCM/include"
+CXXF="$MNL_KFLAGS -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$ROCM/include"
 g++ $CXXF -c "$HERE/mnl_host.cpp" -o "$TMP/mnl_host.o"
 g++ $CXXF -c "$HERE/mnl_comm.cpp" -o "$TMP/mnl_comm.o"
 # Link with g++ so the host's complex arithmetic (__muldc3 / __divdc3 of

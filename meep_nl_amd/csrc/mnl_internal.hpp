@@ -205,9 +205,19 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
 // a PML chunk along the E direction (then it is stored, ping-pong).
 constexpr int FUSED_MAXX = 64, FUSED_MAXY = 160, FUSED_MAXZ = 160;
 constexpr int FUSED_MAXCH = 64;  // longest general chunk (planes)
-constexpr int FUSED_MAXGY = 160, FUSED_MAXNY = 64;
-constexpr int FUSED_GW_ROWS = 10;  // general kernel, wide tiles: own rows per tile
-constexpr int FUSED_GN_ROWS = 39;  // general kernel, 16-column tiles: own rows per tile
+constexpr int FUSED_MAXGY = 256, FUSED_MAXNY = 64;
+#ifndef MNL_GW_ROWS
+#define MNL_GW_ROWS 10
+#endif
+#ifndef MNL_GN_ROWS
+#define MNL_GN_ROWS 39
+#endif
+#ifndef MNL_GEN_BPC
+#define MNL_GEN_BPC 1
+#endif
+constexpr int FUSED_GW_ROWS = MNL_GW_ROWS;  // general kernel, wide tiles: own rows per tile
+constexpr int FUSED_GN_ROWS = MNL_GN_ROWS;  // general kernel, 16-column tiles: own rows per tile
+constexpr int FUSED_GEN_BPC = MNL_GEN_BPC;  // general kernel workgroups per CU
 struct FusedTab {                // per direction, indexed by global half-coordinate q
   const uint8_t *flag[3];        // PML chunk along the direction (f_u / W branches)
   const double *kms[3];          // kap - sig

@@ -2057,7 +2057,7 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
     int wb = 0, we = a.ngen, nb_ = a.ngen, ne = a.ngen + a.ngen_n, line = 8;
     if (which == 2) we = a.ngen_e, ne = a.ngen + a.ngen_ne, line = 10;
     if (which == 3) wb = a.ngen_e, nb_ = a.ngen + a.ngen_ne;
-    long long cus = fused_grid_blocks(1);
+    long long cus = fused_grid_blocks(FUSED_GEN_BPC);
     if (a.wg_limit > 0 && cus > a.wg_limit) cus = a.wg_limit;
     FusedArgs g = a;
     // set up one launch over items [ib, ie) on counter line ln (grouped per XCD

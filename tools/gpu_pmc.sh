@@ -7,7 +7,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 TAG=${TAG:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --no-cpu}
+ARGS=${BENCH_ARGS:---steps 10 --warmup 2 --no-cpu --no-extra}
 run() {  # run <name> <rocprof args...>
   local name=$1; shift
   echo "=== $name"
