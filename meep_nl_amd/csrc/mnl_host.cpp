@@ -806,13 +806,20 @@ int setup_materials(mnl_fields *F) {
       for (const auto *v : {&S.chi2[c], &S.chi3[c]})
         if (!v->empty() && !all_eq(*v, 0.0)) F->upnl = true;
     for (auto &b : S.boxes) F->upnl = F->upnl || ((b.kind == 1 || b.kind == 2) && b.value != 0.0);
-    for (int c = 0; c < 3 && F->upnl; c++)
+    // off-diagonal chi1inv rows: the upstream OFFDIAG averages (step_generic.cpp:597-598)
+    for (int c = 0; c < 3; c++)
       for (int k = 1; k <= 2; k++) {
         const auto &od = S.chi1inv[c][(c + k) % 3];
-        if (!od.empty() && !all_eq(od, 0.0))
-          return fail("upstream nonlinear mode: off-diagonal epsilon is not supported");
+        if (!od.empty() && !all_eq(od, 0.0)) F->upnl = true;
       }
   }
+  auto has_offd = [&](int c) {
+    for (int k = 1; k <= 2; k++) {
+      const auto &od = S.chi1inv[c][(c + k) % 3];
+      if (!od.empty() && !all_eq(od, 0.0)) return true;
+    }
+    return false;
+  };
   // chi2 nontrivial on component c: a host array or a chi2 box (rasterised below)
   bool box_chi2 = false;
   for (auto &b : S.boxes) box_chi2 = box_chi2 || (b.kind == 1 && b.value != 0.0);
@@ -829,7 +836,8 @@ int setup_materials(mnl_fields *F) {
   for (int c = 0; c < 3; c++) {
     if (!has_field(S, c)) continue;
     const auto &diag = S.chi1inv[c][c];
-    bool need = (!diag.empty() && !all_eq(diag, 1.0)) || F->nr || box_eps;
+    bool need = (!diag.empty() && !all_eq(diag, 1.0)) || F->nr || box_eps ||
+                (F->upnl && has_offd(c));
     if (need) {
       double *p;
       if (dev_alloc(F, &p, F->nlocal)) return -1;
@@ -839,11 +847,11 @@ int setup_materials(mnl_fields *F) {
         return fail("fill failed");
       f.inveps[c] = p;
     }
-    if (F->nr) {
+    if (F->nr || F->upnl) {
       for (int k = 0; k < 2; k++) {
         int dd = (c + 1 + k) % 3;
         const auto &od = S.chi1inv[c][dd];
-        if (od.empty()) continue;
+        if (od.empty() || (F->upnl && all_eq(od, 0.0))) continue;
         double *p;
         if (dev_alloc(F, &p, F->nlocal)) return -1;
         if (upload_canonical(F, p, od, c)) return -1;
@@ -868,7 +876,7 @@ int setup_materials(mnl_fields *F) {
   }
   // offdiag presence per reference chunk (zone box)
   std::vector<uint8_t> oz(27, 0);
-  if (F->nr) {
+  if (F->nr || F->upnl) {
     std::vector<ZoneIv> ivs[3];
     for (int d = 0; d < 3; d++) {
       if (S.has[d])
@@ -994,6 +1002,13 @@ int setup_materials(mnl_fields *F) {
         f.pol[k].nz.hi[e] = init[6 * k + 3 + e];
       }
   }
+  // The E update reaches the high metallic wall planes the reference's chunks own
+  // (zeroed only afterwards by step_boundaries): with D = 0 there, E is nonzero
+  // only through neighbour reads (OFFDIAG, Newton-Raphson), and only a
+  // polarization keeps what update_P reads of it.
+  bool any_offd = false;
+  for (int c = 0; c < 3; c++) any_offd = any_offd || f.offd[c][0] || f.offd[c][1];
+  f.wall_e = ((F->upnl && any_offd) || F->nr) && f.npol > 0 ? 1 : 0;
   HIPCHK(hipStreamSynchronize(F->stream));
   return 0;
 }
@@ -1262,7 +1277,11 @@ int build_source_lists(mnl_fields *F) {
       if (st.is_integrated && !mag) {
         // integrated dipoles are read (never written): keep the rank's ghost copies
         // too, so a slab seam sees what one GPU sees; the zone box restricts the
-        // subtraction to readers in the owning reference chunk
+        // subtraction to readers in the owning reference chunk.  A dipole on the
+        // high metallic wall plane stays: the chunk owns that point and its
+        // f_minus_p there (D = 0 minus the dipole) is read by neighbours through
+        // the Newton-Raphson / OFFDIAG sums (src/update_eh.cpp:136-146).
+        li = local_index(F, tgt, jg, true);
         if (li < 0 && F->nranks > 1) {
           bool wall = false;  // high PEC wall of an unshifted direction: nobody owns it
           for (int d = 0; d < 3; d++)
@@ -2749,7 +2768,8 @@ int step_batch(mnl_fields *F, int nsteps) {
       if ((!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) ||
           (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream)))
         return fail("update E launch failed");
-      if (f.aniso && k_aniso_wall(g, f, 0, F->stream)) return fail("wall W launch failed");
+      if (f.aniso && !f.wall_e && k_aniso_wall(g, f, 0, F->stream))
+        return fail("wall W launch failed");
       if (f.aniso && F->nranks > 1 && exchange(F, 4))  // WE_stuff ghosts (step.cpp:111-114)
         return fail("W halo exchange failed");
       if (!fuse && f.npol) {
@@ -2757,7 +2777,8 @@ int step_batch(mnl_fields *F, int nsteps) {
             k_update_pols(F->interior, sl, g, f, F->stream))
           return fail("pols launch failed");
       }
-      if (f.aniso && k_aniso_wall(g, f, 1, F->stream)) return fail("wall W launch failed");
+      if ((f.aniso || f.wall_e) && k_aniso_wall(g, f, 1, F->stream))
+        return fail("wall W launch failed");
       ev_end(k);
       if (F->fused)
         for (int d = 0; d < 3; d++) {
@@ -3594,6 +3615,7 @@ int initialize_field(mnl_fields *F, int c, const double *host) {
     if (k_update_e(F->interior, nullptr, F->g, f, is, 0, false, F->stream) ||
         k_update_e(F->interior, &F->shell_list, F->g, f, is, 0, false, F->stream))
       return fail("update E launch failed");
+    if (f.wall_e && k_aniso_wall(F->g, f, 1, F->stream)) return fail("wall E launch failed");
     if (F->nranks > 1 && exchange(F, 0)) return fail("E halo exchange failed");
   } else if (t == T_B) {  // update_eh(H_stuff); step_boundaries(H_stuff)
     if (!F->h_first_done && h_lazy_copy(F)) return -1;

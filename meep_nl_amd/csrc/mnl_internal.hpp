@@ -97,6 +97,7 @@ struct DevFields {
   const double *chi2[3];
   const double *chi3[3];     // upstream nonlinear mode only (the fork's chi3 is inert)
   int upnl;                  // 1: upstream chi2/chi3 Pade update of E (calc_nonlinear_u)
+  int wall_e;                // 1: E / P also on the high metallic wall planes (see update_e_kernel)
   int npol;
   PolDev pol[MAX_POL];       // in reference pol-list order (reverse of add order)
   PmlDev pml;

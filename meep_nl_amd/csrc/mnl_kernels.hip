@@ -446,6 +446,40 @@ __device__ __forceinline__ unsigned pol_mask(const DevFields &f, const Pt &p) {
   return m;
 }
 
+// Owned by the reference's chunk although the kernels never update it: the high
+// metallic wall plane of a component unshifted along the wall normal
+// (little_owned_corner0..big_corner includes it, src/meep/vec.hpp:1102-1104;
+// zero_metal zeroes f there only in step_boundaries, src/boundaries.cpp:304-339).
+// glob: the whole-cell owned ranges (a neighbour rank's plane counts as owned)
+__device__ __forceinline__ bool on_wall(const DevGrid &g, int c, const Pt &p, bool glob = false) {
+  bool wall = false;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (g.ax[d] < 0) continue;
+    const bool sh = d == c;
+    if (!sh && g.wall[d] && p.j[d] + g.off[d] == g.nglob[d]) {
+      wall = true;
+      continue;
+    }
+    if (glob) {
+      const int jg = p.j[d] + g.off[d];
+      if (jg < (sh ? 0 : 1) || jg > g.nglob[d] - 1) return false;
+    } else {
+      const int lo = sh ? g.owned_lo_sh[d] : g.owned_lo_un[d];
+      const int hi = sh ? g.owned_hi_sh[d] : g.owned_hi_un[d];
+      if (p.j[d] < lo || p.j[d] > hi) return false;
+    }
+  }
+  return wall;
+}
+
+__device__ __forceinline__ int zone_box(const DevFields &f, const DevGrid &g, const Pt &p, int c) {
+  int zb = 0;
+#pragma unroll
+  for (int e = 0; e < 3; e++) zb = zb * 3 + (g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, c, e)] : 1);
+  return zb;
+}
+
 // f_minus_p at the point itself, skipping polarizations that are 0 there
 template <bool ISRC>
 __device__ __forceinline__ double dmp_own(const DevFields &f, const ISrcDev &is, int step, int c,
@@ -501,16 +535,36 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     if (!f.ecomp_present[d]) continue;
-    if (!owned(g, T_E, d, p)) continue;
+    // wall_e: also the high metallic wall plane, which the reference's chunk owns
+    // and updates (D = 0 there) before step_boundaries zeroes it; the transient
+    // E feeds update_P there (aniso_wall_kernel zeroes it afterwards)
+    if (!owned(g, T_E, d, p) && !(f.wall_e && on_wall(g, d, p))) continue;
     const double gs = dmp_own<ISRC>(f, is, step, d, i, pm);
     // reference chunk of this voxel (zone box; interior kernels: 13 = interior chunk)
     int rz = 13;
-    if (SHELL && (NR || ISRC)) {
+    if ((SHELL && (NR || ISRC || f.upnl)) || f.wall_e) {
       int z3[3];
 #pragma unroll
       for (int e = 0; e < 3; e++) z3[e] = g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, d, e)] : 1;
       rz = z3[0] * 9 + z3[1] * 3 + z3[2];
     }
+    // D - P of component e at i [+ s along d] [- s_e along e] as chunk rz holds it:
+    // a wall point another chunk owns is never connected (boundaries.cpp:347-460),
+    // so the reader's copy there stays 0
+    auto nbr = [&](int e, bool up, bool dn) -> double {
+      long long n = i;
+      Pt q = p;
+      if (up) {
+        n += g.sdir[d];
+        if (g.ax[d] >= 0) q.j[d] += 1;
+      }
+      if (dn) {
+        n -= g.sdir[e];
+        if (g.ax[e] >= 0) q.j[e] -= 1;
+      }
+      if (f.wall_e && on_wall(g, e, q, true) && zone_box(f, g, q, e) != rz) return 0.0;
+      return dmp_at<ISRC>(f, is, step, e, n, rz);
+    };
     const double *u = f.inveps[d];
     const double *E = f.E[d];
     double *En = f.En[d];
@@ -521,28 +575,49 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
       pml = pml_at(f, g, d, kw);
     }
     double wv;  // the W field read by update_pols (f_w if allocated, else E)
-    double unl = 0;  // upstream mode: (g*u) * calc_nonlinear_u(...) (step_generic.cpp:668-702,
-                     // 853-884 as the fork comments them out; u = 1 where trivial)
+    double unl = 0;  // upstream mode: step_update_EDHB as upstream Meep runs it
+                     // (src/step_generic.cpp:597-726, 730-886 with the fork's disabled
+                     // branches restored; u = 1 where trivial)
     if (f.upnl) {
       const int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
       const long long s = g.sdir[d];
       auto nsum = [&](int e) {
-        const long long se = g.sdir[e];
-        return dmp_at<ISRC>(f, is, step, e, i, rz) + dmp_at<ISRC>(f, is, step, e, i + s, rz) +
-               dmp_at<ISRC>(f, is, step, e, i - se, rz) +
-               dmp_at<ISRC>(f, is, step, e, i + (s - se), rz);
+        return nbr(e, false, false) + nbr(e, true, false) + nbr(e, false, true) + nbr(e, true, true);
+      };
+      // OFFDIAG(u, g, sx), src/step_generic.cpp:597-598
+      auto offdiag = [&](const double *uo, int e) {
+        return 0.25 * ((nbr(e, false, false) + nbr(e, false, true)) * uo[i] +
+                       (nbr(e, true, false) + nbr(e, true, true)) * uo[i + s]);
       };
       const double us = u ? u[i] : 1.0;
-      double dsq = gs * gs;
       const bool h1 = f.ecomp_present[d1] != 0, h2 = f.ecomp_present[d2] != 0;
-      if (h1 && h2) {
+      // off-diagonal rows this reference chunk keeps (trivial rows are deallocated,
+      // src/anisotropic_averaging.cpp:285-296)
+      const unsigned ob = (f.offd_zone[rz] >> (3 * d)) & 3u;
+      const bool o1 = (ob & 1u) && h1 && f.offd[d][0], o2 = (ob & 2u) && h2 && f.offd[d][1];
+      double v, dsq;
+      if (o1 && o2) {  // 3x3 (617, 772)
+        v = gs * us + offdiag(f.offd[d][0], d1) + offdiag(f.offd[d][1], d2);
         const double g1s = nsum(d1), g2s = nsum(d2);
         dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
-      } else if (h1 || h2) {
-        const double g1s = nsum(h1 ? d1 : d2);
+      } else if (o1 || o2) {  // 2x2, the present row first (590-594, 646, 835)
+        const int e = o1 ? d1 : d2;
+        v = gs * us + offdiag(o1 ? f.offd[d][0] : f.offd[d][1], e);
+        const double g1s = nsum(e);
         dsq = gs * gs + 0.0625 * (g1s * g1s);
+      } else {  // diagonal (668-702, 853-884)
+        v = gs * us;
+        dsq = gs * gs;
+        if (h1 && h2) {
+          const double g1s = nsum(d1), g2s = nsum(d2);
+          dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
+        } else if (h1 || h2) {
+          const double g1s = nsum(h1 ? d1 : d2);
+          dsq = gs * gs + 0.0625 * (g1s * g1s);
+        }
       }
-      unl = (gs * us) * calc_nonlinear_u(dsq, gs, us, f.chi2[d][i], f.chi3[d][i]);
+      // chunks without chi2/chi3 skip the factor; chi2 = chi3 = 0 makes it exactly 1
+      unl = v * calc_nonlinear_u(dsq, gs, us, f.chi2[d][i], f.chi3[d][i]);
     }
     if (pml) {
       double fwprev = f.WE[d][i];
@@ -565,16 +640,11 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
           double chi2new = f.chi2[d][i];
           int zc = (u[i] == 0) + (u1[i] == 0) + (u2[i] == 0);
           if (!(chi2new == 0 || zc > 1)) {
-            const long long s = g.sdir[d], s1 = g.sdir[d1], s2 = g.sdir[d2];
-            double gs_2 = (dmp_at<ISRC>(f, is, step, d1, i, rz) +
-                           dmp_at<ISRC>(f, is, step, d1, i + s, rz) +
-                           dmp_at<ISRC>(f, is, step, d1, i - s1, rz) +
-                           dmp_at<ISRC>(f, is, step, d1, i + (s - s1), rz)) *
+            double gs_2 = (nbr(d1, false, false) + nbr(d1, true, false) + nbr(d1, false, true) +
+                           nbr(d1, true, true)) *
                           0.25;
-            double gs_3 = (dmp_at<ISRC>(f, is, step, d2, i, rz) +
-                           dmp_at<ISRC>(f, is, step, d2, i + s, rz) +
-                           dmp_at<ISRC>(f, is, step, d2, i - s2, rz) +
-                           dmp_at<ISRC>(f, is, step, d2, i + (s - s2), rz)) *
+            double gs_3 = (nbr(d2, false, false) + nbr(d2, true, false) + nbr(d2, false, true) +
+                           nbr(d2, true, true)) *
                           0.25;
             double us = 1 / u[i];
             double us_2 = us, us_3 = us;
@@ -633,7 +703,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, BoxL
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     if (!f.ecomp_present[d]) continue;
-    if (!owned(g, T_E, d, p)) continue;
+    if (!owned(g, T_E, d, p) && !(f.wall_e && on_wall(g, d, p))) continue;
     bool pml = false;
     if (SHELL) pml = pml_at(f, g, d, qcoord(g, p, T_E, d, d));
     const double wv = pml ? f.WE[d][i] : f.En[d][i];
@@ -654,40 +724,6 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_pols_kernel(Box b, BoxL
 // (185-186).  W of a component = f_w where its chunk has PML along its own
 // direction, f elsewhere (update_pols.cpp:44); neighbours read the owner's W,
 // as the WE_stuff ghost exchange (boundaries.cpp:407-408, 508-525) provides.
-// Owned by the reference's chunk although the kernels never update it: the high
-// metallic wall plane of a component unshifted along the wall normal
-// (little_owned_corner0..big_corner includes it, src/meep/vec.hpp:1102-1104;
-// zero_metal zeroes f there only in step_boundaries, src/boundaries.cpp:304-339).
-// glob: the whole-cell owned ranges (a neighbour rank's plane counts as owned)
-__device__ __forceinline__ bool on_wall(const DevGrid &g, int c, const Pt &p, bool glob = false) {
-  bool wall = false;
-#pragma unroll
-  for (int d = 0; d < 3; d++) {
-    if (g.ax[d] < 0) continue;
-    const bool sh = d == c;
-    if (!sh && g.wall[d] && p.j[d] + g.off[d] == g.nglob[d]) {
-      wall = true;
-      continue;
-    }
-    if (glob) {
-      const int jg = p.j[d] + g.off[d];
-      if (jg < (sh ? 0 : 1) || jg > g.nglob[d] - 1) return false;
-    } else {
-      const int lo = sh ? g.owned_lo_sh[d] : g.owned_lo_un[d];
-      const int hi = sh ? g.owned_hi_sh[d] : g.owned_hi_un[d];
-      if (p.j[d] < lo || p.j[d] > hi) return false;
-    }
-  }
-  return wall;
-}
-
-__device__ __forceinline__ int zone_box(const DevFields &f, const DevGrid &g, const Pt &p, int c) {
-  int zb = 0;
-#pragma unroll
-  for (int e = 0; e < 3; e++) zb = zb * 3 + (g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, c, e)] : 1);
-  return zb;
-}
-
 // W of E component c at point q (linear index n) as read by a point of
 // reference chunk zb: f_w where q's chunk has PML along c, f elsewhere
 // (update_pols.cpp:44).  Ghosts hold the owner's W (WE_stuff exchange), except

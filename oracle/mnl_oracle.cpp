@@ -22,14 +22,23 @@
 //     188-281), step_source (src/step.cpp:296-319).
 //   * ghost exchange by copy + PEC zeroing (src/step.cpp:226-288,
 //     src/boundaries.cpp:184-199, 304-339, 347-460).
-//   * source time functions (src/sources.cpp:72-160) and point-source
-//     interpolation weights (src/loop_in_chunks.cpp:263-300, 339-500,
-//     src/sources.cpp:243-312, 455-494), get_field interpolation
-//     (src/vec.cpp:528-621, src/monitor.cpp:127-160).
+//   * source time functions (src/sources.cpp:72-160); point and volume
+//     sources with loop_in_chunks weights per chunk (src/loop_in_chunks.cpp:
+//     263-300, 339-500, src/sources.cpp:243-312, 455-494), amp_func;
+//     get_field interpolation (src/vec.cpp:528-621, src/monitor.cpp:127-160).
+//   * anisotropic (tensor) Lorentzian sigma (src/susceptibility.cpp:188-262
+//     with the offdiagonal neighbour averages), conductivity.
+//   * the upstream chi(2)/chi(3) Pade E update the fork keeps in comments
+//     (set_upstream_nl; src/step_generic.cpp:546-553, 668-702, 853-884).
+//   * initialize_field (src/initialize.cpp:135-161) and the lazy first-update
+//     copies of H / W / f_u (src/update_eh.cpp:67-120, src/step_db.cpp:44-146).
+//   * DFT flux planes (src/dft.cpp:174-300, 533-547, 578-640), field energy
+//     with synchronize_magnetic_fields (src/energy_and_flux.cpp:54-187,
+//     src/integrate.cpp:46-201), array slices (src/array_slice.cpp:251-601).
 //
 // Not restated (out of the configs' scope): cylindrical coordinates, Bloch
-// phases / periodic boundaries, symmetries, magnetic
-// materials, anisotropic Lorentzian, subpixel averaging, DFT/flux.
+// phases / periodic boundaries, symmetries, magnetic materials, subpixel
+// averaging (the structure arrives as per-point chi1inv / sigma arrays).
 //
 // Parity is pinned against the reference's own golden values
 // (tests/known_results.cpp:155-169) and the reference outputs recorded in
@@ -997,28 +1006,54 @@ inline realnum calc_nonlinear_u(realnum Dsqr, realnum Di, realnum chi1inv, realn
   return (1 + c2 + 2 * c3) / (1 + 2 * c2 + 3 * c3);
 }
 
-// Upstream-mode E update with diagonal chi1inv and chi2/chi3: the branches the
-// fork comments out (src/step_generic.cpp:668-702 PML, 853-884 non-PML):
-// f = (g*u) * calc_nonlinear_u(g^2 + (1/16)(g1s^2 + g2s^2), g, u, chi2, chi3),
-// g1s/g2s the four-point sums of the other D components; u = 1 where chi1inv
-// is trivial (deallocated).
-void update_upstream_nl(const GV &g, realnum *f, int fc, const realnum *gg, const realnum *g1,
-                        const realnum *g2, const realnum *u, long sd, long s1, long s2,
-                        const realnum *chi2, const realnum *chi3, realnum *fw, int dsigw,
-                        const realnum *sigw, const realnum *kapw) {
+// Upstream-mode E update: the branches the fork comments out or disables
+// (src/step_generic.cpp:597-726 PML, 730-886 non-PML), as upstream Meep runs
+// them: with off-diagonal chi1inv rows
+//   v = g*u + OFFDIAG(u1, g1, s1) [+ OFFDIAG(u2, g2, s2)]          (617, 632, 659, 772, 823, 844)
+// and, where the chunk has chi3, v *= calc_nonlinear_u(g^2 + (1/16)(g1s^2 [+ g2s^2]), g, u,
+// chi2, chi3) with g1s/g2s the four-point sums of the partner D components; the
+// 2x2 (u1 only) case sums g1 alone.  Diagonal u: v = g*u (u = 1 where trivial),
+// times calc_nonlinear_u with both partner sums present (668-702, 853-884).
+void update_upstream(const GV &g, realnum *f, int fc, const realnum *gg, const realnum *g1,
+                     const realnum *g2, const realnum *u, const realnum *u1, const realnum *u2,
+                     long sd, long s1, long s2, const realnum *chi2, const realnum *chi3,
+                     realnum *fw, int dsigw, const realnum *sigw, const realnum *kapw) {
+  auto offdiag = [&](const realnum *uo, const realnum *go, long sx, long i) -> realnum {
+    return 0.25 * ((go[i] + go[i - sx]) * uo[i] + (go[i + sd] + go[(i + sd) - sx]) * uo[i + sd]);
+  };
   loop_owned(g, fc, [&](long i, const int p[3]) {
     realnum gs = gg[i];
     realnum us = u ? u[i] : 1;
-    realnum dsq = gs * gs;
-    if (g1 && g2) {
-      realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
-      realnum g2s = g2[i] + g2[i + sd] + g2[i - s2] + g2[i + (sd - s2)];
-      dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
-    } else if (g1) {
-      realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
-      dsq = gs * gs + 0.0625 * (g1s * g1s);
+    realnum v;
+    if (u1 && u2) {
+      v = gs * us + offdiag(u1, g1, s1, i) + offdiag(u2, g2, s2, i);
+      if (chi3) {
+        realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
+        realnum g2s = g2[i] + g2[i + sd] + g2[i - s2] + g2[i + (sd - s2)];
+        v = v * calc_nonlinear_u(gs * gs + 0.0625 * (g1s * g1s + g2s * g2s), gs, us, chi2[i],
+                                 chi3[i]);
+      }
+    } else if (u1) {
+      v = gs * us + offdiag(u1, g1, s1, i);
+      if (chi3) {
+        realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
+        v = v * calc_nonlinear_u(gs * gs + 0.0625 * (g1s * g1s), gs, us, chi2[i], chi3[i]);
+      }
+    } else {
+      v = u ? gs * us : gs;
+      if (chi3) {
+        realnum dsq = gs * gs;
+        if (g1 && g2) {
+          realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
+          realnum g2s = g2[i] + g2[i + sd] + g2[i - s2] + g2[i + (sd - s2)];
+          dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
+        } else if (g1) {
+          realnum g1s = g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)];
+          dsq = gs * gs + 0.0625 * (g1s * g1s);
+        }
+        v = (gs * us) * calc_nonlinear_u(dsq, gs, us, chi2[i], chi3[i]);
+      }
     }
-    realnum v = (gs * us) * calc_nonlinear_u(dsq, gs, us, chi2[i], chi3[i]);
     if (dsigw != NO_DIR) {
       int kw = p[dsigw] - g.io[dsigw];
       realnum fwprev = fw[i], kapwkw = kapw[kw], sigwkw = sigw[kw];
@@ -1042,8 +1077,8 @@ void step_update_EDHB(orc_sim *s, const GV &g, realnum *f, int fc, const realnum
     std::swap(u1, u2);
     std::swap(s1, s2);
   }
-  if (s->upstream_nl && chi3 && !u1 && !u2) {
-    update_upstream_nl(g, f, fc, gg, g1, g2, u, sd, s1, s2, chi2, chi3, fw, dsigw, sigw, kapw);
+  if (s->upstream_nl) {
+    update_upstream(g, f, fc, gg, g1, g2, u, u1, u2, sd, s1, s2, chi2, chi3, fw, dsigw, sigw, kapw);
     return;
   }
   if (dsigw != NO_DIR) {  // PML: every u/chi branch reduces to fw = g*u (or g)

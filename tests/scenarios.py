@@ -408,6 +408,24 @@ def sc_nr_probe(make, c2=0.5, steps=40):
     return o
 
 
+def sc_nr_wall_lorentz(make, steps=40):
+    """chi2 Newton-Raphson and a Lorentzian up to the metallic walls (no PML): the
+    reference's chunk updates E on its high wall planes before zeroing them, and
+    update_P keeps what it read there; neighbours see that P through D - P."""
+    o = vol(make, 3, [1.2, 1.0, 1.4], 10)
+    sig = []
+    for c in E_COMPS:
+        for d in range(3):
+            o.set_chi1inv(c, d, np.full(o.shape(), 0.3 if d == c else 2e-3))
+        o.set_chi2(c, np.full(o.shape(), 0.1))
+        sig.append(np.full(o.shape(), 0.3))
+    o.add_lorentzian(1.1, 0.1, sig)
+    o.legacy_point_source(2, 0.6, 0.5, 0.0, 3.0, [1.12, 0.93, 1.31], 1.0)
+    o.add_gaussian_source(0, 0.5, 4.0, 0.0, 30.0, (0.6, 0.95, 0.7), 0.5)
+    o.step(steps)
+    return o
+
+
 def sc_nr_pml_dispersive(make, steps=30):
     """chi2 NR next to a PML with a Lorentzian background and an integrated source
     (exercises the zone tables and the split E / P kernels)."""
@@ -779,11 +797,19 @@ def third_harmonic_1d(make, upstream=True, decay=1e-6):
     return o, o.flux(h1)[0], o.flux(h3)[0]
 
 
+# symmetric off-diagonal chi1inv pairs: value and region (inside the slab)
+OFFD_PAIRS = {(0, 1): (0.04, lambda x, y, z: x < 0.3),
+              (1, 2): (-0.03, lambda x, y, z: y > -0.4),
+              (0, 2): (0.025, lambda x, y, z: z < 0.5)}
+
+
 def sc_upstream_nl_3d(make, steps=50, lorentz=True, isrc=True, chi2=True, pml=True,
-                      upstream=True):
+                      upstream=True, offdiag=False, chi3=True, scale=1.0):
     """Upstream-mode chi2 + chi3 slab (diagonal eps 2.25) crossing the PML boundary,
     a Lorentzian in part of it (D - P neighbour reads), an integrated source and a
-    current source, strong fields (amp 40)."""
+    current source, strong fields (amp 40).  offdiag: symmetric off-diagonal
+    chi1inv pairs, each in its own region (OFFD_PAIRS), so reference chunks keep
+    both rows (3x3), one row (2x2, either order) or none."""
     o = vol(make, 3, [3.2, 3.2, 3.2], 10, center_origin=True)
     if pml:
         o.add_pml(0.8)
@@ -794,14 +820,21 @@ def sc_upstream_nl_3d(make, steps=50, lorentz=True, isrc=True, chi2=True, pml=Tr
         x, y, z = o.coords(c)
         inside = np.abs(z - 0.2) < 0.9
         o.set_chi1inv(c, c, np.where(inside, 1 / 2.25, 1.0))
-        o.set_chi3(c, np.where(inside, 2e-2, 0.0))
+        if chi3:
+            o.set_chi3(c, np.where(inside, 2e-2, 0.0))
+        if offdiag:
+            for k in (1, 2):
+                d = (c + k) % 3
+                val, reg = OFFD_PAIRS[tuple(sorted((c, d)))]
+                o.set_chi1inv(c, d, np.where(inside & reg(x, y, z), val, 0.0))
         if chi2:
             o.set_chi2(c, np.where(inside & (x > -0.5), 3e-2, 0.0))
         sig.append(np.where(inside & (y > 0.2), 0.4, 0.0))
     if lorentz:
         o.add_lorentzian(1.3, 0.08, sig)
-    o.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -0.3), 40.0)
-    o.add_gaussian_source(1, 0.35, 4.0, 0.0, 40.0, (-0.4, 0.25, 0.35), 25.0, is_integrated=isrc)
+    o.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -0.3), 40.0 * scale)
+    o.add_gaussian_source(1, 0.35, 4.0, 0.0, 40.0, (-0.4, 0.25, 0.35), 25.0 * scale,
+                          is_integrated=isrc)
     o.step(steps)
     return o
 

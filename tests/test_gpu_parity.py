@@ -234,3 +234,18 @@ def test_source_values_bitwise(freq, width, end):
         o.step(6)
         res.append(o)
     _bitwise(*res)
+
+
+@pytest.mark.parametrize("G", ["product", "slabs3"])
+def test_nr_lorentz_on_metal_walls(G):
+    """Newton-Raphson E and a Lorentzian reaching the metallic walls: E is updated
+    on the high wall planes the reference's chunks own (D = 0 there, nonzero
+    through the NR neighbour reads), update_P keeps that transient, then the walls
+    are zeroed; across slab seams only the owning chunk sees the wall P."""
+    from scenarios import GroupSim3, sc_nr_wall_lorentz
+    make = ProductSim if G == "product" else GroupSim3
+    p = sc_nr_wall_lorentz(make)
+    o = sc_nr_wall_lorentz(make_oracle)
+    assert float(np.max(np.abs(o.get_array(2)))) > 0
+    assert o.nr_random_fallbacks() == 0  # no random restarts: the streams differ
+    _bitwise(p, o)

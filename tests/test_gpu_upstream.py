@@ -86,3 +86,17 @@ def test_harmonics_cpp_golden_and_scaling(golden):
     assert abs(c2 / a2 - 4.0) <= 0.04 and abs(c3 / a3 - 4.0) <= 0.04
     _, j2, j3 = harmonics_cpp(ProductSim, 0.27e-4, 1e-4, 2.0)
     assert abs(j2 / a2 - 4.0) <= 0.04 and abs(j3 / a3 - 16.0) <= 0.16
+
+
+@pytest.mark.parametrize("chi2,chi3", [(True, True), (False, False), (True, False)])
+def test_upstream_offdiag_bitwise(chi2, chi3):
+    """Off-diagonal chi1inv in upstream mode (OFFDIAG, src/step_generic.cpp:597-598,
+    617, 632, 659, 772, 823, 844): reference chunks with both rows, one row (either
+    order) and none, with and without the Pade factor, PML and non-PML."""
+    kw = dict(offdiag=True, chi2=chi2, chi3=chi3)
+    _bitwise(sc_upstream_nl_3d(ProductSim, **kw), sc_upstream_nl_3d(make_oracle, **kw))
+
+
+def test_upstream_offdiag_slabs():
+    kw = dict(offdiag=True)
+    _bitwise(sc_upstream_nl_3d(GroupSim3, **kw), sc_upstream_nl_3d(make_oracle, **kw))
