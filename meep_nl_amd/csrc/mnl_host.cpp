@@ -1762,10 +1762,14 @@ int dft_flux_values(mnl_fields *F, int h, double *out) {
   DftFluxH &o = *F->dfts[h];
   const size_t nf = o.nfreq;
   std::vector<double> v(2 * ((o.npts + 63) & ~size_t(63)) * nf);
-  if (!v.empty()) {
-    HIPCHK(hipMemcpyAsync(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost, F->stream));
-    HIPCHK(hipStreamSynchronize(F->stream));
-  }
+  bool ok = true;
+  if (!v.empty())
+    ok = hipMemcpyAsync(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost, F->stream) ==
+             hipSuccess &&
+         hipStreamSynchronize(F->stream) == hipSuccess;
+  if (F->nranks > 1 && F->comm->agree_ok(ok, F->stream))  // every rank fails together
+    return fail(ok ? "flux: a rank failed" : "flux: device copy failed");
+  if (!ok) return fail("flux: device copy failed");
   for (size_t i = 0; i < nf; ++i) out[i] = 0;
   for (size_t k = 0; k < o.E.size() && k < o.H.size(); k++)  // dft_flux::flux (src/dft.cpp:533-547)
     for (size_t p = 0; p < o.E[k].N; ++p) {
@@ -1896,15 +1900,19 @@ int get_field(mnl_fields *F, int c, const double pos[3], double *out, bool reduc
   if (F->S.dim == 2) pp[2] = 0;
   interpolate(F->S, c, pp, locs, w);
   cplx res = 0.0;
-  for (int i = 0; i < 8 && w[i]; i++) {
+  bool ok = true;
+  for (int i = 0; i < 8 && w[i] && ok; i++) {
     double v;
-    if (value_at(F, c, locs[i], &v)) return -1;
-    res += w[i] * cplx(v);
+    if (value_at(F, c, locs[i], &v)) ok = false;
+    else res += w[i] * cplx(v);
   }
   double r = real(res);
   if (reduce && F->nranks > 1) {
+    const std::string why = g_err;
+    if (F->comm->agree_ok(ok, F->stream)) return fail(ok ? "get_field: a rank failed" : why);
     if (F->comm->allreduce_sum(&r, 1, F->stream)) return fail("allreduce failed");
   }
+  if (!ok) return -1;
   *out = r;
   return 0;
 }
@@ -3088,6 +3096,20 @@ int structure_load(mnl_structure *S, const char *path) {
   T.boxes.assign(in.ok && nb < (1u << 20) ? nb : 0, BoxSpec{});
   for (auto &b : T.boxes) in.get(b);
   if (!in.ok || in.i != s.size()) return fail("structure file is truncated or corrupt");
+  bool sizes_ok = true;  // every per-point array is absent or whole-cell
+  auto chk = [&](const std::vector<double> &v) { sizes_ok = sizes_ok && (v.empty() || v.size() == T.ntot); };
+  for (int c = 0; c < 3; c++) {
+    for (int d = 0; d < 3; d++) chk(T.chi1inv[c][d]);
+    chk(T.chi2[c]), chk(T.chi3[c]);
+  }
+  for (int t = 0; t < 2; t++)
+    for (int d = 0; d < 3; d++) chk(T.cond[t][d]);
+  for (auto &L : T.lor) {
+    for (int d = 0; d < 3; d++) chk(L.sigma[d]);
+    for (int c = 0; c < 3; c++)
+      for (int d = 0; d < 3; d++) chk(L.off[c][d]);
+  }
+  if (!sizes_ok) return fail("structure file holds an array of the wrong size");
   *S = std::move(T);
   return 0;
 }
@@ -3103,6 +3125,35 @@ int structure_load(mnl_structure *S, const char *path) {
 // from the whole-cell component array, as the reference's CPU loop.
 inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) {
   return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
+}
+
+// This rank's entries of component c inside the whole-cell index box lo..hi
+// (global indices per direction) into out (strides hs, zero elsewhere).
+int copy_component_box(mnl_fields *F, int c, const int lo[3], const int hi[3],
+                       const long long hs[3], double *out) {
+  const mnl_structure &S = F->S;
+  long long n = 1;
+  for (int d = 0; d < 3; d++)
+    if (S.has[d]) n *= hi[d] - lo[d] + 1;
+  if (n <= 0) return 0;
+  memset(out, 0, (size_t)n * sizeof(double));
+  if (!has_field(S, c) || !F->allocated[c]) return 0;
+  const int t = ctype(c), d = cdir(c);
+  const double *src = t == T_E ? F->f.E[d] : t == T_D ? F->f.D[d] : F->f.B[d];
+  const double *hsep = t == T_H ? F->f.H[d] : nullptr;
+  if (!src) return 0;
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  double *buf = nullptr;
+  HIPCHK(hipMalloc(&buf, (size_t)n * sizeof(double)));
+  std::unique_ptr<void, void (*)(void *)> guard(buf, [](void *p) { (void)hipFree(p); });
+  HIPCHK(hipMemsetAsync(buf, 0, (size_t)n * sizeof(double), F->stream));
+  const bool fe = F->fused && t == T_E;
+  if (k_to_box(buf, src, hsep, F->g, t, d, F->f, fe ? &F->fusedG : nullptr, fe ? F->f.D[d] : nullptr,
+               fe ? F->f.inveps[d] : nullptr, lo, hi, hs, F->stream))
+    return fail("to_box launch failed");
+  HIPCHK(hipMemcpyAsync(out, buf, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, F->stream));
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
 }
 
 int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3], int snap,
@@ -3201,55 +3252,119 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   if (nout < nred) return fail("output buffer too small");
   for (long long k = 0; k < nred; k++) out[k] = 0.0;
   if (loops.empty()) return 0;
-  std::vector<double> f(S.ntot);
-  if (mnl_fields_copy_component(F, c, f.data(), f.size())) return -1;
-  // distributed: every rank holds only its own entries (others 0); the four
-  // Yee values of each point are summed over ranks separately -- each has one
-  // owner, so the sums are exact -- and every rank then forms the same average
-  const bool dist = F->nranks > 1;
-  std::vector<double> v4;
-  long long o1 = 0, o2 = 0;
-  for (int d = 0; d < 3; d++)
-    if (S.has[d] && !S.shift(c, d)) {
-      if (o1)
-        o2 = S.cstride(d);
-      else
-        o1 = S.cstride(d);
-    }
   long long ntot = 1;
   for (int k = 0; k < r; k++) ntot *= full[k];
   std::vector<double> arr(ntot, 0.0);
+  // c's global indices the slice reads: the base point of each centred point
+  // and +1 along c's unshifted directions (the four Yee values, o1 / o2)
+  bool unsh[3];
+  int blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++) {
+    unsh[d] = S.has[d] && !S.shift(c, d);
+    if (!S.has[d]) continue;
+    blo[d] = (mn[d] - S.io[d]) / 2;
+    bhi[d] = (mx[d] - S.io[d]) / 2 + (unsh[d] ? 1 : 0);
+  }
+  // Distributed: this rank forms the points whose base value it owns along the
+  // slab axis (one owner each), reading its own entries of the box plus, for
+  // components unshifted along that axis, the next rank's first owned plane;
+  // the finished slice is then summed over ranks (every entry has one
+  // contributor, so the sums are exact).  No whole-cell buffers on any rank.
+  const bool dist = F->nranks > 1;
+  const int sd = F->slab_dir;
+  int rlo = 0, rhi = S.n[sd];  // base indices along sd this rank forms
+  if (dist) {
+    const int lo_cell = F->g.off[sd], hi_cell = lo_cell + F->g.N[F->g.ax[sd]] - 1;
+    if (S.shift(c, sd)) {
+      rlo = lo_cell;
+      rhi = F->rank == F->nranks - 1 ? S.n[sd] : hi_cell - 1;
+    } else {
+      rlo = F->rank == 0 ? 0 : lo_cell + 1;
+      rhi = hi_cell;
+    }
+  }
+  int hlo[3], hhi[3];  // this rank's box of values
+  for (int d = 0; d < 3; d++) hlo[d] = blo[d], hhi[d] = bhi[d];
+  hlo[sd] = std::max(blo[sd], rlo);
+  hhi[sd] = std::min(bhi[sd], rhi + (unsh[sd] ? 1 : 0));
+  long long hs[3] = {0, 0, 0}, hn = 1;  // slab axis slowest: a plane of it is contiguous
+  for (int d = 2; d >= 0; d--)
+    if (S.has[d] && d != sd) {
+      hs[d] = hn;
+      hn *= std::max(0, hhi[d] - hlo[d] + 1);
+    }
+  hs[sd] = hn;
+  hn *= std::max(0, hhi[sd] - hlo[sd] + 1);
+  // B components: a reference chunk without PML along c aliases B to H, so its
+  // ghost copy of a neighbour chunk's point holds that chunk's H (the H
+  // exchange writes through the alias, src/boundaries.cpp:347-460) -- hbh keeps
+  // the H values for those reads
+  const bool bq = ctype(c) == T_B;
+  std::vector<double> hb, hbh;
+  bool ok = true;
+  std::string why;
+  if (hn > 0) {
+    hb.assign(hn, 0.0);
+    if (copy_component_box(F, c, hlo, hhi, hs, hb.data())) ok = false, why = g_err;
+    if (bq && ok) {
+      hbh.assign(hn, 0.0);
+      if (copy_component_box(F, 3 * T_H + cdir(c), hlo, hhi, hs, hbh.data()))
+        ok = false, why = g_err;
+    }
+  }
+  if (dist) {
+    if (F->comm->agree_ok(ok, F->stream)) return fail(ok ? "array slice: a rank failed" : why);
+    if (unsh[sd]) {  // the plane above this rank's last base index comes from the next rank
+      long long pn = 1;
+      for (int d = 0; d < 3; d++)
+        if (S.has[d] && d != sd) pn *= bhi[d] - blo[d] + 1;
+      const int nv = bq ? 2 : 1;  // B: the H plane too
+      std::vector<double> xp((size_t)pn * F->nranks * nv, 0.0);
+      const int first = F->g.off[sd] + 1;  // first owned plane (unshifted along sd)
+      if (F->rank > 0 && hn > 0 && first >= hlo[sd] && first <= hhi[sd])
+        for (int v = 0; v < nv; v++)
+          for (long long q = 0; q < pn; q++)
+            xp[((size_t)F->rank * nv + v) * pn + q] =
+                (v ? hbh : hb)[(size_t)(first - hlo[sd]) * hs[sd] + q];
+      for (size_t q = 0; q < xp.size(); q += 1 << 20) {
+        const int n = (int)std::min<size_t>(1 << 20, xp.size() - q);
+        if (F->comm->allreduce_sum(xp.data() + q, n, F->stream)) return fail("slice allreduce failed");
+      }
+      const int top = rhi + 1;
+      if (F->rank + 1 < F->nranks && hn > 0 && top >= hlo[sd] && top <= hhi[sd])
+        for (int v = 0; v < nv; v++)
+          for (long long q = 0; q < pn; q++)
+            (v ? hbh : hb)[(size_t)(top - hlo[sd]) * hs[sd] + q] =
+                xp[((size_t)(F->rank + 1) * nv + v) * pn + q];
+    }
+  } else if (!ok) {
+    return -1;
+  }
+  long long o1 = 0, o2 = 0;  // offsets of the unshifted neighbours in hb
+  int d1 = -1, d2 = -1;      // and their directions
+  for (int d = 0; d < 3; d++)
+    if (unsh[d]) {
+      if (o1)
+        o2 = hs[d], d2 = d;
+      else
+        o1 = hs[d], d1 = d;
+    }
+  const int cd = cdir(c);
   bool empty_dim[3];
   for (int d = 0; d < 3; d++) empty_dim[d] = S.has[d] && vmax[d] - vmin[d] == 0.0;
   const int yd[3] = {S.dim == 2 ? 2 : 0, S.dim == 2 ? 0 : 1, S.dim == 2 ? 1 : 2};
-  for (int pass = dist ? 0 : 1; pass < 2; pass++) {
-  if (pass == 1 && dist) {  // exact gather of the four values per point
-    for (size_t q = 0; q < v4.size(); q += 1 << 20) {
-      const int n = (int)std::min<size_t>(1 << 20, v4.size() - q);
-      if (F->comm->allreduce_sum(v4.data() + q, n, F->stream)) return fail("slice allreduce failed");
-    }
-  }
-  size_t pi = 0;  // point ordinal over all chunk loops
   for (auto &L : loops) {
     int n[3];
     for (int k = 0; k < 3; k++) n[k] = S.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
     for (int i1 = 0; i1 < n[0]; i1++)
       for (int i2 = 0; i2 < n[1]; i2++)
-        for (int i3 = 0; i3 < n[2]; i3++, pi++) {
+        for (int i3 = 0; i3 < n[2]; i3++) {
           const int ii[3] = {i1, i2, i3};
           int p[3] = {0, 0, 0};
           for (int k = 0; k < 3; k++)
             if (S.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
-          if (pass == 0) {  // distributed, first pass: the four owned values
-            long long idx = 0;
-            for (int d = 0; d < 3; d++)
-              if (S.has[d]) idx += (long long)((p[d] - S.io[d]) / 2) * S.cstride(d);
-            v4.push_back(f[idx]);
-            v4.push_back(f[idx + o1]);
-            v4.push_back(f[idx + o2]);
-            v4.push_back(f[idx + o1 + o2]);
-            continue;
-          }
+          const int jb = S.has[sd] ? (p[sd] - S.io[sd]) / 2 : 0;
+          if (jb < rlo || jb > rhi) continue;  // another rank forms this point
           double w[3];
           for (int k = 0; k < 3; k++) {
             const int d = yd[k];
@@ -3258,18 +3373,38 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
           }
           const double wt = w[2] * (w[1] * (1.0 * w[0]));
           long long idx = 0;
+          int jb3[3] = {0, 0, 0};
           for (int d = 0; d < 3; d++)
-            if (S.has[d]) idx += (long long)((p[d] - S.io[d]) / 2) * S.cstride(d);
-          const double avg =
-              dist ? 0.25 * (v4[4 * pi] + v4[4 * pi + 1] + v4[4 * pi + 2] + v4[4 * pi + 3])
-                   : 0.25 * (f[idx] + f[idx + o1] + f[idx + o2] + f[idx + o1 + o2]);
+            if (S.has[d]) {
+              jb3[d] = (p[d] - S.io[d]) / 2;
+              idx += (long long)(jb3[d] - hlo[d]) * hs[d];
+            }
+          double a4[4] = {hb[idx], hb[idx + o1], hb[idx + o2], hb[idx + o1 + o2]};
+          if (bq && F->h_zone[cd][p[cd] - S.io[cd]] == 1) {  // reader chunk aliases B to H
+            for (int k = 0; k < 4; k++) {
+              int jn[3] = {jb3[0], jb3[1], jb3[2]};
+              if ((k & 1) && d1 >= 0) jn[d1]++;
+              if ((k & 2) && d2 >= 0) jn[d2]++;
+              bool other = false;  // owned by another reference chunk
+              for (int d = 0; d < 3; d++)
+                if (S.has[d])
+                  other = other || F->h_zone[d][2 * jn[d] + S.shift(c, d)] !=
+                                       F->h_zone[d][p[d] - S.io[d]];
+              if (other) a4[k] = hbh[idx + ((k & 1) ? o1 : 0) + ((k & 2) ? o2 : 0)];
+            }
+          }
+          const double avg = 0.25 * (a4[0] + a4[1] + a4[2] + a4[3]);
           const cplx v = wt * cplx(avg, 0.0) * cplx(1.0, 0.0);
           long long oi = 0;
           for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
           arr[oi] = real(v);
         }
   }
-  }
+  if (dist)
+    for (size_t q = 0; q < arr.size(); q += 1 << 20) {
+      const int n = (int)std::min<size_t>(1 << 20, arr.size() - q);
+      if (F->comm->allreduce_sum(arr.data() + q, n, F->stream)) return fail("slice allreduce failed");
+    }
   for (long long q = 0; q < ntot; q++) {  // collapse_array: in full-index order
     long long t = q, ri = 0;
     for (int k = r - 1; k >= 0; k--) {
@@ -3394,32 +3529,41 @@ int integrate_pair(mnl_fields *F, int c, const double *A, const double *Asep, co
                    const double wmin[3], const double wmax[3], double *out) {
   std::vector<double> wtab;
   auto boxes = energy_boxes(F, c, wmin, wmax, wtab);
-  const int NB = 256;
-  double *dw = nullptr, *dp = nullptr;
-  HIPCHK(hipMalloc(&dw, std::max<size_t>(wtab.size(), 1) * 8));
-  HIPCHK(hipMalloc(&dp, 2 * NB * 8));
-  std::unique_ptr<void, void (*)(void *)> g1(dw, [](void *p) { (void)hipFree(p); });
-  std::unique_ptr<void, void (*)(void *)> g2(dp, [](void *p) { (void)hipFree(p); });
-  if (!wtab.empty())
-    HIPCHK(hipMemcpyAsync(dw, wtab.data(), wtab.size() * 8, hipMemcpyHostToDevice, F->stream));
-  std::vector<double> chunk(boxes.size(), 0.0), part(2 * NB);
-  for (size_t k = 0; k < boxes.size(); k++) {
-    const EBox &b = boxes[k];
-    const long long n = (long long)b.dn[0] * b.dn[1] * b.dn[2];
-    if (n == 0 || !A || !Bv) continue;
-    const int nb = (int)std::min<long long>(NB, (n + 255) / 256);
-    if (k_energy(A, Asep, Bv, F->g, F->f, ctype(c), cdir(c), b, dw, dp, nb, F->stream))
-      return fail("energy kernel launch failed");
-    HIPCHK(hipMemcpyAsync(part.data(), dp, 2 * nb * 8, hipMemcpyDeviceToHost, F->stream));
-    HIPCHK(hipStreamSynchronize(F->stream));
-    long double acc = 0.0L;
-    for (int i = 0; i < nb; i++) acc += (long double)part[2 * i] + (long double)part[2 * i + 1];
-    chunk[k] = (double)acc;
-  }
+  std::vector<double> chunk(boxes.size(), 0.0);
+  // the local part; a failure is agreed on before the collective so that every
+  // rank returns instead of waiting in the allreduce
+  const int lrc = [&]() -> int {
+    const int NB = 256;
+    double *dw = nullptr, *dp = nullptr;
+    HIPCHK(hipMalloc(&dw, std::max<size_t>(wtab.size(), 1) * 8));
+    std::unique_ptr<void, void (*)(void *)> g1(dw, [](void *p) { (void)hipFree(p); });
+    HIPCHK(hipMalloc(&dp, 2 * NB * 8));
+    std::unique_ptr<void, void (*)(void *)> g2(dp, [](void *p) { (void)hipFree(p); });
+    if (!wtab.empty())
+      HIPCHK(hipMemcpyAsync(dw, wtab.data(), wtab.size() * 8, hipMemcpyHostToDevice, F->stream));
+    std::vector<double> part(2 * NB);
+    for (size_t k = 0; k < boxes.size(); k++) {
+      const EBox &b = boxes[k];
+      const long long n = (long long)b.dn[0] * b.dn[1] * b.dn[2];
+      if (n == 0 || !A || !Bv) continue;
+      const int nb = (int)std::min<long long>(NB, (n + 255) / 256);
+      if (k_energy(A, Asep, Bv, F->g, F->f, ctype(c), cdir(c), b, dw, dp, nb, F->stream))
+        return fail("energy kernel launch failed");
+      HIPCHK(hipMemcpyAsync(part.data(), dp, 2 * nb * 8, hipMemcpyDeviceToHost, F->stream));
+      HIPCHK(hipStreamSynchronize(F->stream));
+      long double acc = 0.0L;
+      for (int i = 0; i < nb; i++) acc += (long double)part[2 * i] + (long double)part[2 * i + 1];
+      chunk[k] = (double)acc;
+    }
+    return 0;
+  }();
   if (F->nranks > 1) {
-    if (F->comm->agree_ok(true, F->stream)) return fail("energy: a rank failed");
+    const std::string why = g_err;
+    if (F->comm->agree_ok(lrc == 0, F->stream)) return fail(lrc ? why : "energy: a rank failed");
     if (F->comm->allreduce_sum(chunk.data(), (int)chunk.size(), F->stream))
       return fail("energy allreduce failed");
+  } else if (lrc) {
+    return -1;
   }
   double sum = 0.0;
   for (double v : chunk) sum += v;

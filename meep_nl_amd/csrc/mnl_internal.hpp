@@ -312,6 +312,12 @@ int k_from_canonical(double *dst, const double *src, const DevGrid &g, int comp_
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
                    int comp_type, int comp_dir, const DevFields &f, const Box *fusedF,
                    const double *dsrc, const double *usrc, void *stream);
+// the same into a box of the whole-cell array: global indices blo..bhi per
+// direction, destination strides bs (entries this rank does not own untouched)
+int k_to_box(double *dst, const double *src, const double *hsep, const DevGrid &g, int comp_type,
+             int comp_dir, const DevFields &f, const Box *fusedF, const double *dsrc,
+             const double *usrc, const int blo[3], const int bhi[3], const long long bs[3],
+             void *stream);
 // bounding box (local indices per direction, as Pt::j) of the points where any array is nonzero
 int k_nonzero_box(const double *const a[3], const DevGrid &g, int *dev_box6, void *stream);
 int k_box_fill(double *dst, const DevGrid &g, int comp_type, int comp_dir, const double *pos_lo,

@@ -532,7 +532,6 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
   if (!map_pt<SHELL>(b, bl, g, p)) return;
   const long long i = p.idx;
   const unsigned pm = pol_mask(f, p);
-#pragma unroll
   for (int d = 0; d < 3; d++) {
     if (!f.ecomp_present[d]) continue;
     // wall_e: also the high metallic wall plane, which the reference's chunk owns
@@ -861,14 +860,17 @@ __global__ void from_canonical_kernel(double *dst, const double *src, DevGrid g,
   dst[(long long)i0 + i1 * g.st[1] + i2 * g.st[2]] = src[cidx];
 }
 
-__global__ void to_canonical_kernel(double *dst, const double *src, const double *hsep, DevGrid g,
-                                    DevFields f, int type, int c, long long cs0, long long cs1,
-                                    long long cs2, Box Fb, int use_fb, const double *dsrc,
-                                    const double *usrc) {
-  int i0 = blockIdx.x * MNL_BX + threadIdx.x;
-  int i1 = blockIdx.y * MNL_BY + threadIdx.y;
-  int i2 = blockIdx.z;
-  if (i0 >= g.N[0] || i1 >= g.N[1]) return;
+// Rank-owned entries of one component into a box of the whole-cell array
+// (global indices blo..bhi per direction, strides bs); the launch covers the
+// local index range lo.. of that box.
+__global__ void to_box_kernel(double *dst, const double *src, const double *hsep, DevGrid g,
+                              DevFields f, int type, int c, int l0, int l1, int l2, int n0, int n1,
+                              long long bs0, long long bs1, long long bs2, int blo0, int blo1,
+                              int blo2, int use_fb, const double *dsrc, const double *usrc) {
+  const int i0 = l0 + blockIdx.x * MNL_BX + threadIdx.x;
+  const int i1 = l1 + blockIdx.y * MNL_BY + threadIdx.y;
+  const int i2 = l2 + blockIdx.z;
+  if (i0 >= l0 + n0 || i1 >= l1 + n1) return;
   int ii[3] = {i0, i1, i2};
   Pt p;
   for (int d = 0; d < 3; d++) p.j[d] = g.ax[d] >= 0 ? ii[g.ax[d]] : 0;
@@ -882,10 +884,11 @@ __global__ void to_canonical_kernel(double *dst, const double *src, const double
     if (!sh && g.wall[d] && p.j[d] + g.off[d] == g.nglob[d]) hi = p.j[d];  // wall plane (= 0)
     if (p.j[d] < lo || p.j[d] > hi) return;
   }
+  const long long bs[3] = {bs0, bs1, bs2};
+  const int blo[3] = {blo0, blo1, blo2};
   long long cidx = 0;
-  long long cs[3] = {cs0, cs1, cs2};
   for (int d = 0; d < 3; d++)
-    if (g.ax[d] >= 0) cidx += (long long)(p.j[d] + g.off[d]) * cs[d];
+    if (g.ax[d] >= 0) cidx += (long long)(p.j[d] + g.off[d] - blo[d]) * bs[d];
   long long i = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
   double v = src[i];
   if (hsep && pml_at(f, g, c, qcoord(g, p, T_H, c, c))) v = hsep[i];
@@ -2504,18 +2507,41 @@ int k_init_add(double *dst, double *alt, const double *src, const DevGrid &g, co
   return rc();
 }
 
+int k_to_box(double *dst, const double *src, const double *hsep, const DevGrid &g, int comp_type,
+             int comp_dir, const DevFields &f, const Box *fusedF, const double *dsrc,
+             const double *usrc, const int blo[3], const int bhi[3], const long long bs[3],
+             void *stream) {
+  (void)fusedF;
+  int l[3] = {0, 0, 0}, n[3] = {1, 1, 1};
+  for (int d = 0; d < 3; d++) {
+    const int a = g.ax[d];
+    if (a < 0) continue;
+    const int lo = std::max(blo[d] - g.off[d], 0), hi = std::min(bhi[d] - g.off[d], g.N[a] - 1);
+    if (hi < lo) return 0;
+    l[a] = lo;
+    n[a] = hi - lo + 1;
+  }
+  int bl[3] = {0, 0, 0};
+  long long bst[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++)
+    if (g.ax[d] >= 0) bl[d] = blo[d], bst[d] = bs[d];
+  dim3 grd((n[0] + MNL_BX - 1) / MNL_BX, (n[1] + MNL_BY - 1) / MNL_BY, n[2]);
+  to_box_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(
+      dst, src, hsep, g, f, comp_type, comp_dir, l[0], l[1], l[2], n[0], n[1], bst[0], bst[1],
+      bst[2], bl[0], bl[1], bl[2], fusedF ? 1 : 0, dsrc, usrc);
+  return rc();
+}
+
 int k_to_canonical(double *dst, const double *src, const double *hsep, const DevGrid &g,
                    int comp_type, int comp_dir, const DevFields &f, const Box *fusedF,
                    const double *dsrc, const double *usrc, void *stream) {
   long long cs[3];
   canon_strides(g, cs);
-  dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
-  Box fb{};
-  if (fusedF) fb = *fusedF;
-  to_canonical_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(
-      dst, src, hsep, g, f, comp_type, comp_dir, cs[0], cs[1], cs[2], fb, fusedF ? 1 : 0, dsrc,
-      usrc);
-  return rc();
+  int blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0};
+  for (int d = 0; d < 3; d++)
+    if (g.ax[d] >= 0) bhi[d] = g.nglob[d];
+  return k_to_box(dst, src, hsep, g, comp_type, comp_dir, f, fusedF, dsrc, usrc, blo, bhi, cs,
+                  stream);
 }
 
 __global__ void nonzero_box_kernel(const double *a0, const double *a1, const double *a2,

@@ -17,6 +17,10 @@ VOL2 = [([-10, -10, 0], [10, 10, 0]), ([-10, 0.33, 0], [10, 0.33, 0]),
 VOL3 = [([-1.6, -1.6, 0.12], [1.6, 1.6, 0.12]), ([-1.2, -0.65, -1.0], [0.9, 0.45, 0.3]),
         ([0.05, 0.05, 0.05], [0.05, 0.05, 0.05]), ([-1.6, 0.61, -0.63], [1.6, 0.61, -0.63]),
         ([-0.9, -1.6, -1.6], [-0.9, 1.6, 1.6])]
+# whole cell, and planes on / between the 3-slab seams (global z = 11, 22)
+VOL3_SEAM = [([-1.6, -1.6, -1.6], [1.6, 1.6, 1.6]), ([-1.6, -1.6, -0.5], [1.6, 1.6, -0.5]),
+             ([-1.6, -1.6, -0.45], [1.6, 1.6, -0.45]), ([-1.3, -0.2, 0.6], [0.4, 1.1, 0.6]),
+             ([-0.3, 0.2, -0.55], [0.3, 0.2, 0.62])]
 
 
 def _same(p, o, comps, vols):
@@ -41,6 +45,14 @@ def test_slices_3d(G):
     of each point gathered exactly over the slabs."""
     _same(sc_vacuum_pml_3d(G, steps=40), sc_vacuum_pml_3d(make_oracle, steps=40),
           (0, 2, 3, 5, 7), VOL3)
+
+
+@pytest.mark.parametrize("G", [ProductSim, GroupSim, GroupSim3])
+def test_slices_3d_seams(G):
+    """Whole-cell and seam-plane slices over slabs: each rank reads only its own
+    box of values plus the next rank's first plane (no whole-cell buffers)."""
+    _same(sc_vacuum_pml_3d(G, steps=30), sc_vacuum_pml_3d(make_oracle, steps=30),
+          (0, 1, 2, 4, 5, 6, 8, 9, 11), VOL3_SEAM)
 
 
 def test_slices_2d_slabs():
