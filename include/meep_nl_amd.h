@@ -246,6 +246,32 @@ size_t mnl_fields_ntot(mnl_fields *f);
  * FieldUpdateB/H/D/E, BoundarySteppingB/H, src/meep.hpp:1610-1633);
  * out[6]. */
 int mnl_fields_timers(mnl_fields *f, double out[6]);
+/* Time sinks in the reference's enum order (meep::time_sink,
+ * src/meep.hpp:1610-1633; print_times labels src/time.cpp:28-51). */
+enum {
+  MNL_SINK_CONNECTING, MNL_SINK_STEPPING, MNL_SINK_BOUNDARIES, MNL_SINK_MPI_ALL,
+  MNL_SINK_MPI_ONE, MNL_SINK_FIELD_OUTPUT, MNL_SINK_FOURIER, MNL_SINK_MPB,
+  MNL_SINK_FARFIELDS, MNL_SINK_OTHER, MNL_SINK_UPDATE_B, MNL_SINK_UPDATE_H,
+  MNL_SINK_UPDATE_D, MNL_SINK_UPDATE_E, MNL_SINK_BSTEP_B, MNL_SINK_BSTEP_WH,
+  MNL_SINK_BSTEP_PH, MNL_SINK_BSTEP_H, MNL_SINK_BSTEP_D, MNL_SINK_BSTEP_WE,
+  MNL_SINK_BSTEP_PE, MNL_SINK_BSTEP_E, MNL_NUM_TIME_SINKS
+};
+/* fields::get_time_spent_on for every sink of this rank, seconds (replaces
+ * src/time.cpp:136-139 / timing_data_vector): wall time of mnl_fields_step
+ * goes to "time stepping" except, with profiling on, the GPU time of the
+ * unfused update kernels (B/H/D/E), halo exchanges ("copying boundaries")
+ * and DFT updates ("Fourier transforming"); collectives of slices / energies
+ * / fluxes / get_field to "all-all communication".  out[MNL_NUM_TIME_SINKS]. */
+int mnl_fields_time_spent(mnl_fields *f, double *out);
+/* fields::reset_timers (src/time.cpp:124-128). */
+int mnl_fields_reset_timers(mnl_fields *f);
+/* sum_to_all over the ranks of distributed fields (in place, n doubles);
+ * a no-op on one rank.  Collective. */
+int mnl_fields_allreduce(mnl_fields *f, double *v, int n);
+/* meep::verbosity (default 1).  At > 0 rank 0 prints "on time step N
+ * (time=T), S s/step" at most every 4 s of stepping (src/step.cpp:49-56). */
+void mnl_set_verbosity(int level);
+int mnl_get_verbosity(void);
 /* Newton-Raphson attempts that fell back to random seeds (never in the
  * reference runs recorded in SURVEY.md; counted instead of printed). */
 int mnl_fields_nr_fallbacks(mnl_fields *f, long long *count);

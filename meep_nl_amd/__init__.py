@@ -12,6 +12,7 @@ from .simulation import (ALL, AUTOMATIC, Block, ContinuousSource, CustomSource, 
                          PML, Simulation, Source, Vector3, Volume, after_sources, after_time,
                          air, at_beginning, at_end, at_every, before_time, combine_step_funcs,
                          during_sources, get_flux_freqs, get_fluxes, inf, stop_after_walltime,
-                         stop_when_fields_decayed, vacuum, when_false, when_true)
+                         stop_when_fields_decayed, vacuum, when_false, when_true, verbosity,
+                         quiet, wall_time)
 
 __version__ = "0.1.0"

@@ -79,6 +79,11 @@ _SIGS = {
     "mnl_fields_copy_component": (c_int, [c_void, c_int, dptr, c_size]),
     "mnl_fields_ntot": (c_size, [c_void]),
     "mnl_fields_timers": (c_int, [c_void, dptr]),
+    "mnl_fields_time_spent": (c_int, [c_void, dptr]),
+    "mnl_fields_reset_timers": (c_int, [c_void]),
+    "mnl_fields_allreduce": (c_int, [c_void, dptr, c_int]),
+    "mnl_set_verbosity": (None, [c_int]),
+    "mnl_get_verbosity": (c_int, []),
     "mnl_fields_nr_fallbacks": (c_int, [c_void, llptr]),
     "mnl_fields_set_profiling": (c_int, [c_void, c_int]),
     "mnl_fields_set_fused": (c_int, [c_void, c_int]),

@@ -20,6 +20,31 @@ from ._lib import check, dptr, lib, ptr
 
 Ex, Ey, Ez, Hx, Hy, Hz, Dx, Dy, Dz, Bx, By, Bz = range(12)
 X, Y, Z = 0, 1, 2
+
+# meep::time_sink (src/meep.hpp:1610-1633) and the print_times labels
+# (DescriptionByTimeSink, src/time.cpp:28-51), in enum order
+TIME_SINKS = (
+    ("Connecting", "connecting chunks"), ("Stepping", "time stepping"),
+    ("Boundaries", "copying boundaries"), ("MpiAllTime", "all-all communication"),
+    ("MpiOneTime", "1-1 communication"), ("FieldOutput", "outputting fields"),
+    ("FourierTransforming", "Fourier transforming"), ("MPBTime", "MPB mode solver"),
+    ("GetFarfieldsTime", "far-field transform"), ("Other", "everything else"),
+    ("FieldUpdateB", "updating B field"), ("FieldUpdateH", "updating H field"),
+    ("FieldUpdateD", "updating D field"), ("FieldUpdateE", "updating E field"),
+    ("BoundarySteppingB", "boundary stepping B"), ("BoundarySteppingWH", "boundary stepping WH"),
+    ("BoundarySteppingPH", "boundary stepping PH"), ("BoundarySteppingH", "boundary stepping H"),
+    ("BoundarySteppingD", "boundary stepping D"), ("BoundarySteppingWE", "boundary stepping WE"),
+    ("BoundarySteppingPE", "boundary stepping PE"), ("BoundarySteppingE", "boundary stepping E"),
+)
+
+
+def set_verbosity(level):
+    """meep::verbosity of the native library (rank 0's "on time step" lines)."""
+    lib().mnl_set_verbosity(int(level))
+
+
+def get_verbosity():
+    return lib().mnl_get_verbosity()
 COMPONENT_NAMES = ["ex", "ey", "ez", "hx", "hy", "hz", "dx", "dy", "dz", "bx", "by", "bz"]
 
 
@@ -418,6 +443,22 @@ class Fields:
         check(lib().mnl_fields_timers(self.h, ptr(out)))
         return dict(zip(["FieldUpdateB", "FieldUpdateH", "FieldUpdateD", "FieldUpdateE",
                          "Sources", "BoundarySteppingHalo"], out.tolist()))
+
+    def time_spent(self):
+        """This rank's seconds per time sink, in meep::time_sink order
+        (TIME_SINKS; mnl_fields_time_spent)."""
+        out = np.zeros(len(TIME_SINKS))
+        check(lib().mnl_fields_time_spent(self.h, ptr(out)))
+        return out
+
+    def reset_timers(self):
+        check(lib().mnl_fields_reset_timers(self.h))
+
+    def sum_to_all(self, values):
+        """Sum of a float64 vector over the ranks of distributed fields (collective)."""
+        v = np.ascontiguousarray(values, dtype=np.float64).copy()
+        check(lib().mnl_fields_allreduce(self.h, ptr(v), v.size))
+        return v
 
     def nr_fallbacks(self):
         v = ctypes.c_longlong()

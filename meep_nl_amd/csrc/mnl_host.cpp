@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <complex>
 #include <cstdio>
@@ -295,6 +296,10 @@ struct mnl_fields {
   double dt;
   // timers / profiling
   bool profiling = false;
+  // fields::times_spent by time_sink (src/meep.hpp:1610-1633 order), seconds
+  double sink_s[MNL_NUM_TIME_SINKS] = {0};
+  double last_out_wall = -1;  // "on time step" output (src/step.cpp:44-56)
+  long long last_out_t = 0;
   double timer_ms[16] = {0};
   long long timer_count[16] = {0};
   std::vector<hipEvent_t> ev_pool;
@@ -1757,6 +1762,8 @@ bool dft_due(const mnl_fields *F, long long t) {
   return false;
 }
 
+int timed_allreduce(mnl_fields *F, double *v, int n);
+
 int dft_flux_values(mnl_fields *F, int h, double *out) {
   if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
   DftFluxH &o = *F->dfts[h];
@@ -1784,7 +1791,7 @@ int dft_flux_values(mnl_fields *F, int h, double *out) {
     }
   if (F->nranks > 1)
     for (size_t i0 = 0; i0 < nf; i0 += 64)
-      if (F->comm->allreduce_sum(out + i0, (int)std::min<size_t>(64, nf - i0), F->stream))
+      if (timed_allreduce(F, out + i0, (int)std::min<size_t>(64, nf - i0)))
         return fail("flux allreduce failed");
   return 0;
 }
@@ -1910,7 +1917,7 @@ int get_field(mnl_fields *F, int c, const double pos[3], double *out, bool reduc
   if (reduce && F->nranks > 1) {
     const std::string why = g_err;
     if (F->comm->agree_ok(ok, F->stream)) return fail(ok ? "get_field: a rank failed" : why);
-    if (F->comm->allreduce_sum(&r, 1, F->stream)) return fail("allreduce failed");
+    if (timed_allreduce(F, &r, 1)) return fail("allreduce failed");
   }
   if (!ok) return -1;
   *out = r;
@@ -3328,7 +3335,7 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
                 (v ? hbh : hb)[(size_t)(first - hlo[sd]) * hs[sd] + q];
       for (size_t q = 0; q < xp.size(); q += 1 << 20) {
         const int n = (int)std::min<size_t>(1 << 20, xp.size() - q);
-        if (F->comm->allreduce_sum(xp.data() + q, n, F->stream)) return fail("slice allreduce failed");
+        if (timed_allreduce(F, xp.data() + q, n)) return fail("slice allreduce failed");
       }
       const int top = rhi + 1;
       if (F->rank + 1 < F->nranks && hn > 0 && top >= hlo[sd] && top <= hhi[sd])
@@ -3403,7 +3410,7 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   if (dist)
     for (size_t q = 0; q < arr.size(); q += 1 << 20) {
       const int n = (int)std::min<size_t>(1 << 20, arr.size() - q);
-      if (F->comm->allreduce_sum(arr.data() + q, n, F->stream)) return fail("slice allreduce failed");
+      if (timed_allreduce(F, arr.data() + q, n)) return fail("slice allreduce failed");
     }
   for (long long q = 0; q < ntot; q++) {  // collapse_array: in full-index order
     long long t = q, ri = 0;
@@ -3560,7 +3567,7 @@ int integrate_pair(mnl_fields *F, int c, const double *A, const double *Asep, co
   if (F->nranks > 1) {
     const std::string why = g_err;
     if (F->comm->agree_ok(lrc == 0, F->stream)) return fail(lrc ? why : "energy: a rank failed");
-    if (F->comm->allreduce_sum(chunk.data(), (int)chunk.size(), F->stream))
+    if (timed_allreduce(F, chunk.data(), (int)chunk.size()))
       return fail("energy allreduce failed");
   } else if (lrc) {
     return -1;
@@ -3691,7 +3698,50 @@ int energy_in_box(mnl_fields *F, int which, const double wmin[3], const double w
 // fields::step() n times: the NaN guard (src/step.cpp:138-139) every nan_every
 // steps; the first step after construction (or after E / H were set directly)
 // runs unfused (see e_first_done)
+static int g_verbosity = 1;  // meep::verbosity (src/meep.hpp: default 1)
+
+static double wall_now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// sum_to_all over the fields' ranks, timed as all-all communication
+int timed_allreduce(mnl_fields *F, double *v, int n) {
+  const double t0 = wall_now();
+  const int r = F->comm->allreduce_sum(v, n, F->stream);
+  F->sink_s[MNL_SINK_MPI_ALL] += wall_now() - t0;
+  return r;
+}
+
+int fields_step_batches(mnl_fields *F, int nsteps);
+
+// fields::step (src/step.cpp:40-140) over nsteps: the time spent goes to the
+// reference's time sinks (per-phase kernel times when profiling is on, the
+// rest to "time stepping"), and rank 0 prints "on time step ..." at most every
+// MEEP_MIN_OUTPUT_TIME (4 s, src/meep.hpp:48) when verbosity > 0.
 int fields_step(mnl_fields *F, int nsteps) {
+  const double w0 = wall_now();
+  double ms0[TM_N];
+  for (int k = 0; k < TM_N; k++) ms0[k] = F->timer_ms[k];
+  if (F->t == 0 || F->last_out_wall < 0) F->last_out_wall = w0, F->last_out_t = F->t;
+  const int r = fields_step_batches(F, nsteps);
+  const double wall = wall_now() - w0;
+  auto dsec = [&](int k) { return (F->timer_ms[k] - ms0[k]) * 1e-3; };
+  double parts[MNL_NUM_TIME_SINKS] = {0};
+  if (F->profiling) {
+    parts[MNL_SINK_UPDATE_B] = dsec(TM_B) + (F->fused ? 0.0 : dsec(TM_BINT));
+    parts[MNL_SINK_UPDATE_H] = dsec(TM_H);
+    parts[MNL_SINK_UPDATE_D] = dsec(TM_D) + dsec(TM_DINT);
+    parts[MNL_SINK_UPDATE_E] = dsec(TM_E);
+    parts[MNL_SINK_BOUNDARIES] = dsec(TM_HALO);
+    parts[MNL_SINK_FOURIER] = dsec(TM_DFT) + dsec(TM_DFTF);
+  }
+  double rest = wall;
+  for (int k = 0; k < MNL_NUM_TIME_SINKS; k++) F->sink_s[k] += parts[k], rest -= parts[k];
+  F->sink_s[MNL_SINK_STEPPING] += std::max(rest, 0.0);
+  return r;
+}
+
+int fields_step_batches(mnl_fields *F, int nsteps) {
   while (nsteps > 0) {
     int m;
     if (!F->e_first_done || !F->h_first_done || !F->u_first_done[0] || !F->u_first_done[1] ||
@@ -3711,6 +3761,16 @@ int fields_step(mnl_fields *F, int nsteps) {
     }
     nsteps -= m;
     if (nan_check(F)) return -1;
+    if (g_verbosity > 0 && F->rank == 0) {
+      const double now = wall_now();
+      if (now > F->last_out_wall + 4.0 && F->t > F->last_out_t) {
+        printf("on time step %lld (time=%g), %g s/step\n", F->t, F->t * F->dt,
+               (now - F->last_out_wall) / double(F->t - F->last_out_t));
+        fflush(stdout);
+        F->last_out_wall = now;
+        F->last_out_t = F->t;
+      }
+    }
   }
   return 0;
 }
@@ -4282,6 +4342,28 @@ int mnl_fields_copy_component(mnl_fields *F, int comp, double *host, size_t n) {
   HIPCHK(hipStreamSynchronize(F->stream));
   return 0;
 }
+
+int mnl_fields_time_spent(mnl_fields *F, double *out) {
+  if (!F || !out) return fail("bad argument");
+  for (int k = 0; k < MNL_NUM_TIME_SINKS; k++) out[k] = F->sink_s[k];
+  return 0;
+}
+
+int mnl_fields_reset_timers(mnl_fields *F) {
+  if (!F) return fail("null fields");
+  for (int k = 0; k < MNL_NUM_TIME_SINKS; k++) F->sink_s[k] = 0;
+  return 0;
+}
+
+int mnl_fields_allreduce(mnl_fields *F, double *v, int n) {
+  if (!F || (n > 0 && !v) || n < 0) return fail("bad argument");
+  if (F->nranks == 1 || n == 0) return 0;
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  return timed_allreduce(F, v, n) ? fail("allreduce failed") : 0;
+}
+
+void mnl_set_verbosity(int level) { g_verbosity = level; }
+int mnl_get_verbosity(void) { return g_verbosity; }
 
 int mnl_fields_timers(mnl_fields *F, double out[6]) {
   if (!F) return fail("null fields");

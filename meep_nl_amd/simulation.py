@@ -517,12 +517,87 @@ def _dist_barrier():
             dist.barrier()
 
 
+# ---------------------------------------------------------------- verbosity
+class Verbosity:
+    """meep.verbosity (python/verbosity_mgr.py): one process-wide level, 0 quiet,
+    1 progress messages (default), 2 more; `verbosity(2)` or `verbosity.meep = 2`
+    sets it, also for the native library's "on time step" lines."""
+    _instance = None
+
+    def __new__(cls):
+        if cls._instance is None:
+            cls._instance = super().__new__(cls)
+            cls._instance._level = 1
+        return cls._instance
+
+    def get(self):
+        return self._level
+
+    def set(self, level):
+        self._level = int(level)
+        try:
+            core.set_verbosity(self._level)
+        except Exception:  # native library absent: the level still applies here
+            pass
+        return self._level
+
+    def __call__(self, level=None):
+        return self.get() if level is None else self.set(level)
+
+    @property
+    def meep(self):
+        return self._level
+
+    @meep.setter
+    def meep(self, level):
+        self.set(level)
+
+    def __int__(self):
+        return self._level
+
+    def __repr__(self):
+        return f"Verbosity: level={self._level}"
+
+
+verbosity = Verbosity()
+
+
+def quiet(quietval=True):
+    """meep.quiet: verbosity 0 (or back to 1)."""
+    verbosity(0 if quietval else 1)
+
+
+def wall_time():
+    return time.time()
+
+
+def _progress(t0, t, dt):
+    """display_progress (python/simulation.py:5468-5489): every dt seconds of wall
+    time, "Meep progress: ..." while running until t0 + t."""
+    start = time.time()
+    last = {"t": start}
+
+    def show(sim):
+        now = time.time()
+        if now - last["t"] < dt:
+            return
+        done = sim.meep_time() - t0
+        pct = done / (0.01 * t)
+        el = now - start
+        togo = (el * (t / done) - el) if done != 0 else 0
+        if verbosity.meep > 0 and sim._is_master():
+            print("Meep progress: {}/{} = {:.1f}% done in {:.1f}s, {:.1f}s to go".format(
+                done, t, pct, el, togo))
+        last["t"] = now
+    return show
+
+
 # ---------------------------------------------------------------- Simulation
 class Simulation:
     def __init__(self, cell_size, resolution, geometry=(), sources=(), boundary_layers=(),
                  default_material=Medium(), Courant=0.5, eps_averaging=True, dimensions=None,
                  force_complex_fields=False, k_point=False, symmetries=(), parallel=None,
-                 nonlinear_mode="fork", **kwargs):
+                 nonlinear_mode="fork", progress_interval=4, **kwargs):
         self.cell_size = Vector3(*cell_size)
         self.resolution = float(resolution)
         self.geometry = list(geometry)
@@ -542,6 +617,8 @@ class Simulation:
         # "upstream": Meep's Pade chi2/chi3 E update instead of the fork's (an
         # extension; the fork's behaviour is the default)
         self.nonlinear_mode = nonlinear_mode
+        self.progress_interval = progress_interval
+        self.run_index = 0
         self.fields = None
         self.structure = None
         self.dft_objects = []
@@ -667,6 +744,8 @@ class Simulation:
                                       nccl_id=nid)
         else:
             self.fields = core.Fields(self.structure)
+        # per-phase GPU times for print_times (HIP events; ~0.3 % of a step)
+        self.fields.set_profiling(True)
         for src in self.sources:
             src.add_source(self.fields)
         if getattr(self, "load_fields_file", None):  # delayed load (python/simulation.py:2509-2510)
@@ -725,16 +804,28 @@ class Simulation:
         step_funcs = list(step_funcs)
         t0 = self.round_time()
         if not step_funcs and all(isinstance(c, numbers.Number) for c in conds):
-            # every condition is a time: count the steps on the host, step in one call
+            # every condition is a time: count the steps on the host, step in
+            # batches (one call each; a progress message between batches)
             stop = t0 + min(conds)
             t, dt = self.fields._time()
             n = 0
             while float(np.float32((t + n) * dt)) < stop:
                 n += 1
-            self.fields.step(n)
+            show = _progress(t0, min(conds), self.progress_interval)
+            batch = 64
+            while n > 0:
+                m = min(n, batch)
+                w = time.time()
+                self.fields.step(m)
+                n -= m
+                show(self)
+                if time.time() - w < 0.25:
+                    batch *= 2
+            self._run_finished()
             return
         for i, c in enumerate(conds):
             if isinstance(c, numbers.Number):
+                step_funcs.append(_progress(t0, c, self.progress_interval))
                 conds[i] = (lambda T: lambda sim: sim.round_time() >= t0 + T)(c)
             elif not callable(c):
                 raise TypeError(f"Stopping condition {c} is not a number or a function")
@@ -746,6 +837,79 @@ class Simulation:
             _eval_step_func(self, fn, "step")
         for fn in step_funcs:
             _eval_step_func(self, fn, "finish")
+        self._run_finished()
+
+    def _is_master(self):
+        return self.fields is None or self.fields.rank == 0
+
+    def _run_finished(self):
+        if verbosity.meep > 0 and self._is_master():
+            print("run {} finished at t = {} ({} timesteps)".format(
+                self.run_index, self.meep_time(), self.fields.t))
+        self.run_index += 1
+
+    # -- timing (python/simulation.py:4542-4601 -> src/time.cpp:130-215)
+    def _times_all(self):
+        """Per-process seconds, shape (n_sinks, nprocs) (timing_data_vector_from_all)."""
+        self.init_sim()
+        n = self.fields.nranks
+        mine = self.fields.time_spent()
+        allt = np.zeros((len(core.TIME_SINKS), n))
+        allt[:, self.fields.rank] = mine
+        return self.fields.sum_to_all(allt.ravel()).reshape(allt.shape)
+
+    def print_times(self):
+        """fields::print_times: mean (and stddev over processes) of each time sink."""
+        if self.fields is None:
+            return
+        allt = self._times_all()
+        n = allt.shape[1]
+        if not self._is_master():
+            return
+        print("\nField time usage:")
+        for (_, label), row in zip(core.TIME_SINKS, allt):
+            mean = float(np.sum(row)) / n
+            var = float(np.sum(row * row)) - n * mean * mean
+            sd = 0.0 if (n == 1 or var <= 0) else math.sqrt(var / (n - 1))
+            if mean != 0:
+                if sd != 0:
+                    print("    %21s: %4.6g s +/- %4.6g s" % (label, mean, sd))
+                else:
+                    print("    %21s: %4.6g s" % (label, mean))
+        print()
+        if verbosity.meep > 1:
+            print("\nField time usage for all processes:")
+            for (_, label), row in zip(core.TIME_SINKS, allt):
+                print("    %21s: " % label + ", ".join("%4.6g" % v for v in row))
+            print()
+
+    def time_spent_on(self, time_sink):
+        """Seconds each process spent on time_sink (meep::time_sink enum value)."""
+        return self._times_all()[int(time_sink)].tolist()
+
+    def mean_time_spent_on(self, time_sink):
+        t = self.time_spent_on(time_sink)
+        return sum(t) / len(t)
+
+    def get_timing_data(self):
+        allt = self._times_all()
+        return {k: allt[k].tolist() for k in range(allt.shape[0])}
+
+    def output_times(self, fname):
+        """fields::output_times: CSV, one header row of sink labels, one row per process."""
+        if self.fields is None:
+            return
+        if not fname.endswith(".csv"):
+            fname += ".csv"
+        allt = self._times_all()
+        if not self._is_master():
+            return
+        if verbosity.meep > 0:
+            print('outputting timing statistics to file "%s"...' % fname)
+        with open(fname, "w") as fh:
+            fh.write(", ".join(label for _, label in core.TIME_SINKS) + "\n")
+            for j in range(allt.shape[1]):
+                fh.write(", ".join("%g" % v for v in allt[:, j]) + "\n")
 
     def _run_sources_until(self, cond, step_funcs):
         self.init_sim()

@@ -84,3 +84,35 @@ def test_simulation_setup_host_side(libpath):
     with pytest.raises(NotImplementedError):
         mp.Source(mp.GaussianSource(1.0, fwidth=1.0), mp.Ez, center=mp.Vector3(),
                   amp_func_file="x.h5:amp")
+
+
+def test_time_sinks_follow_reference_enum():
+    """TIME_SINKS (python) and the MNL_SINK_* enum (include/meep_nl_amd.h) list
+    meep::time_sink in its order (src/meep.hpp:1610-1633)."""
+    import re
+    from meep_nl_amd import core
+    hdr = open(os.path.join(ROOT, "include", "meep_nl_amd.h")).read()
+    body = re.search(r"enum \{\s*(MNL_SINK_CONNECTING.*?)MNL_NUM_TIME_SINKS", hdr, re.S).group(1)
+    names = [n.strip() for n in body.split(",") if n.strip()]
+    assert len(names) == len(core.TIME_SINKS) == 22
+    ref = ["Connecting", "Stepping", "Boundaries", "MpiAllTime", "MpiOneTime", "FieldOutput",
+           "FourierTransforming", "MPBTime", "GetFarfieldsTime", "Other", "FieldUpdateB",
+           "FieldUpdateH", "FieldUpdateD", "FieldUpdateE", "BoundarySteppingB",
+           "BoundarySteppingWH", "BoundarySteppingPH", "BoundarySteppingH", "BoundarySteppingD",
+           "BoundarySteppingWE", "BoundarySteppingPE", "BoundarySteppingE"]
+    assert [k for k, _ in core.TIME_SINKS] == ref
+
+
+def test_verbosity_singleton():
+    import meep_nl_amd as mp
+    v = mp.verbosity
+    old = v.get()
+    try:
+        mp.verbosity(2)
+        assert v.meep == 2 and mp.simulation.Verbosity() is v
+        v.meep = 0
+        assert mp.verbosity() == 0
+        mp.quiet(False)
+        assert v.get() == 1
+    finally:
+        v.set(old)
