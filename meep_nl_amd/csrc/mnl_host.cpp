@@ -222,6 +222,11 @@ struct mnl_fields {
   std::vector<double> h_sig[3], h_kap[3], h_siginv[3];
   std::vector<void *> dev_allocs;
   Box interior;
+  // chi(2) Newton-Raphson runs only where chi2 != 0: the interior E update splits
+  // into the bounding box of those points (NR kernel) and the rest (plain kernel)
+  bool nr_split_done = false;
+  Box nr_in{};
+  std::vector<Box> nr_rest;
   std::vector<Box> shell;
   BoxList shell_list;
   // fused mode (DESIGN.md "Fused step")
@@ -282,6 +287,7 @@ struct mnl_fields {
   std::vector<long long> srcB_idx, srcD_idx, isrc_idx;  // local linear indices
   std::vector<int> srcB_comp, srcD_comp, isrc_comp;
   std::vector<unsigned char> isrc_zone;  // owning reference chunk (zone box) per isrc point
+  ISrcDev isrc_dev{};                    // device copy (sorted), built with the lists
   std::vector<std::pair<int, int>> srcB_ref, srcD_ref, isrc_ref;  // (group, point)
   // current sources per field type ([0] B, [1] D), in layer order (SrcDev)
   std::vector<double> src_amp[2];
@@ -1317,8 +1323,35 @@ int build_source_lists(mnl_fields *F) {
       }
     }
   }
-  if (F->isrc_idx.size() > (size_t)MAX_ISRC)
-    return fail("too many integrated source points (max 64)");
+  // integrated dipoles for the E kernels: sorted by local index (stable, so the
+  // entries of one point keep list order), with their position in the table
+  F->isrc_dev = ISrcDev{};
+  if (!F->isrc_idx.empty()) {
+    const size_t n = F->isrc_idx.size();
+    std::vector<int> ord(n);
+    for (size_t k = 0; k < n; k++) ord[k] = (int)k;
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](int a, int b) { return F->isrc_idx[a] < F->isrc_idx[b]; });
+    std::vector<long long> si(n);
+    std::vector<int> sc(n), so(n);
+    std::vector<unsigned char> sz(n);
+    for (size_t k = 0; k < n; k++)
+      si[k] = F->isrc_idx[ord[k]], sc[k] = F->isrc_comp[ord[k]], sz[k] = F->isrc_zone[ord[k]],
+      so[k] = ord[k];
+    long long *di;
+    int *dc, *dor;
+    unsigned char *dz;
+    if (dev_alloc(F, &di, n, false) || dev_alloc(F, &dc, n, false) || dev_alloc(F, &dor, n, false) ||
+        dev_alloc(F, &dz, n, false))
+      return -1;
+    HIPCHK(hipMemcpyAsync(di, si.data(), n * 8, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(dc, sc.data(), n * 4, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(dor, so.data(), n * 4, hipMemcpyHostToDevice, F->stream));
+    HIPCHK(hipMemcpyAsync(dz, sz.data(), n, hipMemcpyHostToDevice, F->stream));
+    F->isrc_dev.n = (int)n;
+    F->isrc_dev.idx = di, F->isrc_dev.comp = dc, F->isrc_dev.orig = dor, F->isrc_dev.zone = dz;
+    F->isrc_dev.imin = si.front(), F->isrc_dev.imax = si.back();
+  }
   // layers: the k-th occurrence of a (component, point) goes to layer k, so a layer
   // is applied in parallel and the layers in list order (step_source order)
   for (int t = 0; t < 2; t++) {
@@ -2511,9 +2544,7 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
     return fail("curl D launch failed");
   if (sD.n && k_source(T_D, g, f, sD, 0, F->stream)) return fail("source launch failed");
   if (!fuseE) {
-    ISrcDev is;
-    is.n = 0;
-    is.val = nullptr;
+    ISrcDev is{};
     if (k_update_e(F->interior, sl, g, f, is, 0, true, F->stream))
       return fail("update E launch failed");
   }
@@ -2564,6 +2595,62 @@ int e_lazy_copy(mnl_fields *F) {
         k_copy(f.WE[d], f.E[d], (long long)F->nlocal, F->stream))
       return fail("copy launch failed");
   F->e_first_done = true;
+  return 0;
+}
+
+// Interior E update with chi(2) Newton-Raphson: the NR kernel over the bounding
+// box of chi2 != 0 inside the interior, the plain kernel over the rest (outside
+// that box chi2 = 0, so every point takes E = chi1inv * (D - P) either way).
+int nr_interior_e(mnl_fields *F, const ISrcDev &is) {
+  const DevGrid &g = F->g;
+  if (!F->nr_split_done) {
+    int *d = nullptr;
+    HIPCHK(hipMalloc(&d, 6 * sizeof(int)));
+    std::unique_ptr<void, void (*)(void *)> guard(d, [](void *p) { (void)hipFree(p); });
+    int box[6] = {INT32_MAX, INT32_MAX, INT32_MAX, -1, -1, -1};
+    HIPCHK(hipMemcpyAsync(d, box, sizeof box, hipMemcpyHostToDevice, F->stream));
+    const double *c2[3] = {F->f.chi2[0], F->f.chi2[1], F->f.chi2[2]};
+    if (k_nonzero_box(c2, g, d, F->stream)) return fail("chi2 box failed");
+    HIPCHK(hipMemcpyAsync(box, d, sizeof box, hipMemcpyDeviceToHost, F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+    const Box &I = F->interior;
+    Box n;
+    bool empty = false;
+    for (int k = 0; k < 3; k++) {  // 3-D: device axis k == direction k
+      n.lo[k] = std::max(box[k], I.lo[k]);
+      n.hi[k] = std::min(box[3 + k], I.hi[k]);
+      empty = empty || n.hi[k] < n.lo[k];
+    }
+    F->nr_rest.clear();
+    if (empty) {
+      F->nr_in.lo[0] = 1, F->nr_in.hi[0] = 0;
+      F->nr_rest.push_back(I);
+    } else {
+      F->nr_in = n;
+      Box r = I;  // peel z, then y, then x slabs off the interior
+      for (int k = 2; k >= 0; k--) {
+        if (r.lo[k] < n.lo[k]) {
+          Box b = r;
+          b.hi[k] = n.lo[k] - 1;
+          F->nr_rest.push_back(b);
+        }
+        if (r.hi[k] > n.hi[k]) {
+          Box b = r;
+          b.lo[k] = n.hi[k] + 1;
+          F->nr_rest.push_back(b);
+        }
+        r.lo[k] = n.lo[k], r.hi[k] = n.hi[k];
+      }
+    }
+    F->nr_split_done = true;
+  }
+  if (F->nr_in.hi[0] >= F->nr_in.lo[0] &&
+      k_update_e(F->nr_in, nullptr, g, F->f, is, 0, false, F->stream))
+    return fail("update E launch failed");
+  DevFields plain = F->f;
+  plain.nr_enabled = 0;
+  for (const Box &b : F->nr_rest)
+    if (k_update_e(b, nullptr, g, plain, is, 0, false, F->stream)) return fail("update E launch failed");
   return 0;
 }
 
@@ -2683,11 +2770,9 @@ int step_batch(mnl_fields *F, int nsteps) {
       const DevGrid &g = F->g;
       const double *vs = F->d_vals + (size_t)s * per;  // this step's table
       const SrcDev sB = src_dev(F, 0, vs), sD = src_dev(F, 1, vs + 2 * ng);
-      ISrcDev is;
+      ISrcDev is = F->isrc_dev;
       is.n = (int)nI;
-      for (size_t k = 0; k < nI; k++)
-        is.idx[k] = F->isrc_idx[k], is.comp[k] = F->isrc_comp[k], is.zone[k] = F->isrc_zone[k];
-      is.val = vs + jofs;  // kernels index val[step * n + k] with step 0
+      is.val = vs + jofs;  // kernels index val[step * n + orig] with step 0
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
         continue;
@@ -2780,8 +2865,12 @@ int step_batch(mnl_fields *F, int nsteps) {
       // neighbour reads of D - P (NR, upstream chi) or of W (anisotropic sigma):
       // P after all of E
       bool fuse = !F->nr && !F->upnl && !f.aniso;
-      if ((!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) ||
-          (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream)))
+      if (!F->fused && F->nr && F->S.dim == 3) {
+        if (nr_interior_e(F, is)) return -1;
+      } else if (!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) {
+        return fail("update E launch failed");
+      }
+      if (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream))
         return fail("update E launch failed");
       if (f.aniso && !f.wall_e && k_aniso_wall(g, f, 0, F->stream))
         return fail("wall W launch failed");
@@ -3811,9 +3900,7 @@ int initialize_field(mnl_fields *F, int c, const double *host) {
     const int kind = t == T_E ? 0 : t == T_D ? 2 : 1;
     if (exchange(F, kind)) return fail("initialize_field halo exchange failed");
   }
-  ISrcDev is;
-  is.n = 0;
-  is.val = nullptr;
+  ISrcDev is{};
   if (t == T_D) {  // update_eh(E_stuff); step_boundaries(E_stuff)
     if (!F->e_first_done && e_lazy_copy(F)) return -1;
     if (k_update_e(F->interior, nullptr, F->g, f, is, 0, false, F->stream) ||

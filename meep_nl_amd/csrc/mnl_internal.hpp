@@ -16,7 +16,6 @@
 namespace mnl {
 
 constexpr int MAX_POL = 4;    // Lorentzian susceptibilities per structure
-constexpr int MAX_ISRC = 64;  // integrated-source points handled inside the E kernel
 constexpr int MAX_BOX = 7;    // interior + 6 shell boxes
 
 enum { T_E = 0, T_H = 1, T_D = 2, T_B = 3 };
@@ -158,12 +157,16 @@ struct SrcDev {
 
 struct ISrcDev {             // integrated sources, read by the E kernel
   int n;
-  long long idx[MAX_ISRC];
-  int comp[MAX_ISRC];
-  // reference chunk (zone box zx*9+zy*3+zz) owning the point: only that chunk's
-  // f_minus_p has the dipole subtracted (src/update_eh.cpp:136-146 loops over the
-  // chunk's own src_vols); another chunk reading it as a ghost sees D - P only
-  unsigned char zone[MAX_ISRC];
+  // entries sorted by local index (stable: one point's entries stay in list
+  // order), each with its component, owning reference chunk (zone box
+  // zx*9+zy*3+zz: only that chunk's f_minus_p has the dipole subtracted,
+  // src/update_eh.cpp:136-146; another chunk reading it as a ghost sees D - P
+  // only) and its position in the per-step value table
+  const long long *idx;
+  const int *comp;
+  const unsigned char *zone;
+  const int *orig;
+  long long imin, imax;      // index range of the entries
   const double *val;         // [step][n] dipole value real(amp*dipole(t+dt))
 };
 

@@ -480,6 +480,38 @@ __device__ __forceinline__ int zone_box(const DevFields &f, const DevGrid &g, co
   return zb;
 }
 
+// a[c] without a runtime index into a kernel-argument array (which makes the
+// compiler copy the whole argument struct to scratch)
+template <typename T>
+__device__ __forceinline__ T sel3(T const (&a)[3], int c) {
+  return c == 0 ? a[0] : (c == 1 ? a[1] : a[2]);
+}
+
+// integrated dipoles subtracted from f_minus_p of component c at index n, in
+// list order; zone_rz >= 0: only those the reader's reference chunk owns
+__device__ __forceinline__ double isrc_sub(const ISrcDev &is, int step, int c, long long n,
+                                           int zone_rz, double v) {
+  if (n < is.imin || n > is.imax) return v;
+  int k = 0;
+  if (is.n > 16) {  // lower bound of n in the sorted entries
+    int hi = is.n;
+    while (k < hi) {
+      const int mid = (k + hi) >> 1;
+      if (is.idx[mid] < n)
+        k = mid + 1;
+      else
+        hi = mid;
+    }
+  }
+  for (; k < is.n; k++) {
+    const long long ik = is.idx[k];
+    if (ik > n) break;
+    if (ik == n && is.comp[k] == c && (zone_rz < 0 || is.zone[k] == zone_rz))
+      v -= is.val[(long long)step * is.n + is.orig[k]];
+  }
+  return v;
+}
+
 // f_minus_p at the point itself, skipping polarizations that are 0 there
 template <bool ISRC>
 __device__ __forceinline__ double dmp_own(const DevFields &f, const ISrcDev &is, int step, int c,
@@ -487,10 +519,7 @@ __device__ __forceinline__ double dmp_own(const DevFields &f, const ISrcDev &is,
   double v = f.Dn[c][n];
   for (int k = 0; k < f.npol; k++)
     if (((pm >> k) & 1) && f.pol[k].P[c]) v -= f.pol[k].P[c][n];
-  if (ISRC) {
-    for (int k = 0; k < is.n; k++)
-      if (is.comp[k] == c && is.idx[k] == n) v -= is.val[(long long)step * is.n + k];
-  }
+  if (ISRC) v = isrc_sub(is, step, c, n, -1, v);
   return v;
 }
 
@@ -500,14 +529,12 @@ __device__ __forceinline__ double dmp_own(const DevFields &f, const ISrcDev &is,
 template <bool ISRC>
 __device__ __forceinline__ double dmp_at(const DevFields &f, const ISrcDev &is, int step, int c,
                                          long long n, int rz) {
-  double v = f.Dn[c][n];
-  for (int k = 0; k < f.npol; k++)
-    if (f.pol[k].P[c]) v -= f.pol[k].P[c][n];
-  if (ISRC) {
-    for (int k = 0; k < is.n; k++)
-      if (is.comp[k] == c && is.idx[k] == n && is.zone[k] == rz)
-        v -= is.val[(long long)step * is.n + k];
+  double v = sel3(f.Dn, c)[n];
+  for (int k = 0; k < f.npol; k++) {
+    const double *P = sel3(f.pol[k].P, c);
+    if (P) v -= P[n];
   }
+  if (ISRC) v = isrc_sub(is, step, c, n, rz, v);
   return v;
 }
 
@@ -524,46 +551,71 @@ __device__ __forceinline__ double calc_nonlinear_u(double Dsqr, double Di, doubl
 // update_eh(E_stuff) -> step_update_EDHB (src/update_eh.cpp:67-283,
 // src/step_generic.cpp:576-906) + lorentzian update_P (src/susceptibility.cpp:
 // 188-262) fused when no Newton-Raphson neighbour reads are needed.
-template <bool SHELL, bool NR, bool ISRC, bool FUSEPOL>
-__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList bl, DevGrid g,
-                                                                   DevFields f, ISrcDev is,
-                                                                   int step) {
-  Pt p;
-  if (!map_pt<SHELL>(b, bl, g, p)) return;
-  const long long i = p.idx;
-  const unsigned pm = pol_mask(f, p);
-  for (int d = 0; d < 3; d++) {
-    if (!f.ecomp_present[d]) continue;
+// D - P of component e at i [+ s along d] [- s_e along e] as the reader's
+// chunk (zone box rz) holds it; WCHK: a wall point another chunk owns is never
+// connected (boundaries.cpp:347-460), so the reader's copy there stays 0.
+// Directions are template arguments: runtime indices into kernel-argument
+// arrays make the compiler copy the argument struct to scratch.
+template <int d, int e, bool UPS, bool DN, bool WCHK, bool ISRC>
+__device__ __forceinline__ double nbr_t(const DevGrid &g, const DevFields &f, const ISrcDev &is,
+                                        int step, const Pt &p, long long i, int rz) {
+  long long n = i;
+  Pt q = p;
+  if (UPS) {
+    n += g.sdir[d];
+    if (g.ax[d] >= 0) q.j[d] += 1;
+  }
+  if (DN) {
+    n -= g.sdir[e];
+    if (g.ax[e] >= 0) q.j[e] -= 1;
+  }
+  if (WCHK && f.wall_e && on_wall(g, e, q, true) && zone_box(f, g, q, e) != rz) return 0.0;
+  return dmp_at<ISRC>(f, is, step, e, n, rz);
+}
+
+// g[i] + g[i + s] + g[i - s_e] + g[i + (s - s_e)] (the four-point sums of
+// src/step_generic.cpp:611-612, 740-743)
+template <int d, int e, bool WCHK, bool ISRC>
+__device__ __forceinline__ double nsum_t(const DevGrid &g, const DevFields &f, const ISrcDev &is,
+                                         int step, const Pt &p, long long i, int rz) {
+  return nbr_t<d, e, false, false, WCHK, ISRC>(g, f, is, step, p, i, rz) +
+         nbr_t<d, e, true, false, WCHK, ISRC>(g, f, is, step, p, i, rz) +
+         nbr_t<d, e, false, true, WCHK, ISRC>(g, f, is, step, p, i, rz) +
+         nbr_t<d, e, true, true, WCHK, ISRC>(g, f, is, step, p, i, rz);
+}
+
+// OFFDIAG(u, g, sx), src/step_generic.cpp:597-598
+template <int d, int e, bool WCHK, bool ISRC>
+__device__ __forceinline__ double offdiag_t(const double *uo, const DevGrid &g, const DevFields &f,
+                                            const ISrcDev &is, int step, const Pt &p, long long i,
+                                            int rz) {
+  const long long s = g.sdir[d];
+  return 0.25 * ((nbr_t<d, e, false, false, WCHK, ISRC>(g, f, is, step, p, i, rz) +
+                  nbr_t<d, e, false, true, WCHK, ISRC>(g, f, is, step, p, i, rz)) * uo[i] +
+                 (nbr_t<d, e, true, false, WCHK, ISRC>(g, f, is, step, p, i, rz) +
+                  nbr_t<d, e, true, true, WCHK, ISRC>(g, f, is, step, p, i, rz)) * uo[i + s]);
+}
+
+// One E component of update_e_kernel; d is a template argument so every
+// per-component kernel-argument array (f.E[d], f.inveps[d], ...) is indexed with
+// a constant (a runtime index makes the compiler copy DevFields to scratch).
+template <int d, bool SHELL, bool NR, bool UP, bool ISRC, bool FUSEPOL>
+__device__ __forceinline__ void e_point(const DevGrid &g, const DevFields &f, const ISrcDev &is,
+                                        int step, const Pt &p, long long i, unsigned pm) {
+    if (!f.ecomp_present[d]) return;
     // wall_e: also the high metallic wall plane, which the reference's chunk owns
     // and updates (D = 0 there) before step_boundaries zeroes it; the transient
     // E feeds update_P there (aniso_wall_kernel zeroes it afterwards)
-    if (!owned(g, T_E, d, p) && !(f.wall_e && on_wall(g, d, p))) continue;
+    if (!owned(g, T_E, d, p) && !((NR || UP) && f.wall_e && on_wall(g, d, p))) return;
     const double gs = dmp_own<ISRC>(f, is, step, d, i, pm);
     // reference chunk of this voxel (zone box; interior kernels: 13 = interior chunk)
     int rz = 13;
-    if ((SHELL && (NR || ISRC || f.upnl)) || f.wall_e) {
+    if ((SHELL && (NR || UP || ISRC)) || ((NR || UP) && f.wall_e)) {
       int z3[3];
 #pragma unroll
       for (int e = 0; e < 3; e++) z3[e] = g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_E, d, e)] : 1;
       rz = z3[0] * 9 + z3[1] * 3 + z3[2];
     }
-    // D - P of component e at i [+ s along d] [- s_e along e] as chunk rz holds it:
-    // a wall point another chunk owns is never connected (boundaries.cpp:347-460),
-    // so the reader's copy there stays 0
-    auto nbr = [&](int e, bool up, bool dn) -> double {
-      long long n = i;
-      Pt q = p;
-      if (up) {
-        n += g.sdir[d];
-        if (g.ax[d] >= 0) q.j[d] += 1;
-      }
-      if (dn) {
-        n -= g.sdir[e];
-        if (g.ax[e] >= 0) q.j[e] -= 1;
-      }
-      if (f.wall_e && on_wall(g, e, q, true) && zone_box(f, g, q, e) != rz) return 0.0;
-      return dmp_at<ISRC>(f, is, step, e, n, rz);
-    };
     const double *u = f.inveps[d];
     const double *E = f.E[d];
     double *En = f.En[d];
@@ -577,43 +629,54 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
     double unl = 0;  // upstream mode: step_update_EDHB as upstream Meep runs it
                      // (src/step_generic.cpp:597-726, 730-886 with the fork's disabled
                      // branches restored; u = 1 where trivial)
-    if (f.upnl) {
-      const int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
+    if (UP) {  // upstream mode (UP == f.upnl)
+      constexpr int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
       const long long s = g.sdir[d];
-      auto nsum = [&](int e) {
-        return nbr(e, false, false) + nbr(e, true, false) + nbr(e, false, true) + nbr(e, true, true);
-      };
-      // OFFDIAG(u, g, sx), src/step_generic.cpp:597-598
-      auto offdiag = [&](const double *uo, int e) {
-        return 0.25 * ((nbr(e, false, false) + nbr(e, false, true)) * uo[i] +
-                       (nbr(e, true, false) + nbr(e, true, true)) * uo[i + s]);
-      };
       const double us = u ? u[i] : 1.0;
       const bool h1 = f.ecomp_present[d1] != 0, h2 = f.ecomp_present[d2] != 0;
+      // D - P of the partner components at i, i + s, i - s_e, i + (s - s_e), read
+      // once: the four-point sums (611-612) and OFFDIAG (597-598) combine them
+      double a[4] = {0, 0, 0, 0}, c[4] = {0, 0, 0, 0};
+      if (h1) {
+        a[0] = nbr_t<d, d1, false, false, true, ISRC>(g, f, is, step, p, i, rz);
+        a[1] = nbr_t<d, d1, true, false, true, ISRC>(g, f, is, step, p, i, rz);
+        a[2] = nbr_t<d, d1, false, true, true, ISRC>(g, f, is, step, p, i, rz);
+        a[3] = nbr_t<d, d1, true, true, true, ISRC>(g, f, is, step, p, i, rz);
+      }
+      if (h2) {
+        c[0] = nbr_t<d, d2, false, false, true, ISRC>(g, f, is, step, p, i, rz);
+        c[1] = nbr_t<d, d2, true, false, true, ISRC>(g, f, is, step, p, i, rz);
+        c[2] = nbr_t<d, d2, false, true, true, ISRC>(g, f, is, step, p, i, rz);
+        c[3] = nbr_t<d, d2, true, true, true, ISRC>(g, f, is, step, p, i, rz);
+      }
+      const double g1s = a[0] + a[1] + a[2] + a[3], g2s = c[0] + c[1] + c[2] + c[3];
+      auto offd = [&](const double *uo, const double *w) {  // OFFDIAG(u, g, sx)
+        return 0.25 * ((w[0] + w[2]) * uo[i] + (w[1] + w[3]) * uo[i + s]);
+      };
       // off-diagonal rows this reference chunk keeps (trivial rows are deallocated,
       // src/anisotropic_averaging.cpp:285-296)
       const unsigned ob = (f.offd_zone[rz] >> (3 * d)) & 3u;
-      const bool o1 = (ob & 1u) && h1 && f.offd[d][0], o2 = (ob & 2u) && h2 && f.offd[d][1];
+      const double *u1 = f.offd[d][0], *u2 = f.offd[d][1];
+      const bool o1 = (ob & 1u) && h1 && u1, o2 = (ob & 2u) && h2 && u2;
       double v, dsq;
       if (o1 && o2) {  // 3x3 (617, 772)
-        v = gs * us + offdiag(f.offd[d][0], d1) + offdiag(f.offd[d][1], d2);
-        const double g1s = nsum(d1), g2s = nsum(d2);
+        v = gs * us + offd(u1, a) + offd(u2, c);
         dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
-      } else if (o1 || o2) {  // 2x2, the present row first (590-594, 646, 835)
-        const int e = o1 ? d1 : d2;
-        v = gs * us + offdiag(o1 ? f.offd[d][0] : f.offd[d][1], e);
-        const double g1s = nsum(e);
+      } else if (o1) {  // 2x2, the present row first (590-594, 646, 835)
+        v = gs * us + offd(u1, a);
         dsq = gs * gs + 0.0625 * (g1s * g1s);
+      } else if (o2) {
+        v = gs * us + offd(u2, c);
+        dsq = gs * gs + 0.0625 * (g2s * g2s);
       } else {  // diagonal (668-702, 853-884)
         v = gs * us;
         dsq = gs * gs;
-        if (h1 && h2) {
-          const double g1s = nsum(d1), g2s = nsum(d2);
+        if (h1 && h2)
           dsq = gs * gs + 0.0625 * (g1s * g1s + g2s * g2s);
-        } else if (h1 || h2) {
-          const double g1s = nsum(h1 ? d1 : d2);
+        else if (h1)
           dsq = gs * gs + 0.0625 * (g1s * g1s);
-        }
+        else if (h2)
+          dsq = gs * gs + 0.0625 * (g2s * g2s);
       }
       // chunks without chi2/chi3 skip the factor; chi2 = chi3 = 0 makes it exactly 1
       unl = v * calc_nonlinear_u(dsq, gs, us, f.chi2[d][i], f.chi3[d][i]);
@@ -621,7 +684,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
     if (pml) {
       double fwprev = f.WE[d][i];
       double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
-      double fw = f.upnl ? unl : (u ? (gs * u[i]) : gs);
+      double fw = UP ? unl : (u ? (gs * u[i]) : gs);
       f.WE[d][i] = fw;
       En[i] = E[i] + ((kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev);
       wv = fw;
@@ -639,12 +702,8 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
           double chi2new = f.chi2[d][i];
           int zc = (u[i] == 0) + (u1[i] == 0) + (u2[i] == 0);
           if (!(chi2new == 0 || zc > 1)) {
-            double gs_2 = (nbr(d1, false, false) + nbr(d1, true, false) + nbr(d1, false, true) +
-                           nbr(d1, true, true)) *
-                          0.25;
-            double gs_3 = (nbr(d2, false, false) + nbr(d2, true, false) + nbr(d2, false, true) +
-                           nbr(d2, true, true)) *
-                          0.25;
+            double gs_2 = nsum_t<d, (d + 1) % 3, true, ISRC>(g, f, is, step, p, i, rz) * 0.25;
+            double gs_3 = nsum_t<d, (d + 2) % 3, true, ISRC>(g, f, is, step, p, i, rz) * 0.25;
             double us = 1 / u[i];
             double us_2 = us, us_3 = us;
             double dummy1 = 0.0, dummy2 = 0.0;
@@ -675,7 +734,7 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
           }
         }
       }
-      if (!done) En[i] = f.upnl ? unl : (u ? (gs * u[i]) : gs);
+      if (!done) En[i] = UP ? unl : (u ? (gs * u[i]) : gs);
       wv = En[i];
     }
     if (FUSEPOL) {
@@ -689,6 +748,18 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList
       }
     }
   }
+
+template <bool SHELL, bool NR, bool UP, bool ISRC, bool FUSEPOL>
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_e_kernel(Box b, BoxList bl, DevGrid g,
+                                                                   DevFields f, ISrcDev is,
+                                                                   int step) {
+  Pt p;
+  if (!map_pt<SHELL>(b, bl, g, p)) return;
+  const long long i = p.idx;
+  const unsigned pm = pol_mask(f, p);
+  e_point<0, SHELL, NR, UP, ISRC, FUSEPOL>(g, f, is, step, p, i, pm);
+  e_point<1, SHELL, NR, UP, ISRC, FUSEPOL>(g, f, is, step, p, i, pm);
+  e_point<2, SHELL, NR, UP, ISRC, FUSEPOL>(g, f, is, step, p, i, pm);
 }
 
 // lorentzian update_P, isotropic (src/susceptibility.cpp:251-258), used after
@@ -970,35 +1041,43 @@ int k_update_h(const BoxList &sh, const DevGrid &g, const DevFields &f, void *st
   return rc();
 }
 
-template <bool SHELL, bool NR, bool ISRC, bool FUSE>
+template <bool SHELL, bool NR, bool UP, bool ISRC, bool FUSE>
 static void launch_e1(const Box &in, const BoxList &bl, const DevGrid &g, const DevFields &f,
                       const ISrcDev &is, int step, hipStream_t s) {
   if (SHELL)
-    update_e_kernel<true, NR, ISRC, FUSE><<<lin_grid(bl), 256, 0, s>>>(in, bl, g, f, is, step);
+    update_e_kernel<true, NR, UP, ISRC, FUSE><<<lin_grid(bl), 256, 0, s>>>(in, bl, g, f, is, step);
   else
-    update_e_kernel<false, NR, ISRC, FUSE><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(
+    update_e_kernel<false, NR, UP, ISRC, FUSE><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(
         in, bl, g, f, is, step);
 }
 
+// kernel variant per mode: Newton-Raphson (fork, chi2 + 3x3 chi1inv), upstream
+// (Pade chi, OFFDIAG), or plain (E = chi1inv * (D - P), Lorentzian P fused when
+// allowed); integrated sources or not
 template <bool SHELL>
 static void launch_e(const Box &in, const BoxList &bl, const DevGrid &g, const DevFields &f,
                      const ISrcDev &is, int step, bool fuse, hipStream_t s) {
-  const bool nr = f.nr_enabled != 0, isrc = is.n > 0;
+  const bool nr = f.nr_enabled != 0, up = f.upnl != 0, isrc = is.n > 0;
   if (nr) {
     if (isrc)
-      launch_e1<SHELL, true, true, false>(in, bl, g, f, is, step, s);
+      launch_e1<SHELL, true, false, true, false>(in, bl, g, f, is, step, s);
     else
-      launch_e1<SHELL, true, false, false>(in, bl, g, f, is, step, s);
+      launch_e1<SHELL, true, false, false, false>(in, bl, g, f, is, step, s);
+  } else if (up) {
+    if (isrc)
+      launch_e1<SHELL, false, true, true, false>(in, bl, g, f, is, step, s);
+    else
+      launch_e1<SHELL, false, true, false, false>(in, bl, g, f, is, step, s);
   } else if (fuse) {
     if (isrc)
-      launch_e1<SHELL, false, true, true>(in, bl, g, f, is, step, s);
+      launch_e1<SHELL, false, false, true, true>(in, bl, g, f, is, step, s);
     else
-      launch_e1<SHELL, false, false, true>(in, bl, g, f, is, step, s);
+      launch_e1<SHELL, false, false, false, true>(in, bl, g, f, is, step, s);
   } else {
     if (isrc)
-      launch_e1<SHELL, false, true, false>(in, bl, g, f, is, step, s);
+      launch_e1<SHELL, false, false, true, false>(in, bl, g, f, is, step, s);
     else
-      launch_e1<SHELL, false, false, false>(in, bl, g, f, is, step, s);
+      launch_e1<SHELL, false, false, false, false>(in, bl, g, f, is, step, s);
   }
 }
 
