@@ -48,6 +48,34 @@ def test_volume_sources_bitwise(G):
     _bitwise(sc_volume_sources(G), sc_volume_sources(make_oracle))
 
 
+def sc_integrated_planes(make, steps=30):
+    """Integrated (dipole) volume sources: ~1700 points on two off-grid planes
+    crossing PML chunks and slab seams, the same plane twice (one point's entries
+    subtracted in list order), a Lorentzian so the dipoles enter D - P."""
+    o = S.vol(make, 3, [3.0, 2.6, 2.8], 10, center_origin=True)
+    o.add_pml(0.6)
+    sig = []
+    for c in range(3):
+        x, y, z = o.coords(c)
+        sig.append(np.where(np.abs(x) < 0.5, 0.3, 0.0))
+    o.add_lorentzian(1.2, 0.1, sig)
+    o.add_gaussian_volume_source(1, 0.3, 4.0, 0.0, 30.0, (0.117, -1.3, -1.4), (0.117, 1.3, 1.4),
+                                 0.7, is_integrated=True)
+    o.add_gaussian_volume_source(1, 0.3, 4.0, 0.0, 30.0, (0.117, -1.3, -1.4), (0.117, 1.3, 1.4),
+                                 0.25, is_integrated=True)
+    o.add_gaussian_volume_source(2, 0.35, 4.0, 0.0, 30.0, (-1.1, -0.43, -1.4), (1.1, -0.43, 1.4),
+                                 complex(0.3, 0.2), is_integrated=True)
+    o.step(steps)
+    return o
+
+
+@pytest.mark.parametrize("G", [ProductSim, GroupSim3])
+def test_integrated_volume_sources_bitwise(G):
+    """Beyond the 64 points the E kernel once took from its arguments: sorted
+    device arrays, binary search per point."""
+    _bitwise(sc_integrated_planes(G), sc_integrated_planes(make_oracle))
+
+
 def test_volume_source_2d_and_custom():
     def run(make):
         o = S.vol(make, 2, [2.3, 1.9], 10)
