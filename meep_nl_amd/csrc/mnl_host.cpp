@@ -2183,14 +2183,31 @@ bool make_fused_boxes(mnl_fields *F) {
         narrow.push_back(tx | (ty << 8) | (ch << 16));
       }
   }
-  a.ngen_n = (int)narrow.size();
-  a.ngen_e = a.ngen_ne = 0;
+  // one launch takes both shapes (bit 31 marks a 16-column tile): chunk-0 items
+  // first (the early launch of multi-rank steps), then the rest longest first
+  // (most planes), so the shortest items fill the launch's tail
+  for (int &v : narrow) v |= (int)0x80000000u;
+  std::vector<int> all;
+  all.reserve(F->gitems.size() + narrow.size());
   for (int v : F->gitems)
-    if ((v >> 16) == 0) a.ngen_e++;
+    if (((v >> 16) & 0x7fff) == 0) all.push_back(v);
   for (int v : narrow)
-    if ((v >> 16) == 0) a.ngen_ne++;
+    if (((v >> 16) & 0x7fff) == 0) all.push_back(v);
+  a.ngen_e = (int)all.size();
+  std::vector<int> rest;
+  for (int v : F->gitems)
+    if (((v >> 16) & 0x7fff) != 0) rest.push_back(v);
+  for (int v : narrow)
+    if (((v >> 16) & 0x7fff) != 0) rest.push_back(v);
+  auto planes = [&](int v) {
+    const int ch = (v >> 16) & 0x7fff;
+    return a.zb[ch + 1] - a.zb[ch];
+  };
+  std::stable_sort(rest.begin(), rest.end(), [&](int x, int y) { return planes(x) > planes(y); });
+  all.insert(all.end(), rest.begin(), rest.end());
+  F->gitems.swap(all);
   a.ngen = (int)F->gitems.size();
-  F->gitems.insert(F->gitems.end(), narrow.begin(), narrow.end());
+  a.ngen_n = a.ngen_ne = 0;
   for (int k = 0; k < 3; k++) {
     a.N[k] = g.N[k];
     a.off[k] = g.off[k];

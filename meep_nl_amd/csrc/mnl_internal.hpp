@@ -222,6 +222,10 @@ constexpr int FUSED_MAXGY = 256, FUSED_MAXNY = 64;
 constexpr int FUSED_GW_ROWS = MNL_GW_ROWS;  // general kernel, wide tiles: own rows per tile
 constexpr int FUSED_GN_ROWS = MNL_GN_ROWS;  // general kernel, 16-column tiles: own rows per tile
 constexpr int FUSED_GEN_BPC = MNL_GEN_BPC;  // general kernel workgroups per CU
+#ifndef MNL_GEN_WPE
+#define MNL_GEN_WPE 1
+#endif
+constexpr int FUSED_GEN_WPE = MNL_GEN_WPE;  // general kernel: minimum waves per SIMD (VGPR cap)
 struct FusedTab {                // per direction, indexed by global half-coordinate q
   const uint8_t *flag[3];        // PML chunk along the direction (f_u / W branches)
   const double *kms[3];          // kap - sig

@@ -1739,7 +1739,9 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   }
 }
 
-// General tiles: items from the host-built list a.gitems (tx | ty << 8 | ch << 16).
+// General tiles: items from the host-built list a.gitems (tx | ty << 8 | ch << 16,
+// bit 31 set for a 16-column tile).  One launch takes both tile shapes, so the
+// two share one tail:
 // TX = 64: tiles of <= 64 columns x FUSED_GW_ROWS rows (ty indexes a.gyb);
 // TX = 16: the narrow x-face tiles, 16 columns x FUSED_GN_ROWS rows (ty indexes
 // a.nyb), four rows per wave so a plane step does as much work as a wide tile.
@@ -1752,19 +1754,46 @@ struct GenShape {
 };
 static_assert(GenShape<64>::R - 1 == FUSED_GW_ROWS && GenShape<16>::R - 1 == FUSED_GN_ROWS,
               "general tile rows");
+static_assert(GenShape<64>::WAVES == GenShape<16>::WAVES, "both tile shapes run in one workgroup");
+constexpr int GEN_WAVES = GenShape<64>::WAVES;
+
+template <int TX>
+struct GenLds {  // LDS of one tile shape (the two shapes share it through a union)
+  static constexpr int R = GenShape<TX>::R;
+  double sE[3][R + 1][TX + 2];
+  double sB[3][R][TX + 1];
+  TabE sTx[TX + 2][2], sTy[R + 1][2], sTz[TPZ][2];
+  unsigned char sFx[TX + 2][2], sFy[R + 1][2], sFz[TPZ][2];
+};
+
 template <int UMODE, int TX, int POL>
-__global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel(FusedArgs a) {
-  constexpr int R = GenShape<TX>::R, NW = GenShape<TX>::NW;
+__device__ __forceinline__ void general_item(const FusedArgs &a, int item, GenLds<TX> &L,
+                                             const double (*sU)[256]) {
+  const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 0x7fff;
+  const int *yb = TX == 64 ? a.gyb : a.nyb;
+  ItemGeo itg;
+  itg.x0 = a.xb[tx];
+  itg.x1 = a.xb[tx + 1] - 1;
+  itg.y0 = yb[ty] - 1;
+  itg.y1 = yb[ty + 1] - 1;
+  itg.zs = a.zb[ch];
+  itg.ze = a.zb[ch + 1];
+  fused_general<UMODE, TX, GenShape<TX>::R, GenShape<TX>::NW, POL>(
+      a, itg, L.sE, L.sB, sU, L.sTx, L.sTy, L.sTz, L.sFx, L.sFy, L.sFz);
+}
+
+template <int UMODE, int POL>
+__global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_kernel(FusedArgs a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
-  __shared__ double sE[3][R + 1][TX + 2];
-  __shared__ double sB[3][R][TX + 1];
-  __shared__ TabE sTx[TX + 2][2], sTy[R + 1][2], sTz[TPZ][2];
-  __shared__ unsigned char sFx[TX + 2][2], sFy[R + 1][2], sFz[TPZ][2];
+  __shared__ union {
+    GenLds<64> w;
+    GenLds<16> n;
+  } L;
   __shared__ int s_item;
   if (UMODE == 2)
     for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) sU[i >> 8][i & 255] = a.utab[i];
   // ngrp > 1: the workgroups sharing an XCD (blockIdx % ngrp) take a contiguous
-  // share of the (chunk-major) item list from their own counter line
+  // share of the item list from their own counter line
   const int grp = a.ngrp > 1 ? (int)(blockIdx.x % a.ngrp) : 0;
   const int ntot = a.gend - a.gbeg;
   const int base = a.gbeg + (int)((long long)ntot * grp / a.ngrp);
@@ -1772,7 +1801,6 @@ __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel
   unsigned long long *ctr =
       a.ctr + 16 * (a.ngrp > 1 ? FUSED_GLINE0 + (a.ctr_line - 8) * 8 + grp : a.ctr_line);
   const unsigned long long cb = a.ngrp > 1 ? a.cbg[grp] : a.cbase;
-  const int *yb = TX == 64 ? a.gyb : a.nyb;
   for (;;) {
     if (threadIdx.x == 0) {
       const unsigned long long v = atomicAdd(ctr, 1ULL) - cb;
@@ -1780,16 +1808,11 @@ __global__ __launch_bounds__(64 * GenShape<TX>::WAVES) void fused_general_kernel
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
-    if (item < 0) break;
-    const int tx = item & 255, ty = (item >> 8) & 255, ch = item >> 16;
-    ItemGeo itg;
-    itg.x0 = a.xb[tx];
-    itg.x1 = a.xb[tx + 1] - 1;
-    itg.y0 = yb[ty] - 1;
-    itg.y1 = yb[ty + 1] - 1;
-    itg.zs = a.zb[ch];
-    itg.ze = a.zb[ch + 1];
-    fused_general<UMODE, TX, R, NW, POL>(a, itg, sE, sB, sU, sTx, sTy, sTz, sFx, sFy, sFz);
+    if (item == -1) break;
+    if (item & (int)0x80000000u)
+      general_item<UMODE, 16, POL>(a, item, L.n, sU);
+    else
+      general_item<UMODE, 64, POL>(a, item, L.w, sU);
   }
 }
 
@@ -2131,23 +2154,22 @@ static int fused_grid_blocks(int bpc) {
   return cus[dev] * bpc;
 }
 
-template <int TX, int UM>
+template <int UM>
 static void launch_general_u(const FusedArgs &g, dim3 gr, dim3 b, hipStream_t s) {
   if (g.npol == 0)
-    fused_general_kernel<UM, TX, 0><<<gr, b, 0, s>>>(g);
+    fused_general_kernel<UM, 0><<<gr, b, 0, s>>>(g);
   else if (g.npol == 1)
-    fused_general_kernel<UM, TX, 1><<<gr, b, 0, s>>>(g);
+    fused_general_kernel<UM, 1><<<gr, b, 0, s>>>(g);
   else
-    fused_general_kernel<UM, TX, 2><<<gr, b, 0, s>>>(g);
+    fused_general_kernel<UM, 2><<<gr, b, 0, s>>>(g);
 }
-template <int TX>
 static void launch_general(const FusedArgs &g, int um, dim3 gr, dim3 b, hipStream_t s) {
   if (um == 2)
-    launch_general_u<TX, 2>(g, gr, b, s);
+    launch_general_u<2>(g, gr, b, s);
   else if (um == 1)
-    launch_general_u<TX, 1>(g, gr, b, s);
+    launch_general_u<1>(g, gr, b, s);
   else
-    launch_general_u<TX, 0>(g, gr, b, s);
+    launch_general_u<0>(g, gr, b, s);
 }
 
 int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bases) {
@@ -2169,42 +2191,31 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
     if (a.zb[t + 1] <= a.zb[t] || a.zb[t + 1] - a.zb[t] > FUSED_MAXCH) return 7;
   hipStream_t s = (hipStream_t)stream;
   const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
-  if (which >= 1) {  // general tiles: wide, then narrow
-    // item ranges in a.gitems: wide [0, ngen), narrow [ngen, ngen + ngen_n); chunk-0
-    // items lead each list
-    int wb = 0, we = a.ngen, nb_ = a.ngen, ne = a.ngen + a.ngen_n, line = 8;
-    if (which == 2) we = a.ngen_e, ne = a.ngen + a.ngen_ne, line = 10;
-    if (which == 3) wb = a.ngen_e, nb_ = a.ngen + a.ngen_ne;
+  if (which >= 1) {  // general tiles (both shapes, one launch)
+    // item range in a.gitems: [0, ngen); chunk-0 items lead ([0, ngen_e))
+    int ib = 0, ie = a.ngen, line = 8;
+    if (which == 2) ie = a.ngen_e, line = 10;
+    if (which == 3) ib = a.ngen_e;
     long long cus = fused_grid_blocks(FUSED_GEN_BPC);
     if (a.wg_limit > 0 && cus > a.wg_limit) cus = a.wg_limit;
-    FusedArgs g = a;
-    // set up one launch over items [ib, ie) on counter line ln (grouped per XCD
-    // when there are enough workgroups and items)
-    auto setup = [&](int ib, int ie, int ln, unsigned nblk) {
-      g.gbeg = ib, g.gend = ie, g.ctr_line = ln, g.cbase = bases[ln];
+    if (ie > ib) {
+      FusedArgs g = a;
+      const unsigned nblk = (unsigned)std::min<long long>(cus, ie - ib);
+      g.gbeg = ib, g.gend = ie, g.ctr_line = line, g.cbase = bases[line];
       const long long n = ie - ib;
       g.ngrp = (a.ngrp_gen > 1 && nblk >= (unsigned)a.ngrp_gen && n >= 4LL * a.ngrp_gen) ? a.ngrp_gen : 1;
       if (g.ngrp == 1) {
-        bases[ln] += (unsigned long long)n + nblk;
-        return;
+        bases[line] += (unsigned long long)n + nblk;
+      } else {
+        for (int q = 0; q < g.ngrp; q++) {
+          const int L = FUSED_GLINE0 + (line - 8) * 8 + q;
+          g.cbg[q] = bases[L];
+          const long long items = n * (q + 1) / g.ngrp - n * q / g.ngrp;
+          const long long blocks = ((long long)nblk - q + g.ngrp - 1) / g.ngrp;
+          bases[L] += (unsigned long long)(items + blocks);
+        }
       }
-      for (int q = 0; q < g.ngrp; q++) {
-        const int L = FUSED_GLINE0 + (ln - 8) * 8 + q;
-        g.cbg[q] = bases[L];
-        const long long items = n * (q + 1) / g.ngrp - n * q / g.ngrp;
-        const long long blocks = ((long long)nblk - q + g.ngrp - 1) / g.ngrp;
-        bases[L] += (unsigned long long)(items + blocks);
-      }
-    };
-    if (we > wb) {
-      const dim3 gr((unsigned)std::min<long long>(cus, we - wb)), b(64 * GenShape<64>::WAVES);
-      setup(wb, we, line, gr.x);
-      launch_general<64>(g, um, gr, b, s);
-    }
-    if (ne > nb_) {
-      const dim3 gr((unsigned)std::min<long long>(cus, ne - nb_)), b(64 * GenShape<16>::WAVES);
-      setup(nb_, ne, line + 1, gr.x);
-      launch_general<16>(g, um, gr, b, s);
+      launch_general(g, um, dim3(nblk), dim3(64 * GEN_WAVES), s);
     }
     return hipPeekAtLastError() == hipSuccess ? 0 : 9;
   }
