@@ -2714,6 +2714,20 @@ int step_batch(mnl_fields *F, int nsteps) {
   auto ev_end = [&](int k) {
     if (k >= 0) hipEventRecord(evs[k].b, F->stream);
   };
+  // a phase that starts where phase k ended: its start is k's end event (one
+  // record fewer between two back-to-back kernels)
+  auto ev_next = [&](int k, int cat) -> int {
+    if (!F->profiling || k < 0) return ev_begin(cat);
+    while (F->ev_pool.size() < 2 * (evi + 1)) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return -1;
+      F->ev_pool.push_back(e);
+    }
+    EvPair p{evs[k].b, F->ev_pool[2 * evi + 1], cat};
+    evs.push_back(p);
+    evi++;
+    return (int)evs.size() - 1;
+  };
   auto flush_events = [&]() -> int {
     if (!F->profiling || evs.empty()) return 0;
     HIPCHK(hipStreamSynchronize(F->stream));
@@ -2832,7 +2846,7 @@ int step_batch(mnl_fields *F, int nsteps) {
           kr = k_fused(fa, 0, F->stream, F->ctr_base);
           if (kr) return fused_fail("fused kernel launch failed", kr);
           ev_end(k);
-          k = ev_begin(TM_GEN);
+          k = ev_next(k, TM_GEN);
           kr = k_fused(fa, 1, F->stream, F->ctr_base);
           if (kr) return fused_fail("fused general kernel launch failed", kr);
         }
@@ -2841,17 +2855,20 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       ev_end(k);
       // shell curl B; the PML H update rides along when no B source sits between
+      // (timing events only around phases that launch something: an event record
+      // between two kernels costs a few microseconds of GPU time)
       const bool fuseH = nB == 0 && !F->first_step_mode;
-      k = ev_begin(TM_B);
+      const bool shell_work = sl->n > 0 && sl->start[sl->n] > 0;
+      k = shell_work ? ev_begin(TM_B) : -1;
       if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream, fuseH))
         return fail("curl B launch failed");
       ev_end(k);
       if (nB && k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
       // ---- H
       if (!F->h_first_done && h_lazy_copy(F)) return -1;
-      k = ev_begin(TM_H);
       bool anyH = false;
       for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
+      k = (!fuseH && anyH && shell_work) ? ev_begin(TM_H) : -1;
       if (!fuseH && anyH && k_update_h(*sl, g, f, F->stream)) return fail("update H launch failed");
       ev_end(k);
       if (F->nranks > 1) {
@@ -2861,14 +2878,14 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       // ---- D
       if (!F->u_first_done[1] && u_lazy_copy(F, 1)) return -1;
-      k = ev_begin(TM_DINT);
+      k = !F->fused ? ev_begin(TM_DINT) : -1;
       if (!F->fused && k_curl(T_D, F->interior, nullptr, g, f, F->planD, F->S.courant, F->stream))
         return fail("curl D launch failed");
       ev_end(k);
       // shell curl D; the shell E update rides along when it only reads its own D
       const bool fuseE = !F->nr && !F->upnl && f.npol == 0 && nI == 0 && !F->dsrc_in_shell &&
                          !F->first_step_mode;
-      k = ev_begin(TM_D);
+      k = shell_work ? ev_begin(TM_D) : -1;
       if (k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->stream, fuseE))
         return fail("curl D launch failed");
       ev_end(k);
@@ -2878,10 +2895,12 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       // ---- E (+ Lorentzian P)
       if (!F->e_first_done && e_lazy_copy(F)) return -1;
-      k = ev_begin(TM_E);
       // neighbour reads of D - P (NR, upstream chi) or of W (anisotropic sigma):
       // P after all of E
       bool fuse = !F->nr && !F->upnl && !f.aniso;
+      k = (!F->fused || (!fuseE && shell_work) || (!fuse && f.npol) || f.aniso || f.wall_e)
+              ? ev_begin(TM_E)
+              : -1;
       if (!F->fused && F->nr && F->S.dim == 3) {
         if (nr_interior_e(F, is)) return -1;
       } else if (!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) {
