@@ -2183,24 +2183,51 @@ bool make_fused_boxes(mnl_fields *F) {
         narrow.push_back(tx | (ty << 8) | (ch << 16));
       }
   }
+  // bits 24-26 of an item: the directions along which its footprint (the
+  // positions whose PML tables the kernel reads) meets a PML chunk or any
+  // non-identity coefficient; the kernel picks a body with the others fixed
+  auto pml_dirs = [&](int v, bool nar) -> int {
+    const int tx = v & 255, ty = (v >> 8) & 255, ch = (v >> 16) & 255;
+    const int TXn = nar ? 16 : 64, R = nar ? (FUSED_GN_ROWS + 1) : (FUSED_GW_ROWS + 1);
+    const int y0 = (nar ? a.nyb[ty] : a.gyb[ty]) - 1;
+    const int lo[3] = {a.xb[tx] - 1, y0, a.zb[ch] - 1};
+    const int hi[3] = {a.xb[tx] + TXn, y0 + R, a.zb[ch + 1] + 1};
+    int m = 0;
+    for (int d = 0; d < 3; d++) {
+      if (F->h_flag[d].empty()) continue;
+      for (int j = std::max(lo[d], 0); j <= std::min(hi[d], g.N[d] - 1) && !(m >> d & 1); j++)
+        for (int sft = 0; sft < 2; sft++) {
+          const size_t q = 2 * (size_t)(j + g.off[d]) + sft;
+          if (q >= F->h_flag[d].size()) continue;
+          const double kap = F->h_kap[d][q], sig = F->h_sig[d][q];
+          if (F->h_flag[d][q] || kap - sig != 1.0 || kap + sig != 1.0 || F->h_siginv[d][q] != 1.0)
+            m |= 1 << d;
+        }
+    }
+    return m;
+  };
+  for (int &v : F->gitems) {
+    const int m = pml_dirs(v, false);
+    v |= ((m & ~2) == 0 ? 2 : (m & ~4) == 0 ? 4 : 7) << 24;
+  }
+  for (int &v : narrow) v |= (((pml_dirs(v, true) & ~1) == 0 ? 1 : 7) << 24) | (int)0x80000000u;
   // one launch takes both shapes (bit 31 marks a 16-column tile): chunk-0 items
   // first (the early launch of multi-rank steps), then the rest longest first
   // (most planes), so the shortest items fill the launch's tail
-  for (int &v : narrow) v |= (int)0x80000000u;
   std::vector<int> all;
   all.reserve(F->gitems.size() + narrow.size());
   for (int v : F->gitems)
-    if (((v >> 16) & 0x7fff) == 0) all.push_back(v);
+    if (((v >> 16) & 255) == 0) all.push_back(v);
   for (int v : narrow)
-    if (((v >> 16) & 0x7fff) == 0) all.push_back(v);
+    if (((v >> 16) & 255) == 0) all.push_back(v);
   a.ngen_e = (int)all.size();
   std::vector<int> rest;
   for (int v : F->gitems)
-    if (((v >> 16) & 0x7fff) != 0) rest.push_back(v);
+    if (((v >> 16) & 255) != 0) rest.push_back(v);
   for (int v : narrow)
-    if (((v >> 16) & 0x7fff) != 0) rest.push_back(v);
+    if (((v >> 16) & 255) != 0) rest.push_back(v);
   auto planes = [&](int v) {
-    const int ch = (v >> 16) & 0x7fff;
+    const int ch = (v >> 16) & 255;
     return a.zb[ch + 1] - a.zb[ch];
   };
   std::stable_sort(rest.begin(), rest.end(), [&](int x, int y) { return planes(x) > planes(y); });

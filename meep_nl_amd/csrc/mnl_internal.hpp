@@ -210,6 +210,8 @@ int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int 
 constexpr int FUSED_MAXX = 64, FUSED_MAXY = 160, FUSED_MAXZ = 160;
 constexpr int FUSED_MAXCH = 64;  // longest general chunk (planes)
 constexpr int FUSED_MAXGY = 256, FUSED_MAXNY = 64;
+// general items pack tx, ty, chunk in 8 bits each (mnl_kernels.hip, general_item)
+static_assert(FUSED_MAXZ <= 256 && FUSED_MAXX <= 256 && FUSED_MAXGY <= 256, "item encoding");
 #ifndef MNL_GW_ROWS
 #define MNL_GW_ROWS 10
 #endif

@@ -1230,6 +1230,8 @@ struct ItemGeo {
 struct TabE {
   double kms, si, kps;
 };
+// the table entry outside every PML chunk (kappa = 1, sigma = 0)
+__device__ constexpr TabE kTabId = {1.0, 1.0, 1.0};
 constexpr int TPZ = FUSED_MAXCH + 2;
 
 // curl update with the per-point branch selection of step_curl
@@ -1265,7 +1267,7 @@ struct GAux {  // general body, PML state of plane k (own lanes), loaded masked
 // update_eh, src/update_eh.cpp:67-363, with the W aux of PML chunks
 // represented by its value: W_H == B_old, W_E == chi1inv * D_old, which the
 // reference stores one step earlier).
-template <int UMODE, int TX, int R, int NW, int POL>
+template <int UMODE, int TX, int R, int NW, int POL, int AX>
 __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo &it,
                                               double (*sE)[R + 1][TX + 2],
                                               double (*sB)[R][TX + 1], const double (*sU)[256],
@@ -1397,8 +1399,8 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   const gup uix = (gup)sgpr_ptr(a.uidx);
   auto pu_ = [&](unsigned ui, int c) -> double { return sU[UMODE == 2 ? c : 0][(ui >> (8 * c)) & 255]; };
   // W flags of E comps (PML chunk along own direction, shifted coordinate)
-  const bool wx = sFx[px][1] != 0, wy = sFy[py][1] != 0;
-  const bool hwx = sFx[hpx][1] != 0, hwy = sFy[hpy][1] != 0;
+  const bool wx = ((AX & 1) && sFx[px][1] != 0), wy = ((AX & 2) && sFy[py][1] != 0);
+  const bool hwx = ((AX & 1) && sFx[hpx][1] != 0), hwy = ((AX & 2) && sFy[hpy][1] != 0);
 
   auto load = [&](int k) -> GBatch<UMODE> {
     GBatch<UMODE> q;
@@ -1428,7 +1430,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
       const int kk = zc(k);
       const unsigned oh = hbl + (unsigned)kk * s2;
       const unsigned oz = ownz_of(k);
-      const bool wz = sFz[tpz(k)][1] != 0;
+      const bool wz = ((AX & 4) && sFz[tpz(k)][1] != 0);
       const bool hp = hpxy && pz_in(k);
       const bool i0 = hA && impl(hc0, hownx, howny, oz, (hc0 == 0 ? hwx : hwy) || hp);
       const bool i2 = hA && impl(2, hownx, howny, oz, wz || hp);
@@ -1452,7 +1454,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
     const unsigned o1 = cbl + (unsigned)zc(k + 1) * s2;
     const int pz = tpz(k), pz1 = tpz(k + 1);
     const unsigned oz1 = ownz_of(k + 1);
-    const bool wz1 = sFz[pz1][1] != 0;
+    const bool wz1 = ((AX & 4) && sFz[pz1][1] != 0);
     const bool p1 = pxy && pz_in(k + 1);
     const bool e0 = inA && !impl(0, ownx, owny, oz1, wx || p1),
                e1 = inA && !impl(1, ownx, owny, oz1, wy || p1),
@@ -1461,8 +1463,8 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
     x.es1 = e1 ? ldg(Ev[1], o1) : 0.0;
     x.es2 = e2 ? ldg(Ev[2], o1) : 0.0;
     // f_u of B comp c: PML chunk along cycle(c,2), shifted coordinate
-    const bool fxs = sFx[px][1] != 0, fys = sFy[py][1] != 0, fzs = sFz[pz][1] != 0;
-    const bool fxu = sFx[px][0] != 0, fyu = sFy[py][0] != 0, fzu = sFz[pz][0] != 0;
+    const bool fxs = ((AX & 1) && sFx[px][1] != 0), fys = ((AX & 2) && sFy[py][1] != 0), fzs = ((AX & 4) && sFz[pz][1] != 0);
+    const bool fxu = ((AX & 1) && sFx[px][0] != 0), fyu = ((AX & 2) && sFy[py][0] != 0), fzu = ((AX & 4) && sFz[pz][0] != 0);
     const bool u0 = inA && fzs, u1 = inA && fxs, u2 = inA && fys;
     x.ub0 = u0 ? ldg(sgpr_ptr(a.UBo[0]), ob) : 0.0;
     x.ub1 = u1 ? ldg(sgpr_ptr(a.UBo[1]), ob) : 0.0;
@@ -1491,7 +1493,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
     const int z = zlo;
     const unsigned o = cbl + (unsigned)zc(z) * s2;
     const unsigned oz = ownz_of(z);
-    const bool wz = sFz[tpz(z)][1] != 0;
+    const bool wz = ((AX & 4) && sFz[tpz(z)][1] != 0);
     const bool p0 = pxy && pz_in(z);
     const bool i0 = inA && impl(0, ownx, owny, oz, wx || p0),
                i1 = inA && impl(1, ownx, owny, oz, wy || p0),
@@ -1524,7 +1526,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
       const GBatch<UMODE> c = load(kl);
       const int pz = tpz(kl), pz1 = tpz(kl + 1);
       const unsigned oz = ownz_of(kl), oz1 = ownz_of(kl + 1);
-      const bool wz1 = sFz[pz1][1] != 0;
+      const bool wz1 = ((AX & 4) && sFz[pz1][1] != 0);
       // E_old(k+1) of this lane
       double e1x, e1y, e1z;
       {
@@ -1565,10 +1567,10 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
       }
       __syncthreads();
       // ---- curl B (E_old) with PML branches, then H
-      const TabE tx_s = sTx[px][1], ty_s = sTy[py][1], tz_s = sTz[pz][1];
-      const TabE tx_u = sTx[px][0], ty_u = sTy[py][0], tz_u = sTz[pz][0];
-      const bool fxs = sFx[px][1] != 0, fys = sFy[py][1] != 0, fzs = sFz[pz][1] != 0;
-      const bool fxu = sFx[px][0] != 0, fyu = sFy[py][0] != 0, fzu = sFz[pz][0] != 0;
+      const TabE tx_s = ((AX & 1) ? sTx[px][1] : kTabId), ty_s = ((AX & 2) ? sTy[py][1] : kTabId), tz_s = ((AX & 4) ? sTz[pz][1] : kTabId);
+      const TabE tx_u = ((AX & 1) ? sTx[px][0] : kTabId), ty_u = ((AX & 2) ? sTy[py][0] : kTabId), tz_u = ((AX & 4) ? sTz[pz][0] : kTabId);
+      const bool fxs = ((AX & 1) && sFx[px][1] != 0), fys = ((AX & 2) && sFy[py][1] != 0), fzs = ((AX & 4) && sFz[pz][1] != 0);
+      const bool fxu = ((AX & 1) && sFx[px][0] != 0), fyu = ((AX & 2) && sFy[py][0] != 0), fzu = ((AX & 4) && sFz[pz][0] != 0);
       const double Ez_yp = sE[2][row + 1][col], Ex_yp = sE[0][row + 1][col];
       const double Ey_xp = sE[1][row][col + 1], Ez_xp = sE[2][row][col + 1];
       double ubx, uby, ubz;
@@ -1739,8 +1741,8 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   }
 }
 
-// General tiles: items from the host-built list a.gitems (tx | ty << 8 | ch << 16,
-// bit 31 set for a 16-column tile).  One launch takes both tile shapes, so the
+// General tiles: items from the host-built list a.gitems (tx | ty << 8 | ch << 16 |
+// pml directions << 24, bit 31 set for a 16-column tile).  One launch takes both tile shapes, so the
 // two share one tail:
 // TX = 64: tiles of <= 64 columns x FUSED_GW_ROWS rows (ty indexes a.gyb);
 // TX = 16: the narrow x-face tiles, 16 columns x FUSED_GN_ROWS rows (ty indexes
@@ -1766,10 +1768,10 @@ struct GenLds {  // LDS of one tile shape (the two shapes share it through a uni
   unsigned char sFx[TX + 2][2], sFy[R + 1][2], sFz[TPZ][2];
 };
 
-template <int UMODE, int TX, int POL>
+template <int UMODE, int TX, int POL, int AX>
 __device__ __forceinline__ void general_item(const FusedArgs &a, int item, GenLds<TX> &L,
                                              const double (*sU)[256]) {
-  const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 0x7fff;
+  const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
   const int *yb = TX == 64 ? a.gyb : a.nyb;
   ItemGeo itg;
   itg.x0 = a.xb[tx];
@@ -1778,7 +1780,7 @@ __device__ __forceinline__ void general_item(const FusedArgs &a, int item, GenLd
   itg.y1 = yb[ty + 1] - 1;
   itg.zs = a.zb[ch];
   itg.ze = a.zb[ch + 1];
-  fused_general<UMODE, TX, GenShape<TX>::R, GenShape<TX>::NW, POL>(
+  fused_general<UMODE, TX, GenShape<TX>::R, GenShape<TX>::NW, POL, AX>(
       a, itg, L.sE, L.sB, sU, L.sTx, L.sTy, L.sTz, L.sFx, L.sFy, L.sFz);
 }
 
@@ -1809,10 +1811,21 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
     if (item == -1) break;
-    if (item & (int)0x80000000u)
-      general_item<UMODE, 16, POL>(a, item, L.n, sU);
-    else
-      general_item<UMODE, 64, POL>(a, item, L.w, sU);
+    // bits 24-26: the PML directions of the tile's footprint (host); a body with
+    // the other directions' tables fixed at identity runs fewer instructions
+    const int ax = (item >> 24) & 7;
+    if (item & (int)0x80000000u) {
+      if (ax == 1)
+        general_item<UMODE, 16, POL, 1>(a, item, L.n, sU);
+      else
+        general_item<UMODE, 16, POL, 7>(a, item, L.n, sU);
+    } else if (ax == 2) {
+      general_item<UMODE, 64, POL, 2>(a, item, L.w, sU);
+    } else if (ax == 4) {
+      general_item<UMODE, 64, POL, 4>(a, item, L.w, sU);
+    } else {
+      general_item<UMODE, 64, POL, 7>(a, item, L.w, sU);
+    }
   }
 }
 
