@@ -2036,6 +2036,13 @@ static void split_range(std::vector<int> &b, int lo, int hi_excl, int step, int 
   }
 }
 
+// general tiles read the lean kernel's B_new on their halo (default); MNL_LEAN_HALO=0
+// recomputes it (in-process A/B: read per step)
+static int lean_halo_reads() {
+  const char *e = getenv("MNL_LEAN_HALO");
+  return e && e[0] == '0' ? 0 : 1;
+}
+
 bool make_fused_boxes(mnl_fields *F) {
   const DevGrid &g = F->g;
   Box G, L;
@@ -2211,6 +2218,25 @@ bool make_fused_boxes(mnl_fields *F) {
     v |= ((m & ~2) == 0 ? 2 : (m & ~4) == 0 ? 4 : 7) << 24;
   }
   for (int &v : narrow) v |= (((pml_dirs(v, true) & ~1) == 0 ? 1 : 7) << 24) | (int)0x80000000u;
+  // bits 27 / 28: the item's x-1 halo column (own rows) / y-1 halo row (own columns) lies
+  // in the box the lean kernel stores (lean chunk, lean columns and rows).  When the general
+  // launch follows the lean one (FusedArgs::lean_after) those lanes read B_new (== H_new:
+  // no PML there) instead of recomputing it from the old fields: identical values, fewer
+  // halo lines (profiles/README.md, round 2)
+  if (anylean) {
+    const int lsx0 = a.xb[a.lx0], lsx1 = a.xb[a.lx1 + 1] - 1;
+    const int lsy0 = a.yb[0], lsy1 = a.yb[a.ny] - 1;
+    auto mark = [&](int &v, bool nar) {
+      const int tx = v & 255, ty = (v >> 8) & 255, ch = (v >> 16) & 255;
+      if (!lean_ch(ch)) return;
+      const int *ybv = nar ? a.nyb : a.gyb;
+      const int x0 = a.xb[tx], x1 = a.xb[tx + 1] - 1, y0 = ybv[ty] - 1, y1 = ybv[ty + 1] - 1;
+      if (x0 - 1 >= lsx0 && x0 - 1 <= lsx1 && y0 + 1 >= lsy0 && y1 <= lsy1) v |= 1 << 27;
+      if (y0 >= lsy0 && y0 <= lsy1 && x0 >= lsx0 && x1 <= lsx1) v |= 1 << 28;
+    };
+    for (int &v : F->gitems) mark(v, false);
+    for (int &v : narrow) mark(v, true);
+  }
   // one launch takes both shapes (bit 31 marks a 16-column tile): chunk-0 items
   // first (the early launch of multi-rank steps), then the rest longest first
   // (most planes), so the shortest items fill the launch's tail
@@ -2576,7 +2602,9 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
   if (kr) return fused_fail("fused kernel launch failed", kr);
   ev_end(k);
   k = ev_begin(TM_GEN);
+  fa.lean_after = lean_halo_reads();  // same stream, after the lean launch
   kr = k_fused(fa, 3, F->stream, F->ctr_base);
+  fa.lean_after = 0;
   if (kr) return fused_fail("fused general kernel launch failed", kr);
   ev_end(k);
   const BoxList *sl = &F->fused_shell;
@@ -2874,7 +2902,9 @@ int step_batch(mnl_fields *F, int nsteps) {
           if (kr) return fused_fail("fused kernel launch failed", kr);
           ev_end(k);
           k = ev_next(k, TM_GEN);
+          fa.lean_after = lean_halo_reads();  // same stream, after the lean launch
           kr = k_fused(fa, 1, F->stream, F->ctr_base);
+          fa.lean_after = 0;
           if (kr) return fused_fail("fused general kernel launch failed", kr);
         }
       } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {

@@ -281,6 +281,9 @@ struct FusedArgs {
   unsigned long long cbase;     // counter value at launch start (counters are never reset)
   int ngrp;                     // work queues (1 or 8: one per XCD group, blockIdx % 8)
   int ngrp_gen;                 // the same for the general kernels (k_fused copies it to ngrp)
+  int lean_after;               // general launch follows the lean launch of this step on the
+                                // same stream: halo B_new of lean-stored points is read, not
+                                // recomputed (item bits 27 / 28)
   unsigned long long cbg[8];    // lean queue g: counter line g's value at launch start
   unsigned long long *ctr;      // FUSED_NCTR work-queue counters (128 B apart); see cbase
 };

@@ -1224,6 +1224,7 @@ struct ItemGeo {
   int y0;      // halo row; own rows y0+1 .. y1
   int y1;
   int zs, ze;  // planes [zs, ze)
+  bool lmx, lmy;  // general body: x-1 halo column / y-1 halo row read B_new (lean-stored)
 };
 
 // PML coefficient table entry of one half-coordinate (FusedTab), staged in LDS
@@ -1342,6 +1343,13 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   }
   const int oy = row;
   const int gx = x0 + ox, gy = y0 + oy;
+  // lean-halo lanes: the x-1 column (col 0) / the y-1 row (row 0) of a tile whose halo
+  // the lean kernel has already stored this step.  Nobody reads their E (LDS column 0 /
+  // row 0 of sE feed only their own recompute), and their new B equals the stored B_new
+  // (H == B outside PML), so they load the two components the neighbours read and
+  // nothing else.
+  const bool lmode = ownlike && ((col == 0 && it.lmx) || (w < NW && row == 0 && it.lmy));
+  const bool lmcol = col == 0;  // x-1 column: Hy, Hz read by col 1; y-1 row: Hx, Hz by row 1
   // lanes past the tile's columns x1+1 / rows y1+1 (narrow or short tiles) load nothing
   const bool inA = ownlike && gx >= 0 && gx < a.N[0] && gy >= 0 && gy < a.N[1] &&
                    gx <= it.x1 + 1 && gy <= it.y1 + 1;
@@ -1488,8 +1496,8 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   };
 
   // prologue: E_old(zs-1)
-  double ex, ey, ez;
-  {
+  double ex = 0, ey = 0, ez = 0;
+  if (!lmode) {
     const int z = zlo;
     const unsigned o = cbl + (unsigned)zc(z) * s2;
     const unsigned oz = ownz_of(z);
@@ -1522,8 +1530,21 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   for (int k = zlo; k < ze; k++) {
     {
       const int kl = k;
-      const GAux ax = load_aux(kl);
-      const GBatch<UMODE> c = load(kl);
+      GAux ax = {};
+      GBatch<UMODE> c = {};
+      double nb0 = 0, nb1 = 0, nb2 = 0;  // lean-halo lanes: B_new of plane k
+      if (!lmode) {
+        ax = load_aux(kl);
+        c = load(kl);
+      } else {
+        const unsigned ok = cbl + (unsigned)zc(kl) * s2;
+        if (lmcol) {
+          nb1 = ldg(sgpr_ptr(a.Bn[1]), ok);
+        } else {
+          nb0 = ldg(sgpr_ptr(a.Bn[0]), ok);
+        }
+        nb2 = ldg(sgpr_ptr(a.Bn[2]), ok);
+      }
       const int pz = tpz(kl), pz1 = tpz(kl + 1);
       const unsigned oz = ownz_of(kl), oz1 = ownz_of(kl + 1);
       const bool wz1 = ((AX & 4) && sFz[pz1][1] != 0);
@@ -1582,9 +1603,10 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
       const double Bz = pml_curl(c.b2, ax.ub2, Ey_xp - ey + ex - Ex_yp, C, fys, tx_s.kms, tx_s.si,
                                  ty_s.kms, ty_s.si, &ubz);
       // H_c (update_eh H_stuff): separate where the chunk has PML along c
-      const double Hx = fxu ? ax.ho0 + (tx_u.kps * Bx - tx_u.kms * c.b0) : Bx;
-      const double Hy = fyu ? ax.ho1 + (ty_u.kps * By - ty_u.kms * c.b1) : By;
-      const double Hz = fzu ? ax.ho2 + (tz_u.kps * Bz - tz_u.kms * c.b2) : Bz;
+      double Hx = fxu ? ax.ho0 + (tx_u.kps * Bx - tx_u.kms * c.b0) : Bx;
+      double Hy = fyu ? ax.ho1 + (ty_u.kps * By - ty_u.kms * c.b1) : By;
+      double Hz = fzu ? ax.ho2 + (tz_u.kps * Bz - tz_u.kms * c.b2) : Bz;
+      if (lmode) Hx = nb0, Hy = nb1, Hz = nb2;  // never stored by these lanes
       const bool kin = k >= zs && k < ze;
       const bool sk = stl && kin;
       {
@@ -1780,6 +1802,8 @@ __device__ __forceinline__ void general_item(const FusedArgs &a, int item, GenLd
   itg.y1 = yb[ty + 1] - 1;
   itg.zs = a.zb[ch];
   itg.ze = a.zb[ch + 1];
+  itg.lmx = a.lean_after && (item & (1 << 27));
+  itg.lmy = a.lean_after && (item & (1 << 28));
   fused_general<UMODE, TX, GenShape<TX>::R, GenShape<TX>::NW, POL, AX>(
       a, itg, L.sE, L.sB, sU, L.sTx, L.sTy, L.sTz, L.sFx, L.sFy, L.sFz);
 }

@@ -14,7 +14,7 @@ sys.argv = [sys.argv[0], "--no-cpu"] + extra
 args = bench.parse()
 if args.workload is None:
     args.workload = "vacuum" if args.vacuum else "waveguide"
-gv, s, f = bench.build_fields(args, 0, 1, 0, None)
+gv, s, f = bench.build_fields(args.workload, args.size, 0, 1, 0, None)
 f.step(10)
 res = {v: [] for v in variants}
 for rep in range(4):
