@@ -112,6 +112,29 @@ int mnl_structure_set_nonlinear_mode(mnl_structure *s, int mode);
  * 2 = chi3, 3 = Lorentz sigma of susceptibility #index. */
 int mnl_structure_set_box(mnl_structure *s, int kind, int index, const double box[6],
                           double value);
+/* structure::set_epsilon(material_function &eps, bool use_anisotropic_averaging,
+ * double tol, int maxeval) (src/meep.hpp:841, src/structure.cpp:397-401) ->
+ * structure_chunk::set_chi1inv (src/anisotropic_averaging.cpp:221-298) with the
+ * default material_function::eff_chi1inv_row / normal_vector subpixel averaging
+ * (58-219), for a material function given as geometric objects of isotropic
+ * permittivity (later objects win, `default_eps` elsewhere), computed on HIP
+ * device `device`.  objs: nobj records of MNL_GEO_STRIDE doubles
+ * {kind, eps, cx, cy, cz, p0, p1, p2}: kind 0 = block (p = size, |r - c| <= p/2),
+ * 1 = sphere (p0 = radius), 2 = cylinder (p0 = radius, p1 = height, p2 = axis
+ * 0/1/2).  Coordinates of absent dimensions are 0.  use_averaging = 0 gives
+ * 1/eps at each pixel centre (the reference's maxeval = 0 path).  Replaces every
+ * chi1inv row of the E components (trivial rows dropped). */
+#define MNL_GEO_STRIDE 8
+int mnl_structure_set_epsilon_geometry(mnl_structure *s, int device, int nobj,
+                                       const double *objs, double default_eps,
+                                       int use_averaging, double tol, int maxeval);
+/* Copy chi1inv[comp][dir] (whole cell, canonical layout) to host; returns 1
+ * (nothing copied) when the row is trivial / absent. */
+int mnl_structure_get_chi1inv(mnl_structure *s, int comp, int dir, double *host);
+/* The unit-sphere quadrature of src/sphere-quad.cpp (the reference's generated
+ * sphere-quad.h) for dim 1/2/3: writes {x, y, z, weight} per point if xyzw is
+ * non-null, returns the number of points (2, 12, 50).  Host only. */
+int mnl_sphere_quadrature(int dim, double *xyzw);
 
 /* ---- fields (replaces meep::fields, src/meep.hpp:1731-2330) -------------- */
 

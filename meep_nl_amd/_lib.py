@@ -53,6 +53,10 @@ _SIGS = {
     "mnl_structure_load": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_add_lorentzian": (c_int, [c_void, c_double, c_double, c_int, dptr, dptr, dptr]),
     "mnl_structure_set_box": (c_int, [c_void, c_int, c_int, dptr, c_double]),
+    "mnl_structure_set_epsilon_geometry": (c_int, [c_void, c_int, c_int, dptr, c_double, c_int,
+                                                   c_double, c_int]),
+    "mnl_structure_get_chi1inv": (c_int, [c_void, c_int, c_int, dptr]),
+    "mnl_sphere_quadrature": (c_int, [c_int, dptr]),
     "mnl_structure_set_nonlinear_mode": (c_int, [c_void, c_int]),
     "mnl_fields_create": (c_void, [c_void, c_int]),
     "mnl_fields_create_dist": (c_void, [c_void, c_int, c_int, c_int, ctypes.c_char_p]),

@@ -142,6 +142,27 @@ class Structure:
                 continue
             self.set_chi1inv(c, c % 3, 1.0 / fn(*self.gv.coords(c)))
 
+    def set_epsilon_geometry(self, objects, default_eps=1.0, use_anisotropic_averaging=True,
+                             tol=1e-4, maxeval=100000, device=-1):
+        """structure::set_epsilon(material_function &, use_anisotropic_averaging, tol,
+        maxeval) (src/structure.cpp:397-401; subpixel averaging of
+        src/anisotropic_averaging.cpp:58-298) for a material function made of
+        geometric objects, computed on a HIP device.  objects: rows
+        {kind, eps, cx, cy, cz, p0, p1, p2} (include/meep_nl_amd.h), later rows win."""
+        o = np.ascontiguousarray(np.asarray(objects, dtype=np.float64).reshape(-1, 8))
+        check(lib().mnl_structure_set_epsilon_geometry(
+            self.h, int(device), o.shape[0], ptr(o) if o.shape[0] else None, float(default_eps),
+            int(bool(use_anisotropic_averaging)), float(tol), int(maxeval)))
+
+    def get_chi1inv(self, comp, d):
+        """chi1inv[comp][d] over the whole cell (canonical layout); None if trivial."""
+        out = np.empty(self.gv.shape(), dtype=np.float64)
+        rc = lib().mnl_structure_get_chi1inv(self.h, comp, d, ptr(out))
+        if rc == 1:
+            return None
+        check(rc)
+        return out
+
     def set_chi2(self, comp, arr):
         check(lib().mnl_structure_set_chi2(self.h, comp, ptr(self._arr(arr))))
 

@@ -4249,6 +4249,217 @@ int mnl_structure_set_nonlinear_mode(mnl_structure *s, int mode) {
   return 0;
 }
 
+// ------------------------------------------------------------------ subpixel averaging
+// Quadrature points and weights on the unit sphere for 1-D / 2-D / 3-D, the table
+// the reference generates at build time (src/sphere-quad.cpp -> sphere-quad.h):
+// 1-D {0,0,+-1}, 2-D 12 points on the circle, 3-D the 50-point degree-11 formula
+// (McLaren; Stroud U3:11-1) with octahedral symmetry, each list reordered to
+// maximise every point's distance from the earlier ones (squared distances
+// compared in single precision, as the generator does).
+namespace {
+void sq_sort(int n, double *x, double *y, double *z, double *w) {
+  for (int i = 1; i < n; ++i) {
+    double best = 0, bestsum = 0;
+    int jb = i;
+    for (int j = i; j < n; ++j) {
+      double mn = 1e20, sum = 0;
+      for (int k = 0; k < i; ++k) {
+        const double dx = x[k] - x[j], dy = y[k] - y[j], dz = z[k] - z[j];
+        const double d2 = float(dx * dx + dy * dy + dz * dz);
+        mn = mn < d2 ? mn : d2;
+        sum += d2;
+      }
+      if (mn > best || (mn == best && sum > bestsum)) best = mn, bestsum = sum, jb = j;
+    }
+    std::swap(x[i], x[jb]);
+    std::swap(y[i], y[jb]);
+    std::swap(z[i], z[jb]);
+    std::swap(w[i], w[jb]);
+  }
+}
+// rotate (a, b, c) -> (c, a, b)
+inline void rot3(double &a, double &b, double &c) {
+  const double t = c;
+  c = b;
+  b = a;
+  a = t;
+}
+void sphere_quad50(double *x, double *y, double *z, double *w) {
+  int n = 0;
+  auto put = [&](double a, double b, double c, double wt) {
+    x[n] = a, y[n] = b, z[n] = c, w[n++] = wt;
+  };
+  double a = 1, b = 0, c = 0;  // 6 axis points
+  for (int i = 0; i < 2; ++i) {
+    a = -a;
+    for (int j = 0; j < 3; ++j) rot3(a, b, c), put(a, b, c, 9216 / 725760.0);
+  }
+  a = b = sqrt(0.5), c = 0;  // 12 edge midpoints
+  for (int i = 0; i < 2; ++i) {
+    a = -a;
+    for (int j = 0; j < 2; ++j) {
+      b = -b;
+      for (int k = 0; k < 3; ++k) rot3(a, b, c), put(a, b, c, 16384 / 725760.0);
+    }
+  }
+  a = b = c = sqrt(1.0 / 3.0);  // 8 cube corners
+  for (int i = 0; i < 2; ++i) {
+    a = -a;
+    for (int j = 0; j < 2; ++j) {
+      b = -b;
+      for (int k = 0; k < 2; ++k) c = -c, put(a, b, c, 15309 / 725760.0);
+    }
+  }
+  a = b = sqrt(1.0 / 11.0), c = 3 * a;  // 24 points (1, 1, 3) / sqrt(11)
+  for (int i = 0; i < 2; ++i) {
+    a = -a;
+    for (int j = 0; j < 2; ++j) {
+      b = -b;
+      for (int k = 0; k < 2; ++k) {
+        c = -c;
+        for (int l = 0; l < 3; ++l) rot3(a, b, c), put(a, b, c, 14641 / 725760.0);
+      }
+    }
+  }
+}
+}  // namespace
+
+// q[dim-1][i] = {x, y, z, weight}, nq = {2, 12, 50}
+void sphere_quad_table(double q[3][AVG_MAXQ][4], int nq[3]) {
+  memset(q, 0, sizeof(double) * 3 * AVG_MAXQ * 4);
+  nq[0] = 2, nq[1] = 12, nq[2] = 50;
+  q[0][0][2] = 1, q[0][0][3] = 0.5;
+  q[0][1][2] = -1, q[0][1][3] = 0.5;
+  double x[AVG_MAXQ], y[AVG_MAXQ], z[AVG_MAXQ], w[AVG_MAXQ];
+  const double pi = 3.141592653589793238462643383279502884197;
+  for (int i = 0; i < 12; ++i) {
+    x[i] = cos(2 * i * pi / 12);
+    y[i] = sin(2 * i * pi / 12);
+    z[i] = 0.0;
+    w[i] = 1.0 / 12;
+  }
+  sq_sort(12, x, y, z, w);
+  for (int i = 0; i < 12; ++i) q[1][i][0] = x[i], q[1][i][1] = y[i], q[1][i][2] = z[i], q[1][i][3] = w[i];
+  sphere_quad50(x, y, z, w);
+  sq_sort(50, x, y, z, w);
+  for (int i = 0; i < 50; ++i) q[2][i][0] = x[i], q[2][i][1] = y[i], q[2][i][2] = z[i], q[2][i][3] = w[i];
+}
+
+int mnl_sphere_quadrature(int dim, double *xyzw) {
+  if (dim < 1 || dim > 3) return fail("sphere quadrature: dim must be 1, 2 or 3");
+  double q[3][AVG_MAXQ][4];
+  int nq[3];
+  sphere_quad_table(q, nq);
+  if (xyzw) memcpy(xyzw, q[dim - 1], sizeof(double) * 4 * nq[dim - 1]);
+  return nq[dim - 1];
+}
+
+// structure::set_epsilon(material_function &, use_anisotropic_averaging, tol, maxeval)
+// (src/structure.cpp:397-401 -> structure_chunk::set_chi1inv, src/anisotropic_averaging.cpp:
+// 221-298) for a material function made of geometric objects, evaluated on a GPU.  The
+// per-point values do not depend on the chunking, so the whole cell is computed once;
+// which rows each reference chunk keeps (its trivial test) is decided per chunk when the
+// fields are created, as for arrays set with mnl_structure_set_chi1inv.
+int mnl_structure_set_epsilon_geometry(mnl_structure *s, int device, int nobj, const double *objs,
+                                       double default_eps, int use_averaging, double tol,
+                                       int maxeval) {
+  if (!s || nobj < 0 || (nobj > 0 && !objs)) return fail("set_epsilon_geometry: bad arguments");
+  std::vector<GeoObj> h(nobj);
+  for (int o = 0; o < nobj; o++) {
+    const double *r = objs + MNL_GEO_STRIDE * o;
+    GeoObj &g = h[o];
+    g.kind = (int)r[0];
+    if (g.kind < 0 || g.kind > 2 || r[0] != g.kind) return fail("set_epsilon_geometry: bad object kind");
+    g.eps = r[1];
+    for (int d = 0; d < 3; d++) g.c[d] = r[2 + d], g.p[d] = r[5 + d];
+    if (g.kind == 2 && !(g.p[2] == 0 || g.p[2] == 1 || g.p[2] == 2))
+      return fail("set_epsilon_geometry: cylinder axis must be 0, 1 or 2");
+  }
+  if (device >= 0) HIPCHK(hipSetDevice(device));
+  double q[3][AVG_MAXQ][4];
+  AvgArgs A{};
+  sphere_quad_table(q, A.nq);
+  A.ndir = 0;
+  for (int d = 0; d < 3; d++) {
+    A.has[d] = s->has[d];
+    A.n[d] = s->n[d];
+    A.io[d] = s->io[d];
+    if (s->has[d]) A.dirs[A.ndir++] = d;
+  }
+  A.inva = 1.0 / s->a;
+  A.default_eps = default_eps;
+  A.nobj = nobj;
+  A.maxeval = use_averaging ? maxeval : 0;  // set_chi1inv: !use_anisotropic_averaging -> 0
+  A.tol = tol;
+  A.ntot = (long long)s->ntot;
+  // E components with a field and the rows the chunk allocates (FOR_FT_COMPONENTS with
+  // has_field): 1-D Ex only, with its x row; 2-D and 3-D Ex, Ey, Ez with all three
+  const int ncomp = s->dim == 1 ? 1 : 3;
+  GeoObj *dobj = nullptr;
+  double *dq = nullptr, *dout = nullptr;
+  auto cleanup = [&]() {
+    if (dobj) hipFree(dobj);
+    if (dq) hipFree(dq);
+    if (dout) hipFree(dout);
+  };
+  auto chk = [&](hipError_t e, const char *what) {
+    if (e == hipSuccess) return 0;
+    cleanup();
+    return fail(std::string("set_epsilon_geometry: ") + what + ": " + hipGetErrorString(e));
+  };
+  if (nobj > 0) {
+    if (chk(hipMalloc(&dobj, sizeof(GeoObj) * nobj), "hipMalloc")) return -1;
+    if (chk(hipMemcpy(dobj, h.data(), sizeof(GeoObj) * nobj, hipMemcpyHostToDevice), "copy")) return -1;
+  }
+  if (chk(hipMalloc(&dq, sizeof(q)), "hipMalloc")) return -1;
+  if (chk(hipMemcpy(dq, q, sizeof(q), hipMemcpyHostToDevice), "copy")) return -1;
+  const int nrow = s->dim == 1 ? 1 : 3;
+  if (chk(hipMalloc(&dout, sizeof(double) * s->ntot * nrow), "hipMalloc")) return -1;
+  A.objs = dobj;
+  A.quad = dq;
+  for (int c = 0; c < ncomp; c++) {
+    A.c = c;
+    for (int d = 0; d < 3; d++) A.out[d] = nullptr;
+    for (int d = 0; d < nrow; d++) A.out[d] = dout + s->ntot * d;
+    if (k_avg_chi1inv(A, nullptr)) {
+      cleanup();
+      return fail("set_epsilon_geometry: kernel launch failed");
+    }
+    if (chk(hipDeviceSynchronize(), "kernel")) return -1;
+    for (int d = 0; d < nrow; d++) {
+      auto &dst = s->chi1inv[c][d];
+      dst.resize(s->ntot);
+      if (chk(hipMemcpy(dst.data(), A.out[d], sizeof(double) * s->ntot, hipMemcpyDeviceToHost),
+              "copy back"))
+        return -1;
+    }
+    // the reference deletes trivial off-diagonal rows, and the diagonal when the whole
+    // tensor is trivial (src/anisotropic_averaging.cpp:282-296); done here over the whole
+    // cell, per chunk at field creation
+    bool triv[3];
+    for (int d = 0; d < nrow; d++) {
+      const double tv = d == c ? 1.0 : 0.0;
+      const auto &v = s->chi1inv[c][d];
+      triv[d] = std::all_of(v.begin(), v.end(), [&](double x) { return x == tv; });
+    }
+    for (int d = nrow; d < 3; d++) triv[d] = true;
+    for (int d = 0; d < nrow; d++)
+      if (d != c && triv[d]) std::vector<double>().swap(s->chi1inv[c][d]);
+    if (triv[0] && triv[1] && triv[2] && c < nrow) std::vector<double>().swap(s->chi1inv[c][c]);
+  }
+  cleanup();
+  return 0;
+}
+
+int mnl_structure_get_chi1inv(mnl_structure *s, int comp, int dir, double *host) {
+  if (!s || comp < MNL_EX || comp > MNL_EZ || dir < 0 || dir > 2)
+    return fail("chi1inv: E components only");
+  const auto &v = s->chi1inv[comp][dir];
+  if (v.empty()) return 1;
+  if (host) memcpy(host, v.data(), sizeof(double) * v.size());
+  return 0;
+}
+
 int mnl_structure_set_box(mnl_structure *s, int kind, int index, const double box[6],
                           double value) {
   if (!s || kind < 0 || kind > 3) return fail("bad box kind");

@@ -332,6 +332,30 @@ int k_to_box(double *dst, const double *src, const double *hsep, const DevGrid &
              void *stream);
 // bounding box (local indices per direction, as Pt::j) of the points where any array is nonzero
 int k_nonzero_box(const double *const a[3], const DevGrid &g, int *dev_box6, void *stream);
+// structure::set_epsilon with a geometric material function (subpixel averaging),
+// src/anisotropic_averaging.cpp:58-298: one thread per canonical point of E comp c
+struct GeoObj {
+  int kind;       // 0 block (p = size), 1 sphere (p0 = radius), 2 cylinder (p0 = radius,
+                  // p1 = height, p2 = axis 0/1/2)
+  double eps;     // isotropic permittivity (chi1p1)
+  double c[3], p[3];
+};
+constexpr int AVG_MAXQ = 50;  // quadrature points of the largest (3-D) table
+struct AvgArgs {
+  int ndir, dirs[3];  // present directions in LOOP_OVER_DIRECTIONS order
+  int has[3], n[3], io[3];
+  int c;              // E component (= its direction)
+  double inva, default_eps;
+  int nobj;
+  const GeoObj *objs;
+  const double *quad;  // [3][AVG_MAXQ][4] (x, y, z, weight)
+  int nq[3];
+  int maxeval;         // 0: no averaging (1 / chi1p1 at the pixel centre)
+  double tol;
+  double *out[3];      // rows d = 0..2 over the canonical grid (null: not wanted)
+  long long ntot;
+};
+int k_avg_chi1inv(const AvgArgs &a, void *stream);
 int k_box_fill(double *dst, const DevGrid &g, int comp_type, int comp_dir, const double *pos_lo,
                const double *pos_hi, double value, int invert, double a, const int *io,
                void *stream);

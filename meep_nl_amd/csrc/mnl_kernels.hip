@@ -988,6 +988,193 @@ __global__ void box_fill_kernel(double *dst, DevGrid g, int type, int c, double 
   dst[(long long)i0 + i1 * g.st[1] + i2 * g.st[2]] = invert ? 1.0 / value : value;
 }
 
+// ------------------------------------------------------ subpixel averaging
+// structure_chunk::set_chi1inv with a material_function (src/anisotropic_averaging.cpp:
+// 221-298) over a list of geometric objects of isotropic permittivity (later objects
+// win): per point the rownum'th row of the effective tensor at dV(here) (diagonal
+// entry) and at dV(here - shift1) (off-diagonal entries), material_function::
+// eff_chi1inv_row / normal_vector (58-219), in the reference's operation order.
+__device__ double geo_chi1p1(const AvgArgs &A, const double r[3]) {
+  for (int o = A.nobj - 1; o >= 0; o--) {
+    const GeoObj &g = A.objs[o];
+    const double dx = r[0] - g.c[0], dy = r[1] - g.c[1], dz = r[2] - g.c[2];
+    bool in;
+    if (g.kind == 0) {
+      in = fabs(dx) <= 0.5 * g.p[0] && fabs(dy) <= 0.5 * g.p[1] && fabs(dz) <= 0.5 * g.p[2];
+    } else if (g.kind == 1) {
+      in = dx * dx + dy * dy + dz * dz <= g.p[0] * g.p[0];
+    } else {
+      const int ax = (int)g.p[2];
+      const double da = ax == 0 ? dx : ax == 1 ? dy : dz;
+      const double u = ax == 0 ? dy : dx, v = ax == 2 ? dy : dz;
+      in = fabs(da) <= 0.5 * g.p[1] && u * u + v * v <= g.p[0] * g.p[0];
+    }
+    if (in) return g.eps;
+  }
+  return A.default_eps;
+}
+
+__device__ void eff_chi1inv_row(const AvgArgs &A, const double vmin[3], const double vmax[3],
+                                double row[3]) {
+  const int rownum = A.c;
+  double cen[3] = {0, 0, 0};
+  for (int k = 0; k < A.ndir; k++) {
+    const int d = A.dirs[k];
+    cen[d] = (vmin[d] + vmax[d]) * 0.5;
+  }
+  double meps = 1, minveps = 1;
+  double grad[3] = {0, 0, 0};
+  if (A.maxeval) {
+    // normal_vector: sphere quadrature of diameter R around the centre
+    double R = 0.0;
+    for (int k = 0; k < A.ndir; k++) R = fmax(R, vmax[A.dirs[k]] - vmin[A.dirs[k]]);
+    const int nd = A.ndir, min_iters = 1 << nd;
+    const double *q = A.quad + (nd - 1) * AVG_MAXQ * 4;
+    double prev = 0;
+    bool break_early = true, uniform = false;
+    for (int i = 0; i < A.nq[nd - 1]; ++i) {
+      const double w = q[4 * i + 3];
+      double pt[3] = {0, 0, 0};
+      if (nd == 1) {
+        pt[2] = cen[2] + q[4 * i + 2] * R;
+      } else {
+        for (int k = 0; k < nd; k++) pt[k] = cen[k] + q[4 * i + k] * R;
+      }
+      const double val = geo_chi1p1(A, pt);
+      if (i > 0 && i < min_iters) {
+        if (val != prev) break_early = false;
+        if (i == min_iters - 1 && break_early) {
+          uniform = true;
+          break;
+        }
+      }
+      prev = val;
+      for (int k = 0; k < nd; k++) {
+        const int d = A.dirs[k];
+        grad[d] += (pt[d] - cen[d]) * (w * val);
+      }
+    }
+    double g2 = 0.0;
+    for (int k = 0; k < nd; k++) g2 += grad[A.dirs[k]] * grad[A.dirs[k]];
+    if (!uniform && !(sqrt(g2) < 1e-8)) {
+      double dd[3] = {0, 0, 0};
+      for (int k = 0; k < nd; k++) dd[A.dirs[k]] = vmax[A.dirs[k]] - vmin[A.dirs[k]];
+      int ms = 10, iter = 0;
+      double old_meps = 0, old_minveps = 0;
+      bool trivial = false;
+      for (;;) {
+        const bool go = nd == 3 ? (fabs(meps - old_meps) > A.tol * fabs(old_meps)) &&
+                                      (fabs(minveps - old_minveps) > A.tol * fabs(old_minveps))
+                                : (fabs(meps - old_meps) > A.tol * old_meps) &&
+                                      (fabs(minveps - old_minveps) > A.tol * old_minveps);
+        if (!go) break;
+        old_meps = meps;
+        old_minveps = minveps;
+        meps = minveps = 0;
+        if (nd == 3) {
+          for (int k = 0; k < ms && !trivial; k++)
+            for (int j = 0; j < ms && !trivial; j++)
+              for (int i = 0; i < ms; i++) {
+                const double pt[3] = {vmin[0] + i * dd[0] / ms, vmin[1] + j * dd[1] / ms,
+                                      vmin[2] + k * dd[2] / ms};
+                const double ep = geo_chi1p1(A, pt);
+                if (ep < 0) {
+                  trivial = true;
+                  break;
+                }
+                meps += ep;
+                minveps += 1 / ep;
+              }
+          if (trivial) break;
+          meps /= ms * ms * ms;
+          minveps /= ms * ms * ms;
+          ms *= 2;
+          if (A.maxeval && (iter += ms * ms * ms) >= A.maxeval) break;
+        } else if (nd == 2) {
+          for (int j = 0; j < ms && !trivial; j++)
+            for (int i = 0; i < ms; i++) {
+              const double pt[3] = {vmin[0] + i * dd[0] / ms, vmin[1] + j * dd[1] / ms, 0.0};
+              const double ep = geo_chi1p1(A, pt);
+              if (ep < 0) {
+                trivial = true;
+                break;
+              }
+              meps += ep;
+              minveps += 1 / ep;
+            }
+          if (trivial) break;
+          meps /= ms * ms;
+          minveps /= ms * ms;
+          ms *= 2;
+          if (A.maxeval && (iter += ms * ms) >= A.maxeval) break;
+        } else {
+          bool neg = false;
+          for (int i = 0; i < ms; i++) {
+            const double pt[3] = {0.0, 0.0, vmin[2] + i * dd[2] / ms};
+            const double ep = geo_chi1p1(A, pt);
+            if (ep < 0) {
+              meps = geo_chi1p1(A, cen);
+              minveps = 1 / meps;
+              neg = true;
+              break;
+            }
+            meps += ep;
+            minveps += 1 / ep;
+          }
+          if (neg) break;
+          meps /= ms;
+          minveps /= ms;
+          ms *= 2;
+          if (A.maxeval && (iter += ms * ms) >= A.maxeval) break;
+        }
+      }
+      if (!trivial) {
+        double n[3] = {0, 0, 0};
+        const double nabsinv = 1.0 / sqrt(g2);
+        for (int k = 0; k < nd; k++) n[A.dirs[k]] = grad[A.dirs[k]] * nabsinv;
+        for (int i = 0; i < 3; ++i) row[i] = n[rownum] * n[i] * (minveps - 1 / meps);
+        row[rownum] += 1 / meps;
+        return;
+      }
+    }
+  }
+  row[0] = row[1] = row[2] = 0.0;
+  row[rownum] = 1 / geo_chi1p1(A, cen);
+}
+
+__global__ void avg_chi1inv_kernel(AvgArgs A) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.ntot) return;
+  // canonical index -> point (z fastest, then y, then x)
+  int idx[3] = {0, 0, 0};
+  long long r = i;
+  for (int d = 2; d >= 0; d--)
+    if (A.has[d]) {
+      idx[d] = (int)(r % (A.n[d] + 1));
+      r /= A.n[d] + 1;
+    }
+  const double h = 0.5 * A.inva;  // grid_volume::dV: hinva = 0.5 * inva * diameter (1.0)
+  double vmin[3] = {0, 0, 0}, vmax[3] = {0, 0, 0}, omin[3] = {0, 0, 0}, omax[3] = {0, 0, 0};
+  for (int k = 0; k < A.ndir; k++) {
+    const int d = A.dirs[k];
+    const int here = A.io[d] + 2 * idx[d] + (d == A.c ? 1 : 0);
+    const double hp = here * (0.5 * A.inva), hm = (here - (d == A.c ? 1 : 0)) * (0.5 * A.inva);
+    vmax[d] = hp + h;
+    vmin[d] = hp - h;
+    omax[d] = hm + h;  // here - shift1 (E: shifted back half a pixel along c)
+    omin[d] = hm - h;
+  }
+  double row[3];
+  eff_chi1inv_row(A, vmin, vmax, row);
+  if (A.out[A.c]) A.out[A.c][i] = row[A.c];
+  bool off = false;
+  for (int d = 0; d < 3; d++) off = off || (d != A.c && A.out[d]);
+  if (!off) return;
+  eff_chi1inv_row(A, omin, omax, row);
+  for (int d = 0; d < 3; d++)
+    if (d != A.c && A.out[d]) A.out[d][i] = row[d];
+}
+
 // ----------------------------------------------------------------- launchers
 static dim3 grid_for(const Box &b) {
   int n0 = b.hi[0] - b.lo[0] + 1, n1 = b.hi[1] - b.lo[1] + 1, n2 = b.hi[2] - b.lo[2] + 1;
@@ -2692,6 +2879,12 @@ int k_nonzero_box(const double *const a[3], const DevGrid &g, int *box, void *st
   dim3 grd((g.N[0] + MNL_BX - 1) / MNL_BX, (g.N[1] + MNL_BY - 1) / MNL_BY, g.N[2]);
   nonzero_box_kernel<<<grd, dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(a[0], a[1], a[2], g,
                                                                            box);
+  return rc();
+}
+
+int k_avg_chi1inv(const AvgArgs &a, void *stream) {
+  if (a.ntot <= 0) return 0;
+  avg_chi1inv_kernel<<<(unsigned)((a.ntot + 255) / 256), 256, 0, (hipStream_t)stream>>>(a);
   return rc();
 }
 

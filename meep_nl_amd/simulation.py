@@ -127,6 +127,55 @@ class Block:
         return ((np.abs(x - c.x) <= 0.5 * s.x) & (np.abs(y - c.y) <= 0.5 * s.y) &
                 (np.abs(z - c.z) <= 0.5 * s.z))
 
+    def geo_record(self, eps):
+        """Row of mnl_structure_set_epsilon_geometry (kind 0 = block)."""
+        c, s = self.center, self.size
+        return [0, eps, c.x, c.y, c.z, s.x, s.y, s.z]
+
+
+class Sphere:
+    """meep.Sphere (python/geom.py): |r - center| <= radius."""
+
+    def __init__(self, radius, center=Vector3(), material=Medium(), **kw):
+        self.radius = float(radius)
+        self.center = Vector3(*center)
+        self.material = material
+
+    def contains(self, x, y, z):
+        c = self.center
+        dx, dy, dz = x - c.x, y - c.y, z - c.z
+        return dx * dx + dy * dy + dz * dz <= self.radius * self.radius
+
+    def geo_record(self, eps):
+        c = self.center
+        return [1, eps, c.x, c.y, c.z, self.radius, 0.0, 0.0]
+
+
+class Cylinder:
+    """meep.Cylinder (python/geom.py) with its axis along x, y or z."""
+
+    def __init__(self, radius, height=1e20, axis=Vector3(0, 0, 1), center=Vector3(),
+                 material=Medium(), **kw):
+        self.radius = float(radius)
+        self.height = float(height)
+        self.center = Vector3(*center)
+        self.material = material
+        ax = [abs(v) for v in Vector3(*axis)]
+        if sorted(ax) != [0.0, 0.0, max(ax)] or max(ax) == 0:
+            raise NotImplementedError("only cylinders along x, y or z are supported")
+        self.axis = ax.index(max(ax))
+
+    def contains(self, x, y, z):
+        c = self.center
+        d = [x - c.x, y - c.y, z - c.z]
+        a = d[self.axis]
+        u, v = [d[k] for k in range(3) if k != self.axis]
+        return (np.abs(a) <= 0.5 * self.height) & (u * u + v * v <= self.radius * self.radius)
+
+    def geo_record(self, eps):
+        c = self.center
+        return [2, eps, c.x, c.y, c.z, self.radius, self.height, float(self.axis)]
+
 
 class PML:
     def __init__(self, thickness, direction=ALL, side=ALL, R_asymptotic=1e-15, mean_stretch=1.0):
@@ -606,6 +655,8 @@ class Simulation:
         self.default_material = default_material
         self.Courant = float(Courant)
         self.eps_averaging = eps_averaging
+        self.subpixel_tol = float(kwargs.pop("subpixel_tol", 1e-4))
+        self.subpixel_maxeval = int(kwargs.pop("subpixel_maxeval", 100000))
         if force_complex_fields or k_point or symmetries:
             raise NotImplementedError("complex fields / Bloch k_point / symmetries are out of scope")
         if dimensions is None:
@@ -646,7 +697,7 @@ class Simulation:
         mats = [self.default_material] + [g.material for g in self.geometry]
         return idx + 1, mats
 
-    def _init_structure(self):
+    def _init_structure(self, device=-1):
         gv = self._create_grid_volume()
         s = core.Structure(gv, self.Courant)
         if self.nonlinear_mode != "fork":
@@ -659,11 +710,27 @@ class Simulation:
             s.add_pml(layer.thickness, dirs, sides, layer.R_asymptotic, layer.mean_stretch)
         media = [self.default_material] + [g.material for g in self.geometry]
         uniform = len(self.geometry) == 0
-        if self.eps_averaging and not uniform:
-            warnings.warn("eps_averaging (subpixel smoothing) is not implemented; materials are "
-                          "sampled at the Yee points as with eps_averaging=False", RuntimeWarning)
         need_eps = any(m.epsilon_diag != Vector3(1, 1, 1) or m.epsilon_offdiag != Vector3()
                        for m in media)
+        # subpixel averaging (structure::set_epsilon with anisotropic averaging, the C++
+        # core's material_function algorithm, src/anisotropic_averaging.cpp:58-298) on the
+        # device, for media of isotropic permittivity; Python Meep's libctl averaging
+        # (meepgeom.cpp) is not available, see DESIGN.md
+        iso = all(m.epsilon_diag.x == m.epsilon_diag.y == m.epsilon_diag.z and
+                  m.epsilon_offdiag == Vector3() for m in media)
+        averaged = False
+        if self.eps_averaging and not uniform and need_eps:
+            if iso:
+                s.set_epsilon_geometry([g.geo_record(g.material.epsilon_diag.x)
+                                        for g in self.geometry],
+                                       default_eps=self.default_material.epsilon_diag.x,
+                                       use_anisotropic_averaging=True,
+                                       tol=self.subpixel_tol, maxeval=self.subpixel_maxeval,
+                                       device=device)
+                averaged = True
+            else:
+                warnings.warn("eps_averaging over anisotropic media is not implemented; "
+                              "materials are sampled at the Yee points", RuntimeWarning)
         need_chi2 = any(m.E_chi2 != 0 for m in media)
         need_chi3 = any(m.E_chi3 != 0 for m in media)
         sus_keys = []
@@ -678,7 +745,7 @@ class Simulation:
             which, mats = self._materials_at(gv, c)
             def table(f):
                 return np.array([f(m) for m in mats], dtype=np.float64)[which]
-            if need_eps:
+            if need_eps and not averaged:
                 # chi1inv row of the inverse permittivity tensor of each medium
                 # (Medium.epsilon_diag / epsilon_offdiag = (xy, xz, yz)); the fork only
                 # uses the diagonal value and whether off-diagonal entries are zero.
@@ -735,9 +802,9 @@ class Simulation:
     def init_sim(self):
         if self.fields is not None:
             return
-        if self.structure is None:
-            self._init_structure()
         ctx = _dist_context() if self.parallel is not False else None
+        if self.structure is None:
+            self._init_structure(device=ctx[2] if ctx else -1)
         if ctx:
             rank, world, local, nid = ctx
             self.fields = core.Fields(self.structure, device=local, rank=rank, nranks=world,

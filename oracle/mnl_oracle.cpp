@@ -36,9 +36,12 @@
 //     with synchronize_magnetic_fields (src/energy_and_flux.cpp:54-187,
 //     src/integrate.cpp:46-201), array slices (src/array_slice.cpp:251-601).
 //
+//   * subpixel averaging of epsilon over geometric objects: set_chi1inv with
+//     material_function::eff_chi1inv_row / normal_vector and the sphere
+//     quadrature of src/sphere-quad.cpp (src/anisotropic_averaging.cpp:33-298).
+//
 // Not restated (out of the configs' scope): cylindrical coordinates, Bloch
-// phases / periodic boundaries, symmetries, magnetic materials, subpixel
-// averaging (the structure arrives as per-point chi1inv / sigma arrays).
+// phases / periodic boundaries, symmetries, magnetic materials.
 //
 // Parity is pinned against the reference's own golden values
 // (tests/known_results.cpp:155-169) and the reference outputs recorded in
@@ -51,6 +54,7 @@
 
 #include "mnl_oracle.h"
 
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <cstdint>
@@ -2596,6 +2600,379 @@ int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3
     out[ri] += arr[q];
   }
   (void)m;
+  return 0;
+}
+
+}  // extern "C"
+
+// ======================================================================
+// Subpixel averaging: structure_chunk::set_chi1inv with a material_function
+// (src/anisotropic_averaging.cpp:221-298), material_function::normal_vector and
+// the default eff_chi1inv_row (58-219), sphere quadrature of src/sphere-quad.cpp.
+// The material function is a list of geometric objects with isotropic epsilon
+// (later objects win), the same convention as mnl_structure_set_epsilon_geometry.
+namespace {
+
+struct AVec {  // meep::vec restricted to what the averaging uses
+  int dim;     // 1 (Z only), 2 (X, Y), 3 (X, Y, Z)
+  double t[3] = {0, 0, 0};
+};
+int avg_ndirs(int dim) { return dim; }
+int avg_dir(int dim, int k) { return dim == 1 ? 2 : k; }  // LOOP_OVER_DIRECTIONS order
+
+struct AvgGeo {
+  int nobj;
+  const double *objs;
+  double def;
+  double chi1p1(const AVec &r) const {  // material_function::chi1p1(E_stuff, r)
+    for (int o = nobj - 1; o >= 0; o--) {
+      const double *g = objs + 8 * o;
+      const double dx = r.t[0] - g[2], dy = r.t[1] - g[3], dz = r.t[2] - g[4];
+      bool in;
+      if (g[0] == 0) {
+        in = fabs(dx) <= 0.5 * g[5] && fabs(dy) <= 0.5 * g[6] && fabs(dz) <= 0.5 * g[7];
+      } else if (g[0] == 1) {
+        in = dx * dx + dy * dy + dz * dz <= g[5] * g[5];
+      } else {
+        const int ax = (int)g[7];
+        const double da = ax == 0 ? dx : ax == 1 ? dy : dz;
+        const double u = ax == 0 ? dy : dx, v = ax == 2 ? dy : dz;
+        in = fabs(da) <= 0.5 * g[6] && u * u + v * v <= g[5] * g[5];
+      }
+      if (in) return g[1];
+    }
+    return def;
+  }
+};
+
+// sphere-quad.cpp: spherical_quadrature_points(50), sort_by_distance, main()
+struct SphereQuad {
+  int num[3] = {2, 12, 50};
+  double q[3][50][4];
+  static void shift3(double &x, double &y, double &z) {  // SHIFT3 macro
+    double d = z;
+    z = y;
+    y = x;
+    x = d;
+  }
+  static void sort_by_distance(int n, double x[], double y[], double z[], double w[]) {
+    for (int i = 1; i < n; ++i) {
+      double d2max = 0, d2maxsum = 0;
+      int jmax = i;
+      for (int j = i; j < n; ++j) {
+        double d2min = 1e20, d2sum = 0;
+        for (int k = 0; k < i; ++k) {
+          const double a = x[k] - x[j], b = y[k] - y[j], c = z[k] - z[j];
+          double d2 = float(a * a + b * b + c * c);
+          d2min = d2min < d2 ? d2min : d2;
+          d2sum += d2;
+        }
+        if (d2min > d2max || (d2min == d2max && d2sum > d2maxsum)) {
+          d2max = d2min;
+          d2maxsum = d2sum;
+          jmax = j;
+        }
+      }
+      double t;
+      t = x[i], x[i] = x[jmax], x[jmax] = t;
+      t = y[i], y[i] = y[jmax], y[jmax] = t;
+      t = z[i], z[i] = z[jmax], z[jmax] = t;
+      t = w[i], w[i] = w[jmax], w[jmax] = t;
+    }
+  }
+  SphereQuad() {
+    memset(q, 0, sizeof(q));
+    q[0][0][2] = 1, q[0][0][3] = 0.5, q[0][1][2] = -1, q[0][1][3] = 0.5;
+    double x[50], y[50], z[50], w[50];
+    const double K_PI = 3.141592653589793238462643383279502884197;
+    for (int i = 0; i < 12; ++i) {
+      x[i] = cos(2 * i * K_PI / 12);
+      y[i] = sin(2 * i * K_PI / 12);
+      z[i] = 0.0;
+      w[i] = 1.0 / 12;
+    }
+    sort_by_distance(12, x, y, z, w);
+    for (int i = 0; i < 12; ++i) q[1][i][0] = x[i], q[1][i][1] = y[i], q[1][i][2] = z[i], q[1][i][3] = w[i];
+    int n = 0;
+    double x0 = 1, y0 = 0, z0 = 0, wt = 9216 / 725760.0;
+    for (int i = 0; i < 2; ++i) {
+      x0 = -x0;
+      for (int j = 0; j < 3; ++j) {
+        shift3(x0, y0, z0);
+        x[n] = x0, y[n] = y0, z[n] = z0, w[n++] = wt;
+      }
+    }
+    x0 = y0 = sqrt(0.5), z0 = 0, wt = 16384 / 725760.0;
+    for (int i = 0; i < 2; ++i) {
+      x0 = -x0;
+      for (int j = 0; j < 2; ++j) {
+        y0 = -y0;
+        for (int k = 0; k < 3; ++k) {
+          shift3(x0, y0, z0);
+          x[n] = x0, y[n] = y0, z[n] = z0, w[n++] = wt;
+        }
+      }
+    }
+    x0 = y0 = z0 = sqrt(1.0 / 3.0), wt = 15309 / 725760.0;
+    for (int i = 0; i < 2; ++i) {
+      x0 = -x0;
+      for (int j = 0; j < 2; ++j) {
+        y0 = -y0;
+        for (int k = 0; k < 2; ++k) {
+          z0 = -z0;
+          x[n] = x0, y[n] = y0, z[n] = z0, w[n++] = wt;
+        }
+      }
+    }
+    x0 = y0 = sqrt(1.0 / 11.0), z0 = 3 * x0, wt = 14641 / 725760.0;
+    for (int i = 0; i < 2; ++i) {
+      x0 = -x0;
+      for (int j = 0; j < 2; ++j) {
+        y0 = -y0;
+        for (int k = 0; k < 2; ++k) {
+          z0 = -z0;
+          for (int l = 0; l < 3; ++l) {
+            shift3(x0, y0, z0);
+            x[n] = x0, y[n] = y0, z[n] = z0, w[n++] = wt;
+          }
+        }
+      }
+    }
+    sort_by_distance(50, x, y, z, w);
+    for (int i = 0; i < 50; ++i) q[2][i][0] = x[i], q[2][i][1] = y[i], q[2][i][2] = z[i], q[2][i][3] = w[i];
+  }
+};
+const SphereQuad &sphere_quad() {
+  static const SphereQuad sq;
+  return sq;
+}
+
+struct AVol {  // meep::volume
+  AVec mn, mx;
+  AVec center() const {
+    AVec c{mn.dim};
+    for (int k = 0; k < avg_ndirs(mn.dim); k++) {
+      const int d = avg_dir(mn.dim, k);
+      c.t[d] = (mn.t[d] + mx.t[d]) * 0.5;
+    }
+    return c;
+  }
+  double diameter() const {
+    double diam = 0.0;
+    for (int k = 0; k < avg_ndirs(mn.dim); k++) {
+      const int d = avg_dir(mn.dim, k);
+      diam = std::max(diam, mx.t[d] - mn.t[d]);
+    }
+    return diam;
+  }
+};
+
+AVec sphere_pt(const AVec &cent, double R, int n, double &weight) {  // anisotropic_averaging.cpp:33-56
+  const auto &sq = sphere_quad().q;
+  AVec r = cent;
+  switch (cent.dim) {
+    case 1:
+      weight = sq[0][n][3];
+      r.t[2] = cent.t[2] + sq[0][n][2] * R;
+      break;
+    case 2:
+      weight = sq[1][n][3];
+      r.t[0] = cent.t[0] + sq[1][n][0] * R;
+      r.t[1] = cent.t[1] + sq[1][n][1] * R;
+      break;
+    default:
+      weight = sq[2][n][3];
+      for (int d = 0; d < 3; d++) r.t[d] = cent.t[d] + sq[2][n][d] * R;
+  }
+  return r;
+}
+
+AVec normal_vector(const AvgGeo &m, const AVol &v) {  // anisotropic_averaging.cpp:60-85
+  const int dim = v.mn.dim;
+  AVec gradient{dim};
+  AVec p = v.center();
+  const double R = v.diameter();
+  const int num_dirs = avg_ndirs(dim), min_iters = 1 << num_dirs;
+  double chi1p1_prev = 0;
+  bool break_early = true;
+  for (int i = 0; i < sphere_quad().num[num_dirs - 1]; ++i) {
+    double weight;
+    AVec pt = sphere_pt(p, R, i, weight);
+    const double chi1p1_val = m.chi1p1(pt);
+    if (i > 0 && i < min_iters) {
+      if (chi1p1_val != chi1p1_prev) break_early = false;
+      if (i == min_iters - 1 && break_early) return AVec{dim};
+    }
+    chi1p1_prev = chi1p1_val;
+    for (int k = 0; k < num_dirs; k++) {
+      const int d = avg_dir(dim, k);
+      gradient.t[d] += (pt.t[d] - p.t[d]) * (weight * chi1p1_val);
+    }
+  }
+  return gradient;
+}
+
+double vabs(const AVec &v) {  // abs(vec) = sqrt(v & v)
+  double r = 0.0;
+  for (int k = 0; k < avg_ndirs(v.dim); k++) {
+    const int d = avg_dir(v.dim, k);
+    r += v.t[d] * v.t[d];
+  }
+  return sqrt(r);
+}
+
+// material_function::eff_chi1inv_row (anisotropic_averaging.cpp:91-219), Cartesian
+void eff_chi1inv_row(const AvgGeo &m, int rownum, double row[3], const AVol &v, double tol,
+                     int maxeval) {
+  const int dim = v.mn.dim;
+  if (!maxeval) {
+  trivial:
+    row[0] = row[1] = row[2] = 0.0;
+    row[rownum] = 1 / m.chi1p1(v.center());
+    return;
+  }
+  {
+    AVec gradient = normal_vector(m, v);
+    if (vabs(gradient) < 1e-8) goto trivial;
+    double meps = 1, minveps = 1;
+    AVec d{dim};
+    for (int k = 0; k < avg_ndirs(dim); k++) {
+      const int dd = avg_dir(dim, k);
+      d.t[dd] = v.mx.t[dd] - v.mn.t[dd];
+    }
+    int ms = 10;
+    double old_meps = 0, old_minveps = 0;
+    int iter = 0;
+    AVec pt{dim};
+    switch (dim) {
+      case 3:
+        while ((fabs(meps - old_meps) > tol * fabs(old_meps)) &&
+               (fabs(minveps - old_minveps) > tol * fabs(old_minveps))) {
+          old_meps = meps;
+          old_minveps = minveps;
+          meps = minveps = 0;
+          for (int k = 0; k < ms; k++)
+            for (int j = 0; j < ms; j++)
+              for (int i = 0; i < ms; i++) {
+                pt.t[0] = v.mn.t[0] + i * d.t[0] / ms;
+                pt.t[1] = v.mn.t[1] + j * d.t[1] / ms;
+                pt.t[2] = v.mn.t[2] + k * d.t[2] / ms;
+                double ep = m.chi1p1(pt);
+                if (ep < 0) goto trivial;
+                meps += ep;
+                minveps += 1 / ep;
+              }
+          meps /= ms * ms * ms;
+          minveps /= ms * ms * ms;
+          ms *= 2;
+          if (maxeval && (iter += ms * ms * ms) >= maxeval) goto done;
+        }
+        break;
+      case 2:
+        while ((fabs(meps - old_meps) > tol * old_meps) &&
+               (fabs(minveps - old_minveps) > tol * old_minveps)) {
+          old_meps = meps;
+          old_minveps = minveps;
+          meps = minveps = 0;
+          for (int j = 0; j < ms; j++)
+            for (int i = 0; i < ms; i++) {
+              pt.t[0] = v.mn.t[0] + i * d.t[0] / ms;
+              pt.t[1] = v.mn.t[1] + j * d.t[1] / ms;
+              double ep = m.chi1p1(pt);
+              if (ep < 0) goto trivial;
+              meps += ep;
+              minveps += 1 / ep;
+            }
+          meps /= ms * ms;
+          minveps /= ms * ms;
+          ms *= 2;
+          if (maxeval && (iter += ms * ms) >= maxeval) goto done;
+        }
+        break;
+      case 1:
+        while ((fabs(meps - old_meps) > tol * old_meps) &&
+               (fabs(minveps - old_minveps) > tol * old_minveps)) {
+          old_meps = meps;
+          old_minveps = minveps;
+          meps = minveps = 0;
+          for (int i = 0; i < ms; i++) {
+            pt.t[2] = v.mn.t[2] + i * d.t[2] / ms;
+            double ep = m.chi1p1(pt);
+            if (ep < 0) {
+              meps = m.chi1p1(v.center());
+              minveps = 1 / meps;
+              goto done;
+            }
+            meps += ep;
+            minveps += 1 / ep;
+          }
+          meps /= ms;
+          minveps /= ms;
+          ms *= 2;
+          if (maxeval && (iter += ms * ms) >= maxeval) goto done;
+        }
+        break;
+    }
+  done : {
+    double n[3] = {0, 0, 0};
+    const double nabsinv = 1.0 / vabs(gradient);
+    for (int k = 0; k < avg_ndirs(dim); k++) {
+      const int dd = avg_dir(dim, k);
+      n[dd % 3] = gradient.t[dd] * nabsinv;
+    }
+    for (int i = 0; i < 3; ++i) row[i] = n[rownum] * n[i] * (minveps - 1 / meps);
+    row[rownum] += 1 / meps;
+  }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int orc_sphere_quadrature(int dim, double *xyzw) {
+  if (dim < 1 || dim > 3) return set_err("dim must be 1, 2 or 3");
+  const SphereQuad &sq = sphere_quad();
+  if (xyzw) memcpy(xyzw, sq.q[dim - 1], sizeof(double) * 4 * sq.num[dim - 1]);
+  return sq.num[dim - 1];
+}
+
+// structure_chunk::set_chi1inv(c, medium, use_anisotropic_averaging, tol, maxeval)
+// (anisotropic_averaging.cpp:221-298) for E comp `comp` over the canonical whole-cell
+// grid: out[d] (NULL = not wanted) receives row d: the diagonal from dV(here), the
+// off-diagonal entries from dV(here - shift1), smoothing diameter 1.
+int orc_eps_average(int dim, const int n[3], const int io[3], double a, int comp, int nobj,
+                    const double *objs, double default_eps, int use_averaging, double tol,
+                    int maxeval, double *out0, double *out1, double *out2) {
+  if (dim < 1 || dim > 3 || comp < 0 || comp > 2) return set_err("bad averaging arguments");
+  if (!use_averaging) maxeval = 0;
+  AvgGeo m{nobj, objs, default_eps};
+  bool has[3] = {dim >= 2, dim >= 2, dim != 2};
+  long long ext[3], ntot = 1;
+  for (int d = 0; d < 3; d++) ext[d] = has[d] ? n[d] + 1 : 1, ntot *= ext[d];
+  double *out[3] = {out0, out1, out2};
+  const double inva = 1.0 / a;
+#pragma omp parallel for schedule(dynamic, 256)
+  for (long long i = 0; i < ntot; i++) {
+    long long r = i;
+    int idx[3];
+    for (int d = 2; d >= 0; d--) idx[d] = (int)(r % ext[d]), r /= ext[d];
+    AVol v{AVec{dim}, AVec{dim}}, vo{AVec{dim}, AVec{dim}};
+    const double hinva = 0.5 * inva * 1.0;  // grid_volume::dV(here, diameter = 1)
+    for (int k = 0; k < avg_ndirs(dim); k++) {
+      const int d = avg_dir(dim, k);
+      const int here = io[d] + 2 * idx[d] + (d == comp ? 1 : 0);  // E: Yee-shifted along comp
+      const int hm = here - (d == comp ? 1 : 0);                 // here - shift1
+      const double h = here * (0.5 * inva), ho = hm * (0.5 * inva);
+      v.mx.t[d] = h + hinva, v.mn.t[d] = h - hinva;
+      vo.mx.t[d] = ho + hinva, vo.mn.t[d] = ho - hinva;
+    }
+    double row[3], rowo[3];
+    eff_chi1inv_row(m, comp, row, v, tol, maxeval);
+    eff_chi1inv_row(m, comp, rowo, vo, tol, maxeval);
+    for (int d = 0; d < 3; d++)
+      if (out[d]) out[d][i] = d == comp ? row[d] : rowo[d];
+  }
   return 0;
 }
 

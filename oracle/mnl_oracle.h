@@ -86,6 +86,14 @@ long long orc_dft_size(orc_sim *s, int h);
 int orc_dft_data(orc_sim *s, int h, int which, double *out, long long n);
 int orc_dft_decimation(orc_sim *s, int h);
 
+/* Subpixel averaging (src/anisotropic_averaging.cpp:58-298) over geometric
+ * objects {kind, eps, cx, cy, cz, p0, p1, p2} (see mnl_structure_set_epsilon_geometry):
+ * rows of E comp `comp` over the canonical grid (NULL = skip). */
+int orc_eps_average(int dim, const int n[3], const int io[3], double a, int comp, int nobj,
+                    const double *objs, double default_eps, int use_averaging, double tol,
+                    int maxeval, double *out0, double *out1, double *out2);
+int orc_sphere_quadrature(int dim, double *xyzw);
+
 #ifdef __cplusplus
 }
 #endif

@@ -80,6 +80,9 @@ def lib():
         L.orc_dft_size.argtypes = [c_void, c_int]
         L.orc_dft_data.argtypes = [c_void, c_int, c_int, dptr, ctypes.c_longlong]
         L.orc_dft_decimation.argtypes = [c_void, c_int]
+        L.orc_eps_average.argtypes = [c_int, iptr, iptr, c_double, c_int, c_int, dptr, c_double,
+                                      c_int, c_double, c_int, dptr, dptr, dptr]
+        L.orc_sphere_quadrature.argtypes = [c_int, dptr]
         _LIB = L
     return _LIB
 
@@ -103,6 +106,34 @@ def _dp(a):
 
 def set_threads(n):
     return lib().orc_set_threads(int(n))
+
+
+def sphere_quadrature(dim):
+    """The restated src/sphere-quad.cpp table for dim 1/2/3: (n, 4) array of
+    x, y, z, weight."""
+    n = lib().orc_sphere_quadrature(int(dim), None)
+    out = np.zeros((n, 4))
+    lib().orc_sphere_quadrature(int(dim), _dp(out))
+    return out
+
+
+def eps_average(dim, n, io, a, comp, objs, default_eps=1.0, use_averaging=True, tol=1e-4,
+                maxeval=100000):
+    """structure_chunk::set_chi1inv with subpixel averaging over geometric objects
+    (rows {kind, eps, cx, cy, cz, p0, p1, p2}; src/anisotropic_averaging.cpp:58-298).
+    Returns the three rows of E comp `comp` over the canonical grid (1-D: row 0 only)."""
+    has = [dim >= 2, dim >= 2, dim != 2]
+    shape = tuple(int(n[d]) + 1 for d in range(3) if has[d])
+    o = np.ascontiguousarray(np.asarray(objs, dtype=np.float64).reshape(-1, 8))
+    rows = [np.zeros(shape) for _ in range(3)]
+    if dim == 1:
+        rows[1] = rows[2] = None
+    na = (ctypes.c_int * 3)(*[int(v) for v in n])
+    ia = (ctypes.c_int * 3)(*[int(v) for v in io])
+    _chk(lib().orc_eps_average(int(dim), na, ia, float(a), int(comp), o.shape[0], _dp(o),
+                               float(default_eps), int(bool(use_averaging)), float(tol),
+                               int(maxeval), *[_dp(r) for r in rows]))
+    return rows
 
 
 class Oracle:
@@ -169,6 +200,20 @@ class Oracle:
                 continue
             pts = self.coords(c)
             self.set_chi1inv(c, c % 3, 1.0 / fn(*pts))
+
+    def set_epsilon_geometry(self, objs, default_eps=1.0, use_averaging=True, tol=1e-4,
+                             maxeval=100000):
+        """structure::set_epsilon(material_function &, use_anisotropic_averaging, tol,
+        maxeval) over geometric objects: every E component's rows from eps_average,
+        trivial off-diagonal rows (and all-trivial tensors) dropped."""
+        for c in ((Ex,) if self.dim == 1 else (Ex, Ey, Ez)):
+            rows = eps_average(self.dim, self.n, self.io, self.a, c, objs, default_eps,
+                               use_averaging, tol, maxeval)
+            triv = [r is None or np.all(r == (1.0 if d == c else 0.0)) for d, r in enumerate(rows)]
+            for d, r in enumerate(rows):
+                if r is None or (d != c and triv[d]) or all(triv):
+                    continue
+                self.set_chi1inv(c, d, r)
 
     def set_chi2(self, comp, arr):
         arr = np.ascontiguousarray(arr, dtype=np.float64).ravel()

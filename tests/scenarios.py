@@ -54,6 +54,10 @@ class ProductSim:
     def set_chi2(self, c, arr):
         self.s.set_chi2(c, arr)
 
+    def set_epsilon_geometry(self, objs, default_eps=1.0, use_averaging=True, tol=1e-4,
+                             maxeval=100000):
+        self.s.set_epsilon_geometry(objs, default_eps, use_averaging, tol, maxeval)
+
     def set_chi3(self, c, arr):
         self.s.set_chi3(c, arr)
 
