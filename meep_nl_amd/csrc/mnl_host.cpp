@@ -267,6 +267,11 @@ struct mnl_fields {
   bool any_dsrc_w = false;  // a D current source on a W-form (PML-along-E) point
   unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedG (null: f64 chi1inv)
   double *d_utab = nullptr;    // 3 x 256 palette values
+  unsigned *d_uflag = nullptr;  // per lean item: uniform palette word or ~0u (k_lean_uniform)
+  size_t uflag_n = 0;
+  unsigned long long uflag_sig = 0;  // geometry the flags were built for
+  unsigned *d_gflag = nullptr;  // per general item (k_general_uniform)
+  size_t gflag_n = 0;
   bool allow_fused = true;
   // the reference allocates H (as a copy of B) and the W auxiliary fields (as a
   // copy of E / H) on the first update_eh (src/update_eh.cpp:204-216); the first
@@ -321,6 +326,8 @@ struct mnl_fields {
     if (d_scratch) hipFree(d_scratch);
     if (d_vals) hipFree(d_vals);
     if (d_gitems) hipFree(d_gitems);
+    if (d_uflag) hipFree(d_uflag);
+    if (d_gflag) hipFree(d_gflag);
     comm.reset();
     for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
       if (e) hipEventDestroy(e);
@@ -2542,6 +2549,43 @@ FusedArgs &fused_args(mnl_fields *F) {
   fa.gitems = F->d_gitems;
   fa.uidx = F->d_uidx;
   fa.utab = F->d_utab;
+  fa.uflag = nullptr;
+  fa.gflag = nullptr;
+  const char *ue = getenv("MNL_UNIFORM");  // 0: per-cell palette loads everywhere (A/B)
+  if (F->d_uidx && !(ue && ue[0] == '0')) {
+    // flags of the current tile / chunk geometry (rebuilt if make_fused_boxes changed it)
+    unsigned long long sig = 1469598103934665603ULL;
+    auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
+    for (int i = 0; i <= fa.nx; i++) mix(fa.xb[i]);
+    for (int i = 0; i <= fa.ny; i++) mix(fa.yb[i]);
+    for (int i = 0; i <= fa.nch; i++) mix(fa.zb[i]);
+    for (int k = 0; k < 3; k++) mix(fa.L.lo[k]), mix(fa.L.hi[k]);
+    mix(fa.lx0), mix(fa.lx1), mix(fa.ly0), mix(fa.ly1), mix(fa.nch);
+    for (int i = 0; i <= fa.ngy; i++) mix(fa.gyb[i]);
+    for (int i = 0; i <= fa.nny; i++) mix(fa.nyb[i]);
+    for (int v : F->gitems) mix(v);
+    const long long ntile = (long long)(fa.lx1 - fa.lx0 + 1) * (fa.ly1 - fa.ly0 + 1);
+    const size_t n = ntile > 0 ? (size_t)ntile * fa.nch : 0, ng = F->gitems.size();
+    auto grow = [](unsigned *&p, size_t &cap, size_t want) {
+      if (cap >= want) return true;
+      if (p) hipFree(p);
+      p = nullptr;
+      const bool r = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(unsigned)) == hipSuccess;
+      cap = r ? want : 0;
+      return r;
+    };
+    bool ok = true;
+    if (F->uflag_sig != sig) {
+      ok = grow(F->d_uflag, F->uflag_n, n) && grow(F->d_gflag, F->gflag_n, ng) &&
+           k_lean_uniform(fa, F->d_uflag, F->stream) == 0 &&
+           k_general_uniform(fa, F->d_gflag, F->stream) == 0;
+      F->uflag_sig = ok ? sig : 0;
+    }
+    if (ok) {
+      fa.uflag = n ? F->d_uflag : nullptr;
+      fa.gflag = ng ? F->d_gflag : nullptr;
+    }
+  }
   fa.ctr = F->d_fused_ctr;
   fa.ngrp = 1;  // lean queue groups (MNL_LEAN_GROUPS); general: MNL_GEN_GROUPS
   if (const char *e = getenv("MNL_LEAN_GROUPS")) fa.ngrp = atoi(e) == 8 ? 8 : 1;

@@ -281,6 +281,10 @@ struct FusedArgs {
   unsigned long long cbase;     // counter value at launch start (counters are never reset)
   int ngrp;                     // work queues (1 or 8: one per XCD group, blockIdx % 8)
   int ngrp_gen;                 // the same for the general kernels (k_fused copies it to ngrp)
+  const unsigned *gflag;        // general items (index in gitems): the same (k_general_uniform)
+  const unsigned *uflag;        // lean items (tile * nch + ch): the palette word shared by
+                                // every cell whose chi1inv the item uses, or ~0u (mixed);
+                                // null: none (k_lean_uniform)
   int lean_after;               // general launch follows the lean launch of this step on the
                                 // same stream: halo B_new of lean-stored points is read, not
                                 // recomputed (item bits 27 / 28)
@@ -296,6 +300,11 @@ struct FusedArgs {
 // queue), FUSED_GLINE0 + (line - 8) * 8 + g: general line split per XCD group g
 constexpr int FUSED_GLINE0 = 16, FUSED_NCTR = 48;
 int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bases);
+// per lean item, whether the chi1inv palette word is uniform over the cells it uses
+// (flags: ntile * nch words); the lean kernel then reads one cached word instead of
+// a palette index per cell
+int k_lean_uniform(const FusedArgs &a, unsigned *flags, void *stream);
+int k_general_uniform(const FusedArgs &a, unsigned *flags, void *stream);
 int k_cu_count();
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
                  const Box &F, long long st1, long long st2, int *bad, void *stream);

@@ -1412,6 +1412,7 @@ struct ItemGeo {
   int y1;
   int zs, ze;  // planes [zs, ze)
   bool lmx, lmy;  // general body: x-1 halo column / y-1 halo row read B_new (lean-stored)
+  unsigned uw;    // general body: palette word uniform over the item, or ~0u
 };
 
 // PML coefficient table entry of one half-coordinate (FusedTab), staged in LDS
@@ -1593,6 +1594,12 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   }
   const gup uix = (gup)sgpr_ptr(a.uidx);
   auto pu_ = [&](unsigned ui, int c) -> double { return sU[UMODE == 2 ? c : 0][(ui >> (8 * c)) & 255]; };
+  // palette word uniform over the item: every index load reads one cached word (the
+  // first cell of the footprint in G) instead of one word per cell
+  const bool uni = __builtin_amdgcn_readfirstlane(it.uw) != ~0u;
+  const unsigned ufix = (unsigned)((max(x0 - 1, 0) + (long long)max(y0, 0) * a.st1 +
+                                    (long long)max(zs - 1, 0) * a.st2) * 4);
+  auto uoff = [&](unsigned o8) { return uni ? ufix : (o8 >> 1); };
   // W flags of E comps (PML chunk along own direction, shifted coordinate)
   const bool wx = ((AX & 1) && sFx[px][1] != 0), wy = ((AX & 2) && sFy[py][1] != 0);
   const bool hwx = ((AX & 1) && sFx[hpx][1] != 0), hwy = ((AX & 2) && sFy[hpy][1] != 0);
@@ -1605,7 +1612,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
     q.d1 = ldg(Dv[1], o);
     q.d2 = ldg(Dv[2], o);
     if (UMODE == 2) {
-      q.ui = ldu(uix, o >> 1);
+      q.ui = ldu(uix, uoff(o));
     } else if (HAS_U) {
       q.u0 = ldg(Uv[0], o);
       q.u1 = ldg(Uv[1], o);
@@ -1632,7 +1639,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
       q.h0 = ldg(i0 ? (hc0 ? Dv[1] : Dv[0]) : (hc0 ? Ev[1] : Ev[0]), oh);
       q.h1 = ldg(i2 ? Dv[2] : Ev[2], oh);
       if (UMODE == 2) {
-        q.hui = ldu(uix, oh >> 1);
+        q.hui = ldu(uix, uoff(oh));
       } else if (HAS_U) {
         q.hu0 = ldg(hc0 ? Uv[1] : Uv[0], oh);
         q.hu1 = ldg(Uv[2], oh);
@@ -1697,7 +1704,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
     ey = ldg(i1 ? Dv[1] : Ev[1], o);
     ez = ldg(i2 ? Dv[2] : Ev[2], o);
     if (UMODE == 2) {
-      const unsigned ui = ldu(uix, o >> 1);
+      const unsigned ui = ldu(uix, uoff(o));
       if (i0) ex *= pu_(ui, 0);
       if (i1) ey *= pu_(ui, 1);
       if (i2) ez *= pu_(ui, 2);
@@ -1978,8 +1985,8 @@ struct GenLds {  // LDS of one tile shape (the two shapes share it through a uni
 };
 
 template <int UMODE, int TX, int POL, int AX>
-__device__ __forceinline__ void general_item(const FusedArgs &a, int item, GenLds<TX> &L,
-                                             const double (*sU)[256]) {
+__device__ __forceinline__ void general_item(const FusedArgs &a, int item, unsigned uw,
+                                             GenLds<TX> &L, const double (*sU)[256]) {
   const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
   const int *yb = TX == 64 ? a.gyb : a.nyb;
   ItemGeo itg;
@@ -1991,6 +1998,7 @@ __device__ __forceinline__ void general_item(const FusedArgs &a, int item, GenLd
   itg.ze = a.zb[ch + 1];
   itg.lmx = a.lean_after && (item & (1 << 27));
   itg.lmy = a.lean_after && (item & (1 << 28));
+  itg.uw = uw;
   fused_general<UMODE, TX, GenShape<TX>::R, GenShape<TX>::NW, POL, AX>(
       a, itg, L.sE, L.sB, sU, L.sTx, L.sTy, L.sTz, L.sFx, L.sFy, L.sFz);
 }
@@ -2003,6 +2011,7 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
     GenLds<16> n;
   } L;
   __shared__ int s_item;
+  __shared__ unsigned s_uw;
   if (UMODE == 2)
     for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) sU[i >> 8][i & 255] = a.utab[i];
   // ngrp > 1: the workgroups sharing an XCD (blockIdx % ngrp) take a contiguous
@@ -2018,24 +2027,26 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
     if (threadIdx.x == 0) {
       const unsigned long long v = atomicAdd(ctr, 1ULL) - cb;
       s_item = (long long)v < n ? a.gitems[base + v] : -1;
+      s_uw = ((long long)v < n && UMODE == 2 && a.gflag) ? a.gflag[base + v] : ~0u;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
+    const unsigned uw = s_uw;
     if (item == -1) break;
     // bits 24-26: the PML directions of the tile's footprint (host); a body with
     // the other directions' tables fixed at identity runs fewer instructions
     const int ax = (item >> 24) & 7;
     if (item & (int)0x80000000u) {
       if (ax == 1)
-        general_item<UMODE, 16, POL, 1>(a, item, L.n, sU);
+        general_item<UMODE, 16, POL, 1>(a, item, uw, L.n, sU);
       else
-        general_item<UMODE, 16, POL, 7>(a, item, L.n, sU);
+        general_item<UMODE, 16, POL, 7>(a, item, uw, L.n, sU);
     } else if (ax == 2) {
-      general_item<UMODE, 64, POL, 2>(a, item, L.w, sU);
+      general_item<UMODE, 64, POL, 2>(a, item, uw, L.w, sU);
     } else if (ax == 4) {
-      general_item<UMODE, 64, POL, 4>(a, item, L.w, sU);
+      general_item<UMODE, 64, POL, 4>(a, item, uw, L.w, sU);
     } else {
-      general_item<UMODE, 64, POL, 7>(a, item, L.w, sU);
+      general_item<UMODE, 64, POL, 7>(a, item, uw, L.w, sU);
     }
   }
 }
@@ -2178,6 +2189,14 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
     // per-lane source of E inside L's z range: D (then E = D*u) or stored E
     const gdp pO0 = colF ? Dv[0] : Ev[0], pO1 = colF ? Dv[1] : Ev[1], pO2 = colF ? Dv[2] : Ev[2];
     const gdp pH0 = hF ? hD0 : hE0, pH1 = hF ? hD1 : hE1;
+    // palette word uniform over the item: every index load reads the same cached word
+    // (the first cell of the item's footprint in L) instead of one word per cell
+    const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[(long long)tile * a.nch + ch] : ~0u;
+    const bool uni = __builtin_amdgcn_readfirstlane(uw) != ~0u;
+    const unsigned ufix =
+        (unsigned)((max(x0 - 1, flo0) + (long long)max(y0, flo1) * a.st1 +
+                    (long long)max(zs - 1, flo2) * a.st2) * 4);
+    auto uoff = [&](unsigned o8) { return uni ? ufix : (o8 >> 1); };
 
     auto load = [&](int k) -> FBatch {
       FBatch q;
@@ -2189,7 +2208,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
       q.d1 = ldg(zf ? pO1 : Ev[1], o);
       q.d2 = ldg(zf ? pO2 : Ev[2], o);
       if (UMODE == 2) {
-        q.ui = ldu(uix, o >> 1);
+        q.ui = ldu(uix, uoff(o));
       } else if (HAS_U) {
         q.u0 = ldg(Uv[0], o);
         q.u1 = ldg(Uv[1], o);
@@ -2211,7 +2230,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
         q.h0 = ldg(zk ? pH0 : hE0, oh);
         q.h1 = ldg(zk ? pH1 : hE1, oh);
         if (UMODE == 2) {
-          q.hui = ldu(uix, oh >> 1);
+          q.hui = ldu(uix, uoff(oh));
         } else if (HAS_U) {
           q.hu0 = ldg(hU0, oh);
           q.hu1 = ldg(hU1, oh);
@@ -2230,7 +2249,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
       ey = ldg(f0 ? Dv[1] : Ev[1], o);
       ez = ldg(f0 ? Dv[2] : Ev[2], o);
       if (UMODE == 2) {
-        const unsigned ui = ldu(uix, o >> 1);
+        const unsigned ui = ldu(uix, uoff(o));
         if (f0) {  // palette visible: stored before the item loop's barrier
           ex *= pu(ui, 0);
           ey *= pu(ui, 1);
@@ -2310,6 +2329,61 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
       }
     }
   }
+}
+
+// Per lean item (tile t, chunk ch; grid ntile x nch): the palette word if every cell
+// of the item whose chi1inv the lean body uses -- its footprint (columns x0-1 ..
+// x0+FX, rows y0 .. y0+FR, planes zs-1 .. ze) inside the lean box L -- has the same
+// word, else ~0u (a word never has its top byte set).
+__global__ void lean_uniform_kernel(FusedArgs a, unsigned *flags) {
+  const int t = blockIdx.x, ch = blockIdx.y;
+  const int nlx = a.lx1 - a.lx0 + 1;
+  const int tx = a.lx0 + t % nlx, ty = a.ly0 + t / nlx;
+  const int x0 = max(a.xb[tx] - 1, a.L.lo[0]), x1 = min(a.xb[tx] + FX, a.L.hi[0]);
+  const int y0 = max(a.yb[ty] - 1, a.L.lo[1]), y1 = min(a.yb[ty] - 1 + FR, a.L.hi[1]);
+  const int z0 = max(a.zb[ch] - 1, a.L.lo[2]), z1 = min(a.zb[ch + 1], a.L.hi[2]);
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const long long nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
+  unsigned ref = 0;
+  if (nx > 0 && ny > 0 && nz > 0) {
+    ref = a.uidx[x0 + (long long)y0 * a.st1 + (long long)z0 * a.st2];
+    for (long long i = threadIdx.x; i < nx * ny * nz; i += blockDim.x) {
+      const long long x = x0 + i % nx, y = y0 + (i / nx) % ny, z = z0 + i / (nx * ny);
+      if (a.uidx[x + y * a.st1 + z * a.st2] != ref) bad = 1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) flags[(long long)t * a.nch + ch] = bad ? ~0u : ref;
+}
+
+// The same per general item (index in gitems): footprint columns x0-1 .. x0+TX, rows
+// y0 .. y0+R, planes zs-1 .. ze inside G (chi1inv is only used at owned points of G).
+__global__ void general_uniform_kernel(FusedArgs a, unsigned *flags) {
+  const int idx = blockIdx.x;
+  const int item = a.gitems[idx];
+  const bool nar = item & (int)0x80000000u;
+  const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
+  const int TX = nar ? 16 : 64, R = nar ? GenShape<16>::R : GenShape<64>::R;
+  const int yb = nar ? a.nyb[ty] : a.gyb[ty];
+  const int x0 = max(a.xb[tx] - 1, a.G.lo[0]), x1 = min(a.xb[tx] + TX, a.G.hi[0]);
+  const int y0 = max(yb - 1, a.G.lo[1]), y1 = min(yb - 1 + R, a.G.hi[1]);
+  const int z0 = max(a.zb[ch] - 1, a.G.lo[2]), z1 = min(a.zb[ch + 1], a.G.hi[2]);
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const long long nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
+  unsigned ref = 0;
+  if (nx > 0 && ny > 0 && nz > 0) {
+    ref = a.uidx[x0 + (long long)y0 * a.st1 + (long long)z0 * a.st2];
+    for (long long i = threadIdx.x; i < nx * ny * nz; i += blockDim.x) {
+      const long long x = x0 + i % nx, y = y0 + (i / nx) % ny, z = z0 + i / (nx * ny);
+      if (a.uidx[x + y * a.st1 + z * a.st2] != ref) bad = 1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) flags[idx] = bad ? ~0u : ref;
 }
 
 // chi1inv palette indices over box F: uidx[i] = idx0 | idx1 << 8 | idx2 << 16,
@@ -2394,6 +2468,19 @@ static void launch_general(const FusedArgs &g, int um, dim3 gr, dim3 b, hipStrea
     launch_general_u<1>(g, gr, b, s);
   else
     launch_general_u<0>(g, gr, b, s);
+}
+
+int k_lean_uniform(const FusedArgs &a, unsigned *flags, void *stream) {
+  const int ntile = (a.lx1 - a.lx0 + 1) * (a.ly1 - a.ly0 + 1);
+  if (ntile <= 0 || a.nch <= 0 || !a.uidx) return 0;
+  lean_uniform_kernel<<<dim3(ntile, a.nch), 256, 0, (hipStream_t)stream>>>(a, flags);
+  return rc();
+}
+
+int k_general_uniform(const FusedArgs &a, unsigned *flags, void *stream) {
+  if (a.ngen <= 0 || !a.uidx || !a.gitems) return 0;
+  general_uniform_kernel<<<a.ngen, 256, 0, (hipStream_t)stream>>>(a, flags);
+  return rc();
 }
 
 int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bases) {
