@@ -272,6 +272,10 @@ struct mnl_fields {
   unsigned long long uflag_sig = 0;  // geometry the flags were built for
   unsigned *d_gflag = nullptr;  // per general item (k_general_uniform)
   size_t gflag_n = 0;
+  // cells of lean / general items that still read a palette index per cell (the
+  // algorithmic bytes of bench.py's roofline count 4 B of chi1inv for those only)
+  double lean_cells_nu = -1, gen_cells_nu = -1;
+  bool uflag_active = false;
   bool allow_fused = true;
   // the reference allocates H (as a copy of B) and the W auxiliary fields (as a
   // copy of E / H) on the first update_eh (src/update_eh.cpp:204-216); the first
@@ -2580,12 +2584,42 @@ FusedArgs &fused_args(mnl_fields *F) {
            k_lean_uniform(fa, F->d_uflag, F->stream) == 0 &&
            k_general_uniform(fa, F->d_gflag, F->stream) == 0;
       F->uflag_sig = ok ? sig : 0;
+      if (ok) {  // per-item cell counts of the mixed items (traffic model)
+        std::vector<unsigned> hl(n), hg(ng);
+        ok = (n == 0 || hipMemcpyAsync(hl.data(), F->d_uflag, n * 4, hipMemcpyDeviceToHost,
+                                       F->stream) == hipSuccess) &&
+             (ng == 0 || hipMemcpyAsync(hg.data(), F->d_gflag, ng * 4, hipMemcpyDeviceToHost,
+                                        F->stream) == hipSuccess) &&
+             hipStreamSynchronize(F->stream) == hipSuccess;
+        double ln = 0, gn = 0;
+        const int nlx = fa.lx1 - fa.lx0 + 1;
+        for (size_t i = 0; ok && i < n; i++) {
+          const int t = (int)(i / fa.nch), ch = (int)(i % fa.nch);
+          bool lean = false;
+          for (int r = 0; r < fa.nlzr; r++) lean = lean || (ch >= fa.lzr[r][0] && ch <= fa.lzr[r][1]);
+          if (!lean || hl[i] != ~0u) continue;
+          const int tx = fa.lx0 + t % nlx, ty = fa.ly0 + t / nlx;
+          ln += double(fa.xb[tx + 1] - fa.xb[tx]) * (fa.yb[ty + 1] - fa.yb[ty]) *
+                (fa.zb[ch + 1] - fa.zb[ch]);
+        }
+        for (size_t i = 0; ok && i < ng; i++) {
+          if (hg[i] != ~0u) continue;
+          const int v = F->gitems[i], tx = v & 255, ty = (v >> 8) & 255, ch = (v >> 16) & 255;
+          const int *yb = (v & (int)0x80000000u) ? fa.nyb : fa.gyb;
+          gn += double(fa.xb[tx + 1] - fa.xb[tx]) * (yb[ty + 1] - yb[ty]) *
+                (fa.zb[ch + 1] - fa.zb[ch]);
+        }
+        F->lean_cells_nu = ln;
+        F->gen_cells_nu = gn;
+        if (!ok) F->uflag_sig = 0;
+      }
     }
     if (ok) {
       fa.uflag = n ? F->d_uflag : nullptr;
       fa.gflag = ng ? F->d_gflag : nullptr;
     }
   }
+  F->uflag_active = fa.uflag || fa.gflag;
   fa.ctr = F->d_fused_ctr;
   fa.ngrp = 1;  // lean queue groups (MNL_LEAN_GROUPS); general: MNL_GEN_GROUPS
   if (const char *e = getenv("MNL_LEAN_GROUPS")) fa.ngrp = atoi(e) == 8 ? 8 : 1;
@@ -4846,7 +4880,10 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
   int nu = 0;
   for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
   const double ub = F->d_uidx ? 4.0 : 8.0 * nu;
-  *lean_bytes = double(F->lean_cells) * (96.0 + ub);
+  // with per-item uniform palette words only the mixed items read chi1inv per cell
+  const bool uni = F->d_uidx && F->uflag_active && F->lean_cells_nu >= 0;
+  const double lean_u = uni ? F->lean_cells_nu : double(F->lean_cells);
+  *lean_bytes = double(F->lean_cells) * 96.0 + lean_u * ub;
   double extra = 0;
   // count of local indices j in [lo, hi] of axis e with an optional flag condition
   auto cnt = [&](int e, int lo, int hi, int qshift, bool need_flag) -> double {
@@ -4890,7 +4927,8 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
   }
   double gcells = 1;
   for (int e = 0; e < 3; e++) gcells *= double(F->fusedG.hi[e] - F->fusedG.lo[e] + 1);
-  *gen_bytes = (gcells - double(F->lean_cells)) * (96.0 + ub) + extra;
+  const double gen_u = uni ? F->gen_cells_nu : gcells - double(F->lean_cells);
+  *gen_bytes = (gcells - double(F->lean_cells)) * 96.0 + gen_u * ub + extra;
 }
 
 int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, double *total_ms,

@@ -64,7 +64,7 @@ def test_simulation_sigma_offdiag_structure():
     su = mp.LorentzianSusceptibility(frequency=1.1, gamma=0.05, sigma_diag=(0.5, 0.4, 0.3),
                                      sigma_offdiag=(0.1, 0.2, 0.3))
     assert su.sigma_row(0) == [0.5, 0.1, 0.2] and su.sigma_row(2) == [0.2, 0.3, 0.3]
-    sim = mp.Simulation(cell_size=mp.Vector3(1.2, 1.2, 1.2), resolution=10,
+    sim = mp.Simulation(cell_size=mp.Vector3(1.2, 1.2, 1.2), resolution=10, eps_averaging=False,
                         geometry=[mp.Block(mp.Vector3(0.6, 0.6, 0.6),
                                            material=mp.Medium(epsilon=2.0, E_susceptibilities=[su]))])
     sim._init_structure()

@@ -60,7 +60,7 @@ def test_simulation_medium_conductivity_structure():
     """Medium(D_conductivity / B_conductivity_diag) reaches set_conductivity of the
     D / B components (host-side structure build; no GPU needed)."""
     import meep_nl_amd as mp
-    sim = mp.Simulation(cell_size=mp.Vector3(2, 2), resolution=10,
+    sim = mp.Simulation(cell_size=mp.Vector3(2, 2), resolution=10, eps_averaging=False,
                         geometry=[mp.Block(mp.Vector3(1, mp.inf, mp.inf),
                                            material=mp.Medium(epsilon=2.0, D_conductivity=0.3,
                                                               B_conductivity_diag=(0, 0, 0.2)))])
