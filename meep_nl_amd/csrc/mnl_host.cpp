@@ -2637,6 +2637,7 @@ int fused_fail(const char *what, int kr) {
 // of the step's work (general tile-planes cost ~2.5x a lean cell's bandwidth
 // time per cell), or MNL_GEN_CUS; 0 = run the two kernels one after the other
 int gen_split(const mnl_fields *F) {
+  if (const char *e = getenv("MNL_GEN_CUS_STEP")) return std::max(0, atoi(e));  // A/B per step
   if (F->gen_cus >= 0) return F->gen_cus;
   return 0;
 }
