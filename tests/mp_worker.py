@@ -45,6 +45,8 @@ def run_case(name, make):
         o = S.sc_nr_pml_dispersive(make)
     elif name == "nr_seam":
         o = S.sc_nr_isrc_seam(make)
+    elif name == "averaged_up":
+        o = S.sc_averaged(make, upstream=True)
     elif name == "flux":
         o, hs = S.sc_flux_3d(make, steps=40)
         for k, h in enumerate(hs):

@@ -1048,3 +1048,28 @@ def sc_custom_source_3d(make, steps=50):
                         (0.2, -0.3, -0.1), 0.8, is_integrated=True)
     o.step(steps)
     return o
+
+
+# subpixel-averaged structure (mnl_structure_set_epsilon_geometry): a core along x,
+# a sphere overriding it, cylinders along z and x
+OBJS_3D = [
+    [0, 6.0, 0.0, 0.0, 0.0, 1e20, 0.43, 0.37],           # waveguide core along x
+    [1, 11.0, 0.121, -0.087, 0.053, 0.52, 0.0, 0.0],      # sphere (overrides the core)
+    [2, 2.5, -0.31, 0.27, 0.0, 0.18, 0.9, 2.0],           # cylinder along z
+    [2, 3.5, 0.0, 0.33, -0.29, 0.15, 1.1, 0.0],           # cylinder along x
+]
+
+
+def sc_averaged(make, upstream=False, steps=30):
+    o = vol(make, 3, [3.0, 2.8, 3.2], 10, center_origin=True)
+    o.add_pml(0.6)
+    o.set_epsilon_geometry(OBJS_3D, 1.7)
+    if upstream:
+        o.set_upstream_nl(True)
+        for c in range(3):
+            x, y, z = o.coords(c)
+            o.set_chi3(c, np.where(np.abs(z) < 0.5, 1e-2, 0.0))
+    o.add_gaussian_source(2, 0.3, 3.0, 0.0, 30.0, (0.05, 0.05, 0.05), 1.0)
+    o.add_gaussian_source(0, 0.35, 3.0, 0.0, 30.0, (-0.2, 0.1, -0.3), 0.7)
+    o.step(steps)
+    return o

@@ -10,7 +10,7 @@ import pytest
 
 import oracle.oracle as orc
 import scenarios as S
-from scenarios import GroupSim3, ProductSim, make_oracle
+from scenarios import OBJS_3D, GroupSim3, ProductSim, make_oracle, sc_averaged
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
@@ -45,14 +45,6 @@ def _same(p, o):
                 assert a.tobytes() == b.tobytes(), (c, d, np.max(np.abs(a - b)))
 
 
-OBJS_3D = [
-    [0, 6.0, 0.0, 0.0, 0.0, 1e20, 0.43, 0.37],           # waveguide core along x
-    [1, 11.0, 0.121, -0.087, 0.053, 0.52, 0.0, 0.0],      # sphere (overrides the core)
-    [2, 2.5, -0.31, 0.27, 0.0, 0.18, 0.9, 2.0],           # cylinder along z
-    [2, 3.5, 0.0, 0.33, -0.29, 0.15, 1.1, 0.0],           # cylinder along x
-]
-
-
 @pytest.mark.parametrize("use_avg,maxeval", [(True, 100000), (True, 5000), (False, 100000)])
 def test_rows_3d_bitwise(use_avg, maxeval):
     n, io = [22, 20, 24], [-22, -20, -24]
@@ -70,21 +62,6 @@ def test_rows_2d_and_1d_bitwise():
     objs1 = [[0, 5.0, 0.0, 0.0, 0.0317, 0.0, 0.0, 0.841], [0, 2.0, 0.0, 0.0, 0.4, 0.0, 0.0, 0.233]]
     _same(_product_rows(1, [0, 0, 40], [0, 0, -40], objs1, 1.0),
           _oracle_rows(1, [0, 0, 40], [0, 0, -40], objs1, 1.0))
-
-
-def sc_averaged(make, upstream=False, steps=30):
-    o = S.vol(make, 3, [3.0, 2.8, 3.2], 10, center_origin=True)
-    o.add_pml(0.6)
-    o.set_epsilon_geometry(OBJS_3D, 1.7)
-    if upstream:
-        o.set_upstream_nl(True)
-        for c in range(3):
-            x, y, z = o.coords(c)
-            o.set_chi3(c, np.where(np.abs(z) < 0.5, 1e-2, 0.0))
-    o.add_gaussian_source(2, 0.3, 3.0, 0.0, 30.0, (0.05, 0.05, 0.05), 1.0)
-    o.add_gaussian_source(0, 0.35, 3.0, 0.0, 30.0, (-0.2, 0.1, -0.3), 0.7)
-    o.step(steps)
-    return o
 
 
 @pytest.mark.parametrize("upstream", [False, True])

@@ -23,7 +23,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CASES2 = ["vacuum_pml", "big_box", "kerr_lorentz", "nr_dispersive", "nr_seam", "flux"]
-CASES3 = ["big_box", "flux"]
+CASES3 = ["big_box", "flux", "averaged_up"]
 
 
 def _launch(nranks, cases, out):
@@ -72,6 +72,8 @@ def _oracle(name):
         return S.sc_nr_pml_dispersive(make_oracle), {}
     if name == "nr_seam":
         return S.sc_nr_isrc_seam(make_oracle), {}
+    if name == "averaged_up":
+        return S.sc_averaged(make_oracle, upstream=True), {}
     o, hs = S.sc_flux_3d(make_oracle, steps=40)
     ex = {f"flux{k}": o.flux(h) for k, h in enumerate(hs)}
     ex["slice_plane"] = o.get_array_slice(2, [-1.6, -1.6, 0.3], [1.6, 1.6, 0.3])
