@@ -319,6 +319,8 @@ struct mnl_fields {
   long long timer_count[16] = {0};
   std::vector<hipEvent_t> ev_pool;
   unsigned long long *d_nr_fallbacks = nullptr;
+  NRHard *d_nr_hard = nullptr;      // deferred Newton-Raphson problems (NR runs only)
+  unsigned *d_nr_hard_cnt = nullptr;
   double *d_scratch = nullptr;  // canonical-size staging buffer
   size_t scratch_cap = 0;
   std::vector<std::unique_ptr<DftFluxH>> dfts;  // DFT flux objects (add_dft_flux order)
@@ -2805,6 +2807,23 @@ int nr_interior_e(mnl_fields *F, const ISrcDev &is) {
   return 0;
 }
 
+constexpr int NR_HARD_CAP = 4096;  // deferred NR problems per E update (more: solved in place)
+
+// Before an E update that may run the NR branch: enable deferral (MNL_NR_DEFER=0 solves
+// every problem in place, sequentially) and clear the list; after it, the parallel pass.
+int nr_defer_begin(mnl_fields *F) {
+  if (!F->d_nr_hard) return 0;
+  const char *e = getenv("MNL_NR_DEFER");
+  F->f.nr_hard = (e && e[0] == '0') ? nullptr : F->d_nr_hard;
+  if (F->f.nr_hard) HIPCHK(hipMemsetAsync(F->d_nr_hard_cnt, 0, sizeof(unsigned), F->stream));
+  return 0;
+}
+int nr_defer_end(mnl_fields *F) {
+  if (!F->f.nr_hard) return 0;
+  if (k_nr_hard(F->f, F->stream)) return fail("NR parallel-attempt kernel launch failed");
+  return 0;
+}
+
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
   if (set_fused(F, fused_agreed(F))) return -1;
@@ -3037,6 +3056,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       k = (!F->fused || (!fuseE && shell_work) || (!fuse && f.npol) || f.aniso || f.wall_e)
               ? ev_begin(TM_E)
               : -1;
+      if (nr_defer_begin(F)) return -1;
       if (!F->fused && F->nr && F->S.dim == 3) {
         if (nr_interior_e(F, is)) return -1;
       } else if (!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) {
@@ -3044,6 +3064,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       if (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream))
         return fail("update E launch failed");
+      if (nr_defer_end(F)) return -1;
       if (f.aniso && !f.wall_e && k_aniso_wall(g, f, 0, F->stream))
         return fail("wall W launch failed");
       if (f.aniso && F->nranks > 1 && exchange(F, 4))  // WE_stuff ghosts (step.cpp:111-114)
@@ -3114,6 +3135,11 @@ int finalize_fields(mnl_fields *F) {
   make_shell_list(F);
   if (dev_alloc(F, &F->d_nr_fallbacks, 1)) return -1;
   F->f.nr_fallbacks = F->d_nr_fallbacks;
+  if (F->nr) {  // first attempts that fail are finished in parallel by nr_hard_kernel
+    if (dev_alloc(F, &F->d_nr_hard, NR_HARD_CAP) || dev_alloc(F, &F->d_nr_hard_cnt, 1)) return -1;
+    F->f.nr_hard_cnt = F->d_nr_hard_cnt;
+    F->f.nr_hard_cap = NR_HARD_CAP;
+  }
   make_plans(F);
   return 0;
 }
@@ -4075,9 +4101,11 @@ int initialize_field(mnl_fields *F, int c, const double *host) {
   ISrcDev is{};
   if (t == T_D) {  // update_eh(E_stuff); step_boundaries(E_stuff)
     if (!F->e_first_done && e_lazy_copy(F)) return -1;
+    if (nr_defer_begin(F)) return -1;
     if (k_update_e(F->interior, nullptr, F->g, f, is, 0, false, F->stream) ||
         k_update_e(F->interior, &F->shell_list, F->g, f, is, 0, false, F->stream))
       return fail("update E launch failed");
+    if (nr_defer_end(F)) return -1;
     if (f.wall_e && k_aniso_wall(F->g, f, 1, F->stream)) return fail("wall E launch failed");
     if (F->nranks > 1 && exchange(F, 0)) return fail("E halo exchange failed");
   } else if (t == T_B) {  // update_eh(H_stuff); step_boundaries(H_stuff)

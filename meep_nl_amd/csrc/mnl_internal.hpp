@@ -108,6 +108,11 @@ struct DevFields {
   const uint8_t *offd_zone;
   const uint8_t *zone[3];    // per direction, global half-coordinate q -> zone 0/1/2
   unsigned long long *nr_fallbacks;
+  // Newton-Raphson problems whose first attempt failed, deferred to nr_hard_kernel
+  // (the later attempts run in parallel, one per lane); null: solve in place
+  struct NRHard *nr_hard;
+  unsigned *nr_hard_cnt;
+  int nr_hard_cap;
   // fused mode active: inside box fG, E is implicit (chi1inv * D, not stored)
   // wherever it is owned and not in a PML chunk along its own direction
   int fused;
@@ -343,6 +348,18 @@ int k_to_box(double *dst, const double *src, const double *hsep, const DevGrid &
 int k_nonzero_box(const double *const a[3], const DevGrid &g, int *dev_box6, void *stream);
 // structure::set_epsilon with a geometric material function (subpixel averaging),
 // src/anisotropic_averaging.cpp:58-298: one thread per canonical point of E comp c
+// one deferred chi(2) Newton-Raphson problem (run_nr after a failed first attempt)
+struct NRHard {
+  double p[15];       // NRP p1, p2, p3 (A, B, F, G, H each)
+  double seed[3];     // the first attempt's seeds
+  double fw0[3];      // *fw, *fw_2, *fw_3 on entry (the tolerances)
+  double *En;         // result array; the solution component d goes to En[i]
+  long long i;
+  unsigned long long rng;
+  int d;
+};
+int k_nr_hard(const DevFields &f, void *stream);
+
 struct GeoObj {
   int kind;       // 0 block (p = size), 1 sphere (p0 = radius), 2 cylinder (p0 = radius,
                   // p1 = height, p2 = axis 0/1/2)

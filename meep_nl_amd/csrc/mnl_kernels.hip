@@ -396,9 +396,42 @@ __device__ double nr_random(unsigned long long &st) {
   return exp(1.0 + 90.0 * gg) * (2.0 * u3 - 1.0);
 }
 
+// Seeds of attempt a >= 1 of runNR (the state the sequential loop below reaches):
+// attempts 1-14 scale / negate the seeds (newton_raphson.cpp:266-330), attempts >= 15
+// draw three deterministic random seeds each (rng advanced by 9 draws per attempt).
+__device__ void nr_attempt_seeds(int a, double seed1, double seed2, double seed3,
+                                 unsigned long long rng, double &s1, double &s2, double &s3) {
+  const double M = 1e33;
+  s1 = seed1, s2 = seed2, s3 = seed3;
+  switch (a) {
+    case 1: s1 = seed1 * M; break;
+    case 2: s2 = seed2 * M; break;
+    case 3: s3 = seed3 * M; break;
+    case 4: s1 = -seed1 * M; break;
+    case 5: s2 = -seed2 * M; break;
+    case 6: s3 = -seed3 * M; break;
+    case 7: s1 = seed1 * M, s2 = seed2 * M; break;
+    case 8: s1 = seed1 * M, s3 = seed3 * M; break;
+    case 9: s2 = seed2 * M, s3 = seed3 * M; break;
+    case 10: s1 = -seed1 * M, s2 = -seed2 * M; break;
+    case 11: s1 = -seed1 * M, s3 = -seed3 * M; break;
+    case 12: s2 = -seed2 * M, s3 = -seed3 * M; break;
+    case 13: s1 = seed1 * M, s2 = seed2 * M, s3 = seed3 * M; break;
+    case 14: s1 = -seed1 * M, s2 = -seed2 * M, s3 = -seed3 * M; break;
+    default: {
+      unsigned long long st = rng + 9ull * (unsigned long long)(a - 15) * 0x9E3779B97F4A7C15ull;
+      s1 = nr_random(st);
+      s2 = nr_random(st);
+      s3 = nr_random(st);
+    }
+  }
+}
+
 __device__ void run_nr(double seed1, double seed2, double seed3, double *fw, double *fw_2,
                        double *fw_3, const NRP &p1, const NRP &p2, const NRP &p3,
-                       unsigned long long rng, unsigned long long *fallbacks) {
+                       unsigned long long rng, unsigned long long *fallbacks,
+                       const DevFields *df = nullptr, double *En = nullptr, long long idx = 0,
+                       int dcomp = 0) {
   const double TOL = 1e-8, seedMax = 1e33;
   int max_it = 250;
   double tol1 = fmax(fabs(TOL * (*fw)) * 0.0001, TOL);
@@ -406,7 +439,31 @@ __device__ void run_nr(double seed1, double seed2, double seed3, double *fw, dou
   double tol3 = fmax(fabs(TOL * (*fw_3)) * 0.0001, TOL);
   double s1 = seed1, s2 = seed2, s3 = seed3;
   for (int a = 0; a < 100; ++a) {
+    const double in0 = *fw, in1 = *fw_2, in2 = *fw_3;
     if (nr_solve(s1, s2, s3, p1, p2, p3, fw, fw_2, fw_3, tol1, tol2, tol3, max_it)) return;
+    if (a == 0 && df && df->nr_hard) {
+      // defer the remaining attempts to nr_hard_kernel (run in parallel there); the
+      // caller stores the unchanged *fw of its component, overwritten on success
+      const unsigned slot = atomicAdd(df->nr_hard_cnt, 1u);
+      if (slot < (unsigned)df->nr_hard_cap) {
+        NRHard &h = df->nr_hard[slot];
+        const NRP *pp[3] = {&p1, &p2, &p3};
+        for (int q = 0; q < 3; q++) {
+          h.p[5 * q + 0] = pp[q]->A;
+          h.p[5 * q + 1] = pp[q]->B;
+          h.p[5 * q + 2] = pp[q]->F;
+          h.p[5 * q + 3] = pp[q]->G;
+          h.p[5 * q + 4] = pp[q]->H;
+        }
+        h.seed[0] = seed1, h.seed[1] = seed2, h.seed[2] = seed3;
+        h.fw0[0] = in0, h.fw0[1] = in1, h.fw0[2] = in2;  // unchanged by a failed attempt
+        h.En = En;
+        h.i = idx;
+        h.rng = rng;
+        h.d = dcomp;
+        return;
+      }
+    }
     switch (a) {  // newton_raphson.cpp:266-338
       case 0: s1 = seed1 * seedMax; max_it = 600; break;
       case 1: s1 = seed1; s2 = seed2 * seedMax; break;
@@ -428,6 +485,53 @@ __device__ void run_nr(double seed1, double seed2, double seed3, double *fw, dou
         s2 = nr_random(rng);
         s3 = nr_random(rng);
         break;
+    }
+  }
+}
+
+// The deferred Newton-Raphson problems: one wave per problem, lane t runs attempt
+// base + t (attempts 1..99, the sequential loop's seeds and max_it = 600); the lowest
+// successful attempt is the one the sequential runNR would have returned, so the
+// result is identical.  The fallback counter gets the random attempts the sequential
+// loop would have started (newton_raphson.cpp:331-336).
+__global__ __launch_bounds__(256) void nr_hard_kernel(DevFields f) {
+  const unsigned n = min(*f.nr_hard_cnt, (unsigned)f.nr_hard_cap);
+  const int lane = threadIdx.x & 63;
+  const unsigned wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
+  const double TOL = 1e-8;
+  for (unsigned e = wv; e < n; e += nw) {
+    const NRHard &h = f.nr_hard[e];
+    const NRP p1 = {h.p[0], h.p[1], h.p[2], h.p[3], h.p[4]};
+    const NRP p2 = {h.p[5], h.p[6], h.p[7], h.p[8], h.p[9]};
+    const NRP p3 = {h.p[10], h.p[11], h.p[12], h.p[13], h.p[14]};
+    const double tol1 = fmax(fabs(TOL * h.fw0[0]) * 0.0001, TOL);
+    const double tol2 = fmax(fabs(TOL * h.fw0[1]) * 0.0001, TOL);
+    const double tol3 = fmax(fabs(TOL * h.fw0[2]) * 0.0001, TOL);
+    int found = -1;
+    double rx = 0, ry = 0, rz = 0;
+    for (int base = 1; base < 100 && found < 0; base += 64) {
+      const int a = base + lane;
+      double ox = h.fw0[0], oy = h.fw0[1], oz = h.fw0[2];
+      bool ok = false;
+      if (a < 100) {
+        double s1, s2, s3;
+        nr_attempt_seeds(a, h.seed[0], h.seed[1], h.seed[2], h.rng, s1, s2, s3);
+        ok = nr_solve(s1, s2, s3, p1, p2, p3, &ox, &oy, &oz, tol1, tol2, tol3, 600);
+      }
+      const unsigned long long m = __ballot(ok);
+      if (m) {
+        const int w = __ffsll((long long)m) - 1;
+        found = base + w;
+        rx = __shfl(ox, w);
+        ry = __shfl(oy, w);
+        rz = __shfl(oz, w);
+      }
+    }
+    if (lane == 0) {
+      const unsigned long long fb = found < 0 ? 86ull : (found > 14 ? (unsigned long long)(found - 14) : 0ull);
+      if (fb) atomicAdd(f.nr_fallbacks, fb);
+      if (found >= 0) h.En[h.i] = h.d == 0 ? rx : h.d == 1 ? ry : rz;
     }
   }
 }
@@ -715,19 +819,19 @@ __device__ __forceinline__ void e_point(const DevGrid &g, const DevFields &f, co
               NRP p2 = {gs_2, us_2, 0.0, chi2new, 0.0};
               NRP p3 = {gs_3, us_3, 0.0, 0.0, chi2new};
               run_nr(fv, gs_2 * u[i], gs_3 * u[i], &fv, &dummy1, &dummy2, p1, p2, p3, rng,
-                     f.nr_fallbacks);
+                     f.nr_fallbacks, &f, En, i, d);
             } else if (d == 1) {
               NRP p1 = {gs_3, us_3, chi2new, 0.0, 0.0};
               NRP p2 = {gs, us, 0.0, chi2new, 0.0};
               NRP p3 = {gs_2, us_2, 0.0, 0.0, chi2new};
               run_nr(gs_3 * u[i], fv, gs_2 * u[i], &dummy1, &fv, &dummy2, p1, p2, p3, rng,
-                     f.nr_fallbacks);
+                     f.nr_fallbacks, &f, En, i, d);
             } else {
               NRP p1 = {gs_2, us_2, chi2new, 0.0, 0.0};
               NRP p2 = {gs_3, us_3, 0.0, chi2new, 0.0};
               NRP p3 = {gs, us, 0.0, 0.0, chi2new};
               run_nr(gs_2 * u[i], gs_3 * u[i], fv, &dummy1, &dummy1, &fv, p1, p2, p3, rng,
-                     f.nr_fallbacks);
+                     f.nr_fallbacks, &f, En, i, d);
             }
             En[i] = fv;
             done = true;
@@ -1278,6 +1382,12 @@ int k_update_e(const Box &in, const BoxList *sh, const DevGrid &g, const DevFiel
     if (sh->n == 0 || sh->start[sh->n] == 0) return 0;
     launch_e<true>(in, *sh, g, f, is, step, fuse_pols, (hipStream_t)stream);
   }
+  return rc();
+}
+
+int k_nr_hard(const DevFields &f, void *stream) {
+  if (!f.nr_hard) return 0;
+  nr_hard_kernel<<<64, 256, 0, (hipStream_t)stream>>>(f);
   return rc();
 }
 

@@ -1073,3 +1073,34 @@ def sc_averaged(make, upstream=False, steps=30):
     o.add_gaussian_source(0, 0.35, 3.0, 0.0, 30.0, (-0.2, 0.1, -0.3), 0.7)
     o.step(steps)
     return o
+
+
+def sc_c4_nr(make, steps=25, n=256):
+    """BASELINE configs[3] NR sub-variant at full size (bench.py --workload kerr_nr):
+    Kerr chi3 + Lorentzian slab |z| <= 2 (eps 2.25), chi2 0.5 in the box |x|,|y| <= 3,
+    |z| <= 1.5 with chi1inv off-diagonal 1e-3 strictly inside it (the Newton-Raphson E
+    update), PML(1.0), Ex Gaussian at z = -3 with amplitude 50, fields from zero.  Its
+    strong fields make some voxels' first NR attempts fail (random-seed fallbacks
+    included), which exercises the deferred parallel-attempt pass."""
+    L = n / 10.0
+    o = vol(make, 3, [L, L, L], 10, center_origin=True)
+    o.add_pml(1.0)
+    sig = []
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        slab = np.abs(z) <= 2.0
+        o.set_chi1inv(c, c, np.where(slab, 1 / 2.25, 1.0))
+        o.set_chi3(c, np.where(slab, 1e-2, 0.0))
+        sig.append(np.where(slab, 0.5, 0.0))
+        box = (np.abs(x) <= 3.0) & (np.abs(y) <= 3.0) & (np.abs(z) <= 1.5)
+        o.set_chi2(c, np.where(box, 0.5, 0.0))
+        inner = (np.abs(x) < 3.0) & (np.abs(y) < 3.0) & (np.abs(z) < 1.5)
+        off = np.where(inner, 1e-3, 0.0)
+        for d in range(3):
+            if d != c:
+                o.set_chi1inv(c, d, off)
+        del x, y, z, slab, box, inner, off
+    o.add_lorentzian(1.1, 0.05, sig)
+    o.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -3.0), 50.0)
+    o.step(steps)
+    return o
