@@ -2074,9 +2074,10 @@ bool make_fused_boxes(mnl_fields *F) {
   memset(&a, 0, sizeof(a));
   a.G = G;
   a.L = L;
-  // default 24 planes: measured 3.13 ms/step vs 3.17 (16) and 3.27 (32) at 512^3 (median
-  // over 5-9 processes each, profiles/README.md)
-  const int zc = std::min(F->fused_zchunk > 0 ? F->fused_zchunk : 24, FUSED_MAXCH);
+  // z-chunk: MNL_FUSED_ZCHUNK, else chosen below (after the lean geometry is known) so
+  // that the lean items fill whole rounds of one workgroup per CU; 512^3 gets 24 planes
+  // (measured 3.13 ms/step vs 3.17 (16) and 3.27 (32), profiles/README.md)
+  int zc = std::min(F->fused_zchunk > 0 ? F->fused_zchunk : 24, FUSED_MAXCH);
   // ---- x tiles (<= 64 columns, starts on 16-double = 128-byte boundaries).  Lean
   // tiles store columns [lx_first, x_end]: footprint x0-1 .. x1+1 inside L (the
   // lanes past x1 load but only feed values that are never stored).
@@ -2106,6 +2107,26 @@ bool make_fused_boxes(mnl_fields *F) {
     }
   }
   const bool anylean = x_end >= lx_first && y_end >= ly_first && !lean_seg.empty();
+  if (anylean && F->fused_zchunk <= 0) {
+    // score = (items / whole rounds of items) x (planes / (planes + the halo plane))
+    std::vector<int> tx;
+    split_range(tx, lx_first, x_end + 1, FX_HOST, 16);
+    const long long ntile = (long long)tx.size() * ((y_end - ly_first + 14) / 14);
+    const long long cus = std::max(1, k_cu_count());
+    double best = -1;
+    for (int cand : {12, 14, 16, 18, 20, 22, 24, 28, 32}) {
+      long long nch = 0, planes = 0;
+      for (auto &sg : lean_seg) {
+        nch += (sg.second - sg.first + cand - 1) / cand;
+        planes += sg.second - sg.first;
+      }
+      const long long items = ntile * nch;
+      const double fill = double(items) / double(((items + cus - 1) / cus) * cus);
+      const double per = double(planes) / double(nch);
+      const double score = fill * per / (per + 1.0);
+      if (score >= best - 1e-12) best = score, zc = cand;  // ties: the longer chunk
+    }
+  }
   std::vector<int> yb, gyb, zb;
   const int gstep = FUSED_GW_ROWS;  // general wide-tile rows
   int gly0 = -1, gly1 = -2;  // general row tiles inside the lean row range
