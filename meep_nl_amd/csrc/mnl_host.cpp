@@ -225,6 +225,7 @@ struct mnl_fields {
   // chi(2) Newton-Raphson runs only where chi2 != 0: the interior E update splits
   // into the bounding box of those points (NR kernel) and the rest (plain kernel)
   bool nr_split_done = false;
+  bool nr_shell_free = false;  // the chi2 box lies inside the interior: plain shell E kernels
   Box nr_in{};
   std::vector<Box> nr_rest;
   std::vector<Box> shell;
@@ -2790,10 +2791,13 @@ int nr_interior_e(mnl_fields *F, const ISrcDev &is) {
     const Box &I = F->interior;
     Box n;
     bool empty = false;
+    F->nr_shell_free = true;  // chi2 != 0 nowhere outside the interior box
     for (int k = 0; k < 3; k++) {  // 3-D: device axis k == direction k
       n.lo[k] = std::max(box[k], I.lo[k]);
       n.hi[k] = std::min(box[3 + k], I.hi[k]);
       empty = empty || n.hi[k] < n.lo[k];
+      if (box[3 + k] >= box[k] && (box[k] < I.lo[k] || box[3 + k] > I.hi[k]))
+        F->nr_shell_free = false;
     }
     F->nr_rest.clear();
     if (empty) {
@@ -3083,8 +3087,14 @@ int step_batch(mnl_fields *F, int nsteps) {
       } else if (!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) {
         return fail("update E launch failed");
       }
-      if (!fuseE && k_update_e(F->interior, sl, g, f, is, 0, fuse, F->stream))
-        return fail("update E launch failed");
+      if (!fuseE) {
+        // no chi2 outside the interior: the shell boxes never take the NR branch, so
+        // they run the plain E kernel (same values, without the NR kernel's registers)
+        DevFields plain = f;
+        if (F->nr && F->nr_split_done && F->nr_shell_free) plain.nr_enabled = 0;
+        if (k_update_e(F->interior, sl, g, plain, is, 0, fuse, F->stream))
+          return fail("update E launch failed");
+      }
       if (nr_defer_end(F)) return -1;
       if (f.aniso && !f.wall_e && k_aniso_wall(g, f, 0, F->stream))
         return fail("wall W launch failed");
