@@ -1412,9 +1412,19 @@ int k_update_pols(const Box &in, const BoxList *sh, const DevGrid &g, const DevF
 }
 
 int k_aniso_wall(const DevGrid &g, const DevFields &f, int zero, void *stream) {
-  Box all;
-  for (int a = 0; a < 3; a++) all.lo[a] = 0, all.hi[a] = g.N[a] - 1;
-  aniso_wall_kernel<<<grid_for(all), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(all, g, f, zero);
+  // wall points (on_wall) lie on the high wall plane of some direction: one launch per
+  // such plane this rank holds (an edge point done twice writes the same value)
+  for (int d = 0; d < 3; d++) {
+    const int a = g.ax[d];
+    if (a < 0 || !g.wall[d]) continue;
+    const int j = g.nglob[d] - g.off[d];
+    if (j < 0 || j > g.N[a] - 1) continue;
+    Box pl;
+    for (int e = 0; e < 3; e++) pl.lo[e] = 0, pl.hi[e] = g.N[e] - 1;
+    pl.lo[a] = pl.hi[a] = j;
+    aniso_wall_kernel<<<grid_for(pl), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(pl, g, f,
+                                                                                     zero);
+  }
   return rc();
 }
 
