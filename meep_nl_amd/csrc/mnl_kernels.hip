@@ -1397,10 +1397,23 @@ int k_update_pols(const Box &in, const BoxList *sh, const DevGrid &g, const DevF
   BoxList none{};
   if (!sh) {
     if (empty(in)) return 0;
-    if (f.aniso)
+    if (f.aniso) {
       update_pols_aniso_kernel<false><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(in, none, g, f);
-    else
-      update_pols_kernel<false><<<grid_for(in), dim3(MNL_BX, MNL_BY), 0, s>>>(in, none, g, f);
+    } else {
+      // isotropic P changes only inside its susceptibility's nonzero box: launch over
+      // the interior's intersection with their union
+      Box u = in;  // device axes; the nz boxes are indexed by direction (Pt::j)
+      for (int d = 0; d < 3; d++) {
+        const int a = g.ax[d];
+        if (a < 0) continue;
+        int lo = INT32_MAX, hi = -1;
+        for (int k = 0; k < f.npol; k++) lo = min(lo, f.pol[k].nz.lo[d]), hi = max(hi, f.pol[k].nz.hi[d]);
+        u.lo[a] = max(lo, in.lo[a]);
+        u.hi[a] = min(hi, in.hi[a]);
+      }
+      if (empty(u)) return 0;
+      update_pols_kernel<false><<<grid_for(u), dim3(MNL_BX, MNL_BY), 0, s>>>(u, none, g, f);
+    }
   } else {
     if (sh->n == 0 || sh->start[sh->n] == 0) return 0;
     if (f.aniso)
