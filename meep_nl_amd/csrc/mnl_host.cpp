@@ -4513,7 +4513,15 @@ int mnl_structure_set_epsilon_geometry(mnl_structure *s, int device, int nobj, c
     if (g.kind == 2 && !(g.p[2] == 0 || g.p[2] == 1 || g.p[2] == 2))
       return fail("set_epsilon_geometry: cylinder axis must be 0, 1 or 2");
   }
+  int prev_dev = -1;
+  HIPCHK(hipGetDevice(&prev_dev));
   if (device >= 0) HIPCHK(hipSetDevice(device));
+  struct RestoreDev {  // leave the caller's current device as it was
+    int d;
+    ~RestoreDev() {
+      if (d >= 0) (void)hipSetDevice(d);
+    }
+  } restore{prev_dev};
   double q[3][AVG_MAXQ][4];
   AvgArgs A{};
   sphere_quad_table(q, A.nq);
