@@ -187,3 +187,27 @@ def test_oracle_set_epsilon_geometry_drops_trivial_rows():
     # runs a step without complaint (rows accepted per chunk)
     o.add_gaussian_source(2, 0.3, 3.0, 0.0, 20.0, (0.0, 0.0, 0.0), 1.0)
     o.step(5)
+
+
+def test_simulation_objects_match_geometry_records():
+    """Simulation's Block / Sphere / Cylinder (used for non-averaged properties) and
+    their mnl_structure_set_epsilon_geometry records (used for averaged epsilon)
+    describe the same regions: without averaging the rows are 1/eps at the pixel
+    centres, which is what the objects' contains() gives at the Yee points."""
+    import meep_nl_amd as mp
+    geom = [mp.Block(size=mp.Vector3(1e20, 0.43, 0.37), material=mp.Medium(epsilon=6.0)),
+            mp.Sphere(0.52, center=mp.Vector3(0.121, -0.087, 0.053), material=mp.Medium(epsilon=9.0)),
+            mp.Cylinder(0.18, height=0.9, axis=mp.Vector3(0, 0, 1),
+                        center=mp.Vector3(-0.31, 0.27, 0.013), material=mp.Medium(epsilon=2.5)),
+            mp.Cylinder(0.15, height=1.1, axis=mp.Vector3(1, 0, 0),
+                        center=mp.Vector3(0.017, 0.33, -0.29), material=mp.Medium(epsilon=3.5))]
+    objs = [g.geo_record(g.material.epsilon_diag.x) for g in geom]
+    n, io = [22, 20, 24], [-22, -20, -24]
+    o = orc.Oracle(3, n, 10.0, io=io)
+    for c in range(3):
+        rows = orc.eps_average(3, n, io, 10.0, c, objs, 1.7, use_averaging=False)
+        x, y, z = o.coords(c)
+        eps = np.full(x.shape, 1.7)
+        for g in geom:
+            eps = np.where(g.contains(x, y, z), g.material.epsilon_diag.x, eps)
+        assert np.array_equal(rows[c], 1.0 / eps), c
