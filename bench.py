@@ -15,6 +15,10 @@ At N=1 the same JSON line also carries the other single-GPU BASELINE configs,
 measured in the same run ("configs"): C2 256^3 vacuum + PML, C4 256^3 Kerr +
 Lorentzian slab, and C4's chi(2) Newton-Raphson sub-variant (NR solves/s).
 
+BASELINE configs[4] (C5: 1024x512x512 cells z-slab-decomposed over 8 GPUs) is
+--workload c5: vacuum + PML(1.0), 512 x 512 x 128 cells per GPU, global
+512 x 512 x (128*N) (the long axis is the slab axis z).
+
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size S] [--vacuum]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
@@ -41,6 +45,8 @@ WORKLOADS = {
     "kerr": "C4 3-D Kerr chi3 + Lorentzian slab |z|<2 + PML(1.0), Ex source at z=-3 amp 50",
     "kerr_nr": "C4-NR: C4 + chi2 0.5 and chi1inv off-diagonal 1e-3 in the box |x|,|y|<3, "
                "|z|<1.5 (Newton-Raphson E update)",
+    "c5": "C5 3-D vacuum + PML(1.0), z-slab decomposed, per GPU S x S x S/4 cells "
+          "(S=512: 512x512x128 per GPU, 512x512x1024 = the 1024x512x512 domain at N=8)",
 }
 NR_BOX = (-3.0, 3.0, -3.0, 3.0, -1.5, 1.5)
 
@@ -71,7 +77,7 @@ def build_fields(workload, size, rank, world, device, nid):
     size x size x size*world, center_origin, res 10, Courant 0.5)."""
     from meep_nl_amd import core
     import numpy as np
-    n = [size, size, size * world]
+    n = [size, size, (size // 4 if workload == "c5" else size) * world]
     io = [-(v - (v & 1)) for v in n]  # center_origin()
     gv = core.GridVolume(3, n, 10.0, io)
     s = core.Structure(gv, 0.5)
@@ -253,7 +259,7 @@ def launch_ranks(args):
 
 def main():
     args = parse()
-    if args.workload == "vacuum":
+    if args.workload in ("vacuum", "c5"):
         args.vacuum = True
     if args.workload is None:
         args.workload = "vacuum" if args.vacuum else "waveguide"
@@ -308,7 +314,11 @@ def main():
     total_cells = float(gv.n[0]) * gv.n[1] * gv.n[2]
     value = total_cells * args.steps / el / 1e6
     roof = roofline(f)
-    roof["traffic"] = pmc_traffic(args.size, args.vacuum) if f.fused_active() else None
+    roof["traffic"] = (pmc_traffic(args.size, args.vacuum)
+                       if f.fused_active() and args.workload in ("waveguide", "vacuum") else None)
+    if world > 1 and os.environ.get("MNL_BENCH_DEVICE"):
+        roof["note"] = ("all ranks share one GPU (rehearsal): the per-launch rate is a share "
+                        "of one device, not a roofline fraction")
     if args.flux:
         d_n, d_ms, d_bytes = f.kernel_stats(3)
         if d_n:
@@ -353,10 +363,13 @@ def main():
         "data": "synthetic (Gaussian point source; fields start at zero)",
         "config": {
             "workload": WORKLOADS[args.workload] +
-                        f", {args.size}x{args.size}x({args.size}*N) cells, res 10, real fields" +
+                        (f", {args.size}x{args.size}x({args.size // 4}*N) cells" if args.workload == "c5"
+                         else f", {args.size}x{args.size}x({args.size}*N) cells") +
+                        ", res 10, real fields" +
                         (", Ez Gaussian current at (0.05,0.05,0.05)"
-                         if args.workload in ("waveguide", "vacuum") else ""),
-            "grid": list(gv.n), "per_gpu_cells": args.size ** 3, "parallelism": f"z-slab x{world}",
+                         if args.workload in ("waveguide", "vacuum", "c5") else ""),
+            "grid": list(gv.n), "per_gpu_cells": int(gv.n[0]) * int(gv.n[1]) * int(gv.n[2]) // world,
+            "parallelism": f"z-slab x{world}",
             "transport": transport, "fused": fused,
             "flux_planes": args.flux, "flux_nfreq": args.nfreq if args.flux else 0,
             "model_bytes_per_cell_step": bpc,

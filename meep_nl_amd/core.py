@@ -614,7 +614,19 @@ def ipc_id(nranks):
     shared-memory control block; pass it as nccl_id to every rank's Fields."""
     buf = ctypes.create_string_buffer(128)
     check(lib().mnl_comm_ipc_id(buf, int(nranks)))
-    return buf.raw
+    raw = buf.raw
+    # rank 0 unlinks the segment once every rank has joined (mnl_comm.cpp init_ipc); if
+    # the group never forms (a rank fails before creating its Fields) the creator removes
+    # it at exit instead, so nothing stays in /dev/shm
+    import atexit
+
+    def _unlink(r=raw):
+        try:
+            lib().mnl_comm_ipc_unlink(ctypes.create_string_buffer(r, 128))
+        except Exception:
+            pass
+    atexit.register(_unlink)
+    return raw
 
 
 def pick_transport(world, local_rank):

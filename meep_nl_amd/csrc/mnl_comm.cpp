@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cerrno>
+#include <csignal>
 #include <fcntl.h>
 #include <mutex>
 #include <sched.h>
@@ -76,7 +78,7 @@ struct IpcSlot {
   hipIpcMemHandle_t h;
   uint64_t gen;
   int nposts;
-  int pad;
+  int pid;  // the rank's process (liveness checks of the waits)
   IpcPost posts[IPC_MAXPOST];
   double red[IPC_RED];
 };
@@ -135,13 +137,28 @@ int Comm::init_ipc(const void *id128) {
   if (p == MAP_FAILED) return -1;
   ipc_ = (IpcCtl *)p;
   int expect = 0;
-  if (!ipc_->nranks.compare_exchange_strong(expect, nranks) && expect != nranks) return -1;
+  if (!ipc_->nranks.compare_exchange_strong(expect, nranks) && expect != nranks) {
+    ipc_abort();  // the peers would otherwise wait for this rank until their timeout
+    return -1;
+  }
   if (const char *t = getenv("MNL_IPC_TIMEOUT")) ipc_timeout_s_ = std::max(1.0, atof(t));
   peer_base_.assign(nranks, nullptr);
   peer_gen_.assign(nranks, 0);
-  if (ipc_barrier()) return -1;
+  ipc_->slot[rank].pid = (int)getpid();
+  if (ipc_barrier()) return -1;  // the setup barrier: bounded by MNL_IPC_TIMEOUT
+  ipc_ready_ = true;              // later waits: as long as every peer process lives
   if (rank == 0) shm_unlink(name);  // every rank has it mapped: nothing leaks in /dev/shm
   return 0;
+}
+
+// a peer's process has exited (its pid no longer exists)
+bool Comm::ipc_peer_dead() const {
+  for (int r = 0; r < nranks; r++) {
+    const int pid = ipc_->slot[r].pid;
+    if (r == rank || pid <= 0) continue;
+    if (kill(pid, 0) != 0 && errno == ESRCH) return true;
+  }
+  return false;
 }
 
 void Comm::ipc_abort() {
@@ -157,6 +174,11 @@ int Comm::ipc_barrier() {
     C.gen.fetch_add(1, std::memory_order_release);
     return 0;
   }
+  // Setup waits are bounded by MNL_IPC_TIMEOUT (300 s); once every rank has joined, a
+  // wait lasts as long as the peers' processes live (a rank-0-only output or a whole-cell
+  // setup can legitimately keep the others waiting for minutes), and MNL_IPC_TIMEOUT
+  // bounds it only when set explicitly.
+  static const bool explicit_timeout = getenv("MNL_IPC_TIMEOUT") != nullptr;
   auto t0 = std::chrono::steady_clock::now();
   long spins = 0;
   while (C.gen.load(std::memory_order_acquire) == g) {
@@ -164,11 +186,17 @@ int Comm::ipc_barrier() {
     if (++spins > 2000) {
       struct timespec d = {0, 20000};
       nanosleep(&d, nullptr);
-      if ((spins & 1023) == 0 &&
-          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
-              ipc_timeout_s_) {
-        ipc_abort();  // a peer died or diverged: fail every rank instead of hanging
-        return -1;
+      if ((spins & 1023) == 0) {
+        if (ipc_ready_ && ipc_peer_dead()) {
+          ipc_abort();  // a peer died: fail every rank instead of hanging
+          return -1;
+        }
+        if ((!ipc_ready_ || explicit_timeout) &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+                ipc_timeout_s_) {
+          ipc_abort();  // a peer never joined or diverged: fail every rank
+          return -1;
+        }
       }
     } else {
       sched_yield();

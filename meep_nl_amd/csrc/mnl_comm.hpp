@@ -57,6 +57,8 @@ class Comm {
   std::vector<double *> peer_base_;
   std::vector<uint64_t> peer_gen_;
   double ipc_timeout_s_ = 300.0;
+  bool ipc_ready_ = false;  // every rank joined (setup barrier passed)
+  bool ipc_peer_dead() const;
   struct Op {
     double *dst;
     const double *src;

@@ -239,6 +239,19 @@ struct mnl_fields {
   std::vector<int> gitems;   // general-kernel items
   int *d_gitems = nullptr;
   size_t d_gitems_cap = 0;
+  // tile mode (MNL_TILE, default on): one tile kernel over every chunk outside the
+  // polarization chunks (lean + PML bodies), the general kernel over those chunks only
+  bool tile_mode = true;
+  bool tile_zcut = true;      // cut z chunks at the lean box's z range (short z-PML items)
+  int tile_body_mask = -1;   // MNL_TILE_BODY_MASK: step only these bodies (timing experiments)
+  std::vector<int> titems;   // tile-kernel items (FusedArgs::titems)
+  int *d_titems = nullptr;
+  size_t d_titems_cap = 0;
+  unsigned *d_tflag = nullptr;  // per tile item: uniform palette word or ~0u
+  size_t tflag_n = 0;
+  long long tile_cells = 0;     // own cells of the tile items
+  double tile_cells_nu = -1;    // ... of those that read a palette index per cell
+  std::vector<char> tile_z;     // per local z plane: stepped by the tile kernel
   long long lean_cells = 0, gen_cells = 0;
   FusedTab d_tab{};          // per-direction PML coefficient tables for the fused kernels
   // multi-rank fused stepping: chunk 0 on s_aux, halo exchange on s_comm,
@@ -333,6 +346,8 @@ struct mnl_fields {
     if (d_scratch) hipFree(d_scratch);
     if (d_vals) hipFree(d_vals);
     if (d_gitems) hipFree(d_gitems);
+    if (d_titems) hipFree(d_titems);
+    if (d_tflag) hipFree(d_tflag);
     if (d_uflag) hipFree(d_uflag);
     if (d_gflag) hipFree(d_gflag);
     comm.reset();
@@ -2057,6 +2072,232 @@ static int lean_halo_reads() {
   return e && e[0] == '0' ? 0 : 1;
 }
 
+// Tile mode.  Tiles of the lean body's shape over all of G:
+// columns in pieces of <= 64 from G.lo (128-byte aligned), rows in balanced pieces of
+// <= 14, z chunks; every chunk whose footprint (planes zs-1 .. ze) misses the
+// polarization boxes' z range is stepped by the tile kernel, one item per (tile, chunk),
+// with the body its footprint needs (lean inside L, else the PML body of the directions
+// whose tables are not the identity there).  The remaining (polarization) chunks keep the
+// general kernel's items (wide tiles).  Multi-rank: chunk 0 = planes 0..1 (the B the
+// lower neighbour needs), launched first.
+bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
+  const DevGrid &g = F->g;
+  FusedArgs &a = F->fgeo;
+  std::vector<int> xb, yb, zb, gyb;
+  split_range(xb, G.lo[0], G.hi[0] + 1, FX_HOST, 16);
+  {
+    const int ny = G.hi[1] - G.lo[1] + 1, nt = (ny + 13) / 14;
+    for (int t = 0; t < nt; t++) yb.push_back(G.lo[1] + (int)((long long)ny * t / nt));
+  }
+  int pzl = INT32_MAX, pzh = -1;
+  for (int k = 0; k < F->f.npol; k++)
+    if (F->f.pol[k].nz.lo[2] <= F->f.pol[k].nz.hi[2]) {
+      pzl = std::min(pzl, F->f.pol[k].nz.lo[2]);
+      pzh = std::max(pzh, F->f.pol[k].nz.hi[2]);
+    }
+  // z segments: [lo, hi) with a flag "polarization chunk"
+  // (cut at plane 2 on multi-rank runs so that chunk 0 = planes 0..1, and at the ends of
+  // the polarization chunks [pzl-1, pzh+2), the planes whose tile footprint would meet
+  // the polarization boxes)
+  std::vector<std::pair<std::pair<int, int>, bool>> seg;
+  {
+    const int z0 = G.lo[2], zend = G.hi[2] + 1;
+    const int p0 = pzh >= 0 ? std::max(z0, pzl - 1) : zend, p1 = pzh >= 0 ? std::min(zend, pzh + 2) : zend;
+    std::vector<int> cut = {z0, zend};
+    if (F->nranks > 1 && zend - z0 > 2) cut.push_back(z0 + 2);
+    // the lean box's z range: chunks from L.lo+1 to L.hi can run the lean body (their
+    // halo planes lie in L), the ones outside hold the z-PML planes (short PML items)
+    if (F->tile_zcut && L.lo[2] <= L.hi[2]) {
+      if (L.lo[2] + 1 > z0 && L.lo[2] + 1 < zend) cut.push_back(L.lo[2] + 1);
+      if (L.hi[2] > z0 && L.hi[2] < zend) cut.push_back(L.hi[2]);
+    }
+    if (p0 < p1) cut.push_back(p0), cut.push_back(p1);
+    std::sort(cut.begin(), cut.end());
+    cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
+    for (size_t i = 0; i + 1 < cut.size(); i++)
+      seg.push_back({{cut[i], cut[i + 1]}, cut[i] >= p0 && cut[i + 1] <= p1 && p0 < p1});
+  }
+  // chunk length: MNL_FUSED_ZCHUNK, else the candidate whose item count fills whole
+  // rounds of one workgroup per CU best (with the halo-plane overhead 1 / planes)
+  const long long ntile = (long long)xb.size() * yb.size();
+  int zc = F->fused_zchunk > 0 ? std::min(F->fused_zchunk, FUSED_MAXCH) : 24;
+  if (F->fused_zchunk <= 0) {
+    const long long cus = std::max(1, k_cu_count());
+    double best = -1;
+    for (int cand : {12, 14, 16, 18, 20, 22, 24, 28, 32}) {
+      long long nch = 0, planes = 0;
+      for (auto &sg : seg) {
+        if (sg.second) continue;
+        nch += (sg.first.second - sg.first.first + cand - 1) / cand;
+        planes += sg.first.second - sg.first.first;
+      }
+      if (nch == 0) break;
+      const long long items = ntile * nch;
+      const double fill = double(items) / double(((items + cus - 1) / cus) * cus);
+      const double per = double(planes) / double(nch);
+      const double score = fill * per / (per + 1.0);
+      if (score >= best - 1e-12) best = score, zc = cand;
+    }
+  }
+  // polarization chunks (general kernel, wide tiles): short enough that their items
+  // number at least two per CU
+  int pzc = FUSED_MAXCH;
+  {
+    const long long per_chunk = (long long)xb.size() *
+                                ((G.hi[1] - G.lo[1] + FUSED_GW_ROWS) / FUSED_GW_ROWS);
+    long long pplanes = 0;
+    for (auto &sg : seg)
+      if (sg.second) pplanes += sg.first.second - sg.first.first;
+    if (pplanes > 0) {
+      const long long want = 2LL * std::max(1, k_cu_count());
+      const long long nch = std::max(1LL, (want + per_chunk - 1) / per_chunk);
+      pzc = (int)std::max(4LL, std::min<long long>(FUSED_MAXCH, (pplanes + nch - 1) / nch));
+    }
+  }
+  std::vector<char> polch;
+  auto split_bal = [&](int lo, int hi, int step, bool pol) {  // balanced pieces of <= step
+    const int n = hi - lo, nt = (n + step - 1) / step;
+    for (int t = 0; t < nt; t++) {
+      zb.push_back(lo + (int)((long long)n * t / nt));
+      polch.push_back(pol);
+    }
+  };
+  for (auto &sg : seg) split_bal(sg.first.first, sg.first.second, sg.second ? pzc : zc, sg.second);
+  split_range(gyb, G.lo[1], G.hi[1] + 1, FUSED_GW_ROWS, 1);
+  if ((int)xb.size() > FUSED_MAXX || (int)yb.size() > FUSED_MAXY ||
+      (int)gyb.size() > FUSED_MAXGY || (int)zb.size() > FUSED_MAXZ)
+    return false;
+  a.nx = (int)xb.size();
+  a.ny = (int)yb.size();
+  a.ngy = (int)gyb.size();
+  a.nny = 0;
+  a.nch = (int)zb.size();
+  for (size_t i = 0; i < xb.size(); i++) a.xb[i] = xb[i];
+  a.xb[xb.size()] = G.hi[0] + 1;
+  for (size_t i = 0; i < yb.size(); i++) a.yb[i] = yb[i];
+  a.yb[yb.size()] = G.hi[1] + 1;
+  for (size_t i = 0; i < gyb.size(); i++) a.gyb[i] = gyb[i];
+  a.gyb[gyb.size()] = G.hi[1] + 1;
+  a.nyb[0] = G.lo[1], a.nyb[1] = G.hi[1] + 1;
+  for (size_t i = 0; i < zb.size(); i++) a.zb[i] = zb[i];
+  a.zb[zb.size()] = G.hi[2] + 1;
+  a.lx0 = 0, a.lx1 = -1, a.ly0 = 0, a.ly1 = -1, a.nlzr = 0;  // no lean-only launch
+  for (int k = 0; k < 3; k++) {
+    a.N[k] = g.N[k];
+    a.off[k] = g.off[k];
+    a.osh_lo[k] = g.owned_lo_sh[k];
+    a.osh_hi[k] = std::min(g.owned_hi_sh[k], G.hi[k]);
+    a.oun_lo[k] = g.owned_lo_un[k];
+    a.oun_hi[k] = std::min(g.owned_hi_un[k], G.hi[k]);
+  }
+  // directions whose PML tables are not the identity somewhere in [lo, hi] (per axis)
+  auto pml_dirs = [&](const int lo[3], const int hi[3]) -> int {
+    int m = 0;
+    for (int d = 0; d < 3; d++) {
+      if (F->h_flag[d].empty()) continue;
+      for (int j = std::max(lo[d], 0); j <= std::min(hi[d], g.N[d] - 1) && !(m >> d & 1); j++)
+        for (int sft = 0; sft < 2; sft++) {
+          const size_t q = 2 * (size_t)(j + g.off[d]) + sft;
+          if (q >= F->h_flag[d].size()) continue;
+          const double kap = F->h_kap[d][q], sig = F->h_sig[d][q];
+          if (F->h_flag[d][q] || kap - sig != 1.0 || kap + sig != 1.0 || F->h_siginv[d][q] != 1.0)
+            m |= 1 << d;
+        }
+    }
+    return m;
+  };
+  // ---- tile items
+  F->titems.clear();
+  F->gitems.clear();
+  F->tile_cells = F->lean_cells = F->gen_cells = 0;
+  F->tile_z.assign(std::max(g.N[2], 1), 0);
+  std::vector<int> early, heavy, lean, gen_e, gen_r;
+  for (int ch = 0; ch < a.nch; ch++) {
+    const int zs = a.zb[ch], ze = a.zb[ch + 1];
+    if (polch[ch]) {
+      for (int ty = 0; ty < a.ngy; ty++)
+        for (int tx = 0; tx < a.nx; tx++) {
+          const int y0 = a.gyb[ty] - 1;
+          const int lo[3] = {a.xb[tx] - 1, y0, zs - 1};
+          const int hi[3] = {a.xb[tx] + FX_HOST, y0 + FUSED_GW_ROWS + 1, ze + 1};
+          const int m = pml_dirs(lo, hi);
+          const int v = tx | (ty << 8) | (ch << 16) |
+                        (((m & ~2) == 0 ? 2 : (m & ~4) == 0 ? 4 : 7) << 24);
+          F->gen_cells += (long long)(a.xb[tx + 1] - a.xb[tx]) * (a.gyb[ty + 1] - a.gyb[ty]) *
+                          (ze - zs);
+          (ch == 0 ? gen_e : gen_r).push_back(v);
+        }
+      continue;
+    }
+    for (int z = zs; z < ze; z++) F->tile_z[z] = 1;
+    for (int ty = 0; ty < a.ny; ty++)
+      for (int tx = 0; tx < a.nx; tx++) {
+        const int x0 = a.xb[tx], x1 = a.xb[tx + 1] - 1, y0 = a.yb[ty] - 1, y1 = a.yb[ty + 1] - 1;
+        const long long cells = (long long)(x1 - x0 + 1) * (y1 - y0) * (ze - zs);
+        F->tile_cells += cells;
+        const bool in_l = x0 - 1 >= L.lo[0] && x1 + 1 <= L.hi[0] && y0 >= L.lo[1] &&
+                          y1 + 1 <= L.hi[1] && zs - 1 >= L.lo[2] && ze <= L.hi[2];
+        int body = 0;
+        if (in_l) {
+          F->lean_cells += cells;
+        } else {
+          const int lo[3] = {x0 - 1, y0, zs - 1}, hi[3] = {x0 + FX_HOST, y0 + 15, ze};
+          const int m = pml_dirs(lo, hi);
+          body = m == 1 ? 1 : m == 2 ? 2 : m == 4 ? 3 : m == 0 ? 4 : m == 3 ? 6 : m == 5 ? 7 : 5;
+        }
+        const int v = tx | (ty << 8) | (ch << 16) | (body << 24);
+        if (F->tile_body_mask >= 0 && !((F->tile_body_mask >> body) & 1)) continue;  // timing only
+        if (F->nranks > 1 && ch == 0)
+          early.push_back(v);
+        else
+          (body ? heavy : lean).push_back(v);
+      }
+  }
+  auto planes = [&](int v) { const int ch = (v >> 16) & 255; return a.zb[ch + 1] - a.zb[ch]; };
+  auto longest_first = [&](std::vector<int> &v) {
+    std::stable_sort(v.begin(), v.end(), [&](int x, int y) { return planes(x) > planes(y); });
+  };
+  longest_first(heavy);
+  longest_first(lean);
+  if (getenv("MNL_TILE_STATS")) {  // per-body item / cell counts (diagnostics)
+    long long ni[8] = {0}, nc[8] = {0};
+    for (auto *v : {&early, &heavy, &lean})
+      for (int it : *v) {
+        const int b = (it >> 24) & 7, tx = it & 255, ty = (it >> 8) & 255, ch = (it >> 16) & 255;
+        ni[b]++;
+        nc[b] += (long long)(a.xb[tx + 1] - a.xb[tx]) * (a.yb[ty + 1] - a.yb[ty]) *
+                 (a.zb[ch + 1] - a.zb[ch]);
+      }
+    fprintf(stderr, "tile: nx %d ny %d nch %d zc %d pzc %d gen %zu+%zu\n", a.nx, a.ny, a.nch, zc,
+            pzc, gen_e.size(), gen_r.size());
+    for (int b = 0; b < 8; b++) fprintf(stderr, "tile body %d: %lld items %lld cells\n", b, ni[b], nc[b]);
+  }
+  F->titems = early;
+  F->titems.insert(F->titems.end(), heavy.begin(), heavy.end());
+  F->titems.insert(F->titems.end(), lean.begin(), lean.end());
+  a.ntit = (int)F->titems.size();
+  a.ntit_e = (int)early.size();
+  longest_first(gen_r);
+  F->gitems = gen_e;
+  F->gitems.insert(F->gitems.end(), gen_r.begin(), gen_r.end());
+  a.ngen = (int)F->gitems.size();
+  a.ngen_e = (int)gen_e.size();
+  a.ngen_n = a.ngen_ne = 0;
+  // ---- shell: the top plane of a rank with an upper neighbour
+  BoxList &bl = F->fused_shell;
+  memset(&bl, 0, sizeof(bl));
+  if (F->nranks > 1 && F->rank + 1 < F->nranks) {
+    Box b;
+    for (int k = 0; k < 3; k++) b.lo[k] = 0, b.hi[k] = g.N[k] - 1;
+    b.lo[2] = b.hi[2] = g.N[2] - 1;
+    bl.b[0] = b;
+    bl.start[0] = 0;
+    bl.start[1] = (long long)g.N[0] * g.N[1];
+    bl.n = 1;
+  }
+  return true;
+}
+
 bool make_fused_boxes(mnl_fields *F) {
   const DevGrid &g = F->g;
   Box G, L;
@@ -2075,6 +2316,7 @@ bool make_fused_boxes(mnl_fields *F) {
   memset(&a, 0, sizeof(a));
   a.G = G;
   a.L = L;
+  if (F->tile_mode) return make_tile_boxes(F, G, L);
   // z-chunk: MNL_FUSED_ZCHUNK, else chosen below (after the lean geometry is known) so
   // that the lean items fill whole rounds of one workgroup per CU; 512^3 gets 24 planes
   // (measured 3.13 ms/step vs 3.17 (16) and 3.27 (32), profiles/README.md)
@@ -2493,6 +2735,15 @@ int set_fused(mnl_fields *F, bool on) {
     if (!F->gitems.empty())
       HIPCHK(hipMemcpyAsync(F->d_gitems, F->gitems.data(), F->gitems.size() * sizeof(int),
                             hipMemcpyHostToDevice, F->stream));
+    if (F->d_titems_cap < F->titems.size()) {
+      if (F->d_titems) hipFree(F->d_titems);
+      F->d_titems = nullptr;
+      HIPCHK(hipMalloc(&F->d_titems, F->titems.size() * sizeof(int)));
+      F->d_titems_cap = F->titems.size();
+    }
+    if (!F->titems.empty())
+      HIPCHK(hipMemcpyAsync(F->d_titems, F->titems.data(), F->titems.size() * sizeof(int),
+                            hipMemcpyHostToDevice, F->stream));
     if (build_palette(F)) return -1;
     // ping-pong partners; the second buffer starts as a copy (ghost / wall entries
     // that no kernel writes)
@@ -2575,6 +2826,8 @@ FusedArgs &fused_args(mnl_fields *F) {
       fa.pbox.hi[e] = std::max(fa.pbox.hi[e], f.pol[k].nz.hi[e]);
     }
   fa.gitems = F->d_gitems;
+  fa.titems = F->d_titems;
+  fa.tflag = nullptr;
   fa.uidx = F->d_uidx;
   fa.utab = F->d_utab;
   fa.uflag = nullptr;
@@ -2592,8 +2845,10 @@ FusedArgs &fused_args(mnl_fields *F) {
     for (int i = 0; i <= fa.ngy; i++) mix(fa.gyb[i]);
     for (int i = 0; i <= fa.nny; i++) mix(fa.nyb[i]);
     for (int v : F->gitems) mix(v);
+    for (int v : F->titems) mix(v);
     const long long ntile = (long long)(fa.lx1 - fa.lx0 + 1) * (fa.ly1 - fa.ly0 + 1);
     const size_t n = ntile > 0 ? (size_t)ntile * fa.nch : 0, ng = F->gitems.size();
+    const size_t nt = F->titems.size();
     auto grow = [](unsigned *&p, size_t &cap, size_t want) {
       if (cap >= want) return true;
       if (p) hipFree(p);
@@ -2605,13 +2860,17 @@ FusedArgs &fused_args(mnl_fields *F) {
     bool ok = true;
     if (F->uflag_sig != sig) {
       ok = grow(F->d_uflag, F->uflag_n, n) && grow(F->d_gflag, F->gflag_n, ng) &&
+           grow(F->d_tflag, F->tflag_n, nt) &&
            k_lean_uniform(fa, F->d_uflag, F->stream) == 0 &&
-           k_general_uniform(fa, F->d_gflag, F->stream) == 0;
+           k_general_uniform(fa, F->d_gflag, F->stream) == 0 &&
+           k_tile_uniform(fa, F->d_tflag, F->stream) == 0;
       F->uflag_sig = ok ? sig : 0;
       if (ok) {  // per-item cell counts of the mixed items (traffic model)
-        std::vector<unsigned> hl(n), hg(ng);
+        std::vector<unsigned> hl(n), hg(ng), ht(nt);
         ok = (n == 0 || hipMemcpyAsync(hl.data(), F->d_uflag, n * 4, hipMemcpyDeviceToHost,
                                        F->stream) == hipSuccess) &&
+             (nt == 0 || hipMemcpyAsync(ht.data(), F->d_tflag, nt * 4, hipMemcpyDeviceToHost,
+                                        F->stream) == hipSuccess) &&
              (ng == 0 || hipMemcpyAsync(hg.data(), F->d_gflag, ng * 4, hipMemcpyDeviceToHost,
                                         F->stream) == hipSuccess) &&
              hipStreamSynchronize(F->stream) == hipSuccess;
@@ -2633,17 +2892,26 @@ FusedArgs &fused_args(mnl_fields *F) {
           gn += double(fa.xb[tx + 1] - fa.xb[tx]) * (yb[ty + 1] - yb[ty]) *
                 (fa.zb[ch + 1] - fa.zb[ch]);
         }
+        double tn = 0;
+        for (size_t i = 0; ok && i < nt; i++) {
+          if (ht[i] != ~0u) continue;
+          const int v = F->titems[i], tx = v & 255, ty = (v >> 8) & 255, ch = (v >> 16) & 255;
+          tn += double(fa.xb[tx + 1] - fa.xb[tx]) * (fa.yb[ty + 1] - fa.yb[ty]) *
+                (fa.zb[ch + 1] - fa.zb[ch]);
+        }
         F->lean_cells_nu = ln;
         F->gen_cells_nu = gn;
+        F->tile_cells_nu = tn;
         if (!ok) F->uflag_sig = 0;
       }
     }
     if (ok) {
       fa.uflag = n ? F->d_uflag : nullptr;
       fa.gflag = ng ? F->d_gflag : nullptr;
+      fa.tflag = nt ? F->d_tflag : nullptr;
     }
   }
-  F->uflag_active = fa.uflag || fa.gflag;
+  F->uflag_active = fa.uflag || fa.gflag || fa.tflag;
   fa.ctr = F->d_fused_ctr;
   fa.ngrp = 1;  // lean queue groups (MNL_LEAN_GROUPS); general: MNL_GEN_GROUPS
   if (const char *e = getenv("MNL_LEAN_GROUPS")) fa.ngrp = atoi(e) == 8 ? 8 : 1;
@@ -2694,22 +2962,25 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
   HIPCHK(hipEventRecord(F->ev_start, F->stream));
   HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
   HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_x0, 0));
-  int kr = k_fused(fa, 2, F->s_aux, F->ctr_base);
+  int kr = F->tile_mode ? k_fused(fa, 5, F->s_aux, F->ctr_base) : 0;
+  if (!kr) kr = k_fused(fa, 2, F->s_aux, F->ctr_base);
   if (kr) return fused_fail("fused early kernel launch failed", kr);
   HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
   HIPCHK(hipStreamWaitEvent(F->s_comm, F->ev_early, 0));
   if (exchange(F, 1, F->s_comm)) return fail("H halo exchange failed");
   HIPCHK(hipEventRecord(F->ev_x1, F->s_comm));
   int k = ev_begin(TM_BINT);
-  kr = k_fused(fa, 0, F->stream, F->ctr_base);
+  kr = k_fused(fa, F->tile_mode ? 6 : 0, F->stream, F->ctr_base);
   if (kr) return fused_fail("fused kernel launch failed", kr);
   ev_end(k);
-  k = ev_begin(TM_GEN);
-  fa.lean_after = lean_halo_reads();  // same stream, after the lean launch
-  kr = k_fused(fa, 3, F->stream, F->ctr_base);
-  fa.lean_after = 0;
-  if (kr) return fused_fail("fused general kernel launch failed", kr);
-  ev_end(k);
+  if (!F->tile_mode || fa.ngen > fa.ngen_e) {
+    k = ev_begin(TM_GEN);
+    fa.lean_after = F->tile_mode ? 0 : lean_halo_reads();  // same stream, after the lean launch
+    kr = k_fused(fa, 3, F->stream, F->ctr_base);
+    fa.lean_after = 0;
+    if (kr) return fused_fail("fused general kernel launch failed", kr);
+    ev_end(k);
+  }
   const BoxList *sl = &F->fused_shell;
   if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream, true))
     return fail("curl B launch failed");
@@ -2851,6 +3122,30 @@ int nr_defer_end(mnl_fields *F) {
 
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
+  // in-process A/B of the fused geometry (tools/ab_inproc.py): MNL_TILE_STEP /
+  // MNL_ZCHUNK_STEP change the mode / chunk length between batches (leaving fused mode
+  // first, so the next entry rebuilds and uploads the items)
+  if (const char *e = getenv("MNL_TILE_STEP")) {
+    const bool want = atoi(e) != 0;
+    if (want != F->tile_mode) {
+      if (F->fused && set_fused(F, false)) return -1;
+      F->tile_mode = want;
+    }
+  }
+  if (const char *e = getenv("MNL_ZCUT_STEP")) {
+    const bool want = atoi(e) != 0;
+    if (want != F->tile_zcut) {
+      if (F->fused && set_fused(F, false)) return -1;
+      F->tile_zcut = want;
+    }
+  }
+  if (const char *e = getenv("MNL_ZCHUNK_STEP")) {
+    const int want = std::max(0, atoi(e));
+    if (want != F->fused_zchunk) {
+      if (F->fused && set_fused(F, false)) return -1;
+      F->fused_zchunk = want;
+    }
+  }
   if (set_fused(F, fused_agreed(F))) return -1;
   {  // does a D source point lie in the shell (outside the box the interior kernels own)?
     const Box &ib = F->fused ? F->fusedG : F->interior;
@@ -2977,6 +3272,7 @@ int step_batch(mnl_fields *F, int nsteps) {
     for (int s = 0; s < ns; s++) {
       DevFields &f = F->f;
       const DevGrid &g = F->g;
+      f.nr_t = F->t + s;  // seeds of the NR random fallback (nr_voxel_seed)
       const double *vs = F->d_vals + (size_t)s * per;  // this step's table
       const SrcDev sB = src_dev(F, 0, vs), sD = src_dev(F, 1, vs + 2 * ng);
       ISrcDev is = F->isrc_dev;
@@ -2997,7 +3293,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       int k = ev_begin(TM_BINT);
       if (F->fused) {
         FusedArgs &fa = fused_args(F);
-        const int split = gen_split(F);
+        const int split = F->tile_mode ? 0 : gen_split(F);
         int kr;
         if (split > 0) {
           // general tiles on `split` CUs of a side stream, lean tiles on the others,
@@ -3021,14 +3317,18 @@ int step_batch(mnl_fields *F, int nsteps) {
           F->fused_concurrent = true;
         } else {
           F->fused_concurrent = false;
-          kr = k_fused(fa, 0, F->stream, F->ctr_base);
+          kr = k_fused(fa, F->tile_mode ? 4 : 0, F->stream, F->ctr_base);
           if (kr) return fused_fail("fused kernel launch failed", kr);
-          ev_end(k);
-          k = ev_next(k, TM_GEN);
-          fa.lean_after = lean_halo_reads();  // same stream, after the lean launch
-          kr = k_fused(fa, 1, F->stream, F->ctr_base);
-          fa.lean_after = 0;
-          if (kr) return fused_fail("fused general kernel launch failed", kr);
+          if (!F->tile_mode || fa.ngen > 0) {
+            ev_end(k);
+            k = ev_next(k, TM_GEN);
+            // lean mode: same stream, after the lean launch (tile mode: the general
+            // items are polarization chunks, whose halos no lean launch stores)
+            fa.lean_after = F->tile_mode ? 0 : lean_halo_reads();
+            kr = k_fused(fa, 1, F->stream, F->ctr_base);
+            fa.lean_after = 0;
+            if (kr) return fused_fail("fused general kernel launch failed", kr);
+          }
         }
       } else if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream)) {
         return fail("curl B launch failed");
@@ -4193,6 +4493,8 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   }
   if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(0, atoi(zc));
   if (const char *bp = getenv("MNL_FUSED_BPC")) F->fused_bpc = std::max(1, atoi(bp));
+  if (const char *tm = getenv("MNL_TILE")) F->tile_mode = atoi(tm) != 0;
+  if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
   if (const char *ne = getenv("MNL_NAN_EVERY")) F->nan_every = std::max(1, atoi(ne));
@@ -4776,6 +5078,7 @@ int mnl_fields_initialize_field(mnl_fields *F, int comp, const double *host, siz
   if (n < F->S.ntot) return fail("initialize_field: array smaller than the cell");
   if (!has_field(F->S, comp)) return fail("component not present in this dimensionality");
   if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  F->f.nr_t = F->t;  // its update_eh(E) solves at the current time step
   return initialize_field(F, comp, host);
 }
 
@@ -4952,11 +5255,16 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
   const bool uni = F->d_uidx && F->uflag_active && F->lean_cells_nu >= 0;
   const double lean_u = uni ? F->lean_cells_nu : double(F->lean_cells);
   *lean_bytes = double(F->lean_cells) * 96.0 + lean_u * ub;
-  double extra = 0;
-  // count of local indices j in [lo, hi] of axis e with an optional flag condition
+  double extra = 0, extra_t = 0;
+  // count of local indices j in [lo, hi] of axis e with an optional flag condition;
+  // zsel (axis 2): 0 every plane, 1 the tile kernel's planes, 2 the others
+  int zsel = 0;
   auto cnt = [&](int e, int lo, int hi, int qshift, bool need_flag) -> double {
     double n = 0;
     for (int j = lo; j <= hi; j++) {
+      if (e == 2 && zsel && (j < 0 || j >= (int)F->tile_z.size() ||
+                             (F->tile_z[j] != 0) != (zsel == 1)))
+        continue;
       if (need_flag) {
         if (!F->S.has[e] || F->h_flag[e].empty()) continue;
         if (!F->h_flag[e][2 * (j + g.off[e]) + qshift]) continue;
@@ -4965,21 +5273,29 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
     }
     return n;
   };
-  for (int c = 0; c < 3; c++)
-    for (int kind = 0; kind < 4; kind++) {
-      // kind 0: f_u of B_c (flag along c+2, shifted); 1: H_c (along c, unshifted);
-      // 2: f_u of D_c (along c+2, unshifted); 3: W-form E_c (along c, shifted)
-      const bool btype = kind < 2;
-      const int fe = (kind == 0 || kind == 2) ? (c + 2) % 3 : c;
-      const int qs = (kind == 0 || kind == 3) ? 1 : 0;
-      double n = 1;
-      for (int e = 0; e < 3; e++) {
-        const bool sh = btype ? (e != c) : (e == c);
-        const int lo = sh ? a.osh_lo[e] : a.oun_lo[e], hi = sh ? a.osh_hi[e] : a.oun_hi[e];
-        n *= cnt(e, lo, hi, qs, e == fe);
+  for (int pass = 0; pass < (F->tile_mode ? 2 : 1); pass++) {
+    zsel = F->tile_mode ? (pass == 0 ? 1 : 2) : 0;
+    for (int c = 0; c < 3; c++)
+      for (int kind = 0; kind < 4; kind++) {
+        // kind 0: f_u of B_c (flag along c+2, shifted); 1: H_c (along c, unshifted);
+        // 2: f_u of D_c (along c+2, unshifted); 3: W-form E_c (along c, shifted)
+        const bool btype = kind < 2;
+        const int fe = (kind == 0 || kind == 2) ? (c + 2) % 3 : c;
+        const int qs = (kind == 0 || kind == 3) ? 1 : 0;
+        double n = 1;
+        for (int e = 0; e < 3; e++) {
+          const bool sh = btype ? (e != c) : (e == c);
+          const int lo = sh ? a.osh_lo[e] : a.oun_lo[e], hi = sh ? a.osh_hi[e] : a.oun_hi[e];
+          n *= cnt(e, lo, hi, qs, e == fe);
+        }
+        (zsel == 1 ? extra_t : extra) += 16.0 * n;
       }
-      extra += 16.0 * n;
-    }
+  }
+  if (F->tile_mode) {  // tile kernel = "lean" slot of the statistics, general = the rest
+    const bool tuni = F->d_uidx && F->uflag_active && F->tile_cells_nu >= 0;
+    *lean_bytes = double(F->tile_cells) * 96.0 +
+                  (tuni ? F->tile_cells_nu : double(F->tile_cells)) * ub + extra_t;
+  }
   // polarization boxes: stored E (read + write), P and Pprev (read + write) and
   // sigma (read) per component and susceptibility
   for (int k = 0; k < F->f.npol; k++) {
@@ -4995,6 +5311,12 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
   }
   double gcells = 1;
   for (int e = 0; e < 3; e++) gcells *= double(F->fusedG.hi[e] - F->fusedG.lo[e] + 1);
+  if (F->tile_mode) {
+    const bool guni = F->d_uidx && F->uflag_active && F->gen_cells_nu >= 0;
+    *gen_bytes = double(F->gen_cells) * 96.0 +
+                 (guni ? F->gen_cells_nu : double(F->gen_cells)) * ub + extra;
+    return;
+  }
   const double gen_u = uni ? F->gen_cells_nu : gcells - double(F->lean_cells);
   *gen_bytes = (gcells - double(F->lean_cells)) * 96.0 + gen_u * ub + extra;
 }

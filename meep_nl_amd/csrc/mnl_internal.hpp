@@ -108,6 +108,7 @@ struct DevFields {
   const uint8_t *offd_zone;
   const uint8_t *zone[3];    // per direction, global half-coordinate q -> zone 0/1/2
   unsigned long long *nr_fallbacks;
+  long long nr_t;            // time step of the E update (seeds of the NR random fallback)
   // Newton-Raphson problems whose first attempt failed, deferred to nr_hard_kernel
   // (the later attempts run in parallel, one per lane); null: solve in place
   struct NRHard *nr_hard;
@@ -293,11 +294,18 @@ struct FusedArgs {
   int lean_after;               // general launch follows the lean launch of this step on the
                                 // same stream: halo B_new of lean-stored points is read, not
                                 // recomputed (item bits 27 / 28)
+  // tile kernel: items tx | ty << 8 | ch << 16 | body << 24 over the
+  // lean-shaped tiles (xb, yb, zb) of every chunk outside the polarization chunks; chunk-0
+  // items first (ntit_e of them: the early launch of multi-rank steps)
+  const int *titems;
+  int ntit, ntit_e;
+  const unsigned *tflag;        // per tile item: palette word uniform over its footprint, or ~0u
   unsigned long long cbg[8];    // lean queue g: counter line g's value at launch start
   unsigned long long *ctr;      // FUSED_NCTR work-queue counters (128 B apart); see cbase
 };
 // which: 0 = lean tiles, 1 = all general tiles, 2 = general tiles of chunk 0
-// only (early launch), 3 = the other general tiles.  Every launch reads old /
+// only (early launch), 3 = the other general tiles; tile kernel: 4 = all tile items,
+// 5 = tile items of chunk 0 (early launch), 6 = the other tile items.  Every launch reads old /
 // writes new buffers only, on disjoint points, so any order is valid.
 // bases[FUSED_NCTR]: host copy of each counter line's value, advanced by every launch
 // (items + workgroups), so no counter reset (memset launch) is needed per step
@@ -309,6 +317,7 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
 // (flags: ntile * nch words); the lean kernel then reads one cached word instead of
 // a palette index per cell
 int k_lean_uniform(const FusedArgs &a, unsigned *flags, void *stream);
+int k_tile_uniform(const FusedArgs &a, unsigned *flags, void *stream);
 int k_general_uniform(const FusedArgs &a, unsigned *flags, void *stream);
 int k_cu_count();
 int k_build_uidx(unsigned *uidx, const double *const u[3], const double *tab, const int n[3],
@@ -349,6 +358,25 @@ int k_nonzero_box(const double *const a[3], const DevGrid &g, int *dev_box6, voi
 // structure::set_epsilon with a geometric material function (subpixel averaging),
 // src/anisotropic_averaging.cpp:58-298: one thread per canonical point of E comp c
 // one deferred chi(2) Newton-Raphson problem (run_nr after a failed first attempt)
+// Seed of the deterministic stand-in for the std::random_device fallback of runNR
+// (newton_raphson.cpp:196-206, 331-336): a counter-based value of the point's global
+// half-coordinates q (relative to the cell's little corner; 0 for absent directions), the
+// E component d and the time step t, so the oracle (oracle/mnl_oracle.cpp) reproduces the
+// product's draws whatever the order, the thread or the rank a point is solved on.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline unsigned long long nr_voxel_seed(long long q0, long long q1, long long q2, int d,
+                                        long long t) {
+  unsigned long long h = 0x9E3779B97F4A7C15ull;
+  h ^= (unsigned long long)q0 * 0xBF58476D1CE4E5B9ull;
+  h ^= (unsigned long long)q1 * 0x94D049BB133111EBull;
+  h ^= (unsigned long long)q2 * 0xD6E8FEB86659FD93ull;
+  h ^= (unsigned long long)d * 0x2545F4914F6CDD1Dull;
+  h ^= (unsigned long long)t * 0x9FB21C651E98DF25ull;
+  return h;
+}
+
 struct NRHard {
   double p[15];       // NRP p1, p2, p3 (A, B, F, G, H each)
   double seed[3];     // the first attempt's seeds

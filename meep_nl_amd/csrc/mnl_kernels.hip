@@ -15,6 +15,12 @@
 
 #include "mnl_internal.hpp"
 
+// Every kernel here is written for 64-lane wavefronts (gfx950): the fused bodies map one
+// 64-column row to a wave, nr_hard_kernel runs one attempt per lane with a 64-bit ballot.
+#if defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "mnl_kernels.hip needs wave64 (build for gfx950)"
+#endif
+
 namespace mnl {
 
 #define MNL_BX 64
@@ -389,11 +395,14 @@ __device__ double nr_random(unsigned long long &st) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
   };
-  double u1 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-  double u2 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-  double u3 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-  double gg = sqrt(-2.0 * log(u1)) * cos(2 * 3.141592653589793238462643383276 * u2);
-  return exp(1.0 + 90.0 * gg) * (2.0 * u3 - 1.0);
+  // a log-uniform magnitude over 2^-300 .. 2^300 (the reference draws lognormal(1, 90) x
+  // uniform(-1, 1): the same role, seeds spread over hundreds of decades) with a random
+  // sign, from exact operations only (no libm), so the oracle's draws are bitwise equal
+  const unsigned long long r1 = next(), r2 = next(), r3 = next();
+  const int e = (int)(r1 % 601ull) - 300;
+  const double m = 1.0 + (double)(r2 >> 11) * (1.0 / 9007199254740992.0);
+  const double v = ldexp(m, e);
+  return (r3 >> 63) ? -v : v;
 }
 
 // Seeds of attempt a >= 1 of runNR (the state the sequential loop below reaches):
@@ -812,8 +821,9 @@ __device__ __forceinline__ void e_point(const DevGrid &g, const DevFields &f, co
             double us_2 = us, us_3 = us;
             double dummy1 = 0.0, dummy2 = 0.0;
             double fv = E[i];
-            unsigned long long rng = 0x9E3779B97F4A7C15ull ^ (unsigned long long)i * 31ull ^
-                                     ((unsigned long long)step << 40) ^ (unsigned long long)d;
+            const unsigned long long rng = nr_voxel_seed(
+                g.ax[0] >= 0 ? qcoord(g, p, T_E, d, 0) : 0, g.ax[1] >= 0 ? qcoord(g, p, T_E, d, 1) : 0,
+                g.ax[2] >= 0 ? qcoord(g, p, T_E, d, 2) : 0, d, f.nr_t);
             if (d == 0) {
               NRP p1 = {gs, us, chi2new, 0.0, 0.0};
               NRP p2 = {gs_2, us_2, 0.0, chi2new, 0.0};
@@ -2184,21 +2194,20 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
   }
 }
 
+// Lean body over one item (tile columns x0..x1, own rows y0+1..y1, planes [zs, ze)):
+// its whole footprint (columns x0-1 .. x1+1, rows y0 .. y1+1, planes zs-1 .. ze) lies in
+// the lean box L: no PML, every component owned, H == B, E implicit.  1024 threads:
+// waves 0..FR-1 hold one row each (row 0 = the y-1 halo row, B recomputed), wave FR the
+// x-1 column (B recomputed), the E of the x+64 column and a corner.
 template <int UMODE, int DIST>
-__global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
+__device__ __forceinline__ void lean_body(const FusedArgs &a, const ItemGeo &itg, unsigned uw,
+                                          const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
+                                          double (*sB)[FR][FX + 1]) {
   constexpr bool HAS_U = UMODE != 0;
-  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
-  __shared__ double sE[3][FR + 1][FX + 2];
-  __shared__ double sB[3][FR][FX + 1];
-  __shared__ long long s_item;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool hwave = __builtin_amdgcn_readfirstlane(w) >= FR - 1;  // wave-uniform
   const int flo0 = a.L.lo[0], flo1 = a.L.lo[1], flo2 = a.L.lo[2];
   const int fhi0 = a.L.hi[0], fhi1 = a.L.hi[1], fhi2 = a.L.hi[2];
-  int nlch = 0;
-  for (int r = 0; r < a.nlzr; r++) nlch += a.lzr[r][1] - a.lzr[r][0] + 1;
-  const int nlx = a.lx1 - a.lx0 + 1;
-  const long long ntile = (long long)nlx * (a.ly1 - a.ly0 + 1);
   const unsigned s2 = (unsigned)(a.st2 * 8);  // byte stride of one z plane
   const double C = a.C;
   const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
@@ -2261,47 +2270,8 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   const unsigned safe = (unsigned)((flo0 + (long long)flo1 * a.st1) * 8);
   auto zin = [&](int z) { return z >= flo2 && z <= fhi2; };
   auto e_of = [](double d, double u, bool fz) { return (HAS_U && fz) ? d * u : d; };
-  if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
-    for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
-  }
   auto pu = [&](unsigned ui, int c) -> double { return sU[UMODE == 2 ? c : 0][(ui >> (8 * c)) & 255]; };
-
-  // Work queues, chunk-major: consecutive items are neighbouring tiles of one
-  // chunk, so the workgroups sweep z roughly together.  With ngrp = 8 the
-  // workgroups sharing an XCD (blockIdx % 8, observed round-robin placement;
-  // speed only) own a contiguous range of each chunk's tiles (x fastest), so
-  // the halo lines neighbouring tiles share are fetched once into that XCD's L2.
-  const int grp = a.ngrp > 1 ? (int)(blockIdx.x % a.ngrp) : 0;
-  const long long gt0 = ntile * grp / a.ngrp, gt1 = ntile * (grp + 1) / a.ngrp;
-  const long long gtile = gt1 - gt0;
-  unsigned long long *gctr = a.ctr + 16 * grp;
-  const unsigned long long gbase = a.ngrp > 1 ? a.cbg[grp] : a.cbase;
-  for (;;) {
-    if (threadIdx.x == 0) {
-      const unsigned long long v = atomicAdd(gctr, 1ULL) - gbase;
-      s_item = (long long)v < gtile * nlch ? (long long)v : -1;
-    }
-    __syncthreads();  // also separates LDS use of consecutive items
-    const long long item = s_item;
-    if (item < 0) break;
-    int ch = (int)(item / gtile);  // lean chunk ordinal -> chunk index
-    for (int r = 0; r < a.nlzr; r++) {
-      const int n = a.lzr[r][1] - a.lzr[r][0] + 1;
-      if (ch < n) {
-        ch += a.lzr[r][0];
-        break;
-      }
-      ch -= n;
-    }
-    const int tile = (int)(gt0 + item % gtile);
-    const int tx = a.lx0 + tile % nlx, ty = a.ly0 + tile / nlx;
-    ItemGeo itg;
-    itg.x0 = a.xb[tx];
-    itg.x1 = a.xb[tx + 1] - 1;
-    itg.y0 = a.yb[ty] - 1;
-    itg.y1 = a.yb[ty + 1] - 1;
-    itg.zs = a.zb[ch];
-    itg.ze = a.zb[ch + 1];
+  {
     // ---------------- lean body: rows y0-1 .. y1+1, columns x0-1 .. x1+1, planes
     // zs-1 .. ze lie in L (lanes past x1 / y1 only feed values that are not stored)
     const int zs = itg.zs, ze = itg.ze;  // planes [zs, ze)
@@ -2324,7 +2294,6 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
     const gdp pH0 = hF ? hD0 : hE0, pH1 = hF ? hD1 : hE1;
     // palette word uniform over the item: every index load reads the same cached word
     // (the first cell of the item's footprint in L) instead of one word per cell
-    const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[(long long)tile * a.nch + ch] : ~0u;
     const bool uni = __builtin_amdgcn_readfirstlane(uw) != ~0u;
     const unsigned ufix =
         (unsigned)((max(x0 - 1, flo0) + (long long)max(y0, flo1) * a.st1 +
@@ -2461,6 +2430,549 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
         ez = e1z;
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tile kernel: one persistent launch over every tile of G
+// outside the polarization chunks, in the lean body's 1024-thread layout (64 x 14
+// own cells per plane, z-march).  Items whose footprint lies in L run lean_body;
+// the others run pml_body<AX>, specialised by the PML directions AX its footprint
+// meets (faces: 1 = x, 2 = y, 4 = z; 7 = edges / corners; 0 = boundary planes
+// without PML).  The PML quantities of a lane are fixed along the march for x
+// (per lane) and y (per row) and uniform per plane for z, so every face body is
+// the lean body plus per-direction table reads (LDS) and the PML state of that
+// direction only, loaded and stored through buffer descriptors with out-of-range
+// offsets where a point holds none (no branches around memory operations).
+
+// PML coefficient tables of one tile item's footprint:
+// v[axis][0 = kap - sig, 1 = 1 / (kap + sig), 2 = kap + sig][half s][position]
+// f[axis][half s][position] = the PML-chunk flag (src/structure.cpp:118-137)
+struct PTabL {
+  double v[3][3][2][TPZ];
+  unsigned char f[3][2][TPZ];
+};
+static_assert(TPZ >= FX + 2 && TPZ >= FR + 1, "table positions");
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, unsigned nrec) {
+  // null: zero records, every access out of range (loads 0, stores dropped)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, p ? (int)nrec : 0,
+                                           0x00020000);
+}
+__device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
+// ownership bits of an index along one axis: bit0 = shifted components owned, bit1 = unshifted
+__device__ __forceinline__ unsigned own_bits_of(int v, int sl, int sh, int ul, int uh) {
+  return ((v >= sl && v <= sh) ? 1u : 0u) | ((v >= ul && v <= uh) ? 2u : 0u);
+}
+
+template <int UMODE, int DIST, int AX>
+__device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, unsigned uw,
+                                         const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
+                                         double (*sB)[FR][FX + 1], PTabL &P) {
+  constexpr bool HAS_U = UMODE != 0;
+  constexpr bool PX = (AX & 1) != 0, PY = (AX & 2) != 0, PZ = (AX & 4) != 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool hwave = __builtin_amdgcn_readfirstlane(w) >= FR - 1;  // wave-uniform
+  const int x0 = it.x0, y0 = it.y0, zs = it.zs, ze = it.ze;
+  const int zlo = zs - 1;  // z table position 0
+  // ---- PML tables of the footprint -> LDS (x: x0-1 .. x0+64, y: y0 .. y0+FR,
+  // z: zs-1 .. ze), only the directions of this body
+  {
+    constexpr int NX = PX ? 2 * (FX + 2) : 0, NY = PY ? 2 * (FR + 1) : 0, NZ = PZ ? 2 * TPZ : 0;
+    for (int i = threadIdx.x; i < NX + NY + NZ; i += 1024) {
+      int ax, pos, base;
+      if (i < NX) {
+        ax = 0, pos = i >> 1, base = x0 - 1;
+      } else if (i < NX + NY) {
+        ax = 1, pos = (i - NX) >> 1, base = y0;
+      } else {
+        ax = 2, pos = (i - NX - NY) >> 1, base = zlo;
+      }
+      const int sft = i & 1;
+      const int jj = min(max(base + pos, 0), a.N[ax] - 1);
+      const int q = 2 * (jj + a.off[ax]) + sft;
+      P.v[ax][0][sft][pos] = a.tab.kms[ax][q];
+      P.v[ax][1][sft][pos] = a.tab.siginv[ax][q];
+      P.v[ax][2][sft][pos] = a.tab.kps[ax][q];
+      P.f[ax][sft][pos] = a.tab.flag[ax][q];
+    }
+  }
+  // ---- lane roles (the lean body's)
+  int row, col;
+  bool ownlike;
+  int hrow = 0, hcol = 0, hc0 = 0, hdx = 0, hdy = 0;
+  bool hslot = false;
+  if (w < FR) {
+    row = w;
+    col = lane + 1;
+    ownlike = true;
+    if (w == FR - 1) {  // y+1 row
+      hslot = true, hrow = FR, hcol = col, hc0 = 0, hdx = lane, hdy = FR;
+    }
+  } else {
+    row = lane + 1;
+    col = 0;
+    ownlike = lane < FOWN;
+    if (lane >= 16 && lane < 16 + FR) {  // x+64 column
+      hslot = true, hrow = lane - 16, hcol = FX + 1, hc0 = 1, hdx = FX, hdy = lane - 16;
+    } else if (lane == 31) {  // E(x0-1, y0+FR)
+      hslot = true, hrow = FR, hcol = 0, hc0 = 0, hdx = -1, hdy = FR;
+    }
+  }
+  // (no lambda below refers to `a`: a closure holding its address makes the compiler
+  // copy the whole argument block to scratch)
+  const int N0 = a.N[0], N1 = a.N[1];
+  const long long st1 = a.st1;
+  const int ox = (w < FR) ? lane : -1;
+  const int gx = x0 + ox, gy = y0 + row;
+  const bool inA = ownlike && gx >= 0 && gx < N0 && gy >= 0 && gy < N1;
+  const unsigned cb = (unsigned)((gx + (long long)gy * st1) * 8);
+  const unsigned cbl = inA ? cb : 0u;
+  // per-axis ownership (within G): bit0 = components shifted along the axis, bit1 = unshifted
+  const unsigned ownx = own_bits_of(gx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
+  const unsigned owny = own_bits_of(gy, a.osh_lo[1], a.osh_hi[1], a.oun_lo[1], a.oun_hi[1]);
+  const int zsl = a.osh_lo[2], zsh = a.osh_hi[2], zul = a.oun_lo[2], zuh = a.oun_hi[2];
+  auto own_e = [](int c, unsigned ox_, unsigned oy_, unsigned oz_) {
+    return ((c == 0 ? ox_ : ox_ >> 1) & (c == 1 ? oy_ : oy_ >> 1) & (c == 2 ? oz_ : oz_ >> 1) & 1u) != 0;
+  };
+  auto own_b = [](int c, unsigned ox_, unsigned oy_, unsigned oz_) {
+    return ((c == 0 ? ox_ >> 1 : ox_) & (c == 1 ? oy_ >> 1 : oy_) & (c == 2 ? oz_ >> 1 : oz_) & 1u) != 0;
+  };
+  const bool stl = ownlike && w < FR && row >= 1 && gx <= it.x1 && gy <= it.y1;
+  const int hx = x0 + hdx, hy = y0 + hdy;
+  const bool hA = hslot && hx >= 0 && hx < N0 && hy >= 0 && hy < N1;
+  const unsigned hbl = hA ? (unsigned)((hx + (long long)hy * st1) * 8) : cbl;
+  const unsigned hownx = own_bits_of(hx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
+  const unsigned howny = own_bits_of(hy, a.osh_lo[1], a.osh_hi[1], a.oun_lo[1], a.oun_hi[1]);
+  const int zmax = a.N[2] - 1;
+#define zc(z) min(max((z), 0), zmax)
+#define ownz_of(z) own_bits_of((z), zsl, zsh, zul, zuh)
+  const unsigned s2 = (unsigned)(a.st2 * 8);
+  const double C = a.C;
+  const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
+  // buffer descriptors of the PML state (null arrays: every access out of range)
+  const __amdgpu_buffer_rsrc_t rBn0 = brsrc(a.Bn[0], nrec), rBn1 = brsrc(a.Bn[1], nrec),
+                               rBn2 = brsrc(a.Bn[2], nrec);
+  const __amdgpu_buffer_rsrc_t rDn0 = brsrc(a.Dn[0], nrec), rDn1 = brsrc(a.Dn[1], nrec),
+                               rDn2 = brsrc(a.Dn[2], nrec);
+  const __amdgpu_buffer_rsrc_t rEo0 = brsrc(a.E[0], nrec), rEo1 = brsrc(a.E[1], nrec),
+                               rEo2 = brsrc(a.E[2], nrec);
+  const __amdgpu_buffer_rsrc_t rEn0 = brsrc(a.En[0], nrec), rEn1 = brsrc(a.En[1], nrec),
+                               rEn2 = brsrc(a.En[2], nrec);
+  const __amdgpu_buffer_rsrc_t rUBo0 = brsrc(a.UBo[0], nrec), rUBo1 = brsrc(a.UBo[1], nrec),
+                               rUBo2 = brsrc(a.UBo[2], nrec);
+  const __amdgpu_buffer_rsrc_t rUBn0 = brsrc(a.UBn[0], nrec), rUBn1 = brsrc(a.UBn[1], nrec),
+                               rUBn2 = brsrc(a.UBn[2], nrec);
+  const __amdgpu_buffer_rsrc_t rHo0 = brsrc(a.Ho[0], nrec), rHo1 = brsrc(a.Ho[1], nrec),
+                               rHo2 = brsrc(a.Ho[2], nrec);
+  const __amdgpu_buffer_rsrc_t rHn0 = brsrc(a.Hn[0], nrec), rHn1 = brsrc(a.Hn[1], nrec),
+                               rHn2 = brsrc(a.Hn[2], nrec);
+  const __amdgpu_buffer_rsrc_t rUD0 = brsrc(a.UD[0], nrec), rUD1 = brsrc(a.UD[1], nrec),
+                               rUD2 = brsrc(a.UD[2], nrec);
+  // array pointers as scalars (a per-lane choice between two entries of a local
+  // pointer array makes the array, and with it the kernel arguments, a scratch copy)
+  const gdp D0 = sgpr_ptr(a.Do[0]), D1 = sgpr_ptr(a.Do[1]), D2 = sgpr_ptr(a.Do[2]);
+  const gdp E0 = sgpr_ptr(a.E[0]), E1 = sgpr_ptr(a.E[1]), E2 = sgpr_ptr(a.E[2]);
+  const gdp B0 = sgpr_ptr(a.Bo[0]), B1 = sgpr_ptr(a.Bo[1]), B2 = sgpr_ptr(a.Bo[2]);
+  const gdp U0 = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[0]) : nullptr;
+  const gdp U1 = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[1]) : nullptr;
+  const gdp U2 = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[2]) : nullptr;
+  const gup uix = (gup)sgpr_ptr(a.uidx);
+  // halo-slot sources (per lane)
+  const gdp hE0 = hc0 ? E1 : E0, hD0 = hc0 ? D1 : D0, hU0 = hc0 ? U1 : U0;
+#define pu(ui, c) sU[UMODE == 2 ? (c) : 0][((ui) >> (8 * (c))) & 255]
+  const bool uni = __builtin_amdgcn_readfirstlane(uw) != ~0u;
+  const unsigned ufix = (unsigned)((max(x0 - 1, 0) + (long long)max(y0, 0) * st1 +
+                                    (long long)max(zs - 1, 0) * a.st2) * 4);
+#define uoff(o8) (uni ? ufix : ((o8) >> 1))
+  __syncthreads();  // tables visible
+  // table accessors: direction d at this lane (x: column, y: row, z: plane position)
+  const int px = col, py = row;
+#define T(d, coef, sft, pz) \
+  (((AX >> (d)) & 1) ? P.v[d][coef][sft][(d) == 0 ? px : ((d) == 1 ? py : (pz))] : 1.0)
+#define F(d, sft, pz) \
+  (((AX >> (d)) & 1) ? P.f[d][sft][(d) == 0 ? px : ((d) == 1 ? py : (pz))] != 0 : false)
+  // W flags (PML chunk along the E component's own direction, shifted coordinate)
+  const bool Wx = F(0, 1, 0), Wy = F(1, 1, 0);
+#define Wz(pz) F(2, 1, pz)
+  const bool hW0 = hc0 == 0 ? (PX && P.f[0][1][hdx + 1] != 0) : (PY && P.f[1][1][hdy] != 0);
+
+  struct PBatch {  // plane k: D(k+1) (or stored E where not owned), u(k+1), B(k),
+                   // stored E(k+1) of W-form components, halo E(k)
+    double d0, d1, d2, u0, u1, u2, b0, b1, b2, es0, es1, es2, h0, h1, hu0, hu1;
+    unsigned ui, hui;
+  };
+#define PML_LOAD(QQ, KK) \
+  do { \
+    const int z1 = zc(KK + 1); \
+    const unsigned o = cbl + (unsigned)z1 * s2; \
+    const unsigned oz1 = ownz_of(KK + 1); \
+    const int pz1 = KK + 1 - zlo; \
+    const bool o0 = inA && own_e(0, ownx, owny, oz1), o1 = inA && own_e(1, ownx, owny, oz1), \
+               o2 = inA && own_e(2, ownx, owny, oz1); \
+    QQ.d0 = ldg(o0 ? D0 : E0, o); \
+    QQ.d1 = ldg(o1 ? D1 : E1, o); \
+    QQ.d2 = ldg(o2 ? D2 : E2, o); \
+    if (UMODE == 2) { \
+      QQ.ui = ldu(uix, uoff(o)); \
+    } else if (HAS_U) { \
+      QQ.u0 = ldg(U0, o); \
+      QQ.u1 = ldg(U1, o); \
+      QQ.u2 = ldg(U2, o); \
+    } else { \
+      QQ.u0 = QQ.u1 = QQ.u2 = 1.0; \
+    } \
+    QQ.es0 = QQ.es1 = QQ.es2 = 0.0; \
+    if (PX) QQ.es0 = bld(rEo0, (o0 && Wx) ? o : MNL_OOB); \
+    if (PY) QQ.es1 = bld(rEo1, (o1 && Wy) ? o : MNL_OOB); \
+    if (PZ) QQ.es2 = bld(rEo2, (o2 && Wz(pz1)) ? o : MNL_OOB); \
+    const unsigned ob = cbl + (unsigned)zc(KK) * s2; \
+    QQ.b0 = ldg(B0, ob); \
+    QQ.b1 = ldg(B1, ob); \
+    QQ.b2 = ldg(B2, ob); \
+    QQ.h0 = QQ.h1 = 0.0; \
+    QQ.hu0 = QQ.hu1 = 1.0; \
+    QQ.hui = 0; \
+    if (hwave) { \
+      const unsigned oh = hbl + (unsigned)zc(KK) * s2; \
+      const unsigned oz = ownz_of(KK); \
+      const bool i0 = hA && own_e(hc0, hownx, howny, oz) && !hW0; \
+      const bool i2 = hA && own_e(2, hownx, howny, oz) && !Wz(KK - zlo); \
+      QQ.h0 = ldg(i0 ? hD0 : hE0, oh); \
+      QQ.h1 = ldg(i2 ? D2 : E2, oh); \
+      if (UMODE == 2) { \
+        QQ.hui = ldu(uix, uoff(oh)); \
+      } else if (HAS_U) { \
+        QQ.hu0 = ldg(hU0, oh); \
+        QQ.hu1 = ldg(U2, oh); \
+      } \
+    } \
+  } while (0)
+
+  // prologue: E_old(zs-1): implicit (chi1inv * D) where owned and not W-form, else stored
+  double ex, ey, ez;
+  {
+    const int z = zlo;
+    const unsigned o = cbl + (unsigned)zc(z) * s2;
+    const unsigned oz = ownz_of(z);
+    const bool i0 = inA && own_e(0, ownx, owny, oz) && !Wx,
+               i1 = inA && own_e(1, ownx, owny, oz) && !Wy,
+               i2 = inA && own_e(2, ownx, owny, oz) && !Wz(0);
+    ex = ldg(i0 ? D0 : E0, o);
+    ey = ldg(i1 ? D1 : E1, o);
+    ez = ldg(i2 ? D2 : E2, o);
+    if (UMODE == 2) {
+      const unsigned ui = ldu(uix, uoff(o));
+      if (i0) ex *= pu(ui, 0);
+      if (i1) ey *= pu(ui, 1);
+      if (i2) ez *= pu(ui, 2);
+    } else if (HAS_U) {
+      if (i0) ex *= ldg(U0, o);
+      if (i1) ey *= ldg(U1, o);
+      if (i2) ez *= ldg(U2, o);
+    }
+  }
+  PBatch q[DIST + 1];
+#pragma unroll
+  for (int j = 0; j < DIST; j++) PML_LOAD(q[j], min(zs - 1 + j, ze - 1));
+  // f_u of B comp c: PML along cycle(c,2) (shifted); separate H: along c (unshifted);
+  // f_u of D comp c: along cycle(c,2) (unshifted; owner lanes only).  Plane KK's values
+  // are loaded at the end of iteration KK-1, so they land during its E / LDS phase.
+  double ub0 = 0, ub1 = 0, ub2 = 0, ho0 = 0, ho1 = 0, ho2 = 0, ud0 = 0, ud1 = 0, ud2 = 0;
+#define PML_AUX(KK) \
+  do { \
+    const int apz = (KK) - zlo; \
+    const unsigned aob = cbl + (unsigned)zc(KK) * s2; \
+    if (PZ) ub0 = bld(rUBo0, (inA && F(2, 1, apz)) ? aob : MNL_OOB); \
+    if (PX) ub1 = bld(rUBo1, (inA && F(0, 1, apz)) ? aob : MNL_OOB); \
+    if (PY) ub2 = bld(rUBo2, (inA && F(1, 1, apz)) ? aob : MNL_OOB); \
+    if (PX) ho0 = bld(rHo0, (inA && F(0, 0, apz)) ? aob : MNL_OOB); \
+    if (PY) ho1 = bld(rHo1, (inA && F(1, 0, apz)) ? aob : MNL_OOB); \
+    if (PZ) ho2 = bld(rHo2, (inA && F(2, 0, apz)) ? aob : MNL_OOB); \
+    if (PZ) ud0 = bld(rUD0, (stl && F(2, 0, apz)) ? aob : MNL_OOB); \
+    if (PX) ud1 = bld(rUD1, (stl && F(0, 0, apz)) ? aob : MNL_OOB); \
+    if (PY) ud2 = bld(rUD2, (stl && F(1, 0, apz)) ? aob : MNL_OOB); \
+  } while (0)
+  PML_AUX(zs - 1);
+  double dx = 0, dy = 0, dz = 0, hmx = 0, hmy = 0;
+  unsigned uik = 0;                  // palette word of plane k (UMODE 2)
+  double uk0 = 1, uk1 = 1, uk2 = 1;  // chi1inv of plane k (UMODE 1)
+  const int rowm = row > 0 ? row - 1 : 0, colm = col > 0 ? col - 1 : 0;
+  const int ngrp = (ze - zs + 1 + DIST) / (DIST + 1);
+  for (int g = 0; g < ngrp; g++) {
+#pragma unroll
+    for (int j = 0; j <= DIST; j++) {
+      const int k = zs - 1 + g * (DIST + 1) + j;
+      PML_LOAD(q[(j + DIST) % (DIST + 1)], min(k + DIST, ze - 1));
+      const PBatch &c = q[j];
+      const int pz = k - zlo, pz1 = pz + 1;
+      const unsigned oz = ownz_of(k), oz1 = ownz_of(k + 1);
+      // PML state of plane k: loaded at the end of the previous iteration (PML_AUX)
+      const bool fxs = F(0, 1, pz), fys = F(1, 1, pz), fzs = F(2, 1, pz);
+      const bool fxu = F(0, 0, pz), fyu = F(1, 0, pz), fzu = F(2, 0, pz);
+      const bool kin = k >= zs && k < ze;
+      const bool sk = stl && kin;
+      const unsigned ok = cb + (unsigned)k * s2;
+      // E_old(k+1) of this lane
+      double e1x, e1y, e1z;
+      {
+        const bool o0 = inA && own_e(0, ownx, owny, oz1), o1 = inA && own_e(1, ownx, owny, oz1),
+                   o2 = inA && own_e(2, ownx, owny, oz1);
+        double v0 = c.d0, v1 = c.d1, v2 = c.d2;
+        if (UMODE == 2) {
+          v0 = v0 * pu(c.ui, 0);
+          v1 = v1 * pu(c.ui, 1);
+          v2 = v2 * pu(c.ui, 2);
+        } else if (HAS_U) {
+          v0 = v0 * c.u0;
+          v1 = v1 * c.u1;
+          v2 = v2 * c.u2;
+        }
+        e1x = o0 ? ((PX && Wx) ? c.es0 : v0) : c.d0;
+        e1y = o1 ? ((PY && Wy) ? c.es1 : v1) : c.d1;
+        e1z = o2 ? ((PZ && Wz(pz1)) ? c.es2 : v2) : c.d2;
+      }
+      if (ownlike) {
+        sE[0][row][col] = ex;
+        sE[1][row][col] = ey;
+        sE[2][row][col] = ez;
+      }
+      if (hslot) {
+        const bool i0 = hA && own_e(hc0, hownx, howny, oz) && !hW0;
+        const bool i2 = hA && own_e(2, hownx, howny, oz) && !Wz(pz);
+        double h0 = c.h0, h1 = c.h1;
+        if (UMODE == 2) {
+          if (i0) h0 = h0 * pu(c.hui, hc0);
+          if (i2) h1 = h1 * pu(c.hui, 2);
+        } else if (HAS_U) {
+          if (i0) h0 = h0 * c.hu0;
+          if (i2) h1 = h1 * c.hu1;
+        }
+        sE[hc0][hrow][hcol] = h0;
+        sE[2][hrow][hcol] = h1;
+      }
+      __syncthreads();
+      // ---- curl B (E_old) with the PML branches of step_curl, then H (update_eh)
+      const double Ez_yp = sE[2][row + 1][col], Ex_yp = sE[0][row + 1][col];
+      const double Ey_xp = sE[1][row][col + 1], Ez_xp = sE[2][row][col + 1];
+      double ubx, uby, ubz;
+      const double Bx = pml_curl(c.b0, ub0, Ez_yp - ez + ey - e1y, C, fzs, T(1, 0, 1, pz),
+                                 T(1, 1, 1, pz), T(2, 0, 1, pz), T(2, 1, 1, pz), &ubx);
+      const double By = pml_curl(c.b1, ub1, e1x - ex + ez - Ez_xp, C, fxs, T(2, 0, 1, pz),
+                                 T(2, 1, 1, pz), T(0, 0, 1, pz), T(0, 1, 1, pz), &uby);
+      const double Bz = pml_curl(c.b2, ub2, Ey_xp - ey + ex - Ex_yp, C, fys, T(0, 0, 1, pz),
+                                 T(0, 1, 1, pz), T(1, 0, 1, pz), T(1, 1, 1, pz), &ubz);
+      const double Hx = fxu ? ho0 + (T(0, 2, 0, pz) * Bx - T(0, 0, 0, pz) * c.b0) : Bx;
+      const double Hy = fyu ? ho1 + (T(1, 2, 0, pz) * By - T(1, 0, 0, pz) * c.b1) : By;
+      const double Hz = fzu ? ho2 + (T(2, 2, 0, pz) * Bz - T(2, 0, 0, pz) * c.b2) : Bz;
+      {
+        const unsigned b0 = (sk && own_b(0, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned b1 = (sk && own_b(1, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned b2 = (sk && own_b(2, ownx, owny, oz)) ? ok : MNL_OOB;
+        bst(rBn0, b0, Bx);
+        bst(rBn1, b1, By);
+        bst(rBn2, b2, Bz);
+        if (PZ) bst(rUBn0, fzs ? b0 : MNL_OOB, ubx);
+        if (PX) bst(rUBn1, fxs ? b1 : MNL_OOB, uby);
+        if (PY) bst(rUBn2, fys ? b2 : MNL_OOB, ubz);
+        if (PX) bst(rHn0, fxu ? b0 : MNL_OOB, Hx);
+        if (PY) bst(rHn1, fyu ? b1 : MNL_OOB, Hy);
+        if (PZ) bst(rHn2, fzu ? b2 : MNL_OOB, Hz);
+      }
+      if (ownlike) {
+        sB[0][row][col] = Hx;
+        sB[1][row][col] = Hy;
+        sB[2][row][col] = Hz;
+      }
+      __syncthreads();
+      // ---- curl D (H_new) with the PML branches, then E in the W form where PML
+      // lies along its direction (src/step_generic.cpp:576-600: W_E(old) == chi1inv * D_old)
+      const double Hz_ym = sB[2][rowm][col], Hx_ym = sB[0][rowm][col];
+      const double Hz_xm = sB[2][row][colm], Hy_xm = sB[1][row][colm];
+      double udx, udy, udz;
+      const double Dx = pml_curl(dx, ud0, Hz_ym - Hz + Hy - hmy, C, fzu, T(1, 0, 0, pz),
+                                 T(1, 1, 0, pz), T(2, 0, 0, pz), T(2, 1, 0, pz), &udx);
+      const double Dy = pml_curl(dy, ud1, hmx - Hx + Hz - Hz_xm, C, fxu, T(2, 0, 0, pz),
+                                 T(2, 1, 0, pz), T(0, 0, 0, pz), T(0, 1, 0, pz), &udy);
+      const double Dz = pml_curl(dz, ud2, Hy_xm - Hy + Hx - Hx_ym, C, fyu, T(0, 0, 0, pz),
+                                 T(0, 1, 0, pz), T(1, 0, 0, pz), T(1, 1, 0, pz), &udz);
+      {
+        const unsigned e0 = (sk && own_e(0, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned e1 = (sk && own_e(1, ownx, owny, oz)) ? ok : MNL_OOB;
+        const unsigned e2 = (sk && own_e(2, ownx, owny, oz)) ? ok : MNL_OOB;
+        bst(rDn0, e0, Dx);
+        bst(rDn1, e1, Dy);
+        bst(rDn2, e2, Dz);
+        if (PZ) bst(rUD0, fzu ? e0 : MNL_OOB, udx);
+        if (PX) bst(rUD1, fxu ? e1 : MNL_OOB, udy);
+        if (PY) bst(rUD2, fyu ? e2 : MNL_OOB, udz);
+        double k0 = 1, k1 = 1, k2 = 1;
+        if (UMODE == 2) {
+          k0 = pu(uik, 0), k1 = pu(uik, 1), k2 = pu(uik, 2);
+        } else if (HAS_U) {
+          k0 = uk0, k1 = uk1, k2 = uk2;
+        }
+        if (PX) {
+          const double fw = HAS_U ? Dx * k0 : Dx, fp = HAS_U ? dx * k0 : dx;
+          bst(rEn0, fxs ? e0 : MNL_OOB, ex + (T(0, 2, 1, pz) * fw - T(0, 0, 1, pz) * fp));
+        }
+        if (PY) {
+          const double fw = HAS_U ? Dy * k1 : Dy, fp = HAS_U ? dy * k1 : dy;
+          bst(rEn1, fys ? e1 : MNL_OOB, ey + (T(1, 2, 1, pz) * fw - T(1, 0, 1, pz) * fp));
+        }
+        if (PZ) {
+          const double fw = HAS_U ? Dz * k2 : Dz, fp = HAS_U ? dz * k2 : dz;
+          bst(rEn2, fzs ? e2 : MNL_OOB, ez + (T(2, 2, 1, pz) * fw - T(2, 0, 1, pz) * fp));
+        }
+      }
+      hmx = Hx;
+      hmy = Hy;
+      dx = c.d0;
+      dy = c.d1;
+      dz = c.d2;
+      if (UMODE == 2) {
+        uik = c.ui;
+      } else if (HAS_U) {
+        uk0 = c.u0, uk1 = c.u1, uk2 = c.u2;
+      }
+      ex = e1x;
+      ey = e1y;
+      ez = e1z;
+      PML_AUX(min(k + 1, ze - 1));
+    }
+  }
+}
+#undef PML_AUX
+#undef PML_LOAD
+#undef pu
+#undef uoff
+#undef zc
+#undef ownz_of
+#undef T
+#undef F
+#undef Wz
+
+// body codes of tile items (bits 24-26): 0 lean, 1..7 pml_body<AX = 1, 2, 4, 0, 7, 3, 5>
+// (y-z edges, AX = 6, are few: they take the AX = 7 body)
+template <int UMODE, int DIST>
+__global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
+  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
+  __shared__ double sE[3][FR + 1][FX + 2];
+  __shared__ double sB[3][FR][FX + 1];
+  __shared__ PTabL sP;
+  __shared__ int s_item;
+  __shared__ unsigned s_uw;
+  if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
+    for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
+  }
+  const long long n = a.gend - a.gbeg;
+  unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
+      s_item = (long long)v < n ? a.titems[a.gbeg + v] : -1;
+      s_uw = ((long long)v < n && UMODE == 2 && a.tflag) ? a.tflag[a.gbeg + v] : ~0u;
+    }
+    __syncthreads();  // also separates LDS use of consecutive items
+    const int item = s_item;
+    const unsigned uw = s_uw;
+    if (item == -1) break;
+    const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
+    ItemGeo itg;
+    itg.x0 = a.xb[tx];
+    itg.x1 = a.xb[tx + 1] - 1;
+    itg.y0 = a.yb[ty] - 1;
+    itg.y1 = a.yb[ty + 1] - 1;
+    itg.zs = a.zb[ch];
+    itg.ze = a.zb[ch + 1];
+#ifndef MNL_TILE_BODIES
+#define MNL_TILE_BODIES 255  // register-budget experiments: compile a subset of the bodies
+#endif
+    switch ((item >> 24) & 7) {
+      case 0:
+        if (MNL_TILE_BODIES & 1) lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
+        break;
+      case 1:
+        if (MNL_TILE_BODIES & 2) pml_body<UMODE, DIST, 1>(a, itg, uw, sU, sE, sB, sP);
+        break;
+      case 2:
+        if (MNL_TILE_BODIES & 4) pml_body<UMODE, DIST, 2>(a, itg, uw, sU, sE, sB, sP);
+        break;
+      case 3:
+        if (MNL_TILE_BODIES & 8) pml_body<UMODE, DIST, 4>(a, itg, uw, sU, sE, sB, sP);
+        break;
+      case 4:
+        if (MNL_TILE_BODIES & 16) pml_body<UMODE, DIST, 0>(a, itg, uw, sU, sE, sB, sP);
+        break;
+      case 5:
+        if (MNL_TILE_BODIES & 32) pml_body<UMODE, DIST, 7>(a, itg, uw, sU, sE, sB, sP);
+        break;
+      case 6:
+        if (MNL_TILE_BODIES & 64) pml_body<UMODE, DIST, 3>(a, itg, uw, sU, sE, sB, sP);
+        break;
+      default:
+        if (MNL_TILE_BODIES & 128) pml_body<UMODE, DIST, 5>(a, itg, uw, sU, sE, sB, sP);
+        break;
+    }
+  }
+}
+
+// Lean tiles only (the original two-launch fused step: this kernel, then
+// fused_general_kernel over the PML / boundary tiles; MNL_TILE=0).  Work queues,
+// chunk-major: consecutive items are neighbouring tiles of one chunk, so the
+// workgroups sweep z roughly together.  With ngrp = 8 the workgroups sharing an XCD
+// (blockIdx % 8, observed round-robin placement; speed only) own a contiguous range of
+// each chunk's tiles (x fastest), so the halo lines neighbouring tiles share are
+// fetched once into that XCD's L2.
+template <int UMODE, int DIST>
+__global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
+  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
+  __shared__ double sE[3][FR + 1][FX + 2];
+  __shared__ double sB[3][FR][FX + 1];
+  __shared__ long long s_item;
+  if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
+    for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
+  }
+  int nlch = 0;
+  for (int r = 0; r < a.nlzr; r++) nlch += a.lzr[r][1] - a.lzr[r][0] + 1;
+  const int nlx = a.lx1 - a.lx0 + 1;
+  const long long ntile = (long long)nlx * (a.ly1 - a.ly0 + 1);
+  const int grp = a.ngrp > 1 ? (int)(blockIdx.x % a.ngrp) : 0;
+  const long long gt0 = ntile * grp / a.ngrp, gt1 = ntile * (grp + 1) / a.ngrp;
+  const long long gtile = gt1 - gt0;
+  unsigned long long *gctr = a.ctr + 16 * grp;
+  const unsigned long long gbase = a.ngrp > 1 ? a.cbg[grp] : a.cbase;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = atomicAdd(gctr, 1ULL) - gbase;
+      s_item = (long long)v < gtile * nlch ? (long long)v : -1;
+    }
+    __syncthreads();  // also separates LDS use of consecutive items
+    const long long item = s_item;
+    if (item < 0) break;
+    int ch = (int)(item / gtile);  // lean chunk ordinal -> chunk index
+    for (int r = 0; r < a.nlzr; r++) {
+      const int n = a.lzr[r][1] - a.lzr[r][0] + 1;
+      if (ch < n) {
+        ch += a.lzr[r][0];
+        break;
+      }
+      ch -= n;
+    }
+    const int tile = (int)(gt0 + item % gtile);
+    const int tx = a.lx0 + tile % nlx, ty = a.ly0 + tile / nlx;
+    ItemGeo itg;
+    itg.x0 = a.xb[tx];
+    itg.x1 = a.xb[tx + 1] - 1;
+    itg.y0 = a.yb[ty] - 1;
+    itg.y1 = a.yb[ty + 1] - 1;
+    itg.zs = a.zb[ch];
+    itg.ze = a.zb[ch + 1];
+    const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[(long long)tile * a.nch + ch] : ~0u;
+    lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
   }
 }
 
@@ -2616,10 +3128,73 @@ int k_general_uniform(const FusedArgs &a, unsigned *flags, void *stream) {
   return rc();
 }
 
+// Per tile item (index in titems): the palette word if every cell of its footprint
+// (columns x0-1 .. x0+FX, rows y0 .. y0+FR, planes zs-1 .. ze) inside G has the same
+// word, else ~0u (chi1inv is used only at owned points of G).
+__global__ void tile_uniform_kernel(FusedArgs a, unsigned *flags) {
+  const int idx = blockIdx.x;
+  const int item = a.titems[idx];
+  const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
+  const int x0 = max(a.xb[tx] - 1, a.G.lo[0]), x1 = min(a.xb[tx] + FX, a.G.hi[0]);
+  const int y0 = max(a.yb[ty] - 1, a.G.lo[1]), y1 = min(a.yb[ty] - 1 + FR, a.G.hi[1]);
+  const int z0 = max(a.zb[ch] - 1, a.G.lo[2]), z1 = min(a.zb[ch + 1], a.G.hi[2]);
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const long long nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
+  unsigned ref = 0;
+  if (nx > 0 && ny > 0 && nz > 0) {
+    ref = a.uidx[x0 + (long long)y0 * a.st1 + (long long)z0 * a.st2];
+    for (long long i = threadIdx.x; i < nx * ny * nz; i += blockDim.x) {
+      const long long x = x0 + i % nx, y = y0 + (i / nx) % ny, z = z0 + i / (nx * ny);
+      if (a.uidx[x + y * a.st1 + z * a.st2] != ref) bad = 1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) flags[idx] = bad ? ~0u : ref;
+}
+
+int k_tile_uniform(const FusedArgs &a, unsigned *flags, void *stream) {
+  if (a.ntit <= 0 || !a.uidx || !a.titems) return 0;
+  tile_uniform_kernel<<<a.ntit, 256, 0, (hipStream_t)stream>>>(a, flags);
+  return rc();
+}
+
 int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bases) {
   for (int d = 0; d < 3; d++)
     if (a.G.hi[d] < a.G.lo[d]) return 0;
   if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr) return 2;  // host guarantees < 4 GiB arrays
+  if (which >= 4) {  // tile kernel: 4 all items, 5 the chunk-0 items, 6 the others
+    if (a.nx < 1 || a.nx > FUSED_MAXX || a.ny < 1 || a.ny > FUSED_MAXY || a.nch < 1 ||
+        a.nch > FUSED_MAXZ)
+      return 3;
+    for (int t = 0; t < a.nx; t++)  // tiles at most 64 columns wide, 128-byte aligned
+      if (a.xb[t + 1] - a.xb[t] > FX || a.xb[t + 1] <= a.xb[t] || (a.xb[t] & 15)) return 4;
+    for (int t = 0; t < a.ny; t++)
+      if (a.yb[t + 1] - a.yb[t] > FOWN || a.yb[t + 1] <= a.yb[t]) return 5;
+    for (int t = 0; t < a.nch; t++)
+      if (a.zb[t + 1] <= a.zb[t] || a.zb[t + 1] - a.zb[t] > FUSED_MAXCH) return 7;
+    int ib = 0, ie = a.ntit, line = 0;
+    if (which == 5) ie = a.ntit_e, line = 1;
+    if (which == 6) ib = a.ntit_e, line = 2;
+    if (ie <= ib) return 0;
+    long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
+    if (a.wg_limit > 0 && nb > a.wg_limit) nb = a.wg_limit;
+    if (nb > ie - ib) nb = ie - ib;
+    FusedArgs t = a;
+    t.gbeg = ib, t.gend = ie, t.ctr_line = line, t.cbase = bases[line];
+    bases[line] += (unsigned long long)(ie - ib) + nb;
+    const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grd((unsigned)nb), blk(1024);
+    if (um == 2)
+      fused_tile_kernel<2, 1><<<grd, blk, 0, s>>>(t);
+    else if (um == 1)
+      fused_tile_kernel<1, 1><<<grd, blk, 0, s>>>(t);
+    else
+      fused_tile_kernel<0, 1><<<grd, blk, 0, s>>>(t);
+    return hipPeekAtLastError() == hipSuccess ? 0 : 9;
+  }
   if (a.nx < 1 || a.nx > FUSED_MAXX || a.ny < 0 || a.ny > FUSED_MAXY || a.nch < 1 ||
       a.nch > FUSED_MAXZ || a.ngy < 1 || a.ngy > FUSED_MAXGY || a.nny < 0 || a.nny > FUSED_MAXNY)
     return 3;

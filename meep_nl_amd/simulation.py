@@ -642,11 +642,14 @@ def _progress(t0, t, dt):
 
 
 # ---------------------------------------------------------------- Simulation
+_WARNED_AVERAGING = False
+
+
 class Simulation:
     def __init__(self, cell_size, resolution, geometry=(), sources=(), boundary_layers=(),
                  default_material=Medium(), Courant=0.5, eps_averaging=True, dimensions=None,
                  force_complex_fields=False, k_point=False, symmetries=(), parallel=None,
-                 nonlinear_mode="fork", progress_interval=4, **kwargs):
+                 nonlinear_mode="fork", progress_interval=4, time_phases=True, **kwargs):
         self.cell_size = Vector3(*cell_size)
         self.resolution = float(resolution)
         self.geometry = list(geometry)
@@ -669,6 +672,10 @@ class Simulation:
         # extension; the fork's behaviour is the default)
         self.nonlinear_mode = nonlinear_mode
         self.progress_interval = progress_interval
+        # per-phase GPU times (HIP events) for print_times / time_spent_on; False skips
+        # the event records (bench.py --no-events measures their cost: about 0.3 % of a
+        # fused 512^3 step, profiles/README.md)
+        self.time_phases = bool(time_phases)
         self.run_index = 0
         self.fields = None
         self.structure = None
@@ -721,6 +728,16 @@ class Simulation:
         averaged = False
         if self.eps_averaging and not uniform and need_eps:
             if iso:
+                global _WARNED_AVERAGING
+                if not _WARNED_AVERAGING:
+                    _WARNED_AVERAGING = True
+                    warnings.warn(
+                        "eps_averaging: subpixel averaging follows the C++ core's "
+                        "material_function algorithm (src/anisotropic_averaging.cpp), not "
+                        "Python Meep's libctl averaging (meepgeom.cpp), so epsilon near "
+                        "interfaces differs from Python Meep at the averaging tolerance "
+                        "(parity unpinned: no reference value covers it, DESIGN.md section 22)",
+                        RuntimeWarning)
                 s.set_epsilon_geometry([g.geo_record(g.material.epsilon_diag.x)
                                         for g in self.geometry],
                                        default_eps=self.default_material.epsilon_diag.x,
@@ -812,7 +829,7 @@ class Simulation:
         else:
             self.fields = core.Fields(self.structure)
         # per-phase GPU times for print_times (HIP events; ~0.3 % of a step)
-        self.fields.set_profiling(True)
+        self.fields.set_profiling(self.time_phases)
         for src in self.sources:
             src.add_source(self.fields)
         if getattr(self, "load_fields_file", None):  # delayed load (python/simulation.py:2509-2510)

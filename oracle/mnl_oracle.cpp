@@ -49,8 +49,10 @@
 //
 // Random fallback of runNR (src/newton_raphson.cpp:331-336, attempts >= 14)
 // uses std::random_device in the reference (non-deterministic).  Here it is
-// replaced by a deterministic splitmix64 stream; attempts that reach it are
-// counted (orc_nr_failures) so tests can assert they never happen.
+// replaced by the product's deterministic stand-in: a splitmix64 stream seeded per
+// point and time step (nr_voxel_seed) and a log-uniform magnitude with a random sign
+// (det_random), so product and oracle draw the same seeds; attempts that reach it are
+// counted (orc_nr_failures).
 
 #include "mnl_oracle.h"
 
@@ -311,16 +313,33 @@ double det_random(NRState &st) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
   };
-  double u1 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-  double u2 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-  double u3 = ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-  double g = sqrt(-2.0 * log(u1)) * cos(2 * pi * u2);
-  return exp(1.0 + 90.0 * g) * (2.0 * u3 - 1.0);
+  // the product's stand-in (nr_random, mnl_kernels.hip): log-uniform magnitude over
+  // 2^-300 .. 2^300, random sign, exact operations only
+  const uint64_t r1 = next(), r2 = next(), r3 = next();
+  const int e = (int)(r1 % 601ull) - 300;
+  const double m = 1.0 + (double)(r2 >> 11) * (1.0 / 9007199254740992.0);
+  const double v = std::ldexp(m, e);
+  return (r3 >> 63) ? -v : v;
 }
-void runNR(NRState &st, realnum seed1, realnum seed2, realnum seed3, realnum *fw, realnum *fw_2,
-           realnum *fw_3, const Params &p1, const Params &p2, const Params &p3) {
+// Seed of the random fallback at one point: the product's counter-based value
+// (nr_voxel_seed, meep_nl_amd/csrc/mnl_internal.hpp) of the point's global
+// half-coordinates q (relative to the cell's little corner, 0 for absent directions),
+// the E component's direction d and the time step t, restated here.
+uint64_t nr_voxel_seed(long long q0, long long q1, long long q2, int d, long long t) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  h ^= (uint64_t)q0 * 0xBF58476D1CE4E5B9ull;
+  h ^= (uint64_t)q1 * 0x94D049BB133111EBull;
+  h ^= (uint64_t)q2 * 0xD6E8FEB86659FD93ull;
+  h ^= (uint64_t)d * 0x2545F4914F6CDD1Dull;
+  h ^= (uint64_t)t * 0x9FB21C651E98DF25ull;
+  return h;
+}
+
+void runNR(NRState &st, uint64_t seed, realnum seed1, realnum seed2, realnum seed3, realnum *fw,
+           realnum *fw_2, realnum *fw_3, const Params &p1, const Params &p2, const Params &p3) {
   // newton_raphson.cpp:209-359
   st.max_iterations = 250;
+  st.rng = seed;
   double tol1 = fmax(fabs(TOLERANCE * (*fw)) * 0.0001, TOLERANCE);
   double tol2 = fmax(fabs(TOLERANCE * (*fw_2)) * 0.0001, TOLERANCE);
   double tol3 = fmax(fabs(TOLERANCE * (*fw_3)) * 0.0001, TOLERANCE);
@@ -1099,8 +1118,12 @@ void step_update_EDHB(orc_sim *s, const GV &g, realnum *f, int fc, const realnum
   }
   if (u1 && u2 && chi3) {  // 3x3 with chi: Newton-Raphson branch (730-816)
     int cd = cdir(fc);
-    loop_owned(g, fc, [&](long i, const int *) {
+    loop_owned(g, fc, [&](long i, const int *pt) {
       NRState &st = s->nr[tid() % s->nr.size()];
+      long long q[3] = {0, 0, 0};
+      for (int e = 0; e < 3; e++)
+        if (s->gv.has[e]) q[e] = pt[e] - s->gv.io[e];
+      const uint64_t seed = nr_voxel_seed(q[0], q[1], q[2], cd, s->t);
       realnum gs = gg[i];
       realnum gs_2 = (g1[i] + g1[i + sd] + g1[i - s1] + g1[i + (sd - s1)]) * 0.25;
       realnum gs_3 = (g2[i] + g2[i + sd] + g2[i - s2] + g2[i + (sd - s2)]) * 0.25;
@@ -1120,17 +1143,17 @@ void step_update_EDHB(orc_sim *s, const GV &g, realnum *f, int fc, const realnum
         Params p1 = {gs, us, 0.0, 0.0, 0.0, chi2new, 0.0, 0.0};
         Params p2 = {gs_2, us_2, 0.0, 0.0, 0.0, 0.0, chi2new, 0.0};
         Params p3 = {gs_3, us_3, 0.0, 0.0, 0.0, 0.0, 0.0, chi2new};
-        runNR(st, f[i], gs_2 * u[i], gs_3 * u[i], &f[i], &dummyF1, &dummyF2, p1, p2, p3);
+        runNR(st, seed, f[i], gs_2 * u[i], gs_3 * u[i], &f[i], &dummyF1, &dummyF2, p1, p2, p3);
       } else if (cd == Y) {
         Params p1 = {gs_3, us_3, 0.0, 0.0, 0.0, chi2new, 0.0, 0.0};
         Params p2 = {gs, us, 0.0, 0.0, 0.0, 0.0, chi2new, 0.0};
         Params p3 = {gs_2, us_2, 0.0, 0.0, 0.0, 0.0, 0.0, chi2new};
-        runNR(st, gs_3 * u[i], f[i], gs_2 * u[i], &dummyF1, &f[i], &dummyF2, p1, p2, p3);
+        runNR(st, seed, gs_3 * u[i], f[i], gs_2 * u[i], &dummyF1, &f[i], &dummyF2, p1, p2, p3);
       } else {
         Params p1 = {gs_2, us_2, 0.0, 0.0, 0.0, chi2new, 0.0, 0.0};
         Params p2 = {gs_3, us_3, 0.0, 0.0, 0.0, 0.0, chi2new, 0.0};
         Params p3 = {gs, us, 0.0, 0.0, 0.0, 0.0, 0.0, chi2new};
-        runNR(st, gs_2 * u[i], gs_3 * u[i], f[i], &dummyF1, &dummyF1, &f[i], p1, p2, p3);
+        runNR(st, seed, gs_2 * u[i], gs_3 * u[i], f[i], &dummyF1, &dummyF1, &f[i], p1, p2, p3);
       }
     });
     return;

@@ -47,6 +47,8 @@ def run_case(name, make):
         o = S.sc_nr_isrc_seam(make)
     elif name == "averaged_up":
         o = S.sc_averaged(make, upstream=True)
+    elif name == "c5_small":
+        o = S.sc_c5_small(make)
     elif name == "flux":
         o, hs = S.sc_flux_3d(make, steps=40)
         for k, h in enumerate(hs):

@@ -340,6 +340,18 @@ def sc_vacuum_pml_3d(make, L=3.2, steps=60, dpml=1.0):
     return o
 
 
+def sc_c5_small(make, nranks=8, nxy=64, nz_per=16, steps=30):
+    """BASELINE configs[4] (C5) decomposition at reduced x-y: vacuum + PML(1.0) on a
+    nxy x nxy x (nz_per * nranks) grid at resolution 10 (C5 is 512 x 512 x (128 * 8)),
+    z-slab split over nranks ranks (the 10-plane z-PML lies on the end ranks only, the
+    interior ranks have two neighbours), Ez Gaussian current at the centre."""
+    o = vol(make, 3, [nxy / 10.0, nxy / 10.0, nz_per * nranks / 10.0], 10, center_origin=True)
+    o.add_pml(1.0)
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    o.step(steps)
+    return o
+
+
 def sc_waveguide_3d(make, L=3.2, steps=40, eps=12.0):
     """Config 3 shape scaled down: eps=12 core |y|,|z| < 0.5 along x, PML, no averaging."""
     o = vol(make, 3, [L, L, L], 10, center_origin=True)

@@ -24,6 +24,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 HERE = os.path.dirname(os.path.abspath(__file__))
 CASES2 = ["vacuum_pml", "big_box", "kerr_lorentz", "nr_dispersive", "nr_seam", "flux"]
 CASES3 = ["big_box", "flux", "averaged_up"]
+CASES8 = ["c5_small"]  # BASELINE C5's decomposition (8 z-slabs) at reduced x-y
 
 
 def _launch(nranks, cases, out):
@@ -50,7 +51,7 @@ def _launch(nranks, cases, out):
 @pytest.fixture(scope="module")
 def mp_runs(tmp_path_factory):
     out = {}
-    for n, cases in ((2, CASES2), (3, CASES3)):
+    for n, cases in ((2, CASES2), (3, CASES3), (8, CASES8)):
         d = tmp_path_factory.mktemp(f"mp{n}")
         _launch(n, cases, d)
         out[n] = d
@@ -74,6 +75,8 @@ def _oracle(name):
         return S.sc_nr_isrc_seam(make_oracle), {}
     if name == "averaged_up":
         return S.sc_averaged(make_oracle, upstream=True), {}
+    if name == "c5_small":
+        return S.sc_c5_small(make_oracle), {}
     o, hs = S.sc_flux_3d(make_oracle, steps=40)
     ex = {f"flux{k}": o.flux(h) for k, h in enumerate(hs)}
     ex["slice_plane"] = o.get_array_slice(2, [-1.6, -1.6, 0.3], [1.6, 1.6, 0.3])
@@ -82,7 +85,8 @@ def _oracle(name):
     return o, ex
 
 
-@pytest.mark.parametrize("nranks,name", [(2, c) for c in CASES2] + [(3, c) for c in CASES3])
+@pytest.mark.parametrize("nranks,name", [(2, c) for c in CASES2] + [(3, c) for c in CASES3] +
+                         [(8, c) for c in CASES8])
 def test_multiprocess_slabs_bitwise(mp_runs, nranks, name):
     ranks = _load(mp_runs[nranks], name, nranks)
     assert all(str(r["transport"]) == "ipc" for r in ranks)
