@@ -207,8 +207,8 @@ int mnl_fields_add_custom_point_source(mnl_fields *f, int comp, mnl_src_func fun
  * (afunc NULL: A = 1); zero-width directions scale amp by the resolution (J as
  * a delta function); a volume up to one pixel wider than the cell is clamped,
  * wider fails ("Source width > cell width").  kind / params as
- * mnl_fields_add_point_source (not CUSTOM).  Integrated (dipole) sources are
- * limited to 64 points per fields object. */
+ * mnl_fields_add_point_source (not CUSTOM).  Integrated (dipole) volume sources
+ * have no point limit (sorted device arrays, binary search per reader). */
 int mnl_fields_add_volume_source(mnl_fields *f, int comp, int kind, const double *params, int np,
                                  const double vmin[3], const double vmax[3], double amp_re,
                                  double amp_im, int is_integrated, mnl_amp_func afunc,
@@ -356,6 +356,22 @@ int mnl_fields_dft_size(mnl_fields *f, int handle, long long *n);
 int mnl_fields_dft_data(mnl_fields *f, int handle, int which, double *out, long long n);
 /* the decimation factor the object was created with */
 int mnl_fields_dft_decimation(mnl_fields *f, int handle, int *decimation);
+/* fields::add_dft_fields(components, ncomp, volume(vmin, vmax), freq, Nfreq,
+ * use_centered_grid = !yee_grid, decimation_factor) (src/dft.cpp:889-903; Python
+ * Simulation.add_dft_fields, python/simulation.py:2976-3036): E / H components
+ * (MNL_EX..MNL_HZ), accumulated on the device with the flux objects' kernels.
+ * *handle is shared with the flux handles (mnl_fields_dft_data, _decimation). */
+int mnl_fields_add_dft_fields(mnl_fields *f, int ncomp, const int *comps, const double vmin[3],
+                              const double vmax[3], const double *freqs, int nfreq, int yee_grid,
+                              int decimation, int *handle);
+/* fields::get_dft_array(dft_fields or dft_flux, c, num_freq) (src/dft.cpp:1240-1280,
+ * process_dft_component 908-1240, collapse_array src/array_slice.cpp:554-601): the
+ * complex DFT of component comp at frequency index num_freq over the object's volume,
+ * empty dimensions collapsed, summed over ranks.  *rank and dims[0..rank-1] (row-major,
+ * X before Y before Z); out (2*nout doubles, re/im interleaved) may be NULL to query the
+ * size.  rank 0 means the object holds no chunk of comp (no values). */
+int mnl_fields_dft_array(mnl_fields *f, int handle, int comp, int num_freq, int *rank,
+                         long long dims[3], double *out, long long nout);
 
 #ifdef __cplusplus
 }

@@ -7,7 +7,7 @@ Both call libmnl.so (HIP kernels for gfx950 + C-ABI, include/meep_nl_amd.h).
 from .core import (Bx, By, Bz, Dx, Dy, Dz, Ex, Ey, Ez, Fields, GridVolume, Hx, Hy, Hz,
                    Structure, X, Y, Z, device_count)
 from .simulation import (ALL, AUTOMATIC, Block, ContinuousSource, CustomSource, Cylinder,
-                         DftFlux, Sphere,
+                         DftFields, DftFlux, Sphere,
                          DrudeSusceptibility,
                          FluxRegion, GaussianSource, High, LorentzianSusceptibility, Low, Medium,
                          PML, Simulation, Source, Vector3, Volume, after_sources, after_time,

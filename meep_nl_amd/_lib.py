@@ -99,6 +99,10 @@ _SIGS = {
     "mnl_fields_dft_size": (c_int, [c_void, c_int, llptr]),
     "mnl_fields_dft_data": (c_int, [c_void, c_int, c_int, dptr, ctypes.c_longlong]),
     "mnl_fields_dft_decimation": (c_int, [c_void, c_int, iptr]),
+    "mnl_fields_add_dft_fields": (c_int, [c_void, c_int, iptr, dptr, dptr, dptr, c_int, c_int,
+                                          c_int, iptr]),
+    "mnl_fields_dft_array": (c_int, [c_void, c_int, c_int, c_int, iptr,
+                                     ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]),
 }
 
 

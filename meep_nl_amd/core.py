@@ -572,6 +572,39 @@ class Fields:
         check(lib().mnl_fields_dft_decimation(self.h, h, ctypes.byref(v)))
         return v.value
 
+    # -- DFT fields (fields::add_dft_fields / get_dft_array, src/dft.cpp:889-903, 1240-1280)
+    def add_dft_fields(self, comps, vmin, vmax, freqs, yee_grid=False, decimation=0):
+        """E / H components over [vmin, vmax] on the centered grid (or each
+        component's Yee grid); returns a handle (shared with the flux handles)."""
+        cs = np.ascontiguousarray(comps, dtype=np.int32)
+        lo = np.ascontiguousarray(vmin, dtype=np.float64)
+        hi = np.ascontiguousarray(vmax, dtype=np.float64)
+        f = np.ascontiguousarray(freqs, dtype=np.float64)
+        h = ctypes.c_int()
+        check(lib().mnl_fields_add_dft_fields(self.h, len(cs), cs.ctypes.data_as(
+            ctypes.POINTER(ctypes.c_int)), ptr(lo), ptr(hi), ptr(f), len(f), int(bool(yee_grid)),
+            int(decimation), ctypes.byref(h)))
+        self._dft_nf = getattr(self, "_dft_nf", {})
+        self._dft_nf[h.value] = len(f)
+        return h.value
+
+    def dft_array(self, h, comp, num_freq):
+        """fields::get_dft_array(obj, comp, num_freq) for flux and fields handles:
+        complex array over the object's volume, empty dimensions collapsed (an empty
+        array when the object holds no chunk of comp).  Collective on several ranks."""
+        rank = ctypes.c_int()
+        dims = (ctypes.c_longlong * 3)()
+        check(lib().mnl_fields_dft_array(self.h, h, comp, num_freq, ctypes.byref(rank), dims,
+                                         None, 0))
+        shape = tuple(dims[k] for k in range(rank.value))
+        n = int(np.prod(shape)) if rank.value else 0
+        out = np.zeros(2 * max(n, 1), dtype=np.float64)
+        check(lib().mnl_fields_dft_array(self.h, h, comp, num_freq, ctypes.byref(rank), dims,
+                                         ptr(out), n))
+        if not rank.value:
+            return np.zeros(0, dtype=np.complex128)
+        return (out[0:2 * n:2] + 1j * out[1:2 * n:2]).reshape(shape)
+
 
 class LocalHub:
     """In-process slab group (mnl_local_hub_create): several z-slabs of one grid on

@@ -180,10 +180,18 @@ struct DftChunkH {
   cplx scale;
   int avgmode;       // 0: point, 1: two Yee points, 2: four
   size_t N, p0;      // points, first point in the flux object's point arrays
+  // the chunk's loop (for get_dft_array): corners, boundary weights, dV0,
+  // include_dV_and_interp_weights, stored_weight
+  int is[3], ie[3];
+  double s0[3], s1[3], e0[3], e1[3], dV0;
+  bool incl;
+  cplx stored;
 };
 struct DftFluxH {
   std::vector<double> omega;
   int nfreq = 0, decim = 1;
+  bool fields = false;                // dft_fields (add_dft_fields): chunks in E only
+  double wmin[3] = {0, 0, 0}, wmax[3] = {0, 0, 0};  // `where` (get_dft_array's collapse)
   std::vector<DftChunkH> E, H;        // list order (next_in_dft)
   size_t npts = 0;                    // E points, then H points
   std::vector<int> h_pj;              // 3 local indices per point (-1: not this rank's)
@@ -1508,19 +1516,24 @@ std::vector<std::array<int, 6>> reference_chunks(const mnl_structure &S) {
   return out;
 }
 
-// fields::add_dft for component c over [wmin, wmax] on the centered grid: the
-// chunks loop_in_chunks creates, prepended to `list` (their points appended to
-// the flux object's point arrays)
+// fields::add_dft for component c over [wmin, wmax]: the chunks loop_in_chunks
+// creates, prepended to `list` (their points appended to the flux object's point
+// arrays).  Centered grid, or with yee the component's own grid (loop_in_chunks(...,
+// cgrid = c), src/loop_in_chunks.cpp:350-356: where shifted by yee_shift(Centered) -
+// yee_shift(c), rounded to the dielectric grid, shifted back by iyee_c).
 void dft_add(mnl_fields *F, DftFluxH &o, int c, const double wmin[3], const double wmax[3],
              bool incl, cplx stored_weight, double dt_factor, std::vector<DftChunkH> &list,
-             std::vector<double> &pw) {
+             std::vector<double> &pw, bool yee = false) {
   const mnl_structure &S = F->S;
   const DevGrid &g = F->g;
-  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0}, sh[3] = {1, 1, 1};
   for (int d = 0; d < 3; d++) {
     if (!S.has[d]) continue;
-    is[d] = 1 + 2 * int(floor(wmin[d] * S.a - .5));  // vec2diel_floor / ceil, equal_shift 0
-    ie[d] = 1 + 2 * int(ceil(wmax[d] * S.a - .5));
+    if (yee) sh[d] = S.shift(c, d);
+    const int iyc = 1 - sh[d];                                          // iyee_c
+    const double yc = 1 * (0.5 * (1.0 / S.a)) - sh[d] * (0.5 * (1.0 / S.a));  // yee_c
+    is[d] = 1 + 2 * int(floor((wmin[d] + yc) * S.a - .5)) - iyc;  // vec2diel_floor, equal_shift 0
+    ie[d] = 1 + 2 * int(ceil((wmax[d] + yc) * S.a - .5)) - iyc;
   }
   double s0[3], s1[3], e0[3], e1[3];
   dft_boundary_weights(S, wmin, wmax, is, ie, s0, e0, s1, e1);
@@ -1544,7 +1557,9 @@ void dft_add(mnl_fields *F, DftFluxH &o, int c, const double wmin[3], const doub
         isc[d] = iec[d] = 0;
         continue;
       }
-      const int uoc = S.io[d] + 1, coc = ch[d] + 1, cbo = ch[d] + 2 * ch[3 + d] - 1;
+      // little_owned_corner(cgrid) = io + 2 - iyee_shift, big_owned_corner = big - iyee_shift
+      const int uoc = S.io[d] + 2 - sh[d], coc = ch[d] + 2 - sh[d],
+                cbo = ch[d] + 2 * ch[3 + d] - sh[d];
       const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
       isc[d] = std::max(is[d], iscoS);
       iec[d] = std::min(ie[d], iecoS);
@@ -1583,8 +1598,15 @@ void dft_add(mnl_fields *F, DftFluxH &o, int c, const double wmin[3], const doub
     dc.scale = stored_weight * cplx(1.0) * dt_factor;
     int nun = 0;
     for (int d = 0; d < 3; d++)
-      if (S.has[d] && !S.shift(c, d)) nun++;
+      if (!yee && S.has[d] && !S.shift(c, d)) nun++;
     dc.avgmode = nun;
+    for (int d = 0; d < 3; d++) {
+      dc.is[d] = isc[d], dc.ie[d] = iec[d];
+      dc.s0[d] = s0c[d], dc.s1[d] = s1c[d], dc.e0[d] = e0c[d], dc.e1[d] = e1c[d];
+    }
+    dc.dV0 = dV0;
+    dc.incl = incl;
+    dc.stored = stored_weight;
     long ln[3];
     for (int k = 0; k < 3; k++) ln[k] = S.has[yd[k]] ? (iec[yd[k]] - isc[yd[k]]) / 2 + 1 : 1;
     dc.N = size_t(ln[0] * ln[1] * ln[2]);
@@ -1617,6 +1639,12 @@ void dft_add(mnl_fields *F, DftFluxH &o, int c, const double wmin[3], const doub
           bool mine = true;
           for (int d = 0; d < 3; d++) {
             if (!S.has[d]) continue;
+            if (yee) {  // the Yee point itself; owned along d by one rank (walls included)
+              j[d] = (p[d] - S.io[d] - sh[d]) / 2 - g.off[d];
+              const int nloc = g.N[g.ax[d]] - 1;  // this rank's cells along d
+              if (sh[d] ? (j[d] < 0 || j[d] > nloc - 1) : (j[d] < 1 || j[d] > nloc)) mine = false;
+              continue;
+            }
             const int base = p[d] - (S.shift(c, d) ? 0 : 1);  // Yee point of c at/below p
             j[d] = (base - S.io[d] - S.shift(c, d)) / 2 - g.off[d];
             const int jc = (p[d] - S.io[d] - 1) / 2 - g.off[d];  // centered index
@@ -1632,58 +1660,37 @@ void dft_add(mnl_fields *F, DftFluxH &o, int c, const double wmin[3], const doub
   for (auto &m : made) list.insert(list.begin(), m);
 }
 
-int dft_add_flux(mnl_fields *F, int nreg, const double *regions, const double *freqs, int nfreq,
-                 int decimation) {
-  if (F->src_dirty && build_source_lists(F)) return -1;
-  if (nreg < 1 || nfreq < 1) return fail("add_dft_flux: no regions / frequencies");
-  std::unique_ptr<DftFluxH> o(new DftFluxH);
-  o->nfreq = nfreq;
-  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
-  int decim = decimation;
-  if (decim == 0) {  // fields::add_dft (src/dft.cpp:190-213)
-    double src_freq_max = 0;
-    for (auto &st : F->srcs) {
-      const double fw = st.kind == 0 ? sqrt(-2.0 * log(1e-7)) / (st.width * pi) : 0.0;
-      if (fw == 0)
-        decim = 1;
-      else
-        src_freq_max =
-            std::max(src_freq_max, std::abs(st.kind == 0 ? st.freq : st.cfreq.real()) + 0.5 * fw);
-    }
-    double freq_max = 0;
-    for (int i = 0; i < nfreq; ++i) freq_max = std::max(freq_max, std::abs(freqs[i]));
-    bool nonlinear = false;  // structure_chunk::has_nonlinearities: nonzero chi2/chi3
-    for (int c = 0; c < 3; c++) {
-      for (double v : F->S.chi2[c]) nonlinear = nonlinear || v != 0.0;
-      for (double v : F->S.chi3[c]) nonlinear = nonlinear || v != 0.0;
-    }
-    for (auto &b : F->S.boxes) nonlinear = nonlinear || ((b.kind == 1 || b.kind == 2) && b.value != 0.0);
-    // (src/dft.cpp:207-210 overwrites the fwidth == 0 case above)
-    if ((freq_max > 0) && (src_freq_max > 0) && !nonlinear)
-      decim = std::max(1, int(std::floor(1 / (F->dt * (freq_max + src_freq_max)))));
-    else
+// decimation_factor of fields::add_dft (src/dft.cpp:190-213)
+int dft_decimation(mnl_fields *F, const double *freqs, int nfreq, int decim) {
+  if (decim != 0) return decim;
+  double src_freq_max = 0;
+  for (auto &st : F->srcs) {
+    const double fw = st.kind == 0 ? sqrt(-2.0 * log(1e-7)) / (st.width * pi) : 0.0;
+    if (fw == 0)
       decim = 1;
+    else
+      src_freq_max =
+          std::max(src_freq_max, std::abs(st.kind == 0 ? st.freq : st.cfreq.real()) + 0.5 * fw);
   }
-  o->decim = decim;
-  if (const char *e = getenv("MNL_DFT_BLOCK")) o->kb = std::max(1, std::min(DFT_KB, atoi(e)));
-  const double dt_factor = F->dt / sqrt(2.0 * pi) * decim;
-  std::vector<double> pwE, pwH;
-  DftFluxH ho;  // H points collected separately, appended after the E points
-  for (int r = 0; r < nreg; r++) {
-    const double *R = regions + 8 * r;
-    const int d = int(R[6]);
-    const double wgt = R[7];
-    int cE[2], cH[2];
-    switch (d) {  // fields::add_dft_flux (src/dft.cpp:601-617)
-      case 0: cE[0] = MNL_EY, cE[1] = MNL_EZ, cH[0] = MNL_HZ, cH[1] = MNL_HY; break;
-      case 1: cE[0] = MNL_EZ, cE[1] = MNL_EX, cH[0] = MNL_HX, cH[1] = MNL_HZ; break;
-      default: cE[0] = MNL_EX, cE[1] = MNL_EY, cH[0] = MNL_HY, cH[1] = MNL_HX; break;
-    }
-    for (int i = 0; i < 2; ++i) {
-      dft_add(F, *o, cE[i], R, R + 3, true, cplx(wgt * double(1 - 2 * i)), dt_factor, o->E, pwE);
-      dft_add(F, ho, cH[i], R, R + 3, false, cplx(1.0), dt_factor, o->H, pwH);
-    }
+  double freq_max = 0;
+  for (int i = 0; i < nfreq; ++i) freq_max = std::max(freq_max, std::abs(freqs[i]));
+  bool nonlinear = false;  // structure_chunk::has_nonlinearities: nonzero chi2/chi3
+  for (int c = 0; c < 3; c++) {
+    for (double v : F->S.chi2[c]) nonlinear = nonlinear || v != 0.0;
+    for (double v : F->S.chi3[c]) nonlinear = nonlinear || v != 0.0;
   }
+  for (auto &b : F->S.boxes) nonlinear = nonlinear || ((b.kind == 1 || b.kind == 2) && b.value != 0.0);
+  // (src/dft.cpp:207-210 overwrites the fwidth == 0 case above)
+  if ((freq_max > 0) && (src_freq_max > 0) && !nonlinear)
+    return std::max(1, int(std::floor(1 / (F->dt * (freq_max + src_freq_max)))));
+  return 1;
+}
+
+// Device layout of a DFT object whose E list holds the points of `pwE` and whose
+// H points (ho) follow: per-point chunk ids, wave-blocked DFT array, slots.
+int dft_layout(mnl_fields *F, std::unique_ptr<DftFluxH> &o, DftFluxH &ho, std::vector<double> &pwE,
+               std::vector<double> &pwH) {
+  const int nfreq = o->nfreq;
   // lay out: E points (creation order), then H points; chunks keep their p0
   const size_t nE = o->h_pj.size() / 3;
   for (auto &h : o->H) h.p0 += nE;
@@ -1750,6 +1757,61 @@ int dft_add_flux(mnl_fields *F, int nreg, const double *regions, const double *f
   }
   F->dfts.push_back(std::move(o));
   return int(F->dfts.size()) - 1;
+}
+
+int dft_add_flux(mnl_fields *F, int nreg, const double *regions, const double *freqs, int nfreq,
+                 int decimation) {
+  if (F->src_dirty && build_source_lists(F)) return -1;
+  if (nreg < 1 || nfreq < 1) return fail("add_dft_flux: no regions / frequencies");
+  std::unique_ptr<DftFluxH> o(new DftFluxH);
+  o->nfreq = nfreq;
+  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
+  o->decim = dft_decimation(F, freqs, nfreq, decimation);
+  for (int d = 0; d < 3; d++) o->wmin[d] = regions[d], o->wmax[d] = regions[3 + d];
+  if (const char *e = getenv("MNL_DFT_BLOCK")) o->kb = std::max(1, std::min(DFT_KB, atoi(e)));
+  const double dt_factor = F->dt / sqrt(2.0 * pi) * o->decim;
+  std::vector<double> pwE, pwH;
+  DftFluxH ho;  // H points collected separately, appended after the E points
+  for (int r = 0; r < nreg; r++) {
+    const double *R = regions + 8 * r;
+    const int d = int(R[6]);
+    const double wgt = R[7];
+    int cE[2], cH[2];
+    switch (d) {  // fields::add_dft_flux (src/dft.cpp:601-617)
+      case 0: cE[0] = MNL_EY, cE[1] = MNL_EZ, cH[0] = MNL_HZ, cH[1] = MNL_HY; break;
+      case 1: cE[0] = MNL_EZ, cE[1] = MNL_EX, cH[0] = MNL_HX, cH[1] = MNL_HZ; break;
+      default: cE[0] = MNL_EX, cE[1] = MNL_EY, cH[0] = MNL_HY, cH[1] = MNL_HX; break;
+    }
+    for (int i = 0; i < 2; ++i) {
+      dft_add(F, *o, cE[i], R, R + 3, true, cplx(wgt * double(1 - 2 * i)), dt_factor, o->E, pwE);
+      dft_add(F, ho, cH[i], R, R + 3, false, cplx(1.0), dt_factor, o->H, pwH);
+    }
+  }
+  return dft_layout(F, o, ho, pwE, pwH);
+}
+
+// fields::add_dft_fields (src/dft.cpp:889-903): per component (in order) add_dft
+// without dV / interpolation weights, stored_weight 1, prepended to one list; on
+// the centered grid or (yee) each component's own grid
+int dft_add_fields(mnl_fields *F, int ncomp, const int *comps, const double wmin[3],
+                   const double wmax[3], const double *freqs, int nfreq, int yee, int decimation) {
+  if (F->src_dirty && build_source_lists(F)) return -1;
+  if (ncomp < 1 || nfreq < 1) return fail("add_dft_fields: no components / frequencies");
+  for (int k = 0; k < ncomp; k++)
+    if (comps[k] < 0 || comps[k] >= 6) return fail("add_dft_fields: E or H components only");
+  std::unique_ptr<DftFluxH> o(new DftFluxH);
+  o->fields = true;
+  o->nfreq = nfreq;
+  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
+  o->decim = dft_decimation(F, freqs, nfreq, decimation);
+  for (int d = 0; d < 3; d++) o->wmin[d] = wmin[d], o->wmax[d] = wmax[d];
+  if (const char *e = getenv("MNL_DFT_BLOCK")) o->kb = std::max(1, std::min(DFT_KB, atoi(e)));
+  const double dt_factor = F->dt / sqrt(2.0 * pi) * o->decim;
+  std::vector<double> pwE, pwH;
+  DftFluxH ho;
+  for (int k = 0; k < ncomp; k++)
+    dft_add(F, *o, comps[k], wmin, wmax, false, cplx(1.0), dt_factor, o->E, pwE, yee != 0);
+  return dft_layout(F, o, ho, pwE, pwH);
 }
 
 // phases of every DFT update in steps [t0+1, t0+ns] -> device (one row per update)
@@ -5373,6 +5435,134 @@ int mnl_fields_mode(mnl_fields *F, int *fused) {
   *fused = (F->fused ? 1 : 0) | (F->fused && F->d_uidx ? 2 : 0) | (F->contig ? 4 : 0) |
            (std::min(F->contig_fallbacks, 255) << 8);
   return 0;
+}
+
+// fields::get_dft_array(dft_flux / dft_fields, c, num_freq) (src/dft.cpp:1240-1280):
+// process_dft_component into a whole array (get_dft_component_dims corners; every
+// chunk of c in list order; dft / stored_weight, divided by the loop weight when the
+// chunk stored it; times the interpolation weights of the empty dimensions,
+// src/dft.cpp:908-1040), summed over ranks (sum_to_all: one owner per point), then
+// collapse_array (src/array_slice.cpp:554-601).  out: re/im interleaved.
+static int dft_array_values(mnl_fields *F, int h, int c, int num_freq, int *rank,
+                            long long dims[3], double *out, long long nout) {
+  if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
+  DftFluxH &o = *F->dfts[h];
+  if (num_freq < 0 || num_freq > o.nfreq - 1)
+    return fail(("process_dft_component: frequency index " + std::to_string(num_freq) +
+                 " is outside the range of the frequency array of size " +
+                 std::to_string(o.nfreq)).c_str());
+  const mnl_structure &S = F->S;
+  std::vector<const DftChunkH *> L;
+  for (auto &dc : o.E)
+    if (dc.c == c) L.push_back(&dc);
+  for (auto &dc : o.H)
+    if (dc.c == c) L.push_back(&dc);
+  int mn[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, mx[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  for (auto *dc : L)
+    for (int d = 0; d < 3; d++) mn[d] = std::min(mn[d], dc->is[d]), mx[d] = std::max(mx[d], dc->ie[d]);
+  int r = 0, ds[3] = {0, 0, 0};
+  long long full[3] = {1, 1, 1};
+  if (!L.empty())
+    for (int d = 0; d < 3; d++) {
+      if (!S.has[d]) continue;
+      long long n = (mx[d] - mn[d]) / 2 + 1;
+      if (n > 1) ds[r] = d, full[r++] = n;
+    }
+  int rr = 0;  // collapse_array: directions empty in `where` are summed out
+  long long rd[3] = {1, 1, 1};
+  for (int k = 0; k < r; k++)
+    if (o.wmax[ds[k]] - o.wmin[ds[k]] != 0.0) rd[rr++] = full[k];
+  *rank = rr;
+  for (int k = 0; k < 3; k++) dims[k] = k < rr ? rd[k] : 1;
+  if (!out) return 0;
+  long long rs[3] = {0, 0, 0}, nred = 1;
+  for (int k = r - 1; k >= 0; k--)
+    if (o.wmax[ds[k]] - o.wmin[ds[k]] != 0.0) rs[k] = nred, nred *= full[k];
+  if (r == 0) nred = 0;
+  if (nout < nred) return fail("output buffer too small");
+  for (long long k = 0; k < 2 * nred; k++) out[k] = 0.0;
+  if (r == 0) return 0;
+  const size_t nf = o.nfreq;
+  std::vector<double> v(2 * ((o.npts + 63) & ~size_t(63)) * nf);
+  bool ok = true;
+  if (!v.empty())
+    ok = hipMemcpyAsync(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost, F->stream) ==
+             hipSuccess &&
+         hipStreamSynchronize(F->stream) == hipSuccess;
+  if (F->nranks > 1 && F->comm->agree_ok(ok, F->stream))  // every rank fails together
+    return fail(ok ? "get_dft_array: a rank failed" : "get_dft_array: device copy failed");
+  if (!ok) return fail("get_dft_array: device copy failed");
+  long long ntot = 1;
+  for (int k = 0; k < r; k++) ntot *= full[k];
+  std::vector<double> arr(2 * ntot, 0.0);
+  bool empty_dim[3];
+  for (int d = 0; d < 3; d++) empty_dim[d] = S.has[d] && o.wmax[d] - o.wmin[d] == 0.0;
+  const int yd[3] = {S.dim == 2 ? 2 : 0, S.dim == 2 ? 0 : 1, S.dim == 2 ? 1 : 2};
+  for (auto *dc : L) {
+    int n[3];
+    for (int k = 0; k < 3; k++) n[k] = S.has[yd[k]] ? (dc->ie[yd[k]] - dc->is[yd[k]]) / 2 + 1 : 1;
+    size_t pidx = 0;  // chunk_idx: points in LOOP_OVER_IVECS order
+    for (int i1 = 0; i1 < n[0]; i1++)
+      for (int i2 = 0; i2 < n[1]; i2++)
+        for (int i3 = 0; i3 < n[2]; i3++, pidx++) {
+          const size_t pt = dc->p0 + pidx;
+          const int *pj = &o.h_pj[3 * pt];
+          if (pj[0] < 0 && pj[1] < 0 && pj[2] < 0) continue;  // another rank's point
+          const int ii[3] = {i1, i2, i3};
+          int p[3] = {0, 0, 0};
+          for (int k = 0; k < 3; k++)
+            if (S.has[yd[k]]) p[yd[k]] = dc->is[yd[k]] + 2 * ii[k];
+          double wl[3], wi[3];
+          for (int k = 0; k < 3; k++) {
+            const int d = yd[k];
+            wl[k] = loop_w1(dc->s0[d], dc->s1[d], dc->e0[d], dc->e1[d], ii[k], n[k]);
+            wi[k] = empty_dim[d] ? wl[k] : loop_w1(1.0, 1.0, 1.0, 1.0, ii[k], n[k]);
+          }
+          const double w = wl[2] * (wl[1] * ((dc->dV0 + 0.0 * i2) * wl[0]));
+          const double interp_w = wi[2] * (wi[1] * (1.0 * wi[0]));
+          const size_t q = dft_at(o.slot[pt], num_freq, nf);
+          cplx dft_val = cplx(v[2 * q], v[2 * q + 1]) / dc->stored;
+          if (dc->incl && dft_val != 0.0) dft_val /= w;
+          long long oi = 0;
+          for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
+          const cplx val = interp_w * dft_val;
+          arr[2 * oi] = val.real();
+          arr[2 * oi + 1] = val.imag();
+        }
+  }
+  if (F->nranks > 1)
+    for (size_t q = 0; q < arr.size(); q += 1 << 20) {
+      const int n = (int)std::min<size_t>(1 << 20, arr.size() - q);
+      if (timed_allreduce(F, arr.data() + q, n)) return fail("get_dft_array allreduce failed");
+    }
+  for (long long q = 0; q < ntot; q++) {  // collapse_array, in full-index order
+    long long t = q, ri = 0;
+    for (int k = r - 1; k >= 0; k--) {
+      ri += (t % full[k]) * rs[k];
+      t /= full[k];
+    }
+    out[2 * ri] += arr[2 * q];
+    out[2 * ri + 1] += arr[2 * q + 1];
+  }
+  return 0;
+}
+
+int mnl_fields_add_dft_fields(mnl_fields *F, int ncomp, const int *comps, const double vmin[3],
+                              const double vmax[3], const double *freqs, int nfreq, int yee_grid,
+                              int decimation, int *handle) {
+  if (!F || !comps || !vmin || !vmax || !freqs || !handle) return fail("null argument");
+  if (decimation < 0) return fail("decimation must be >= 0");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  const int h = dft_add_fields(F, ncomp, comps, vmin, vmax, freqs, nfreq, yee_grid, decimation);
+  if (h < 0) return -1;
+  *handle = h;
+  return 0;
+}
+
+int mnl_fields_dft_array(mnl_fields *F, int h, int comp, int num_freq, int *rank, long long dims[3],
+                         double *out, long long nout) {
+  if (!F || !rank || !dims) return fail("null argument");
+  return dft_array_values(F, h, comp, num_freq, rank, dims, out, nout);
 }
 
 int mnl_fields_add_dft_flux(mnl_fields *F, int nreg, const double *regions, const double *freqs,

@@ -395,6 +395,24 @@ class DftFlux:
         return list(self.sim.fields.flux(self.handle))
 
 
+class DftFields:
+    """python/simulation.py:793-810 (dft_fields object, created by add_dft_fields);
+    the DFT lives on the GPU."""
+
+    def __init__(self, sim, components, freq, lo, hi, yee_grid, decimation_factor):
+        self.sim = sim
+        self.components = [int(c) for c in components]
+        self.freq = [float(f) for f in freq]
+        self.lo, self.hi = lo, hi
+        self.yee_grid = bool(yee_grid)
+        self.decimation_factor = int(decimation_factor)
+        self.handle = None
+
+    def _create(self):
+        self.handle = self.sim.fields.add_dft_fields(self.components, self.lo, self.hi, self.freq,
+                                                     self.yee_grid, self.decimation_factor)
+
+
 def get_flux_freqs(f):
     """python/simulation.py:6014-6019"""
     return list(f.freq)
@@ -1018,6 +1036,53 @@ class Simulation:
         flux._create()
         self.dft_objects.append(flux)
         return flux
+
+    def _where_bounds(self, where=None, center=None, size=None):
+        """_volume_from_kwargs (python/simulation.py:2253-2262): where, else center +
+        size, else the whole grid volume (fields::total_volume)."""
+        if where is not None:
+            center, size = where.center, where.size
+        dirs = (2,) if self.dimensions == 1 else ((0, 1) if self.dimensions == 2 else (0, 1, 2))
+        lo, hi = [0.0] * 3, [0.0] * 3
+        if center is None or size is None:
+            gv = self.structure.gv
+            for d in dirs:
+                lo[d] = gv.io[d] * (0.5 / gv.a)
+                hi[d] = (gv.io[d] + 2 * gv.n[d]) * (0.5 / gv.a)
+            return lo, hi
+        center, size = Vector3(*center), Vector3(*size)
+        for d in dirs:
+            lo[d] = center[d] - 0.5 * size[d]
+            hi[d] = center[d] + 0.5 * size[d]
+        return lo, hi
+
+    def add_dft_fields(self, *args, **kwargs):
+        """add_dft_fields(cs, fcen, df, nfreq | freq, where=None, center=None, size=None,
+        yee_grid=False, decimation_factor=0) (python/simulation.py:2976-3036) ->
+        fields::add_dft_fields (src/dft.cpp:889-903); initialises the fields first."""
+        components = list(args[0])
+        args = fix_dft_args(args, 1)
+        freq = args[1]
+        self.init_sim()
+        lo, hi = self._where_bounds(kwargs.get("where"), kwargs.get("center"), kwargs.get("size"))
+        if kwargs.get("persist", False):
+            pass  # persist only keeps chunks across a structure change (not modelled here)
+        dftf = DftFields(self, components, freq, lo, hi, kwargs.get("yee_grid", False),
+                         kwargs.get("decimation_factor", 0))
+        dftf._create()
+        self.dft_objects.append(dftf)
+        return dftf
+
+    def get_dft_array(self, dft_obj=None, component=None, num_freq=None):
+        """Simulation.get_dft_array (python/simulation.py:3988-4026) for dft_fields and
+        dft_flux objects -> fields::get_dft_array (src/dft.cpp:1240-1280): a complex
+        array over the object's volume (empty dimensions collapsed)."""
+        if not self.dft_objects:
+            raise RuntimeError("DFT monitor dft_obj must be initialized before calling "
+                               "get_dft_array")
+        if not isinstance(dft_obj, (DftFields, DftFlux)):
+            raise ValueError(f"Invalid type of dft object: {dft_obj}")
+        return self.fields.dft_array(dft_obj.handle, int(component), int(num_freq))
 
     # -- checkpoint (python/simulation.py:2293-2450); flat binary files, not HDF5
     def _load_dump_dirname(self, dirname, single_parallel_file=True):

@@ -1906,10 +1906,11 @@ namespace {
 struct DftChunk {
   int ci;                  // chunk index
   int c;                   // component
-  int is[3], ie[3];        // centered-grid corners of this chunk's piece
+  int is[3], ie[3];        // corners of this chunk's piece (centered grid, or c's Yee grid)
   double s0[3], s1[3], e0[3], e1[3];
   double dV0;
   bool incl;               // include_dV_and_interp_weights
+  cplx stored;             // stored_weight
   cplx scale;
   long avg1, avg2;         // yee2cent_offsets in the chunk's strides
   size_t N;
@@ -1919,6 +1920,8 @@ struct DftFluxObj {
   std::vector<double> omega;
   size_t nfreq = 0;
   int decim = 1;
+  bool fields = false;         // dft_fields (add_dft_fields): chunks in E only
+  double wmin[3], wmax[3];     // `where` of the object (get_dft_array's collapse)
   std::vector<DftChunk> E, H;  // in dft list order (next_in_dft)
 };
 
@@ -1954,6 +1957,10 @@ void boundary_weights(const GV &G, const double wmin[3], const double wmax[3], c
   }
 }
 
+inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) {  // vec.hpp:372-378
+  return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
+}
+
 // yucky directions of the ivec loops (3D: X,Y,Z; 2D: Z,X,Y; 1D: X,Y,Z)
 void yucky(const GV &G, int yd[3]) {
   if (G.dim == 2)
@@ -1962,16 +1969,23 @@ void yucky(const GV &G, int yd[3]) {
     yd[0] = X, yd[1] = Y, yd[2] = Z;
 }
 
-// fields::add_dft for component c over where (centered grid): one DftChunk per
-// intersecting chunk, prepended to `list` as loop_in_chunks creates them.
+// fields::add_dft for component c over where: one DftChunk per intersecting
+// chunk, prepended to `list` as loop_in_chunks creates them.  The grid is the
+// centered one, or with yee the component's own (loop_in_chunks(..., cgrid = c),
+// src/loop_in_chunks.cpp:350-356: where shifted by yee_shift(Centered) -
+// yee_shift(c), rounded to the dielectric grid, shifted back by iyee_c).
 void add_dft(orc_sim *s, int c, const double wmin[3], const double wmax[3], bool incl,
-             cplx stored_weight, double dt_factor, std::vector<DftChunk> &list, size_t nfreq) {
+             cplx stored_weight, double dt_factor, std::vector<DftChunk> &list, size_t nfreq,
+             bool yee = false) {
   const GV &G = s->gv;
-  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
+  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0}, sh[3] = {1, 1, 1};
   for (int d = 0; d < 3; d++) {
     if (!G.has[d]) continue;
-    is[d] = 1 + 2 * int(floor(wmin[d] * G.a - .5));  // vec2diel_floor, equal_shift 0
-    ie[d] = 1 + 2 * int(ceil(wmax[d] * G.a - .5));
+    if (yee) sh[d] = G.shift(c, d);
+    const int iyc = 1 - sh[d];                                  // iyee_c
+    const double yc = 1 * (0.5 * G.inva) - sh[d] * (0.5 * G.inva);  // yee_c (vec difference)
+    is[d] = 1 + 2 * int(floor((wmin[d] + yc) * G.a - .5)) - iyc;  // vec2diel_floor, equal_shift 0
+    ie[d] = 1 + 2 * int(ceil((wmax[d] + yc) * G.a - .5)) - iyc;
   }
   double s0[3], s1[3], e0[3], e1[3];
   boundary_weights(G, wmin, wmax, is, ie, s0, e0, s1, e1);
@@ -1992,7 +2006,8 @@ void add_dft(orc_sim *s, int c, const double wmin[3], const double wmax[3], bool
         isc[d] = iec[d] = 0;
         continue;
       }
-      const int uoc = G.io[d] + 1, coc = g.io[d] + 1, cbo = g.big(d) - 1;  // Centered: shift 1
+      // little_owned_corner(cgrid) = io + 2 - iyee_shift(cgrid), big_owned_corner = big - iyee
+      const int uoc = G.io[d] + 2 - sh[d], coc = g.io[d] + 2 - sh[d], cbo = g.big(d) - sh[d];
       const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
       isc[d] = std::max(is[d], iscoS);
       iec[d] = std::min(ie[d], iecoS);
@@ -2035,10 +2050,11 @@ void add_dft(orc_sim *s, int c, const double wmin[3], const double wmax[3], bool
     }
     dc.dV0 = dV0;
     dc.incl = incl;
+    dc.stored = stored_weight;
     dc.scale = stored_weight * cplx(1.0) * dt_factor;  // phase_factor 1 (no symmetry / Bloch)
-    dc.avg1 = dc.avg2 = 0;  // grid_volume::yee2cent_offsets (src/vec.cpp:333-344)
+    dc.avg1 = dc.avg2 = 0;  // grid_volume::yee2cent_offsets (src/vec.cpp:333-344), centered only
     for (int d = 0; d < 3; d++)
-      if (G.has[d] && !G.shift(c, d)) {
+      if (!yee && G.has[d] && !G.shift(c, d)) {
         if (dc.avg1)
           dc.avg2 = g.s[d];
         else
@@ -2110,6 +2126,30 @@ void update_dfts(orc_sim *s) {  // fields::update_dfts after t += 1 (src/step.cp
   }
 }
 
+namespace {
+// decimation_factor of fields::add_dft (src/dft.cpp:190-213)
+int dft_decimation(orc_sim *s, const double *freqs, int nfreq, int decim) {
+  if (decim != 0) return decim;
+  double src_freq_max = 0;
+  for (auto &st : s->srcs) {
+    const double fw = st.kind == 0 ? sqrt(-2.0 * log(1e-7)) / (st.width * pi) : 0.0;
+    if (fw == 0)
+      decim = 1;
+    else
+      src_freq_max = std::max(src_freq_max, std::abs(st.kind == 0 ? st.freq : st.cfreq.real()) + 0.5 * fw);
+  }
+  double freq_max = 0;
+  for (int i = 0; i < nfreq; ++i) freq_max = std::max(freq_max, std::abs(freqs[i]));
+  bool nonlinear = false;
+  for (auto &ch : s->chunks)
+    for (int c = 0; c < NCOMP; c++) nonlinear = nonlinear || !ch.chi2[c].empty() || !ch.chi3[c].empty();
+  // (src/dft.cpp:207-210 overwrites the fwidth == 0 case above)
+  if ((freq_max > 0) && (src_freq_max > 0) && !nonlinear)
+    return std::max(1, int(std::floor(1 / (s->dt * (freq_max + src_freq_max)))));
+  return 1;
+}
+}  // namespace
+
 extern "C" {
 
 // regions: nreg x {min x,y,z, max x,y,z, direction (0..2), weight}
@@ -2120,29 +2160,9 @@ int orc_add_dft_flux(orc_sim *s, int nreg, const double *regions, const double *
   std::unique_ptr<DftFluxObj> o(new DftFluxObj);
   o->nfreq = (size_t)nfreq;
   for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
-  int decim = decimation;
-  if (decim == 0) {  // fields::add_dft (src/dft.cpp:190-213)
-    double src_freq_max = 0;
-    for (auto &st : s->srcs) {
-      const double fw = st.kind == 0 ? sqrt(-2.0 * log(1e-7)) / (st.width * pi) : 0.0;
-      if (fw == 0)
-        decim = 1;
-      else
-        src_freq_max = std::max(src_freq_max, std::abs(st.kind == 0 ? st.freq : st.cfreq.real()) + 0.5 * fw);
-    }
-    double freq_max = 0;
-    for (int i = 0; i < nfreq; ++i) freq_max = std::max(freq_max, std::abs(freqs[i]));
-    bool nonlinear = false;
-    for (auto &ch : s->chunks)
-      for (int c = 0; c < NCOMP; c++) nonlinear = nonlinear || !ch.chi2[c].empty() || !ch.chi3[c].empty();
-    // (src/dft.cpp:207-210 overwrites the fwidth == 0 case above)
-    if ((freq_max > 0) && (src_freq_max > 0) && !nonlinear)
-      decim = std::max(1, int(std::floor(1 / (s->dt * (freq_max + src_freq_max)))));
-    else
-      decim = 1;
-  }
-  o->decim = decim;
-  const double dt_factor = s->dt / sqrt(2.0 * pi) * decim;
+  o->decim = dft_decimation(s, freqs, nfreq, decimation);
+  for (int d = 0; d < 3; d++) o->wmin[d] = regions[d], o->wmax[d] = regions[3 + d];
+  const double dt_factor = s->dt / sqrt(2.0 * pi) * o->decim;
   for (int r = 0; r < nreg; r++) {
     const double *R = regions + 8 * r;
     const int d = int(R[6]);
@@ -2160,6 +2180,121 @@ int orc_add_dft_flux(orc_sim *s, int nreg, const double *regions, const double *
   }
   s->dfts.push_back(std::move(o));
   return int(s->dfts.size()) - 1;
+}
+
+// fields::add_dft_fields (src/dft.cpp:889-903): per component (in order) add_dft
+// without dV / interpolation weights, stored_weight 1, prepended to one list;
+// yee_grid: on the component's own grid (use_centered_grid = false)
+int orc_add_dft_fields(orc_sim *s, int ncomp, const int *comps, const double wmin[3],
+                       const double wmax[3], const double *freqs, int nfreq, int yee_grid,
+                       int decimation) {
+  finalize(s);
+  if (ncomp < 1 || nfreq < 1) return set_err("add_dft_fields: no components / frequencies");
+  std::unique_ptr<DftFluxObj> o(new DftFluxObj);
+  o->fields = true;
+  o->nfreq = (size_t)nfreq;
+  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
+  o->decim = dft_decimation(s, freqs, nfreq, decimation);
+  for (int d = 0; d < 3; d++) o->wmin[d] = wmin[d], o->wmax[d] = wmax[d];
+  const double dt_factor = s->dt / sqrt(2.0 * pi) * o->decim;
+  for (int k = 0; k < ncomp; k++) {
+    if (comps[k] < 0 || comps[k] >= 6) return set_err("add_dft_fields: E or H components only");
+    add_dft(s, comps[k], wmin, wmax, false, cplx(1.0), dt_factor, o->E, o->nfreq, yee_grid != 0);
+  }
+  s->dfts.push_back(std::move(o));
+  return int(s->dfts.size()) - 1;
+}
+
+// fields::get_dft_array(dft_flux / dft_fields, c, num_freq) (src/dft.cpp:1240-1280):
+// process_dft_component into a whole array (get_dft_component_dims corners, every
+// chunk of c in list order, dft / stored_weight, divided by the loop weight when the
+// chunk stored it, times the interpolation weights of the empty dimensions,
+// src/dft.cpp:908-1040), then collapse_array (src/array_slice.cpp:554-601).
+// out: re/im interleaved, nout complex values; NULL queries rank / dims.
+int orc_dft_array(orc_sim *s, int h, int c, int num_freq, int *rank, long long dims[3],
+                  double *out, long long nout) {
+  if (h < 0 || h >= (int)s->dfts.size()) return set_err("bad dft handle");
+  DftFluxObj &o = *s->dfts[h];
+  if (num_freq < 0 || num_freq > int(o.nfreq) - 1)
+    return set_err(("process_dft_component: frequency index " + std::to_string(num_freq) +
+                    " is outside the range of the frequency array of size " +
+                    std::to_string(o.nfreq)).c_str());
+  const GV &G = s->gv;
+  std::vector<const DftChunk *> L;
+  for (auto &dc : o.E)
+    if (dc.c == c) L.push_back(&dc);
+  for (auto &dc : o.H)
+    if (dc.c == c) L.push_back(&dc);
+  int mn[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, mx[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+  for (auto *dc : L)
+    for (int d = 0; d < 3; d++) mn[d] = std::min(mn[d], dc->is[d]), mx[d] = std::max(mx[d], dc->ie[d]);
+  int r = 0, ds[3];
+  long long full[3] = {1, 1, 1};
+  if (!L.empty())
+    for (int d = 0; d < 3; d++) {
+      if (!G.has[d]) continue;
+      long long n = (mx[d] - mn[d]) / 2 + 1;
+      if (n > 1) ds[r] = d, full[r++] = n;
+    }
+  // collapse_array: directions empty in `where` are summed out (rank 0 stays rank 0)
+  int rr = 0;
+  long long rd[3] = {1, 1, 1};
+  for (int k = 0; k < r; k++)
+    if (o.wmax[ds[k]] - o.wmin[ds[k]] != 0.0) rd[rr++] = full[k];
+  *rank = rr;
+  for (int k = 0; k < 3; k++) dims[k] = k < rr ? rd[k] : 1;
+  if (!out) return 0;
+  long long rs[3] = {0, 0, 0}, nred = 1;
+  for (int k = r - 1; k >= 0; k--)
+    if (o.wmax[ds[k]] - o.wmin[ds[k]] != 0.0) rs[k] = nred, nred *= full[k];
+  if (r == 0) nred = 0;
+  if (nout < nred) return set_err("output buffer too small");
+  for (long long k = 0; k < 2 * nred; k++) out[k] = 0.0;
+  if (r == 0) return 0;
+  long long ntot = 1;
+  for (int k = 0; k < r; k++) ntot *= full[k];
+  std::vector<cplx> arr(ntot, cplx(0.0));
+  bool empty_dim[3];
+  for (int d = 0; d < 3; d++) empty_dim[d] = G.has[d] && o.wmax[d] - o.wmin[d] == 0.0;
+  int yd[3];
+  yucky(G, yd);
+  const size_t Nf = o.nfreq;
+  for (auto *dc : L) {
+    int n[3];
+    for (int k = 0; k < 3; k++) n[k] = G.has[yd[k]] ? (dc->ie[yd[k]] - dc->is[yd[k]]) / 2 + 1 : 1;
+    size_t pidx = 0;  // chunk_idx: points in LOOP_OVER_IVECS order
+    for (int i1 = 0; i1 < n[0]; i1++)
+      for (int i2 = 0; i2 < n[1]; i2++)
+        for (int i3 = 0; i3 < n[2]; i3++, pidx++) {
+          const int ii[3] = {i1, i2, i3};
+          int p[3] = {0, 0, 0};
+          for (int k = 0; k < 3; k++)
+            if (G.has[yd[k]]) p[yd[k]] = dc->is[yd[k]] + 2 * ii[k];
+          double wl[3], wi[3];
+          for (int k = 0; k < 3; k++) {
+            const int d = yd[k];
+            wl[k] = loop_w1(dc->s0[d], dc->s1[d], dc->e0[d], dc->e1[d], ii[k], n[k]);
+            wi[k] = empty_dim[d] ? wl[k] : loop_w1(1.0, 1.0, 1.0, 1.0, ii[k], n[k]);
+          }
+          const double w = wl[2] * (wl[1] * ((dc->dV0 + 0.0 * i2) * wl[0]));
+          const double interp_w = wi[2] * (wi[1] * (1.0 * wi[0]));
+          cplx dft_val = dc->dft[Nf * pidx + num_freq] / dc->stored;
+          if (dc->incl && dft_val != 0.0) dft_val /= w;
+          long long oi = 0;
+          for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
+          arr[oi] = interp_w * dft_val;
+        }
+  }
+  for (long long q = 0; q < ntot; q++) {  // collapse_array, in full-index order
+    long long t = q, ri = 0;
+    for (int k = r - 1; k >= 0; k--) {
+      ri += (t % full[k]) * rs[k];
+      t /= full[k];
+    }
+    out[2 * ri] += arr[q].real();
+    out[2 * ri + 1] += arr[q].imag();
+  }
+  return 0;
 }
 
 int orc_dft_flux(orc_sim *s, int h, double *out) {  // dft_flux::flux (src/dft.cpp:533-547)
@@ -2339,9 +2474,6 @@ std::vector<SliceLoop> slice_loops(orc_sim *s, const double wmin[3], const doubl
   return out;
 }
 
-inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) {  // vec.hpp:372-378
-  return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
-}
 
 // ---------------------------------------------------------------- field energy
 // loop_in_chunks(where, cgrid = c) (src/loop_in_chunks.cpp:325-520) restricted

@@ -85,6 +85,15 @@ int orc_dft_flux(orc_sim *s, int h, double *out);
 long long orc_dft_size(orc_sim *s, int h);
 int orc_dft_data(orc_sim *s, int h, int which, double *out, long long n);
 int orc_dft_decimation(orc_sim *s, int h);
+/* DFT fields (fields::add_dft_fields, src/dft.cpp:889-903): E / H components over
+ * [wmin, wmax], centered grid or (yee_grid) each component's own grid. */
+int orc_add_dft_fields(orc_sim *s, int ncomp, const int *comps, const double wmin[3],
+                       const double wmax[3], const double *freqs, int nfreq, int yee_grid,
+                       int decimation);
+/* fields::get_dft_array(obj, c, num_freq) (src/dft.cpp:1240-1280) for flux and
+ * fields objects: re/im interleaved, empty dimensions collapsed; out NULL = size query */
+int orc_dft_array(orc_sim *s, int h, int c, int num_freq, int *rank, long long dims[3],
+                  double *out, long long nout);
 
 /* Subpixel averaging (src/anisotropic_averaging.cpp:58-298) over geometric
  * objects {kind, eps, cx, cy, cz, p0, p1, p2} (see mnl_structure_set_epsilon_geometry):

@@ -80,6 +80,10 @@ def lib():
         L.orc_dft_size.argtypes = [c_void, c_int]
         L.orc_dft_data.argtypes = [c_void, c_int, c_int, dptr, ctypes.c_longlong]
         L.orc_dft_decimation.argtypes = [c_void, c_int]
+        L.orc_add_dft_fields.argtypes = [c_void, c_int, iptr, dptr, dptr, dptr, c_int, c_int,
+                                         c_int]
+        L.orc_dft_array.argtypes = [c_void, c_int, c_int, c_int, iptr,
+                                    ctypes.POINTER(ctypes.c_longlong), dptr, ctypes.c_longlong]
         L.orc_eps_average.argtypes = [c_int, iptr, iptr, c_double, c_int, c_int, dptr, c_double,
                                       c_int, c_double, c_int, dptr, dptr, dptr]
         L.orc_sphere_quadrature.argtypes = [c_int, dptr]
@@ -440,6 +444,34 @@ class Oracle:
 
     def dft_decimation(self, h):
         return lib().orc_dft_decimation(self.h, h)
+
+    # ---- DFT fields (fields::add_dft_fields / get_dft_array, src/dft.cpp:889-903, 1240-1280)
+    def add_dft_fields(self, comps, vmin, vmax, freqs, yee_grid=False, decimation=0):
+        cs = np.ascontiguousarray(comps, dtype=np.int32)
+        lo = np.ascontiguousarray(vmin, dtype=np.float64)
+        hi = np.ascontiguousarray(vmax, dtype=np.float64)
+        f = np.ascontiguousarray(freqs, dtype=np.float64)
+        h = lib().orc_add_dft_fields(self.h, len(cs), cs.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                     _dp(lo), _dp(hi), _dp(f), len(f), int(bool(yee_grid)),
+                                     int(decimation))
+        if h < 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        self._dft_nf = getattr(self, "_dft_nf", {})
+        self._dft_nf[h] = len(f)
+        return h
+
+    def dft_array(self, h, comp, num_freq):
+        """get_dft_array(obj, comp, num_freq): complex array, empty dimensions collapsed."""
+        rank = ctypes.c_int(0)
+        dims = (ctypes.c_longlong * 3)()
+        _chk(lib().orc_dft_array(self.h, h, comp, num_freq, ctypes.byref(rank), dims, None, 0))
+        shape = tuple(dims[k] for k in range(rank.value))
+        if not rank.value:  # no chunk of comp (process_dft_component: rank 0, no array)
+            return np.zeros(0, dtype=np.complex128)
+        n = int(np.prod(shape))
+        out = np.zeros(2 * max(n, 1), dtype=np.float64)
+        _chk(lib().orc_dft_array(self.h, h, comp, num_freq, ctypes.byref(rank), dims, _dp(out), n))
+        return (out[0:2 * n:2] + 1j * out[1:2 * n:2]).reshape(shape)
 
     def center(self):
         """grid_volume::center() (src/vec.cpp:1089-1103): io + round_down_to_even(n)."""

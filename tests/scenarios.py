@@ -150,6 +150,12 @@ class ProductSim:
     def dft_decimation(self, h):
         return self._fields().dft_decimation(h)
 
+    def add_dft_fields(self, comps, vmin, vmax, freqs, yee_grid=False, decimation=0):
+        return self._fields().add_dft_fields(comps, vmin, vmax, freqs, yee_grid, decimation)
+
+    def dft_array(self, h, comp, num_freq):
+        return self._fields().dft_array(h, comp, num_freq)
+
     def dump(self, path):
         self._fields().dump(path)
 
@@ -290,6 +296,16 @@ class GroupSim(ProductSim):
     def dft_data(self, h, which):
         # each point is accumulated by the rank that owns it, the others hold 0
         return sum(f.dft_data(h, which) for f in self._all())
+
+    def add_dft_fields(self, comps, vmin, vmax, freqs, yee_grid=False, decimation=0):
+        hs = [f.add_dft_fields(comps, vmin, vmax, freqs, yee_grid, decimation) for f in self._all()]
+        assert all(h == hs[0] for h in hs)
+        return hs[0]
+
+    def dft_array(self, h, comp, num_freq):
+        vals = self._par(lambda f: f.dft_array(h, comp, num_freq))  # collective, summed
+        assert all(np.array_equal(v, vals[0]) for v in vals)
+        return vals[0]
 
 
     def dump(self, path):
@@ -756,6 +772,57 @@ def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=No
         extra(o)
     o.step(steps - steps // 2)
     return o, hs
+
+
+DFTF_FREQS = [0.12, 0.2]
+
+
+def sc_dft_fields_3d(make, steps=60, lorentz=False, sizes=None):
+    """sc_flux_3d's waveguide + PML with DFT-field objects (fields::add_dft_fields,
+    src/dft.cpp:889-903): every E / H component over the whole cell on the centered
+    grid; Ez, Hx, Hy on their Yee grids over a box crossing PML chunks; an x-normal
+    plane (collapsed to 2-D); a y-z line on the Yee grid (two empty dimensions); a
+    flux plane (get_dft_array of a dft_flux).  Returns (sim, [(handle, comps)])."""
+    sizes = sizes or [3.2, 3.2, 3.2]
+    o = vol(make, 3, sizes, 10, center_origin=True)
+    o.add_pml(1.0)
+    sig = []
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        o.set_chi1inv(c, c, np.where((np.abs(y) < 0.5) & (np.abs(z) < 0.5), 1 / 12.0, 1.0))
+        sig.append(np.where(np.abs(z - 0.3) < 0.25, 0.5, 0.0))
+    if lorentz:
+        o.add_lorentzian(1.1, 0.05, sig)
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    o.add_gaussian_source(1, 0.2, 6.0, 0.0, 60.0, (-0.33, 0.12, 0.41), 0.7)
+    hx, hy, hz = [0.5 * s for s in sizes]
+    objs = [
+        (o.add_dft_fields([0, 1, 2, 3, 4, 5], [-hx, -hy, -hz], [hx, hy, hz], DFTF_FREQS, False, 1),
+         [0, 1, 2, 3, 4, 5]),
+        (o.add_dft_fields([2, 3, 4], [-1.23, -0.71, -1.3], [0.94, 1.42, 0.57], DFTF_FREQS, True, 1),
+         [2, 3, 4]),
+        (o.add_dft_fields([1, 5], [0.33, -hy, -hz], [0.33, hy, hz], DFTF_FREQS, False, 0), [1, 5]),
+        (o.add_dft_fields([0], [-0.9, 0.27, -0.15], [1.1, 0.27, -0.15], DFTF_FREQS, True, 1), [0]),
+        (o.add_dft_flux([([-0.52, -hy, -hz], [-0.52, hy, hz], 0, 1.0)], DFTF_FREQS, 1), [1, 2, 4, 5]),
+    ]
+    o.step(steps)
+    return o, objs
+
+
+def sc_dft_fields_2d(make, steps=200):
+    """2-D TM + TE (Ez and Hz sources) with PML: centered and Yee-grid DFT fields."""
+    o = vol(make, 2, [4.0, 3.0], 10)
+    o.add_pml(0.7)
+    o.add_gaussian_source(2, 0.3, 5.0, 0.0, 50.0, (1.3, 1.1, 0), 1.0)
+    o.add_gaussian_source(5, 0.25, 4.0, 0.0, 40.0, (2.6, 1.7, 0), 0.5)
+    objs = [
+        (o.add_dft_fields([0, 1, 2, 3, 4, 5], [0, 0, 0], [4.0, 3.0, 0], DFTF_FREQS, False, 1),
+         [0, 1, 2, 3, 4, 5]),
+        (o.add_dft_fields([2, 5, 0], [0.25, 0.4, 0], [3.3, 2.9, 0], DFTF_FREQS, True, 1), [2, 5, 0]),
+        (o.add_dft_fields([2, 3], [0.5, 1.55, 0], [3.5, 1.55, 0], DFTF_FREQS, False, 1), [2, 3]),
+    ]
+    o.step(steps)
+    return o, objs
 
 
 def sc_flux_1d(make, steps=1500, chi3=1e-2):
