@@ -138,7 +138,10 @@ def roofline(f, kind=0):
     achieved = k_bytes / (avg_ms * 1e-3) / 1e9 if n_launch and avg_ms > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": (("fused_kernel + fused_general_kernel concurrently (whole step, one pass)"
+            "kernel": (("fused_tile_kernel (one persistent launch over the fused box: lean "
+                        "tiles + per-direction PML bodies; curl B + H + curl D + E, one pass)"
+                        if f.tile_mode() else
+                        "fused_kernel + fused_general_kernel concurrently (whole step, one pass)"
                         if f.kernel_stats(2)[0] == 0 else
                         "fused_kernel (lean tiles: curl B + curl D + E=chi1inv*D, one pass)")
                        if f.fused_active() else "curl_kernel<B, interior> (step_db(B_stuff))"),
@@ -149,7 +152,8 @@ def roofline(f, kind=0):
         if g_n:
             g_avg = g_ms / g_n
             roof["general_kernel"] = {
-                "kernel": "fused_general_kernel (PML / boundary tiles, same pass)",
+                "kernel": ("fused_general_kernel (polarization chunks, same pass)" if f.tile_mode()
+                           else "fused_general_kernel (PML / boundary tiles, same pass)"),
                 "bytes_per_launch": g_bytes, "avg_launch_ms": round(g_avg, 4),
                 "achieved": round(g_bytes / (g_avg * 1e-3) / 1e9, 1)}
     return roof

@@ -495,6 +495,12 @@ class Fields:
         check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
         return bool(v.value & 1)
 
+    def tile_mode(self):
+        """True if the fused step runs as one tile kernel (lean + PML bodies)."""
+        v = ctypes.c_int()
+        check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
+        return bool(v.value & 16)
+
     def fused_palette(self):
         """True if the fused kernel reads chi1inv through the byte palette."""
         v = ctypes.c_int()

@@ -5433,7 +5433,7 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
 int mnl_fields_mode(mnl_fields *F, int *fused) {
   if (!F) return fail("null fields");
   *fused = (F->fused ? 1 : 0) | (F->fused && F->d_uidx ? 2 : 0) | (F->contig ? 4 : 0) |
-           (std::min(F->contig_fallbacks, 255) << 8);
+           (F->fused && F->tile_mode ? 16 : 0) | (std::min(F->contig_fallbacks, 255) << 8);
   return 0;
 }
 
