@@ -68,10 +68,12 @@ int mnl_structure_add_pml(mnl_structure *s, int dir, int side, double thickness,
                           double R_asymptotic, double mean_stretch);
 
 /* structure_chunk::set_chi1inv row (src/anisotropic_averaging.cpp:211-298)
- * for E component comp and direction dir; host array in the layout above
+ * for E component comp (epsilon) or H component comp (mu: structure::set_mu,
+ * src/structure.cpp) and direction dir; host array in the layout above
  * (values at every point, ghosts included).  Off-diagonal entries are
  * accepted but only their presence/zeros enter the arithmetic, exactly as in
- * the fork (src/step_generic.cpp:631-633, 730-760). NULL resets to trivial. */
+ * the fork (src/step_generic.cpp:631-633, 730-760; the H update always takes
+ * the diagonal branch). NULL resets to trivial. */
 int mnl_structure_set_chi1inv(mnl_structure *s, int comp, int dir, const double *host);
 /* structure_chunk::set_chi2 / set_chi3 (src/structure.cpp:795-866).  chi3 is
  * inert in the fork (src/step_generic.cpp:829-886) and only recorded. */
@@ -99,6 +101,13 @@ int mnl_structure_add_lorentzian(mnl_structure *s, double omega0, double gamma, 
  * reference chunk. */
 int mnl_structure_add_lorentzian_tensor(mnl_structure *s, double omega0, double gamma, int drude,
                                         const double *const sigma[9]);
+/* structure::add_susceptibility(sigma, H_stuff, lorentzian_susceptibility(omega0,
+ * gamma, drude)) (src/anisotropic_averaging.cpp:300-372): a magnetic Lorentzian / Drude
+ * susceptibility, diagonal sigma per H component at its Yee points (NULL = 0), updated
+ * by update_pols(H_stuff) after update_eh(H_stuff) (src/step.cpp:75-92).  At most 2. */
+int mnl_structure_add_magnetic_lorentzian(mnl_structure *s, double omega0, double gamma,
+                                          int drude, const double *sigma_x,
+                                          const double *sigma_y, const double *sigma_z);
 /* Nonlinear E update: 0 = the fork (chi2 through Newton-Raphson where the
  * 3x3 chi1inv is present, chi3 inert; default), 1 = upstream Meep (chi2/chi3
  * through the Pade approximant calc_nonlinear_u, src/step_generic.cpp:546-553,

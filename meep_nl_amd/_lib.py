@@ -52,6 +52,8 @@ _SIGS = {
     "mnl_structure_dump": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_load": (c_int, [c_void, ctypes.c_char_p]),
     "mnl_structure_add_lorentzian": (c_int, [c_void, c_double, c_double, c_int, dptr, dptr, dptr]),
+    "mnl_structure_add_magnetic_lorentzian": (c_int, [c_void, c_double, c_double, c_int, dptr,
+                                                      dptr, dptr]),
     "mnl_structure_set_box": (c_int, [c_void, c_int, c_int, dptr, c_double]),
     "mnl_structure_set_epsilon_geometry": (c_int, [c_void, c_int, c_int, dptr, c_double, c_int,
                                                    c_double, c_int]),

@@ -142,6 +142,14 @@ class Structure:
                 continue
             self.set_chi1inv(c, c % 3, 1.0 / fn(*self.gv.coords(c)))
 
+    def set_mu_fn(self, fn):
+        """structure::set_mu without averaging: chi1inv of the H components =
+        1/mu(location) (set_chi1inv(H_stuff), src/anisotropic_averaging.cpp:221-298)."""
+        for c in (Hx, Hy, Hz):
+            if self.gv.dim == 1 and c != Hy:
+                continue
+            self.set_chi1inv(c, c % 3, 1.0 / fn(*self.gv.coords(c)))
+
     def set_epsilon_geometry(self, objects, default_eps=1.0, use_anisotropic_averaging=True,
                              tol=1e-4, maxeval=100000, device=-1):
         """structure::set_epsilon(material_function &, use_anisotropic_averaging, tol,
@@ -202,6 +210,13 @@ class Structure:
         ptrs = (dptr * 9)(*[ptr(a) if a is not None else None for a in arrs])
         check(lib().mnl_structure_add_lorentzian_tensor(self.h, float(omega0), float(gamma),
                                                          int(drude), ptrs))
+
+    def add_magnetic_lorentzian(self, omega0, gamma, sigmas, drude=False):
+        """add_susceptibility(sigma, H_stuff, lorentzian_susceptibility): diagonal
+        sigma per H component at its Yee points (None = 0)."""
+        s = [None if v is None else self._arr(v) for v in sigmas]
+        check(lib().mnl_structure_add_magnetic_lorentzian(self.h, float(omega0), float(gamma),
+                                                          int(drude), *[ptr(v) for v in s]))
 
     def set_box(self, kind, box, value, index=0):
         b = np.ascontiguousarray(box, dtype=np.float64)

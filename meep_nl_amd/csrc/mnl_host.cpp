@@ -150,6 +150,11 @@ struct mnl_structure {
   std::vector<double> chi2[3], chi3[3];
   std::vector<double> cond[2][3];     // conductivity of [B, D][dir], canonical (empty = 0)
   std::vector<Lorentz> lor;
+  // H side: chi1inv of the H components (structure::set_mu ->
+  // set_chi1inv(H_stuff), [H comp][dir], canonical) and the magnetic susceptibilities
+  // (add_susceptibility(sigma, H_stuff, ...), diagonal sigma at the H components' points)
+  std::vector<double> mu1inv[3][3];
+  std::vector<Lorentz> hlor;
   std::vector<BoxSpec> boxes;
   size_t ntot;
   int nl_mode = 0;  // 0: the fork (NR chi2, inert chi3); 1: upstream Meep (Pade chi2/chi3)
@@ -311,6 +316,8 @@ struct mnl_fields {
   CurlPlan planB, planD;
   bool nr = false;
   bool upnl = false;  // upstream chi2/chi3 update active (nl_mode 1 with nonzero chi)
+  bool hall = false;  // H-side materials: H stored everywhere (DevFields::hall)
+  std::vector<uint8_t> h_hsep_zone;  // host copy of DevFields::hsep_zone (27 zone boxes)
   // sources
   std::vector<SrcTime> srcs;
   std::vector<SrcGroup> groups;
@@ -707,10 +714,12 @@ int alloc_component(mnl_fields *F, int c) {
   if (t == T_H) {
     if (!F->f.B[d] && dev_alloc(F, &F->f.B[d], F->nlocal)) return -1;
     F->f.Bn[d] = F->f.B[d];
-    if (F->pml_any[d]) {  // H separate in chunks with PML along d (src/update_eh.cpp:204-209)
+    // H separate in chunks with PML along d (src/update_eh.cpp:204-209); with H-side
+    // materials stored everywhere (a copy of B where the chunk aliases it)
+    if (F->pml_any[d] || F->hall)
       if (dev_alloc(F, &F->f.H[d], F->nlocal)) return -1;
+    if (F->pml_any[d])
       if (dev_alloc(F, &F->f.WH[d], F->nlocal)) return -1;
-    }
   }
   if (t == T_B) F->f.Bn[d] = F->f.B[d];
   if (t == T_E) F->f.En[d] = F->f.E[d];
@@ -741,6 +750,19 @@ int require_component(mnl_fields *F, int c) {  // src/fields.cpp:566-586
       if (F->allocated[d] && !L.sigma[d].empty() && pd.sigma[d] && !pd.P[d]) {
         if (dev_alloc(F, &pd.P[d], F->nlocal)) return -1;
         if (dev_alloc(F, &pd.Pp[d], F->nlocal)) return -1;
+      }
+  }
+  // magnetic polarizations: P of every allocated H comp with nontrivial sigma; then
+  // f_minus_p of B exists in every chunk (needs_P uses the global sigma flags,
+  // src/update_eh.cpp:84-100), so H is separate everywhere (src/update_eh.cpp:204-209)
+  for (int k = 0; k < F->f.nhpol; k++) {
+    const Lorentz &L = F->S.hlor[F->S.hlor.size() - 1 - k];
+    PolDev &pd = F->f.hpol[k];
+    for (int d = 0; d < 3; d++)
+      if (F->allocated[3 * T_H + d] && !L.sigma[d].empty() && pd.sigma[d] && !pd.P[d]) {
+        if (dev_alloc(F, &pd.P[d], F->nlocal)) return -1;
+        if (dev_alloc(F, &pd.Pp[d], F->nlocal)) return -1;
+        F->f.hsep_all = 1;
       }
   }
   make_plans(F);
@@ -840,6 +862,87 @@ int setup_conductivity(mnl_fields *F) {
   HIPCHK(hipMemcpyAsync(dcz, cz.data(), 27, hipMemcpyHostToDevice, F->stream));
   HIPCHK(hipStreamSynchronize(F->stream));
   f.cnd_zone = dcz;
+  return 0;
+}
+
+// H-side materials: chi1inv of the H components (set_mu) and
+// magnetic Lorentzian susceptibilities.  The fork's update_eh(H_stuff) takes
+// step_update_EDHB's diagonal branch whatever off-diagonal rows exist (its 3x3 branch
+// needs chi3, which no H component has, src/step_generic.cpp:730-906), so only the
+// diagonal enters the arithmetic; the rows still decide per reference chunk whether H is
+// separate from B (chi1inv[H_c][c] kept: the diagonal given and some entry of the row
+// nontrivial in the chunk, src/anisotropic_averaging.cpp:279-296, src/update_eh.cpp:204-209).
+int setup_h_materials(mnl_fields *F) {
+  const mnl_structure &S = F->S;
+  DevFields &f = F->f;
+  bool mu_any = false, hl_any = false, off_any = false;
+  for (int c = 0; c < 3; c++) {
+    if (!has_field(S, 3 * T_H + c)) continue;
+    for (int d = 0; d < 3; d++) {
+      const auto &v = S.mu1inv[c][d];
+      if (v.empty() || all_eq(v, d == c ? 1.0 : 0.0)) continue;
+      mu_any = true;
+      off_any = off_any || d != c;
+    }
+  }
+  for (const Lorentz &L : S.hlor)
+    for (int d = 0; d < 3; d++)
+      hl_any = hl_any || (!L.sigma[d].empty() && has_field(S, 3 * T_H + d));
+  F->hall = mu_any || hl_any;
+  f.hall = F->hall ? 1 : 0;
+  if (!F->hall) return 0;
+  if (S.nl_mode == 1 && off_any)  // upstream Meep would average them in (OFFDIAG)
+    return fail("off-diagonal mu is not supported in the upstream nonlinear mode");
+  if ((int)S.hlor.size() > MAX_HPOL) return fail("too many magnetic susceptibilities (max 2)");
+  for (int c = 0; c < 3; c++) {
+    const auto &diag = S.mu1inv[c][c];
+    if (!has_field(S, 3 * T_H + c) || diag.empty() || all_eq(diag, 1.0)) continue;
+    double *p;
+    if (dev_alloc(F, &p, F->nlocal)) return -1;
+    if (upload_canonical(F, p, diag, 3 * T_H + c)) return -1;
+    f.invmu[c] = p;
+  }
+  std::vector<uint8_t> hz(27, 0);
+  auto ivx = zone_ivs_or_one(S, 0), ivy = zone_ivs_or_one(S, 1), ivz = zone_ivs_or_one(S, 2);
+  for (auto &zx : ivx)
+    for (auto &zy : ivy)
+      for (auto &zz : ivz) {
+        const ZoneIv *zv[3] = {&zx, &zy, &zz};
+        for (int c = 0; c < 3; c++) {
+          if (!has_field(S, 3 * T_H + c) || S.mu1inv[c][c].empty()) continue;
+          bool nt = false;
+          for (int d = 0; d < 3 && !nt; d++) {
+            const auto &v = S.mu1inv[c][d];
+            nt = !v.empty() && nontrivial_in_zone(S, v, 3 * T_H + c, zv, d == c ? 1.0 : 0.0);
+          }
+          if (nt) hz[zx.zone * 9 + zy.zone * 3 + zz.zone] |= 1 << c;
+        }
+      }
+  uint8_t *dz;
+  if (dev_alloc(F, &dz, 27)) return -1;
+  HIPCHK(hipMemcpyAsync(dz, hz.data(), 27, hipMemcpyHostToDevice, F->stream));
+  f.hsep_zone = dz;
+  F->h_hsep_zone = hz;
+  // magnetic pol list: reverse add order (as the E side)
+  const int nh = (int)S.hlor.size();
+  f.nhpol = nh;
+  for (int k = 0; k < nh; k++) {
+    const Lorentz &L = S.hlor[nh - 1 - k];
+    PolDev &pd = f.hpol[k];
+    const double omega2pi = 2 * pi * L.omega0, g2pi = L.gamma * 2 * pi;
+    pd.omega0dtsqr = omega2pi * omega2pi * F->dt * F->dt;
+    pd.gamma1inv = 1 / (1 + g2pi * F->dt / 2);
+    pd.gamma1 = (1 - g2pi * F->dt / 2);
+    pd.omega0dtsqr_denom = L.drude ? 0 : pd.omega0dtsqr;
+    for (int d = 0; d < 3; d++) {
+      if (L.sigma[d].empty() || !has_field(S, 3 * T_H + d)) continue;
+      double *p;
+      if (dev_alloc(F, &p, F->nlocal)) return -1;
+      if (upload_canonical(F, p, L.sigma[d], 3 * T_H + d)) return -1;
+      pd.sigma[d] = p;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(F->stream));
   return 0;
 }
 
@@ -1050,6 +1153,7 @@ int setup_materials(mnl_fields *F) {
         f.pol[k].nz.hi[e] = init[6 * k + 3 + e];
       }
   }
+  if (setup_h_materials(F)) return -1;
   // The E update reaches the high metallic wall planes the reference's chunks own
   // (zeroed only afterwards by step_boundaries): with D = 0 there, E is nonzero
   // only through neighbour reads (OFFDIAG, Newton-Raphson), and only a
@@ -1999,7 +2103,9 @@ int value_at(mnl_fields *F, int c, const int p[3], double *out) {
     case T_B: src = F->f.B[d]; break;
     case T_H: {
       src = F->f.B[d];
-      if (F->f.H[d] && S.has[d]) {
+      if (F->hall) {  // H stored everywhere once the first H update has run
+        if (F->h_first_done) src = F->f.H[d];
+      } else if (F->f.H[d] && S.has[d]) {
         int q = 2 * jg[d];
         if (F->h_flag[d][q]) src = F->f.H[d];
       }
@@ -2651,7 +2757,7 @@ bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
 }
 
 bool fused_possible(mnl_fields *F) {
-  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->upnl || F->f.aniso) return false;
+  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->upnl || F->f.aniso || F->hall) return false;
   for (int t = 0; t < 2; t++)
     for (int d = 0; d < 3; d++)
       if (F->f.cnd[t][d]) return false;
@@ -3106,6 +3212,21 @@ int e_lazy_copy(mnl_fields *F) {
   return 0;
 }
 
+// update_eh(H_stuff) [+ update_pols(H_stuff) when pols]: the PML W update over the shell boxes, or,
+// with H-side materials, the H kernel over the whole rank-local box
+int update_h_any(mnl_fields *F, const BoxList &sl, bool pols) {
+  if (F->hall) {
+    Box all;
+    for (int k = 0; k < 3; k++) all.lo[k] = 0, all.hi[k] = F->g.N[k] - 1;
+    if (k_update_hmat(all, F->g, F->f, pols ? 1 : 0, F->stream)) return fail("update H launch failed");
+    return 0;
+  }
+  bool anyH = false;
+  for (int d = 0; d < 3; d++) anyH = anyH || F->f.H[d];
+  if (anyH && k_update_h(sl, F->g, F->f, F->stream)) return fail("update H launch failed");
+  return 0;
+}
+
 // Interior E update with chi(2) Newton-Raphson: the NR kernel over the bounding
 // box of chi2 != 0 inside the interior, the plain kernel over the rest (outside
 // that box chi2 = 0, so every point takes E = chi1inv * (D - P) either way).
@@ -3399,7 +3520,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       // shell curl B; the PML H update rides along when no B source sits between
       // (timing events only around phases that launch something: an event record
       // between two kernels costs a few microseconds of GPU time)
-      const bool fuseH = nB == 0 && !F->first_step_mode;
+      const bool fuseH = nB == 0 && !F->first_step_mode && !F->hall;
       const bool shell_work = sl->n > 0 && sl->start[sl->n] > 0;
       k = shell_work ? ev_begin(TM_B) : -1;
       if (k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->stream, fuseH))
@@ -3408,10 +3529,10 @@ int step_batch(mnl_fields *F, int nsteps) {
       if (nB && k_source(T_B, g, f, sB, 0, F->stream)) return fail("source launch failed");
       // ---- H
       if (!F->h_first_done && h_lazy_copy(F)) return -1;
-      bool anyH = false;
+      bool anyH = F->hall;
       for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
-      k = (!fuseH && anyH && shell_work) ? ev_begin(TM_H) : -1;
-      if (!fuseH && anyH && k_update_h(*sl, g, f, F->stream)) return fail("update H launch failed");
+      k = (!fuseH && anyH && (shell_work || F->hall)) ? ev_begin(TM_H) : -1;
+      if (!fuseH && update_h_any(F, *sl, true)) return -1;
       ev_end(k);
       if (F->nranks > 1) {
         int kk = ev_begin(TM_HALO);
@@ -3582,6 +3703,11 @@ std::vector<CkEntry> ckpt_entries(mnl_fields *F) {
     DftFluxH &o = *F->dfts[h];
     add(11, (int)h, o.nfreq, o.d_dft, 2 * ((o.npts + 63) & ~size_t(63)) * o.nfreq);
   }
+  for (int k = 0; k < f.nhpol; k++)  // magnetic polarizations
+    for (int d = 0; d < 3; d++) {
+      add(12, k, d, f.hpol[k].P[d], n);
+      add(13, k, d, f.hpol[k].Pp[d], n);
+    }
   return v;
 }
 
@@ -3735,6 +3861,19 @@ int structure_dump(const mnl_structure *S, const char *path) {
   }
   put(o, (uint64_t)S->boxes.size());
   for (auto &b : S->boxes) put(o, b);
+  bool hside = !S->hlor.empty();  // optional H-side section (absent in older files)
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) hside = hside || !S->mu1inv[c][d].empty();
+  if (hside) {
+    put(o, (uint64_t)0x4853494445ull);  // "HSIDE"
+    for (int c = 0; c < 3; c++)
+      for (int d = 0; d < 3; d++) put_vec(o, S->mu1inv[c][d]);
+    put(o, (uint64_t)S->hlor.size());
+    for (auto &L : S->hlor) {
+      put(o, L.omega0), put(o, L.gamma), put(o, L.drude);
+      for (int d = 0; d < 3; d++) put_vec(o, L.sigma[d]);
+    }
+  }
   FILE *fp = fopen(path, "wb");
   if (!fp) return fail(std::string("cannot create structure output file ") + path);
   size_t w = fwrite(o.data(), 1, o.size(), fp);
@@ -3782,6 +3921,22 @@ int structure_load(mnl_structure *S, const char *path) {
   in.get(nb);
   T.boxes.assign(in.ok && nb < (1u << 20) ? nb : 0, BoxSpec{});
   for (auto &b : T.boxes) in.get(b);
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) T.mu1inv[c][d].clear();
+  T.hlor.clear();
+  if (in.ok && in.i < s.size()) {  // H-side section
+    uint64_t tag = 0, nh = 0;
+    in.get(tag);
+    if (tag != 0x4853494445ull) in.ok = false;
+    for (int c = 0; c < 3; c++)
+      for (int d = 0; d < 3; d++) in.get_vec(T.mu1inv[c][d]);
+    in.get(nh);
+    T.hlor.assign(in.ok && nh <= (uint64_t)MAX_HPOL ? nh : 0, Lorentz{});
+    for (auto &L : T.hlor) {
+      in.get(L.omega0), in.get(L.gamma), in.get(L.drude);
+      for (int d = 0; d < 3; d++) in.get_vec(L.sigma[d]);
+    }
+  }
   if (!in.ok || in.i != s.size()) return fail("structure file is truncated or corrupt");
   bool sizes_ok = true;  // every per-point array is absent or whole-cell
   auto chk = [&](const std::vector<double> &v) { sizes_ok = sizes_ok && (v.empty() || v.size() == T.ntot); };
@@ -3796,12 +3951,27 @@ int structure_load(mnl_structure *S, const char *path) {
     for (int c = 0; c < 3; c++)
       for (int d = 0; d < 3; d++) chk(L.off[c][d]);
   }
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++) chk(T.mu1inv[c][d]);
+  for (auto &L : T.hlor)
+    for (int d = 0; d < 3; d++) chk(L.sigma[d]);
   if (!sizes_ok) return fail("structure file holds an array of the wrong size");
   *S = std::move(T);
   return 0;
 }
 
 // ------------------------------------------------------------- array slices
+// H-side materials: H_d separate in the reference chunk holding the point at absolute
+// half-coordinates p (not counting PML along d; DevFields::hsep_zone / hsep_all)
+bool h_sep_zone(const mnl_fields *F, const int p[3], int d) {
+  if (!F->hall || !F->h_first_done) return false;
+  if (F->f.hsep_all) return true;
+  int zb = 0;
+  for (int e = 0; e < 3; e++)
+    zb = zb * 3 + (F->S.has[e] ? F->h_zone[e][p[e] - F->S.io[e]] : 1);
+  return (F->h_hsep_zone[zb] >> d) & 1;
+}
+
 // fields::get_array_slice(volume, c) for real fields without symmetry
 // (src/array_slice.cpp:251-433, 447-507, 525-601, 611-704): loop_in_chunks over
 // the Centered grid in the reference's chunks, each point the average of the
@@ -3827,7 +3997,7 @@ int copy_component_box(mnl_fields *F, int c, const int lo[3], const int hi[3],
   if (!has_field(S, c) || !F->allocated[c]) return 0;
   const int t = ctype(c), d = cdir(c);
   const double *src = t == T_E ? F->f.E[d] : t == T_D ? F->f.D[d] : F->f.B[d];
-  const double *hsep = t == T_H ? F->f.H[d] : nullptr;
+  const double *hsep = (t == T_H && !(F->hall && !F->h_first_done)) ? F->f.H[d] : nullptr;
   if (!src) return 0;
   if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
   double *buf = nullptr;
@@ -4067,7 +4237,7 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
               idx += (long long)(jb3[d] - hlo[d]) * hs[d];
             }
           double a4[4] = {hb[idx], hb[idx + o1], hb[idx + o2], hb[idx + o1 + o2]};
-          if (bq && F->h_zone[cd][p[cd] - S.io[cd]] == 1) {  // reader chunk aliases B to H
+          if (bq && F->h_zone[cd][p[cd] - S.io[cd]] == 1 && !h_sep_zone(F, p, cd)) {  // reader chunk aliases B to H
             for (int k = 0; k < 4; k++) {
               int jn[3] = {jb3[0], jb3[1], jb3[2]};
               if ((k & 1) && d1 >= 0) jn[d1]++;
@@ -4341,9 +4511,7 @@ int sync_magnetic(mnl_fields *F, MagBackup &bk) {
     HIPCHK(hipStreamSynchronize(F->stream));
   }
   if (!F->h_first_done && h_lazy_copy(F)) return -1;
-  bool anyH = false;
-  for (int d = 0; d < 3; d++) anyH = anyH || f.H[d];
-  if (anyH && k_update_h(F->shell_list, g, f, F->stream)) return fail("update H launch failed");
+  if (update_h_any(F, F->shell_list, false)) return -1;  // no update_pols here (reference)
   if (F->nranks > 1 && exchange(F, 1)) return fail("H halo exchange failed");
   for (auto &a : bk.avg)
     if (k_average(a.first, a.second, (long long)n, F->stream)) return fail("average launch failed");
@@ -4503,10 +4671,7 @@ int initialize_field(mnl_fields *F, int c, const double *host) {
     if (F->nranks > 1 && exchange(F, 0)) return fail("E halo exchange failed");
   } else if (t == T_B) {  // update_eh(H_stuff); step_boundaries(H_stuff)
     if (!F->h_first_done && h_lazy_copy(F)) return -1;
-    bool anyH = false;
-    for (int e = 0; e < 3; e++) anyH = anyH || f.H[e];
-    if (anyH && k_update_h(F->shell_list, F->g, f, F->stream))
-      return fail("update H launch failed");
+    if (update_h_any(F, F->shell_list, false)) return -1;  // update_eh(H_stuff) only
     if (F->nranks > 1 && exchange(F, 1)) return fail("H halo exchange failed");
   } else {
     F->force_unfused_next = true;  // E (or H) differs from what D (B) implies
@@ -4686,12 +4851,13 @@ int mnl_structure_add_pml(mnl_structure *s, int dir, int side, double thickness,
 }
 
 int mnl_structure_set_chi1inv(mnl_structure *s, int comp, int dir, const double *host) {
-  if (!s || comp < MNL_EX || comp > MNL_EZ || dir < 0 || dir > 2)
-    return fail("chi1inv: E components only");
+  if (!s || comp < MNL_EX || comp > MNL_HZ || dir < 0 || dir > 2)
+    return fail("chi1inv: E or H components only");
+  auto &dst = comp <= MNL_EZ ? s->chi1inv[comp][dir] : s->mu1inv[comp - MNL_HX][dir];
   if (host)
-    s->chi1inv[comp][dir].assign(host, host + s->ntot);
+    dst.assign(host, host + s->ntot);
   else
-    s->chi1inv[comp][dir].clear();
+    dst.clear();
   return 0;
 }
 int mnl_structure_set_chi2(mnl_structure *s, int comp, const double *host) {
@@ -4743,6 +4909,24 @@ int mnl_structure_add_lorentzian_tensor(mnl_structure *s, double omega0, double 
       if (all_eq(dst, 0.0)) dst.clear();
     }
   s->lor.push_back(std::move(L));
+  return 0;
+}
+int mnl_structure_add_magnetic_lorentzian(mnl_structure *s, double omega0, double gamma,
+                                          int drude, const double *sx, const double *sy,
+                                          const double *sz) {
+  if (!s) return fail("null argument");
+  if ((int)s->hlor.size() >= MAX_HPOL) return fail("too many magnetic susceptibilities (max 2)");
+  Lorentz L;
+  L.omega0 = omega0;
+  L.gamma = gamma;
+  L.drude = drude;
+  const double *sv[3] = {sx, sy, sz};
+  for (int d = 0; d < 3; d++) {
+    if (!sv[d]) continue;
+    L.sigma[d].assign(sv[d], sv[d] + s->ntot);
+    if (all_eq(L.sigma[d], 0.0)) L.sigma[d].clear();
+  }
+  s->hlor.push_back(std::move(L));
   return 0;
 }
 int mnl_structure_set_nonlinear_mode(mnl_structure *s, int mode) {
@@ -4962,9 +5146,9 @@ int mnl_structure_set_epsilon_geometry(mnl_structure *s, int device, int nobj, c
 }
 
 int mnl_structure_get_chi1inv(mnl_structure *s, int comp, int dir, double *host) {
-  if (!s || comp < MNL_EX || comp > MNL_EZ || dir < 0 || dir > 2)
-    return fail("chi1inv: E components only");
-  const auto &v = s->chi1inv[comp][dir];
+  if (!s || comp < MNL_EX || comp > MNL_HZ || dir < 0 || dir > 2)
+    return fail("chi1inv: E or H components only");
+  const auto &v = comp <= MNL_EZ ? s->chi1inv[comp][dir] : s->mu1inv[comp - MNL_HX][dir];
   if (v.empty()) return 1;
   if (host) memcpy(host, v.data(), sizeof(double) * v.size());
   return 0;
@@ -5225,7 +5409,7 @@ int mnl_fields_copy_component(mnl_fields *F, int comp, double *host, size_t n) {
     case T_B: src = F->f.B[d]; break;
     case T_H:
       src = F->f.B[d];
-      hsep = F->f.H[d];
+      hsep = (F->hall && !F->h_first_done) ? nullptr : F->f.H[d];
       break;
   }
   if (!src) return 0;

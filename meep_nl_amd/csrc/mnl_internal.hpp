@@ -16,6 +16,7 @@
 namespace mnl {
 
 constexpr int MAX_POL = 4;    // Lorentzian susceptibilities per structure
+constexpr int MAX_HPOL = 2;   // magnetic (H_stuff) Lorentzian susceptibilities
 constexpr int MAX_BOX = 7;    // interior + 6 shell boxes
 
 enum { T_E = 0, T_H = 1, T_D = 2, T_B = 3 };
@@ -129,6 +130,19 @@ struct DevFields {
   const uint8_t *cnd_zone;
   double cnd_dt2;            // dt * 0.5 (src/step_generic.cpp:92)
   int aniso;                 // some susceptibility has off-diagonal sigma
+  // H-side materials (mu != 1, magnetic Lorentzian).  hall = 1:
+  // H is stored at every point (update_hmat_kernel), a copy of B where the point's
+  // reference chunk aliases H to B (src/update_eh.cpp:204-209), and every reader of H
+  // reads that array.  hsep_zone: per zone box, bit d set if H_d is separate in that
+  // chunk for a reason other than PML along d (chi1inv[H_d] row kept, or f_minus_p of
+  // B allocated because a magnetic susceptibility needs P).
+  int hall;
+  const double *invmu[3];    // diagonal chi1inv of H comps (null = trivial)
+  const uint8_t *hsep_zone;
+  int hsep_all;              // some magnetic susceptibility needs P: f_minus_p of B in every
+                             // chunk, so H is separate everywhere
+  int nhpol;
+  PolDev hpol[MAX_HPOL];     // magnetic pol list (reverse of add order), isotropic sigma
 };
 
 // One reference chunk's integration box on a component grid (field energy):
@@ -197,6 +211,9 @@ struct Launch {
 int k_curl(int ft, const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
            const CurlPlan &p, double courant, void *stream, bool fuseup = false);
 int k_update_h(const BoxList &shell, const DevGrid &g, const DevFields &f, void *stream);
+// update_eh(H_stuff) [+ update_pols(H_stuff) if pols] over box b when H is stored
+// everywhere (f.hall)
+int k_update_hmat(const Box &b, const DevGrid &g, const DevFields &f, int pols, void *stream);
 int k_update_e(const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
                const ISrcDev &is, int step, bool fuse_pols, void *stream);
 int k_update_pols(const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,

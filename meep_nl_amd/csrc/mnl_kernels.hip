@@ -267,9 +267,9 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void curl_kernel(Box b, BoxList bl,
       } else {
         s1 = -s1;
         s2 = -s2;
-        g1 = f.Bn[c1];  // H == B (new) outside PML chunks
-        g2 = f.Bn[c2];
-        if (SHELL) {  // H separate only in chunks with PML along the H direction
+        g1 = f.hall ? f.Hn[c1] : f.Bn[c1];  // H == B (new) outside PML chunks
+        g2 = f.hall ? f.Hn[c2] : f.Bn[c2];
+        if (SHELL && !f.hall) {  // H separate only in chunks with PML along the H direction
           if (f.H[c1] && pml_at(f, g, c1, qcoord(g, p, T_H, c1, c1))) g1 = f.Hn[c1];
           if (f.H[c2] && pml_at(f, g, c2, qcoord(g, p, T_H, c2, c2))) g2 = f.Hn[c2];
         }
@@ -317,6 +317,65 @@ __global__ __launch_bounds__(MNL_BX *MNL_BY) void update_h_kernel(BoxList bl, De
     f.WH[d][i] = fw;
     f.Hn[d][i] = f.H[d][i] + ((kapwkw + sigwkw) * fw - (kapwkw - sigwkw) * fwprev);
   }
+}
+
+// ----------------------------------------------------------------- H-side materials
+// update_eh(H_stuff) (src/update_eh.cpp:67-283 -> step_update_EDHB, src/step_generic.cpp:
+// 576-906 with H = chi1inv_H * (B - P_H)) followed by update_pols(H_stuff) (isotropic
+// lorentzian update_P, src/susceptibility.cpp:251-258, W = f_w or H, update_pols.cpp:44)
+// when H is stored everywhere (f.hall: mu != 1 or magnetic susceptibilities).  The fork's
+// H update takes the diagonal branch whatever off-diagonal mu rows exist (its 3x3 branch
+// needs chi3, which no H component has), so only diag(chi1inv_H) enters.  Where the point's
+// reference chunk aliases H to B, H = B (a copy, so every reader reads one array).
+template <int d>
+__device__ __forceinline__ void h_point(const DevGrid &g, const DevFields &f, const Pt &p,
+                                        long long i, int pols) {
+  if (!f.hcomp_present[d] || !owned(g, T_H, d, p)) return;
+  const int kw = qcoord(g, p, T_H, d, d);
+  const bool pml = pml_at(f, g, d, kw);
+  int rz = 0;
+#pragma unroll
+  for (int e = 0; e < 3; e++) rz = rz * 3 + (g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, T_H, d, e)] : 1);
+  const bool sep = pml || f.hsep_all || ((f.hsep_zone[rz] >> d) & 1);
+  double *Hn = f.Hn[d];
+  double gs = f.Bn[d][i];
+  double wv;
+  if (!sep) {
+    Hn[i] = gs;
+    wv = gs;
+  } else {
+    for (int k = 0; k < f.nhpol; k++)  // subtract_P in pol-list order
+      if (f.hpol[k].P[d]) gs -= f.hpol[k].P[d][i];
+    const double *u = f.invmu[d];
+    const double v = u ? (gs * u[i]) : gs;
+    if (pml) {
+      const double fwprev = f.WH[d][i];
+      const double kapwkw = f.pml.kap[d][kw], sigwkw = f.pml.sig[d][kw];
+      f.WH[d][i] = v;
+      Hn[i] = f.H[d][i] + ((kapwkw + sigwkw) * v - (kapwkw - sigwkw) * fwprev);
+    } else {
+      Hn[i] = v;
+    }
+    wv = v;
+  }
+  for (int k = 0; k < (pols ? f.nhpol : 0); k++) {
+    const PolDev &pd = f.hpol[k];
+    if (!pd.P[d]) continue;
+    const double pcur = pd.P[d][i];
+    pd.P[d][i] = pd.gamma1inv * (pcur * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * pd.Pp[d][i] +
+                                 pd.omega0dtsqr * (pd.sigma[d][i] * wv));
+    pd.Pp[d][i] = pcur;
+  }
+}
+
+__global__ __launch_bounds__(MNL_BX *MNL_BY) void update_hmat_kernel(Box b, DevGrid g,
+                                                                      DevFields f, int pols) {
+  Pt p;
+  if (!make_pt(b, g, p)) return;
+  const long long i = p.idx;
+  h_point<0>(g, f, p, i, pols);
+  h_point<1>(g, f, p, i, pols);
+  h_point<2>(g, f, p, i, pols);
 }
 
 // ----------------------------------------------------------------- chi(2) NR
@@ -1076,7 +1135,7 @@ __global__ void to_box_kernel(double *dst, const double *src, const double *hsep
     if (g.ax[d] >= 0) cidx += (long long)(p.j[d] + g.off[d] - blo[d]) * bs[d];
   long long i = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
   double v = src[i];
-  if (hsep && pml_at(f, g, c, qcoord(g, p, T_H, c, c))) v = hsep[i];
+  if (hsep && (f.hall || pml_at(f, g, c, qcoord(g, p, T_H, c, c)))) v = hsep[i];
   p.idx = i;
   if (use_fb && type == T_E && e_implicit(f, g, c, p))  // fused: E = chi1inv * D (not stored)
     v = usrc ? (dsrc[i] * usrc[i]) : dsrc[i];
@@ -1333,6 +1392,13 @@ int k_curl(int ft, const Box &in, const BoxList *sh, const DevGrid &g, const Dev
         curl_kernel<T_D, true, false><<<grd, 256, 0, s>>>(in, *sh, g, f, p, courant);
     }
   }
+  return rc();
+}
+
+int k_update_hmat(const Box &b, const DevGrid &g, const DevFields &f, int pols, void *stream) {
+  if (empty(b)) return 0;
+  update_hmat_kernel<<<grid_for(b), dim3(MNL_BX, MNL_BY), 0, (hipStream_t)stream>>>(b, g, f,
+                                                                                      pols);
   return rc();
 }
 
@@ -3339,7 +3405,7 @@ __global__ void dft_sample_kernel(const int *__restrict__ pj, const double *__re
   }
   auto val = [&](const Pt &q) -> double {
     if (mag) {
-      const bool sep = f.H[d] && pml_at(f, g, d, qcoord(g, q, T_H, d, d));
+      const bool sep = f.H[d] && (f.hall || pml_at(f, g, d, qcoord(g, q, T_H, d, d)));
       return sep ? f.H[d][q.idx] : f.B[d][q.idx];
     }
     if (e_implicit(f, g, d, q)) {
@@ -3501,9 +3567,17 @@ __global__ void init_add_kernel(double *dst, double *alt, const double *src, Dev
     if (!shift_of(type, c, d) && p.j[d] + g.off[d] == g.nglob[d]) wall = true;
   }
   double *t = dst;
-  if (alt && !pml_at(f, g, c, qcoord(g, p, type, c, c))) t = alt;
+  bool sep = pml_at(f, g, c, qcoord(g, p, type, c, c));
+  if (f.hall && alt && !sep) {  // H-side materials: H separate in this point's chunk?
+    int rz = 0;
+    for (int e = 0; e < 3; e++) rz = rz * 3 + (g.ax[e] >= 0 ? f.zone[e][qcoord(g, p, type, c, e)] : 1);
+    sep = f.hsep_all || ((f.hsep_zone[rz] >> c) & 1);
+  }
+  if (alt && !sep) t = alt;
   const long long li = (long long)i0 + i1 * g.st[1] + i2 * g.st[2];
-  t[li] = wall ? 0.0 : t[li] + src[cidx];
+  const double v = wall ? 0.0 : t[li] + src[cidx];
+  t[li] = v;
+  if (f.hall && alt && !sep) dst[li] = v;  // the H copy of an aliasing chunk follows B
 }
 
 // ------------------------------------------------------------- energy
@@ -3546,7 +3620,7 @@ __global__ __launch_bounds__(256) void energy_kernel(const double *A, const doub
     // IVEC_LOOP_WEIGHT order: W(yd[2]) * (W(yd[1]) * (dV * W(yd[0])))
     const double wgt = w[box.yd[2]] * (w[box.yd[1]] * (box.dV0 * w[box.yd[0]]));
     const double *src = A;
-    if (Asep && pml_at(f, g, c, qcoord(g, p, type, c, c))) src = Asep;  // H separate here
+    if (Asep && (f.hall || pml_at(f, g, c, qcoord(g, p, type, c, c)))) src = Asep;  // H separate here
     const double x = src[li], y = Bv[li];
     const double xv = 0.25 * (((x + x) + x) + x), yv = 0.25 * (((y + y) + y) + y);
     const double t = (xv * yv) * wgt;

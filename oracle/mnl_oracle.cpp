@@ -411,6 +411,7 @@ struct Chunk {
 struct Lorentz {
   double omega0, gamma;
   bool drude;
+  int ft = T_E;  // E_stuff or H_stuff (structure::add_susceptibility(sigma, ft, ...))
   bool nontrivial[3];
   bool nt_off[3][3] = {};  // global (and_to_all) off-diagonal flags, structure.cpp:491-506
 };
@@ -440,7 +441,7 @@ struct orc_sim {
   std::vector<realnum> g_chi1inv[NCOMP][3], g_chi2[NCOMP], g_chi3[NCOMP];
   std::vector<realnum> g_cond[NCOMP];  // D / B comps
   std::vector<Lorentz> lor;
-  std::vector<std::vector<realnum>> g_lsig[3];  // per E-comp dir: per susceptibility
+  std::vector<std::vector<realnum>> g_lsig[3];  // per comp dir (E or H by Lorentz::ft): per susceptibility
   std::vector<std::vector<realnum>> g_lsig_off[3][3];  // [c][d], d != c: per susceptibility
   std::vector<SrcTime> srcs;
   void (*pending_func)(double, void *, double *, double *) = nullptr;  // custom source being added
@@ -679,7 +680,8 @@ void finalize(orc_sim *s) {
   build_chunks(s);
   for (auto &ch : s->chunks) {
     apply_pml(s, ch);
-    for (int c = Ex; c <= Ez; c++) {
+    // chi1inv of E (epsilon) and H (mu) components, set_chi1inv per chunk
+    for (int c : {Ex, Ey, Ez, Hx, Hy, Hz}) {
       if (!G.has_field(c)) continue;
       int dc = cdir(c);
       bool provided = false;
@@ -687,7 +689,7 @@ void finalize(orc_sim *s) {
       if (provided) {
         bool triv[3];
         for (int d = 0; d < 3; d++) {
-          if (!G.has_field(tcomp(T_E, d)) || s->g_chi1inv[c][d].empty()) {
+          if (!G.has_field(tcomp(ctype(c), d)) || s->g_chi1inv[c][d].empty()) {
             triv[d] = true;
             continue;
           }
@@ -698,6 +700,7 @@ void finalize(orc_sim *s) {
           if (d != dc && triv[d]) ch.chi1inv[c][d].clear();
         if (triv[0] && triv[1] && triv[2]) ch.chi1inv[c][dc].clear();
       }
+      if (is_magnetic(c)) continue;  // chi2 / chi3 of E components only
       // chi3 first (structure.cpp:381-383, 795-828)
       if (!s->g_chi3[c].empty()) {
         if (ch.chi1inv[c][dc].empty()) ch.chi1inv[c][dc].assign(ch.gv.ntot, 1.0);
@@ -743,15 +746,17 @@ void finalize(orc_sim *s) {
     ch.pol.assign(nl, PolData());
     for (size_t k = 0; k < nl; k++) {
       size_t src = nl - 1 - k;  // pol index k <- susceptibility added at position src
-      for (int c = Ex; c <= Ez; c++) {
-        if (!G.has_field(c)) continue;
+      const int ft = s->lor[src].ft;
+      for (int c = 0; c < 3; c++) {  // direction of the comp tcomp(ft, c)
+        const int cc = tcomp(ft, c);
+        if (!G.has_field(cc)) continue;
         // anisotropic_averaging.cpp:317-362: trivial off-diagonal arrays are
         // deleted per chunk, the diagonal one only if the whole row is trivial
         bool row = false;
         for (int d = 0; d < 3; d++) {
           if (d == c || s->g_lsig_off[c][d][src].empty()) continue;
           std::vector<realnum> v;
-          scatter_to_chunk(G, ch, c, s->g_lsig_off[c][d][src], v);
+          scatter_to_chunk(G, ch, cc, s->g_lsig_off[c][d][src], v);
           if (!all_equal(v, 0.0)) {
             ch.psoff[k * 9 + 3 * c + d] = std::move(v);
             row = true;
@@ -759,7 +764,7 @@ void finalize(orc_sim *s) {
         }
         std::vector<realnum> v;
         if (!s->g_lsig[c][src].empty())
-          scatter_to_chunk(G, ch, c, s->g_lsig[c][src], v);
+          scatter_to_chunk(G, ch, cc, s->g_lsig[c][src], v);
         else if (row)
           v.assign(ch.gv.ntot, 0.0);
         if (!v.empty() && (row || !all_equal(v, 0.0))) ch.psigma[k * 3 + c] = std::move(v);
@@ -817,8 +822,9 @@ void connect_chunks(orc_sim *s) {
             Chunk &cj = s->chunks[j];
             if (is_B(c) && ch.h_alias[cdir(c)] && cj.h_alias[cdir(c)]) continue;  // B_redundant
             s->conn[i].push_back({c, g.index(c, p), j, cj.gv.index(c, p)});
-            if (is_electric(c)) {
-              // Lorentzian P ghosts (num_cinternal_notowned_needed, susceptibility.cpp:283-288)
+            if (is_electric(c) || is_magnetic(c)) {
+              // Lorentzian P ghosts (num_cinternal_notowned_needed, susceptibility.cpp:283-288;
+              // PE_stuff / PH_stuff)
               s->pconn[i].push_back({c, g.index(c, p), j, cj.gv.index(c, p)});
             }
           }
@@ -875,15 +881,16 @@ void step_boundaries_W(orc_sim *s) {
   }
 }
 
-void step_boundaries_P(orc_sim *s) {  // PE_stuff
+void step_boundaries_P(orc_sim *s, int ft) {  // PE_stuff / PH_stuff
   if (!s->conn_valid) connect_chunks(s);
   for (size_t i = 0; i < s->chunks.size(); i++) {
     Chunk &ch = s->chunks[i];
     for (size_t k = 0; k < ch.pol.size(); k++) {
-      if (!ch.pol[k].allocated) continue;
+      if (!ch.pol[k].allocated || s->lor[s->lor.size() - 1 - k].ft != ft) continue;
       for (const auto &cn : s->pconn[i]) {
-        auto &dst = ch.pol[k].P[cn.c];
-        auto &src = s->chunks[cn.jc].pol[k].P[cn.c];
+        if (ctype(cn.c) != ft) continue;
+        auto &dst = ch.pol[k].P[cdir(cn.c)];
+        auto &src = s->chunks[cn.jc].pol[k].P[cdir(cn.c)];
         if (!dst.empty() && !src.empty()) dst[cn.dst] = src[cn.src];
       }
     }
@@ -1168,9 +1175,10 @@ void step_update_EDHB(orc_sim *s, const GV &g, realnum *f, int fc, const realnum
 // susceptibility::needs_P (susceptibility.cpp:76-82, global trivial flags): some
 // sigma[c][d] nontrivial whose W (E component d) exists
 bool lor_needs_P(const orc_sim *s, const Lorentz &L, int c) {
+  if (ctype(c) != L.ft) return false;
   for (int d = 0; d < 3; d++) {
     const bool nt = d == cdir(c) ? L.nontrivial[d] : L.nt_off[cdir(c)][d];
-    if (nt && s->allocated[tcomp(T_E, d)]) return true;
+    if (nt && s->allocated[tcomp(L.ft, d)]) return true;
   }
   return false;
 }
@@ -1205,7 +1213,7 @@ void update_eh(orc_sim *s, int ftype) {
       bool need_fmp = false;
       if (s->allocated[ec] && ch.F(ec)) {
         need_fmp = have_int_sources;
-        if (ftype == T_E && !need_fmp) need_fmp = pol_needs_P(s, ec);
+        if (!need_fmp) need_fmp = pol_needs_P(s, ec);
       }
       if (need_fmp) {
         if (ch.fmp[dc].empty()) ch.fmp[dc].assign(g.ntot, 0.0);
@@ -1218,17 +1226,17 @@ void update_eh(orc_sim *s, int ftype) {
       int ec = tcomp(ftype, d), dc = tcomp(ft2, d);
       if (s->allocated[ec] && !ch.fmp[dc].empty()) ch.fmp[dc] = ch.f[dc];  // memcpy(D)
     }
-    if (ftype == T_E)
-      for (auto &pd : ch.pol) {  // subtract_P, susceptibility.cpp:264-281
-        if (!pd.allocated) continue;
-        for (int d = 0; d < 3; d++) {
-          int dc = tcomp(T_D, d);
-          if (pd.P[d].empty() || ch.fmp[dc].empty()) continue;
-          realnum *fmp = ch.fmp[dc].data();
-          const realnum *p = pd.P[d].data();
-          for (size_t i = 0; i < g.ntot; ++i) fmp[i] -= p[i];
-        }
+    for (size_t k = 0; k < ch.pol.size(); k++) {  // subtract_P, susceptibility.cpp:264-281
+      const PolData &pd = ch.pol[k];
+      if (!pd.allocated || s->lor[s->lor.size() - 1 - k].ft != ftype) continue;
+      for (int d = 0; d < 3; d++) {
+        int dc = tcomp(ft2, d);
+        if (pd.P[d].empty() || ch.fmp[dc].empty()) continue;
+        realnum *fmp = ch.fmp[dc].data();
+        const realnum *p = pd.P[d].data();
+        for (size_t i = 0; i < g.ntot; ++i) fmp[i] -= p[i];
       }
+    }
     if (have_f_minus_p && ftype == T_E) {  // update_eh.cpp:136-146
       for (auto &sv : ch.srcD) {
         const SrcTime &st = s->srcs[sv.st];
@@ -1277,17 +1285,18 @@ void update_eh(orc_sim *s, int ftype) {
   }
 }
 
-// fields_chunk::update_pols + lorentzian update_P (isotropic), update_pols.cpp:40-62,
-// susceptibility.cpp:188-262
-void update_pols(orc_sim *s) {
+// fields_chunk::update_pols(ft) + lorentzian update_P (isotropic), update_pols.cpp:40-62,
+// susceptibility.cpp:188-262; E_stuff after update_eh(E), H_stuff after update_eh(H)
+void update_pols(orc_sim *s, int ft) {
   for (auto &ch : s->chunks) {
     const GV &g = ch.gv;
     for (size_t k = 0; k < ch.pol.size(); k++) {
       PolData &pd = ch.pol[k];
       const Lorentz &L = s->lor[s->lor.size() - 1 - k];
+      if (L.ft != ft) continue;
       if (!pd.allocated) {
         for (int d = 0; d < 3; d++)
-          if (s->allocated[tcomp(T_E, d)] && lor_needs_P(s, L, tcomp(T_E, d))) {
+          if (s->allocated[tcomp(ft, d)] && lor_needs_P(s, L, tcomp(ft, d))) {
             pd.P[d].assign(g.ntot, 0.0);
             pd.Pp[d].assign(g.ntot, 0.0);
           }
@@ -1304,7 +1313,7 @@ void update_pols(orc_sim *s) {
       };
       for (int d = 0; d < 3; d++) {
         if (pd.P[d].empty()) continue;
-        int c = tcomp(T_E, d);
+        int c = tcomp(ft, d);
         const realnum *w = W(c);
         const std::vector<realnum> &sv = ch.psigma[k * 3 + d];
         if (!w || sv.empty()) continue;
@@ -1314,7 +1323,7 @@ void update_pols(orc_sim *s) {
         const long is = g.s[d];
         int d1 = (d + 1) % 3, d2 = (d + 2) % 3;
         long is1 = g.s[d1], is2 = g.s[d2];
-        const realnum *w1 = W(tcomp(T_E, d1)), *w2 = W(tcomp(T_E, d2));
+        const realnum *w1 = W(tcomp(ft, d1)), *w2 = W(tcomp(ft, d2));
         auto off = [&](int dd) -> const realnum * {
           const auto &v = ch.psoff[k * 9 + 3 * d + dd];
           return v.empty() ? nullptr : v.data();
@@ -1374,6 +1383,8 @@ void step_once(orc_sim *s) {  // fields::step, src/step.cpp:35-140
   step_boundaries(s, T_B);
   calc_sources(s, time + 0.5 * s->dt);
   update_eh(s, T_H);
+  update_pols(s, T_H);
+  step_boundaries_P(s, T_H);
   step_boundaries(s, T_H);
   calc_sources(s, time + 0.5 * s->dt);
   step_db(s, T_D);
@@ -1382,8 +1393,8 @@ void step_once(orc_sim *s) {  // fields::step, src/step.cpp:35-140
   calc_sources(s, time + s->dt);
   update_eh(s, T_E);
   step_boundaries_W(s);
-  update_pols(s);
-  step_boundaries_P(s);
+  update_pols(s, T_E);
+  step_boundaries_P(s, T_E);
   step_boundaries(s, T_E);
   s->t += 1;
   update_dfts(s);
@@ -1690,7 +1701,7 @@ int orc_add_pml(orc_sim *s, int dir, int side, double thickness, double R, doubl
 
 int orc_set_chi1inv(orc_sim *s, int comp, int dir, const double *arr) {
   if (s->finalized) return set_err("structure already finalized");
-  if (comp < Ex || comp > Ez || dir < 0 || dir > 2) return set_err("chi1inv: E components only");
+  if (comp < Ex || comp > Hz || dir < 0 || dir > 2) return set_err("chi1inv: E or H components only");
   if (arr)
     s->g_chi1inv[comp][dir].assign(arr, arr + s->gv.ntot);
   else
@@ -1736,13 +1747,25 @@ int orc_add_lorentzian(orc_sim *s, double omega0, double gamma, int drude, const
 // caller samples the off-diagonal entries half a pixel back along c, 334-341)
 int orc_add_lorentzian_tensor(orc_sim *s, double omega0, double gamma, int drude,
                               const double *const sig[9]) {
+  return orc_add_susceptibility(s, T_E, omega0, gamma, drude, sig);
+}
+
+// structure::add_susceptibility(sigma, ft, lorentzian_susceptibility) for E_stuff
+// (ft 0) or H_stuff (ft 1, magnetic: sigma at the H components' Yee points)
+int orc_add_susceptibility(orc_sim *s, int ft, double omega0, double gamma, int drude,
+                           const double *const sig[9]) {
   if (s->finalized) return set_err("structure already finalized");
+  if (ft != T_E && ft != T_H) return set_err("susceptibility: E_stuff or H_stuff");
+  for (int c = 0; c < 3; c++)
+    for (int d = 0; d < 3; d++)
+      if (ft == T_H && d != c && sig[3 * c + d])
+        return set_err("magnetic susceptibilities: diagonal sigma only");
   for (int c = 0; c < 3; c++)
     for (int d = 0; d < 3; d++) {
       if (d == c) continue;
       std::vector<realnum> v;
       bool nt = false;
-      if (sig[3 * c + d] && s->gv.has_field(tcomp(T_E, c))) {
+      if (sig[3 * c + d] && s->gv.has_field(tcomp(ft, c))) {
         v.assign(sig[3 * c + d], sig[3 * c + d] + s->gv.ntot);
         nt = !all_equal(v, 0.0);
       }
@@ -1755,10 +1778,11 @@ int orc_add_lorentzian_tensor(orc_sim *s, double omega0, double gamma, int drude
   L.omega0 = omega0;
   L.gamma = gamma;
   L.drude = drude != 0;
+  L.ft = ft;
   for (int d = 0; d < 3; d++) {
     std::vector<realnum> v;
     L.nontrivial[d] = false;
-    if (sv[d] && s->gv.has_field(tcomp(T_E, d))) {
+    if (sv[d] && s->gv.has_field(tcomp(ft, d))) {
       v.assign(sv[d], sv[d] + s->gv.ntot);
       L.nontrivial[d] = !all_equal(v, 0.0);
     }

@@ -33,6 +33,10 @@ int orc_add_lorentzian(orc_sim *s, double omega0, double gamma, int drude, const
 /* sigma tensor: sig[3*c + d] (row of E comp c, column d; NULL = 0) */
 int orc_add_lorentzian_tensor(orc_sim *s, double omega0, double gamma, int drude,
                               const double *const sig[9]);
+/* add_susceptibility(sigma, ft, lorentzian) with ft 0 = E_stuff, 1 = H_stuff
+ * (magnetic: diagonal sigma only, at the H components' points). */
+int orc_add_susceptibility(orc_sim *s, int ft, double omega0, double gamma, int drude,
+                           const double *const sig[9]);
 int orc_add_point_source(orc_sim *s, int comp, int kind, const double *params, int nparams,
                          const double pos[3], double amp_re, double amp_im, int is_integrated);
 int orc_add_custom_point_source(orc_sim *s, int comp,

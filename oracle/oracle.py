@@ -51,6 +51,8 @@ def lib():
         L.orc_add_lorentzian_tensor.argtypes = [c_void, ctypes.c_double, ctypes.c_double, c_int,
                                                 ctypes.POINTER(dptr)]
         L.orc_add_lorentzian.argtypes = [c_void, c_double, c_double, c_int, dptr, dptr, dptr]
+        L.orc_add_susceptibility.argtypes = [c_void, c_int, c_double, c_double, c_int,
+                                             ctypes.POINTER(dptr)]
         L.orc_add_point_source.argtypes = [c_void, c_int, c_int, dptr, c_int, dptr, c_double,
                                            c_double, c_int]
         L.orc_require_component.argtypes = [c_void, c_int]
@@ -273,6 +275,25 @@ class Oracle:
         s = [None if v is None else np.ascontiguousarray(v, dtype=np.float64).ravel()
              for v in sigmas]
         _chk(lib().orc_add_lorentzian(self.h, omega0, gamma, int(drude), *[_dp(v) for v in s]))
+
+    def add_magnetic_lorentzian(self, omega0, gamma, sigmas, drude=False):
+        """add_susceptibility(sigma, H_stuff, lorentzian): diagonal sigma at the H
+        components' points (None = 0)."""
+        arrs = [None] * 9
+        for d in range(3):
+            if sigmas[d] is not None:
+                arrs[4 * d] = np.ascontiguousarray(sigmas[d], dtype=np.float64).ravel()
+        self._keep = getattr(self, "_keep", []) + [a for a in arrs if a is not None]
+        ptrs = (ctypes.POINTER(ctypes.c_double) * 9)(*[_dp(a) if a is not None else None for a in arrs])
+        _chk(lib().orc_add_susceptibility(self.h, 1, omega0, gamma, int(drude), ptrs))
+
+    def set_mu_fn(self, fn):
+        """Non-averaged mu: chi1inv of the H components = 1/mu(loc) (set_mu)."""
+        for c in (Hx, Hy, Hz):
+            if self.dim == 1 and c != Hy:
+                continue
+            pts = self.coords(c)
+            self.set_chi1inv(c, c % 3, 1.0 / fn(*pts))
 
     # ---- fields
     def add_point_source(self, comp, kind, params, pos, amp=1.0, is_integrated=False):

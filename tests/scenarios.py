@@ -61,6 +61,12 @@ class ProductSim:
     def set_chi3(self, c, arr):
         self.s.set_chi3(c, arr)
 
+    def set_mu_fn(self, fn):
+        self.s.set_mu_fn(fn)
+
+    def add_magnetic_lorentzian(self, *a, **k):
+        self.s.add_magnetic_lorentzian(*a, **k)
+
     def set_conductivity(self, c, arr):
         self.s.set_conductivity(c, arr)
 
@@ -1181,5 +1187,78 @@ def sc_c4_nr(make, steps=25, n=256):
         del x, y, z, slab, box, inner, off
     o.add_lorentzian(1.1, 0.05, sig)
     o.add_gaussian_source(0, 0.3, 5.0, 0.0, 50.0, (0.05, 0.05, -3.0), 50.0)
+    o.step(steps)
+    return o
+
+
+# ------------------------------------------------------------------ H-side materials
+# mu != 1 (chi1inv of the H components, structure::set_mu) and magnetic Lorentzian
+# susceptibilities (update_eh(H_stuff) + update_pols(H_stuff), src/step.cpp:75-92,
+# src/update_eh.cpp:67-283): DESIGN.md section 23.
+
+def _box_fn(lo, hi, inside, outside=1.0):
+    def fn(*p):
+        m = np.ones_like(p[0], dtype=bool)
+        for k, x in enumerate(p):
+            m &= (x > lo[k]) & (x < hi[k])
+        return np.where(m, inside, outside)
+    return fn
+
+
+def sc_mu_1d(make, steps=300, lorentz=False):
+    """1-D: a mu = 3 slab inside the cell, PML at both ends, Ex Gaussian current."""
+    o = vol(make, 1, [12.0], 10, center_origin=True)
+    o.add_pml(1.0)
+    o.set_mu_fn(_box_fn((-1.5,), (2.0,), 3.0))
+    if lorentz:  # magnetic Drude-Lorentz slab overlapping the mu slab
+        z = o.coords(4)[-1]
+        o.add_magnetic_lorentzian(1.1, 0.05, [None, np.where(np.abs(z - 1.0) < 1.5, 0.5, 0.0), None])
+    o.add_gaussian_source(0, 0.3, 3.0, 0.0, 30.0, (0, 0, -3.0), 1.0)
+    o.step(steps)
+    return o
+
+
+def sc_mu_2d(make, te=True, steps=120, lorentz=False):
+    """2-D TE (Hz source) or TM (Ez source): an anisotropic (diagonal) mu block that
+    crosses the one-sided PML chunk boundary, odd grid."""
+    o = vol(make, 2, [3.1, 2.7], 10)
+    o.add_pml(0.5, dirs=(0,), sides=(1,))
+    o.add_pml(0.4, dirs=(1,), sides=(0,))
+    for c, m in ((3, 2.0), (4, 1.5), (5, 3.0)):
+        o.set_chi1inv(c, c % 3, 1.0 / _box_fn((1.0, 0.2), (3.0, 1.6), m)(*o.coords(c)))
+    if lorentz:
+        sig = []
+        for c in (3, 4, 5):
+            sig.append(_box_fn((0.5, 0.9), (2.0, 2.2), 0.4, 0.0)(*o.coords(c)))
+        o.add_magnetic_lorentzian(0.8, 0.1, sig)
+    if te:
+        o.add_gaussian_source(5, 0.4, 3.0, 0.0, 30.0, (1.03, 0.77), 2.0)
+    else:
+        o.add_gaussian_source(2, 0.4, 3.0, 0.0, 30.0, (1.03, 0.77), 2.0)
+    o.step(steps)
+    return o
+
+
+def sc_mu_3d(make, steps=40, lorentz=False, offdiag=False, eps=True, sizes=(3.2, 3.0, 3.4)):
+    """3-D with PML: a mu block crossing PML chunks (diagonal mu 2 / 3 / 1.5), an eps
+    waveguide, optionally a magnetic Lorentzian box and an off-diagonal mu row confined
+    to the +x PML chunk (inert in the fork's H update, but it keeps H separate there)."""
+    o = vol(make, 3, list(sizes), 10, center_origin=True)
+    o.add_pml(0.7)
+    lo, hi = (-0.6, -0.9, -2.0), (1.2, 0.5, 0.3)
+    for c, m in ((3, 2.0), (4, 3.0), (5, 1.5)):
+        o.set_chi1inv(c, c % 3, 1.0 / _box_fn(lo, hi, m)(*o.coords(c)))
+    if offdiag:
+        x, y, z = o.coords(4)
+        o.set_chi1inv(4, 0, np.where(x > 1.05, 1e-3, 0.0))
+    if eps:
+        for c in (0, 1, 2):
+            o.set_chi1inv(c, c, 1.0 / _box_fn((-9, -0.4, -0.3), (9, 0.4, 0.3), 6.0)(*o.coords(c)))
+    if lorentz:
+        sig = [_box_fn((-0.8, -0.5, -0.6), (0.6, 1.3, 1.5), 0.6, 0.0)(*o.coords(c)) for c in (3, 4, 5)]
+        o.add_magnetic_lorentzian(0.9, 0.08, sig)
+        o.add_magnetic_lorentzian(1.0, 0.2, [None, sig[1] * 0.5, None], drude=True)
+    o.add_gaussian_source(2, 0.3, 3.0, 0.0, 30.0, (0.05, -0.15, 0.1), 1.0)
+    o.add_gaussian_source(4, 0.35, 3.0, 0.0, 30.0, (-0.3, 0.2, -0.4), 0.5)
     o.step(steps)
     return o

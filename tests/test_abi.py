@@ -45,8 +45,11 @@ def test_structure_host_calls(libpath):
     s.set_chi2(0, np.zeros(gv.shape()))
     s.add_lorentzian(1.0, 0.1, [np.ones(gv.shape()), None, None])
     s.set_box(0, [-0.1, 0.1, -0.1, 0.1, -0.1, 0.1], 4.0)
+    s.set_chi1inv(5, 2, np.full(gv.shape(), 0.25))  # mu of Hz (set_mu)
+    assert np.array_equal(s.get_chi1inv(5, 2), np.full(gv.shape(), 0.25))
+    s.add_magnetic_lorentzian(1.0, 0.1, [None, np.ones(gv.shape()), None])
     with pytest.raises(RuntimeError):
-        s.set_chi1inv(5, 0, np.ones(gv.shape()))  # H has no chi1inv here
+        s.set_chi1inv(8, 0, np.ones(gv.shape()))  # D has no chi1inv
 
 
 def test_errors_are_meep_aborts(libpath):
