@@ -33,6 +33,9 @@ enum {
   MNL_EX = 0, MNL_EY, MNL_EZ, MNL_HX, MNL_HY, MNL_HZ,
   MNL_DX, MNL_DY, MNL_DZ, MNL_BX, MNL_BY, MNL_BZ, MNL_NUM_COMPONENTS
 };
+/* derived components of array slices (the reference's Dielectric / Permeability,
+ * src/meep/vec.hpp:52-53): epsilon / mu on the Centered grid from the diagonal chi1inv */
+enum { MNL_DIELECTRIC = 12, MNL_PERMEABILITY = 13 };
 enum { MNL_X = 0, MNL_Y = 1, MNL_Z = 2 };
 enum { MNL_LOW = 0, MNL_HIGH = 1 };
 enum { MNL_SRC_GAUSSIAN = 0, MNL_SRC_CONTINUOUS = 1, MNL_SRC_CUSTOM = 2 };
@@ -253,6 +256,14 @@ int mnl_fields_initialize_field(mnl_fields *f, int comp, const double *host, siz
 /* t (timesteps) and dt; time() = t*dt, round_time() = float(t*dt)
  * (src/meep.hpp:1891-1892). */
 int mnl_fields_time(mnl_fields *f, long long *t, double *dt);
+/* fields::t = t (the Python binding's fields.t assignment, python/simulation.py
+ * restart_fields). */
+int mnl_fields_set_time(mnl_fields *f, long long t);
+/* fields::zero_fields (src/fields.cpp:638-664): all field / auxiliary arrays and the
+ * polarizations to 0 (DFT accumulators kept). */
+int mnl_fields_zero_fields(mnl_fields *f);
+/* fields::remove_sources (src/fields.cpp:601-610). */
+int mnl_fields_remove_sources(mnl_fields *f);
 /* fields::get_field(c, vec) with 8-point interpolation
  * (src/monitor.cpp:127-160, src/vec.cpp:558-621).  Distributed: every rank
  * returns the global value (sum over ranks, as get_field(..., parallel=true)). */
@@ -263,6 +274,8 @@ int mnl_fields_get_field(mnl_fields *f, int comp, const double pos[3], double *o
  * are filled, the rest is 0 (sum over ranks gives the global array). */
 int mnl_fields_copy_component(mnl_fields *f, int comp, double *host, size_t n);
 /* fields::get_array_slice(volume, c) (src/array_slice.cpp:611-704, with
+ * comp = MNL_DIELECTRIC / MNL_PERMEABILITY: src/array_slice.cpp:385-408, the
+ * Dielectric / Permeability slices of Simulation.get_epsilon / get_mu;
  * get_array_slice_dimensions 447-507): the component on the Centered grid
  * points of the volume [vmin, vmax] (average of its Yee neighbours), empty
  * dimensions interpolated and collapsed (snap = 0) or snapped to the

@@ -4,8 +4,8 @@
 time stepper; ``meep_nl_amd.core`` mirrors the C++ structure/fields API.
 Both call libmnl.so (HIP kernels for gfx950 + C-ABI, include/meep_nl_amd.h).
 """
-from .core import (Bx, By, Bz, Dx, Dy, Dz, Ex, Ey, Ez, Fields, GridVolume, Hx, Hy, Hz,
-                   Structure, X, Y, Z, device_count)
+from .core import (Bx, By, Bz, Dielectric, Dx, Dy, Dz, Ex, Ey, Ez, Fields, GridVolume, Hx, Hy,
+                   Hz, Permeability, Structure, X, Y, Z, device_count)
 from .simulation import (ALL, AUTOMATIC, Block, ContinuousSource, CustomSource, Cylinder,
                          DftFields, DftFlux, Sphere,
                          DrudeSusceptibility,

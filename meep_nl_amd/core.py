@@ -19,6 +19,7 @@ from . import _lib
 from ._lib import check, dptr, lib, ptr
 
 Ex, Ey, Ez, Hx, Hy, Hz, Dx, Dy, Dz, Bx, By, Bz = range(12)
+Dielectric, Permeability = 12, 13  # derived slice components (src/meep/vec.hpp:52-53)
 X, Y, Z = 0, 1, 2
 
 # meep::time_sink (src/meep.hpp:1610-1633) and the print_times labels
@@ -403,6 +404,19 @@ class Fields:
     @property
     def t(self):
         return self._time()[0]
+
+    @t.setter
+    def t(self, value):  # the SWIG binding's fields.t assignment
+        check(lib().mnl_fields_set_time(self.h, int(value)))
+
+    def zero_fields(self):
+        """fields::zero_fields (src/fields.cpp:638-664); DFT accumulators are kept."""
+        check(lib().mnl_fields_zero_fields(self.h))
+
+    def remove_sources(self):
+        """fields::remove_sources (src/fields.cpp:601-610)."""
+        check(lib().mnl_fields_remove_sources(self.h))
+        self._last_times = []
 
     @property
     def dt(self):

@@ -4013,6 +4013,29 @@ int copy_component_box(mnl_fields *F, int c, const int lo[3], const int hi[3],
   return 0;
 }
 
+// Diagonal chi1inv of E (t = T_E, epsilon) or H (mu) component k at global index j, as
+// structure_chunk::get_chi1inv_at_pt returns it (src/structure.cpp; 1 where the row is
+// absent or was deleted as trivial): the host arrays, then the epsilon boxes rasterised
+// exactly as box_fill_kernel does (later boxes win).
+double mat_diag_at(const mnl_structure &S, int t, int k, const int j[3]) {
+  const auto &v = t == T_E ? S.chi1inv[k][k] : S.mu1inv[k][k];
+  long long idx = 0;
+  for (int d = 0; d < 3; d++) idx += (long long)j[d] * S.cstride(d);
+  double val = v.empty() ? 1.0 : v[idx];
+  if (t == T_E)
+    for (const BoxSpec &b : S.boxes) {
+      if (b.kind != 0) continue;
+      bool in = true;
+      for (int d = 0; d < 3 && in; d++) {
+        if (!S.has[d]) continue;
+        const double pos = (S.io[d] + 2 * j[d] + S.shift(k, d)) * (0.5 * (1.0 / S.a));
+        in = !(pos < b.box[2 * d] || pos > b.box[2 * d + 1]);
+      }
+      if (in) val = 1.0 / b.value;
+    }
+  return val;
+}
+
 int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3], int snap,
                 int *rank, long long dims[3], double *out, long long nout) {
   const mnl_structure &S = F->S;
@@ -4112,6 +4135,70 @@ int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3]
   long long ntot = 1;
   for (int k = 0; k < r; k++) ntot *= full[k];
   std::vector<double> arr(ntot, 0.0);
+  if (c == MNL_DIELECTRIC || c == MNL_PERMEABILITY) {
+    // Dielectric / Permeability (src/array_slice.cpp:385-408, 649-676): per centred point
+    // (4 n) / sum over the n E (H) components of the grid of the four diagonal chi1inv
+    // values at the component's yee2cent points, times the empty-dimension weights;
+    // from the host structure every rank holds (no device access, no collective)
+    const int t = c == MNL_DIELECTRIC ? T_E : T_H;
+    std::vector<int> ks;
+    for (int k = 0; k < 3; k++)
+      if (has_field(S, 3 * t + k)) ks.push_back(k);
+    bool empty_dim[3];
+    for (int d = 0; d < 3; d++) empty_dim[d] = S.has[d] && vmax[d] - vmin[d] == 0.0;
+    const int yd[3] = {S.dim == 2 ? 2 : 0, S.dim == 2 ? 0 : 1, S.dim == 2 ? 1 : 2};
+    for (auto &L : loops) {
+      int n[3];
+      for (int k = 0; k < 3; k++) n[k] = S.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
+      for (int i1 = 0; i1 < n[0]; i1++)
+        for (int i2 = 0; i2 < n[1]; i2++)
+          for (int i3 = 0; i3 < n[2]; i3++) {
+            const int ii[3] = {i1, i2, i3};
+            int p[3] = {0, 0, 0};
+            for (int k = 0; k < 3; k++)
+              if (S.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
+            double w[3];
+            for (int k = 0; k < 3; k++) {
+              const int d = yd[k];
+              w[k] = empty_dim[d] ? loop_w1(L.s0[d], L.s1[d], L.e0[d], L.e1[d], ii[k], n[k])
+                                  : loop_w1(1.0, 1.0, 1.0, 1.0, ii[k], n[k]);
+            }
+            const double wt = w[2] * (w[1] * (1.0 * w[0]));
+            cplx tr(0.0, 0.0);
+            for (int k : ks) {
+              const int ck = 3 * t + k;
+              int j0[3] = {0, 0, 0}, o[2] = {-1, -1}, no = 0;
+              for (int d = 0; d < 3; d++)
+                if (S.has[d]) {
+                  j0[d] = (p[d] - S.io[d]) / 2;
+                  if (!S.shift(ck, d)) o[no++] = d;
+                }
+              double v[4];
+              for (int q = 0; q < 4; q++) {
+                int jq[3] = {j0[0], j0[1], j0[2]};
+                if ((q & 1) && o[0] >= 0) jq[o[0]]++;
+                if ((q & 2) && o[1] >= 0) jq[o[1]]++;
+                v[q] = mat_diag_at(S, t, k, jq);
+              }
+              tr += v[0] + v[1] + v[2] + v[3];
+              if (std::abs(tr) == 0.0) tr += 4.0;
+            }
+            const cplx val = wt * (4.0 * (double)ks.size()) / tr;
+            long long oi = 0;
+            for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
+            arr[oi] = real(val);
+          }
+    }
+    for (long long q = 0; q < ntot; q++) {  // collapse_array: in full-index order
+      long long tq = q, ri = 0;
+      for (int k = r - 1; k >= 0; k--) {
+        ri += (tq % full[k]) * rs[k];
+        tq /= full[k];
+      }
+      out[ri] += arr[q];
+    }
+    return 0;
+  }
   // c's global indices the slice reads: the base point of each centred point
   // and +1 along c's unshifted directions (the four Yee values, o1 / o2)
   bool unsh[3];
@@ -5349,7 +5436,9 @@ int mnl_fields_set_nan_check(mnl_fields *F, int every) {
 
 int mnl_fields_array_slice(mnl_fields *F, int comp, const double vmin[3], const double vmax[3],
                            int snap, int *rank, long long dims[3], double *out, long long nout) {
-  if (!F || check_comp(comp) || !vmin || !vmax || !rank || !dims) return fail("bad argument");
+  if (!F || !vmin || !vmax || !rank || !dims) return fail("bad argument");
+  if (comp != MNL_DIELECTRIC && comp != MNL_PERMEABILITY && check_comp(comp))
+    return fail("bad argument");
   return array_slice(F, comp, vmin, vmax, snap, rank, dims, out, nout);
 }
 
@@ -5383,6 +5472,35 @@ int mnl_fields_time(mnl_fields *F, long long *t, double *dt) {
   if (!F) return fail("null fields");
   if (t) *t = F->t;
   if (dt) *dt = F->dt;
+  return 0;
+}
+
+int mnl_fields_set_time(mnl_fields *F, long long t) {
+  if (!F || t < 0) return fail("bad argument");
+  F->t = t;
+  return 0;
+}
+
+int mnl_fields_zero_fields(mnl_fields *F) {
+  // fields_chunk::zero_fields (src/fields.cpp:638-664): every field, f_u, f_w and f_cond
+  // array to 0 and the polarizations re-initialised (P = P_prev = 0); the DFT
+  // accumulators are kept.  Leaves fused mode first (its ping-pong partners are
+  // rebuilt from the zeroed arrays when it is entered again).
+  if (!F) return fail("null fields");
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  if (F->fused && set_fused(F, false)) return -1;
+  for (const CkEntry &e : ckpt_entries(F))
+    if (e.kind != 11) HIPCHK(hipMemsetAsync(e.p, 0, e.n * sizeof(double), F->stream));
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
+int mnl_fields_remove_sources(mnl_fields *F) {
+  // fields::remove_sources (src/fields.cpp:601-610): every source and its src_time
+  if (!F) return fail("null fields");
+  F->groups.clear();
+  F->srcs.clear();
+  F->src_dirty = true;
   return 0;
 }
 

@@ -18,7 +18,7 @@ import warnings
 import numpy as np
 
 from . import core
-from .core import Bx, By, Bz, Dx, Dy, Dz, Ex, Ey, Ez, Hx, Hy, Hz, X, Y, Z
+from .core import Bx, By, Bz, Dielectric, Dx, Dy, Dz, Ex, Ey, Ez, Hx, Hy, Hz, Permeability, X, Y, Z
 
 ALL = -1
 Low, High = 0, 1
@@ -92,7 +92,8 @@ class Medium:
     def __init__(self, epsilon=1.0, epsilon_diag=None, epsilon_offdiag=None, E_chi2=0.0,
                  E_chi3=0.0, chi2=None, chi3=None, E_susceptibilities=(), index=None, mu=1.0,
                  D_conductivity=None, B_conductivity=None, D_conductivity_diag=None,
-                 B_conductivity_diag=None):
+                 B_conductivity_diag=None, mu_diag=None, mu_offdiag=None,
+                 H_susceptibilities=()):
         if index is not None:
             epsilon = index * index
         self.epsilon_diag = Vector3(*(epsilon_diag if epsilon_diag is not None else
@@ -107,8 +108,14 @@ class Medium:
                                              else (D_conductivity or 0.0,) * 3))
         self.B_conductivity_diag = Vector3(*(B_conductivity_diag if B_conductivity_diag is not None
                                              else (B_conductivity or 0.0,) * 3))
-        if mu != 1.0:
-            raise NotImplementedError("magnetic materials (mu != 1) are outside the hot-path scope")
+        # permeability (python/geom.py Medium: mu_diag / mu_offdiag = (xy, xz, yz)) and
+        # magnetic susceptibilities (H_susceptibilities; diagonal sigma only here)
+        self.mu_diag = Vector3(*(mu_diag if mu_diag is not None else (mu, mu, mu)))
+        self.mu_offdiag = Vector3(*(mu_offdiag if mu_offdiag is not None else (0, 0, 0)))
+        self.H_susceptibilities = list(H_susceptibilities)
+        for su in self.H_susceptibilities:
+            if su.sigma_offdiag != Vector3():
+                raise NotImplementedError("magnetic susceptibilities: diagonal sigma only")
 
 
 vacuum = air = Medium()
@@ -820,6 +827,7 @@ class Simulation:
                                 [sig(m, col=col) for m in mats_o], dtype=np.float64)[which_o]
         for key in sus_keys:
             s.add_lorentzian_tensor(key[0], key[1], sus_sig[key], drude=key[2])
+        self._init_h_materials(gv, s, media)
         # structure::set_materials -> set_conductivity(c, mat) for the D and B
         # components with nonzero conductivity (src/structure.cpp:378-380, 868-905),
         # sampled at each component's own Yee points
@@ -833,6 +841,53 @@ class Simulation:
                                                dtype=np.float64)[which])
         self.structure = s
         return s
+
+    def _init_h_materials(self, gv, s, media):
+        """structure::set_mu (chi1inv of the H components, sampled at the H Yee points:
+        no subpixel averaging of mu here) and add_susceptibility(sigma, H_stuff, ...) for
+        the media's H_susceptibilities (src/anisotropic_averaging.cpp:221-372)."""
+        need_mu = any(m.mu_diag != Vector3(1, 1, 1) or m.mu_offdiag != Vector3() for m in media)
+        hkeys = []
+        for m in media:
+            for su in m.H_susceptibilities:
+                if su.key() not in hkeys:
+                    hkeys.append(su.key())
+        if not need_mu and not hkeys:
+            return
+        if need_mu and self.eps_averaging and len(self.geometry) > 0:
+            warnings.warn("mu is sampled at the H Yee points (no subpixel averaging of mu)",
+                          RuntimeWarning)
+        comps = (Hy,) if self.dimensions == 1 else (Hx, Hy, Hz)
+        hsig = {k: [None, None, None] for k in hkeys}
+        for c in comps:
+            d = c % 3
+            which, mats = self._materials_at(gv, c)
+            if need_mu:
+                inv = []
+                for m in mats:
+                    e, o = m.mu_diag, m.mu_offdiag
+                    T = np.array([[e.x, o.x, o.y], [o.x, e.y, o.z], [o.y, o.z, e.z]])
+                    inv.append(np.linalg.inv(T) if any(v != 0 for v in o) else
+                               np.diag([1.0 / e.x, 1.0 / e.y, 1.0 / e.z]))
+                inv = np.array(inv)
+                s.set_chi1inv(c, d, inv[:, d, d][which])
+                if any(m.mu_offdiag != Vector3() for m in mats):
+                    for k in (1, 2):
+                        s.set_chi1inv(c, (d + k) % 3, inv[:, d, (d + k) % 3][which])
+            for key in hkeys:
+                def sig(m, key=key, row=d):
+                    for su in m.H_susceptibilities:
+                        if su.key() == key:
+                            return su.sigma_row(row)[row]
+                    return 0.0
+                hsig[key][d] = np.array([sig(m) for m in mats], dtype=np.float64)[which]
+        for key in hkeys:
+            s.add_magnetic_lorentzian(key[0], key[1], hsig[key], drude=key[2])
+
+    def has_mu(self):
+        """Simulation.has_mu (python/simulation.py): some medium has mu != 1."""
+        media = [self.default_material] + [g.material for g in self.geometry]
+        return any(m.mu_diag != Vector3(1, 1, 1) or m.mu_offdiag != Vector3() for m in media)
 
     def init_sim(self):
         if self.fields is not None:
@@ -1174,6 +1229,58 @@ class Simulation:
             arr[...] = out
             return arr
         return out
+
+    def get_epsilon(self, frequency=0, snap=False):
+        """Simulation.get_epsilon (python/simulation.py:4603-4604) = get_array(Dielectric):
+        epsilon on the Centered grid from the diagonal chi1inv (src/array_slice.cpp:385-396)."""
+        return self.get_array(component=Dielectric, frequency=frequency, snap=snap)
+
+    def get_mu(self, frequency=0, snap=False):
+        """Simulation.get_mu = get_array(Permeability) (src/array_slice.cpp:397-408)."""
+        return self.get_array(component=Permeability, frequency=frequency, snap=snap)
+
+    def change_sources(self, new_sources):
+        """Simulation.change_sources (python/simulation.py:4454-4463): replace the
+        sources, in the running fields too (fields::remove_sources + add_source)."""
+        self.sources = list(new_sources)
+        if self.fields is not None:
+            self.fields.remove_sources()
+            for src in self.sources:
+                src.add_source(self.fields)
+
+    def restart_fields(self):
+        """Simulation.restart_fields (python/simulation.py:4479-4490): time 0, zero
+        fields (fields::zero_fields); the Fourier transforms keep accumulating."""
+        if self.fields is not None:
+            self.fields.t = 0
+            self.fields.zero_fields()
+        else:
+            self.init_sim()
+
+    def reset_meep(self):
+        """Simulation.reset_meep (python/simulation.py:4465-4477): drop fields, structure
+        and DFT objects."""
+        self.fields = None
+        self.structure = None
+        self.dft_objects = []
+
+    def _energy(self, which, box, center, size):
+        if self.fields is None:
+            raise RuntimeError(f"Fields must be initialized before using {which}")
+        lo, hi = self._where_bounds(box, center, size)
+        return getattr(self.fields, which)(lo, hi)
+
+    def electric_energy_in_box(self, box=None, center=None, size=None):
+        """python/simulation.py:3655-3674 -> fields::electric_energy_in_box."""
+        return self._energy("electric_energy_in_box", box, center, size)
+
+    def magnetic_energy_in_box(self, box=None, center=None, size=None):
+        """python/simulation.py:3676-3695 -> fields::magnetic_energy_in_box."""
+        return self._energy("magnetic_energy_in_box", box, center, size)
+
+    def field_energy_in_box(self, box=None, center=None, size=None):
+        """python/simulation.py:3697-3716 -> fields::field_energy_in_box."""
+        return self._energy("field_energy_in_box", box, center, size)
 
     def get_component_array(self, component=Ez):
         """The raw whole-cell array of a component (Yee layout, ghosts 0)."""

@@ -2723,12 +2723,20 @@ int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3
   bool empty_dim[3];
   for (int d = 0; d < 3; d++) empty_dim[d] = G.has[d] && vmax[d] - vmin[d] == 0.0;
   const int yd[3] = {G.dim == 2 ? 2 : 0, G.dim == 2 ? 0 : 1, G.dim == 2 ? 1 : 2};
+  // Dielectric (12) / Permeability (13), src/array_slice.cpp:385-408, 649-676: the E (H)
+  // components of the grid, their yee2cent offsets; get_chi1inv_at_pt returns 1 where the
+  // chunk holds no diagonal row
+  const bool mat = c == 12 || c == 13;
+  std::vector<int> mcs;
+  if (mat)
+    for (int k = 0; k < 3; k++)
+      if (G.has_field(tcomp(c == 12 ? T_E : T_H, k))) mcs.push_back(tcomp(c == 12 ? T_E : T_H, k));
   for (auto &L : loops) {
     Chunk &ch = s->chunks[L.ci];
     const GV &g = ch.gv;
-    const realnum *f = ch.F(c);
+    const realnum *f = mat ? nullptr : ch.F(c);
     long o1 = 0, o2 = 0;
-    for (int d = 0; d < 3; d++)
+    for (int d = 0; d < 3 && !mat; d++)
       if (G.has[d] && !G.shift(c, d)) {
         if (o1)
           o2 = g.s[d];
@@ -2756,7 +2764,20 @@ int orc_array_slice(orc_sim *s, int c, const double vmin[3], const double vmax[3
             if (G.has[d]) idx += long((p[d] - g.io[d]) / 2) * g.s[d];
           double avg = 0;
           if (f) avg = 0.25 * (f[idx] + f[idx + o1] + f[idx + o2] + f[idx + o1 + o2]);
-          const cplx v = wt * cplx(avg, 0.0) * cplx(1.0, 0.0);
+          cplx v = wt * cplx(avg, 0.0) * cplx(1.0, 0.0);
+          if (mat) {
+            cplx tr(0.0, 0.0);
+            for (int ck : mcs) {
+              long q1 = 0, q2 = 0;
+              for (int d = 0; d < 3; d++)
+                if (G.has[d] && !G.shift(ck, d)) (q1 ? q2 : q1) = g.s[d];
+              const auto &u = ch.chi1inv[ck][cdir(ck)];
+              auto at = [&](long i) -> double { return u.empty() ? 1.0 : double(u[i]); };
+              tr += (at(idx) + at(idx + q1) + at(idx + q2) + at(idx + q1 + q2));
+              if (std::abs(tr) == 0.0) tr += 4.0;
+            }
+            v = wt * (4.0 * double(mcs.size())) / tr;
+          }
           long long oi = 0;
           for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
           arr[oi] = real(v);
