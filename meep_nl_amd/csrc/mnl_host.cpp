@@ -256,6 +256,7 @@ struct mnl_fields {
   // polarization chunks (lean + PML bodies), the general kernel over those chunks only
   bool tile_mode = true;
   bool tile_zcut = true;      // cut z chunks at the lean box's z range (short z-PML items)
+  int last_no_ownc = 0;       // MNL_NO_OWNC seen by the last batch (A/B: rebuild on change)
   int tile_body_mask = -1;   // MNL_TILE_BODY_MASK: step only these bodies (timing experiments)
   std::vector<int> titems;   // tile-kernel items (FusedArgs::titems)
   int *d_titems = nullptr;
@@ -2413,7 +2414,17 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
           const int m = pml_dirs(lo, hi);
           body = m == 1 ? 1 : m == 2 ? 2 : m == 4 ? 3 : m == 0 ? 4 : m == 3 ? 6 : m == 5 ? 7 : 5;
         }
-        const int v = tx | (ty << 8) | (ch << 16) | (body << 24);
+        // single-axis PML bodies whose footprint (rows y0 .. y0+15, planes zs-1 .. ze) is
+        // owned in y and z for every component: pml_body<AX, OWNC = true> (bit 29)
+        int ownc = 0;
+        const char *noc = getenv("MNL_NO_OWNC");
+        if (body >= 1 && body <= 3 && !(noc && atoi(noc))) {
+          const int ylo = std::max(a.osh_lo[1], a.oun_lo[1]), yhi = std::min(a.osh_hi[1], a.oun_hi[1]);
+          const int zlo = std::max(a.osh_lo[2], a.oun_lo[2]), zhi = std::min(a.osh_hi[2], a.oun_hi[2]);
+          ownc = (y0 >= ylo && y0 + 15 <= yhi && zs - 1 >= zlo && ze <= zhi &&
+                  y0 + 15 <= g.N[1] - 1 && ze <= g.N[2] - 1) ? 1 : 0;
+        }
+        const int v = tx | (ty << 8) | (ch << 16) | (body << 24) | (ownc << 29);
         if (F->tile_body_mask >= 0 && !((F->tile_body_mask >> body) & 1)) continue;  // timing only
         if (F->nranks > 1 && ch == 0)
           early.push_back(v);
@@ -3320,6 +3331,13 @@ int step_batch(mnl_fields *F, int nsteps) {
     if (want != F->tile_zcut) {
       if (F->fused && set_fused(F, false)) return -1;
       F->tile_zcut = want;
+    }
+  }
+  if (const char *e = getenv("MNL_NO_OWNC")) {  // in-process A/B of the OWNC item flag
+    const int want = atoi(e) != 0;
+    if (want != F->last_no_ownc) {
+      if (F->fused && set_fused(F, false)) return -1;
+      F->last_no_ownc = want;
     }
   }
   if (const char *e = getenv("MNL_ZCHUNK_STEP")) {

@@ -23,6 +23,24 @@
 
 namespace mnl {
 
+// tile-kernel code-generation switches (variant builds for A/B timing; defaults are the
+// measured choices)
+#ifndef MNL_RS_AT
+#define MNL_RS_AT 1
+#endif
+#ifndef MNL_SKIP_B
+#define MNL_SKIP_B 1
+#endif
+#ifndef MNL_HOIST_X
+#define MNL_HOIST_X 0
+#endif
+#ifndef MNL_OWNC
+#define MNL_OWNC 1
+#endif
+#ifndef MNL_MULTI_DIST  // prefetch distance of the multi-axis PML bodies (AX = 3, 5, 7)
+#define MNL_MULTI_DIST 0
+#endif
+
 #define MNL_BX 64
 #define MNL_BY 4
 
@@ -2265,13 +2283,15 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
 // the lean box L: no PML, every component owned, H == B, E implicit.  1024 threads:
 // waves 0..FR-1 hold one row each (row 0 = the y-1 halo row, B recomputed), wave FR the
 // x-1 column (B recomputed), the E of the x+64 column and a corner.
-template <int UMODE, int DIST>
+template <int UMODE, int DIST, int VAR = 0>
 __device__ __forceinline__ void lean_body(const FusedArgs &a, const ItemGeo &itg, unsigned uw,
                                           const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
                                           double (*sB)[FR][FX + 1]) {
   constexpr bool HAS_U = UMODE != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const bool hwave = __builtin_amdgcn_readfirstlane(w) >= FR - 1;  // wave-uniform
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform
+  const bool hwave = wu >= FR - 1;
+  constexpr bool SKIPB = MNL_SKIP_B && !(VAR & 2);
   const int flo0 = a.L.lo[0], flo1 = a.L.lo[1], flo2 = a.L.lo[2];
   const int fhi0 = a.L.hi[0], fhi1 = a.L.hi[1], fhi2 = a.L.hi[2];
   const unsigned s2 = (unsigned)(a.st2 * 8);  // byte stride of one z plane
@@ -2385,8 +2405,10 @@ __device__ __forceinline__ void lean_body(const FusedArgs &a, const ItemGeo &itg
         q.u0 = q.u1 = q.u2 = 1.0;
       }
       const unsigned ob = cbl + (unsigned)k * s2;
-      q.b0 = ldg(Bv[0], ob);
-      q.b1 = ldg(Bv[1], ob);
+      // Bx of the x-1 column (wave FR) and By of the y-1 row (wave 0) feed no update: those
+      // lanes read one cached line instead of a line per row (MNL_SKIP_B)
+      q.b0 = ldg(Bv[0], (SKIPB && wu == FR) ? safe : ob);
+      q.b1 = ldg(Bv[1], (SKIPB && wu == 0) ? safe : ob);
       q.b2 = ldg(Bv[2], ob);
       q.hf = hF && zin(k);
       q.h0 = q.h1 = 0.0;
@@ -2525,6 +2547,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, unsigned 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, p ? (int)nrec : 0,
                                            0x00020000);
 }
+// descriptor of a scalar pointer built where it is used (the empty asm keeps the compiler
+// from hoisting it out of the loop); null: zero records, every access out of range
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc_at(unsigned long long v, unsigned nrec) {
+  asm volatile("" : "+s"(v));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, v ? (int)nrec : 0, 0x00020000);
+}
+// a PML-state array as pml_body holds it: a scalar pointer turned into a descriptor at each
+// use (R) or a descriptor built once
+template <bool R>
+struct RsArr {
+  __device__ static unsigned long long make(const void *p, unsigned) {
+    return (unsigned long long)sgpr_ptr(p);
+  }
+  __device__ static __amdgpu_buffer_rsrc_t get(unsigned long long v, unsigned nrec) {
+    return brsrc_at(v, nrec);
+  }
+};
+template <>
+struct RsArr<false> {
+  __device__ static __amdgpu_buffer_rsrc_t make(const void *p, unsigned nrec) {
+    return brsrc(p, nrec);
+  }
+  __device__ static __amdgpu_buffer_rsrc_t get(__amdgpu_buffer_rsrc_t r, unsigned) { return r; }
+};
 __device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
@@ -2534,14 +2580,21 @@ __device__ __forceinline__ unsigned own_bits_of(int v, int sl, int sh, int ul, i
   return ((v >= sl && v <= sh) ? 1u : 0u) | ((v >= ul && v <= uh) ? 2u : 0u);
 }
 
-template <int UMODE, int DIST, int AX>
+// OWNC: every point of the item's footprint is owned in y and z (item bit 29, set by the
+// host): the y / z ownership terms are the constant 3, so every ownership test and the
+// E-load source of a lane are fixed along the march (no per-plane recomputation), and the
+// z index needs no clamp
+template <int UMODE, int DIST, int AX, bool OWNC, int VAR = 0>
 __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, unsigned uw,
                                          const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
                                          double (*sB)[FR][FX + 1], PTabL &P) {
   constexpr bool HAS_U = UMODE != 0;
   constexpr bool PX = (AX & 1) != 0, PY = (AX & 2) != 0, PZ = (AX & 4) != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const bool hwave = __builtin_amdgcn_readfirstlane(w) >= FR - 1;  // wave-uniform
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform
+  const bool hwave = wu >= FR - 1;
+  constexpr bool SKIPB = MNL_SKIP_B && !(VAR & 2);
+  constexpr bool RSAT = MNL_RS_AT && !(VAR & 1);
   const int x0 = it.x0, y0 = it.y0, zs = it.zs, ze = it.ze;
   const int zlo = zs - 1;  // z table position 0
   // ---- PML tables of the footprint -> LDS (x: x0-1 .. x0+64, y: y0 .. y0+FR,
@@ -2599,7 +2652,7 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   const unsigned cbl = inA ? cb : 0u;
   // per-axis ownership (within G): bit0 = components shifted along the axis, bit1 = unshifted
   const unsigned ownx = own_bits_of(gx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
-  const unsigned owny = own_bits_of(gy, a.osh_lo[1], a.osh_hi[1], a.oun_lo[1], a.oun_hi[1]);
+  const unsigned owny = OWNC ? 3u : own_bits_of(gy, a.osh_lo[1], a.osh_hi[1], a.oun_lo[1], a.oun_hi[1]);
   const int zsl = a.osh_lo[2], zsh = a.osh_hi[2], zul = a.oun_lo[2], zuh = a.oun_hi[2];
   auto own_e = [](int c, unsigned ox_, unsigned oy_, unsigned oz_) {
     return ((c == 0 ? ox_ : ox_ >> 1) & (c == 1 ? oy_ : oy_ >> 1) & (c == 2 ? oz_ : oz_ >> 1) & 1u) != 0;
@@ -2612,32 +2665,46 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   const bool hA = hslot && hx >= 0 && hx < N0 && hy >= 0 && hy < N1;
   const unsigned hbl = hA ? (unsigned)((hx + (long long)hy * st1) * 8) : cbl;
   const unsigned hownx = own_bits_of(hx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
-  const unsigned howny = own_bits_of(hy, a.osh_lo[1], a.osh_hi[1], a.oun_lo[1], a.oun_hi[1]);
+  const unsigned howny = OWNC ? 3u : own_bits_of(hy, a.osh_lo[1], a.osh_hi[1], a.oun_lo[1], a.oun_hi[1]);
   const int zmax = a.N[2] - 1;
-#define zc(z) min(max((z), 0), zmax)
-#define ownz_of(z) own_bits_of((z), zsl, zsh, zul, zuh)
+#define zc(z) (OWNC ? (z) : min(max((z), 0), zmax))
+#define ownz_of(z) (OWNC ? 3u : own_bits_of((z), zsl, zsh, zul, zuh))
   const unsigned s2 = (unsigned)(a.st2 * 8);
   const double C = a.C;
   const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
-  // buffer descriptors of the PML state (null arrays: every access out of range)
-  const __amdgpu_buffer_rsrc_t rBn0 = brsrc(a.Bn[0], nrec), rBn1 = brsrc(a.Bn[1], nrec),
-                               rBn2 = brsrc(a.Bn[2], nrec);
-  const __amdgpu_buffer_rsrc_t rDn0 = brsrc(a.Dn[0], nrec), rDn1 = brsrc(a.Dn[1], nrec),
-                               rDn2 = brsrc(a.Dn[2], nrec);
-  const __amdgpu_buffer_rsrc_t rEo0 = brsrc(a.E[0], nrec), rEo1 = brsrc(a.E[1], nrec),
-                               rEo2 = brsrc(a.E[2], nrec);
-  const __amdgpu_buffer_rsrc_t rEn0 = brsrc(a.En[0], nrec), rEn1 = brsrc(a.En[1], nrec),
-                               rEn2 = brsrc(a.En[2], nrec);
-  const __amdgpu_buffer_rsrc_t rUBo0 = brsrc(a.UBo[0], nrec), rUBo1 = brsrc(a.UBo[1], nrec),
-                               rUBo2 = brsrc(a.UBo[2], nrec);
-  const __amdgpu_buffer_rsrc_t rUBn0 = brsrc(a.UBn[0], nrec), rUBn1 = brsrc(a.UBn[1], nrec),
-                               rUBn2 = brsrc(a.UBn[2], nrec);
-  const __amdgpu_buffer_rsrc_t rHo0 = brsrc(a.Ho[0], nrec), rHo1 = brsrc(a.Ho[1], nrec),
-                               rHo2 = brsrc(a.Ho[2], nrec);
-  const __amdgpu_buffer_rsrc_t rHn0 = brsrc(a.Hn[0], nrec), rHn1 = brsrc(a.Hn[1], nrec),
-                               rHn2 = brsrc(a.Hn[2], nrec);
-  const __amdgpu_buffer_rsrc_t rUD0 = brsrc(a.UD[0], nrec), rUD1 = brsrc(a.UD[1], nrec),
-                               rUD2 = brsrc(a.UD[2], nrec);
+#define RSV(x) (RsArr<RSAT>::make((x), nrec))
+#define RS(p) (RsArr<RSAT>::get((p), nrec))
+  // PML-state arrays (null: every access out of range).  MNL_RS_AT (default): scalar
+  // pointers whose buffer descriptors are rebuilt at each use (RS): 4-SGPR descriptors of
+  // every array live across the z loop overflow the SGPRs and spill into VGPR lanes (a
+  // v_readlane per reload); MNL_RS_AT=0: descriptors built once before the loop
+  const auto pBn0 = RSV(a.Bn[0]);
+  const auto pBn1 = RSV(a.Bn[1]);
+  const auto pBn2 = RSV(a.Bn[2]);
+  const auto pDn0 = RSV(a.Dn[0]);
+  const auto pDn1 = RSV(a.Dn[1]);
+  const auto pDn2 = RSV(a.Dn[2]);
+  const auto pEo0 = RSV(a.E[0]);
+  const auto pEo1 = RSV(a.E[1]);
+  const auto pEo2 = RSV(a.E[2]);
+  const auto pEn0 = RSV(a.En[0]);
+  const auto pEn1 = RSV(a.En[1]);
+  const auto pEn2 = RSV(a.En[2]);
+  const auto pUBo0 = RSV(a.UBo[0]);
+  const auto pUBo1 = RSV(a.UBo[1]);
+  const auto pUBo2 = RSV(a.UBo[2]);
+  const auto pUBn0 = RSV(a.UBn[0]);
+  const auto pUBn1 = RSV(a.UBn[1]);
+  const auto pUBn2 = RSV(a.UBn[2]);
+  const auto pHo0 = RSV(a.Ho[0]);
+  const auto pHo1 = RSV(a.Ho[1]);
+  const auto pHo2 = RSV(a.Ho[2]);
+  const auto pHn0 = RSV(a.Hn[0]);
+  const auto pHn1 = RSV(a.Hn[1]);
+  const auto pHn2 = RSV(a.Hn[2]);
+  const auto pUD0 = RSV(a.UD[0]);
+  const auto pUD1 = RSV(a.UD[1]);
+  const auto pUD2 = RSV(a.UD[2]);
   // array pointers as scalars (a per-lane choice between two entries of a local
   // pointer array makes the array, and with it the kernel arguments, a scratch copy)
   const gdp D0 = sgpr_ptr(a.Do[0]), D1 = sgpr_ptr(a.Do[1]), D2 = sgpr_ptr(a.Do[2]);
@@ -2657,10 +2724,23 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   __syncthreads();  // tables visible
   // table accessors: direction d at this lane (x: column, y: row, z: plane position)
   const int px = col, py = row;
+  // MNL_HOIST_X: the x coefficients of a lane are the same on every plane; held in
+  // registers instead of re-read from LDS after every barrier
+  double tbx[3][2] = {{1, 1}, {1, 1}, {1, 1}};
+  bool hfx[2] = {false, false};
+  if (MNL_HOIST_X && PX) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) tbx[k][0] = P.v[0][k][0][px], tbx[k][1] = P.v[0][k][1][px];
+    hfx[0] = P.f[0][0][px] != 0, hfx[1] = P.f[0][1][px] != 0;
+  }
 #define T(d, coef, sft, pz) \
-  (((AX >> (d)) & 1) ? P.v[d][coef][sft][(d) == 0 ? px : ((d) == 1 ? py : (pz))] : 1.0)
+  (((AX >> (d)) & 1) ? ((d) == 0 && MNL_HOIST_X ? tbx[coef][sft] \
+                                                : P.v[d][coef][sft][(d) == 0 ? px : ((d) == 1 ? py : (pz))]) \
+                     : 1.0)
 #define F(d, sft, pz) \
-  (((AX >> (d)) & 1) ? P.f[d][sft][(d) == 0 ? px : ((d) == 1 ? py : (pz))] != 0 : false)
+  (((AX >> (d)) & 1) ? ((d) == 0 && MNL_HOIST_X ? hfx[sft] \
+                                                : P.f[d][sft][(d) == 0 ? px : ((d) == 1 ? py : (pz))] != 0) \
+                     : false)
   // W flags (PML chunk along the E component's own direction, shifted coordinate)
   const bool Wx = F(0, 1, 0), Wy = F(1, 1, 0);
 #define Wz(pz) F(2, 1, pz)
@@ -2692,12 +2772,12 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
       QQ.u0 = QQ.u1 = QQ.u2 = 1.0; \
     } \
     QQ.es0 = QQ.es1 = QQ.es2 = 0.0; \
-    if (PX) QQ.es0 = bld(rEo0, (o0 && Wx) ? o : MNL_OOB); \
-    if (PY) QQ.es1 = bld(rEo1, (o1 && Wy) ? o : MNL_OOB); \
-    if (PZ) QQ.es2 = bld(rEo2, (o2 && Wz(pz1)) ? o : MNL_OOB); \
+    if (PX) QQ.es0 = bld(RS(pEo0), (o0 && Wx) ? o : MNL_OOB); \
+    if (PY) QQ.es1 = bld(RS(pEo1), (o1 && Wy) ? o : MNL_OOB); \
+    if (PZ) QQ.es2 = bld(RS(pEo2), (o2 && Wz(pz1)) ? o : MNL_OOB); \
     const unsigned ob = cbl + (unsigned)zc(KK) * s2; \
-    QQ.b0 = ldg(B0, ob); \
-    QQ.b1 = ldg(B1, ob); \
+    QQ.b0 = ldg(B0, (SKIPB && wu == FR) ? 0u : ob); /* unused: see lean_body */ \
+    QQ.b1 = ldg(B1, (SKIPB && wu == 0) ? 0u : ob); \
     QQ.b2 = ldg(B2, ob); \
     QQ.h0 = QQ.h1 = 0.0; \
     QQ.hu0 = QQ.hu1 = 1.0; \
@@ -2752,15 +2832,15 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   do { \
     const int apz = (KK) - zlo; \
     const unsigned aob = cbl + (unsigned)zc(KK) * s2; \
-    if (PZ) ub0 = bld(rUBo0, (inA && F(2, 1, apz)) ? aob : MNL_OOB); \
-    if (PX) ub1 = bld(rUBo1, (inA && F(0, 1, apz)) ? aob : MNL_OOB); \
-    if (PY) ub2 = bld(rUBo2, (inA && F(1, 1, apz)) ? aob : MNL_OOB); \
-    if (PX) ho0 = bld(rHo0, (inA && F(0, 0, apz)) ? aob : MNL_OOB); \
-    if (PY) ho1 = bld(rHo1, (inA && F(1, 0, apz)) ? aob : MNL_OOB); \
-    if (PZ) ho2 = bld(rHo2, (inA && F(2, 0, apz)) ? aob : MNL_OOB); \
-    if (PZ) ud0 = bld(rUD0, (stl && F(2, 0, apz)) ? aob : MNL_OOB); \
-    if (PX) ud1 = bld(rUD1, (stl && F(0, 0, apz)) ? aob : MNL_OOB); \
-    if (PY) ud2 = bld(rUD2, (stl && F(1, 0, apz)) ? aob : MNL_OOB); \
+    if (PZ) ub0 = bld(RS(pUBo0), (inA && F(2, 1, apz)) ? aob : MNL_OOB); \
+    if (PX) ub1 = bld(RS(pUBo1), (inA && F(0, 1, apz)) ? aob : MNL_OOB); \
+    if (PY) ub2 = bld(RS(pUBo2), (inA && F(1, 1, apz)) ? aob : MNL_OOB); \
+    if (PX) ho0 = bld(RS(pHo0), (inA && F(0, 0, apz)) ? aob : MNL_OOB); \
+    if (PY) ho1 = bld(RS(pHo1), (inA && F(1, 0, apz)) ? aob : MNL_OOB); \
+    if (PZ) ho2 = bld(RS(pHo2), (inA && F(2, 0, apz)) ? aob : MNL_OOB); \
+    if (PZ) ud0 = bld(RS(pUD0), (stl && F(2, 0, apz)) ? aob : MNL_OOB); \
+    if (PX) ud1 = bld(RS(pUD1), (stl && F(0, 0, apz)) ? aob : MNL_OOB); \
+    if (PY) ud2 = bld(RS(pUD2), (stl && F(1, 0, apz)) ? aob : MNL_OOB); \
   } while (0)
   PML_AUX(zs - 1);
   double dx = 0, dy = 0, dz = 0, hmx = 0, hmy = 0;
@@ -2838,15 +2918,15 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
         const unsigned b0 = (sk && own_b(0, ownx, owny, oz)) ? ok : MNL_OOB;
         const unsigned b1 = (sk && own_b(1, ownx, owny, oz)) ? ok : MNL_OOB;
         const unsigned b2 = (sk && own_b(2, ownx, owny, oz)) ? ok : MNL_OOB;
-        bst(rBn0, b0, Bx);
-        bst(rBn1, b1, By);
-        bst(rBn2, b2, Bz);
-        if (PZ) bst(rUBn0, fzs ? b0 : MNL_OOB, ubx);
-        if (PX) bst(rUBn1, fxs ? b1 : MNL_OOB, uby);
-        if (PY) bst(rUBn2, fys ? b2 : MNL_OOB, ubz);
-        if (PX) bst(rHn0, fxu ? b0 : MNL_OOB, Hx);
-        if (PY) bst(rHn1, fyu ? b1 : MNL_OOB, Hy);
-        if (PZ) bst(rHn2, fzu ? b2 : MNL_OOB, Hz);
+        bst(RS(pBn0), b0, Bx);
+        bst(RS(pBn1), b1, By);
+        bst(RS(pBn2), b2, Bz);
+        if (PZ) bst(RS(pUBn0), fzs ? b0 : MNL_OOB, ubx);
+        if (PX) bst(RS(pUBn1), fxs ? b1 : MNL_OOB, uby);
+        if (PY) bst(RS(pUBn2), fys ? b2 : MNL_OOB, ubz);
+        if (PX) bst(RS(pHn0), fxu ? b0 : MNL_OOB, Hx);
+        if (PY) bst(RS(pHn1), fyu ? b1 : MNL_OOB, Hy);
+        if (PZ) bst(RS(pHn2), fzu ? b2 : MNL_OOB, Hz);
       }
       if (ownlike) {
         sB[0][row][col] = Hx;
@@ -2869,12 +2949,12 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
         const unsigned e0 = (sk && own_e(0, ownx, owny, oz)) ? ok : MNL_OOB;
         const unsigned e1 = (sk && own_e(1, ownx, owny, oz)) ? ok : MNL_OOB;
         const unsigned e2 = (sk && own_e(2, ownx, owny, oz)) ? ok : MNL_OOB;
-        bst(rDn0, e0, Dx);
-        bst(rDn1, e1, Dy);
-        bst(rDn2, e2, Dz);
-        if (PZ) bst(rUD0, fzu ? e0 : MNL_OOB, udx);
-        if (PX) bst(rUD1, fxu ? e1 : MNL_OOB, udy);
-        if (PY) bst(rUD2, fyu ? e2 : MNL_OOB, udz);
+        bst(RS(pDn0), e0, Dx);
+        bst(RS(pDn1), e1, Dy);
+        bst(RS(pDn2), e2, Dz);
+        if (PZ) bst(RS(pUD0), fzu ? e0 : MNL_OOB, udx);
+        if (PX) bst(RS(pUD1), fxu ? e1 : MNL_OOB, udy);
+        if (PY) bst(RS(pUD2), fyu ? e2 : MNL_OOB, udz);
         double k0 = 1, k1 = 1, k2 = 1;
         if (UMODE == 2) {
           k0 = pu(uik, 0), k1 = pu(uik, 1), k2 = pu(uik, 2);
@@ -2883,15 +2963,15 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
         }
         if (PX) {
           const double fw = HAS_U ? Dx * k0 : Dx, fp = HAS_U ? dx * k0 : dx;
-          bst(rEn0, fxs ? e0 : MNL_OOB, ex + (T(0, 2, 1, pz) * fw - T(0, 0, 1, pz) * fp));
+          bst(RS(pEn0), fxs ? e0 : MNL_OOB, ex + (T(0, 2, 1, pz) * fw - T(0, 0, 1, pz) * fp));
         }
         if (PY) {
           const double fw = HAS_U ? Dy * k1 : Dy, fp = HAS_U ? dy * k1 : dy;
-          bst(rEn1, fys ? e1 : MNL_OOB, ey + (T(1, 2, 1, pz) * fw - T(1, 0, 1, pz) * fp));
+          bst(RS(pEn1), fys ? e1 : MNL_OOB, ey + (T(1, 2, 1, pz) * fw - T(1, 0, 1, pz) * fp));
         }
         if (PZ) {
           const double fw = HAS_U ? Dz * k2 : Dz, fp = HAS_U ? dz * k2 : dz;
-          bst(rEn2, fzs ? e2 : MNL_OOB, ez + (T(2, 2, 1, pz) * fw - T(2, 0, 1, pz) * fp));
+          bst(RS(pEn2), fzs ? e2 : MNL_OOB, ez + (T(2, 2, 1, pz) * fw - T(2, 0, 1, pz) * fp));
         }
       }
       hmx = Hx;
@@ -2913,6 +2993,8 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
 }
 #undef PML_AUX
 #undef PML_LOAD
+#undef RS
+#undef RSV
 #undef pu
 #undef uoff
 #undef zc
@@ -2923,8 +3005,12 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
 
 // body codes of tile items (bits 24-26): 0 lean, 1..7 pml_body<AX = 1, 2, 4, 0, 7, 3, 5>
 // (y-z edges, AX = 6, are few: they take the AX = 7 body)
-template <int UMODE, int DIST>
+// VAR (A/B builds with MNL_TILE_AB only; 0 in production): bit 0 = descriptors built once
+// (MNL_RS_AT off), bit 1 = unused B loads kept (MNL_SKIP_B off), bit 2 = multi-axis bodies
+// with prefetch distance 1
+template <int UMODE, int DIST, int VAR = 0>
 __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
+  constexpr int MD = (VAR & 4) ? 1 : MNL_MULTI_DIST;
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
   __shared__ double sE[3][FR + 1][FX + 2];
   __shared__ double sB[3][FR][FX + 1];
@@ -2957,33 +3043,48 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
 #ifndef MNL_TILE_BODIES
 #define MNL_TILE_BODIES 255  // register-budget experiments: compile a subset of the bodies
 #endif
+    const bool ownc = MNL_OWNC && ((item >> 29) & 1);  // OWNC bodies (pml_body)
     switch ((item >> 24) & 7) {
       case 0:
-        if (MNL_TILE_BODIES & 1) lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
+        if (MNL_TILE_BODIES & 1) lean_body<UMODE, DIST, VAR>(a, itg, uw, sU, sE, sB);
         break;
       case 1:
-        if (MNL_TILE_BODIES & 2) pml_body<UMODE, DIST, 1>(a, itg, uw, sU, sE, sB, sP);
+        if (MNL_TILE_BODIES & 2) {
+          if (ownc)
+            pml_body<UMODE, DIST, 1, true, VAR>(a, itg, uw, sU, sE, sB, sP);
+          else
+            pml_body<UMODE, DIST, 1, false, VAR>(a, itg, uw, sU, sE, sB, sP);
+        }
         break;
       case 2:
-        if (MNL_TILE_BODIES & 4) pml_body<UMODE, DIST, 2>(a, itg, uw, sU, sE, sB, sP);
+        if (MNL_TILE_BODIES & 4) {
+          if (ownc)
+            pml_body<UMODE, DIST, 2, true, VAR>(a, itg, uw, sU, sE, sB, sP);
+          else
+            pml_body<UMODE, DIST, 2, false, VAR>(a, itg, uw, sU, sE, sB, sP);
+        }
         break;
       case 3:
-        if (MNL_TILE_BODIES & 8) pml_body<UMODE, DIST, 4>(a, itg, uw, sU, sE, sB, sP);
+        if (MNL_TILE_BODIES & 8) {
+          if (ownc)
+            pml_body<UMODE, DIST, 4, true, VAR>(a, itg, uw, sU, sE, sB, sP);
+          else
+            pml_body<UMODE, DIST, 4, false, VAR>(a, itg, uw, sU, sE, sB, sP);
+        }
         break;
       case 4:
-        if (MNL_TILE_BODIES & 16) pml_body<UMODE, DIST, 0>(a, itg, uw, sU, sE, sB, sP);
+        if (MNL_TILE_BODIES & 16) pml_body<UMODE, DIST, 0, false, VAR>(a, itg, uw, sU, sE, sB, sP);
         break;
       case 5:
-        if (MNL_TILE_BODIES & 32) pml_body<UMODE, DIST, 7>(a, itg, uw, sU, sE, sB, sP);
+        if (MNL_TILE_BODIES & 32) pml_body<UMODE, MD, 7, false, VAR>(a, itg, uw, sU, sE, sB, sP);
         break;
       case 6:
-        if (MNL_TILE_BODIES & 64) pml_body<UMODE, DIST, 3>(a, itg, uw, sU, sE, sB, sP);
+        if (MNL_TILE_BODIES & 64) pml_body<UMODE, MD, 3, false, VAR>(a, itg, uw, sU, sE, sB, sP);
         break;
       default:
-        if (MNL_TILE_BODIES & 128) pml_body<UMODE, DIST, 5>(a, itg, uw, sU, sE, sB, sP);
+        if (MNL_TILE_BODIES & 128) pml_body<UMODE, MD, 5, false, VAR>(a, itg, uw, sU, sE, sB, sP);
         break;
-    }
-  }
+    }  }
 }
 
 // Lean tiles only (the original two-launch fused step: this kernel, then
@@ -3253,6 +3354,23 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
     const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
     hipStream_t s = (hipStream_t)stream;
     const dim3 grd((unsigned)nb), blk(1024);
+#ifdef MNL_TILE_AB
+    const char *ve = getenv("MNL_TILE_VAR");
+    const int var = ve ? atoi(ve) : 0;
+    if (var == 1 && um != 1) {
+      if (um == 2) fused_tile_kernel<2, 1, 1><<<grd, blk, 0, s>>>(t);
+      else fused_tile_kernel<0, 1, 1><<<grd, blk, 0, s>>>(t);
+    } else if (var == 2 && um != 1) {
+      if (um == 2) fused_tile_kernel<2, 1, 2><<<grd, blk, 0, s>>>(t);
+      else fused_tile_kernel<0, 1, 2><<<grd, blk, 0, s>>>(t);
+    } else if (var == 4 && um != 1) {
+      if (um == 2) fused_tile_kernel<2, 1, 4><<<grd, blk, 0, s>>>(t);
+      else fused_tile_kernel<0, 1, 4><<<grd, blk, 0, s>>>(t);
+    } else if (var == 7 && um != 1) {
+      if (um == 2) fused_tile_kernel<2, 1, 7><<<grd, blk, 0, s>>>(t);
+      else fused_tile_kernel<0, 1, 7><<<grd, blk, 0, s>>>(t);
+    } else
+#endif
     if (um == 2)
       fused_tile_kernel<2, 1><<<grd, blk, 0, s>>>(t);
     else if (um == 1)
