@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-tune", action="store_true",
+                    help="keep the automatic z-chunk (skip Fields.tune_zchunk before the warm-up)")
     ap.add_argument("--size", type=int, default=512, help="cells per side of each GPU's slab")
     ap.add_argument("--vacuum", action="store_true", help="north-star vacuum variant (no core)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None)
@@ -179,11 +181,12 @@ def pmc_traffic(size, vacuum):
     return None
 
 
-def measure_extra(workload, size, steps, warmup):
+def measure_extra(workload, size, steps, warmup, tune=True):
     """One single-GPU BASELINE config in the same process: warm-up, K timed
     steps (stream-synchronized), its own roofline."""
     dev = int(os.environ.get("MNL_BENCH_DEVICE", "0"))
     gv, s, f = build_fields(workload, size, 0, 1, dev, None)
+    zc = f.tune_zchunk() if tune else None
     f.step(warmup)
     f.set_profiling(True)
     t0 = time.perf_counter()
@@ -194,7 +197,7 @@ def measure_extra(workload, size, steps, warmup):
     out = {"workload": WORKLOADS[workload] + f", {size}^3 cells, res 10, real fields, fp64",
            "value": round(cells * steps / el / 1e6, 1), "unit": "Mcells*steps/s",
            "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "warmup": warmup,
-           "fused": f.fused_active(), "model_bytes_per_cell_step": round(bpc, 2),
+           "fused": f.fused_active(), "zchunk_tuned": zc, "model_bytes_per_cell_step": round(bpc, 2),
            "model_fraction_of_peak": round(bpc * cells / (el / steps) / 1e9 / HBM_PEAK_GBS, 4),
            "roofline": roofline(f)}
     if workload == "kerr_nr":
@@ -302,6 +305,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # untimed set-up: the z-chunk length timed over real steps (identical results)
+    zc = None if args.no_tune else f.tune_zchunk()
     f.step(args.warmup)
     barrier()
     f.set_profiling(not args.no_events)
@@ -343,7 +348,7 @@ def main():
         extra = {}
         for wl in ("c2", "kerr", "kerr_nr"):
             try:
-                extra[wl] = measure_extra(wl, args.extra_size, 20, 5)
+                extra[wl] = measure_extra(wl, args.extra_size, 20, 5, not args.no_tune)
             except Exception as e:  # an extra config must never hide the headline number
                 extra[wl] = {"error": str(e)}
     cpu = None
@@ -374,7 +379,7 @@ def main():
                          if args.workload in ("waveguide", "vacuum", "c5") else ""),
             "grid": list(gv.n), "per_gpu_cells": int(gv.n[0]) * int(gv.n[1]) * int(gv.n[2]) // world,
             "parallelism": f"z-slab x{world}",
-            "transport": transport, "fused": fused,
+            "transport": transport, "fused": fused, "zchunk_tuned": zc,
             "flux_planes": args.flux, "flux_nfreq": args.nfreq if args.flux else 0,
             "model_bytes_per_cell_step": bpc,
             "model_fraction_of_peak": round(bpc * total_cells / world / (el / args.steps) / 1e9

@@ -236,6 +236,14 @@ int mnl_fields_require_component(mnl_fields *f, int comp);
  * centre (src/step.cpp:138-139) every `every` steps (default 100, and after the
  * last step): fails with "meep: simulation fields are NaN or Inf". */
 int mnl_fields_step(mnl_fields *f, int nsteps);
+/* No reference counterpart (a tuning knob of this implementation): chooses the z-chunk
+ * length of the tile kernel by timing each candidate (automatic, 16, 20, 24, 32, 48) over
+ * `reps` real steps after one warm-up step each.  Advances the fields by up to
+ * 2 + 6 * (1 + reps) steps (the first steps until the fused mode is on), with results
+ * identical to plain stepping.  *chosen = the length kept (0 = automatic), or -1 when
+ * nothing was tuned (not in the fused tile mode: at most 2 steps taken; MNL_FUSED_ZCHUNK
+ * set: none). */
+int mnl_fields_tune_zchunk(mnl_fields *f, int reps, int *chosen);
 int mnl_fields_set_nan_check(mnl_fields *f, int every);
 /* Field energy over the box [vmin, vmax] (NULL, NULL: the whole cell,
  * user_volume.surroundings()), src/energy_and_flux.cpp:48-178:

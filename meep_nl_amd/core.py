@@ -395,6 +395,15 @@ class Fields:
     def step(self, n=1):
         check(lib().mnl_fields_step(self.h, int(n)))
 
+    def tune_zchunk(self, reps=3):
+        """Time the tile kernel's z-chunk candidates over real steps and keep the fastest
+        (mnl_fields_tune_zchunk; advances the fields by up to 2 + 6 * (1 + reps) steps,
+        results identical to plain stepping).  Returns the chunk length kept (0 = auto),
+        -1 when nothing was tuned (not in the fused tile mode)."""
+        c = ctypes.c_int(0)
+        check(lib().mnl_fields_tune_zchunk(self.h, int(reps), ctypes.byref(c)))
+        return c.value
+
     def _time(self):
         t = ctypes.c_longlong()
         dt = ctypes.c_double()

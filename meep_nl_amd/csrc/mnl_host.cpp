@@ -5424,6 +5424,49 @@ int mnl_fields_step(mnl_fields *F, int nsteps) {
   return fields_step(F, nsteps);
 }
 
+// z-chunk tuning: the tile kernel's item count / chunk length
+// trade-off (fill of the last round of items vs. the halo planes of short chunks) is
+// measured rather than modelled.  Every candidate length is stepped for real (results do
+// not depend on the chunk length: each point's update is the same arithmetic), so the
+// call advances the fields by 1 + ncand * (1 + reps) steps.
+int mnl_fields_tune_zchunk(mnl_fields *F, int reps, int *chosen) {
+  if (!F || reps < 1) return fail("bad argument");
+  if (chosen) *chosen = -1;
+  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
+  if (getenv("MNL_FUSED_ZCHUNK") || getenv("MNL_ZCHUNK_STEP")) return 0;  // fixed by the user
+  // the first step runs unfused (lazy first updates); the second takes the fused decision
+  for (int i = 0; i < 2 && !F->fused; i++)
+    if (fields_step(F, 1)) return -1;
+  if (!F->fused || !F->tile_mode) return 0;
+  static const int cand[] = {0, 16, 20, 24, 32, 48};
+  // the fused launches' own GPU time (profiling events around them), not the host's
+  // per-batch work
+  const bool prof = F->profiling;
+  F->profiling = true;
+  int best = F->fused_zchunk;
+  double best_ms = 0;
+  int rc = 0;
+  const bool verbose = getenv("MNL_TUNE_VERBOSE") != nullptr;
+  for (int c : cand) {
+    if (F->fused && set_fused(F, false)) { rc = -1; break; }
+    F->fused_zchunk = c;
+    if (fields_step(F, 1)) { rc = -1; break; }  // rebuild + warm-up
+    if (!F->fused) break;
+    const double t0 = F->timer_ms[TM_BINT] + F->timer_ms[TM_GEN];
+    if (fields_step(F, reps)) { rc = -1; break; }
+    const double ms = F->timer_ms[TM_BINT] + F->timer_ms[TM_GEN] - t0;
+    if (verbose)
+      fprintf(stderr, "tune_zchunk rank %d: zchunk %d: %.4f ms/step\n", F->rank, c, ms / reps);
+    if (best_ms == 0 || ms < best_ms) best_ms = ms, best = c;
+  }
+  F->profiling = prof;
+  if (rc) return rc;
+  if (F->fused && set_fused(F, false)) return -1;  // the next step rebuilds with `best`
+  F->fused_zchunk = best;
+  if (chosen) *chosen = best;
+  return 0;
+}
+
 int mnl_fields_initialize_field(mnl_fields *F, int comp, const double *host, size_t n) {
   if (!F || check_comp(comp) || !host) return fail("bad argument");
   if (n < F->S.ntot) return fail("initialize_field: array smaller than the cell");
