@@ -22,7 +22,8 @@ import scenarios as S
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CASES2 = ["vacuum_pml", "big_box", "kerr_lorentz", "nr_dispersive", "nr_seam", "flux"]
+CASES2 = ["vacuum_pml", "big_box", "big_box_tuned", "kerr_lorentz", "nr_dispersive", "nr_seam",
+          "flux"]
 CASES3 = ["big_box", "flux", "averaged_up"]
 CASES8 = ["c5_small"]  # BASELINE C5's decomposition (8 z-slabs) at reduced x-y
 
@@ -67,6 +68,8 @@ def _oracle(name):
         return S.sc_vacuum_pml_3d(make_oracle), {}
     if name == "big_box":
         return S.sc_big_box_3d(make_oracle, steps=16), {}
+    if name == "big_box_tuned":
+        return S.sc_big_box_3d(make_oracle, steps=30), {}
     if name == "kerr_lorentz":
         return S.sc_kerr_lorentz_3d(make_oracle), {}
     if name == "nr_dispersive":
@@ -97,6 +100,8 @@ def test_multiprocess_slabs_bitwise(mp_runs, nranks, name):
         assert got.shape == ref.shape
         d = float(np.max(np.abs(got - ref))) if ref.size else 0.0
         assert d == 0.0, (c, d)
+    if name == "big_box_tuned":  # each rank tuned (its own choice), then stepped to 30
+        assert all(int(r["zchunk"][0]) in (0, 16, 20, 24, 32, 48) for r in ranks)
     for k, v in ex.items():
         for r in ranks:  # collectives: every rank holds the same result
             np.testing.assert_array_equal(r[k], ranks[0][k])
