@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-tune", action="store_true",
-                    help="keep the automatic z-chunk (skip Fields.tune_zchunk before the warm-up)")
+                    help="keep the default knobs (skip Fields.tune before the warm-up)")
     ap.add_argument("--size", type=int, default=512, help="cells per side of each GPU's slab")
     ap.add_argument("--vacuum", action="store_true", help="north-star vacuum variant (no core)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None)
@@ -186,7 +186,7 @@ def measure_extra(workload, size, steps, warmup, tune=True):
     steps (stream-synchronized), its own roofline."""
     dev = int(os.environ.get("MNL_BENCH_DEVICE", "0"))
     gv, s, f = build_fields(workload, size, 0, 1, dev, None)
-    zc = f.tune_zchunk() if tune else None
+    zc = f.tune() if tune else None
     f.step(warmup)
     f.set_profiling(True)
     t0 = time.perf_counter()
@@ -197,7 +197,7 @@ def measure_extra(workload, size, steps, warmup, tune=True):
     out = {"workload": WORKLOADS[workload] + f", {size}^3 cells, res 10, real fields, fp64",
            "value": round(cells * steps / el / 1e6, 1), "unit": "Mcells*steps/s",
            "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "warmup": warmup,
-           "fused": f.fused_active(), "zchunk_tuned": zc, "model_bytes_per_cell_step": round(bpc, 2),
+           "fused": f.fused_active(), "tuned_zchunk_gen_cus": zc, "model_bytes_per_cell_step": round(bpc, 2),
            "model_fraction_of_peak": round(bpc * cells / (el / steps) / 1e9 / HBM_PEAK_GBS, 4),
            "roofline": roofline(f)}
     if workload == "kerr_nr":
@@ -305,8 +305,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # untimed set-up: the z-chunk length timed over real steps (identical results)
-    zc = None if args.no_tune else f.tune_zchunk()
+    # untimed set-up: the fused step's knobs timed over real steps (identical results)
+    zc = None if args.no_tune else f.tune()
     f.step(args.warmup)
     barrier()
     f.set_profiling(not args.no_events)
@@ -379,7 +379,7 @@ def main():
                          if args.workload in ("waveguide", "vacuum", "c5") else ""),
             "grid": list(gv.n), "per_gpu_cells": int(gv.n[0]) * int(gv.n[1]) * int(gv.n[2]) // world,
             "parallelism": f"z-slab x{world}",
-            "transport": transport, "fused": fused, "zchunk_tuned": zc,
+            "transport": transport, "fused": fused, "tuned_zchunk_gen_cus": zc,
             "flux_planes": args.flux, "flux_nfreq": args.nfreq if args.flux else 0,
             "model_bytes_per_cell_step": bpc,
             "model_fraction_of_peak": round(bpc * total_cells / world / (el / args.steps) / 1e9

@@ -236,14 +236,16 @@ int mnl_fields_require_component(mnl_fields *f, int comp);
  * centre (src/step.cpp:138-139) every `every` steps (default 100, and after the
  * last step): fails with "meep: simulation fields are NaN or Inf". */
 int mnl_fields_step(mnl_fields *f, int nsteps);
-/* No reference counterpart (a tuning knob of this implementation): chooses the z-chunk
- * length of the tile kernel by timing each candidate (automatic, 16, 20, 24, 32, 48) over
- * `reps` real steps after one warm-up step each.  Advances the fields by up to
- * 2 + 6 * (1 + reps) steps (the first steps until the fused mode is on), with results
- * identical to plain stepping.  *chosen = the length kept (0 = automatic), or -1 when
- * nothing was tuned (not in the fused tile mode: at most 2 steps taken; MNL_FUSED_ZCHUNK
- * set: none). */
-int mnl_fields_tune_zchunk(mnl_fields *f, int reps, int *chosen);
+/* No reference counterpart (tuning knobs of this implementation).  Times, over real steps
+ * (one warm-up and `reps` timed steps per candidate): (1) the tile kernel's z-chunk length
+ * (automatic, 16, 20, 24, 32, 48; skipped with MNL_FUSED_ZCHUNK set), (2) on one rank with
+ * polarization chunks, the CUs of their general kernel running beside the tile kernel
+ * (0 and five splits around the balanced one; skipped with MNL_TILE_GEN_CUS set), and keeps
+ * the fastest.  Advances the fields by at most 2 + 12 * (1 + reps) steps, with results
+ * identical to plain stepping.  *zchunk = the length kept (0 = automatic), *gen_cus = the
+ * CUs kept (0 = one launch after the other); -1 = not tuned (not in the fused tile mode:
+ * at most 2 steps taken). */
+int mnl_fields_tune(mnl_fields *f, int reps, int *zchunk, int *gen_cus);
 int mnl_fields_set_nan_check(mnl_fields *f, int every);
 /* Field energy over the box [vmin, vmax] (NULL, NULL: the whole cell,
  * user_volume.surroundings()), src/energy_and_flux.cpp:48-178:

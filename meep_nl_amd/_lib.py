@@ -77,7 +77,7 @@ _SIGS = {
                                             c_double, c_int]),
     "mnl_fields_require_component": (c_int, [c_void, c_int]),
     "mnl_fields_step": (c_int, [c_void, c_int]),
-    "mnl_fields_tune_zchunk": (c_int, [c_void, c_int, ctypes.POINTER(c_int)]),
+    "mnl_fields_tune": (c_int, [c_void, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "mnl_fields_set_nan_check": (c_int, [c_void, c_int]),
     "mnl_fields_energy_in_box": (c_int, [c_void, c_int, dptr, dptr, dptr]),
     "mnl_fields_initialize_field": (c_int, [c_void, c_int, dptr, c_size]),

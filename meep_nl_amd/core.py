@@ -395,14 +395,15 @@ class Fields:
     def step(self, n=1):
         check(lib().mnl_fields_step(self.h, int(n)))
 
-    def tune_zchunk(self, reps=3):
-        """Time the tile kernel's z-chunk candidates over real steps and keep the fastest
-        (mnl_fields_tune_zchunk; advances the fields by up to 2 + 6 * (1 + reps) steps,
-        results identical to plain stepping).  Returns the chunk length kept (0 = auto),
-        -1 when nothing was tuned (not in the fused tile mode)."""
-        c = ctypes.c_int(0)
-        check(lib().mnl_fields_tune_zchunk(self.h, int(reps), ctypes.byref(c)))
-        return c.value
+    def tune(self, reps=3):
+        """Time the fused step's knobs over real steps and keep the fastest (mnl_fields_tune:
+        the tile kernel's z-chunk length, then on one rank with polarization chunks the CUs
+        of their general kernel beside the tile kernel).  Advances the fields by at most
+        2 + 12 * (1 + reps) steps, results identical to plain stepping.  Returns (zchunk,
+        gen_cus); -1 = not tuned (not in the fused tile mode)."""
+        z, g = ctypes.c_int(0), ctypes.c_int(0)
+        check(lib().mnl_fields_tune(self.h, int(reps), ctypes.byref(z), ctypes.byref(g)))
+        return z.value, g.value
 
     def _time(self):
         t = ctypes.c_longlong()

@@ -281,6 +281,7 @@ struct mnl_fields {
   int fused_dist = 1;
   int gen_cus = -1;  // CUs for the general kernel running beside the lean one (0: serial)
   bool fused_concurrent = false;  // last fused step ran lean + general concurrently
+  int tile_gen_cus = 0;           // tile mode: general kernel beside the tile kernel (CUs)
   unsigned long long *d_fused_ctr = nullptr;  // work-item counters of the fused kernels
   unsigned long long ctr_base[FUSED_NCTR] = {0};  // their values at the next launch
   int stagger = 0, nstagger = 0;  // dev_alloc offset step (bytes) for field arrays
@@ -3113,6 +3114,15 @@ int gen_split(const mnl_fields *F) {
   return 0;
 }
 
+// tile mode, one rank: CUs of the polarization chunks' general kernel beside the tile
+// kernel (0: after it on the same stream).  MNL_TILE_GEN_CUS: read every batch (A/B).
+int tile_gen_split(const mnl_fields *F) {
+  int v = F->tile_gen_cus;
+  if (const char *e = getenv("MNL_TILE_GEN_CUS")) v = atoi(e);
+  const int cus = k_cu_count();
+  return (v > 0 && v < cus) ? v : 0;
+}
+
 // streams / events of the overlapped multi-rank step; the E ghost plane is made
 // valid once (kind 0) since each step ends with the exchange for the next one
 int multi_begin(mnl_fields *F) {
@@ -3512,6 +3522,27 @@ int step_batch(mnl_fields *F, int nsteps) {
           HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
           fa.wg_limit = k_cu_count() - split;
           kr = k_fused(fa, 0, F->stream, F->ctr_base);
+          fa.wg_limit = 0;
+          if (kr) return fused_fail("fused kernel launch failed", kr);
+          HIPCHK(hipStreamWaitEvent(F->stream, F->ev_early, 0));
+          F->fused_concurrent = true;
+        } else if (const int ts = F->tile_mode && fa.ngen > 0 ? tile_gen_split(F) : 0) {
+          // tile mode: the polarization chunks' general items on `ts` CUs of a side
+          // stream beside the tile kernel on the others (both read only the old buffers
+          // and write the ping-pong partners: no ordering between them)
+          if (!F->s_aux) {
+            HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming));
+          }
+          HIPCHK(hipEventRecord(F->ev_start, F->stream));
+          HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
+          fa.wg_limit = ts;
+          kr = k_fused(fa, 1, F->s_aux, F->ctr_base);
+          if (kr) return fused_fail("fused general kernel launch failed", kr);
+          HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
+          fa.wg_limit = k_cu_count() - ts;
+          kr = k_fused(fa, 4, F->stream, F->ctr_base);
           fa.wg_limit = 0;
           if (kr) return fused_fail("fused kernel launch failed", kr);
           HIPCHK(hipStreamWaitEvent(F->stream, F->ev_early, 0));
@@ -5424,47 +5455,88 @@ int mnl_fields_step(mnl_fields *F, int nsteps) {
   return fields_step(F, nsteps);
 }
 
-// z-chunk tuning: the tile kernel's item count / chunk length
-// trade-off (fill of the last round of items vs. the halo planes of short chunks) is
-// measured rather than modelled.  Every candidate length is stepped for real (results do
-// not depend on the chunk length: each point's update is the same arithmetic), so the
-// call advances the fields by 1 + ncand * (1 + reps) steps.
-int mnl_fields_tune_zchunk(mnl_fields *F, int reps, int *chosen) {
+// Tuning of the fused step, measured rather than modelled:
+// (1) the tile kernel's z-chunk length (fill of the last round of items vs. the halo planes
+// of short chunks); (2) on one rank with polarization chunks, the CUs given to their general
+// kernel running beside the tile kernel (a split that balances the two launches; too few
+// or too many CUs and one of them runs alone at the end).  Every candidate is stepped for
+// real: results do not depend on either knob (each point's update is the same arithmetic).
+// Times are the fused launches' own (profiling events around them), not the host's
+// per-batch work.
+int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
   if (!F || reps < 1) return fail("bad argument");
-  if (chosen) *chosen = -1;
+  if (zchunk) *zchunk = -1;
+  if (gen_cus) *gen_cus = -1;
   if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
-  if (getenv("MNL_FUSED_ZCHUNK") || getenv("MNL_ZCHUNK_STEP")) return 0;  // fixed by the user
   // the first step runs unfused (lazy first updates); the second takes the fused decision
   for (int i = 0; i < 2 && !F->fused; i++)
     if (fields_step(F, 1)) return -1;
   if (!F->fused || !F->tile_mode) return 0;
-  static const int cand[] = {0, 16, 20, 24, 32, 48};
-  // the fused launches' own GPU time (profiling events around them), not the host's
-  // per-batch work
   const bool prof = F->profiling;
   F->profiling = true;
-  int best = F->fused_zchunk;
-  double best_ms = 0;
-  int rc = 0;
   const bool verbose = getenv("MNL_TUNE_VERBOSE") != nullptr;
-  for (int c : cand) {
-    if (F->fused && set_fused(F, false)) { rc = -1; break; }
-    F->fused_zchunk = c;
-    if (fields_step(F, 1)) { rc = -1; break; }  // rebuild + warm-up
-    if (!F->fused) break;
-    const double t0 = F->timer_ms[TM_BINT] + F->timer_ms[TM_GEN];
-    if (fields_step(F, reps)) { rc = -1; break; }
-    const double ms = F->timer_ms[TM_BINT] + F->timer_ms[TM_GEN] - t0;
-    if (verbose)
-      fprintf(stderr, "tune_zchunk rank %d: zchunk %d: %.4f ms/step\n", F->rank, c, ms / reps);
-    if (best_ms == 0 || ms < best_ms) best_ms = ms, best = c;
+  auto timed = [&](double *tile_ms, double *gen_ms) -> int {  // one warm-up, `reps` timed
+    if (fields_step(F, 1)) return -1;
+    const double b0 = F->timer_ms[TM_BINT], g0 = F->timer_ms[TM_GEN];
+    if (fields_step(F, reps)) return -1;
+    *tile_ms = (F->timer_ms[TM_BINT] - b0) / reps;
+    *gen_ms = (F->timer_ms[TM_GEN] - g0) / reps;
+    return 0;
+  };
+  int rc = 0;
+  const int split0 = F->tile_gen_cus;
+  if (!getenv("MNL_FUSED_ZCHUNK") && !getenv("MNL_ZCHUNK_STEP")) {
+    static const int cand[] = {0, 16, 20, 24, 32, 48};
+    F->tile_gen_cus = 0;  // the two launches one after the other while the length is chosen
+    int best = F->fused_zchunk;
+    double best_ms = 0;
+    for (int c : cand) {
+      if (F->fused && set_fused(F, false)) { rc = -1; break; }
+      F->fused_zchunk = c;
+      double tm, gm;
+      if (timed(&tm, &gm)) { rc = -1; break; }
+      if (!F->fused) break;
+      if (verbose)
+        fprintf(stderr, "tune rank %d: zchunk %d: %.4f ms/step (tile %.4f, general %.4f)\n",
+                F->rank, c, tm + gm, tm, gm);
+      if (best_ms == 0 || tm + gm < best_ms) best_ms = tm + gm, best = c;
+    }
+    F->tile_gen_cus = split0;
+    if (!rc && F->fused && set_fused(F, false)) rc = -1;  // the next step rebuilds with `best`
+    F->fused_zchunk = best;
+    if (!rc && zchunk) *zchunk = best;
+  }
+  if (!rc && F->nranks == 1 && !getenv("MNL_TILE_GEN_CUS")) {
+    F->tile_gen_cus = 0;
+    double tm = 0, gm = 0;
+    if (timed(&tm, &gm)) rc = -1;
+    if (!rc && F->fused && F->tile_mode && gm > 0) {
+      // start from the split that gives both launches the same time at their measured
+      // one-after-the-other rates, in multiples of 8 CUs (one per XCD)
+      const int cus = k_cu_count();
+      const int s0 = 8 * (int)std::lround(cus * gm / (gm + tm) / 8.0);
+      int best = 0;
+      double best_ms = tm + gm;
+      if (verbose)
+        fprintf(stderr, "tune rank %d: general CUs 0: %.4f ms/step\n", F->rank, best_ms);
+      for (int d : {-16, -8, 0, 8, 16}) {
+        const int sc = s0 + d;
+        if (sc < 8 || sc > cus - 8) continue;
+        F->tile_gen_cus = sc;
+        double t2, g2;
+        if (timed(&t2, &g2)) { rc = -1; break; }
+        if (verbose)
+          fprintf(stderr, "tune rank %d: general CUs %d: %.4f ms/step\n", F->rank, sc, t2 + g2);
+        if (t2 + g2 < best_ms) best_ms = t2 + g2, best = sc;
+      }
+      F->tile_gen_cus = best;
+      if (!rc && gen_cus) *gen_cus = best;
+    } else {
+      F->tile_gen_cus = split0;
+    }
   }
   F->profiling = prof;
-  if (rc) return rc;
-  if (F->fused && set_fused(F, false)) return -1;  // the next step rebuilds with `best`
-  F->fused_zchunk = best;
-  if (chosen) *chosen = best;
-  return 0;
+  return rc;
 }
 
 int mnl_fields_initialize_field(mnl_fields *F, int comp, const double *host, size_t n) {

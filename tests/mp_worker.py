@@ -41,7 +41,7 @@ def run_case(name, make):
         o = S.sc_big_box_3d(make, steps=16)
     elif name == "big_box_tuned":  # z-chunk tuner on every rank (collective steps), then 30
         o = S.sc_big_box_3d(make, steps=0)
-        extra["zchunk"] = np.array([o._fields().tune_zchunk(reps=1)])
+        extra["zchunk"] = np.array([o._fields().tune(reps=1)[0]])
         o.step(30 - o.t)
     elif name == "kerr_lorentz":
         o = S.sc_kerr_lorentz_3d(make)
