@@ -5472,7 +5472,10 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
   for (int i = 0; i < 2 && !F->fused; i++)
     if (fields_step(F, 1)) return -1;
   if (!F->fused || !F->tile_mode) return 0;
-  const bool prof = F->profiling;
+  const bool prof = F->profiling;  // restored with the timers after tuning
+  double tms[16];
+  long long tcnt[16];
+  for (int k = 0; k < 16; k++) tms[k] = F->timer_ms[k], tcnt[k] = F->timer_count[k];
   F->profiling = true;
   const bool verbose = getenv("MNL_TUNE_VERBOSE") != nullptr;
   auto timed = [&](double *tile_ms, double *gen_ms) -> int {  // one warm-up, `reps` timed
@@ -5536,6 +5539,7 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
     }
   }
   F->profiling = prof;
+  for (int k = 0; k < 16; k++) F->timer_ms[k] = tms[k], F->timer_count[k] = tcnt[k];
   return rc;
 }
 
