@@ -233,8 +233,8 @@ int mnl_fields_add_custom_volume_source(mnl_fields *f, int comp, mnl_src_func fu
 int mnl_fields_require_component(mnl_fields *f, int comp);
 /* fields::step() x nsteps (src/step.cpp:35-140).  Collective for
  * distributed fields.  NaN/Inf check of the D energy density at the cell
- * centre (src/step.cpp:138-139) every `every` steps (default 100, and after the
- * last step): fails with "meep: simulation fields are NaN or Inf". */
+ * centre (src/step.cpp:138-139) every `every` steps, counted across calls (default
+ * 100): fails with "meep: simulation fields are NaN or Inf". */
 int mnl_fields_step(mnl_fields *f, int nsteps);
 /* No reference counterpart (tuning knobs of this implementation).  Times, over real steps
  * (one warm-up and `reps` timed steps per candidate): (1) the tile kernel's z-chunk length

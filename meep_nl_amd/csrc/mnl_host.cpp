@@ -314,7 +314,8 @@ struct mnl_fields {
                                           // (src/step_db.cpp:71-75)
   bool first_step_mode = false;
   bool force_unfused_next = false;  // E / H set directly (initialize_field): E != chi1inv D
-  int nan_every = 100;              // NaN guard cadence inside a batch (src/step.cpp:138-139)
+  int nan_every = 100;              // NaN guard cadence (src/step.cpp:138-139)
+  int since_nan = 0;                // steps since the last NaN guard (across calls)
   CurlPlan planB, planD;
   bool nr = false;
   bool upnl = false;  // upstream chi2/chi3 update active (nl_mode 1 with nonzero chi)
@@ -2795,6 +2796,10 @@ bool fused_possible(mnl_fields *F) {
   if (nu != 0 && nu != 3) return false;
   // the fused kernels address arrays with 32-bit byte offsets
   if (F->nlocal * 8 >= 0xFFFFFFF0ull) return false;
+  // the tile / chunk geometry is built on entering the fused mode and uploaded by
+  // set_fused; every change of its inputs (z-chunk, A/B switches) leaves the mode first,
+  // so a batch that is already fused reuses it (no per-call host rebuild)
+  if (F->fused) return true;
   if (!make_fused_boxes(F)) return false;
   return true;
 }
@@ -4680,7 +4685,7 @@ int energy_in_box(mnl_fields *F, int which, const double wmin[3], const double w
 }
 
 // fields::step() n times: the NaN guard (src/step.cpp:138-139) every nan_every
-// steps; the first step after construction (or after E / H were set directly)
+// steps (counted across calls); the first step after construction (or after E / H were set directly)
 // runs unfused (see e_first_done)
 static int g_verbosity = 1;  // meep::verbosity (src/meep.hpp: default 1)
 
@@ -4740,11 +4745,17 @@ int fields_step_batches(mnl_fields *F, int nsteps) {
       F->force_unfused_next = false;
       m = 1;
     } else {
-      m = std::min(nsteps, F->nan_every);
+      m = std::min(nsteps, std::max(1, F->nan_every - F->since_nan));
       if (step_batch(F, m)) return -1;
     }
     nsteps -= m;
-    if (nan_check(F)) return -1;
+    // every nan_every steps, counted across calls (a loop of one-step calls pays the
+    // guard's device round trips once per nan_every steps, not once per call)
+    F->since_nan += m;
+    if (F->since_nan >= F->nan_every) {
+      F->since_nan = 0;
+      if (nan_check(F)) return -1;
+    }
     if (g_verbosity > 0 && F->rank == 0) {
       const double now = wall_now();
       if (now > F->last_out_wall + 4.0 && F->t > F->last_out_t) {
