@@ -62,10 +62,12 @@ def build(make, seed):
             o.set_chi3(c, np.where(_inside(o, c, lo, hi), 1e-2, 0.0))
     for _ in range(int(rng.integers(1, 4))):
         comp = int(rng.choice([0, 1, 2, 0, 1, 2, 3, 4, 5]))
-        pos = tuple(float(rng.uniform(-0.4, 0.4) * L) for L in sizes)
+        cen = o.center()  # the cell is [0, L] without center_origin
+        pos = tuple(float(cen[d] + rng.uniform(-0.4, 0.4) * L) for d, L in enumerate(sizes))
         f = float(rng.uniform(0.15, 0.5))
-        o.add_gaussian_source(comp, f, float(rng.uniform(2.0, 10.0)), 0.0,
-                              float(rng.uniform(20.0, 100.0)), pos, float(rng.uniform(0.5, 2.0)))
+        end = float(rng.uniform(20.0, 100.0))  # start = -end: the pulse peaks at t = 0
+        o.add_gaussian_source(comp, f, float(rng.uniform(2.0, 10.0)), -end, end, pos,
+                              float(rng.uniform(0.5, 2.0)))
     if rng.random() < 0.5:
         random_init(o, (6, 7, 8, 9, 10, 11), seed=seed)
     steps = int(rng.integers(3, 31))
@@ -78,6 +80,7 @@ def test_fuzz_one_gpu(seed):
     p, _ = build(ProductSim, seed)
     o, _ = build(make_oracle, seed)
     assert p.t == o.t
+    assert any(np.any(o.get_array(c) != 0) for c in ALL_COMPS)  # not a trivial comparison
     for c in ALL_COMPS:
         a, b = p.get_array(c), o.get_array(c)
         assert a.shape == b.shape, c
@@ -138,6 +141,7 @@ def build_rich(make, seed):
 def test_fuzz_rich(seed):
     p, hp = build_rich(ProductSim, seed)
     o, ho = build_rich(make_oracle, seed)
+    assert any(np.any(o.get_array(c) != 0) for c in ALL_COMPS)
     for c in ALL_COMPS:
         a, b = p.get_array(c), o.get_array(c)
         assert np.array_equal(a, b), (seed, c, float(np.max(np.abs(a - b))))
@@ -165,11 +169,71 @@ def test_fuzz_2d(seed):
                 o.set_chi1inv(c, c, np.where(m, 1.0 / eps, 1.0))
         for _ in range(int(rng.integers(1, 4))):
             comp = int(rng.choice([0, 1, 2, 3, 4, 5]))
-            pos = tuple(float(rng.uniform(-0.4, 0.4) * L) for L in sizes)
-            o.add_gaussian_source(comp, float(rng.uniform(0.15, 0.5)), 5.0, 0.0, 60.0, pos, 1.0)
+            cen = o.center()
+            pos = tuple(float(cen[d] + rng.uniform(-0.4, 0.4) * L) for d, L in enumerate(sizes))
+            o.add_gaussian_source(comp, float(rng.uniform(0.15, 0.5)), 5.0, -60.0, 60.0, pos, 1.0)
         o.step(int(rng.integers(10, 80)))
         return o
     p, o = build2(ProductSim), build2(make_oracle)
+    assert any(np.any(o.get_array(c) != 0) for c in ALL_COMPS if o.get_array(c).size)
     for c in ALL_COMPS:
         a, b = p.get_array(c), o.get_array(c)
         assert np.array_equal(a, b), (seed, c, float(np.max(np.abs(a - b))) if a.size else 0)
+
+
+# ---- physics family: anisotropic Lorentzian sigma (diagonal + one symmetric off-diagonal
+# pair), upstream Meep's Pade chi2 / chi3 mode, mu boxes with a magnetic Lorentzian
+@pytest.mark.parametrize("seed", list(range(30)))
+def test_fuzz_physics(seed):
+    def build3(make):
+        rng = np.random.default_rng(13000 + seed)
+        sizes = [float(rng.choice([2.0, 2.7, 3.3])) for _ in range(3)]
+        o = vol(make, 3, sizes, 10, center_origin=True)
+        if rng.random() < 0.7:
+            o.add_pml(0.5)
+        kind = int(rng.integers(0, 3))
+        lo, hi = _box(rng, sizes)
+        if kind == 0:  # anisotropic sigma
+            a, b = sorted(rng.choice(3, 2, replace=False))
+            sig = [[None] * 3 for _ in range(3)]
+            v = float(rng.uniform(0.05, 0.15))
+            for c in E_COMPS:
+                m = _inside(o, c, lo, hi)
+                sig[c][c] = np.where(m, float(rng.uniform(0.2, 0.6)), 0.0)
+                h = 0.05  # off-diagonal entries half a pixel back along c
+                xyz = [q - h * (d == c) for d, q in enumerate(o.coords(c))]
+                ms = np.ones_like(xyz[0], dtype=bool)
+                for d in range(3):
+                    ms &= (xyz[d] >= lo[d]) & (xyz[d] <= hi[d])
+                if c == a:
+                    sig[c][b] = np.where(ms, v, 0.0)
+                if c == b:
+                    sig[c][a] = np.where(ms, v, 0.0)
+            o.add_lorentzian_tensor(float(rng.uniform(0.8, 1.3)), 0.05, sig)
+        elif kind == 1:  # upstream nonlinear mode
+            o.set_upstream_nl(True)
+            for c in E_COMPS:
+                m = _inside(o, c, lo, hi)
+                o.set_chi1inv(c, c, np.where(m, 1 / 2.25, 1.0))
+                o.set_chi3(c, np.where(m, 2e-2, 0.0))
+                if rng.random() < 0.5:
+                    o.set_chi2(c, np.where(m, 3e-2, 0.0))
+        else:  # mu box and a magnetic Lorentzian
+            mu = float(rng.uniform(1.5, 4.0))
+            o.set_mu_fn(lambda x, y, z: np.where((x >= lo[0]) & (x <= hi[0]) & (y >= lo[1]) &
+                                                 (y <= hi[1]) & (z >= lo[2]) & (z <= hi[2]), mu, 1.0))
+            if rng.random() < 0.6:
+                o.add_magnetic_lorentzian(float(rng.uniform(0.8, 1.3)), 0.1,
+                                          [np.where(_inside(o, c, lo, hi), 0.3, 0.0)
+                                           for c in (3, 4, 5)])
+        for _ in range(int(rng.integers(1, 3))):
+            pos = tuple(float(rng.uniform(-0.3, 0.3) * L) for L in sizes)
+            o.add_gaussian_source(int(rng.integers(0, 3)), 0.3, 4.0, 0.0, 40.0, pos,
+                                  float(rng.uniform(1.0, 20.0)))
+        o.step(int(rng.integers(5, 31)))
+        return o
+    p, o = build3(ProductSim), build3(make_oracle)
+    assert any(np.any(o.get_array(c) != 0) for c in ALL_COMPS)
+    for c in ALL_COMPS:
+        a, b = p.get_array(c), o.get_array(c)
+        assert np.array_equal(a, b), (seed, c, float(np.max(np.abs(a - b))))
