@@ -53,6 +53,9 @@ def run_case(name, make):
         o = S.sc_averaged(make, upstream=True)
     elif name == "c5_small":
         o = S.sc_c5_small(make)
+    elif name.startswith("fuzz"):  # a seeded random configuration (tests/test_gpu_fuzz.py)
+        from test_gpu_fuzz import build
+        o, _ = build(make, int(name[4:]))
     elif name == "flux":
         o, hs = S.sc_flux_3d(make, steps=40)
         for k, h in enumerate(hs):

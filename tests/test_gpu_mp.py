@@ -23,8 +23,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CASES2 = ["vacuum_pml", "big_box", "big_box_tuned", "kerr_lorentz", "nr_dispersive", "nr_seam",
-          "flux"]
-CASES3 = ["big_box", "flux", "averaged_up"]
+          "flux", "fuzz0", "fuzz2", "fuzz9", "fuzz16"]
+CASES3 = ["big_box", "flux", "averaged_up", "fuzz5", "fuzz24"]
 CASES8 = ["c5_small"]  # BASELINE C5's decomposition (8 z-slabs) at reduced x-y
 
 
@@ -80,6 +80,9 @@ def _oracle(name):
         return S.sc_averaged(make_oracle, upstream=True), {}
     if name == "c5_small":
         return S.sc_c5_small(make_oracle), {}
+    if name.startswith("fuzz"):
+        from test_gpu_fuzz import build
+        return build(make_oracle, int(name[4:]))[0], {}
     o, hs = S.sc_flux_3d(make_oracle, steps=40)
     ex = {f"flux{k}": o.flux(h) for k, h in enumerate(hs)}
     ex["slice_plane"] = o.get_array_slice(2, [-1.6, -1.6, 0.3], [1.6, 1.6, 0.3])
