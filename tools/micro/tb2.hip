@@ -82,9 +82,12 @@ __global__ void ref_d(Grid g, F6 s, F6 t) {  // reads t.b (new B), s.d; writes t
 }
 
 // ---- tile kernels: TWO = 2-step march, else the same structure doing one step
-constexpr int LX = 64, LY = 16, HXL = 8, HYL = 2, OWNX = 48, OWNY = 12;
+constexpr int LX = 64, LY = 16, HYL = 2, OWNY = 12;
+// x shape: own columns per tile OX, lanes left of them HX, origin X0 of tile 0's own
+// range (48 / 8 / -40: 512-B aligned loads, whole-sector stores; 56 / 4 / -52: 64-B aligned
+// loads, 32-B offset stores, 17 % more own points per item)
 
-template <bool TWO, bool PF = false>  // PF: next plane's loads issued one iteration ahead
+template <bool TWO, bool PF = false, int OWNX = 48, int HXL = 8, int X0 = -40>  // PF: prefetch
 __global__ __launch_bounds__(1024) void tile_kernel(Grid g, F6 s, F6 t, int ntx, int nty, int chunk) {
   __shared__ double sE1[3][LY][LX], sH1[3][LY][LX], sE2[3][LY][LX], sH2[3][LY][LX];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -93,7 +96,7 @@ __global__ __launch_bounds__(1024) void tile_kernel(Grid g, F6 s, F6 t, int ntx,
   item /= ntx;
   const int ty = item % nty;
   const int ch = item / nty;
-  const int x0 = -40 + OWNX * tx, y0 = 2 + OWNY * ty;
+  const int x0 = X0 + OWNX * tx, y0 = 2 + OWNY * ty;
   const int zs = 2 + chunk * ch, ze = min(zs + chunk, g.nz - 2);
   const int i = x0 - HXL + lane, j = y0 - HYL + w;
   const int ic = min(max(i, 0), g.nx - 1), jc = min(max(j, 0), g.ny - 1);
@@ -235,7 +238,9 @@ int main(int argc, char **argv) {
     init_kernel<<<4096, 256>>>(A.b[c], n, 101 + c);
   }
   CK(hipDeviceSynchronize());
+  const int OWNX = 48;
   const int ntx = (N - 3 + 40) / OWNX + 1, nty = (N - 5) / OWNY + 1, nch = (N - 4 + chunk - 1) / chunk;
+  const int ntx56 = (N - 3 + 52) / 56 + 1, items56 = ntx56 * nty * nch;
   const int items = ntx * nty * nch;
   // shapes the kernels assume (checked before any launch)
   if (N < 16 || chunk < 1 || -40 + OWNX * (ntx - 1) > N - 3 || 2 + OWNY * (nty - 1) > N - 3 ||
@@ -279,8 +284,17 @@ int main(int argc, char **argv) {
     if (v == 1) tile_kernel<true><<<items, 1024>>>(g, src, dst, ntx, nty, chunk);
     if (v == 2) tile_kernel<false, true><<<items, 1024>>>(g, src, dst, ntx, nty, chunk);
     if (v == 3) tile_kernel<true, true><<<items, 1024>>>(g, src, dst, ntx, nty, chunk);
+    if (v == 5) tile_kernel<true, true, 56, 4, -52><<<items56, 1024>>>(g, src, dst, ntx56, nty, chunk);
   };
-  for (int v = 0; v < 4; v++) {
+  {  // parity of the 56-wide shape
+    copy6(B, A, n);
+    launch(5, A, B);
+    CK(hipDeviceSynchronize());
+    printf("parity: 2-step 56-wide %s\n", same6(B, R, n, "2-step 56-wide vs naive") ? "bitwise" : "DIFFERS");
+    copy6(B, A, n);
+  }
+  for (int v = 0; v < 6; v++) {
+    if (v == 4) continue;
     const int two = v & 1;
     for (int wu = 0; wu < 2; wu++) launch(v, A, B);
     CK(hipEventRecord(e0));
@@ -293,9 +307,9 @@ int main(int argc, char **argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double per = ms / reps, steps = two ? 2.0 : 1.0;
-    printf("%s%s: %.4f ms per launch, %.1f G cell-steps/s (%d^3, chunk %d, %d items), "
+    printf("%s%s%s: %.4f ms per launch, %.1f G cell-steps/s (%d^3, chunk %d, %d items), "
            "algorithmic 96 B/cell-step -> %.2f TB/s equivalent\n",
-           two ? "2-step" : "1-step", v >= 2 ? " (prefetch)" : "", per, cells * steps / per / 1e6, N, chunk, items,
+           two ? "2-step" : "1-step", v >= 2 ? " (prefetch)" : "", v == 5 ? " 56-wide" : "", per, cells * steps / per / 1e6, N, chunk, v == 5 ? items56 : items,
            cells * steps * 96.0 / per / 1e9);
   }
   return ok1 && ok2 ? 0 : 2;
