@@ -273,11 +273,6 @@ struct mnl_fields {
   hipStream_t s_aux = nullptr, s_comm = nullptr;
   hipEvent_t ev_start = nullptr, ev_early = nullptr, ev_x1 = nullptr, ev_shell = nullptr,
              ev_x0 = nullptr;
-  // one-rank fused stepping with DFT monitors: sampling / accumulation on s_dft beside the
-  // next step; ev_dft[t & 1] = the DFT work on state t is done
-  hipStream_t s_dft = nullptr;
-  hipEvent_t ev_dstep = nullptr, ev_dft[2] = {nullptr, nullptr};
-  bool dft_pending[2] = {false, false};
   double *pp_B[3] = {nullptr, nullptr, nullptr}, *pp_D[3] = {nullptr, nullptr, nullptr};
   double *pp_E[3] = {nullptr, nullptr, nullptr}, *pp_H[3] = {nullptr, nullptr, nullptr};
   double *pp_UB[3] = {nullptr, nullptr, nullptr};
@@ -374,9 +369,8 @@ struct mnl_fields {
     if (d_uflag) hipFree(d_uflag);
     if (d_gflag) hipFree(d_gflag);
     comm.reset();
-    for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0, ev_dstep, ev_dft[0], ev_dft[1]})
+    for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
       if (e) hipEventDestroy(e);
-    if (s_dft) hipStreamDestroy(s_dft);
     if (s_aux) hipStreamDestroy(s_aux);
     if (s_comm) hipStreamDestroy(s_comm);
     if (stream) hipStreamDestroy(stream);
@@ -1928,10 +1922,7 @@ int dft_add_fields(mnl_fields *F, int ncomp, const int *comps, const double wmin
 }
 
 // phases of every DFT update in steps [t0+1, t0+ns] -> device (one row per update)
-constexpr bool DFT_SIDE_DEFAULT = false;  // DFT work beside the next step (step_batch)
-
 int dft_prepare(mnl_fields *F, long long t0, int ns) {
-  if (F->s_dft) HIPCHK(hipStreamSynchronize(F->s_dft));  // its accumulations read the phases
   for (auto &op : F->dfts) {
     DftFluxH &o = *op;
     o.row = 0;
@@ -1969,31 +1960,29 @@ int dft_prepare(mnl_fields *F, long long t0, int ns) {
 }
 
 // accumulate the buffered updates of one flux object
-int dft_flush(mnl_fields *F, DftFluxH &o, hipStream_t st = nullptr) {
+int dft_flush(mnl_fields *F, DftFluxH &o) {
   if (!o.nbuf) return 0;
-  if (!st) st = F->stream;
   const size_t nch = o.E.size() + o.H.size();
   const long long rstride = (long long)(nch * o.nfreq);
   if (k_dft_accum(o.d_pj, o.d_pch, o.d_dft, o.d_fr, o.nbuf,
                   o.d_ph + 2 * (size_t)(o.row - o.nbuf) * rstride, rstride, o.nfreq,
-                  (long long)o.npts, st))
+                  (long long)o.npts, F->stream))
     return fail("dft accumulate launch failed");
   o.nbuf = 0;
   return 0;
 }
 
 // after step t (fields::update_dfts, src/dft.cpp:249-263)
-int dft_update(mnl_fields *F, long long t, hipStream_t st = nullptr) {
-  if (!st) st = F->stream;
+int dft_update(mnl_fields *F, long long t) {
   for (auto &op : F->dfts) {
     DftFluxH &o = *op;
     if (t % o.decim || !o.npts) continue;
     if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, o.d_fr + (size_t)o.nbuf * o.npts,
-                     (long long)o.npts, F->g, F->f, st))
+                     (long long)o.npts, F->g, F->f, F->stream))
       return fail("dft sample launch failed");
     o.nbuf++;
     o.row++;
-    if (o.nbuf == o.kb && dft_flush(F, o, st)) return -1;
+    if (o.nbuf == o.kb && dft_flush(F, o)) return -1;
   }
   return 0;
 }
@@ -3443,28 +3432,9 @@ int step_batch(mnl_fields *F, int nsteps) {
   };
   // fields::update_dfts after t += 1 (src/step.cpp:125-127); a rank's averages
   // read its low ghost planes, which must hold this step's values first
-  // one rank, fused (ping-pong buffers): the DFT work on state t runs on s_dft beside step
-  // t + 1, which reads the same buffers and writes the others; step t + 2, which writes
-  // them, waits for it (ev_dft[t & 1]).  MNL_DFT_SIDE=0: on the stepping stream (A/B).
-  const char *dse = getenv("MNL_DFT_SIDE");
-  const bool dft_side = F->fused && F->nranks == 1 && !F->dfts.empty() &&
-                        (dse ? atoi(dse) != 0 : DFT_SIDE_DEFAULT);
-  if (dft_side && !F->s_dft) {
-    HIPCHK(hipStreamCreateWithFlags(&F->s_dft, hipStreamNonBlocking));
-    for (hipEvent_t *e : {&F->ev_dstep, &F->ev_dft[0], &F->ev_dft[1]})
-      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  }
   auto post_step = [&](int s) -> int {
     const long long tn = F->t + s + 1;
     if (!dft_due(F, tn)) return 0;
-    if (dft_side) {
-      HIPCHK(hipEventRecord(F->ev_dstep, F->stream));
-      HIPCHK(hipStreamWaitEvent(F->s_dft, F->ev_dstep, 0));
-      if (dft_update(F, tn, F->s_dft)) return -1;
-      HIPCHK(hipEventRecord(F->ev_dft[tn & 1], F->s_dft));
-      F->dft_pending[tn & 1] = true;
-      return 0;
-    }
     if (F->nranks > 1) {
       if (F->fused)
         HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
@@ -3518,13 +3488,6 @@ int step_batch(mnl_fields *F, int nsteps) {
     for (int s = 0; s < ns; s++) {
       DevFields &f = F->f;
       const DevGrid &g = F->g;
-      {  // this step writes the buffers of state t - 1: their DFT work must be done
-        const int q = (int)((F->t + s + 1) & 1);
-        if (F->dft_pending[q]) {
-          HIPCHK(hipStreamWaitEvent(F->stream, F->ev_dft[q], 0));
-          F->dft_pending[q] = false;
-        }
-      }
       f.nr_t = F->t + s;  // seeds of the NR random fallback (nr_voxel_seed)
       const double *vs = F->d_vals + (size_t)s * per;  // this step's table
       const SrcDev sB = src_dev(F, 0, vs), sD = src_dev(F, 1, vs + 2 * ng);
@@ -3693,9 +3656,9 @@ int step_batch(mnl_fields *F, int nsteps) {
       if (post_step(s)) return -1;
     }
     if (!F->dfts.empty()) {
-      const int k = dft_side ? -1 : ev_begin(TM_DFTF);
+      const int k = ev_begin(TM_DFTF);
       for (auto &o : F->dfts)
-        if (dft_flush(F, *o, dft_side ? F->s_dft : F->stream)) return -1;
+        if (dft_flush(F, *o)) return -1;
       ev_end(k);
     }
     F->t += ns;
@@ -3704,10 +3667,6 @@ int step_batch(mnl_fields *F, int nsteps) {
   if (F->s_comm) {
     HIPCHK(hipStreamSynchronize(F->s_comm));
     HIPCHK(hipStreamSynchronize(F->s_aux));
-  }
-  if (F->s_dft) {
-    HIPCHK(hipStreamSynchronize(F->s_dft));
-    F->dft_pending[0] = F->dft_pending[1] = false;
   }
   HIPCHK(hipStreamSynchronize(F->stream));
   HIPCHK(hipGetLastError());
