@@ -353,9 +353,22 @@ int mnl_fields_set_profiling(mnl_fields *f, int on);
  * which = 2: general fused kernel (PML / boundary tiles);
  * which = 3: the DFT updates of one step (all flux objects);
  * which = 4: the E update (update_eh(E_stuff): chi(2) Newton-Raphson,
- *            Lorentzian P), unfused mode; bytes 0 (not HBM-bound). */
+ *            Lorentzian P), unfused mode; bytes 0 (not HBM-bound);
+ * which = 5: the two-step (temporal-blocking) kernel, one launch per pair of
+ *            steps; bytes of its two steps;
+ * which = 6: the rim launches of those pairs (two per pair), one step each. */
 int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch);
+/* Temporal blocking (no reference counterpart: how this build steps pairs of
+ * fields::step(), src/step.cpp:35-140).  out[0..n) of:
+ * active (1: the current fused geometry steps pairs), own cells of the two-step
+ * items, border points (upper bound), own cells of mixed-palette two-step items,
+ * rim cells, mixed-palette rim cells, two-step items, rim items, planes of the
+ * first two-step item. */
+int mnl_fields_tb_info(mnl_fields *f, double *out, int n);
+/* Allow (1, the default; MNL_TB=0 at creation turns it off) or forbid (0) stepping
+ * pairs of steps with the two-step kernel.  Results are identical either way. */
+int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
 
 /* ---- checkpoint (src/fields_dump.cpp, src/structure_dump.cpp) -----------
  * fields::dump / fields::load (src/fields_dump.cpp:108-145, 232-270): t and

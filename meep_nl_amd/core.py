@@ -566,6 +566,21 @@ class Fields:
                                             ctypes.byref(b)))
         return n.value, ms.value, b.value
 
+    def set_temporal_blocking(self, on=True):
+        """Allow / forbid stepping pairs of steps with the two-step kernel (identical
+        results either way)."""
+        check(lib().mnl_fields_set_temporal_blocking(self.h, 1 if on else 0))
+
+    def tb_info(self):
+        """Temporal blocking of the current fused geometry: dict of
+        active, two-step own cells / border points / mixed-palette cells, rim cells /
+        mixed-palette rim cells, item counts and the first item's planes."""
+        v = (ctypes.c_double * 9)()
+        check(lib().mnl_fields_tb_info(self.h, v, 9))
+        keys = ("active", "tb_cells", "tb_border", "tb_cells_mixed", "rim_cells",
+                "rim_cells_mixed", "tb_items", "rim_items", "tb_planes")
+        return {k: (bool(x) if k == "active" else int(x)) for k, x in zip(keys, v)}
+
     def traffic_model(self):
         b = ctypes.c_double()
         c = ctypes.c_double()

@@ -35,7 +35,8 @@ using namespace mnl;
 typedef std::complex<double> cplx;
 
 namespace {
-constexpr int FX_HOST = 64;  // fused tile width (FX in mnl_kernels.hip)
+constexpr int FX_HOST = 64;    // fused tile width (FX in mnl_kernels.hip)
+constexpr int FOWN_HOST = 14;  // own rows of a tile item (FOWN in mnl_kernels.hip)
 
 const double pi = 3.141592653589793238462643383276;  // meep::pi
 thread_local std::string g_err;
@@ -314,6 +315,26 @@ struct mnl_fields {
                                           // (src/step_db.cpp:71-75)
   bool first_step_mode = false;
   bool force_unfused_next = false;  // E / H set directly (initialize_field): E != chi1inv D
+  // temporal blocking: pairs of steps as rim (one-step tile kernel) +
+  // L2 (two-step kernel) + rim, over three buffer sets
+  bool tb_enabled = true;           // MNL_TB=0 at creation: never
+  int tb_zchunk = 0;                // planes per two-step item (0: automatic)
+  unsigned fused_epoch = 0;         // bumped on every entry into the fused mode
+  unsigned long long tb_sig = 0;    // inputs of the current plan (0: none)
+  bool tb_have = false;             // the current plan has two-step items
+  bool tb_mid_fresh = false;        // middle set holds a copy of the state (ghost / wall entries)
+  std::vector<int> tb_ritems, tb_rgeo;  // rim items (tile-kernel codes) and their own boxes
+  std::vector<TB2Item> tb_items;        // two-step items
+  int *d_tb_ritems = nullptr, *d_tb_rgeo = nullptr;
+  unsigned *d_tb_rflag = nullptr, *d_tb_uflag = nullptr;
+  TB2Item *d_tb_items = nullptr;
+  size_t tb_rcap = 0, tb_gcap = 0, tb_icap = 0;
+  double *pp3_B[3] = {nullptr, nullptr, nullptr}, *pp3_D[3] = {nullptr, nullptr, nullptr};
+  double *pp3_E[3] = {nullptr, nullptr, nullptr}, *pp3_H[3] = {nullptr, nullptr, nullptr};
+  double *pp3_UB[3] = {nullptr, nullptr, nullptr};
+  double tb_cells = 0, tb_border = 0, tb_cells_nu = 0;  // own / border points of the items,
+                                                        // own points of the mixed-palette ones
+  double rim_cells = 0, rim_lean = 0, rim_cells_nu = 0;  // rim items: own / lean / mixed cells
   int nan_every = 100;              // NaN guard cadence (src/step.cpp:138-139)
   int since_nan = 0;                // steps since the last NaN guard (across calls)
   CurlPlan planB, planD;
@@ -368,6 +389,9 @@ struct mnl_fields {
     if (d_tflag) hipFree(d_tflag);
     if (d_uflag) hipFree(d_uflag);
     if (d_gflag) hipFree(d_gflag);
+    for (void *p : {(void *)d_tb_ritems, (void *)d_tb_rgeo, (void *)d_tb_rflag, (void *)d_tb_uflag,
+                    (void *)d_tb_items})
+      if (p) hipFree(p);
     comm.reset();
     for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
       if (e) hipEventDestroy(e);
@@ -2251,6 +2275,49 @@ static int lean_halo_reads() {
 // whose tables are not the identity there).  The remaining (polarization) chunks keep the
 // general kernel's items (wide tiles).  Multi-rank: chunk 0 = planes 0..1 (the B the
 // lower neighbour needs), launched first.
+// directions whose PML tables are not the identity somewhere in [lo, hi] (per axis)
+int pml_dirs_in(const mnl_fields *F, const int lo[3], const int hi[3]) {
+  const DevGrid &g = F->g;
+  int m = 0;
+  for (int d = 0; d < 3; d++) {
+    if (F->h_flag[d].empty()) continue;
+    for (int j = std::max(lo[d], 0); j <= std::min(hi[d], g.N[d] - 1) && !(m >> d & 1); j++)
+      for (int sft = 0; sft < 2; sft++) {
+        const size_t q = 2 * (size_t)(j + g.off[d]) + sft;
+        if (q >= F->h_flag[d].size()) continue;
+        const double kap = F->h_kap[d][q], sig = F->h_sig[d][q];
+        if (F->h_flag[d][q] || kap - sig != 1.0 || kap + sig != 1.0 || F->h_siginv[d][q] != 1.0)
+          m |= 1 << d;
+      }
+  }
+  return m;
+}
+
+// Body code (bits 24-26) and OWNC flag (bit 29) of a tile item with own columns x0 .. x1,
+// halo row y0 (own rows y0+1 .. y1) and planes [zs, ze): the lean body when its footprint
+// lies in L, else the PML body of the directions whose tables are not the identity over the
+// footprint; OWNC when a single-axis body's footprint is owned in y and z for every component.
+int tile_item_code(const mnl_fields *F, const FusedArgs &a, const Box &L, int x0, int x1, int y0,
+                   int y1, int zs, int ze, bool *lean) {
+  const DevGrid &g = F->g;
+  *lean = x0 - 1 >= L.lo[0] && x1 + 1 <= L.hi[0] && y0 >= L.lo[1] && y1 + 1 <= L.hi[1] &&
+          zs - 1 >= L.lo[2] && ze <= L.hi[2];
+  int body = 0;
+  if (!*lean) {
+    const int lo[3] = {x0 - 1, y0, zs - 1}, hi[3] = {x0 + FX_HOST, y0 + 15, ze};
+    const int m = pml_dirs_in(F, lo, hi);
+    body = m == 1 ? 1 : m == 2 ? 2 : m == 4 ? 3 : m == 0 ? 4 : m == 3 ? 6 : m == 5 ? 7 : 5;
+  }
+  int ownc = 0;
+  if (body >= 1 && body <= 3 && !F->last_no_ownc) {
+    const int ylo = std::max(a.osh_lo[1], a.oun_lo[1]), yhi = std::min(a.osh_hi[1], a.oun_hi[1]);
+    const int zlo = std::max(a.osh_lo[2], a.oun_lo[2]), zhi = std::min(a.osh_hi[2], a.oun_hi[2]);
+    ownc = (y0 >= ylo && y0 + 15 <= yhi && zs - 1 >= zlo && ze <= zhi && y0 + 15 <= g.N[1] - 1 &&
+            ze <= g.N[2] - 1) ? 1 : 0;
+  }
+  return (body << 24) | (ownc << 29);
+}
+
 bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
   const DevGrid &g = F->g;
   FusedArgs &a = F->fgeo;
@@ -2361,22 +2428,7 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
     a.oun_lo[k] = g.owned_lo_un[k];
     a.oun_hi[k] = std::min(g.owned_hi_un[k], G.hi[k]);
   }
-  // directions whose PML tables are not the identity somewhere in [lo, hi] (per axis)
-  auto pml_dirs = [&](const int lo[3], const int hi[3]) -> int {
-    int m = 0;
-    for (int d = 0; d < 3; d++) {
-      if (F->h_flag[d].empty()) continue;
-      for (int j = std::max(lo[d], 0); j <= std::min(hi[d], g.N[d] - 1) && !(m >> d & 1); j++)
-        for (int sft = 0; sft < 2; sft++) {
-          const size_t q = 2 * (size_t)(j + g.off[d]) + sft;
-          if (q >= F->h_flag[d].size()) continue;
-          const double kap = F->h_kap[d][q], sig = F->h_sig[d][q];
-          if (F->h_flag[d][q] || kap - sig != 1.0 || kap + sig != 1.0 || F->h_siginv[d][q] != 1.0)
-            m |= 1 << d;
-        }
-    }
-    return m;
-  };
+  auto pml_dirs = [&](const int lo[3], const int hi[3]) { return pml_dirs_in(F, lo, hi); };
   // ---- tile items
   F->titems.clear();
   F->gitems.clear();
@@ -2406,27 +2458,11 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
         const int x0 = a.xb[tx], x1 = a.xb[tx + 1] - 1, y0 = a.yb[ty] - 1, y1 = a.yb[ty + 1] - 1;
         const long long cells = (long long)(x1 - x0 + 1) * (y1 - y0) * (ze - zs);
         F->tile_cells += cells;
-        const bool in_l = x0 - 1 >= L.lo[0] && x1 + 1 <= L.hi[0] && y0 >= L.lo[1] &&
-                          y1 + 1 <= L.hi[1] && zs - 1 >= L.lo[2] && ze <= L.hi[2];
-        int body = 0;
-        if (in_l) {
-          F->lean_cells += cells;
-        } else {
-          const int lo[3] = {x0 - 1, y0, zs - 1}, hi[3] = {x0 + FX_HOST, y0 + 15, ze};
-          const int m = pml_dirs(lo, hi);
-          body = m == 1 ? 1 : m == 2 ? 2 : m == 4 ? 3 : m == 0 ? 4 : m == 3 ? 6 : m == 5 ? 7 : 5;
-        }
-        // single-axis PML bodies whose footprint (rows y0 .. y0+15, planes zs-1 .. ze) is
-        // owned in y and z for every component: pml_body<AX, OWNC = true> (bit 29)
-        int ownc = 0;
-        const char *noc = getenv("MNL_NO_OWNC");
-        if (body >= 1 && body <= 3 && !(noc && atoi(noc))) {
-          const int ylo = std::max(a.osh_lo[1], a.oun_lo[1]), yhi = std::min(a.osh_hi[1], a.oun_hi[1]);
-          const int zlo = std::max(a.osh_lo[2], a.oun_lo[2]), zhi = std::min(a.osh_hi[2], a.oun_hi[2]);
-          ownc = (y0 >= ylo && y0 + 15 <= yhi && zs - 1 >= zlo && ze <= zhi &&
-                  y0 + 15 <= g.N[1] - 1 && ze <= g.N[2] - 1) ? 1 : 0;
-        }
-        const int v = tx | (ty << 8) | (ch << 16) | (body << 24) | (ownc << 29);
+        bool in_l;
+        const int code = tile_item_code(F, a, L, x0, x1, y0, y1, zs, ze, &in_l);
+        if (in_l) F->lean_cells += cells;
+        const int body = (code >> 24) & 7;
+        const int v = tx | (ty << 8) | (ch << 16) | code;
         if (F->tile_body_mask >= 0 && !((F->tile_body_mask >> body) & 1)) continue;  // timing only
         if (F->nranks > 1 && ch == 0)
           early.push_back(v);
@@ -2947,6 +2983,8 @@ int set_fused(mnl_fields *F, bool on) {
     }
     f.fG = F->fusedG;
     f.fused = 1;
+    F->fused_epoch++;  // the temporal-blocking plan and its middle set are rebuilt
+    F->tb_mid_fresh = false;
   } else {
     // materialise implicit E and the W aux fields over G (needs f.fused == 1),
     // then step in place again
@@ -2970,7 +3008,12 @@ int set_fused(mnl_fields *F, bool on) {
   return 0;
 }
 
-enum { TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT, TM_GEN, TM_DFT, TM_DFTF, TM_N };
+enum {
+  TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT, TM_GEN, TM_DFT, TM_DFTF,
+  TM_TB,   // two-step kernel (temporal blocking), one launch per pair of steps
+  TM_RIM,  // rim launches of the pairs (two per pair)
+  TM_N
+};
 
 struct EvPair {
   hipEvent_t a, b;
@@ -3329,6 +3372,409 @@ int nr_defer_end(mnl_fields *F) {
   return 0;
 }
 
+// ------------------------------------------------------------ temporal blocking
+// (DESIGN.md section 24).  Two steps n -> n+2 of a one-rank fused run as three launches over
+// three buffer sets (cur = state n, mid, nxt):
+//   R1: the tile kernel over the rim items, cur -> mid (state n+1 on the rim);
+//   source(n) into mid;
+//   L:  the two-step kernel over the L2 items, cur -> nxt (state n+2), plus the state n+1 of
+//       the L2 points on a face that borders the rim, into mid;
+//   R2: the tile kernel over the rim items, mid -> nxt;  source(n+1) into nxt.
+// L2 = the lean box shrunk by 2 minus boxes around the source points, so every value the
+// two-step march computes is the lean body's (same expression, same operands): the pair is
+// bitwise two one-step launches.  The rim is everything else of G: PML, walls, the ring of
+// width >= 2 inside the lean box and the holes.
+
+bool box_meets(const Box &a, const Box &b) {
+  for (int k = 0; k < 3; k++)
+    if (a.hi[k] < b.lo[k] || b.hi[k] < a.lo[k]) return false;
+  return true;
+}
+
+// Disjoint boxes of G: `two` covers L2 minus the holes, `rim` the rest.  Cells of the grid of
+// all box bounds, merged into x runs, then along y, then along z.
+void tb_regions(const Box &G, const Box &L2, const std::vector<Box> &holes, std::vector<Box> &two,
+                std::vector<Box> &rim) {
+  std::vector<int> cut[3];
+  for (int k = 0; k < 3; k++) {
+    std::vector<int> &c = cut[k];
+    c = {G.lo[k], G.hi[k] + 1, L2.lo[k], L2.hi[k] + 1};
+    for (const Box &h : holes) c.push_back(h.lo[k]), c.push_back(h.hi[k] + 1);
+    std::sort(c.begin(), c.end());
+    c.erase(std::unique(c.begin(), c.end()), c.end());
+    c.erase(std::remove_if(c.begin(), c.end(), [&](int v) { return v < G.lo[k] || v > G.hi[k] + 1; }),
+            c.end());
+  }
+  auto is_two = [&](int x, int y, int z) {
+    const int p[3] = {x, y, z};
+    for (int k = 0; k < 3; k++)
+      if (p[k] < L2.lo[k] || p[k] > L2.hi[k]) return false;
+    for (const Box &h : holes) {
+      bool in = true;
+      for (int k = 0; k < 3; k++) in = in && p[k] >= h.lo[k] && p[k] <= h.hi[k];
+      if (in) return false;
+    }
+    return true;
+  };
+  std::vector<Box> out[2];
+  const int nx = (int)cut[0].size() - 1, ny = (int)cut[1].size() - 1, nz = (int)cut[2].size() - 1;
+  for (int l = 0; l < nz; l++)
+    for (int j = 0; j < ny; j++)
+      for (int i = 0; i < nx;) {
+        const bool c = is_two(cut[0][i], cut[1][j], cut[2][l]);
+        int i2 = i;
+        while (i2 + 1 < nx && is_two(cut[0][i2 + 1], cut[1][j], cut[2][l]) == c) i2++;
+        Box b;
+        b.lo[0] = cut[0][i], b.hi[0] = cut[0][i2 + 1] - 1;
+        b.lo[1] = cut[1][j], b.hi[1] = cut[1][j + 1] - 1;
+        b.lo[2] = cut[2][l], b.hi[2] = cut[2][l + 1] - 1;
+        out[c ? 1 : 0].push_back(b);
+        i = i2 + 1;
+      }
+  auto merge = [](std::vector<Box> &v, int ax) {
+    for (bool changed = true; changed;) {
+      changed = false;
+      for (size_t a = 0; a < v.size() && !changed; a++)
+        for (size_t b = 0; b < v.size(); b++) {
+          if (a == b || v[b].lo[ax] != v[a].hi[ax] + 1) continue;
+          bool ok = true;
+          for (int k = 0; k < 3 && ok; k++)
+            if (k != ax) ok = v[a].lo[k] == v[b].lo[k] && v[a].hi[k] == v[b].hi[k];
+          if (!ok) continue;
+          v[a].hi[ax] = v[b].hi[ax];
+          v.erase(v.begin() + (long)b);
+          changed = true;
+          break;
+        }
+    }
+  };
+  for (auto *v : {&out[0], &out[1]}) merge(*v, 1), merge(*v, 2);
+  rim.swap(out[0]);
+  two.swap(out[1]);
+}
+
+template <class T>
+int dev_upload(mnl_fields *F, T **d, size_t &cap, const std::vector<T> &h) {
+  if (h.empty()) return 0;
+  if (cap < h.size()) {
+    if (*d) (void)hipFree(*d);
+    *d = nullptr;
+    HIPCHK(hipMalloc(d, h.size() * sizeof(T)));
+    cap = h.size();
+  }
+  HIPCHK(hipMemcpyAsync(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, F->stream));
+  return 0;
+}
+
+// Build (or keep) the plan of the current fused geometry and source points.  No plan (tb_have
+// false) when L2 is empty or an item would not fit the kernels' shapes.
+int tb_plan(mnl_fields *F) {
+  unsigned long long sig = 1469598103934665603ULL;
+  auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
+  mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
+  mix((long long)F->srcD_idx.size());
+  for (long long v : F->srcD_idx) mix(v);
+  if (sig == F->tb_sig) return 0;
+  F->tb_sig = sig;
+  F->tb_have = false;
+  F->tb_ritems.clear(), F->tb_rgeo.clear(), F->tb_items.clear();
+  const Box &G = F->fusedG, &L = F->fusedL;
+  const FusedArgs &a = F->fgeo;
+  const DevGrid &g = F->g;
+  if (F->S.dim != 3 || g.N[0] > 65535 || g.N[1] > 65535 || g.N[2] > 65535) return 0;
+  Box L2;
+  for (int k = 0; k < 3; k++) L2.lo[k] = L.lo[k] + 2, L2.hi[k] = L.hi[k] - 2;
+  // two-step tiles start 4 columns past a 64-byte boundary (their lanes start on it); the rim
+  // to the right of L2 starts on a 128-byte boundary (tile-kernel items)
+  L2.lo[0] += ((4 - L2.lo[0]) % 8 + 8) % 8;
+  L2.hi[0] = (L2.hi[0] + 1) / 16 * 16 - 1;
+  for (int k = 0; k < 3; k++)
+    if (L2.hi[k] - L2.lo[k] < 7) return 0;
+  // holes: no source point within distance 1 of a two-step own point (the march's D^{n+1}
+  // would miss the current); a box of +-2 for margin, x widened to the alignments above and
+  // to the L2 edge when that leaves fewer than 8 columns
+  std::vector<Box> holes;
+  for (long long idx : F->srcD_idx) {
+    const long long i2 = idx / g.st[2], r = idx % g.st[2];
+    const int s[3] = {(int)(r % g.st[1]), (int)(r / g.st[1]), (int)i2};
+    Box h;
+    for (int k = 0; k < 3; k++) h.lo[k] = s[k] - 2, h.hi[k] = s[k] + 2;
+    if (!box_meets(h, L2)) continue;
+    h.lo[0] = std::max(h.lo[0], 0) / 16 * 16;
+    while ((h.hi[0] + 1) % 8 != 4) h.hi[0]++;
+    for (int k = 0; k < 3; k++) h.lo[k] = std::max(h.lo[k], L2.lo[k]), h.hi[k] = std::min(h.hi[k], L2.hi[k]);
+    if (h.lo[0] - L2.lo[0] < 8) h.lo[0] = L2.lo[0];
+    if (L2.hi[0] - h.hi[0] < 8) h.hi[0] = L2.hi[0];
+    holes.push_back(h);
+  }
+  std::vector<Box> two, rim;
+  tb_regions(G, L2, holes, two, rim);
+  if (two.empty()) return 0;
+  // ---- rim items: tile-kernel shapes (columns <= 64 from 128-byte boundaries, rows <= 14,
+  // chunks <= zc cut at the lean box's z range), bodies as make_tile_boxes
+  const int zc = F->fused_zchunk > 0 ? std::min(F->fused_zchunk, FUSED_MAXCH) : 24;
+  struct RI {
+    int code, g0, g1, g2, planes;
+  };
+  std::vector<RI> heavy, lean;
+  F->rim_cells = F->rim_lean = 0;
+  for (const Box &b : rim) {
+    if (b.lo[0] % 16) return 0;  // cannot happen with the alignments above
+    std::vector<int> xs, zs;
+    split_range(xs, b.lo[0], b.hi[0] + 1, FX_HOST, 16);
+    xs.push_back(b.hi[0] + 1);
+    std::vector<int> zcut = {b.lo[2], b.hi[2] + 1};
+    for (int v : {L.lo[2] + 1, L.hi[2]})
+      if (v > b.lo[2] && v < b.hi[2] + 1) zcut.push_back(v);
+    std::sort(zcut.begin(), zcut.end());
+    for (size_t s = 0; s + 1 < zcut.size(); s++) {
+      const int n = zcut[s + 1] - zcut[s], nt = (n + zc - 1) / zc;
+      for (int t = 0; t < nt; t++) zs.push_back(zcut[s] + (int)((long long)n * t / nt));
+    }
+    zs.push_back(b.hi[2] + 1);
+    const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + FOWN_HOST - 1) / FOWN_HOST;
+    for (size_t iz = 0; iz + 1 < zs.size(); iz++)
+      for (int ty = 0; ty < nty; ty++)
+        for (size_t ix = 0; ix + 1 < xs.size(); ix++) {
+          const int x0 = xs[ix], x1 = xs[ix + 1] - 1;
+          const int yf = b.lo[1] + (int)((long long)ny * ty / nty);
+          const int y1 = b.lo[1] + (int)((long long)ny * (ty + 1) / nty) - 1;
+          const int z0 = zs[iz], z1 = zs[iz + 1];
+          bool in_l;
+          const int code = tile_item_code(F, a, L, x0, x1, yf - 1, y1, z0, z1, &in_l);
+          const double cells = double(x1 - x0 + 1) * (y1 - yf + 1) * (z1 - z0);
+          F->rim_cells += cells;
+          if (in_l) F->rim_lean += cells;
+          RI it{code, x0 | (x1 << 16), yf | (y1 << 16), z0 | (z1 << 16), z1 - z0};
+          (((code >> 24) & 7) ? heavy : lean).push_back(it);
+        }
+  }
+  auto longest_first = [](std::vector<RI> &v) {
+    std::stable_sort(v.begin(), v.end(), [](const RI &x, const RI &y) { return x.planes > y.planes; });
+  };
+  longest_first(heavy);
+  longest_first(lean);
+  for (auto *v : {&heavy, &lean})
+    for (const RI &it : *v) {
+      F->tb_ritems.push_back(it.code);
+      F->tb_rgeo.push_back(it.g0), F->tb_rgeo.push_back(it.g1), F->tb_rgeo.push_back(it.g2);
+    }
+  // ---- two-step items: 56 x 12 own points, z chunks of tz planes (automatic: the length
+  // whose item count fills whole rounds of one workgroup per CU best, with the three
+  // halo planes of a chunk as overhead)
+  int tz = F->tb_zchunk;
+  if (tz <= 0) {
+    const long long cus = std::max(1, k_cu_count());
+    double best = -1;
+    for (int cand : {32, 40, 48, 56, 64, 80, 96, 128}) {
+      long long items = 0, chunks = 0, planes = 0;
+      for (const Box &b : two) {
+        const long long ntx = (b.hi[0] - b.lo[0] + TB_OX) / TB_OX;
+        const long long nty = (b.hi[1] - b.lo[1] + TB_OY) / TB_OY;
+        const long long nz = b.hi[2] - b.lo[2] + 1, nch = (nz + cand - 1) / cand;
+        items += ntx * nty * nch;
+        chunks += nch;
+        planes += nz;
+      }
+      const double fill = double(items) / double(((items + cus - 1) / cus) * cus);
+      const double per = double(planes) / double(std::max(chunks, 1LL));
+      const double score = fill * per / (per + 3.0);
+      if (score > best + 1e-12) best = score, tz = cand;
+    }
+  }
+  F->tb_cells = F->tb_border = 0;
+  for (const Box &b : two) {
+    const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + TB_OY - 1) / TB_OY;
+    const int nz = b.hi[2] - b.lo[2] + 1, nch = (nz + tz - 1) / tz;
+    for (int ch = 0; ch < nch; ch++)
+      for (int ty = 0; ty < nty; ty++)
+        for (int x0 = b.lo[0]; x0 <= b.hi[0]; x0 += TB_OX) {
+          Box o;
+          o.lo[0] = x0, o.hi[0] = std::min(x0 + TB_OX - 1, b.hi[0]);
+          o.lo[1] = b.lo[1] + (int)((long long)ny * ty / nty);
+          o.hi[1] = b.lo[1] + (int)((long long)ny * (ty + 1) / nty) - 1;
+          o.lo[2] = b.lo[2] + (int)((long long)nz * ch / nch);
+          o.hi[2] = b.lo[2] + (int)((long long)nz * (ch + 1) / nch) - 1;
+          // faces bordering the rim: the layer outside the face, widened by 1 along the other
+          // axes (points of an edge / corner see diagonal neighbours), meets a rim box
+          int faces = 0;
+          double nb = 0;
+          for (int f = 0; f < 6; f++) {
+            const int ax = f / 2;
+            Box s = o;
+            for (int k = 0; k < 3; k++)
+              if (k != ax) s.lo[k]--, s.hi[k]++;
+            s.lo[ax] = s.hi[ax] = (f & 1) ? o.hi[ax] + 1 : o.lo[ax] - 1;
+            bool m = false;
+            for (const Box &r : rim) m = m || box_meets(s, r);
+            if (m) {
+              faces |= 1 << f;
+              double fc = 1;
+              for (int k = 0; k < 3; k++)
+                if (k != ax) fc *= o.hi[k] - o.lo[k] + 1;
+              nb += fc;
+            }
+          }
+          TB2Item it;
+          it.x = o.lo[0] | (o.hi[0] << 16);
+          it.y = o.lo[1] | (o.hi[1] << 16);
+          it.z = o.lo[2] | ((o.hi[2] + 1) << 16);
+          it.faces = faces;
+          F->tb_items.push_back(it);
+          F->tb_cells += double(o.hi[0] - o.lo[0] + 1) * (o.hi[1] - o.lo[1] + 1) *
+                         (o.hi[2] - o.lo[2] + 1);
+          F->tb_border += nb;  // an upper bound (edges counted twice)
+        }
+  }
+  // ---- upload, palette-uniform flags, mixed-palette cell counts (traffic model)
+  if (dev_upload(F, &F->d_tb_ritems, F->tb_rcap, F->tb_ritems) ||
+      dev_upload(F, &F->d_tb_rgeo, F->tb_gcap, F->tb_rgeo) ||
+      dev_upload(F, &F->d_tb_items, F->tb_icap, F->tb_items))
+    return -1;
+  const int nr = (int)F->tb_ritems.size(), ni = (int)F->tb_items.size();
+  if (F->d_tb_rflag) (void)hipFree(F->d_tb_rflag);
+  if (F->d_tb_uflag) (void)hipFree(F->d_tb_uflag);
+  F->d_tb_rflag = F->d_tb_uflag = nullptr;
+  F->rim_cells_nu = F->rim_cells;
+  F->tb_cells_nu = F->tb_cells;
+  if (F->d_uidx) {
+    HIPCHK(hipMalloc(&F->d_tb_rflag, std::max(nr, 1) * sizeof(unsigned)));
+    HIPCHK(hipMalloc(&F->d_tb_uflag, std::max(ni, 1) * sizeof(unsigned)));
+    FusedArgs fa = F->fgeo;
+    fa.uidx = F->d_uidx;
+    if (k_tile_items_uniform(fa, F->d_tb_ritems, F->d_tb_rgeo, nr, F->d_tb_rflag, F->stream))
+      return fail("rim palette flags failed");
+    TB2Args t{};
+    t.n = ni, t.items = F->d_tb_items, t.uidx = F->d_uidx;
+    for (int k = 0; k < 3; k++) t.N[k] = g.N[k];
+    t.st1 = g.st[1], t.st2 = g.st[2];
+    if (k_tb2_uniform(t, F->d_tb_uflag, F->stream)) return fail("two-step palette flags failed");
+    std::vector<unsigned> hr(nr), hi(ni);
+    if (nr) HIPCHK(hipMemcpyAsync(hr.data(), F->d_tb_rflag, nr * 4, hipMemcpyDeviceToHost, F->stream));
+    if (ni) HIPCHK(hipMemcpyAsync(hi.data(), F->d_tb_uflag, ni * 4, hipMemcpyDeviceToHost, F->stream));
+    HIPCHK(hipStreamSynchronize(F->stream));
+    F->rim_cells_nu = F->tb_cells_nu = 0;
+    for (int i = 0; i < nr; i++)
+      if (hr[i] == ~0u) {
+        const int *q = &F->tb_rgeo[3 * i];
+        F->rim_cells_nu += double((q[0] >> 16) - (q[0] & 0xFFFF) + 1) *
+                           ((q[1] >> 16) - (q[1] & 0xFFFF) + 1) * ((q[2] >> 16) - (q[2] & 0xFFFF));
+      }
+    for (int i = 0; i < ni; i++)
+      if (hi[i] == ~0u) {
+        const TB2Item &q = F->tb_items[i];
+        F->tb_cells_nu += double((q.x >> 16) - (q.x & 0xFFFF) + 1) *
+                          ((q.y >> 16) - (q.y & 0xFFFF) + 1) * ((q.z >> 16) - (q.z & 0xFFFF));
+      }
+  }
+  HIPCHK(hipStreamSynchronize(F->stream));
+  F->tb_have = ni > 0;
+  if (getenv("MNL_TB_STATS"))
+    fprintf(stderr, "tb: L2 [%d..%d]x[%d..%d]x[%d..%d], %zu holes, %zu two-step boxes, %zu rim "
+            "boxes; %d two-step items (%d planes, %.0f cells, %.0f border), %d rim items "
+            "(%.0f cells, %.0f lean)\n",
+            L2.lo[0], L2.hi[0], L2.lo[1], L2.hi[1], L2.lo[2], L2.hi[2], holes.size(), two.size(),
+            rim.size(), ni, tz, F->tb_cells, F->tb_border, nr, F->rim_cells, F->rim_lean);
+  return 0;
+}
+
+// Can the batch step in pairs?  Builds the plan when needed (-1: HIP error).
+int tb_usable(mnl_fields *F, bool *ok) {
+  *ok = false;
+  if (!F->tb_enabled || !F->fused || !F->tile_mode || F->nranks != 1 || F->fgeo.ngen > 0 ||
+      !F->dfts.empty() || F->S.dim != 3)
+    return 0;
+  if (tb_plan(F)) return -1;
+  *ok = F->tb_have;
+  return 0;
+}
+
+template <class EB, class EE>
+int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end) {
+  DevFields &f = F->f;
+  const DevGrid &g = F->g;
+  if (!F->tb_mid_fresh) {  // the middle set starts as a copy (entries no launch writes)
+    auto fresh = [&](double **pp, double *cur) -> int {
+      if (!cur) return 0;
+      if (!*pp && dev_alloc(F, pp, F->nlocal, false)) return -1;
+      HIPCHK(hipMemcpyAsync(*pp, cur, F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
+      return 0;
+    };
+    for (int d = 0; d < 3; d++)
+      if (fresh(&F->pp3_B[d], f.B[d]) || fresh(&F->pp3_D[d], f.D[d]) ||
+          fresh(&F->pp3_E[d], f.E[d]) || fresh(&F->pp3_H[d], f.H[d]) ||
+          fresh(&F->pp3_UB[d], f.UB[d]))
+        return -1;
+    F->tb_mid_fresh = true;
+  }
+  const FusedArgs &fa = fused_args(F);
+  const int nr = (int)F->tb_ritems.size();
+  const unsigned *rflag = F->d_uidx ? F->d_tb_rflag : nullptr;
+  // R1: rim, state n (cur) -> n+1 (mid)
+  FusedArgs r = fa;
+  for (int d = 0; d < 3; d++) {
+    r.Bn[d] = F->pp3_B[d];
+    r.Dn[d] = F->pp3_D[d];
+    r.En[d] = f.E[d] ? F->pp3_E[d] : nullptr;
+    r.Hn[d] = f.H[d] ? F->pp3_H[d] : nullptr;
+    r.UBn[d] = f.UB[d] ? F->pp3_UB[d] : nullptr;
+  }
+  int k = ev_begin(TM_RIM);
+  int kr = k_tile_items(r, F->d_tb_ritems, F->d_tb_rgeo, rflag, nr, 4, F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("rim kernel launch failed", kr);
+  if (s0.n) {
+    DevFields fm = f;
+    for (int d = 0; d < 3; d++) fm.Dn[d] = F->pp3_D[d];
+    if (k_source(T_D, g, fm, s0, 0, F->stream)) return fail("source launch failed");
+  }
+  // L: two steps over L2, cur -> nxt, border points' step n+1 -> mid
+  TB2Args t{};
+  t.n = (int)F->tb_items.size();
+  t.items = F->d_tb_items;
+  t.uflag = F->d_uidx ? F->d_tb_uflag : nullptr;
+  for (int d = 0; d < 3; d++) {
+    t.Bo[d] = f.B[d], t.Do[d] = f.D[d];
+    t.Bm[d] = F->pp3_B[d], t.Dm[d] = F->pp3_D[d];
+    t.Bn[d] = f.Bn[d], t.Dn[d] = f.Dn[d];
+    t.u[d] = f.inveps[d];
+    t.N[d] = g.N[d];
+  }
+  t.uidx = F->d_uidx;
+  t.utab = F->d_utab;
+  t.st1 = g.st[1], t.st2 = g.st[2];
+  t.nelem = (long long)F->nlocal;
+  t.C = F->S.courant;
+  t.ctr = F->d_fused_ctr;
+  t.ctr_line = 3;
+  k = ev_begin(TM_TB);
+  kr = k_tb2(t, F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("two-step kernel launch failed", kr);
+  // R2: rim, n+1 (mid) -> n+2 (nxt)
+  FusedArgs r2 = fa;
+  for (int d = 0; d < 3; d++) {
+    r2.Bo[d] = F->pp3_B[d];
+    r2.Do[d] = F->pp3_D[d];
+    r2.E[d] = f.E[d] ? F->pp3_E[d] : nullptr;
+    r2.Ho[d] = f.H[d] ? F->pp3_H[d] : nullptr;
+    r2.UBo[d] = f.UB[d] ? F->pp3_UB[d] : nullptr;
+  }
+  k = ev_begin(TM_RIM);
+  kr = k_tile_items(r2, F->d_tb_ritems, F->d_tb_rgeo, rflag, nr, 4, F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("rim kernel launch failed", kr);
+  if (s1.n && k_source(T_D, g, f, s1, 0, F->stream)) return fail("source launch failed");
+  for (int d = 0; d < 3; d++) {
+    std::swap(f.B[d], f.Bn[d]);
+    std::swap(f.D[d], f.Dn[d]);
+    std::swap(f.E[d], f.En[d]);
+    std::swap(f.H[d], f.Hn[d]);
+    std::swap(f.UB[d], f.UBn[d]);
+  }
+  return 0;
+}
+
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
   // in-process A/B of the fused geometry (tools/ab_inproc.py): MNL_TILE_STEP /
@@ -3376,6 +3822,8 @@ int step_batch(mnl_fields *F, int nsteps) {
     }
   }
   if (F->fused && F->nranks > 1 && multi_begin(F)) return -1;
+  bool tb_ok = false;  // step in pairs (temporal blocking)
+  if (nsteps >= 2 && tb_usable(F, &tb_ok)) return -1;
   const double dt = F->dt;
   // per-step source values, computed on the host exactly as the reference
   size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
@@ -3494,6 +3942,12 @@ int step_batch(mnl_fields *F, int nsteps) {
       ISrcDev is = F->isrc_dev;
       is.n = (int)nI;
       is.val = vs + jofs;  // kernels index val[step * n + orig] with step 0
+      if (tb_ok && s + 1 < ns) {  // steps s and s + 1 as one pair (no DFT, one rank)
+        const SrcDev sD1 = src_dev(F, 1, vs + per + 2 * ng);
+        if (tb_pair(F, sD, sD1, ev_begin, ev_end)) return -1;
+        s++;
+        continue;
+      }
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
         continue;
@@ -4868,6 +5322,8 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(0, atoi(zc));
   if (const char *bp = getenv("MNL_FUSED_BPC")) F->fused_bpc = std::max(1, atoi(bp));
   if (const char *tm = getenv("MNL_TILE")) F->tile_mode = atoi(tm) != 0;
+  if (const char *tb = getenv("MNL_TB")) F->tb_enabled = atoi(tb) != 0;
+  if (const char *tz = getenv("MNL_TB_ZCHUNK")) F->tb_zchunk = std::max(0, atoi(tz));
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
@@ -5835,7 +6291,31 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
 
 int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch) {
-  if (!F || which < 0 || which > 4) return fail("bad kernel id");
+  if (!F || which < 0 || which > 6) return fail("bad kernel id");
+  if (which == 5 || which == 6) {
+    // temporal blocking: 5 = the two-step kernel (bytes of its two steps: B, D read once and
+    // written once, the palette word where the item is mixed, the border points' step n+1
+    // B, D), 6 = one rim launch (one step of the tile kernel's model over the rim items)
+    *launches = F->timer_count[which == 5 ? TM_TB : TM_RIM];
+    *total_ms = F->timer_ms[which == 5 ? TM_TB : TM_RIM];
+    *bytes_per_launch = 0;
+    if (!F->fused || !F->tb_have) return 0;
+    int nu = 0;
+    for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
+    const double ub = F->d_uidx ? 4.0 : 8.0 * nu;
+    if (which == 5) {
+      *bytes_per_launch = F->tb_cells * 96.0 + (F->d_uidx ? F->tb_cells_nu : F->tb_cells) * ub +
+                          F->tb_border * 48.0;
+    } else {
+      double lb, gb;
+      fused_bytes(F, &lb, &gb);
+      const bool tuni = F->d_uidx && F->uflag_active && F->tile_cells_nu >= 0;
+      *bytes_per_launch = lb - double(F->tile_cells) * 96.0 -
+                          (tuni ? F->tile_cells_nu : double(F->tile_cells)) * ub +
+                          F->rim_cells * 96.0 + (F->d_uidx ? F->rim_cells_nu : F->rim_cells) * ub;
+    }
+    return 0;
+  }
   if (which == 4) {  // E update (update_eh(E_stuff) incl. chi(2) Newton-Raphson, Lorentzian P)
     *launches = F->timer_count[TM_E];
     *total_ms = F->timer_ms[TM_E];
@@ -5877,6 +6357,28 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
   int nsrc = 0;
   for (int d = 0; d < 3; d++) nsrc += F->allocated[3 * (which == 0 ? T_E : T_H) + d] ? 1 : 0;
   *bytes_per_launch = pts * 8.0 * (nsrc + 2 * ncomp);
+  return 0;
+}
+
+int mnl_fields_set_temporal_blocking(mnl_fields *F, int on) {
+  if (!F) return fail("null fields");
+  F->tb_enabled = on != 0;
+  return 0;
+}
+
+int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
+  if (!F || !out || n < 1) return fail("bad argument");
+  const double v[9] = {F->fused && F->tb_have ? 1.0 : 0.0,
+                       F->tb_cells,
+                       F->tb_border,
+                       F->tb_cells_nu,
+                       F->rim_cells,
+                       F->rim_cells_nu,
+                       double(F->tb_items.size()),
+                       double(F->tb_ritems.size()),
+                       F->tb_items.empty() ? 0.0 : double((F->tb_items[0].z >> 16) -
+                                                          (F->tb_items[0].z & 0xFFFF))};
+  for (int i = 0; i < n && i < 9; i++) out[i] = v[i];
   return 0;
 }
 

@@ -319,7 +319,50 @@ struct FusedArgs {
   const unsigned *tflag;        // per tile item: palette word uniform over its footprint, or ~0u
   unsigned long long cbg[8];    // lean queue g: counter line g's value at launch start
   unsigned long long *ctr;      // FUSED_NCTR work-queue counters (128 B apart); see cbase
+  // explicit own boxes of the tile items (null: tx / ty / ch index xb / yb / zb): per item
+  // x0 | x1 << 16 (columns, x0 128-byte aligned), yfirst | y1 << 16 (own rows), zs | ze << 16
+  const int *tgeo;
 };
+
+// Temporal blocking: two Yee steps per z-march over the region L2
+// (points whose L-infinity distance-2 neighbourhood lies in the lean box and holds no
+// source point).  A workgroup's 64 x 16 lanes (one row per wave) cover own columns x0 ..
+// x0+55 (lanes 4 .. 59) and own rows y0 .. y0+11 (waves 2 .. 13); step n runs on every lane,
+// step n+1 is valid on lanes 2 .. 61 and waves 2 .. 13.
+constexpr int TB_LX = 64, TB_LY = 16, TB_HX = 4, TB_OX = 56, TB_HY = 2, TB_OY = 12;
+constexpr int TB_MAXCH = 512;  // planes per item (any length: the march keeps 3 planes)
+struct TB2Item {
+  int x;      // x0 | x1 << 16 (own columns, inclusive)
+  int y;      // y0 | y1 << 16 (own rows, inclusive)
+  int z;      // zs | ze << 16 (own planes [zs, ze))
+  int faces;  // bits 0..5: own face x-lo, x-hi, y-lo, y-hi, z-lo, z-hi borders the rim (its
+              // points' step n+1 values are stored into the middle buffer set)
+};
+struct TB2Args {
+  int n;                  // items
+  const TB2Item *items;
+  const unsigned *uflag;  // per item: palette word uniform over its footprint, or ~0u (null: none)
+  const double *Bo[3], *Do[3];  // state n (read)
+  double *Bm[3], *Dm[3];        // state n+1 at the border points (write)
+  double *Bn[3], *Dn[3];        // state n+2 at the own points (write)
+  const double *u[3];           // UMODE 1: f64 chi1inv
+  const unsigned *uidx;         // UMODE 2: palette indices
+  const double *utab;           // UMODE 2: palette, 3 x 256
+  int N[3];
+  long long st1, st2, nelem;
+  double C;
+  unsigned long long *ctr;      // work-queue counters (FusedArgs::ctr); line ctr_line
+  int ctr_line;
+  unsigned long long cbase;
+};
+int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases);
+int k_tb2_uniform(const TB2Args &a, unsigned *flags, void *stream);
+// the tile kernel over an explicit item list (FusedArgs::tgeo boxes), counter line `line`
+int k_tile_items(const FusedArgs &a, const int *items, const int *geo, const unsigned *flags,
+                 int n, int line, void *stream, unsigned long long *bases);
+// per item of that list: the palette word uniform over its footprint, or ~0u
+int k_tile_items_uniform(const FusedArgs &a, const int *items, const int *geo, int n,
+                         unsigned *flags, void *stream);
 // which: 0 = lean tiles, 1 = all general tiles, 2 = general tiles of chunk 0
 // only (early launch), 3 = the other general tiles; tile kernel: 4 = all tile items,
 // 5 = tile items of chunk 0 (early launch), 6 = the other tile items.  Every launch reads old /

@@ -3015,7 +3015,7 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
   __shared__ double sE[3][FR + 1][FX + 2];
   __shared__ double sB[3][FR][FX + 1];
   __shared__ PTabL sP;
-  __shared__ int s_item;
+  __shared__ int s_item, s_idx;
   __shared__ unsigned s_uw;
   if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
     for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
@@ -3026,20 +3026,31 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
     if (threadIdx.x == 0) {
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
       s_item = (long long)v < n ? a.titems[a.gbeg + v] : -1;
+      s_idx = (int)v;
       s_uw = ((long long)v < n && UMODE == 2 && a.tflag) ? a.tflag[a.gbeg + v] : ~0u;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
     const unsigned uw = s_uw;
     if (item == -1) break;
-    const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
     ItemGeo itg;
-    itg.x0 = a.xb[tx];
-    itg.x1 = a.xb[tx + 1] - 1;
-    itg.y0 = a.yb[ty] - 1;
-    itg.y1 = a.yb[ty + 1] - 1;
-    itg.zs = a.zb[ch];
-    itg.ze = a.zb[ch + 1];
+    if (a.tgeo) {  // explicit own box (temporal-blocking rim items, TileGeo on the host)
+      const int *gp = a.tgeo + 3 * (a.gbeg + s_idx);
+      itg.x0 = gp[0] & 0xFFFF;
+      itg.x1 = gp[0] >> 16;
+      itg.y0 = (gp[1] & 0xFFFF) - 1;
+      itg.y1 = gp[1] >> 16;
+      itg.zs = gp[2] & 0xFFFF;
+      itg.ze = gp[2] >> 16;
+    } else {
+      const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
+      itg.x0 = a.xb[tx];
+      itg.x1 = a.xb[tx + 1] - 1;
+      itg.y0 = a.yb[ty] - 1;
+      itg.y1 = a.yb[ty + 1] - 1;
+      itg.zs = a.zb[ch];
+      itg.ze = a.zb[ch + 1];
+    }
 #ifndef MNL_TILE_BODIES
 #define MNL_TILE_BODIES 255  // register-budget experiments: compile a subset of the bodies
 #endif
@@ -3302,9 +3313,18 @@ __global__ void tile_uniform_kernel(FusedArgs a, unsigned *flags) {
   const int idx = blockIdx.x;
   const int item = a.titems[idx];
   const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
-  const int x0 = max(a.xb[tx] - 1, a.G.lo[0]), x1 = min(a.xb[tx] + FX, a.G.hi[0]);
-  const int y0 = max(a.yb[ty] - 1, a.G.lo[1]), y1 = min(a.yb[ty] - 1 + FR, a.G.hi[1]);
-  const int z0 = max(a.zb[ch] - 1, a.G.lo[2]), z1 = min(a.zb[ch + 1], a.G.hi[2]);
+  int ix0, iy0, izs, ize;  // tile column start, halo row, planes [izs, ize)
+  if (a.tgeo) {
+    ix0 = a.tgeo[3 * idx] & 0xFFFF;
+    iy0 = (a.tgeo[3 * idx + 1] & 0xFFFF) - 1;
+    izs = a.tgeo[3 * idx + 2] & 0xFFFF;
+    ize = a.tgeo[3 * idx + 2] >> 16;
+  } else {
+    ix0 = a.xb[tx], iy0 = a.yb[ty] - 1, izs = a.zb[ch], ize = a.zb[ch + 1];
+  }
+  const int x0 = max(ix0 - 1, a.G.lo[0]), x1 = min(ix0 + FX, a.G.hi[0]);
+  const int y0 = max(iy0, a.G.lo[1]), y1 = min(iy0 + FR, a.G.hi[1]);
+  const int z0 = max(izs - 1, a.G.lo[2]), z1 = min(ize, a.G.hi[2]);
   __shared__ int bad;
   if (threadIdx.x == 0) bad = 0;
   __syncthreads();
@@ -3461,6 +3481,298 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
   else
     MNL_LAUNCH_FUSED(0);
 #undef MNL_LAUNCH_FUSED
+  return hipPeekAtLastError() == hipSuccess ? 0 : 9;
+}
+
+int k_tile_items(const FusedArgs &a, const int *items, const int *geo, const unsigned *flags,
+                 int n, int line, void *stream, unsigned long long *bases) {
+  if (n <= 0) return 0;
+  if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr || !items || !geo || line < 0 ||
+      line >= FUSED_NCTR)
+    return 2;
+  long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
+  if (nb > n) nb = n;
+  FusedArgs t = a;
+  t.titems = items, t.tgeo = geo, t.tflag = flags;
+  t.gbeg = 0, t.gend = n, t.ctr_line = line, t.cbase = bases[line];
+  bases[line] += (unsigned long long)n + nb;
+  const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grd((unsigned)nb), blk(1024);
+  if (um == 2)
+    fused_tile_kernel<2, 1><<<grd, blk, 0, s>>>(t);
+  else if (um == 1)
+    fused_tile_kernel<1, 1><<<grd, blk, 0, s>>>(t);
+  else
+    fused_tile_kernel<0, 1><<<grd, blk, 0, s>>>(t);
+  return hipPeekAtLastError() == hipSuccess ? 0 : 9;
+}
+
+int k_tile_items_uniform(const FusedArgs &a, const int *items, const int *geo, int n,
+                         unsigned *flags, void *stream) {
+  if (n <= 0 || !a.uidx) return 0;
+  FusedArgs t = a;
+  t.titems = items, t.tgeo = geo, t.ntit = n;
+  tile_uniform_kernel<<<n, 256, 0, (hipStream_t)stream>>>(t, flags);
+  return rc();
+}
+
+// ---------------------------------------------------------------------------
+// Temporal blocking: steps n -> n+1 -> n+2 in one z-march over an
+// item of the region L2, where every point within L-infinity distance 2 of an own point is
+// lean (no PML, every component owned, H == B, E implicit) and no source point lies within
+// distance 1 of an own point.  Per plane k of the march: step n at plane k on all 64 x 16
+// lanes (B^{n+1}(k), then D^{n+1}(k) from B^{n+1}(k-1) kept in registers), then step n+1 at
+// plane k-1 from E^{n+1}(k-1) (registers, LDS for the neighbours) and E^{n+1}(k) (this
+// lane).  Per two steps a point's D and B are read once and written once (plus the step-n+1
+// values of the points on a face that borders the rim, which the one-step rim launch of
+// step n+1 reads).  The arithmetic of each update is the lean body's expression, operand
+// for operand (src/step_generic.cpp:106-113 curl, 888-903 E = chi1inv * D), so two steps
+// here are bitwise two one-step launches.
+template <int UMODE, bool UNI>
+__device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, unsigned uw,
+                                         const double (*sU)[256], double (*sE1)[TB_LY][TB_LX],
+                                         double (*sH1)[TB_LY][TB_LX], double (*sE2)[TB_LY][TB_LX],
+                                         double (*sH2)[TB_LY][TB_LX]) {
+  constexpr bool HAS_U = UMODE != 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
+  const int zs = it.z & 0xFFFF, ze = it.z >> 16;
+  const int faces = it.faces;
+  const int gx = x0 - TB_HX + lane, gy = y0 - TB_HY + w;
+  const int N0 = a.N[0], N1 = a.N[1], zmax = a.N[2] - 1;
+  const int cx = min(max(gx, 0), N0 - 1), cy = min(max(gy, 0), N1 - 1);
+  const unsigned col = (unsigned)((cx + (long long)cy * a.st1) * 8);
+  const unsigned s2 = (unsigned)(a.st2 * 8);
+  const double C = a.C;
+  const bool own = gx >= x0 && gx <= x1 && gy >= y0 && gy <= y1;
+  const bool bxy = own && (((faces & 1) && gx == x0) || ((faces & 2) && gx == x1) ||
+                           ((faces & 4) && gy == y0) || ((faces & 8) && gy == y1));
+  const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
+  // output arrays as scalar pointers; a buffer descriptor is built at each store (a
+  // descriptor per array live across the loop would overflow the SGPRs)
+  const unsigned long long pBn0 = (unsigned long long)sgpr_ptr(a.Bn[0]),
+                           pBn1 = (unsigned long long)sgpr_ptr(a.Bn[1]),
+                           pBn2 = (unsigned long long)sgpr_ptr(a.Bn[2]),
+                           pDn0 = (unsigned long long)sgpr_ptr(a.Dn[0]),
+                           pDn1 = (unsigned long long)sgpr_ptr(a.Dn[1]),
+                           pDn2 = (unsigned long long)sgpr_ptr(a.Dn[2]),
+                           pBm0 = (unsigned long long)sgpr_ptr(a.Bm[0]),
+                           pBm1 = (unsigned long long)sgpr_ptr(a.Bm[1]),
+                           pBm2 = (unsigned long long)sgpr_ptr(a.Bm[2]),
+                           pDm0 = (unsigned long long)sgpr_ptr(a.Dm[0]),
+                           pDm1 = (unsigned long long)sgpr_ptr(a.Dm[1]),
+                           pDm2 = (unsigned long long)sgpr_ptr(a.Dm[2]);
+  const gdp D0 = sgpr_ptr(a.Do[0]), D1 = sgpr_ptr(a.Do[1]), D2 = sgpr_ptr(a.Do[2]);
+  const gdp B0 = sgpr_ptr(a.Bo[0]), B1 = sgpr_ptr(a.Bo[1]), B2 = sgpr_ptr(a.Bo[2]);
+  const gdp U0 = UMODE == 1 ? sgpr_ptr(a.u[0]) : nullptr;
+  const gdp U1 = UMODE == 1 ? sgpr_ptr(a.u[1]) : nullptr;
+  const gdp U2 = UMODE == 1 ? sgpr_ptr(a.u[2]) : nullptr;
+  const gup uix = (gup)sgpr_ptr(a.uidx);
+  // chi1inv of a uniform item
+  double cu0 = 1, cu1 = 1, cu2 = 1;
+  if (UMODE == 2 && UNI) {
+    cu0 = sU[0][uw & 255], cu1 = sU[1][(uw >> 8) & 255], cu2 = sU[2][(uw >> 16) & 255];
+  }
+  struct Q {
+    double d0, d1, d2, b0, b1, b2, u0, u1, u2;
+    unsigned ui;
+  };
+  auto zc = [zmax](int z) { return min(max(z, 0), zmax); };
+  // plane k: D(k+1), chi1inv(k+1), B(k)
+  auto load = [&](int k) -> Q {
+    Q q;
+    const unsigned o1 = col + (unsigned)zc(k + 1) * s2, ob = col + (unsigned)zc(k) * s2;
+    q.d0 = ldg(D0, o1);
+    q.d1 = ldg(D1, o1);
+    q.d2 = ldg(D2, o1);
+    q.ui = 0;
+    q.u0 = q.u1 = q.u2 = 1.0;
+    if (UMODE == 2 && !UNI) q.ui = ldu(uix, o1 >> 1);
+    if (UMODE == 1) {
+      q.u0 = ldg(U0, o1);
+      q.u1 = ldg(U1, o1);
+      q.u2 = ldg(U2, o1);
+    }
+    q.b0 = ldg(B0, ob);
+    q.b1 = ldg(B1, ob);
+    q.b2 = ldg(B2, ob);
+    return q;
+  };
+  auto uval = [&](const Q &q, int c) -> double {
+    if (UMODE == 2) {
+      if (UNI) return c == 0 ? cu0 : (c == 1 ? cu1 : cu2);
+      return sU[c][(q.ui >> (8 * c)) & 255];
+    }
+    return c == 0 ? q.u0 : (c == 1 ? q.u1 : q.u2);
+  };
+  const int k0 = zs - 2;
+  // prologue: D^n(k0), E^n(k0)
+  double dnx, dny, dnz, enx, eny, enz;
+  double uk0, uk1, uk2;  // chi1inv at the march plane k (E^{n+1}(k) = D^{n+1}(k) * u(k))
+  {
+    Q p;
+    const unsigned o = col + (unsigned)zc(k0) * s2;
+    p.d0 = ldg(D0, o), p.d1 = ldg(D1, o), p.d2 = ldg(D2, o);
+    p.ui = (UMODE == 2 && !UNI) ? ldu(uix, o >> 1) : 0u;
+    p.u0 = p.u1 = p.u2 = 1.0;
+    if (UMODE == 1) p.u0 = ldg(U0, o), p.u1 = ldg(U1, o), p.u2 = ldg(U2, o);
+    dnx = p.d0, dny = p.d1, dnz = p.d2;
+    if (HAS_U) {
+      enx = dnx * uval(p, 0), eny = dny * uval(p, 1), enz = dnz * uval(p, 2);
+    } else {
+      enx = dnx, eny = dny, enz = dnz;
+    }
+  }
+  Q q = load(k0);
+  uk0 = uk1 = uk2 = 1.0;
+  double h1x = 0, h1y = 0;                // B^{n+1}(k-1) x, y
+  double b1x = 0, b1y = 0, b1z = 0;       // B^{n+1}(k-1)
+  double d1x = 0, d1y = 0, d1z = 0;       // D^{n+1}(k-1)
+  double f1x = 0, f1y = 0, f1z = 0;       // E^{n+1}(k-1)
+  double h2x = 0, h2y = 0;                // B^{n+2}(k-2) x, y
+  const int lp = min(lane + 1, TB_LX - 1), lm = max(lane - 1, 0);
+  const int wp = min(w + 1, TB_LY - 1), wm = max(w - 1, 0);
+  for (int k = k0; k <= ze; k++) {
+    const Q c = q;
+    q = load(min(k + 1, ze));
+    // E^n(k+1); chi1inv(k+1) becomes u(k) of the next plane
+    double e1x, e1y, e1z, v0 = 1, v1 = 1, v2 = 1;
+    if (HAS_U) {
+      v0 = uval(c, 0), v1 = uval(c, 1), v2 = uval(c, 2);
+      e1x = c.d0 * v0, e1y = c.d1 * v1, e1z = c.d2 * v2;
+    } else {
+      e1x = c.d0, e1y = c.d1, e1z = c.d2;
+    }
+    sE1[0][w][lane] = enx, sE1[1][w][lane] = eny, sE1[2][w][lane] = enz;
+    sE2[0][w][lane] = f1x, sE2[1][w][lane] = f1y, sE2[2][w][lane] = f1z;
+    __syncthreads();
+    // ---- step n at plane k: B^{n+1}(k) (curl E^n), H == B
+    const double Bx = c.b0 - C * (sE1[2][wp][lane] - enz + eny - e1y);
+    const double By = c.b1 - C * (e1x - enx + enz - sE1[2][w][lp]);
+    const double Bz = c.b2 - C * (sE1[1][w][lp] - eny + enx - sE1[0][wp][lane]);
+    sH1[0][w][lane] = Bx, sH1[1][w][lane] = By, sH1[2][w][lane] = Bz;
+    __syncthreads();
+    // D^{n+1}(k) (curl H^{n+1}), E^{n+1}(k) = chi1inv * D^{n+1}(k)
+    const double Dx = dnx - C * (sH1[2][wm][lane] - Bz + By - h1y);
+    const double Dy = dny - C * (h1x - Bx + Bz - sH1[2][w][lm]);
+    const double Dz = dnz - C * (sH1[1][w][lm] - By + Bx - sH1[0][wm][lane]);
+    double Ex = Dx, Ey = Dy, Ez = Dz;
+    if (HAS_U) Ex = Dx * uk0, Ey = Dy * uk1, Ez = Dz * uk2;
+    {  // step-n+1 values of the points on a face bordering the rim (read by rim step n+1)
+      const bool kin = k >= zs && k < ze;
+      const bool bd = kin && (bxy || (own && (((faces & 16) && k == zs) || ((faces & 32) && k == ze - 1))));
+      const unsigned ob = bd ? col + (unsigned)k * s2 : MNL_OOB;
+      bst(brsrc_at(pBm0, nrec), ob, Bx);
+      bst(brsrc_at(pBm1, nrec), ob, By);
+      bst(brsrc_at(pBm2, nrec), ob, Bz);
+      bst(brsrc_at(pDm0, nrec), ob, Dx);
+      bst(brsrc_at(pDm1, nrec), ob, Dy);
+      bst(brsrc_at(pDm2, nrec), ob, Dz);
+    }
+    // ---- step n+1 at plane k-1: B^{n+2}(k-1) from E^{n+1}(k-1) (sE2), E^{n+1}(k) (Ex..)
+    const double Fx = b1x - C * (sE2[2][wp][lane] - f1z + f1y - Ey);
+    const double Fy = b1y - C * (Ex - f1x + f1z - sE2[2][w][lp]);
+    const double Fz = b1z - C * (sE2[1][w][lp] - f1y + f1x - sE2[0][wp][lane]);
+    sH2[0][w][lane] = Fx, sH2[1][w][lane] = Fy, sH2[2][w][lane] = Fz;
+    __syncthreads();
+    const double Gx = d1x - C * (sH2[2][wm][lane] - Fz + Fy - h2y);
+    const double Gy = d1y - C * (h2x - Fx + Fz - sH2[2][w][lm]);
+    const double Gz = d1z - C * (sH2[1][w][lm] - Fy + Fx - sH2[0][wm][lane]);
+    {
+      const bool st = own && k - 1 >= zs && k - 1 < ze;
+      const unsigned os = st ? col + (unsigned)(k - 1) * s2 : MNL_OOB;
+      bst(brsrc_at(pBn0, nrec), os, Fx);
+      bst(brsrc_at(pBn1, nrec), os, Fy);
+      bst(brsrc_at(pBn2, nrec), os, Fz);
+      bst(brsrc_at(pDn0, nrec), os, Gx);
+      bst(brsrc_at(pDn1, nrec), os, Gy);
+      bst(brsrc_at(pDn2, nrec), os, Gz);
+    }
+    h2x = Fx, h2y = Fy;
+    h1x = Bx, h1y = By;
+    b1x = Bx, b1y = By, b1z = Bz;
+    d1x = Dx, d1y = Dy, d1z = Dz;
+    f1x = Ex, f1y = Ey, f1z = Ez;
+    enx = e1x, eny = e1y, enz = e1z;
+    dnx = c.d0, dny = c.d1, dnz = c.d2;
+    uk0 = v0, uk1 = v1, uk2 = v2;
+  }
+}
+
+template <int UMODE>
+__global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
+  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
+  __shared__ double sE1[3][TB_LY][TB_LX], sH1[3][TB_LY][TB_LX];
+  __shared__ double sE2[3][TB_LY][TB_LX], sH2[3][TB_LY][TB_LX];
+  __shared__ int s_idx;
+  if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
+    for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
+  }
+  unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
+      s_idx = (long long)v < a.n ? (int)v : -1;
+    }
+    __syncthreads();  // also separates LDS use of consecutive items
+    const int idx = s_idx;
+    if (idx < 0) break;
+    const TB2Item it = a.items[idx];
+    const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[idx] : ~0u;
+    if (UMODE == 2 && __builtin_amdgcn_readfirstlane(uw) != ~0u)
+      tb2_body<UMODE, true>(a, it, uw, sU, sE1, sH1, sE2, sH2);
+    else
+      tb2_body<UMODE, false>(a, it, uw, sU, sE1, sH1, sE2, sH2);
+  }
+}
+
+// Per TB item: the palette word if every cell within distance 2 of its own box (the cells
+// whose chi1inv the two steps use) has the same word, else ~0u.
+__global__ void tb2_uniform_kernel(TB2Args a, unsigned *flags) {
+  const int idx = blockIdx.x;
+  const TB2Item it = a.items[idx];
+  const int x0 = max((it.x & 0xFFFF) - 2, 0), x1 = min((it.x >> 16) + 2, a.N[0] - 1);
+  const int y0 = max((it.y & 0xFFFF) - 2, 0), y1 = min((it.y >> 16) + 2, a.N[1] - 1);
+  const int z0 = max((it.z & 0xFFFF) - 2, 0), z1 = min((it.z >> 16) + 1, a.N[2] - 1);
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const long long nx = x1 - x0 + 1, ny = y1 - y0 + 1, nz = z1 - z0 + 1;
+  const unsigned ref = a.uidx[x0 + (long long)y0 * a.st1 + (long long)z0 * a.st2];
+  for (long long i = threadIdx.x; i < nx * ny * nz; i += blockDim.x) {
+    const long long x = x0 + i % nx, y = y0 + (i / nx) % ny, z = z0 + i / (nx * ny);
+    if (a.uidx[x + y * a.st1 + z * a.st2] != ref) bad = 1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) flags[idx] = bad ? ~0u : ref;
+}
+
+int k_tb2_uniform(const TB2Args &a, unsigned *flags, void *stream) {
+  if (a.n <= 0 || !a.uidx) return 0;
+  tb2_uniform_kernel<<<a.n, 256, 0, (hipStream_t)stream>>>(a, flags);
+  return rc();
+}
+
+int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
+  if (a.n <= 0) return 0;
+  if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr || !a.items || a.ctr_line < 0 ||
+      a.ctr_line >= FUSED_NCTR)
+    return 2;
+  long long nb = fused_grid_blocks(1);
+  if (nb > a.n) nb = a.n;
+  TB2Args t = a;
+  t.cbase = bases[a.ctr_line];
+  bases[a.ctr_line] += (unsigned long long)a.n + nb;
+  const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grd((unsigned)nb), blk(1024);
+  if (um == 2)
+    tb2_kernel<2><<<grd, blk, 0, s>>>(t);
+  else if (um == 1)
+    tb2_kernel<1><<<grd, blk, 0, s>>>(t);
+  else
+    tb2_kernel<0><<<grd, blk, 0, s>>>(t);
   return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 

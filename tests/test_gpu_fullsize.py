@@ -51,7 +51,7 @@ def test_c4_256_random():
 
 
 def test_c3_512_random():
-    kw = dict(sizes=(51.2, 51.2, 51.2), steps=2, eps=12.0)
+    kw = dict(sizes=(51.2, 51.2, 51.2), steps=3, eps=12.0)  # steps 2-3: one pair
     p = sc_random_fields(ProductSim, **kw)
     assert p._fields().fused_active()
     o = sc_random_fields(make_oracle, **kw)

@@ -1,0 +1,116 @@
+"""Temporal blocking: pairs of fields::step() (src/step.cpp:35-140)
+as rim (one-step tile kernel) + L2 (two-step kernel) + rim must be bit for bit the
+one-step path and the CPU oracle.
+
+Grids are large enough for a non-empty L2 (the lean box shrunk by 2, x aligned) and carry
+seeded random D / B everywhere (initialize_field), so every two-step item, rim item, hole
+around a source point and border face holds data from the first step."""
+import os
+
+import numpy as np
+import pytest
+
+from scenarios import ALL_COMPS, ProductSim, make_oracle, random_init, vol
+
+pytestmark = pytest.mark.gpu
+
+E_COMPS = (0, 1, 2)
+SRCS = ((0.37, -0.21, 0.05), (-3.3, 1.6, 2.15), (2.1, 0.3, -2.9), (0.4, -0.2, 0.1))
+
+
+def sc_tb(make, sizes=(9.6, 6.4, 8.0), dpml=0.7, eps=6.0, random_eps=False, srcs=SRCS,
+          steps=(1, 10), tb=True, rand=True, profile=False):
+    """Dielectric slab across the PML boundary, Gaussian currents inside L2 (holes), near
+    its edge and inside the PML; random initial fields; stepped in the given calls."""
+    o = vol(make, 3, list(sizes), 10, center_origin=True)
+    o.add_pml(dpml)
+    if eps:
+        for c in E_COMPS:
+            x, y, z = o.coords(c)
+            inside = (np.abs(y) < 0.8) & (z > -0.4) & (z < 3.0)
+            if random_eps:
+                val = 1.0 / np.random.default_rng(99 + c).uniform(1.0, 12.0, size=x.shape)
+            else:
+                val = 1.0 / eps
+            o.set_chi1inv(c, c, np.where(inside, val, 1.0))
+    for i, p in enumerate(srcs):
+        o.add_gaussian_source(i % 3, 0.25, 4.0, 0.0, 40.0, p, 1.0 - 0.1 * i)
+    if rand:
+        random_init(o, (6, 7, 8, 9, 10, 11))
+    if isinstance(o, ProductSim):
+        o._fields().set_temporal_blocking(tb)
+        if profile:
+            o._fields().set_profiling(True)
+    for n in steps:
+        o.step(n)
+    return o
+
+
+def _same(a, b):
+    bad = {}
+    for c in ALL_COMPS:
+        x, y = a.get_array(c), b.get_array(c)
+        d = float(np.max(np.abs(x - y))) if x.size else 0.0
+        if d != 0.0 or not np.array_equal(np.isnan(x), np.isnan(y)):
+            bad[c] = d
+    assert not bad, f"max|diff| per component: {bad}"
+
+
+def test_tb_active_and_bitwise_vs_oracle():
+    p = sc_tb(ProductSim, profile=True)
+    f = p._fields()
+    info = f.tb_info()
+    assert f.fused_active() and info["active"], info
+    assert info["tb_items"] > 0 and info["rim_items"] > 0
+    assert f.kernel_stats(5)[0] >= 4  # the two-step kernel ran (one launch per pair)
+    _same(p, sc_tb(make_oracle))
+
+
+def test_tb_equals_one_step_path():
+    """Odd calls, one-step calls between pairs: identical to stepping one step at a time."""
+    steps = (1, 7, 1, 4, 2, 3)
+    _same(sc_tb(ProductSim, steps=steps), sc_tb(ProductSim, steps=steps, tb=False))
+
+
+def test_tb_vacuum_no_chi1inv():
+    kw = dict(eps=None, steps=(1, 9))
+    _same(sc_tb(ProductSim, **kw), sc_tb(make_oracle, **kw))
+
+
+def test_tb_f64_chi1inv():
+    """More than 256 distinct chi1inv values: no palette, f64 chi1inv in the two-step kernel."""
+    kw = dict(random_eps=True, steps=(1, 8))
+    _same(sc_tb(ProductSim, **kw), sc_tb(make_oracle, **kw))
+
+
+@pytest.mark.parametrize("zc", [1, 5, 200])
+def test_tb_chunk_lengths(zc):
+    """Two-step items of 1 plane (three halo planes per own plane), 5 and longer than L2."""
+    os.environ["MNL_TB_ZCHUNK"] = str(zc)
+    try:
+        p = sc_tb(ProductSim, steps=(1, 6))
+    finally:
+        del os.environ["MNL_TB_ZCHUNK"]
+    assert p._fields().tb_info()["active"]
+    _same(p, sc_tb(make_oracle, steps=(1, 6)))
+
+
+def test_tb_sources_on_hole_edges():
+    """Source points on and next to L2's faces and corners, two in one hole, one in the
+    x-alignment margin: the holes and the rim faces of the items around them."""
+    srcs = ((-3.45, -1.75, -2.55), (-3.35, -1.65, -2.45), (3.05, 2.35, 2.95), (0.0, 0.0, 0.0),
+            (0.05, 0.0, 0.0), (-3.85, 0.0, 0.0), (0.0, 2.55, 0.0))
+    kw = dict(srcs=srcs, steps=(1, 11))
+    _same(sc_tb(ProductSim, **kw), sc_tb(make_oracle, **kw))
+
+
+def test_tb_no_source():
+    kw = dict(srcs=(), steps=(1, 6))
+    _same(sc_tb(ProductSim, **kw), sc_tb(make_oracle, **kw))
+
+
+def test_tb_too_small_for_l2():
+    """A grid whose lean box leaves no two-step region steps one step at a time."""
+    p = sc_tb(ProductSim, sizes=(3.2, 3.2, 3.2), srcs=((0.05, 0.05, 0.05),), steps=(1, 4))
+    assert not p._fields().tb_info()["active"]
+    _same(p, sc_tb(make_oracle, sizes=(3.2, 3.2, 3.2), srcs=((0.05, 0.05, 0.05),), steps=(1, 4)))
