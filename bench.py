@@ -151,6 +151,37 @@ def roofline(f, kind=0):
                        if f.fused_active() else "curl_kernel<B, interior> (step_db(B_stuff))"),
             "bytes_per_launch": k_bytes, "avg_launch_ms": round(avg_ms, 4),
             "launches": n_launch}
+    tb = f.tb_info() if f.fused_active() else {"active": False}
+    t_n, t_ms, t_bytes = f.kernel_stats(5)
+    if tb["active"] and t_n:
+        # temporal blocking: a pair of steps is two persistent launches
+        # of tb_phase_kernel (rim items one step each + two-step items over L2); the
+        # algorithmic bytes of a pair are the two-step items' two steps (B, D read once and
+        # written once, palette words of mixed items, border points' step n+1) plus two rim
+        # steps.  frac_one_step_model prices the same pair at the one-step model (two steps of
+        # the tile kernel's bytes), i.e. the HBM rate a one-step kernel would need.
+        t_avg = t_ms / t_n
+        achieved = t_bytes / (t_avg * 1e-3) / 1e9
+        r_n, r_ms, r_bytes = f.kernel_stats(6)
+        roof.update({
+            "kernel": "tb_phase_kernel x2 per pair of steps (two-step z-march over the lean "
+                      "region L2 + one-step tile bodies over the PML / wall / ring / source-hole "
+                      "rim, interleaved in one persistent queue)",
+            "bytes_per_launch": t_bytes, "avg_launch_ms": round(t_avg, 4), "launches": t_n,
+            "launch_unit": "pair of steps (two phase launches)",
+            "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "steps_per_launch": 2,
+            "frac_one_step_model": round(2.0 * k_bytes / (t_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "temporal_blocking": tb})
+        if r_n:
+            r_avg = r_ms / r_n
+            roof["rim_alone"] = {
+                "kernel": "fused_tile_kernel over the rim items alone (the last pair's second "
+                          "rim step of a batch), included in the pair time above",
+                "bytes_per_launch": r_bytes, "avg_launch_ms": round(r_avg, 4), "launches": r_n}
+        if n_launch:  # one-step launches of the same run (odd leftovers)
+            roof["tile_kernel_one_step"] = {"bytes_per_launch": k_bytes, "launches": n_launch,
+                                            "avg_launch_ms": round(avg_ms, 4)}
     if f.fused_active():  # the PML / boundary tiles run in the second fused kernel
         g_n, g_ms, g_bytes = f.kernel_stats(2)
         if g_n:

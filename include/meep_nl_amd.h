@@ -354,9 +354,9 @@ int mnl_fields_set_profiling(mnl_fields *f, int on);
  * which = 3: the DFT updates of one step (all flux objects);
  * which = 4: the E update (update_eh(E_stuff): chi(2) Newton-Raphson,
  *            Lorentzian P), unfused mode; bytes 0 (not HBM-bound);
- * which = 5: the two-step (temporal-blocking) kernel, one launch per pair of
- *            steps; bytes of its two steps;
- * which = 6: the rim launches of those pairs (two per pair), one step each. */
+ * which = 5: temporal blocking: launches = pairs of
+ *            steps, total_ms = every launch of the pairs, bytes per pair;
+ * which = 6: rim launches that run alone (one step each). */
 int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch);
 /* Temporal blocking (no reference counterpart: how this build steps pairs of

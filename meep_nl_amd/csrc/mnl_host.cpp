@@ -329,6 +329,15 @@ struct mnl_fields {
   unsigned *d_tb_rflag = nullptr, *d_tb_uflag = nullptr;
   TB2Item *d_tb_items = nullptr;
   size_t tb_rcap = 0, tb_gcap = 0, tb_icap = 0;
+  // queue orders of the two phases (k_tb_phase): A = rim step n+1 of the previous pair +
+  // inner two-step items, I = inner items only (first pair of a batch), B = rim step n +
+  // outer two-step items (those whose distance-2 footprint meets the rim)
+  std::vector<int> tb_order[3];
+  int *d_tb_order[3] = {nullptr, nullptr, nullptr};
+  size_t tb_ocap[3] = {0, 0, 0};
+  bool tb_split = false;  // MNL_TB_SPLIT=1: rim / two-step / rim as three launches (diagnostics)
+  bool tb_pending = false;  // the last pair's rim step n+1 has not run yet (tb_drain)
+  SrcDev tb_pend_src{};     // ... and the source currents applied after it
   double *pp3_B[3] = {nullptr, nullptr, nullptr}, *pp3_D[3] = {nullptr, nullptr, nullptr};
   double *pp3_E[3] = {nullptr, nullptr, nullptr}, *pp3_H[3] = {nullptr, nullptr, nullptr};
   double *pp3_UB[3] = {nullptr, nullptr, nullptr};
@@ -390,7 +399,8 @@ struct mnl_fields {
     if (d_uflag) hipFree(d_uflag);
     if (d_gflag) hipFree(d_gflag);
     for (void *p : {(void *)d_tb_ritems, (void *)d_tb_rgeo, (void *)d_tb_rflag, (void *)d_tb_uflag,
-                    (void *)d_tb_items})
+                    (void *)d_tb_items, (void *)d_tb_order[0], (void *)d_tb_order[1],
+                    (void *)d_tb_order[2]})
       if (p) hipFree(p);
     comm.reset();
     for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
@@ -3554,10 +3564,13 @@ int tb_plan(mnl_fields *F) {
   };
   longest_first(heavy);
   longest_first(lean);
+  std::vector<double> rcost;  // estimated time of a rim item: planes (+ the halo plane), PML
+                              // bodies about twice a lean plane
   for (auto *v : {&heavy, &lean})
     for (const RI &it : *v) {
       F->tb_ritems.push_back(it.code);
       F->tb_rgeo.push_back(it.g0), F->tb_rgeo.push_back(it.g1), F->tb_rgeo.push_back(it.g2);
+      rcost.push_back((it.planes + 1) * (((it.code >> 24) & 7) ? 2.0 : 1.0));
     }
   // ---- two-step items: 56 x 12 own points, z chunks of tz planes (automatic: the length
   // whose item count fills whole rounds of one workgroup per CU best, with the three
@@ -3583,6 +3596,7 @@ int tb_plan(mnl_fields *F) {
     }
   }
   F->tb_cells = F->tb_border = 0;
+  std::vector<int> t_inner, t_outer;
   for (const Box &b : two) {
     const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + TB_OY - 1) / TB_OY;
     const int nz = b.hi[2] - b.lo[2] + 1, nch = (nz + tz - 1) / tz;
@@ -3615,6 +3629,12 @@ int tb_plan(mnl_fields *F) {
               nb += fc;
             }
           }
+          // outer: the distance-2 footprint meets the rim (reads rim values of step n)
+          Box fp = o;
+          for (int k = 0; k < 3; k++) fp.lo[k] -= 2, fp.hi[k] += 2;
+          bool outer = false;
+          for (const Box &r : rim) outer = outer || box_meets(fp, r);
+          (outer ? t_outer : t_inner).push_back((int)F->tb_items.size());
           TB2Item it;
           it.x = o.lo[0] | (o.hi[0] << 16);
           it.y = o.lo[1] | (o.hi[1] << 16);
@@ -3626,6 +3646,36 @@ int tb_plan(mnl_fields *F) {
           F->tb_border += nb;  // an upper bound (edges counted twice)
         }
   }
+  // ---- phase orders: the two kinds interleaved so that both advance in proportion to their
+  // estimated work (a two-step item: two steps of a plane per plane, plus three halo planes)
+  auto tcost = [&](int i) {
+    const TB2Item &q = F->tb_items[i];
+    return ((q.z >> 16) - (q.z & 0xFFFF) + 3) * 2.2;
+  };
+  auto interleave = [&](const std::vector<int> &tl, bool with_rim) {
+    std::vector<int> o;
+    double rt = 0, tt = 0, ra = 0, ta = 0;
+    if (with_rim)
+      for (double c : rcost) rt += c;
+    for (int i : tl) tt += tcost(i);
+    size_t i = 0, j = 0;
+    const size_t nr = with_rim ? rcost.size() : 0;
+    while (i < nr || j < tl.size()) {
+      if (j >= tl.size() || (i < nr && ra / rt <= ta / tt)) {
+        o.push_back((int)i);
+        ra += rcost[i++];
+      } else {
+        o.push_back(~tl[j]);
+        ta += tcost(tl[j++]);
+      }
+    }
+    return o;
+  };
+  F->tb_order[0] = interleave(t_inner, true);
+  F->tb_order[1] = interleave(t_inner, false);
+  F->tb_order[2] = interleave(t_outer, true);
+  for (int k = 0; k < 3; k++)
+    if (dev_upload(F, &F->d_tb_order[k], F->tb_ocap[k], F->tb_order[k])) return -1;
   // ---- upload, palette-uniform flags, mixed-palette cell counts (traffic model)
   if (dev_upload(F, &F->d_tb_ritems, F->tb_rcap, F->tb_ritems) ||
       dev_upload(F, &F->d_tb_rgeo, F->tb_gcap, F->tb_rgeo) ||
@@ -3640,8 +3690,7 @@ int tb_plan(mnl_fields *F) {
   if (F->d_uidx) {
     HIPCHK(hipMalloc(&F->d_tb_rflag, std::max(nr, 1) * sizeof(unsigned)));
     HIPCHK(hipMalloc(&F->d_tb_uflag, std::max(ni, 1) * sizeof(unsigned)));
-    FusedArgs fa = F->fgeo;
-    fa.uidx = F->d_uidx;
+    FusedArgs fa = fused_args(F);  // strides / palette of the current arrays
     if (k_tile_items_uniform(fa, F->d_tb_ritems, F->d_tb_rgeo, nr, F->d_tb_rflag, F->stream))
       return fail("rim palette flags failed");
     TB2Args t{};
@@ -3672,9 +3721,10 @@ int tb_plan(mnl_fields *F) {
   if (getenv("MNL_TB_STATS"))
     fprintf(stderr, "tb: L2 [%d..%d]x[%d..%d]x[%d..%d], %zu holes, %zu two-step boxes, %zu rim "
             "boxes; %d two-step items (%d planes, %.0f cells, %.0f border), %d rim items "
-            "(%.0f cells, %.0f lean)\n",
+            "(%.0f cells, %.0f lean); inner %zu, outer %zu\n",
             L2.lo[0], L2.hi[0], L2.lo[1], L2.hi[1], L2.lo[2], L2.hi[2], holes.size(), two.size(),
-            rim.size(), ni, tz, F->tb_cells, F->tb_border, nr, F->rim_cells, F->rim_lean);
+            rim.size(), ni, tz, F->tb_cells, F->tb_border, nr, F->rim_cells, F->rim_lean,
+            t_inner.size(), t_outer.size());
   return 0;
 }
 
@@ -3689,55 +3739,58 @@ int tb_usable(mnl_fields *F, bool *ok) {
   return 0;
 }
 
-template <class EB, class EE>
-int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end) {
-  DevFields &f = F->f;
-  const DevGrid &g = F->g;
-  if (!F->tb_mid_fresh) {  // the middle set starts as a copy (entries no launch writes)
-    auto fresh = [&](double **pp, double *cur) -> int {
-      if (!cur) return 0;
-      if (!*pp && dev_alloc(F, pp, F->nlocal, false)) return -1;
-      HIPCHK(hipMemcpyAsync(*pp, cur, F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
-      return 0;
-    };
-    for (int d = 0; d < 3; d++)
-      if (fresh(&F->pp3_B[d], f.B[d]) || fresh(&F->pp3_D[d], f.D[d]) ||
-          fresh(&F->pp3_E[d], f.E[d]) || fresh(&F->pp3_H[d], f.H[d]) ||
-          fresh(&F->pp3_UB[d], f.UB[d]))
-        return -1;
-    F->tb_mid_fresh = true;
-  }
-  const FusedArgs &fa = fused_args(F);
-  const int nr = (int)F->tb_ritems.size();
-  const unsigned *rflag = F->d_uidx ? F->d_tb_rflag : nullptr;
-  // R1: rim, state n (cur) -> n+1 (mid)
+// one buffer set of the fused step's per-point state (B, D, stored E, separate H, f_u of B)
+struct Set5 {
+  double *B[3], *D[3], *E[3], *H[3], *UB[3];
+};
+Set5 set_cur(mnl_fields *F) {
+  Set5 s;
+  for (int d = 0; d < 3; d++)
+    s.B[d] = F->f.B[d], s.D[d] = F->f.D[d], s.E[d] = F->f.E[d], s.H[d] = F->f.H[d],
+    s.UB[d] = F->f.UB[d];
+  return s;
+}
+Set5 set_nxt(mnl_fields *F) {
+  Set5 s;
+  for (int d = 0; d < 3; d++)
+    s.B[d] = F->f.Bn[d], s.D[d] = F->f.Dn[d], s.E[d] = F->f.E[d] ? F->f.En[d] : nullptr,
+    s.H[d] = F->f.H[d] ? F->f.Hn[d] : nullptr, s.UB[d] = F->f.UB[d] ? F->f.UBn[d] : nullptr;
+  return s;
+}
+Set5 set_mid(mnl_fields *F) {
+  Set5 s;
+  for (int d = 0; d < 3; d++)
+    s.B[d] = F->pp3_B[d], s.D[d] = F->pp3_D[d], s.E[d] = F->f.E[d] ? F->pp3_E[d] : nullptr,
+    s.H[d] = F->f.H[d] ? F->pp3_H[d] : nullptr, s.UB[d] = F->f.UB[d] ? F->pp3_UB[d] : nullptr;
+  return s;
+}
+
+// tile-kernel arguments of a rim launch: one step from set `o` to set `n`, the rim item list
+FusedArgs rim_args(mnl_fields *F, const FusedArgs &fa, const Set5 &o, const Set5 &n) {
   FusedArgs r = fa;
   for (int d = 0; d < 3; d++) {
-    r.Bn[d] = F->pp3_B[d];
-    r.Dn[d] = F->pp3_D[d];
-    r.En[d] = f.E[d] ? F->pp3_E[d] : nullptr;
-    r.Hn[d] = f.H[d] ? F->pp3_H[d] : nullptr;
-    r.UBn[d] = f.UB[d] ? F->pp3_UB[d] : nullptr;
+    r.Bo[d] = o.B[d], r.Do[d] = o.D[d], r.E[d] = o.E[d], r.Ho[d] = o.H[d], r.UBo[d] = o.UB[d];
+    r.Bn[d] = n.B[d], r.Dn[d] = n.D[d], r.En[d] = n.E[d], r.Hn[d] = n.H[d], r.UBn[d] = n.UB[d];
   }
-  int k = ev_begin(TM_RIM);
-  int kr = k_tile_items(r, F->d_tb_ritems, F->d_tb_rgeo, rflag, nr, 4, F->stream, F->ctr_base);
-  ev_end(k);
-  if (kr) return fused_fail("rim kernel launch failed", kr);
-  if (s0.n) {
-    DevFields fm = f;
-    for (int d = 0; d < 3; d++) fm.Dn[d] = F->pp3_D[d];
-    if (k_source(T_D, g, fm, s0, 0, F->stream)) return fail("source launch failed");
-  }
-  // L: two steps over L2, cur -> nxt, border points' step n+1 -> mid
+  r.titems = F->d_tb_ritems;
+  r.tgeo = F->d_tb_rgeo;
+  r.tflag = F->d_uidx ? F->d_tb_rflag : nullptr;
+  r.gbeg = 0, r.gend = (int)F->tb_ritems.size();
+  return r;
+}
+
+// two-step arguments: state n in `o`, border step n+1 into `m`, step n+2 into `n`
+TB2Args tb_args(mnl_fields *F, const Set5 &o, const Set5 &m, const Set5 &n) {
+  const DevGrid &g = F->g;
   TB2Args t{};
   t.n = (int)F->tb_items.size();
   t.items = F->d_tb_items;
   t.uflag = F->d_uidx ? F->d_tb_uflag : nullptr;
   for (int d = 0; d < 3; d++) {
-    t.Bo[d] = f.B[d], t.Do[d] = f.D[d];
-    t.Bm[d] = F->pp3_B[d], t.Dm[d] = F->pp3_D[d];
-    t.Bn[d] = f.Bn[d], t.Dn[d] = f.Dn[d];
-    t.u[d] = f.inveps[d];
+    t.Bo[d] = o.B[d], t.Do[d] = o.D[d];
+    t.Bm[d] = m.B[d], t.Dm[d] = m.D[d];
+    t.Bn[d] = n.B[d], t.Dn[d] = n.D[d];
+    t.u[d] = F->f.inveps[d];
     t.N[d] = g.N[d];
   }
   t.uidx = F->d_uidx;
@@ -3747,24 +3800,36 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   t.C = F->S.courant;
   t.ctr = F->d_fused_ctr;
   t.ctr_line = 3;
-  k = ev_begin(TM_TB);
-  kr = k_tb2(t, F->stream, F->ctr_base);
-  ev_end(k);
-  if (kr) return fused_fail("two-step kernel launch failed", kr);
-  // R2: rim, n+1 (mid) -> n+2 (nxt)
-  FusedArgs r2 = fa;
-  for (int d = 0; d < 3; d++) {
-    r2.Bo[d] = F->pp3_B[d];
-    r2.Do[d] = F->pp3_D[d];
-    r2.E[d] = f.E[d] ? F->pp3_E[d] : nullptr;
-    r2.Ho[d] = f.H[d] ? F->pp3_H[d] : nullptr;
-    r2.UBo[d] = f.UB[d] ? F->pp3_UB[d] : nullptr;
-  }
-  k = ev_begin(TM_RIM);
-  kr = k_tile_items(r2, F->d_tb_ritems, F->d_tb_rgeo, rflag, nr, 4, F->stream, F->ctr_base);
-  ev_end(k);
-  if (kr) return fused_fail("rim kernel launch failed", kr);
-  if (s1.n && k_source(T_D, g, f, s1, 0, F->stream)) return fail("source launch failed");
+  return t;
+}
+
+int tb_src(mnl_fields *F, const SrcDev &s, double *const D[3]) {
+  if (!s.n) return 0;
+  DevFields fm = F->f;
+  for (int d = 0; d < 3; d++) fm.Dn[d] = D[d];
+  if (k_source(T_D, F->g, fm, s, 0, F->stream)) return fail("source launch failed");
+  return 0;
+}
+
+// the middle set starts as a copy of the state (entries no launch writes: walls, ghosts)
+int tb_mid_init(mnl_fields *F) {
+  if (F->tb_mid_fresh) return 0;
+  DevFields &f = F->f;
+  auto fresh = [&](double **pp, double *cur) -> int {
+    if (!cur) return 0;
+    if (!*pp && dev_alloc(F, pp, F->nlocal, false)) return -1;
+    HIPCHK(hipMemcpyAsync(*pp, cur, F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
+    return 0;
+  };
+  for (int d = 0; d < 3; d++)
+    if (fresh(&F->pp3_B[d], f.B[d]) || fresh(&F->pp3_D[d], f.D[d]) || fresh(&F->pp3_E[d], f.E[d]) ||
+        fresh(&F->pp3_H[d], f.H[d]) || fresh(&F->pp3_UB[d], f.UB[d]))
+      return -1;
+  F->tb_mid_fresh = true;
+  return 0;
+}
+
+void swap_cur_nxt(DevFields &f) {
   for (int d = 0; d < 3; d++) {
     std::swap(f.B[d], f.Bn[d]);
     std::swap(f.D[d], f.Dn[d]);
@@ -3772,6 +3837,74 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
     std::swap(f.H[d], f.Hn[d]);
     std::swap(f.UB[d], f.UBn[d]);
   }
+}
+
+// The rim's step n+1 of the last pair (pending until the next pair's phase A): alone.
+template <class EB, class EE>
+int tb_drain(mnl_fields *F, EB &ev_begin, EE &ev_end) {
+  if (!F->tb_pending) return 0;
+  F->tb_pending = false;
+  const FusedArgs &fa = fused_args(F);
+  const Set5 cur = set_cur(F), mid = set_mid(F);
+  FusedArgs r = rim_args(F, fa, mid, cur);
+  const int k = ev_begin(TM_RIM);
+  const int kr = k_tile_items(r, F->d_tb_ritems, F->d_tb_rgeo, r.tflag, (int)F->tb_ritems.size(), 4,
+                              F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("rim kernel launch failed", kr);
+  return tb_src(F, F->tb_pend_src, cur.D);
+}
+
+// Steps n, n+1 (sources s0, s1).  Pipelined (default): phase A = the previous pair's rim step
+// (mid -> cur) beside the inner two-step items (cur -> nxt); phase B = this pair's rim step n
+// (cur -> mid) beside the outer two-step items (cur -> nxt, border -> mid); the rim's step
+// n+1 stays pending for the next phase A or tb_drain.  Every launch reads and writes disjoint
+// points of its sets (DESIGN.md section 24 has the hazard argument).
+template <class EB, class EE>
+int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end) {
+  if (tb_mid_init(F)) return -1;
+  const FusedArgs &fa = fused_args(F);
+  const Set5 cur = set_cur(F), mid = set_mid(F), nxt = set_nxt(F);
+  const TB2Args t = tb_args(F, cur, mid, nxt);
+  const int nr = (int)F->tb_ritems.size();
+  int k, kr;
+  if (F->tb_split) {  // diagnostics: R1, two-step kernel, R2 as three launches
+    const FusedArgs r1 = rim_args(F, fa, cur, mid), r2 = rim_args(F, fa, mid, nxt);
+    k = ev_begin(TM_RIM);
+    kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
+    ev_end(k);
+    if (kr) return fused_fail("rim kernel launch failed", kr);
+    if (tb_src(F, s0, mid.D)) return -1;
+    k = ev_begin(TM_TB);
+    kr = k_tb2(t, F->stream, F->ctr_base);
+    ev_end(k);
+    if (kr) return fused_fail("two-step kernel launch failed", kr);
+    k = ev_begin(TM_RIM);
+    kr = k_tile_items(r2, r2.titems, r2.tgeo, r2.tflag, nr, 4, F->stream, F->ctr_base);
+    ev_end(k);
+    if (kr) return fused_fail("rim kernel launch failed", kr);
+    if (tb_src(F, s1, nxt.D)) return -1;
+    swap_cur_nxt(F->f);
+    return 0;
+  }
+  // phase A
+  const FusedArgs ra = rim_args(F, fa, mid, cur);
+  const int oa = F->tb_pending ? 0 : 1;
+  k = ev_begin(TM_TB);
+  kr = k_tb_phase(ra, t, F->d_tb_order[oa], (int)F->tb_order[oa].size(), F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("temporal-blocking phase launch failed", kr);
+  if (F->tb_pending && tb_src(F, F->tb_pend_src, cur.D)) return -1;
+  // phase B
+  const FusedArgs rb = rim_args(F, fa, cur, mid);
+  k = ev_begin(TM_TB);
+  kr = k_tb_phase(rb, t, F->d_tb_order[2], (int)F->tb_order[2].size(), F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("temporal-blocking phase launch failed", kr);
+  if (tb_src(F, s0, mid.D)) return -1;
+  swap_cur_nxt(F->f);
+  F->tb_pending = true;
+  F->tb_pend_src = s1;
   return 0;
 }
 
@@ -3948,6 +4081,7 @@ int step_batch(mnl_fields *F, int nsteps) {
         s++;
         continue;
       }
+      if (tb_drain(F, ev_begin, ev_end)) return -1;
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
         continue;
@@ -4109,6 +4243,7 @@ int step_batch(mnl_fields *F, int nsteps) {
         }
       if (post_step(s)) return -1;
     }
+    if (tb_drain(F, ev_begin, ev_end)) return -1;  // sources of this batch's table
     if (!F->dfts.empty()) {
       const int k = ev_begin(TM_DFTF);
       for (auto &o : F->dfts)
@@ -5324,6 +5459,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tm = getenv("MNL_TILE")) F->tile_mode = atoi(tm) != 0;
   if (const char *tb = getenv("MNL_TB")) F->tb_enabled = atoi(tb) != 0;
   if (const char *tz = getenv("MNL_TB_ZCHUNK")) F->tb_zchunk = std::max(0, atoi(tz));
+  if (const char *ts = getenv("MNL_TB_SPLIT")) F->tb_split = atoi(ts) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;
@@ -5945,12 +6081,25 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
   for (int k = 0; k < 16; k++) tms[k] = F->timer_ms[k], tcnt[k] = F->timer_count[k];
   F->profiling = true;
   const bool verbose = getenv("MNL_TUNE_VERBOSE") != nullptr;
-  auto timed = [&](double *tile_ms, double *gen_ms) -> int {  // one warm-up, `reps` timed
-    if (fields_step(F, 1)) return -1;
-    const double b0 = F->timer_ms[TM_BINT], g0 = F->timer_ms[TM_GEN];
-    if (fields_step(F, reps)) return -1;
-    *tile_ms = (F->timer_ms[TM_BINT] - b0) / reps;
-    *gen_ms = (F->timer_ms[TM_GEN] - g0) / reps;
+  // per-step time of the fused launches: tile kernel (+ the pairs' phase and rim launches of
+  // temporal blocking) and the polarization chunks' general kernel
+  auto fused_ms = [&]() {
+    return F->timer_ms[TM_BINT] + F->timer_ms[TM_TB] + F->timer_ms[TM_RIM];
+  };
+  auto timed = [&](double *tile_ms, double *gen_ms) -> int {  // two warm-up steps (a pair
+    if (fields_step(F, 2)) return -1;                           // builds its plan), then an
+    const int r = reps + (reps & 1);                            // even number timed
+    const double b0 = fused_ms(), g0 = F->timer_ms[TM_GEN];
+    if (fields_step(F, r)) return -1;
+    *tile_ms = (fused_ms() - b0) / r;
+    *gen_ms = (F->timer_ms[TM_GEN] - g0) / r;
+    if (F->nranks > 1) {  // every rank keeps the same knobs: the slowest rank's times
+      std::vector<double> v(2 * (size_t)F->nranks, 0.0);
+      v[2 * F->rank] = *tile_ms, v[2 * F->rank + 1] = *gen_ms;
+      if (F->comm->allreduce_sum(v.data(), (int)v.size(), F->stream)) return fail("tune allreduce failed");
+      for (int q = 0; q < F->nranks; q++)
+        *tile_ms = std::max(*tile_ms, v[2 * q]), *gen_ms = std::max(*gen_ms, v[2 * q + 1]);
+    }
     return 0;
   };
   int rc = 0;
@@ -5965,7 +6114,7 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
       F->fused_zchunk = c;
       double tm, gm;
       if (timed(&tm, &gm)) { rc = -1; break; }
-      if (!F->fused) break;
+      if (!F->fused) continue;  // this length does not fit the fused kernels; longer ones may
       if (verbose)
         fprintf(stderr, "tune rank %d: zchunk %d: %.4f ms/step (tile %.4f, general %.4f)\n",
                 F->rank, c, tm + gm, tm, gm);
@@ -6004,6 +6153,22 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
     } else {
       F->tile_gen_cus = split0;
     }
+  }
+  // temporal blocking: planes per two-step item (automatic = the item count that fills whole
+  // rounds of one workgroup per CU best)
+  if (!rc && F->fused && F->tb_have && F->tb_enabled && !getenv("MNL_TB_ZCHUNK")) {
+    const int tz0 = F->tb_zchunk;
+    int best = tz0;
+    double best_ms = 0;
+    for (int c : {0, 32, 48, 64, 96, 128}) {
+      F->tb_zchunk = c;
+      double tm, gm;
+      if (timed(&tm, &gm)) { rc = -1; break; }
+      if (verbose)
+        fprintf(stderr, "tune rank %d: two-step planes %d: %.4f ms/step\n", F->rank, c, tm + gm);
+      if (best_ms == 0 || tm + gm < best_ms) best_ms = tm + gm, best = c;
+    }
+    F->tb_zchunk = rc ? tz0 : best;
   }
   F->profiling = prof;
   for (int k = 0; k < 16; k++) F->timer_ms[k] = tms[k], F->timer_count[k] = tcnt[k];
@@ -6293,26 +6458,33 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
                             double *bytes_per_launch) {
   if (!F || which < 0 || which > 6) return fail("bad kernel id");
   if (which == 5 || which == 6) {
-    // temporal blocking: 5 = the two-step kernel (bytes of its two steps: B, D read once and
-    // written once, the palette word where the item is mixed, the border points' step n+1
-    // B, D), 6 = one rim launch (one step of the tile kernel's model over the rim items)
-    *launches = F->timer_count[which == 5 ? TM_TB : TM_RIM];
-    *total_ms = F->timer_ms[which == 5 ? TM_TB : TM_RIM];
-    *bytes_per_launch = 0;
-    if (!F->fused || !F->tb_have) return 0;
+    // temporal blocking.  5 = whole pairs of steps: launches = pairs, time = every launch of
+    // the pairs (two phase launches each, the drains of the rim's last step), bytes per pair =
+    // the two-step items' two steps (B, D read once and written once, the palette word where
+    // the item is mixed, the border points' step n+1 B, D) + two rim steps.  6 = the rim
+    // launches that run alone (drains; every rim step with MNL_TB_SPLIT), one step each
     int nu = 0;
     for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
     const double ub = F->d_uidx ? 4.0 : 8.0 * nu;
-    if (which == 5) {
-      *bytes_per_launch = F->tb_cells * 96.0 + (F->d_uidx ? F->tb_cells_nu : F->tb_cells) * ub +
-                          F->tb_border * 48.0;
-    } else {
+    double tb_b = 0, rim_b = 0;
+    if (F->fused && F->tb_have) {
+      tb_b = F->tb_cells * 96.0 + (F->d_uidx ? F->tb_cells_nu : F->tb_cells) * ub +
+             F->tb_border * 48.0;
       double lb, gb;
       fused_bytes(F, &lb, &gb);
       const bool tuni = F->d_uidx && F->uflag_active && F->tile_cells_nu >= 0;
-      *bytes_per_launch = lb - double(F->tile_cells) * 96.0 -
-                          (tuni ? F->tile_cells_nu : double(F->tile_cells)) * ub +
-                          F->rim_cells * 96.0 + (F->d_uidx ? F->rim_cells_nu : F->rim_cells) * ub;
+      rim_b = lb - double(F->tile_cells) * 96.0 -
+              (tuni ? F->tile_cells_nu : double(F->tile_cells)) * ub + F->rim_cells * 96.0 +
+              (F->d_uidx ? F->rim_cells_nu : F->rim_cells) * ub;
+    }
+    if (which == 5) {
+      *launches = F->timer_count[TM_TB] / (F->tb_split ? 1 : 2);
+      *total_ms = F->timer_ms[TM_TB] + F->timer_ms[TM_RIM];
+      *bytes_per_launch = tb_b + 2.0 * rim_b;
+    } else {
+      *launches = F->timer_count[TM_RIM];
+      *total_ms = F->timer_ms[TM_RIM];
+      *bytes_per_launch = rim_b;
     }
     return 0;
   }

@@ -356,6 +356,11 @@ struct TB2Args {
   unsigned long long cbase;
 };
 int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases);
+// one phase of a pair: rim items (tile kernel, pointer set of a; a.titems / tgeo / tflag
+// index the rim list) and two-step items (t) from one queue: order[v] >= 0 rim item, < 0
+// two-step item ~order[v]; counter line t.ctr_line
+int k_tb_phase(const FusedArgs &a, const TB2Args &t, const int *order, int n, void *stream,
+               unsigned long long *bases);
 int k_tb2_uniform(const TB2Args &a, unsigned *flags, void *stream);
 // the tile kernel over an explicit item list (FusedArgs::tgeo boxes), counter line `line`
 int k_tile_items(const FusedArgs &a, const int *items, const int *geo, const unsigned *flags,

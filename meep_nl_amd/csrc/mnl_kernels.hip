@@ -2283,7 +2283,7 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
 // the lean box L: no PML, every component owned, H == B, E implicit.  1024 threads:
 // waves 0..FR-1 hold one row each (row 0 = the y-1 halo row, B recomputed), wave FR the
 // x-1 column (B recomputed), the E of the x+64 column and a corner.
-template <int UMODE, int DIST, int VAR = 0>
+template <int UMODE, int DIST>
 __device__ __forceinline__ void lean_body(const FusedArgs &a, const ItemGeo &itg, unsigned uw,
                                           const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
                                           double (*sB)[FR][FX + 1]) {
@@ -2291,7 +2291,7 @@ __device__ __forceinline__ void lean_body(const FusedArgs &a, const ItemGeo &itg
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform
   const bool hwave = wu >= FR - 1;
-  constexpr bool SKIPB = MNL_SKIP_B && !(VAR & 2);
+  constexpr bool SKIPB = MNL_SKIP_B;
   const int flo0 = a.L.lo[0], flo1 = a.L.lo[1], flo2 = a.L.lo[2];
   const int fhi0 = a.L.hi[0], fhi1 = a.L.hi[1], fhi2 = a.L.hi[2];
   const unsigned s2 = (unsigned)(a.st2 * 8);  // byte stride of one z plane
@@ -2584,7 +2584,7 @@ __device__ __forceinline__ unsigned own_bits_of(int v, int sl, int sh, int ul, i
 // host): the y / z ownership terms are the constant 3, so every ownership test and the
 // E-load source of a lane are fixed along the march (no per-plane recomputation), and the
 // z index needs no clamp
-template <int UMODE, int DIST, int AX, bool OWNC, int VAR = 0>
+template <int UMODE, int DIST, int AX, bool OWNC>
 __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, unsigned uw,
                                          const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
                                          double (*sB)[FR][FX + 1], PTabL &P) {
@@ -2593,8 +2593,8 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform
   const bool hwave = wu >= FR - 1;
-  constexpr bool SKIPB = MNL_SKIP_B && !(VAR & 2);
-  constexpr bool RSAT = MNL_RS_AT && !(VAR & 1);
+  constexpr bool SKIPB = MNL_SKIP_B;
+  constexpr bool RSAT = MNL_RS_AT;
   const int x0 = it.x0, y0 = it.y0, zs = it.zs, ze = it.ze;
   const int zlo = zs - 1;  // z table position 0
   // ---- PML tables of the footprint -> LDS (x: x0-1 .. x0+64, y: y0 .. y0+FR,
@@ -3004,13 +3004,78 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
 #undef Wz
 
 // body codes of tile items (bits 24-26): 0 lean, 1..7 pml_body<AX = 1, 2, 4, 0, 7, 3, 5>
-// (y-z edges, AX = 6, are few: they take the AX = 7 body)
-// VAR (A/B builds with MNL_TILE_AB only; 0 in production): bit 0 = descriptors built once
-// (MNL_RS_AT off), bit 1 = unused B loads kept (MNL_SKIP_B off), bit 2 = multi-axis bodies
-// with prefetch distance 1
-template <int UMODE, int DIST, int VAR = 0>
+// (y-z edges, AX = 6, are few: they take the AX = 7 body); bit 29: OWNC
+template <int UMODE, int DIST>
+__device__ __forceinline__ void tile_item_body(const FusedArgs &a, int item, const ItemGeo &itg,
+                                               unsigned uw, const double (*sU)[256],
+                                               double (*sE)[FR + 1][FX + 2],
+                                               double (*sB)[FR][FX + 1], PTabL &sP) {
+  constexpr int MD = MNL_MULTI_DIST;
+  const bool ownc = MNL_OWNC && ((item >> 29) & 1);
+  switch ((item >> 24) & 7) {
+    case 0:
+      lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
+      break;
+    case 1:
+      if (ownc)
+        pml_body<UMODE, DIST, 1, true>(a, itg, uw, sU, sE, sB, sP);
+      else
+        pml_body<UMODE, DIST, 1, false>(a, itg, uw, sU, sE, sB, sP);
+      break;
+    case 2:
+      if (ownc)
+        pml_body<UMODE, DIST, 2, true>(a, itg, uw, sU, sE, sB, sP);
+      else
+        pml_body<UMODE, DIST, 2, false>(a, itg, uw, sU, sE, sB, sP);
+      break;
+    case 3:
+      if (ownc)
+        pml_body<UMODE, DIST, 4, true>(a, itg, uw, sU, sE, sB, sP);
+      else
+        pml_body<UMODE, DIST, 4, false>(a, itg, uw, sU, sE, sB, sP);
+      break;
+    case 4:
+      pml_body<UMODE, DIST, 0, false>(a, itg, uw, sU, sE, sB, sP);
+      break;
+    case 5:
+      pml_body<UMODE, MD, 7, false>(a, itg, uw, sU, sE, sB, sP);
+      break;
+    case 6:
+      pml_body<UMODE, MD, 3, false>(a, itg, uw, sU, sE, sB, sP);
+      break;
+    default:
+      pml_body<UMODE, MD, 5, false>(a, itg, uw, sU, sE, sB, sP);
+      break;
+  }
+}
+
+// own box of tile item `idx`: explicit (FusedArgs::tgeo) or tile / chunk indices
+__device__ __forceinline__ ItemGeo tile_item_geo(const FusedArgs &a, int item, int idx) {
+  ItemGeo itg;
+  if (a.tgeo) {
+    const int *gp = a.tgeo + 3 * idx;
+    itg.x0 = gp[0] & 0xFFFF;
+    itg.x1 = gp[0] >> 16;
+    itg.y0 = (gp[1] & 0xFFFF) - 1;
+    itg.y1 = gp[1] >> 16;
+    itg.zs = gp[2] & 0xFFFF;
+    itg.ze = gp[2] >> 16;
+  } else {
+    const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
+    itg.x0 = a.xb[tx];
+    itg.x1 = a.xb[tx + 1] - 1;
+    itg.y0 = a.yb[ty] - 1;
+    itg.y1 = a.yb[ty + 1] - 1;
+    itg.zs = a.zb[ch];
+    itg.ze = a.zb[ch + 1];
+  }
+  itg.lmx = itg.lmy = false;
+  itg.uw = ~0u;
+  return itg;
+}
+
+template <int UMODE, int DIST>
 __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
-  constexpr int MD = (VAR & 4) ? 1 : MNL_MULTI_DIST;
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
   __shared__ double sE[3][FR + 1][FX + 2];
   __shared__ double sB[3][FR][FX + 1];
@@ -3026,76 +3091,14 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
     if (threadIdx.x == 0) {
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
       s_item = (long long)v < n ? a.titems[a.gbeg + v] : -1;
-      s_idx = (int)v;
+      s_idx = a.gbeg + (int)v;
       s_uw = ((long long)v < n && UMODE == 2 && a.tflag) ? a.tflag[a.gbeg + v] : ~0u;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
-    const unsigned uw = s_uw;
     if (item == -1) break;
-    ItemGeo itg;
-    if (a.tgeo) {  // explicit own box (temporal-blocking rim items, TileGeo on the host)
-      const int *gp = a.tgeo + 3 * (a.gbeg + s_idx);
-      itg.x0 = gp[0] & 0xFFFF;
-      itg.x1 = gp[0] >> 16;
-      itg.y0 = (gp[1] & 0xFFFF) - 1;
-      itg.y1 = gp[1] >> 16;
-      itg.zs = gp[2] & 0xFFFF;
-      itg.ze = gp[2] >> 16;
-    } else {
-      const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
-      itg.x0 = a.xb[tx];
-      itg.x1 = a.xb[tx + 1] - 1;
-      itg.y0 = a.yb[ty] - 1;
-      itg.y1 = a.yb[ty + 1] - 1;
-      itg.zs = a.zb[ch];
-      itg.ze = a.zb[ch + 1];
-    }
-#ifndef MNL_TILE_BODIES
-#define MNL_TILE_BODIES 255  // register-budget experiments: compile a subset of the bodies
-#endif
-    const bool ownc = MNL_OWNC && ((item >> 29) & 1);  // OWNC bodies (pml_body)
-    switch ((item >> 24) & 7) {
-      case 0:
-        if (MNL_TILE_BODIES & 1) lean_body<UMODE, DIST, VAR>(a, itg, uw, sU, sE, sB);
-        break;
-      case 1:
-        if (MNL_TILE_BODIES & 2) {
-          if (ownc)
-            pml_body<UMODE, DIST, 1, true, VAR>(a, itg, uw, sU, sE, sB, sP);
-          else
-            pml_body<UMODE, DIST, 1, false, VAR>(a, itg, uw, sU, sE, sB, sP);
-        }
-        break;
-      case 2:
-        if (MNL_TILE_BODIES & 4) {
-          if (ownc)
-            pml_body<UMODE, DIST, 2, true, VAR>(a, itg, uw, sU, sE, sB, sP);
-          else
-            pml_body<UMODE, DIST, 2, false, VAR>(a, itg, uw, sU, sE, sB, sP);
-        }
-        break;
-      case 3:
-        if (MNL_TILE_BODIES & 8) {
-          if (ownc)
-            pml_body<UMODE, DIST, 4, true, VAR>(a, itg, uw, sU, sE, sB, sP);
-          else
-            pml_body<UMODE, DIST, 4, false, VAR>(a, itg, uw, sU, sE, sB, sP);
-        }
-        break;
-      case 4:
-        if (MNL_TILE_BODIES & 16) pml_body<UMODE, DIST, 0, false, VAR>(a, itg, uw, sU, sE, sB, sP);
-        break;
-      case 5:
-        if (MNL_TILE_BODIES & 32) pml_body<UMODE, MD, 7, false, VAR>(a, itg, uw, sU, sE, sB, sP);
-        break;
-      case 6:
-        if (MNL_TILE_BODIES & 64) pml_body<UMODE, MD, 3, false, VAR>(a, itg, uw, sU, sE, sB, sP);
-        break;
-      default:
-        if (MNL_TILE_BODIES & 128) pml_body<UMODE, MD, 5, false, VAR>(a, itg, uw, sU, sE, sB, sP);
-        break;
-    }  }
+    tile_item_body<UMODE, DIST>(a, item, tile_item_geo(a, item, s_idx), s_uw, sU, sE, sB, sP);
+  }
 }
 
 // Lean tiles only (the original two-launch fused step: this kernel, then
@@ -3374,23 +3377,6 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
     const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
     hipStream_t s = (hipStream_t)stream;
     const dim3 grd((unsigned)nb), blk(1024);
-#ifdef MNL_TILE_AB
-    const char *ve = getenv("MNL_TILE_VAR");
-    const int var = ve ? atoi(ve) : 0;
-    if (var == 1 && um != 1) {
-      if (um == 2) fused_tile_kernel<2, 1, 1><<<grd, blk, 0, s>>>(t);
-      else fused_tile_kernel<0, 1, 1><<<grd, blk, 0, s>>>(t);
-    } else if (var == 2 && um != 1) {
-      if (um == 2) fused_tile_kernel<2, 1, 2><<<grd, blk, 0, s>>>(t);
-      else fused_tile_kernel<0, 1, 2><<<grd, blk, 0, s>>>(t);
-    } else if (var == 4 && um != 1) {
-      if (um == 2) fused_tile_kernel<2, 1, 4><<<grd, blk, 0, s>>>(t);
-      else fused_tile_kernel<0, 1, 4><<<grd, blk, 0, s>>>(t);
-    } else if (var == 7 && um != 1) {
-      if (um == 2) fused_tile_kernel<2, 1, 7><<<grd, blk, 0, s>>>(t);
-      else fused_tile_kernel<0, 1, 7><<<grd, blk, 0, s>>>(t);
-    } else
-#endif
     if (um == 2)
       fused_tile_kernel<2, 1><<<grd, blk, 0, s>>>(t);
     else if (um == 1)
@@ -3725,6 +3711,82 @@ __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
     else
       tb2_body<UMODE, false>(a, it, uw, sU, sE1, sH1, sE2, sH2);
   }
+}
+
+// One phase of a temporal-blocking pair: rim items of the tile kernel
+// (one step, the pointer set of `a`) and two-step items (`t`) from one queue.  order[v] >= 0
+// is a rim item (index into a.titems / a.tgeo / a.tflag), < 0 the two-step item ~order[v];
+// the host interleaves the two kinds so latency-bound rim items run beside
+// bandwidth-bound two-step items.  The LDS of the two body families is one union.
+constexpr int TILE_LDS_D = 3 * (FR + 1) * (FX + 2) + 3 * FR * (FX + 1) + (int)(sizeof(PTabL) + 7) / 8;
+constexpr int TB_LDS_D = 4 * 3 * TB_LY * TB_LX;
+template <int UMODE>
+__global__ __launch_bounds__(1024) void tb_phase_kernel(FusedArgs a, TB2Args t, const int *order,
+                                                        int n) {
+  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
+  __shared__ double sm[TILE_LDS_D > TB_LDS_D ? TILE_LDS_D : TB_LDS_D];
+  __shared__ int s_e, s_item;
+  __shared__ unsigned s_uw;
+  if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
+    for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
+  }
+  double(*sE)[FR + 1][FX + 2] = reinterpret_cast<double(*)[FR + 1][FX + 2]>(sm);
+  double(*sB)[FR][FX + 1] = reinterpret_cast<double(*)[FR][FX + 1]>(sm + 3 * (FR + 1) * (FX + 2));
+  PTabL &sP = *reinterpret_cast<PTabL *>(sm + 3 * (FR + 1) * (FX + 2) + 3 * FR * (FX + 1));
+  constexpr int TBA = 3 * TB_LY * TB_LX;
+  double(*sE1)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm);
+  double(*sH1)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm + TBA);
+  double(*sE2)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm + 2 * TBA);
+  double(*sH2)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm + 3 * TBA);
+  unsigned long long *ctr = t.ctr + 16 * t.ctr_line;
+  constexpr int DONE = -2147483647 - 1;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = atomicAdd(ctr, 1ULL) - t.cbase;
+      const int e = (long long)v < n ? order[v] : DONE;
+      s_e = e;
+      s_item = e >= 0 ? a.titems[e] : 0;
+      unsigned uw = ~0u;
+      if (UMODE == 2 && e >= 0 && a.tflag) uw = a.tflag[e];
+      if (UMODE == 2 && e < 0 && e != DONE && t.uflag) uw = t.uflag[~e];
+      s_uw = uw;
+    }
+    __syncthreads();  // also separates LDS use of consecutive items
+    const int e = s_e;
+    if (e == DONE) break;
+    const unsigned uw = s_uw;
+    if (e >= 0) {
+      const int item = s_item;
+      tile_item_body<UMODE, 1>(a, item, tile_item_geo(a, item, e), uw, sU, sE, sB, sP);
+    } else if (UMODE == 2 && __builtin_amdgcn_readfirstlane(uw) != ~0u) {
+      tb2_body<UMODE, true>(t, t.items[~e], uw, sU, sE1, sH1, sE2, sH2);
+    } else {
+      tb2_body<UMODE, false>(t, t.items[~e], uw, sU, sE1, sH1, sE2, sH2);
+    }
+  }
+}
+
+int k_tb_phase(const FusedArgs &a, const TB2Args &t, const int *order, int n, void *stream,
+               unsigned long long *bases) {
+  if (n <= 0) return 0;
+  if (a.nelem * 8 >= (long long)MNL_OOB || t.nelem * 8 >= (long long)MNL_OOB || !t.ctr ||
+      !order || !a.titems || !a.tgeo || t.ctr_line < 0 || t.ctr_line >= FUSED_NCTR)
+    return 2;
+  long long nb = fused_grid_blocks(1);
+  if (nb > n) nb = n;
+  TB2Args tt = t;
+  tt.cbase = bases[t.ctr_line];
+  bases[t.ctr_line] += (unsigned long long)n + nb;
+  const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grd((unsigned)nb), blk(1024);
+  if (um == 2)
+    tb_phase_kernel<2><<<grd, blk, 0, s>>>(a, tt, order, n);
+  else if (um == 1)
+    tb_phase_kernel<1><<<grd, blk, 0, s>>>(a, tt, order, n);
+  else
+    tb_phase_kernel<0><<<grd, blk, 0, s>>>(a, tt, order, n);
+  return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 
 // Per TB item: the palette word if every cell within distance 2 of its own box (the cells

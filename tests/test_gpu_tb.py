@@ -47,13 +47,17 @@ def sc_tb(make, sizes=(9.6, 6.4, 8.0), dpml=0.7, eps=6.0, random_eps=False, srcs
 
 
 def _same(a, b):
+    """Bitwise equality of all twelve components; on failure, per component the largest
+    difference, the number of differing points and their index bounding box."""
     bad = {}
     for c in ALL_COMPS:
         x, y = a.get_array(c), b.get_array(c)
-        d = float(np.max(np.abs(x - y))) if x.size else 0.0
-        if d != 0.0 or not np.array_equal(np.isnan(x), np.isnan(y)):
-            bad[c] = d
-    assert not bad, f"max|diff| per component: {bad}"
+        neq = (x != y) & ~(np.isnan(x) & np.isnan(y))
+        if neq.any():
+            idx = np.argwhere(neq)
+            bad[c] = (float(np.nanmax(np.abs(x - y))), int(neq.sum()),
+                      idx.min(axis=0).tolist(), idx.max(axis=0).tolist())
+    assert not bad, f"component: (max|diff|, points, index lo, index hi): {bad}"
 
 
 def test_tb_active_and_bitwise_vs_oracle():
@@ -114,3 +118,21 @@ def test_tb_too_small_for_l2():
     p = sc_tb(ProductSim, sizes=(3.2, 3.2, 3.2), srcs=((0.05, 0.05, 0.05),), steps=(1, 4))
     assert not p._fields().tb_info()["active"]
     _same(p, sc_tb(make_oracle, sizes=(3.2, 3.2, 3.2), srcs=((0.05, 0.05, 0.05),), steps=(1, 4)))
+
+
+def test_tb_split_launches():
+    """MNL_TB_SPLIT=1 (rim, two-step kernel, rim as three launches per pair: the diagnostic
+    path) gives the same fields as the pipelined phases."""
+    os.environ["MNL_TB_SPLIT"] = "1"
+    try:
+        p = sc_tb(ProductSim, steps=(1, 9, 1, 4))
+    finally:
+        del os.environ["MNL_TB_SPLIT"]
+    _same(p, sc_tb(ProductSim, steps=(1, 9, 1, 4)))
+
+
+def test_tb_long_batch_pipelined():
+    """Many pairs in one batch (every phase A carries the previous pair's rim step), an odd
+    step at the end (drain, then one step), a NaN-guard batch boundary inside."""
+    kw = dict(steps=(1, 125))
+    _same(sc_tb(ProductSim, **kw), sc_tb(make_oracle, **kw))
