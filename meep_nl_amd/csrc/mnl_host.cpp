@@ -335,7 +335,9 @@ struct mnl_fields {
   std::vector<int> tb_order[3];
   int *d_tb_order[3] = {nullptr, nullptr, nullptr};
   size_t tb_ocap[3] = {0, 0, 0};
-  bool tb_split = false;  // MNL_TB_SPLIT=1: rim / two-step / rim as three launches (diagnostics)
+  // rim / two-step / rim as three launches per pair (default: measured faster than the
+  // pipelined phases, whose merged kernel spills registers; MNL_TB_SPLIT=0 selects those)
+  bool tb_split = true;
   bool tb_pending = false;  // the last pair's rim step n+1 has not run yet (tb_drain)
   SrcDev tb_pend_src{};     // ... and the source currents applied after it
   double *pp3_B[3] = {nullptr, nullptr, nullptr}, *pp3_D[3] = {nullptr, nullptr, nullptr};
@@ -344,8 +346,12 @@ struct mnl_fields {
   double tb_cells = 0, tb_border = 0, tb_cells_nu = 0;  // own / border points of the items,
                                                         // own points of the mixed-palette ones
   double rim_cells = 0, rim_lean = 0, rim_cells_nu = 0;  // rim items: own / lean / mixed cells
-  int nan_every = 100;              // NaN guard cadence (src/step.cpp:138-139)
+  int nan_every = 1;                // NaN guard cadence (src/step.cpp:138-139: every step)
   int since_nan = 0;                // steps since the last NaN guard (across calls)
+  bool nan_due = false;             // a guard is due once the state is complete (pending rim)
+  int nan_launched = 0;             // guards launched in this batch (flag read at its end)
+  NanTerms nan_terms{};             // this batch's interpolation terms (nan_terms_build)
+  int *d_nanflag = nullptr;         // [flag, step]
   CurlPlan planB, planD;
   bool nr = false;
   bool upnl = false;  // upstream chi2/chi3 update active (nl_mode 1 with nonzero chi)
@@ -414,6 +420,10 @@ struct mnl_fields {
 namespace {
 
 bool in_fused_box(const mnl_fields *F, int c, const int jg[3]);
+int nan_launch(mnl_fields *F);
+void nan_count(mnl_fields *F, int k);
+int nan_result(mnl_fields *F);
+int nan_terms_build(mnl_fields *F);
 
 // Field-sized arrays start at staggered offsets (a multiple of 128 B, different
 // for every array) so that the many streams one fused step reads and writes at
@@ -3852,7 +3862,8 @@ int tb_drain(mnl_fields *F, EB &ev_begin, EE &ev_end) {
                               F->stream, F->ctr_base);
   ev_end(k);
   if (kr) return fused_fail("rim kernel launch failed", kr);
-  return tb_src(F, F->tb_pend_src, cur.D);
+  if (tb_src(F, F->tb_pend_src, cur.D)) return -1;
+  return nan_launch(F);  // the state of the last pair is complete now
 }
 
 // Steps n, n+1 (sources s0, s1).  Pipelined (default): phase A = the previous pair's rim step
@@ -3885,7 +3896,8 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
     if (kr) return fused_fail("rim kernel launch failed", kr);
     if (tb_src(F, s1, nxt.D)) return -1;
     swap_cur_nxt(F->f);
-    return 0;
+    nan_count(F, 2);
+    return nan_launch(F);
   }
   // phase A
   const FusedArgs ra = rim_args(F, fa, mid, cur);
@@ -3895,6 +3907,7 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   ev_end(k);
   if (kr) return fused_fail("temporal-blocking phase launch failed", kr);
   if (F->tb_pending && tb_src(F, F->tb_pend_src, cur.D)) return -1;
+  if (F->tb_pending && nan_launch(F)) return -1;  // the previous pair's state is complete
   // phase B
   const FusedArgs rb = rim_args(F, fa, cur, mid);
   k = ev_begin(TM_TB);
@@ -3905,6 +3918,7 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   swap_cur_nxt(F->f);
   F->tb_pending = true;
   F->tb_pend_src = s1;
+  nan_count(F, 2);  // a due guard runs once the pending rim step has (next phase A / drain)
   return 0;
 }
 
@@ -3957,6 +3971,7 @@ int step_batch(mnl_fields *F, int nsteps) {
   if (F->fused && F->nranks > 1 && multi_begin(F)) return -1;
   bool tb_ok = false;  // step in pairs (temporal blocking)
   if (nsteps >= 2 && tb_usable(F, &tb_ok)) return -1;
+  if (nan_terms_build(F)) return -1;  // NaN guard terms of this batch's mode / arrays
   const double dt = F->dt;
   // per-step source values, computed on the host exactly as the reference
   size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
@@ -4084,6 +4099,8 @@ int step_batch(mnl_fields *F, int nsteps) {
       if (tb_drain(F, ev_begin, ev_end)) return -1;
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
+        nan_count(F, 1);
+        if (nan_launch(F)) return -1;
         continue;
       }
       // ---- B: halo of E (low ghost), curl, sources
@@ -4242,6 +4259,8 @@ int step_batch(mnl_fields *F, int nsteps) {
           std::swap(f.UB[d], f.UBn[d]);
         }
       if (post_step(s)) return -1;
+      nan_count(F, 1);
+      if (nan_launch(F)) return -1;
     }
     if (tb_drain(F, ev_begin, ev_end)) return -1;  // sources of this batch's table
     if (!F->dfts.empty()) {
@@ -4259,27 +4278,90 @@ int step_batch(mnl_fields *F, int nsteps) {
   }
   HIPCHK(hipStreamSynchronize(F->stream));
   HIPCHK(hipGetLastError());
-  return 0;
+  return nan_result(F);
 }
 
-int nan_check(mnl_fields *F) {
-  // fields::step: abort if get_field(D_EnergyDensity, center) is not finite
-  // (src/step.cpp:138-139, src/monitor.cpp:96-113)
+// NaN guard (src/step.cpp:138-139): abort when get_field(D_EnergyDensity, gv.center()) is
+// not finite (src/monitor.cpp:96-113: 1/2 sum_d real(conj(E_d) D_d), each value interpolated
+// as get_field does, src/monitor.cpp:127-160).  The terms (this rank's points of the 8-point
+// stencils, which array, weight) are built once per batch on the host; nan_check_kernel sums
+// them on the device after the step, and the host reads the flag once, at the end of the
+// batch (no round trip per step).  Multi-rank: each rank checks its share and the ranks agree.
+int nan_terms_build(mnl_fields *F) {
   const mnl_structure &S = F->S;
+  NanTerms &t = F->nan_terms;
+  t.n = 0;
   double cen[3] = {0, 0, 0};
   for (int d = 0; d < 3; d++)
     if (S.has[d]) {
       int n = S.n[d] - (S.n[d] & 1);
       cen[d] = (S.io[d] + n) * (0.5 * (1.0 / S.a));
     }
-  double sum = 0;
+  if (S.dim == 1) cen[0] = cen[1] = 0;
+  if (S.dim == 2) cen[2] = 0;
   for (int d = 0; d < 3; d++) {
     if (!F->allocated[d] || !F->allocated[3 * T_D + d]) continue;
-    double e, dd;
-    if (get_field(F, d, cen, &e, true) || get_field(F, 3 * T_D + d, cen, &dd, true)) return -1;
-    sum += real(std::conj(cplx(e)) * cplx(dd));
+    for (int which = 0; which < 2; which++) {  // E_d terms, then D_d terms
+      const int c = which == 0 ? d : 3 * T_D + d;
+      int locs[8][3];
+      double w[8];
+      interpolate(S, c, cen, locs, w);
+      for (int i = 0; i < 8 && w[i]; i++) {
+        int jg[3] = {0, 0, 0};
+        bool in = true;
+        for (int e = 0; e < 3; e++)
+          if (S.has[e]) {
+            const int o = locs[i][e] - S.io[e];
+            if (!(o > 0 && o <= 2 * S.n[e])) in = false;
+            jg[e] = (locs[i][e] - S.io[e] - S.shift(c, e)) / 2;
+          }
+        if (!in) continue;
+        const long long li = local_index(F, c, jg, true);
+        if (li < 0) continue;
+        if (t.n >= NAN_MAXT) return fail("NaN guard: too many terms");
+        t.dir[t.n] = (unsigned char)d;
+        t.kind[t.n] = which == 1 ? 2 : (in_fused_box(F, c, jg) ? 1 : 0);
+        t.idx[t.n] = li;
+        t.w[t.n] = w[i];
+        t.n++;
+      }
+    }
   }
-  if (!std::isfinite(sum * 0.5)) return fail("simulation fields are NaN or Inf");
+  return 0;
+}
+
+// launch the guard on the current state if one is due
+int nan_launch(mnl_fields *F) {
+  if (!F->nan_due) return 0;
+  F->nan_due = false;
+  if (!F->d_nanflag && dev_alloc(F, &F->d_nanflag, 2)) return -1;
+  if (F->nan_launched == 0) HIPCHK(hipMemsetAsync(F->d_nanflag, 0, 2 * sizeof(int), F->stream));
+  const double *E[3], *D[3], *U[3];
+  for (int d = 0; d < 3; d++) E[d] = F->f.E[d], D[d] = F->f.D[d], U[d] = F->f.inveps[d];
+  if (k_nan_check(F->nan_terms, E, D, U, F->d_nanflag, 0, F->stream))
+    return fail("NaN guard launch failed");
+  F->nan_launched++;
+  return 0;
+}
+
+// after k steps: count them, mark a guard due every nan_every steps (across calls)
+void nan_count(mnl_fields *F, int k) {
+  F->since_nan += k;
+  if (F->since_nan >= F->nan_every) {
+    F->since_nan = 0;
+    F->nan_due = true;
+  }
+}
+
+// end of a batch (stream synchronized): the reference's abort if a guard saw NaN / Inf
+int nan_result(mnl_fields *F) {
+  if (F->nan_launched == 0) return 0;  // the same on every rank (same step counts)
+  int h[2] = {0, 0};
+  HIPCHK(hipMemcpy(h, F->d_nanflag, sizeof h, hipMemcpyDeviceToHost));
+  F->nan_launched = 0;
+  bool ok = h[0] == 0;
+  if (F->nranks > 1 && F->comm->agree_ok(ok, F->stream)) ok = false;
+  if (!ok) return fail("simulation fields are NaN or Inf");
   return 0;
 }
 
@@ -5273,9 +5355,10 @@ int energy_in_box(mnl_fields *F, int which, const double wmin[3], const double w
   return 0;
 }
 
-// fields::step() n times: the NaN guard (src/step.cpp:138-139) every nan_every
-// steps (counted across calls); the first step after construction (or after E / H were set directly)
-// runs unfused (see e_first_done)
+// fields::step() n times: the NaN guard (src/step.cpp:138-139) after every nan_every-th
+// step (default every step; counted across calls) on the device, its flag read at the end of
+// each batch; the first step after construction (or after E / H were set directly) runs
+// unfused (see e_first_done)
 static int g_verbosity = 1;  // meep::verbosity (src/meep.hpp: default 1)
 
 static double wall_now() {
@@ -5334,17 +5417,10 @@ int fields_step_batches(mnl_fields *F, int nsteps) {
       F->force_unfused_next = false;
       m = 1;
     } else {
-      m = std::min(nsteps, std::max(1, F->nan_every - F->since_nan));
+      m = nsteps;  // the NaN guard runs on the device inside the batch (nan_launch)
       if (step_batch(F, m)) return -1;
     }
     nsteps -= m;
-    // every nan_every steps, counted across calls (a loop of one-step calls pays the
-    // guard's device round trips once per nan_every steps, not once per call)
-    F->since_nan += m;
-    if (F->since_nan >= F->nan_every) {
-      F->since_nan = 0;
-      if (nan_check(F)) return -1;
-    }
     if (g_verbosity > 0 && F->rank == 0) {
       const double now = wall_now();
       if (now > F->last_out_wall + 4.0 && F->t > F->last_out_t) {

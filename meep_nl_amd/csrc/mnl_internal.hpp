@@ -355,6 +355,20 @@ struct TB2Args {
   int ctr_line;
   unsigned long long cbase;
 };
+// NaN guard of fields::step (src/step.cpp:138-139): get_field(D_EnergyDensity, gv.center())
+// = 1/2 sum_d E_d(c) D_d(c), each value the interpolation of src/monitor.cpp:127-160 over
+// this rank's points (terms in interpolate() order: per direction the E terms, then the D
+// terms).  kind 0: stored E, 1: implicit E = D * chi1inv (fused box), 2: D.
+constexpr int NAN_MAXT = 48;
+struct NanTerms {
+  int n;
+  unsigned char dir[NAN_MAXT], kind[NAN_MAXT];
+  long long idx[NAN_MAXT];
+  double w[NAN_MAXT];
+};
+// flag[0] |= 1 (and flag[1] = step, once) when the sum is not finite
+int k_nan_check(const NanTerms &t, const double *const E[3], const double *const D[3],
+                const double *const U[3], int *flag, int step, void *stream);
 int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases);
 // one phase of a pair: rim items (tile kernel, pointer set of a; a.titems / tgeo / tflag
 // index the rim list) and two-step items (t) from one queue: order[v] >= 0 rim item, < 0

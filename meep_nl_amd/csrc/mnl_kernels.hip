@@ -3838,6 +3838,43 @@ int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
   return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 
+// NaN guard (src/step.cpp:138-139): one thread sums the interpolation terms of the D energy
+// density at the cell centre in the host's order (get_field: res += w * value) and flags a
+// non-finite result; no host round trip (the host reads the flag once per batch).
+__global__ void nan_check_kernel(NanTerms t, Ptr3 E, Ptr3 D, Ptr3 U, int *flag, int step) {
+  if (threadIdx.x != 0) return;
+  double sum = 0.0;
+  int i = 0;
+  for (int d = 0; d < 3; d++) {
+    double e = 0.0, dd = 0.0;
+    for (; i < t.n && t.dir[i] == d && t.kind[i] != 2; i++) {
+      const long long k = t.idx[i];
+      double v;
+      if (t.kind[i] == 0)
+        v = E.p[d][k];
+      else
+        v = U.ci[d] ? D.p[d][k] * U.ci[d][k] : D.p[d][k];
+      e += t.w[i] * v;
+    }
+    for (; i < t.n && t.dir[i] == d && t.kind[i] == 2; i++) dd += t.w[i] * D.p[d][t.idx[i]];
+    sum += e * dd;
+  }
+  if (!isfinite(sum * 0.5) && atomicOr(flag, 1) == 0) flag[1] = step;
+}
+
+int k_nan_check(const NanTerms &t, const double *const E[3], const double *const D[3],
+                const double *const U[3], int *flag, int step, void *stream) {
+  if (t.n <= 0) return 0;
+  Ptr3 e, d, u;
+  for (int c = 0; c < 3; c++) {
+    e.p[c] = const_cast<double *>(E[c]), e.ci[c] = nullptr;
+    d.p[c] = const_cast<double *>(D[c]), d.ci[c] = nullptr;
+    u.p[c] = nullptr, u.ci[c] = U[c];
+  }
+  nan_check_kernel<<<1, 64, 0, (hipStream_t)stream>>>(t, e, d, u, flag, step);
+  return rc();
+}
+
 // Leaving fused mode (or reading out): over G, E = chi1inv * D where it is
 // implicit, and the PML W aux fields get the values the reference holds
 // (W_E = chi1inv * D, W_H = B: the last fw of update_eh).

@@ -95,7 +95,8 @@ def test_energy_first_step_semantics():
 def test_nan_guard():
     """fields::step aborts with "simulation fields are NaN or Inf" when the D
     energy density at the cell centre is not finite (src/step.cpp:138-139); the
-    check runs every set_nan_check(k) steps inside a batch."""
+    check runs on the device every set_nan_check(k) steps inside a batch (default
+    every step), and the call raises at the end of the batch in which it fired."""
     from meep_nl_amd import core
     gv = core.GridVolume(3, [20, 20, 20], 10.0, [-20, -20, -20])
     s = core.Structure(gv)
@@ -111,6 +112,9 @@ def test_nan_guard():
     f2 = core.Fields(s)
     f2.initialize_field(8, v)
     f2.set_nan_check(2)
-    with pytest.raises(RuntimeError, match="NaN or Inf"):
-        f2.step(50)  # one call: the guard fires inside the batch
-    assert f2.t < 50
+    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
+        f2.step(50)  # one call: the guard fires inside the batch, the call raises
+    f3 = core.Fields(s)  # default cadence: every step
+    f3.initialize_field(8, v)
+    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
+        f3.step(10)  # one call of a few steps: checked (the old host guard ran every 100)

@@ -120,10 +120,11 @@ def test_tb_too_small_for_l2():
     _same(p, sc_tb(make_oracle, sizes=(3.2, 3.2, 3.2), srcs=((0.05, 0.05, 0.05),), steps=(1, 4)))
 
 
-def test_tb_split_launches():
-    """MNL_TB_SPLIT=1 (rim, two-step kernel, rim as three launches per pair: the diagnostic
-    path) gives the same fields as the pipelined phases."""
-    os.environ["MNL_TB_SPLIT"] = "1"
+def test_tb_pipelined_phases():
+    """MNL_TB_SPLIT=0 (pipelined phases: the previous pair's rim step beside the inner
+    two-step items, rim step n beside the outer ones, in one persistent kernel) gives the
+    same fields as the default three launches per pair."""
+    os.environ["MNL_TB_SPLIT"] = "0"
     try:
         p = sc_tb(ProductSim, steps=(1, 9, 1, 4))
     finally:
@@ -131,8 +132,14 @@ def test_tb_split_launches():
     _same(p, sc_tb(ProductSim, steps=(1, 9, 1, 4)))
 
 
-def test_tb_long_batch_pipelined():
-    """Many pairs in one batch (every phase A carries the previous pair's rim step), an odd
-    step at the end (drain, then one step), a NaN-guard batch boundary inside."""
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_tb_long_batch(split):
+    """Many pairs in one batch (pipelined: every phase A carries the previous pair's rim
+    step), an odd step at the end (drain, then one step), NaN guards inside."""
     kw = dict(steps=(1, 125))
-    _same(sc_tb(ProductSim, **kw), sc_tb(make_oracle, **kw))
+    os.environ["MNL_TB_SPLIT"] = split
+    try:
+        p = sc_tb(ProductSim, **kw)
+    finally:
+        del os.environ["MNL_TB_SPLIT"]
+    _same(p, sc_tb(make_oracle, **kw))
