@@ -339,6 +339,7 @@ struct mnl_fields {
   // pipelined phases, whose merged kernel spills registers; MNL_TB_SPLIT=0 selects those)
   bool tb_split = true;
   bool tb_pending = false;  // the last pair's rim step n+1 has not run yet (tb_drain)
+  bool tb_nopair = false;   // MNL_TB_NOPAIR=1: x-face rim strips one per workgroup (A/B)
   SrcDev tb_pend_src{};     // ... and the source currents applied after it
   double *pp3_B[3] = {nullptr, nullptr, nullptr}, *pp3_D[3] = {nullptr, nullptr, nullptr};
   double *pp3_E[3] = {nullptr, nullptr, nullptr}, *pp3_H[3] = {nullptr, nullptr, nullptr};
@@ -3534,7 +3535,7 @@ int tb_plan(mnl_fields *F) {
   // chunks <= zc cut at the lean box's z range), bodies as make_tile_boxes
   const int zc = F->fused_zchunk > 0 ? std::min(F->fused_zchunk, FUSED_MAXCH) : 24;
   struct RI {
-    int code, g0, g1, g2, planes;
+    int code, g0, g1, g2, g3, planes;
   };
   std::vector<RI> heavy, lean;
   F->rim_cells = F->rim_lean = 0;
@@ -3565,9 +3566,37 @@ int tb_plan(mnl_fields *F) {
           const double cells = double(x1 - x0 + 1) * (y1 - yf + 1) * (z1 - z0);
           F->rim_cells += cells;
           if (in_l) F->rim_lean += cells;
-          RI it{code, x0 | (x1 << 16), yf | (y1 << 16), z0 | (z1 << 16), z1 - z0};
+          RI it{code, x0 | (x1 << 16), yf | (y1 << 16), z0 | (z1 << 16), -1, z1 - z0};
           (((code >> 24) & 7) ? heavy : lean).push_back(it);
         }
+  }
+  // x-face strips of at most 32 columns (the rim left and right of L2) with the same rows,
+  // planes and body (AX = 1) share one workgroup in pairs (pml_body<PAIR>): a narrow item
+  // costs about a whole tile's time per plane (one dependent round per plane)
+  if (!F->tb_nopair) {
+    std::vector<RI> keep;
+    std::vector<size_t> open;  // unpaired strips, by (rows, planes, code)
+    for (const RI &it : heavy) {
+      const int w = (it.g0 >> 16) - (it.g0 & 0xFFFF) + 1;
+      if (((it.code >> 24) & 7) != 1 || w > 32) {
+        keep.push_back(it);
+        continue;
+      }
+      bool done = false;
+      for (size_t k = 0; k < open.size() && !done; k++) {
+        RI &o = keep[open[k]];
+        if (o.g1 == it.g1 && o.g2 == it.g2 && o.code == it.code) {
+          o.g3 = it.g0;
+          open.erase(open.begin() + (long)k);
+          done = true;
+        }
+      }
+      if (!done) {
+        open.push_back(keep.size());
+        keep.push_back(it);
+      }
+    }
+    heavy.swap(keep);
   }
   auto longest_first = [](std::vector<RI> &v) {
     std::stable_sort(v.begin(), v.end(), [](const RI &x, const RI &y) { return x.planes > y.planes; });
@@ -3580,6 +3609,7 @@ int tb_plan(mnl_fields *F) {
     for (const RI &it : *v) {
       F->tb_ritems.push_back(it.code);
       F->tb_rgeo.push_back(it.g0), F->tb_rgeo.push_back(it.g1), F->tb_rgeo.push_back(it.g2);
+      F->tb_rgeo.push_back(it.g3);
       rcost.push_back((it.planes + 1) * (((it.code >> 24) & 7) ? 2.0 : 1.0));
     }
   // ---- two-step items: 56 x 12 own points, z chunks of tz planes (automatic: the length
@@ -3715,9 +3745,11 @@ int tb_plan(mnl_fields *F) {
     F->rim_cells_nu = F->tb_cells_nu = 0;
     for (int i = 0; i < nr; i++)
       if (hr[i] == ~0u) {
-        const int *q = &F->tb_rgeo[3 * i];
-        F->rim_cells_nu += double((q[0] >> 16) - (q[0] & 0xFFFF) + 1) *
-                           ((q[1] >> 16) - (q[1] & 0xFFFF) + 1) * ((q[2] >> 16) - (q[2] & 0xFFFF));
+        const int *q = &F->tb_rgeo[4 * i];
+        const int wx = (q[0] >> 16) - (q[0] & 0xFFFF) + 1 +
+                       (q[3] >= 0 ? (q[3] >> 16) - (q[3] & 0xFFFF) + 1 : 0);
+        F->rim_cells_nu += double(wx) * ((q[1] >> 16) - (q[1] & 0xFFFF) + 1) *
+                           ((q[2] >> 16) - (q[2] & 0xFFFF));
       }
     for (int i = 0; i < ni; i++)
       if (hi[i] == ~0u) {
@@ -5536,6 +5568,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tb = getenv("MNL_TB")) F->tb_enabled = atoi(tb) != 0;
   if (const char *tz = getenv("MNL_TB_ZCHUNK")) F->tb_zchunk = std::max(0, atoi(tz));
   if (const char *ts = getenv("MNL_TB_SPLIT")) F->tb_split = atoi(ts) != 0;
+  if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
   if (const char *nf = getenv("MNL_NO_FUSED")) F->allow_fused = atoi(nf) == 0;

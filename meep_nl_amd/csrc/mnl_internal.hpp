@@ -320,7 +320,9 @@ struct FusedArgs {
   unsigned long long cbg[8];    // lean queue g: counter line g's value at launch start
   unsigned long long *ctr;      // FUSED_NCTR work-queue counters (128 B apart); see cbase
   // explicit own boxes of the tile items (null: tx / ty / ch index xb / yb / zb): per item
-  // x0 | x1 << 16 (columns, x0 128-byte aligned), yfirst | y1 << 16 (own rows), zs | ze << 16
+  // x0 | x1 << 16 (columns, x0 128-byte aligned), yfirst | y1 << 16 (own rows), zs | ze << 16,
+  // and a second x-face strip of at most 32 columns sharing the workgroup (xb0 | xb1 << 16,
+  // both strips <= 32 columns, body AX = 1) or -1
   const int *tgeo;
 };
 

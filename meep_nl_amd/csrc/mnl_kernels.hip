@@ -1635,6 +1635,7 @@ struct FBatch {  // what B(k) needs besides E(k): own raw at k+1, B_old(k), halo
 // Lean-body geometry of one work item (see FusedArgs: bounds come from the host).
 struct ItemGeo {
   int x0, x1;  // tile columns [x0, x1] (x0 128-byte aligned)
+  int xb0, xb1;  // paired item (pml_body<PAIR>): the second sub-tile's columns; xb0 < 0: none
   int y0;      // halo row; own rows y0+1 .. y1
   int y1;
   int zs, ze;  // planes [zs, ze)
@@ -1648,7 +1649,10 @@ struct TabE {
 };
 // the table entry outside every PML chunk (kappa = 1, sigma = 0)
 __device__ constexpr TabE kTabId = {1.0, 1.0, 1.0};
-constexpr int TPZ = FUSED_MAXCH + 2;
+constexpr int TPZ = FUSED_MAXCH + 4;
+// LDS row width of the tile bodies: 64 columns + the x-1 and x+64 halo columns, or (paired
+// items) two 32-column sub-tiles with their own halo columns (34 + 34)
+constexpr int FXL = FX + 4;
 
 // curl update with the per-point branch selection of step_curl
 // (src/step_generic.cpp:84-252), written branch-free: outside a PML chunk
@@ -2285,8 +2289,8 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
 // x-1 column (B recomputed), the E of the x+64 column and a corner.
 template <int UMODE, int DIST>
 __device__ __forceinline__ void lean_body(const FusedArgs &a, const ItemGeo &itg, unsigned uw,
-                                          const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
-                                          double (*sB)[FR][FX + 1]) {
+                                          const double (*sU)[256], double (*sE)[FR + 1][FXL],
+                                          double (*sB)[FR][FXL]) {
   constexpr bool HAS_U = UMODE != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform
@@ -2540,7 +2544,7 @@ struct PTabL {
   double v[3][3][2][TPZ];
   unsigned char f[3][2][TPZ];
 };
-static_assert(TPZ >= FX + 2 && TPZ >= FR + 1, "table positions");
+static_assert(TPZ >= FXL && TPZ >= FR + 1, "table positions");
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, unsigned nrec) {
   // null: zero records, every access out of range (loads 0, stores dropped)
@@ -2584,10 +2588,14 @@ __device__ __forceinline__ unsigned own_bits_of(int v, int sl, int sh, int ul, i
 // host): the y / z ownership terms are the constant 3, so every ownership test and the
 // E-load source of a lane are fixed along the march (no per-plane recomputation), and the
 // z index needs no clamp
-template <int UMODE, int DIST, int AX, bool OWNC>
+// PAIR: two items of at most 32 own columns with the same rows and planes (the rim's x-face
+// strips of temporal blocking) in one workgroup: lanes 0..31 the first (LDS columns 1..32, halo
+// columns 0 and 33), lanes 32..63 the second (it.xb0 .. it.xb1; LDS columns 35..66, halo 34 and
+// 67); the halo wave serves both.  Row and z logic are unchanged.
+template <int UMODE, int DIST, int AX, bool OWNC, bool PAIR = false>
 __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, unsigned uw,
-                                         const double (*sU)[256], double (*sE)[FR + 1][FX + 2],
-                                         double (*sB)[FR][FX + 1], PTabL &P) {
+                                         const double (*sU)[256], double (*sE)[FR + 1][FXL],
+                                         double (*sB)[FR][FXL], PTabL &P) {
   constexpr bool HAS_U = UMODE != 0;
   constexpr bool PX = (AX & 1) != 0, PY = (AX & 2) != 0, PZ = (AX & 4) != 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -2600,11 +2608,13 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   // ---- PML tables of the footprint -> LDS (x: x0-1 .. x0+64, y: y0 .. y0+FR,
   // z: zs-1 .. ze), only the directions of this body
   {
-    constexpr int NX = PX ? 2 * (FX + 2) : 0, NY = PY ? 2 * (FR + 1) : 0, NZ = PZ ? 2 * TPZ : 0;
+    constexpr int NX = PX ? 2 * (PAIR ? FXL : FX + 2) : 0, NY = PY ? 2 * (FR + 1) : 0,
+                  NZ = PZ ? 2 * TPZ : 0;
     for (int i = threadIdx.x; i < NX + NY + NZ; i += 1024) {
       int ax, pos, base;
-      if (i < NX) {
+      if (i < NX) {  // table position = LDS column
         ax = 0, pos = i >> 1, base = x0 - 1;
+        if (PAIR && pos >= FXL / 2) base = it.xb0 - 1 - FXL / 2;
       } else if (i < NX + NY) {
         ax = 1, pos = (i - NX) >> 1, base = y0;
       } else {
@@ -2619,34 +2629,39 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
       P.f[ax][sft][pos] = a.tab.flag[ax][q];
     }
   }
-  // ---- lane roles (the lean body's)
+  // ---- lane roles (the lean body's; PAIR: per 32-lane half, for its sub-tile)
+  constexpr int SW = PAIR ? 32 : FX;        // columns of a (sub-)tile
+  const int sub = PAIR ? (lane >> 5) : 0;  // sub-tile of the lane
+  const int sl = PAIR ? (lane & 31) : lane;
+  const int sx0 = sub ? it.xb0 : x0, sx1 = sub ? it.xb1 : it.x1;  // sub-tile own columns
+  const int cofs = sub * (FXL / 2);        // LDS column of the sub-tile's x-1 halo
   int row, col;
   bool ownlike;
   int hrow = 0, hcol = 0, hc0 = 0, hdx = 0, hdy = 0;
   bool hslot = false;
   if (w < FR) {
     row = w;
-    col = lane + 1;
+    col = cofs + sl + 1;
     ownlike = true;
     if (w == FR - 1) {  // y+1 row
-      hslot = true, hrow = FR, hcol = col, hc0 = 0, hdx = lane, hdy = FR;
+      hslot = true, hrow = FR, hcol = col, hc0 = 0, hdx = sl, hdy = FR;
     }
   } else {
-    row = lane + 1;
-    col = 0;
-    ownlike = lane < FOWN;
-    if (lane >= 16 && lane < 16 + FR) {  // x+64 column
-      hslot = true, hrow = lane - 16, hcol = FX + 1, hc0 = 1, hdx = FX, hdy = lane - 16;
-    } else if (lane == 31) {  // E(x0-1, y0+FR)
-      hslot = true, hrow = FR, hcol = 0, hc0 = 0, hdx = -1, hdy = FR;
+    row = sl + 1;
+    col = cofs;
+    ownlike = sl < FOWN;
+    if (sl >= 16 && sl < 16 + FR) {  // x+SW column
+      hslot = true, hrow = sl - 16, hcol = cofs + SW + 1, hc0 = 1, hdx = SW, hdy = sl - 16;
+    } else if (sl == 31) {  // E(x0-1, y0+FR)
+      hslot = true, hrow = FR, hcol = cofs, hc0 = 0, hdx = -1, hdy = FR;
     }
   }
   // (no lambda below refers to `a`: a closure holding its address makes the compiler
   // copy the whole argument block to scratch)
   const int N0 = a.N[0], N1 = a.N[1];
   const long long st1 = a.st1;
-  const int ox = (w < FR) ? lane : -1;
-  const int gx = x0 + ox, gy = y0 + row;
+  const int ox = (w < FR) ? sl : -1;
+  const int gx = sx0 + ox, gy = y0 + row;
   const bool inA = ownlike && gx >= 0 && gx < N0 && gy >= 0 && gy < N1;
   const unsigned cb = (unsigned)((gx + (long long)gy * st1) * 8);
   const unsigned cbl = inA ? cb : 0u;
@@ -2660,8 +2675,8 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   auto own_b = [](int c, unsigned ox_, unsigned oy_, unsigned oz_) {
     return ((c == 0 ? ox_ >> 1 : ox_) & (c == 1 ? oy_ >> 1 : oy_) & (c == 2 ? oz_ >> 1 : oz_) & 1u) != 0;
   };
-  const bool stl = ownlike && w < FR && row >= 1 && gx <= it.x1 && gy <= it.y1;
-  const int hx = x0 + hdx, hy = y0 + hdy;
+  const bool stl = ownlike && w < FR && row >= 1 && gx <= sx1 && gy <= it.y1;
+  const int hx = sx0 + hdx, hy = y0 + hdy;
   const bool hA = hslot && hx >= 0 && hx < N0 && hy >= 0 && hy < N1;
   const unsigned hbl = hA ? (unsigned)((hx + (long long)hy * st1) * 8) : cbl;
   const unsigned hownx = own_bits_of(hx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
@@ -2744,7 +2759,7 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   // W flags (PML chunk along the E component's own direction, shifted coordinate)
   const bool Wx = F(0, 1, 0), Wy = F(1, 1, 0);
 #define Wz(pz) F(2, 1, pz)
-  const bool hW0 = hc0 == 0 ? (PX && P.f[0][1][hdx + 1] != 0) : (PY && P.f[1][1][hdy] != 0);
+  const bool hW0 = hc0 == 0 ? (PX && P.f[0][1][hcol] != 0) : (PY && P.f[1][1][hdy] != 0);
 
   struct PBatch {  // plane k: D(k+1) (or stored E where not owned), u(k+1), B(k),
                    // stored E(k+1) of W-form components, halo E(k)
@@ -3008,8 +3023,8 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
 template <int UMODE, int DIST>
 __device__ __forceinline__ void tile_item_body(const FusedArgs &a, int item, const ItemGeo &itg,
                                                unsigned uw, const double (*sU)[256],
-                                               double (*sE)[FR + 1][FX + 2],
-                                               double (*sB)[FR][FX + 1], PTabL &sP) {
+                                               double (*sE)[FR + 1][FXL],
+                                               double (*sB)[FR][FXL], PTabL &sP) {
   constexpr int MD = MNL_MULTI_DIST;
   const bool ownc = MNL_OWNC && ((item >> 29) & 1);
   switch ((item >> 24) & 7) {
@@ -3017,10 +3032,16 @@ __device__ __forceinline__ void tile_item_body(const FusedArgs &a, int item, con
       lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
       break;
     case 1:
-      if (ownc)
+      if (itg.xb0 >= 0) {  // paired x-face strips (temporal-blocking rim)
+        if (ownc)
+          pml_body<UMODE, DIST, 1, true, true>(a, itg, uw, sU, sE, sB, sP);
+        else
+          pml_body<UMODE, DIST, 1, false, true>(a, itg, uw, sU, sE, sB, sP);
+      } else if (ownc) {
         pml_body<UMODE, DIST, 1, true>(a, itg, uw, sU, sE, sB, sP);
-      else
+      } else {
         pml_body<UMODE, DIST, 1, false>(a, itg, uw, sU, sE, sB, sP);
+      }
       break;
     case 2:
       if (ownc)
@@ -3052,14 +3073,16 @@ __device__ __forceinline__ void tile_item_body(const FusedArgs &a, int item, con
 // own box of tile item `idx`: explicit (FusedArgs::tgeo) or tile / chunk indices
 __device__ __forceinline__ ItemGeo tile_item_geo(const FusedArgs &a, int item, int idx) {
   ItemGeo itg;
+  itg.xb0 = itg.xb1 = -1;
   if (a.tgeo) {
-    const int *gp = a.tgeo + 3 * idx;
+    const int *gp = a.tgeo + 4 * idx;
     itg.x0 = gp[0] & 0xFFFF;
     itg.x1 = gp[0] >> 16;
     itg.y0 = (gp[1] & 0xFFFF) - 1;
     itg.y1 = gp[1] >> 16;
     itg.zs = gp[2] & 0xFFFF;
     itg.ze = gp[2] >> 16;
+    if (gp[3] >= 0) itg.xb0 = gp[3] & 0xFFFF, itg.xb1 = gp[3] >> 16;
   } else {
     const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
     itg.x0 = a.xb[tx];
@@ -3077,8 +3100,8 @@ __device__ __forceinline__ ItemGeo tile_item_geo(const FusedArgs &a, int item, i
 template <int UMODE, int DIST>
 __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
-  __shared__ double sE[3][FR + 1][FX + 2];
-  __shared__ double sB[3][FR][FX + 1];
+  __shared__ double sE[3][FR + 1][FXL];
+  __shared__ double sB[3][FR][FXL];
   __shared__ PTabL sP;
   __shared__ int s_item, s_idx;
   __shared__ unsigned s_uw;
@@ -3111,8 +3134,8 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
 template <int UMODE, int DIST>
 __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
-  __shared__ double sE[3][FR + 1][FX + 2];
-  __shared__ double sB[3][FR][FX + 1];
+  __shared__ double sE[3][FR + 1][FXL];
+  __shared__ double sB[3][FR][FXL];
   __shared__ long long s_item;
   if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
     for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
@@ -3318,10 +3341,14 @@ __global__ void tile_uniform_kernel(FusedArgs a, unsigned *flags) {
   const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
   int ix0, iy0, izs, ize;  // tile column start, halo row, planes [izs, ize)
   if (a.tgeo) {
-    ix0 = a.tgeo[3 * idx] & 0xFFFF;
-    iy0 = (a.tgeo[3 * idx + 1] & 0xFFFF) - 1;
-    izs = a.tgeo[3 * idx + 2] & 0xFFFF;
-    ize = a.tgeo[3 * idx + 2] >> 16;
+    if (a.tgeo[4 * idx + 3] >= 0) {  // paired item: per-cell palette words
+      if (threadIdx.x == 0) flags[idx] = ~0u;
+      return;
+    }
+    ix0 = a.tgeo[4 * idx] & 0xFFFF;
+    iy0 = (a.tgeo[4 * idx + 1] & 0xFFFF) - 1;
+    izs = a.tgeo[4 * idx + 2] & 0xFFFF;
+    ize = a.tgeo[4 * idx + 2] >> 16;
   } else {
     ix0 = a.xb[tx], iy0 = a.yb[ty] - 1, izs = a.zb[ch], ize = a.zb[ch + 1];
   }
@@ -3718,7 +3745,7 @@ __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
 // is a rim item (index into a.titems / a.tgeo / a.tflag), < 0 the two-step item ~order[v];
 // the host interleaves the two kinds so latency-bound rim items run beside
 // bandwidth-bound two-step items.  The LDS of the two body families is one union.
-constexpr int TILE_LDS_D = 3 * (FR + 1) * (FX + 2) + 3 * FR * (FX + 1) + (int)(sizeof(PTabL) + 7) / 8;
+constexpr int TILE_LDS_D = 3 * (FR + 1) * FXL + 3 * FR * FXL + (int)(sizeof(PTabL) + 7) / 8;
 constexpr int TB_LDS_D = 4 * 3 * TB_LY * TB_LX;
 template <int UMODE>
 __global__ __launch_bounds__(1024) void tb_phase_kernel(FusedArgs a, TB2Args t, const int *order,
@@ -3730,9 +3757,9 @@ __global__ __launch_bounds__(1024) void tb_phase_kernel(FusedArgs a, TB2Args t, 
   if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
     for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
   }
-  double(*sE)[FR + 1][FX + 2] = reinterpret_cast<double(*)[FR + 1][FX + 2]>(sm);
-  double(*sB)[FR][FX + 1] = reinterpret_cast<double(*)[FR][FX + 1]>(sm + 3 * (FR + 1) * (FX + 2));
-  PTabL &sP = *reinterpret_cast<PTabL *>(sm + 3 * (FR + 1) * (FX + 2) + 3 * FR * (FX + 1));
+  double(*sE)[FR + 1][FXL] = reinterpret_cast<double(*)[FR + 1][FXL]>(sm);
+  double(*sB)[FR][FXL] = reinterpret_cast<double(*)[FR][FXL]>(sm + 3 * (FR + 1) * FXL);
+  PTabL &sP = *reinterpret_cast<PTabL *>(sm + 3 * (FR + 1) * FXL + 3 * FR * FXL);
   constexpr int TBA = 3 * TB_LY * TB_LX;
   double(*sE1)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm);
   double(*sH1)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm + TBA);
