@@ -284,6 +284,37 @@ def measure_extra(workload, size, steps, warmup, tune=True):
     return out
 
 
+def measure_c5(args, rank, world, device, dist):
+    """BASELINE C5 on the ranks of this run: per GPU a S x S x S/4 z-slab of the vacuum +
+    PML(1.0) grid (S = --size; 512: the 1024x512x512 domain at N = 8), tuned, warmed up,
+    K steps between barriers, max over ranks."""
+    from meep_nl_amd import core
+    import torch
+    transport, _ = core.pick_transport(world, int(os.environ.get("LOCAL_RANK", "0")))
+    obj = [core.comm_id(world, transport) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    gv, s, f = build_fields("c5", args.size, rank, world, device, obj[0])
+    zc = None if args.no_tune else f.tune()
+    f.step(args.warmup)
+    dist.barrier()
+    t0 = time.perf_counter()
+    f.step(args.steps)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    cells = float(gv.n[0]) * gv.n[1] * gv.n[2]
+    out = {"workload": WORKLOADS["c5"] + f", global {gv.n[0]}x{gv.n[1]}x{gv.n[2]} cells "
+                       f"({world} z-slabs), res 10, real fields",
+           "value": round(cells * args.steps / el / 1e6, 1), "unit": "Mcells*steps/s",
+           "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps,
+           "n_gpus": world, "scaling": "weak", "transport": f.transport(),
+           "fused": f.fused_active(), "tuned_zchunk_gen_cus": zc}
+    del f, s
+    gc.collect()
+    return out
+
+
 def cpu_baseline(args):
     """Time the oracle (CPU restatement, oracle/) on a bounded sample of the
     headline workload on this host's cores: a 128^3 grid of the same waveguide
@@ -362,7 +393,11 @@ def main():
         nid = obj[0]
     elif os.environ.get("MNL_BENCH_DEVICE"):
         device = int(os.environ["MNL_BENCH_DEVICE"])
-    gv, s, f = build_fields(args.workload, args.size, rank, world, device, nid)
+    try:
+        gv, s, f = build_fields(args.workload, args.size, rank, world, device, nid)
+    except RuntimeError as e:  # a failed RCCL setup names RCCL and exits non-zero
+        sys.stderr.write(f"bench.py rank {rank}: {e}\n")
+        sys.exit(3)
     if args.flux:  # on-device DFT flux monitors
         hx = 0.5 * gv.n[0] / 10.0
         hy, hz = 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
@@ -381,11 +416,16 @@ def main():
     # GPU clocks / power sampled while this rank keeps stepping (untimed, <= 10 s), and
     # again right after the timed region
     state_busy = None
-    if rank == 0 and not args.no_smi:
-        proc, t_s = gpu_state_start(), time.perf_counter()
-        while proc is not None and proc.poll() is None and time.perf_counter() - t_s < 10:
-            f.step(10)
-        state_busy = gpu_state_finish(proc)
+    if not args.no_smi:
+        proc = gpu_state_start() if rank == 0 else None
+        if world == 1:
+            t_s = time.perf_counter()
+            while proc is not None and proc.poll() is None and time.perf_counter() - t_s < 10:
+                f.step(10)
+        else:  # every rank steps the same count (the steps are collective)
+            f.step(100)
+        if proc is not None:
+            state_busy = gpu_state_finish(proc)
     barrier()
     f.set_profiling(not args.no_events)
     t0 = time.perf_counter()
@@ -418,11 +458,18 @@ def main():
     fused = f.fused_active()
     del f, s
     gc.collect()
+    extra = None
+    if world > 1 and not args.no_extra and args.workload != "c5":
+        # BASELINE configs[4] (C5) in the same multi-GPU run: 512 x 512 x 128 vacuum + PML
+        # per GPU, its own communicator, timed the same way (max over ranks)
+        try:
+            extra = {"c5": measure_c5(args, rank, world, device, dist)}
+        except Exception as e:  # never hides the headline number
+            extra = {"c5": {"error": str(e)}}
     if rank != 0:
         if dist is not None:
             dist.barrier()
         return
-    extra = None
     if world == 1 and not args.no_extra and not args.flux:
         extra = {}
         for wl in ("c2", "kerr", "kerr_nr"):

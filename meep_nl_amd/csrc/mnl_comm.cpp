@@ -151,12 +151,27 @@ int Comm::init_ipc(const void *id128) {
   return 0;
 }
 
-// a peer's process has exited (its pid no longer exists)
+// a process that has exited: its pid is gone, or it is a zombie (exited, not yet reaped by a
+// launcher that may itself be waiting on another rank) -- /proc/<pid>/stat state Z or X
+static bool pid_exited(int pid) {
+  if (kill(pid, 0) != 0 && errno == ESRCH) return true;
+  char path[64], buf[512];
+  snprintf(path, sizeof path, "/proc/%d/stat", pid);
+  FILE *f = fopen(path, "r");
+  if (!f) return false;  // cannot tell: alive
+  const size_t n = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char *p = strrchr(buf, ')');  // the command name may hold spaces and parentheses
+  return p && p[1] == ' ' && (p[2] == 'Z' || p[2] == 'X');
+}
+
+// a peer's process has exited
 bool Comm::ipc_peer_dead() const {
   for (int r = 0; r < nranks; r++) {
     const int pid = ipc_->slot[r].pid;
     if (r == rank || pid <= 0) continue;
-    if (kill(pid, 0) != 0 && errno == ESRCH) return true;
+    if (pid_exited(pid)) return true;
   }
   return false;
 }
@@ -174,11 +189,13 @@ int Comm::ipc_barrier() {
     C.gen.fetch_add(1, std::memory_order_release);
     return 0;
   }
-  // Setup waits are bounded by MNL_IPC_TIMEOUT (300 s); once every rank has joined, a
-  // wait lasts as long as the peers' processes live (a rank-0-only output or a whole-cell
-  // setup can legitimately keep the others waiting for minutes), and MNL_IPC_TIMEOUT
-  // bounds it only when set explicitly.
+  // Setup waits are bounded by MNL_IPC_TIMEOUT (default 300 s).  Once every rank has joined,
+  // a wait ends when a peer's process exits (or turns zombie), and otherwise after
+  // MNL_IPC_TIMEOUT when set, else 1800 s: a rank-0-only output or a whole-cell setup can
+  // legitimately keep the others waiting for minutes, a peer that took another code path
+  // must not hang them forever.
   static const bool explicit_timeout = getenv("MNL_IPC_TIMEOUT") != nullptr;
+  const double limit = (ipc_ready_ && !explicit_timeout) ? 1800.0 : ipc_timeout_s_;
   auto t0 = std::chrono::steady_clock::now();
   long spins = 0;
   while (C.gen.load(std::memory_order_acquire) == g) {
@@ -191,9 +208,8 @@ int Comm::ipc_barrier() {
           ipc_abort();  // a peer died: fail every rank instead of hanging
           return -1;
         }
-        if ((!ipc_ready_ || explicit_timeout) &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
-                ipc_timeout_s_) {
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+            limit) {
           ipc_abort();  // a peer never joined or diverged: fail every rank
           return -1;
         }
@@ -270,6 +286,9 @@ int Comm::unique_id(void *out128) {
   return 0;
 }
 
+static thread_local char g_comm_err[256] = "";
+const char *comm_last_error() { return g_comm_err; }
+
 int Comm::init(int r, int n, const void *id128) {
   rank = r;
   nranks = n;
@@ -278,7 +297,12 @@ int Comm::init(int r, int n, const void *id128) {
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
   ncclComm_t c;
-  if (ncclCommInitRank(&c, n, id, r) != ncclSuccess) return -1;
+  const ncclResult_t rc = ncclCommInitRank(&c, n, id, r);
+  if (rc != ncclSuccess) {
+    snprintf(g_comm_err, sizeof g_comm_err, "ncclCommInitRank(rank %d of %d): %s", r, n,
+             ncclGetErrorString(rc));
+    return -1;
+  }
   comm_ = c;
   if (hipMalloc(&dscratch_, 64 * sizeof(double)) != hipSuccess) return -1;
   return 0;

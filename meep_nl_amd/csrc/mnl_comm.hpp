@@ -68,6 +68,8 @@ class Comm {
   std::vector<Op> sends_, recvs_;
 };
 
+// detail of the last failed RCCL setup call of this thread ("" if none)
+const char *comm_last_error();
 LocalHub *local_hub_create(int nranks);
 void local_hub_destroy(LocalHub *h);
 

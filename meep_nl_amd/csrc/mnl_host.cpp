@@ -5558,7 +5558,10 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
     if (hub ? F->comm->init_local(rank, nranks, hub) : F->comm->init(rank, nranks, id)) {
       fail(hub ? "local slab group init failed"
                : Comm::is_ipc_id(id) ? "IPC slab group init failed (shared-memory id)"
-                                     : "RCCL communicator init failed");
+                                     : std::string("RCCL communicator init failed (") +
+                                           comm_last_error() +
+                                           "); MNL_COMM=ipc runs the same slabs over the "
+                                           "IPC transport");
       return nullptr;
     }
   }
