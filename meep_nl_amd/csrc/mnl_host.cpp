@@ -340,6 +340,8 @@ struct mnl_fields {
   bool tb_split = true;
   bool tb_pending = false;  // the last pair's rim step n+1 has not run yet (tb_drain)
   bool tb_nopair = false;   // MNL_TB_NOPAIR=1: x-face rim strips one per workgroup (A/B)
+  int tb_rfree = 0;         // leading rim items that read no slab-face data (multi-rank)
+  bool tb_chain_pending = false;  // the last multi-rank pair's s_comm chain not yet joined
   SrcDev tb_pend_src{};     // ... and the source currents applied after it
   double *pp3_B[3] = {nullptr, nullptr, nullptr}, *pp3_D[3] = {nullptr, nullptr, nullptr};
   double *pp3_E[3] = {nullptr, nullptr, nullptr}, *pp3_H[3] = {nullptr, nullptr, nullptr};
@@ -421,7 +423,7 @@ struct mnl_fields {
 namespace {
 
 bool in_fused_box(const mnl_fields *F, int c, const int jg[3]);
-int nan_launch(mnl_fields *F);
+int nan_launch(mnl_fields *F, hipStream_t st = nullptr);
 void nan_count(mnl_fields *F, int k);
 int nan_result(mnl_fields *F);
 int nan_terms_build(mnl_fields *F);
@@ -3509,8 +3511,13 @@ int tb_plan(mnl_fields *F) {
   // to the right of L2 starts on a 128-byte boundary (tile-kernel items)
   L2.lo[0] += ((4 - L2.lo[0]) % 8 + 8) % 8;
   L2.hi[0] = (L2.hi[0] + 1) / 16 * 16 - 1;
-  for (int k = 0; k < 3; k++)
-    if (L2.hi[k] - L2.lo[k] < 7) return 0;
+  bool l2 = true;
+  for (int k = 0; k < 3; k++) l2 = l2 && L2.hi[k] - L2.lo[k] >= 7;
+  // one rank: no two-step region, no pairs.  Multi-rank: a rank without one (thin slab, PML)
+  // still steps pairs as two rim launches (every rank runs the same exchange sequence)
+  if (!l2 && F->nranks == 1) return 0;
+  if (!l2)
+    for (int k = 0; k < 3; k++) L2.lo[k] = 1, L2.hi[k] = 0;
   // holes: no source point within distance 1 of a two-step own point (the march's D^{n+1}
   // would miss the current); a box of +-2 for margin, x widened to the alignments above and
   // to the L2 edge when that leaves fewer than 8 columns
@@ -3520,7 +3527,7 @@ int tb_plan(mnl_fields *F) {
     const int s[3] = {(int)(r % g.st[1]), (int)(r / g.st[1]), (int)i2};
     Box h;
     for (int k = 0; k < 3; k++) h.lo[k] = s[k] - 2, h.hi[k] = s[k] + 2;
-    if (!box_meets(h, L2)) continue;
+    if (!l2 || !box_meets(h, L2)) continue;
     h.lo[0] = std::max(h.lo[0], 0) / 16 * 16;
     while ((h.hi[0] + 1) % 8 != 4) h.hi[0]++;
     for (int k = 0; k < 3; k++) h.lo[k] = std::max(h.lo[k], L2.lo[k]), h.hi[k] = std::min(h.hi[k], L2.hi[k]);
@@ -3529,14 +3536,26 @@ int tb_plan(mnl_fields *F) {
     holes.push_back(h);
   }
   std::vector<Box> two, rim;
-  tb_regions(G, L2, holes, two, rim);
-  if (two.empty()) return 0;
+  if (l2) {
+    tb_regions(G, L2, holes, two, rim);
+  } else {
+    rim.push_back(G);
+  }
+  if (two.empty() && F->nranks == 1) return 0;
   // ---- rim items: tile-kernel shapes (columns <= 64 from 128-byte boundaries, rows <= 14,
   // chunks <= zc cut at the lean box's z range), bodies as make_tile_boxes
   const int zc = F->fused_zchunk > 0 ? std::min(F->fused_zchunk, FUSED_MAXCH) : 24;
   struct RI {
     int code, g0, g1, g2, g3, planes;
+    bool dep;  // multi-rank: reads the ghost plane 0 or the top plane N-1 (slab-face data)
   };
+  const bool lower = F->rank > 0, upper = F->rank + 1 < F->nranks;
+  const int N2 = g.N[2];
+  std::vector<std::array<int, 3>> spts;  // D source points (local indices)
+  for (long long idx : F->srcD_idx) {
+    const long long i2 = idx / g.st[2], r = idx % g.st[2];
+    spts.push_back({(int)(r % g.st[1]), (int)(r / g.st[1]), (int)i2});
+  }
   std::vector<RI> heavy, lean;
   F->rim_cells = F->rim_lean = 0;
   for (const Box &b : rim) {
@@ -3545,8 +3564,10 @@ int tb_plan(mnl_fields *F) {
     split_range(xs, b.lo[0], b.hi[0] + 1, FX_HOST, 16);
     xs.push_back(b.hi[0] + 1);
     std::vector<int> zcut = {b.lo[2], b.hi[2] + 1};
-    for (int v : {L.lo[2] + 1, L.hi[2]})
+    for (int v : {L.lo[2] + 1, L.hi[2], lower ? 2 : -1, upper ? N2 - 2 : -1})
       if (v > b.lo[2] && v < b.hi[2] + 1) zcut.push_back(v);
+    std::sort(zcut.begin(), zcut.end());
+    zcut.erase(std::unique(zcut.begin(), zcut.end()), zcut.end());
     std::sort(zcut.begin(), zcut.end());
     for (size_t s = 0; s + 1 < zcut.size(); s++) {
       const int n = zcut[s + 1] - zcut[s], nt = (n + zc - 1) / zc;
@@ -3566,7 +3587,15 @@ int tb_plan(mnl_fields *F) {
           const double cells = double(x1 - x0 + 1) * (y1 - yf + 1) * (z1 - z0);
           F->rim_cells += cells;
           if (in_l) F->rim_lean += cells;
-          RI it{code, x0 | (x1 << 16), yf | (y1 << 16), z0 | (z1 << 16), -1, z1 - z0};
+          // multi-rank: the sources are applied after the top plane's step (slab-face
+          // chain), so items holding a source point wait for it too
+          bool src_in = false;  // in the footprint (E = chi1inv * D of a neighbour)
+          if (F->nranks > 1)
+            for (const auto &sp : spts)
+              src_in = src_in || (sp[0] >= x0 - 1 && sp[0] <= x1 + 1 && sp[1] >= yf - 1 &&
+                                  sp[1] <= y1 + 1 && sp[2] >= z0 - 1 && sp[2] <= z1);
+          RI it{code, x0 | (x1 << 16), yf | (y1 << 16), z0 | (z1 << 16), -1, z1 - z0,
+                (lower && z0 <= 1) || (upper && z1 >= N2 - 1) || src_in};
           (((code >> 24) & 7) ? heavy : lean).push_back(it);
         }
   }
@@ -3585,7 +3614,7 @@ int tb_plan(mnl_fields *F) {
       bool done = false;
       for (size_t k = 0; k < open.size() && !done; k++) {
         RI &o = keep[open[k]];
-        if (o.g1 == it.g1 && o.g2 == it.g2 && o.code == it.code) {
+        if (o.g1 == it.g1 && o.g2 == it.g2 && o.code == it.code && o.dep == it.dep) {
           o.g3 = it.g0;
           open.erase(open.begin() + (long)k);
           done = true;
@@ -3605,7 +3634,15 @@ int tb_plan(mnl_fields *F) {
   longest_first(lean);
   std::vector<double> rcost;  // estimated time of a rim item: planes (+ the halo plane), PML
                               // bodies about twice a lean plane
-  for (auto *v : {&heavy, &lean})
+  // items that need no slab-face data first (multi-rank: they run before the face exchange)
+  std::vector<RI> order;
+  for (int dep = 0; dep < 2; dep++)
+    for (auto *v : {&heavy, &lean})
+      for (const RI &it : *v)
+        if (it.dep == (dep == 1)) order.push_back(it);
+  F->tb_rfree = 0;
+  for (const RI &it : order) F->tb_rfree += it.dep ? 0 : 1;
+  for (auto *v : {&order})
     for (const RI &it : *v) {
       F->tb_ritems.push_back(it.code);
       F->tb_rgeo.push_back(it.g0), F->tb_rgeo.push_back(it.g1), F->tb_rgeo.push_back(it.g2);
@@ -3759,7 +3796,7 @@ int tb_plan(mnl_fields *F) {
       }
   }
   HIPCHK(hipStreamSynchronize(F->stream));
-  F->tb_have = ni > 0;
+  F->tb_have = ni > 0 || (F->nranks > 1 && nr > 0);
   if (getenv("MNL_TB_STATS"))
     fprintf(stderr, "tb: L2 [%d..%d]x[%d..%d]x[%d..%d], %zu holes, %zu two-step boxes, %zu rim "
             "boxes; %d two-step items (%d planes, %.0f cells, %.0f border), %d rim items "
@@ -3773,11 +3810,16 @@ int tb_plan(mnl_fields *F) {
 // Can the batch step in pairs?  Builds the plan when needed (-1: HIP error).
 int tb_usable(mnl_fields *F, bool *ok) {
   *ok = false;
-  if (!F->tb_enabled || !F->fused || !F->tile_mode || F->nranks != 1 || F->fgeo.ngen > 0 ||
-      !F->dfts.empty() || F->S.dim != 3)
-    return 0;
-  if (tb_plan(F)) return -1;
-  *ok = F->tb_have;
+  bool local = F->tb_enabled && F->fused && F->tile_mode && F->fgeo.ngen == 0 &&
+               F->dfts.empty() && F->S.dim == 3 && F->slab_dir == 2;
+  if (local && tb_plan(F)) return -1;
+  local = local && F->tb_have;
+  if (F->nranks > 1) {  // every rank or none (their exchange sequences differ by mode)
+    double v = local ? 1.0 : 0.0;
+    if (F->comm->allreduce_sum(&v, 1, F->stream)) return fail("allreduce failed");
+    local = v == double(F->nranks);
+  }
+  *ok = local;
   return 0;
 }
 
@@ -3954,6 +3996,109 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   return 0;
 }
 
+// Multi-rank pair (one rank of a z-slab decomposition; fused, no D source on the top
+// plane).  L2 lies >= 2 planes from the slab faces, so only the rim meets them:
+//   main: L (cur -> nxt, border -> mid) on all CUs but RES (the previous pair's slab-face
+//         chain still runs on s_comm), then, once the E ghost of step n is in (ev_x0), R1
+//         (rim, cur -> mid);
+//   s_comm: B/H plane exchange of mid, the top plane's step n (shell kernels, old = cur,
+//         new = mid), source(n), E plane exchange of mid (ev_x0);
+//   main: R2 over the rim items that read no slab-face data and hold no source point
+//         (beside that chain), then the others once it is done;
+//   s_comm: the same chain for nxt -- beside the next pair's L.
+// Every kernel reads and writes disjoint points of its sets.
+constexpr int TB_RES_CUS = 8;  // CUs left to the slab-face chain (one per XCD)
+
+int tb_face_chain(mnl_fields *F, const Set5 &o, const Set5 &n, const SrcDev &src,
+                  hipEvent_t after) {
+  DevFields &f = F->f;
+  const DevGrid &g = F->g;
+  HIPCHK(hipStreamWaitEvent(F->s_comm, after, 0));
+  // exchanges and shell kernels read F->f's pointers when enqueued: point them at the sets
+  const DevFields keep = f;
+  for (int d = 0; d < 3; d++) {
+    f.B[d] = o.B[d], f.D[d] = o.D[d], f.E[d] = o.E[d], f.H[d] = o.H[d], f.UB[d] = o.UB[d];
+    f.Bn[d] = n.B[d], f.Dn[d] = n.D[d], f.En[d] = o.E[d] ? n.E[d] : nullptr;
+    f.Hn[d] = o.H[d] ? n.H[d] : nullptr, f.UBn[d] = o.UB[d] ? n.UB[d] : nullptr;
+  }
+  int r = exchange(F, 1, F->s_comm) ? fail("H halo exchange failed") : 0;
+  const BoxList *sl = &F->fused_shell;
+  if (!r && k_curl(T_B, F->interior, sl, g, f, F->planB, F->S.courant, F->s_comm, true))
+    r = fail("curl B launch failed");
+  // the sources of the step (every D point: after the top plane's curl D, as the one-step
+  // path applies them after all of D); with one on the top plane E follows the source there
+  const bool fuseE = !F->dsrc_in_shell;
+  if (!r && k_curl(T_D, F->interior, sl, g, f, F->planD, F->S.courant, F->s_comm, fuseE))
+    r = fail("curl D launch failed");
+  if (!r && src.n && k_source(T_D, g, f, src, 0, F->s_comm)) r = fail("source launch failed");
+  if (!r && !fuseE) {
+    ISrcDev is{};
+    if (k_update_e(F->interior, sl, g, f, is, 0, true, F->s_comm)) r = fail("update E launch failed");
+  }
+  if (!r) {  // the E plane of the new set goes up
+    for (int d = 0; d < 3; d++) f.E[d] = n.E[d];
+    if (exchange(F, 0, F->s_comm)) r = fail("E halo exchange failed");
+  }
+  const DevFields fresh = f;
+  f = keep;
+  (void)fresh;
+  if (r) return r;
+  HIPCHK(hipEventRecord(F->ev_x0, F->s_comm));
+  return 0;
+}
+
+template <class EB, class EE>
+int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end) {
+  if (tb_mid_init(F)) return -1;
+  const FusedArgs &fa = fused_args(F);
+  const Set5 cur = set_cur(F), mid = set_mid(F), nxt = set_nxt(F);
+  TB2Args t = tb_args(F, cur, mid, nxt);
+  const int cus = k_cu_count();
+  t.wg_limit = cus - TB_RES_CUS;
+  const int nr = (int)F->tb_ritems.size(), nf = F->tb_rfree;
+  int k = ev_begin(TM_TB);
+  int kr = k_tb2(t, F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("two-step kernel launch failed", kr);
+  // R1 once the E ghost (and top plane) of step n are in
+  HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
+  FusedArgs r1 = rim_args(F, fa, cur, mid);
+  k = ev_begin(TM_RIM);
+  kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("rim kernel launch failed", kr);
+  HIPCHK(hipEventRecord(F->ev_early, F->stream));
+  if (tb_face_chain(F, cur, mid, s0, F->ev_early)) return -1;
+  // R2: the items without slab-face reads beside the chain, then the others
+  FusedArgs r2 = rim_args(F, fa, mid, nxt);
+  r2.wg_limit = cus - TB_RES_CUS;
+  k = ev_begin(TM_RIM);
+  kr = k_tile_items(r2, r2.titems, r2.tgeo, r2.tflag, nf, 4, F->stream, F->ctr_base);
+  if (!kr) {
+    HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
+    r2.wg_limit = 0;
+    kr = k_tile_items(r2, r2.titems + nf, r2.tgeo + 4 * nf, r2.tflag ? r2.tflag + nf : nullptr,
+                      nr - nf, 4, F->stream, F->ctr_base);
+  }
+  ev_end(k);
+  if (kr) return fused_fail("rim kernel launch failed", kr);
+  HIPCHK(hipEventRecord(F->ev_early, F->stream));
+  if (tb_face_chain(F, mid, nxt, s1, F->ev_early)) return -1;
+  swap_cur_nxt(F->f);
+  F->tb_chain_pending = true;  // a one-step step next waits for it (tb_chain_join)
+  nan_count(F, 2);
+  return nan_launch(F, F->s_comm);  // after the chain: the top plane of the new state
+}
+
+// Before a one-step step after a multi-rank pair: the pair's last slab-face chain (top plane,
+// sources, E ghost) ran on s_comm; the one-step kernels on the main stream read its results.
+int tb_chain_join(mnl_fields *F) {
+  if (!F->tb_chain_pending) return 0;
+  F->tb_chain_pending = false;
+  HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
+  return 0;
+}
+
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
   // in-process A/B of the fused geometry (tools/ab_inproc.py): MNL_TILE_STEP /
@@ -4122,13 +4267,15 @@ int step_batch(mnl_fields *F, int nsteps) {
       ISrcDev is = F->isrc_dev;
       is.n = (int)nI;
       is.val = vs + jofs;  // kernels index val[step * n + orig] with step 0
-      if (tb_ok && s + 1 < ns) {  // steps s and s + 1 as one pair (no DFT, one rank)
+      if (tb_ok && s + 1 < ns) {  // steps s and s + 1 as one pair (no DFT)
         const SrcDev sD1 = src_dev(F, 1, vs + per + 2 * ng);
-        if (tb_pair(F, sD, sD1, ev_begin, ev_end)) return -1;
+        if ((F->nranks > 1 ? tb_pair_multi(F, sD, sD1, ev_begin, ev_end)
+                           : tb_pair(F, sD, sD1, ev_begin, ev_end)))
+          return -1;
         s++;
         continue;
       }
-      if (tb_drain(F, ev_begin, ev_end)) return -1;
+      if (tb_drain(F, ev_begin, ev_end) || tb_chain_join(F)) return -1;
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
         nan_count(F, 1);
@@ -4308,6 +4455,7 @@ int step_batch(mnl_fields *F, int nsteps) {
     HIPCHK(hipStreamSynchronize(F->s_comm));
     HIPCHK(hipStreamSynchronize(F->s_aux));
   }
+  F->tb_chain_pending = false;
   HIPCHK(hipStreamSynchronize(F->stream));
   HIPCHK(hipGetLastError());
   return nan_result(F);
@@ -4363,14 +4511,14 @@ int nan_terms_build(mnl_fields *F) {
 }
 
 // launch the guard on the current state if one is due
-int nan_launch(mnl_fields *F) {
+int nan_launch(mnl_fields *F, hipStream_t st) {
   if (!F->nan_due) return 0;
   F->nan_due = false;
-  if (!F->d_nanflag && dev_alloc(F, &F->d_nanflag, 2)) return -1;
-  if (F->nan_launched == 0) HIPCHK(hipMemsetAsync(F->d_nanflag, 0, 2 * sizeof(int), F->stream));
+  if (!st) st = F->stream;
+  if (!F->d_nanflag && dev_alloc(F, &F->d_nanflag, 2)) return -1;  // zeroed; reset by nan_result
   const double *E[3], *D[3], *U[3];
   for (int d = 0; d < 3; d++) E[d] = F->f.E[d], D[d] = F->f.D[d], U[d] = F->f.inveps[d];
-  if (k_nan_check(F->nan_terms, E, D, U, F->d_nanflag, 0, F->stream))
+  if (k_nan_check(F->nan_terms, E, D, U, F->d_nanflag, 0, st))
     return fail("NaN guard launch failed");
   F->nan_launched++;
   return 0;
@@ -4390,6 +4538,7 @@ int nan_result(mnl_fields *F) {
   if (F->nan_launched == 0) return 0;  // the same on every rank (same step counts)
   int h[2] = {0, 0};
   HIPCHK(hipMemcpy(h, F->d_nanflag, sizeof h, hipMemcpyDeviceToHost));
+  if (h[0]) HIPCHK(hipMemset(F->d_nanflag, 0, sizeof h));
   F->nan_launched = 0;
   bool ok = h[0] == 0;
   if (F->nranks > 1 && F->comm->agree_ok(ok, F->stream)) ok = false;

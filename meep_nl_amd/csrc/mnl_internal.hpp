@@ -356,6 +356,8 @@ struct TB2Args {
   unsigned long long *ctr;      // work-queue counters (FusedArgs::ctr); line ctr_line
   int ctr_line;
   unsigned long long cbase;
+  int wg_limit;                 // > 0: at most this many persistent workgroups (CUs left to
+                                // the slab-face kernels of multi-rank pairs)
 };
 // NaN guard of fields::step (src/step.cpp:138-139): get_field(D_EnergyDensity, gv.center())
 // = 1/2 sum_d E_d(c) D_d(c), each value the interpolation of src/monitor.cpp:127-160 over

@@ -3504,6 +3504,7 @@ int k_tile_items(const FusedArgs &a, const int *items, const int *geo, const uns
       line >= FUSED_NCTR)
     return 2;
   long long nb = fused_grid_blocks(a.blocks_per_cu > 0 ? a.blocks_per_cu : 1);
+  if (a.wg_limit > 0 && nb > a.wg_limit) nb = a.wg_limit;
   if (nb > n) nb = n;
   FusedArgs t = a;
   t.titems = items, t.tgeo = geo, t.tflag = flags;
@@ -3849,6 +3850,7 @@ int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
       a.ctr_line >= FUSED_NCTR)
     return 2;
   long long nb = fused_grid_blocks(1);
+  if (a.wg_limit > 0 && nb > a.wg_limit) nb = a.wg_limit;
   if (nb > a.n) nb = a.n;
   TB2Args t = a;
   t.cbase = bases[a.ctr_line];

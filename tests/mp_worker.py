@@ -69,6 +69,7 @@ def run_case(name, make):
     arrs = {f"c{c}": o.get_array(c) for c in range(12)}
     arrs.update(extra)
     arrs["transport"] = np.array(o._fields().transport())
+    arrs["tb"] = np.array([o._fields().tb_info()["active"]])  # pairs of steps
     arrs["t"] = np.array([o.t])
     return arrs
 

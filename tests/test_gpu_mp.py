@@ -103,8 +103,11 @@ def test_multiprocess_slabs_bitwise(mp_runs, nranks, name):
         assert got.shape == ref.shape
         d = float(np.max(np.abs(got - ref))) if ref.size else 0.0
         assert d == 0.0, (c, d)
-    if name == "big_box_tuned":  # each rank tuned (its own choice), then stepped to 30
+    if name == "big_box_tuned":  # every rank tuned (the same choice: max over ranks), then 30
         assert all(int(r["zchunk"][0]) in (0, 16, 20, 24, 32, 48) for r in ranks)
+        assert len({int(r["zchunk"][0]) for r in ranks}) == 1
+    if name in ("big_box", "big_box_tuned", "c5_small"):  # multi-rank temporal blocking
+        assert all(bool(r["tb"][0]) for r in ranks)
     for k, v in ex.items():
         for r in ranks:  # collectives: every rank holds the same result
             np.testing.assert_array_equal(r[k], ranks[0][k])

@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from scenarios import ALL_COMPS, ProductSim, make_oracle, random_init, vol
+from scenarios import ALL_COMPS, GroupSim, GroupSim3, ProductSim, make_oracle, random_init, vol
 
 pytestmark = pytest.mark.gpu
 
@@ -38,9 +38,10 @@ def sc_tb(make, sizes=(9.6, 6.4, 8.0), dpml=0.7, eps=6.0, random_eps=False, srcs
     if rand:
         random_init(o, (6, 7, 8, 9, 10, 11))
     if isinstance(o, ProductSim):
-        o._fields().set_temporal_blocking(tb)
-        if profile:
-            o._fields().set_profiling(True)
+        for f in (o._all() if hasattr(o, "_all") else [o._fields()]):
+            f.set_temporal_blocking(tb)
+            if profile:
+                f.set_profiling(True)
     for n in steps:
         o.step(n)
     return o
@@ -143,3 +144,19 @@ def test_tb_long_batch(split):
     finally:
         del os.environ["MNL_TB_SPLIT"]
     _same(p, sc_tb(make_oracle, **kw))
+
+
+@pytest.mark.parametrize("group", [GroupSim, GroupSim3])
+def test_tb_slabs(group):
+    """z-slabs of one grid (in-process transport): every rank steps pairs (L2 >= 2 planes
+    from its slab faces, the faces in the rim: B/H and E plane exchanges of the middle and
+    new sets, the top plane's shell kernels between them), bitwise the oracle."""
+    kw = dict(sizes=(9.6, 6.4, 9.6), steps=(1, 12, 1, 3))
+    p = sc_tb(group, **kw)
+    assert all(f.tb_info()["active"] for f in p._all())
+    _same(p, sc_tb(make_oracle, **kw))
+
+
+def test_tb_slabs_equal_one_step():
+    kw = dict(sizes=(9.6, 6.4, 9.6), steps=(1, 7, 2, 1, 6))
+    _same(sc_tb(GroupSim3, **kw), sc_tb(GroupSim3, tb=False, **kw))
