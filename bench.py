@@ -164,11 +164,14 @@ def roofline(f, kind=0):
         achieved = t_bytes / (t_avg * 1e-3) / 1e9
         r_n, r_ms, r_bytes = f.kernel_stats(6)
         roof.update({
-            "kernel": "tb_phase_kernel x2 per pair of steps (two-step z-march over the lean "
-                      "region L2 + one-step tile bodies over the PML / wall / ring / source-hole "
-                      "rim, interleaved in one persistent queue)",
+            "kernel": ("tb2_kernel (two-step z-march over the lean region L2) + 2 x "
+                       "fused_tile_kernel over the rim items (PML, walls, ring, source holes), "
+                       "one pair of steps" if tb.get("split", True) else
+                       "tb_phase_kernel x2 per pair of steps (two-step z-march over the lean "
+                       "region L2 + one-step tile bodies over the PML / wall / ring / "
+                       "source-hole rim, interleaved in one persistent queue)"),
             "bytes_per_launch": t_bytes, "avg_launch_ms": round(t_avg, 4), "launches": t_n,
-            "launch_unit": "pair of steps (two phase launches)",
+            "launch_unit": "pair of steps (all its launches)",
             "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
             "steps_per_launch": 2,
             "frac_one_step_model": round(2.0 * k_bytes / (t_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

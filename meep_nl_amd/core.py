@@ -398,9 +398,10 @@ class Fields:
     def tune(self, reps=3):
         """Time the fused step's knobs over real steps and keep the fastest (mnl_fields_tune:
         the tile kernel's z-chunk length, then on one rank with polarization chunks the CUs
-        of their general kernel beside the tile kernel).  Advances the fields by at most
-        2 + 12 * (1 + reps) steps, results identical to plain stepping.  Returns (zchunk,
-        gen_cus); -1 = not tuned (not in the fused tile mode)."""
+        of their general kernel beside the tile kernel; with temporal blocking the planes of
+        its two-step items).  Every candidate runs two warm-up steps and reps (rounded up to
+        even) timed ones: at most 2 + 18 * (2 + reps) steps, results identical to plain
+        stepping.  Returns (zchunk, gen_cus); -1 = not tuned (not in the fused tile mode)."""
         z, g = ctypes.c_int(0), ctypes.c_int(0)
         check(lib().mnl_fields_tune(self.h, int(reps), ctypes.byref(z), ctypes.byref(g)))
         return z.value, g.value
@@ -575,11 +576,12 @@ class Fields:
         """Temporal blocking of the current fused geometry: dict of
         active, two-step own cells / border points / mixed-palette cells, rim cells /
         mixed-palette rim cells, item counts and the first item's planes."""
-        v = (ctypes.c_double * 9)()
-        check(lib().mnl_fields_tb_info(self.h, v, 9))
+        v = (ctypes.c_double * 11)()
+        check(lib().mnl_fields_tb_info(self.h, v, 11))
         keys = ("active", "tb_cells", "tb_border", "tb_cells_mixed", "rim_cells",
-                "rim_cells_mixed", "tb_items", "rim_items", "tb_planes")
-        return {k: (bool(x) if k == "active" else int(x)) for k, x in zip(keys, v)}
+                "rim_cells_mixed", "tb_items", "rim_items", "tb_planes", "split", "enabled")
+        flags = ("active", "split", "enabled")
+        return {k: (bool(x) if k in flags else int(x)) for k, x in zip(keys, v)}
 
     def traffic_model(self):
         b = ctypes.c_double()

@@ -6416,12 +6416,14 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
     }
   }
   // temporal blocking: planes per two-step item (automatic = the item count that fills whole
-  // rounds of one workgroup per CU best)
-  if (!rc && F->fused && F->tb_have && F->tb_enabled && !getenv("MNL_TB_ZCHUNK")) {
+  // rounds), and whether pairs beat one-step stepping at all (small grids: the rim is a
+  // large share of the cells)
+  if (!rc && F->fused && F->tb_have && F->tb_enabled) {
     const int tz0 = F->tb_zchunk;
     int best = tz0;
     double best_ms = 0;
     for (int c : {0, 32, 48, 64, 96, 128}) {
+      if (getenv("MNL_TB_ZCHUNK") && c != tz0) continue;
       F->tb_zchunk = c;
       double tm, gm;
       if (timed(&tm, &gm)) { rc = -1; break; }
@@ -6430,6 +6432,14 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
       if (best_ms == 0 || tm + gm < best_ms) best_ms = tm + gm, best = c;
     }
     F->tb_zchunk = rc ? tz0 : best;
+    if (!rc && !getenv("MNL_TB")) {
+      F->tb_enabled = false;
+      double tm, gm;
+      if (timed(&tm, &gm)) rc = -1;
+      if (verbose)
+        fprintf(stderr, "tune rank %d: one-step: %.4f ms/step\n", F->rank, tm + gm);
+      F->tb_enabled = rc || tm + gm >= best_ms;
+    }
   }
   F->profiling = prof;
   for (int k = 0; k < 16; k++) F->timer_ms[k] = tms[k], F->timer_count[k] = tcnt[k];
@@ -6801,7 +6811,7 @@ int mnl_fields_set_temporal_blocking(mnl_fields *F, int on) {
 
 int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
   if (!F || !out || n < 1) return fail("bad argument");
-  const double v[9] = {F->fused && F->tb_have ? 1.0 : 0.0,
+  const double v[11] = {F->fused && F->tb_have && F->tb_enabled ? 1.0 : 0.0,
                        F->tb_cells,
                        F->tb_border,
                        F->tb_cells_nu,
@@ -6810,8 +6820,10 @@ int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
                        double(F->tb_items.size()),
                        double(F->tb_ritems.size()),
                        F->tb_items.empty() ? 0.0 : double((F->tb_items[0].z >> 16) -
-                                                          (F->tb_items[0].z & 0xFFFF))};
-  for (int i = 0; i < n && i < 9; i++) out[i] = v[i];
+                                                          (F->tb_items[0].z & 0xFFFF)),
+                       F->tb_split ? 1.0 : 0.0,
+                       F->tb_enabled ? 1.0 : 0.0};
+  for (int i = 0; i < n && i < 11; i++) out[i] = v[i];
   return 0;
 }
 

@@ -11,7 +11,7 @@ from scenarios import ALL_COMPS, GroupSim, ProductSim, make_oracle, sc_random_fi
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 SIZES = (6.4, 5.2, 9.6)  # 64 x 52 x 96 cells at resolution 10: several z chunks per length
-TOTAL = 32
+TOTAL = 80  # tune(reps=1) steps at most 2 + 18 * (2 + 2) = 74
 ZCS = (0, 16, 20, 24, 32, 48)
 
 
@@ -23,7 +23,7 @@ def _tuned(G, kerr):
         p._all()
         chosen = p._par(lambda f: f.tune(reps=1))
     t = p.t
-    assert 1 + 6 * 2 <= t <= TOTAL, t  # every z-chunk candidate stepped: the tile mode was on
+    assert 1 + 6 * 4 <= t <= TOTAL, t  # every z-chunk candidate stepped: the tile mode was on
     p.step(TOTAL - t)
     return p, chosen
 
