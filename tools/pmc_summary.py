@@ -51,15 +51,23 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--vacuum", action="store_true")
     ap.add_argument("--kernel", default="fused_kernel")
+    ap.add_argument("--pair", action="store_true",
+                    help="temporal blocking: the traffic of a pair of steps = tb2_kernel + 2 x "
+                         "fused_tile_kernel (the rim launches)")
+    ap.add_argument("--dirs", nargs=3, metavar=("STATS", "FETCH", "WRITE"),
+                    help="separate directories of the stats / FETCH_SIZE / WRITE_SIZE runs "
+                         "(tools/gpu.sh prof: / pmc: steps) instead of src/{stats,fetch,write}")
     a = ap.parse_args()
+    sub = dict(zip(("stats", "fetch", "write"), a.dirs)) if a.dirs else {
+        k: os.path.join(a.src, k) for k in ("stats", "fetch", "write")}
     res = {}
-    for f in glob.glob(os.path.join(a.src, "stats", "**", "*kernel_stats.csv"), recursive=True):
+    for f in glob.glob(os.path.join(sub["stats"], "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = short(r["Name"])
             res.setdefault(k, {})
             res[k]["calls"] = int(r["Calls"])
             res[k]["avg_ms"] = float(r["AverageNs"]) / 1e6
-    fe, wr = counters(os.path.join(a.src, "fetch")), counters(os.path.join(a.src, "write"))
+    fe, wr = counters(sub["fetch"]), counters(sub["write"])
     sq, tcc = counters(os.path.join(a.src, "sq")), counters(os.path.join(a.src, "tcc"))
     sq2 = counters(os.path.join(a.src, "sq2"))
     for k in set(fe) | set(wr):
@@ -83,6 +91,19 @@ def main():
     print(json.dumps({k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                           for kk, vv in v.items() if kk in ("avg_ms", "hbm_bytes", "hbm_GBps")}
                       for k, v in res.items()}, indent=1))
+    if a.traffic and a.pair:
+        tb = [k for k in res if k.startswith("tb2_kernel") and "hbm_bytes" in res[k]]
+        rim = [k for k in res if k.startswith("fused_tile_kernel") and "hbm_bytes" in res[k]]
+        if tb and rim:
+            hb = res[tb[0]]["hbm_bytes"] + 2 * res[rim[0]]["hbm_bytes"]
+            with open(a.traffic, "w") as fh:
+                json.dump({"kernels_hash": kernels_hash(), "size": a.size, "vacuum": a.vacuum,
+                           "kernel": "pair: tb2_kernel + 2 x fused_tile_kernel (rim)",
+                           "unit": "pair of steps", "hbm_bytes_per_launch": hb,
+                           "tb2_bytes": res[tb[0]]["hbm_bytes"],
+                           "rim_bytes": res[rim[0]]["hbm_bytes"],
+                           "profile": os.path.basename(a.dst)}, fh, indent=1)
+        return
     if a.traffic:
         ks = [k for k in res if k.startswith(a.kernel) and "hbm_bytes" in res[k]]
         if ks:
