@@ -37,6 +37,7 @@ typedef std::complex<double> cplx;
 namespace {
 constexpr int FX_HOST = 64;    // fused tile width (FX in mnl_kernels.hip)
 constexpr int FOWN_HOST = 14;  // own rows of a tile item (FOWN in mnl_kernels.hip)
+constexpr int TB_RES_CUS = 8;  // multi-rank: CUs left to the slab-face work (one per XCD)
 
 const double pi = 3.141592653589793238462643383276;  // meep::pi
 thread_local std::string g_err;
@@ -213,8 +214,13 @@ struct DftFluxH {
   int nbuf = 0;                       // buffered updates (rows row-nbuf .. row-1)
   int kb = DFT_KB;                    // updates per accumulation
   double bytes = 0;                   // algorithmic bytes of one update (DESIGN.md "DFT")
+  void *d_sidx = nullptr;             // sampling plan (k_dft_plan): 4 int32 indices per point
+  unsigned short *d_ssel = nullptr;   // ... and a selector per point
+  long long plan_key = -1;            // the mode the plan was built for (dft_plan_key)
   ~DftFluxH() {
     if (d_ph) (void)hipFree(d_ph);
+    if (d_sidx) (void)hipFree(d_sidx);
+    if (d_ssel) (void)hipFree(d_ssel);
   }
 };
 
@@ -2020,13 +2026,41 @@ int dft_flush(mnl_fields *F, DftFluxH &o) {
 }
 
 // after step t (fields::update_dfts, src/dft.cpp:249-263)
-int dft_update(mnl_fields *F, long long t) {
+// what a sampling plan depends on: implicit E (the fused mode and its geometry) and which H
+// components are stored separately
+long long dft_plan_key(const mnl_fields *F) {
+  long long k = (long long)F->fused_epoch * 2 + (F->fused ? 1 : 0);
+  for (int d = 0; d < 3; d++) k = k * 2 + (F->f.H[d] ? 1 : 0);
+  return k * 2 + (F->f.hall ? 1 : 0);
+}
+
+// fields: the buffer set to sample (null: the current one; temporal blocking samples the middle
+// step of a pair from the mid set)
+int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr) {
+  const bool planned = F->nlocal < (size_t(1) << 31);  // int32 indices in the plan
   for (auto &op : F->dfts) {
     DftFluxH &o = *op;
     if (t % o.decim || !o.npts) continue;
-    if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, o.d_fr + (size_t)o.nbuf * o.npts,
-                     (long long)o.npts, F->g, F->f, F->stream))
+    double *fr = o.d_fr + (size_t)o.nbuf * o.npts;
+    if (planned) {
+      const long long key = dft_plan_key(F);
+      if (o.plan_key != key) {
+        if (!o.d_sidx) {
+          HIPCHK(hipMalloc(&o.d_sidx, o.npts * 16));
+          HIPCHK(hipMalloc(&o.d_ssel, o.npts * 2));
+        }
+        if (k_dft_plan(o.d_pj, o.d_pch, o.d_ch, (long long)o.npts, F->g, F->f, o.d_sidx,
+                       o.d_ssel, F->stream))
+          return fail("dft plan launch failed");
+        o.plan_key = key;
+      }
+      if (k_dft_sample_plan(o.d_sidx, o.d_ssel, o.d_pw, fr, (long long)o.npts,
+                            fields ? *fields : F->f, F->stream))
+        return fail("dft sample launch failed");
+    } else if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, fr, (long long)o.npts, F->g,
+                            fields ? *fields : F->f, F->stream)) {
       return fail("dft sample launch failed");
+    }
     o.nbuf++;
     o.row++;
     if (o.nbuf == o.kb && dft_flush(F, o)) return -1;
@@ -3230,7 +3264,11 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
   if (exchange(F, 1, F->s_comm)) return fail("H halo exchange failed");
   HIPCHK(hipEventRecord(F->ev_x1, F->s_comm));
   int k = ev_begin(TM_BINT);
+  // the persistent main launch leaves TB_RES_CUS CUs to the chunk-0 launch on s_aux and
+  // the slab-face work after it, so they cannot queue behind it for the whole step
+  fa.wg_limit = F->tile_mode ? k_cu_count() - TB_RES_CUS : 0;
   kr = k_fused(fa, F->tile_mode ? 6 : 0, F->stream, F->ctr_base);
+  fa.wg_limit = 0;
   if (kr) return fused_fail("fused kernel launch failed", kr);
   ev_end(k);
   if (!F->tile_mode || fa.ngen > fa.ngen_e) {
@@ -3497,6 +3535,24 @@ int tb_plan(mnl_fields *F) {
   mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
   mix((long long)F->srcD_idx.size());
   for (long long v : F->srcD_idx) mix(v);
+  // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
+  // the two-step items store step n+1 there too (the middle-step sample reads the mid set)
+  std::vector<Box> dbox;
+  for (auto &op : F->dfts) {
+    Box b;
+    for (int k = 0; k < 3; k++) b.lo[k] = INT32_MAX, b.hi[k] = -1;
+    for (size_t p = 0; p < op->h_pj.size() / 3; p++) {
+      if (op->h_pj[3 * p] < 0) continue;
+      for (int k = 0; k < 3; k++) {
+        b.lo[k] = std::min(b.lo[k], op->h_pj[3 * p + k]);
+        b.hi[k] = std::max(b.hi[k], op->h_pj[3 * p + k] + 1);
+      }
+    }
+    if (b.hi[0] >= 0) dbox.push_back(b);
+  }
+  mix((long long)dbox.size());
+  for (const Box &b : dbox)
+    for (int k = 0; k < 3; k++) mix(b.lo[k]), mix(b.hi[k]);
   if (sig == F->tb_sig) return 0;
   F->tb_sig = sig;
   F->tb_have = false;
@@ -3717,6 +3773,34 @@ int tb_plan(mnl_fields *F) {
           it.y = o.lo[1] | (o.hi[1] << 16);
           it.z = o.lo[2] | ((o.hi[2] + 1) << 16);
           it.faces = faces;
+          it.bx = it.by = it.bz = -1, it.pad = 0;
+          {
+            Box u;  // bounding box of the item's intersections with the DFT boxes
+            bool any = false;
+            for (const Box &db : dbox) {
+              Box x;
+              bool ok = true;
+              for (int k = 0; k < 3; k++) {
+                x.lo[k] = std::max(o.lo[k], db.lo[k]);
+                x.hi[k] = std::min(o.hi[k], db.hi[k]);
+                ok = ok && x.lo[k] <= x.hi[k];
+              }
+              if (!ok) continue;
+              for (int k = 0; k < 3; k++) {
+                u.lo[k] = any ? std::min(u.lo[k], x.lo[k]) : x.lo[k];
+                u.hi[k] = any ? std::max(u.hi[k], x.hi[k]) : x.hi[k];
+              }
+              any = true;
+            }
+            if (any) {
+              it.bx = u.lo[0] | (u.hi[0] << 16);
+              it.by = u.lo[1] | (u.hi[1] << 16);
+              it.bz = u.lo[2] | (u.hi[2] << 16);
+              double nb2 = 1;
+              for (int k = 0; k < 3; k++) nb2 *= u.hi[k] - u.lo[k] + 1;
+              nb += nb2;
+            }
+          }
           F->tb_items.push_back(it);
           F->tb_cells += double(o.hi[0] - o.lo[0] + 1) * (o.hi[1] - o.lo[1] + 1) *
                          (o.hi[2] - o.lo[2] + 1);
@@ -3811,7 +3895,8 @@ int tb_plan(mnl_fields *F) {
 int tb_usable(mnl_fields *F, bool *ok) {
   *ok = false;
   bool local = F->tb_enabled && F->fused && F->tile_mode && F->fgeo.ngen == 0 &&
-               F->dfts.empty() && F->S.dim == 3 && F->slab_dir == 2;
+               F->S.dim == 3 && F->slab_dir == 2 &&
+               (F->dfts.empty() || (F->nranks == 1 && F->tb_split));
   if (local && tb_plan(F)) return -1;
   local = local && F->tb_have;
   if (F->nranks > 1) {  // every rank or none (their exchange sequences differ by mode)
@@ -3946,7 +4031,8 @@ int tb_drain(mnl_fields *F, EB &ev_begin, EE &ev_end) {
 // n+1 stays pending for the next phase A or tb_drain.  Every launch reads and writes disjoint
 // points of its sets (DESIGN.md section 24 has the hazard argument).
 template <class EB, class EE>
-int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end) {
+int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end,
+            long long t_mid) {
   if (tb_mid_init(F)) return -1;
   const FusedArgs &fa = fused_args(F);
   const Set5 cur = set_cur(F), mid = set_mid(F), nxt = set_nxt(F);
@@ -3964,6 +4050,15 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
     kr = k_tb2(t, F->stream, F->ctr_base);
     ev_end(k);
     if (kr) return fused_fail("two-step kernel launch failed", kr);
+    if (dft_due(F, t_mid)) {  // fields::update_dfts after the pair's first step, from mid
+      DevFields fm = F->f;
+      for (int d = 0; d < 3; d++)
+        fm.B[d] = mid.B[d], fm.D[d] = mid.D[d], fm.E[d] = mid.E[d], fm.H[d] = mid.H[d];
+      k = ev_begin(TM_DFT);
+      const int r = dft_update(F, t_mid, &fm);
+      ev_end(k);
+      if (r) return -1;
+    }
     k = ev_begin(TM_RIM);
     kr = k_tile_items(r2, r2.titems, r2.tgeo, r2.tflag, nr, 4, F->stream, F->ctr_base);
     ev_end(k);
@@ -4007,7 +4102,6 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
 //         (beside that chain), then the others once it is done;
 //   s_comm: the same chain for nxt -- beside the next pair's L.
 // Every kernel reads and writes disjoint points of its sets.
-constexpr int TB_RES_CUS = 8;  // CUs left to the slab-face chain (one per XCD)
 
 int tb_face_chain(mnl_fields *F, const Set5 &o, const Set5 &n, const SrcDev &src,
                   hipEvent_t after) {
@@ -4270,9 +4364,10 @@ int step_batch(mnl_fields *F, int nsteps) {
       if (tb_ok && s + 1 < ns) {  // steps s and s + 1 as one pair (no DFT)
         const SrcDev sD1 = src_dev(F, 1, vs + per + 2 * ng);
         if ((F->nranks > 1 ? tb_pair_multi(F, sD, sD1, ev_begin, ev_end)
-                           : tb_pair(F, sD, sD1, ev_begin, ev_end)))
+                           : tb_pair(F, sD, sD1, ev_begin, ev_end, F->t + s + 1)))
           return -1;
         s++;
+        if (post_step(s)) return -1;  // DFT of the pair's second step (the new state)
         continue;
       }
       if (tb_drain(F, ev_begin, ev_end) || tb_chain_join(F)) return -1;

@@ -339,6 +339,10 @@ struct TB2Item {
   int z;      // zs | ze << 16 (own planes [zs, ze))
   int faces;  // bits 0..5: own face x-lo, x-hi, y-lo, y-hi, z-lo, z-hi borders the rim (its
               // points' step n+1 values are stored into the middle buffer set)
+  // a box of own points whose step n+1 values are also stored into the middle set (the DFT
+  // monitors sample step n+1 there): x0 | x1 << 16, y0 | y1 << 16, z0 | z1 << 16 (inclusive);
+  // bx < 0: none
+  int bx, by, bz, pad;
 };
 struct TB2Args {
   int n;                  // items
@@ -416,6 +420,13 @@ constexpr int DFT_KB = 16;
 constexpr int DFT_FT = 16;  // frequency tile of the accumulation
 int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch, double *fr,
                  long long npts, const DevGrid &g, const DevFields &f, void *stream);
+// sampling plan of one flux object (per point: 4 int32 Yee indices, a 16-bit selector; see
+// dft_plan_kernel), then the sample of one update through it
+int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
+               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel,
+               void *stream);
+int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const double *pw, double *fr,
+                      long long npts, const DevFields &f, void *stream);
 int k_dft_accum(const int *pj, const int *pch, double *dft, const double *fr, int n,
                 const double *ph, long long rstride, int nfreq, long long npts, void *stream);
 int k_init_add(double *dst, double *alt, const double *src, const DevGrid &g, const DevFields &f,

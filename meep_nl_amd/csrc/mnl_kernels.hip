@@ -3562,6 +3562,10 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
   const bool own = gx >= x0 && gx <= x1 && gy >= y0 && gy <= y1;
   const bool bxy = own && (((faces & 1) && gx == x0) || ((faces & 2) && gx == x1) ||
                            ((faces & 4) && gy == y0) || ((faces & 8) && gy == y1));
+  // DFT monitor box: step n+1 of these points is stored too (it.bx < 0: none)
+  const bool dxy = own && it.bx >= 0 && gx >= (it.bx & 0xFFFF) && gx <= (it.bx >> 16) &&
+                   gy >= (it.by & 0xFFFF) && gy <= (it.by >> 16);
+  const int dz0 = it.bz & 0xFFFF, dz1 = it.bz >> 16;
   const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
   // output arrays as scalar pointers; a buffer descriptor is built at each store (a
   // descriptor per array live across the loop would overflow the SGPRs)
@@ -3675,7 +3679,8 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
     if (HAS_U) Ex = Dx * uk0, Ey = Dy * uk1, Ez = Dz * uk2;
     {  // step-n+1 values of the points on a face bordering the rim (read by rim step n+1)
       const bool kin = k >= zs && k < ze;
-      const bool bd = kin && (bxy || (own && (((faces & 16) && k == zs) || ((faces & 32) && k == ze - 1))));
+      const bool bd = kin && (bxy || (own && (((faces & 16) && k == zs) || ((faces & 32) && k == ze - 1))) ||
+                              (dxy && k >= dz0 && k <= dz1));
       const unsigned ob = bd ? col + (unsigned)k * s2 : MNL_OOB;
       bst(brsrc_at(pBm0, nrec), ob, Bx);
       bst(brsrc_at(pBm1, nrec), ob, By);
@@ -3988,6 +3993,119 @@ __global__ void dft_sample_kernel(const int *__restrict__ pj, const double *__re
     fr = pw[p] * val(P);
   }
   fr_out[p] = fr;
+}
+
+// Sampling plan (built once per fused-mode epoch): per point the linear indices of the 1-4
+// Yee values its centred average reads and, per value, where it lives (0 stored E, 1 implicit
+// E = D * chi1inv, 2 B (H == B), 3 separate H) -- the per-point table lookups of
+// dft_sample_kernel (PML flags, ownership, fused box) done once, so that the per-step sample
+// is one metadata load and independent value loads.  sel: bits 0-1 component direction,
+// 2-3 avgmode, 4 + 2v: kind of value v; 0xFFFF: another rank's point.
+__global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restrict__ pch,
+                                const DftChunkDev *__restrict__ ch, long long npts, DevGrid g,
+                                DevFields f, int4 *__restrict__ sidx,
+                                unsigned short *__restrict__ ssel) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npts) return;
+  if (pj[3 * p] < 0) {
+    ssel[p] = 0xFFFF;
+    sidx[p] = make_int4(0, 0, 0, 0);
+    return;
+  }
+  const DftChunkDev cd = ch[pch[p]];
+  const int c = cd.c, d = c % 3;
+  const bool mag = c >= 3;
+  Pt P;
+  P.idx = 0;
+  for (int e = 0; e < 3; e++) {
+    P.j[e] = pj[3 * p + e];
+    P.idx += (long long)P.j[e] * g.sdir[e];
+  }
+  auto kind = [&](const Pt &q) -> unsigned {
+    if (mag) return (f.H[d] && (f.hall || pml_at(f, g, d, qcoord(g, q, T_H, d, d)))) ? 3u : 2u;
+    return e_implicit(f, g, d, q) ? 1u : 0u;
+  };
+  auto nb = [&](const Pt &q, int e) {
+    Pt r = q;
+    r.j[e] += 1;
+    r.idx += g.sdir[e];
+    return r;
+  };
+  Pt q[4] = {P, P, P, P};
+  int nv = 1;
+  if (cd.avgmode == 2) {
+    q[1] = nb(P, cd.d1), q[2] = nb(P, cd.d2), q[3] = nb(q[1], cd.d2);
+    nv = 4;
+  } else if (cd.avgmode == 1) {
+    q[1] = nb(P, cd.d1);
+    nv = 2;
+  }
+  unsigned sel = (unsigned)d | ((unsigned)cd.avgmode << 2);
+  int idx[4] = {0, 0, 0, 0};
+  for (int v = 0; v < nv; v++) {
+    sel |= kind(q[v]) << (4 + 2 * v);
+    idx[v] = (int)q[v].idx;
+  }
+  ssel[p] = (unsigned short)sel;
+  sidx[p] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+}
+
+struct DftSrc {  // the current buffer set: E, D, chi1inv, B, H per direction
+  const double *E[3], *D[3], *U[3], *B[3], *H[3];
+};
+
+__device__ __forceinline__ double dft_val(const DftSrc &s, int d, unsigned k, int i) {
+  if (k == 0) return s.E[d][i];
+  if (k == 1) return s.U[d] ? s.D[d][i] * s.U[d][i] : s.D[d][i];
+  return k == 2 ? s.B[d][i] : s.H[d][i];
+}
+
+// fields::update_dfts' sample of one update (src/dft.cpp:265-300): the reference's centred
+// average (w * 0.25) * (((f0 + f1) + f2) + f3) through the plan
+__global__ void dft_sample_plan_kernel(const int4 *__restrict__ sidx,
+                                       const unsigned short *__restrict__ ssel,
+                                       const double *__restrict__ pw, double *__restrict__ fr_out,
+                                       long long npts, DftSrc s) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npts) return;
+  const unsigned sel = ssel[p];
+  if (sel == 0xFFFFu) return;  // another rank's point
+  const int4 ix = sidx[p];
+  const double w = pw[p];
+  const int d = sel & 3, mode = (sel >> 2) & 3;
+  const double v0 = dft_val(s, d, (sel >> 4) & 3, ix.x);
+  double fr;
+  if (mode == 2) {
+    const double v1 = dft_val(s, d, (sel >> 6) & 3, ix.y);
+    const double v2 = dft_val(s, d, (sel >> 8) & 3, ix.z);
+    const double v3 = dft_val(s, d, (sel >> 10) & 3, ix.w);
+    fr = w * (v0 + v1 + v2 + v3);
+  } else if (mode == 1) {
+    fr = w * (v0 + dft_val(s, d, (sel >> 6) & 3, ix.y));
+  } else {
+    fr = w * v0;
+  }
+  fr_out[p] = fr;
+}
+
+int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
+               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel,
+               void *stream) {
+  if (npts <= 0) return 0;
+  dft_plan_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      pj, pch, ch, npts, g, f, (int4 *)sidx, ssel);
+  return rc();
+}
+
+int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const double *pw, double *fr,
+                      long long npts, const DevFields &f, void *stream) {
+  if (npts <= 0) return 0;
+  DftSrc s;
+  for (int d = 0; d < 3; d++)
+    s.E[d] = f.E[d], s.D[d] = f.D[d], s.U[d] = f.inveps[d], s.B[d] = f.B[d], s.H[d] = f.H[d];
+  dft_sample_plan_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const int4 *)sidx, ssel, pw, fr, npts, s);
+  return rc();
 }
 
 // Accumulation: one thread per point; a tile of DFT_FT frequencies is loaded

@@ -160,3 +160,28 @@ def test_tb_slabs(group):
 def test_tb_slabs_equal_one_step():
     kw = dict(sizes=(9.6, 6.4, 9.6), steps=(1, 7, 2, 1, 6))
     _same(sc_tb(GroupSim3, **kw), sc_tb(GroupSim3, tb=False, **kw))
+
+
+def test_tb_dft_flux():
+    """DFT flux monitors with pairs of steps: the middle step is sampled from the mid set
+    (the two-step items store step n+1 of the points the samples average), the second from
+    the new state; every per-point DFT value bitwise the oracle's (src/dft.cpp:249-300)."""
+    from scenarios import sc_flux_3d
+    from test_gpu_dft import _same_dft
+    kw = dict(sizes=[9.6, 6.4, 8.0], steps=24)
+    p, hs = sc_flux_3d(ProductSim, **kw)
+    assert p._fields().tb_info()["active"]
+    o, _ = sc_flux_3d(make_oracle, **kw)
+    _same_dft(p, o, hs)
+
+
+def test_tb_dft_fields():
+    """DFT field monitors (whole-cell components, boxes across PML chunks, planes, lines)
+    with pairs of steps: bitwise the oracle."""
+    from scenarios import sc_dft_fields_3d
+    from test_gpu_dft_fields import _same as same_fields
+    kw = dict(sizes=[9.6, 6.4, 8.0], steps=20)
+    p, objs = sc_dft_fields_3d(ProductSim, **kw)
+    assert p._fields().tb_info()["active"]
+    o, _ = sc_dft_fields_3d(make_oracle, **kw)
+    same_fields(p, o, objs)
