@@ -282,6 +282,18 @@ def measure_extra(workload, size, steps, warmup, tune=True):
                      "e_update_ms_per_step": round(e_ms / max(e_n, 1), 4),
                      "nr_random_fallbacks": f.nr_fallbacks(),
                      "bound": "latency/compute (per-voxel 3x3 Newton iterations), not HBM"}
+    if f.fused_active():  # per-step time of each launch family: which one dominates
+        parts = {}
+        for name, kind in (("fused_tile_kernel", 0),
+                           ("fused_general_kernel (polarization chunks)", 2),
+                           ("E phase (kerr_nr: NR box update_e_kernel<NR> + nr_hard + "
+                            "update_pols)", 4)):
+            n, ms, _ = f.kernel_stats(kind)
+            if n:
+                parts[name] = round(ms / n, 4)
+        if parts:
+            out["step_breakdown_ms"] = parts
+            out["roofline"]["dominant_kernel"] = max(parts, key=parts.get)
     del f, s
     gc.collect()
     return out

@@ -248,6 +248,10 @@ struct mnl_fields {
   bool nr_shell_free = false;  // the chi2 box lies inside the interior: plain shell E kernels
   Box nr_in{};
   std::vector<Box> nr_rest;
+  Box nr_chi2{};  // bounding box of chi2 != 0 (device coordinates; empty: lo > hi)
+  // fused mode with chi(2): the chi2 box grown by one point, whose E / P the fused
+  // kernels leave to the NR E kernel (nr_fused_e); empty: no NR point anywhere
+  Box nr_xbox{};
   std::vector<Box> shell;
   BoxList shell_list;
   // fused mode (DESIGN.md "Fused step")
@@ -263,8 +267,18 @@ struct mnl_fields {
   // polarization chunks (lean + PML bodies), the general kernel over those chunks only
   bool tile_mode = true;
   bool tile_zcut = true;      // cut z chunks at the lean box's z range (short z-PML items)
-  int last_no_ownc = 0;       // MNL_NO_OWNC seen by the last batch (A/B: rebuild on change)
   int tile_body_mask = -1;   // MNL_TILE_BODY_MASK: step only these bodies (timing experiments)
+  // diagnostic / A-B switches, read once when the fields are created (mnl_fields_create)
+  bool ownc = true;           // MNL_NO_OWNC=1: no OWNC item flag
+  bool lean_halo = true;      // MNL_LEAN_HALO=0: general tiles recompute the lean halo
+  bool no_palette = false;    // MNL_NO_PALETTE=1: per-cell chi1inv loads, no byte palette
+  bool uniform = true;        // MNL_UNIFORM=0: per-cell palette loads in uniform items too
+  int lean_groups = 1, gen_groups = 1;  // MNL_LEAN_GROUPS / MNL_GEN_GROUPS: 1 or 8 queues
+  bool tile_gen_cus_env = false;        // MNL_TILE_GEN_CUS given (the tuner keeps it)
+  bool fused_zchunk_env = false;        // MNL_FUSED_ZCHUNK given (the tuner keeps it)
+  bool tb_env = false, tb_zchunk_env = false;  // MNL_TB / MNL_TB_ZCHUNK given (the same)
+  bool nr_defer = true;       // MNL_NR_DEFER=0: every NR problem solved in place
+  bool tile_stats = false, tb_stats = false;  // MNL_TILE_STATS / MNL_TB_STATS: print
   std::vector<int> titems;   // tile-kernel items (FusedArgs::titems)
   int *d_titems = nullptr;
   size_t d_titems_cap = 0;
@@ -2318,11 +2332,8 @@ static void split_range(std::vector<int> &b, int lo, int hi_excl, int step, int 
 }
 
 // general tiles read the lean kernel's B_new on their halo (default); MNL_LEAN_HALO=0
-// recomputes it (in-process A/B: read per step)
-static int lean_halo_reads() {
-  const char *e = getenv("MNL_LEAN_HALO");
-  return e && e[0] == '0' ? 0 : 1;
-}
+// recomputes it
+static int lean_halo_reads(const mnl_fields *F) { return F->lean_halo ? 1 : 0; }
 
 // Tile mode.  Tiles of the lean body's shape over all of G:
 // columns in pieces of <= 64 from G.lo (128-byte aligned), rows in balanced pieces of
@@ -2366,7 +2377,7 @@ int tile_item_code(const mnl_fields *F, const FusedArgs &a, const Box &L, int x0
     body = m == 1 ? 1 : m == 2 ? 2 : m == 4 ? 3 : m == 0 ? 4 : m == 3 ? 6 : m == 5 ? 7 : 5;
   }
   int ownc = 0;
-  if (body >= 1 && body <= 3 && !F->last_no_ownc) {
+  if (body >= 1 && body <= 3 && F->ownc) {
     const int ylo = std::max(a.osh_lo[1], a.oun_lo[1]), yhi = std::min(a.osh_hi[1], a.oun_hi[1]);
     const int zlo = std::max(a.osh_lo[2], a.oun_lo[2]), zhi = std::min(a.osh_hi[2], a.oun_hi[2]);
     ownc = (y0 >= ylo && y0 + 15 <= yhi && zs - 1 >= zlo && ze <= zhi && y0 + 15 <= g.N[1] - 1 &&
@@ -2533,7 +2544,7 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
   };
   longest_first(heavy);
   longest_first(lean);
-  if (getenv("MNL_TILE_STATS")) {  // per-body item / cell counts (diagnostics)
+  if (F->tile_stats) {  // per-body item / cell counts (diagnostics)
     long long ni[8] = {0}, nc[8] = {0};
     for (auto *v : {&early, &heavy, &lean})
       for (int it : *v) {
@@ -2862,8 +2873,40 @@ bool in_fused_box(const mnl_fields *F, int c, const int jg[3]) {
   return !(F->S.has[d] && F->h_flag[d][q]);
 }
 
+int nr_split(mnl_fields *F);
+
+// chi(2) Newton-Raphson in the fused mode (one rank): the fused kernels store D everywhere
+// and leave E and P of the chi2 box grown by one point (the NR neighbour reads of D - P,
+// src/step_generic.cpp:740-743, stay inside it) to the NR E kernel; that box must lie in the
+// interior (no PML, no wall plane) and inside the polarization box, where the fused
+// kernels store E (elsewhere E is implicit and the NR kernel's stores would be lost)
+bool nr_fused_ok(mnl_fields *F) {
+  if (F->nranks > 1 || F->f.npol == 0) return false;
+  if (nr_split(F)) return false;
+  Box &x = F->nr_xbox;
+  const Box &c = F->nr_chi2;
+  if (c.hi[0] < c.lo[0] || c.hi[1] < c.lo[1] || c.hi[2] < c.lo[2]) {  // no chi2 point
+    for (int k = 0; k < 3; k++) x.lo[k] = 1, x.hi[k] = 0;
+    return true;
+  }
+  Box p;
+  for (int k = 0; k < 3; k++) p.lo[k] = INT32_MAX, p.hi[k] = -1;
+  for (int q = 0; q < F->f.npol; q++)
+    for (int k = 0; k < 3; k++) {
+      p.lo[k] = std::min(p.lo[k], F->f.pol[q].nz.lo[k]);
+      p.hi[k] = std::max(p.hi[k], F->f.pol[q].nz.hi[k]);
+    }
+  for (int k = 0; k < 3; k++) {
+    x.lo[k] = c.lo[k] - 1, x.hi[k] = c.hi[k] + 1;
+    if (x.lo[k] < F->interior.lo[k] || x.hi[k] > F->interior.hi[k]) return false;
+    if (x.lo[k] < p.lo[k] || x.hi[k] > p.hi[k]) return false;
+  }
+  return true;
+}
+
 bool fused_possible(mnl_fields *F) {
-  if (!F->allow_fused || F->S.dim != 3 || F->nr || F->upnl || F->f.aniso || F->hall) return false;
+  if (!F->allow_fused || F->S.dim != 3 || F->upnl || F->f.aniso || F->hall) return false;
+  if (F->nr && !nr_fused_ok(F)) return false;
   for (int t = 0; t < 2; t++)
     for (int d = 0; d < 3; d++)
       if (F->f.cnd[t][d]) return false;
@@ -2950,8 +2993,7 @@ int build_palette(mnl_fields *F) {
   const mnl_structure &S = F->S;
   DevFields &f = F->f;
   if (!f.inveps[0] || !f.inveps[1] || !f.inveps[2]) return 0;
-  if (const char *np = getenv("MNL_NO_PALETTE"))
-    if (atoi(np)) return 0;
+  if (F->no_palette) return 0;
   std::vector<double> tab(3 * 256, 0.0);
   int n[3];
   for (int c = 0; c < 3; c++) {
@@ -3110,6 +3152,8 @@ FusedArgs &fused_args(mnl_fields *F) {
       fa.pbox.lo[e] = std::min(fa.pbox.lo[e], f.pol[k].nz.lo[e]);
       fa.pbox.hi[e] = std::max(fa.pbox.hi[e], f.pol[k].nz.hi[e]);
     }
+  for (int e = 0; e < 3; e++) fa.xbox.lo[e] = 1, fa.xbox.hi[e] = 0;
+  if (F->nr) fa.xbox = F->nr_xbox;
   fa.gitems = F->d_gitems;
   fa.titems = F->d_titems;
   fa.tflag = nullptr;
@@ -3117,8 +3161,7 @@ FusedArgs &fused_args(mnl_fields *F) {
   fa.utab = F->d_utab;
   fa.uflag = nullptr;
   fa.gflag = nullptr;
-  const char *ue = getenv("MNL_UNIFORM");  // 0: per-cell palette loads everywhere (A/B)
-  if (F->d_uidx && !(ue && ue[0] == '0')) {
+  if (F->d_uidx && F->uniform) {
     // flags of the current tile / chunk geometry (rebuilt if make_fused_boxes changed it)
     unsigned long long sig = 1469598103934665603ULL;
     auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
@@ -3198,10 +3241,8 @@ FusedArgs &fused_args(mnl_fields *F) {
   }
   F->uflag_active = fa.uflag || fa.gflag || fa.tflag;
   fa.ctr = F->d_fused_ctr;
-  fa.ngrp = 1;  // lean queue groups (MNL_LEAN_GROUPS); general: MNL_GEN_GROUPS
-  if (const char *e = getenv("MNL_LEAN_GROUPS")) fa.ngrp = atoi(e) == 8 ? 8 : 1;
-  fa.ngrp_gen = 1;
-  if (const char *e = getenv("MNL_GEN_GROUPS")) fa.ngrp_gen = atoi(e) == 8 ? 8 : 1;
+  fa.ngrp = F->lean_groups;  // lean queue groups; general: gen_groups
+  fa.ngrp_gen = F->gen_groups;
   return fa;
 }
 
@@ -3213,17 +3254,12 @@ int fused_fail(const char *what, int kr) {
 // CUs given to the general kernel when it runs beside the lean one: its share
 // of the step's work (general tile-planes cost ~2.5x a lean cell's bandwidth
 // time per cell), or MNL_GEN_CUS; 0 = run the two kernels one after the other
-int gen_split(const mnl_fields *F) {
-  if (const char *e = getenv("MNL_GEN_CUS_STEP")) return std::max(0, atoi(e));  // A/B per step
-  if (F->gen_cus >= 0) return F->gen_cus;
-  return 0;
-}
+int gen_split(const mnl_fields *F) { return F->gen_cus >= 0 ? F->gen_cus : 0; }
 
 // tile mode, one rank: CUs of the polarization chunks' general kernel beside the tile
-// kernel (0: after it on the same stream).  MNL_TILE_GEN_CUS: read every batch (A/B).
+// kernel (0: after it on the same stream; the tuner's choice, or MNL_TILE_GEN_CUS)
 int tile_gen_split(const mnl_fields *F) {
-  int v = F->tile_gen_cus;
-  if (const char *e = getenv("MNL_TILE_GEN_CUS")) v = atoi(e);
+  const int v = F->tile_gen_cus;
   const int cus = k_cu_count();
   return (v > 0 && v < cus) ? v : 0;
 }
@@ -3273,7 +3309,7 @@ int step_fused_multi(mnl_fields *F, const SrcDev &sD, EB &ev_begin, EE &ev_end) 
   ev_end(k);
   if (!F->tile_mode || fa.ngen > fa.ngen_e) {
     k = ev_begin(TM_GEN);
-    fa.lean_after = F->tile_mode ? 0 : lean_halo_reads();  // same stream, after the lean launch
+    fa.lean_after = F->tile_mode ? 0 : lean_halo_reads(F);  // same stream, after the lean launch
     kr = k_fused(fa, 3, F->stream, F->ctr_base);
     fa.lean_after = 0;
     if (kr) return fused_fail("fused general kernel launch failed", kr);
@@ -3360,7 +3396,7 @@ int update_h_any(mnl_fields *F, const BoxList &sl, bool pols) {
 // Interior E update with chi(2) Newton-Raphson: the NR kernel over the bounding
 // box of chi2 != 0 inside the interior, the plain kernel over the rest (outside
 // that box chi2 = 0, so every point takes E = chi1inv * (D - P) either way).
-int nr_interior_e(mnl_fields *F, const ISrcDev &is) {
+int nr_split(mnl_fields *F) {
   const DevGrid &g = F->g;
   if (!F->nr_split_done) {
     int *d = nullptr;
@@ -3376,6 +3412,7 @@ int nr_interior_e(mnl_fields *F, const ISrcDev &is) {
     Box n;
     bool empty = false;
     F->nr_shell_free = true;  // chi2 != 0 nowhere outside the interior box
+    for (int k = 0; k < 3; k++) F->nr_chi2.lo[k] = box[k], F->nr_chi2.hi[k] = box[3 + k];
     for (int k = 0; k < 3; k++) {  // 3-D: device axis k == direction k
       n.lo[k] = std::max(box[k], I.lo[k]);
       n.hi[k] = std::min(box[3 + k], I.hi[k]);
@@ -3406,6 +3443,12 @@ int nr_interior_e(mnl_fields *F, const ISrcDev &is) {
     }
     F->nr_split_done = true;
   }
+  return 0;
+}
+
+int nr_interior_e(mnl_fields *F, const ISrcDev &is) {
+  const DevGrid &g = F->g;
+  if (nr_split(F)) return -1;
   if (F->nr_in.hi[0] >= F->nr_in.lo[0] &&
       k_update_e(F->nr_in, nullptr, g, F->f, is, 0, false, F->stream))
     return fail("update E launch failed");
@@ -3422,14 +3465,29 @@ constexpr int NR_HARD_CAP = 4096;  // deferred NR problems per E update (more: s
 // every problem in place, sequentially) and clear the list; after it, the parallel pass.
 int nr_defer_begin(mnl_fields *F) {
   if (!F->d_nr_hard) return 0;
-  const char *e = getenv("MNL_NR_DEFER");
-  F->f.nr_hard = (e && e[0] == '0') ? nullptr : F->d_nr_hard;
+  F->f.nr_hard = F->nr_defer ? F->d_nr_hard : nullptr;
   if (F->f.nr_hard) HIPCHK(hipMemsetAsync(F->d_nr_hard_cnt, 0, sizeof(unsigned), F->stream));
   return 0;
 }
 int nr_defer_end(mnl_fields *F) {
   if (!F->f.nr_hard) return 0;
   if (k_nr_hard(F->f, F->stream)) return fail("NR parallel-attempt kernel launch failed");
+  return 0;
+}
+
+// Fused mode with chi(2) (nr_fused_ok): the fused kernels stored the new D (Dn) everywhere
+// and E / P everywhere but the chi2 box grown by one point; here that box: E by the NR
+// kernel (Newton-Raphson where chi2 != 0, chi1inv * (D - P) at the other points, the
+// values the fused kernels would have stored), then update_P over it, as the unfused
+// NR path orders them (src/step_generic.cpp:730-816, src/susceptibility.cpp:251-258)
+int nr_fused_e(mnl_fields *F, const ISrcDev &is) {
+  const Box &x = F->nr_xbox;
+  if (x.hi[0] < x.lo[0]) return 0;
+  if (nr_defer_begin(F)) return -1;
+  if (k_update_e(x, nullptr, F->g, F->f, is, 0, false, F->stream))
+    return fail("update E launch failed");
+  if (nr_defer_end(F)) return -1;
+  if (k_update_pols(x, nullptr, F->g, F->f, F->stream)) return fail("pols launch failed");
   return 0;
 }
 
@@ -3881,7 +3939,7 @@ int tb_plan(mnl_fields *F) {
   }
   HIPCHK(hipStreamSynchronize(F->stream));
   F->tb_have = ni > 0 || (F->nranks > 1 && nr > 0);
-  if (getenv("MNL_TB_STATS"))
+  if (F->tb_stats)
     fprintf(stderr, "tb: L2 [%d..%d]x[%d..%d]x[%d..%d], %zu holes, %zu two-step boxes, %zu rim "
             "boxes; %d two-step items (%d planes, %.0f cells, %.0f border), %d rim items "
             "(%.0f cells, %.0f lean); inner %zu, outer %zu\n",
@@ -4195,37 +4253,6 @@ int tb_chain_join(mnl_fields *F) {
 
 int step_batch(mnl_fields *F, int nsteps) {
   if (F->src_dirty && build_source_lists(F)) return -1;
-  // in-process A/B of the fused geometry (tools/ab_inproc.py): MNL_TILE_STEP /
-  // MNL_ZCHUNK_STEP change the mode / chunk length between batches (leaving fused mode
-  // first, so the next entry rebuilds and uploads the items)
-  if (const char *e = getenv("MNL_TILE_STEP")) {
-    const bool want = atoi(e) != 0;
-    if (want != F->tile_mode) {
-      if (F->fused && set_fused(F, false)) return -1;
-      F->tile_mode = want;
-    }
-  }
-  if (const char *e = getenv("MNL_ZCUT_STEP")) {
-    const bool want = atoi(e) != 0;
-    if (want != F->tile_zcut) {
-      if (F->fused && set_fused(F, false)) return -1;
-      F->tile_zcut = want;
-    }
-  }
-  if (const char *e = getenv("MNL_NO_OWNC")) {  // in-process A/B of the OWNC item flag
-    const int want = atoi(e) != 0;
-    if (want != F->last_no_ownc) {
-      if (F->fused && set_fused(F, false)) return -1;
-      F->last_no_ownc = want;
-    }
-  }
-  if (const char *e = getenv("MNL_ZCHUNK_STEP")) {
-    const int want = std::max(0, atoi(e));
-    if (want != F->fused_zchunk) {
-      if (F->fused && set_fused(F, false)) return -1;
-      F->fused_zchunk = want;
-    }
-  }
   if (set_fused(F, fused_agreed(F))) return -1;
   {  // does a D source point lie in the shell (outside the box the interior kernels own)?
     const Box &ib = F->fused ? F->fusedG : F->interior;
@@ -4440,7 +4467,7 @@ int step_batch(mnl_fields *F, int nsteps) {
             k = ev_next(k, TM_GEN);
             // lean mode: same stream, after the lean launch (tile mode: the general
             // items are polarization chunks, whose halos no lean launch stores)
-            fa.lean_after = F->tile_mode ? 0 : lean_halo_reads();
+            fa.lean_after = F->tile_mode ? 0 : lean_halo_reads(F);
             kr = k_fused(fa, 1, F->stream, F->ctr_base);
             fa.lean_after = 0;
             if (kr) return fused_fail("fused general kernel launch failed", kr);
@@ -4491,39 +4518,45 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       // ---- E (+ Lorentzian P)
       if (!F->e_first_done && e_lazy_copy(F)) return -1;
-      // neighbour reads of D - P (NR, upstream chi) or of W (anisotropic sigma):
-      // P after all of E
-      bool fuse = !F->nr && !F->upnl && !f.aniso;
-      k = (!F->fused || (!fuseE && shell_work) || (!fuse && f.npol) || f.aniso || f.wall_e)
-              ? ev_begin(TM_E)
-              : -1;
-      if (nr_defer_begin(F)) return -1;
-      if (!F->fused && F->nr && F->S.dim == 3) {
-        if (nr_interior_e(F, is)) return -1;
-      } else if (!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) {
-        return fail("update E launch failed");
-      }
-      if (!fuseE) {
-        // no chi2 outside the interior: the shell boxes never take the NR branch, so
-        // they run the plain E kernel (same values, without the NR kernel's registers)
-        DevFields plain = f;
-        if (F->nr && F->nr_split_done && F->nr_shell_free) plain.nr_enabled = 0;
-        if (k_update_e(F->interior, sl, g, plain, is, 0, fuse, F->stream))
+      if (F->fused && F->nr) {  // one rank: the fused kernels did all but the NR box
+        k = ev_begin(TM_E);
+        if (nr_fused_e(F, is)) return -1;
+        ev_end(k);
+      } else {
+        // neighbour reads of D - P (NR, upstream chi) or of W (anisotropic sigma):
+        // P after all of E
+        bool fuse = !F->nr && !F->upnl && !f.aniso;
+        k = (!F->fused || (!fuseE && shell_work) || (!fuse && f.npol) || f.aniso || f.wall_e)
+                ? ev_begin(TM_E)
+                : -1;
+        if (nr_defer_begin(F)) return -1;
+        if (!F->fused && F->nr && F->S.dim == 3) {
+          if (nr_interior_e(F, is)) return -1;
+        } else if (!F->fused && k_update_e(F->interior, nullptr, g, f, is, 0, fuse, F->stream)) {
           return fail("update E launch failed");
+        }
+        if (!fuseE) {
+          // no chi2 outside the interior: the shell boxes never take the NR branch, so
+          // they run the plain E kernel (same values, without the NR kernel's registers)
+          DevFields plain = f;
+          if (F->nr && F->nr_split_done && F->nr_shell_free) plain.nr_enabled = 0;
+          if (k_update_e(F->interior, sl, g, plain, is, 0, fuse, F->stream))
+            return fail("update E launch failed");
+        }
+        if (nr_defer_end(F)) return -1;
+        if (f.aniso && !f.wall_e && k_aniso_wall(g, f, 0, F->stream))
+          return fail("wall W launch failed");
+        if (f.aniso && F->nranks > 1 && exchange(F, 4))  // WE_stuff ghosts (step.cpp:111-114)
+          return fail("W halo exchange failed");
+        if (!fuse && f.npol) {
+          if (k_update_pols(F->interior, nullptr, g, f, F->stream) ||
+              k_update_pols(F->interior, sl, g, f, F->stream))
+            return fail("pols launch failed");
+        }
+        if ((f.aniso || f.wall_e) && k_aniso_wall(g, f, 1, F->stream))
+          return fail("wall W launch failed");
+        ev_end(k);
       }
-      if (nr_defer_end(F)) return -1;
-      if (f.aniso && !f.wall_e && k_aniso_wall(g, f, 0, F->stream))
-        return fail("wall W launch failed");
-      if (f.aniso && F->nranks > 1 && exchange(F, 4))  // WE_stuff ghosts (step.cpp:111-114)
-        return fail("W halo exchange failed");
-      if (!fuse && f.npol) {
-        if (k_update_pols(F->interior, nullptr, g, f, F->stream) ||
-            k_update_pols(F->interior, sl, g, f, F->stream))
-          return fail("pols launch failed");
-      }
-      if ((f.aniso || f.wall_e) && k_aniso_wall(g, f, 1, F->stream))
-        return fail("wall W launch failed");
-      ev_end(k);
       if (F->fused)
         for (int d = 0; d < 3; d++) {
           std::swap(f.B[d], f.Bn[d]);
@@ -5809,11 +5842,15 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
       return nullptr;
     }
   }
-  if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) F->fused_zchunk = std::max(0, atoi(zc));
+  if (const char *zc = getenv("MNL_FUSED_ZCHUNK")) {
+    F->fused_zchunk = std::max(0, atoi(zc));
+    F->fused_zchunk_env = true;  // the tuner keeps it
+  }
   if (const char *bp = getenv("MNL_FUSED_BPC")) F->fused_bpc = std::max(1, atoi(bp));
   if (const char *tm = getenv("MNL_TILE")) F->tile_mode = atoi(tm) != 0;
-  if (const char *tb = getenv("MNL_TB")) F->tb_enabled = atoi(tb) != 0;
-  if (const char *tz = getenv("MNL_TB_ZCHUNK")) F->tb_zchunk = std::max(0, atoi(tz));
+  if (const char *tb = getenv("MNL_TB")) F->tb_enabled = atoi(tb) != 0, F->tb_env = true;
+  if (const char *tz = getenv("MNL_TB_ZCHUNK"))
+    F->tb_zchunk = std::max(0, atoi(tz)), F->tb_zchunk_env = true;
   if (const char *ts = getenv("MNL_TB_SPLIT")) F->tb_split = atoi(ts) != 0;
   if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
@@ -5825,6 +5862,24 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *ar = getenv("MNL_ARENA")) F->arena_req = std::max(0, atoi(ar));
   if (const char *cg = getenv("MNL_CONTIG")) F->contig = atoi(cg) != 0;
   if (const char *ag = getenv("MNL_ARENA_GAP")) F->arena_gap = std::max(0, atoi(ag)) / 128 * 128;
+  auto env_is = [](const char *name, char v) {
+    const char *e = getenv(name);
+    return e && e[0] == v;
+  };
+  F->ownc = !env_is("MNL_NO_OWNC", '1');
+  F->tile_zcut = !env_is("MNL_ZCUT", '0');
+  F->lean_halo = !env_is("MNL_LEAN_HALO", '0');
+  F->no_palette = env_is("MNL_NO_PALETTE", '1');
+  F->uniform = !env_is("MNL_UNIFORM", '0');
+  F->lean_groups = env_is("MNL_LEAN_GROUPS", '8') ? 8 : 1;
+  F->gen_groups = env_is("MNL_GEN_GROUPS", '8') ? 8 : 1;
+  if (const char *e = getenv("MNL_TILE_GEN_CUS")) {
+    F->tile_gen_cus = std::max(0, atoi(e));
+    F->tile_gen_cus_env = true;
+  }
+  F->nr_defer = !env_is("MNL_NR_DEFER", '0');
+  F->tile_stats = getenv("MNL_TILE_STATS") != nullptr;
+  F->tb_stats = getenv("MNL_TB_STATS") != nullptr;
   if (finalize_fields(F.get())) return nullptr;
   return F.release();
 }
@@ -6460,7 +6515,7 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
   };
   int rc = 0;
   const int split0 = F->tile_gen_cus;
-  if (!getenv("MNL_FUSED_ZCHUNK") && !getenv("MNL_ZCHUNK_STEP")) {
+  if (!F->fused_zchunk_env) {
     static const int cand[] = {0, 16, 20, 24, 32, 48};
     F->tile_gen_cus = 0;  // the two launches one after the other while the length is chosen
     int best = F->fused_zchunk;
@@ -6481,7 +6536,7 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
     F->fused_zchunk = best;
     if (!rc && zchunk) *zchunk = best;
   }
-  if (!rc && F->nranks == 1 && !getenv("MNL_TILE_GEN_CUS")) {
+  if (!rc && F->nranks == 1 && !F->tile_gen_cus_env) {
     F->tile_gen_cus = 0;
     double tm = 0, gm = 0;
     if (timed(&tm, &gm)) rc = -1;
@@ -6518,7 +6573,7 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
     int best = tz0;
     double best_ms = 0;
     for (int c : {0, 32, 48, 64, 96, 128}) {
-      if (getenv("MNL_TB_ZCHUNK") && c != tz0) continue;
+      if (F->tb_zchunk_env && c != tz0) continue;
       F->tb_zchunk = c;
       double tm, gm;
       if (timed(&tm, &gm)) { rc = -1; break; }
@@ -6527,7 +6582,7 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
       if (best_ms == 0 || tm + gm < best_ms) best_ms = tm + gm, best = c;
     }
     F->tb_zchunk = rc ? tz0 : best;
-    if (!rc && !getenv("MNL_TB")) {
+    if (!rc && !F->tb_env) {
       F->tb_enabled = false;
       double tm, gm;
       if (timed(&tm, &gm)) rc = -1;

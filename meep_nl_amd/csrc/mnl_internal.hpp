@@ -297,7 +297,8 @@ struct FusedArgs {
   int npol;
   PolDev pol[MAX_POL];
   Box pbox;                     // union of the pols' nonzero boxes (empty: lo > hi)
-  const int *gitems;            // general items: tx | ty << 8 | ch << 16; wide, then narrow
+  Box xbox;                     // chi(2) box + 1 (inside pbox): E / P left to the NR kernel
+  const int *gitems;           // general items: tx | ty << 8 | ch << 16; wide, then narrow
   int ngen, ngen_n;             // wide / narrow item counts (chunk-major order)
   int ngen_e, ngen_ne;          // leading items of chunk 0 (the early launch of multi-rank steps)
   int gbeg, gend, ctr_line;     // set per launch by k_fused: item range and counter line

@@ -1798,6 +1798,10 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   const bool hpxy = POL && hx >= a.pbox.lo[0] && hx <= a.pbox.hi[0] && hy >= a.pbox.lo[1] &&
                     hy <= a.pbox.hi[1];
   auto pz_in = [&](int z) { return POL && z >= a.pbox.lo[2] && z <= a.pbox.hi[2]; };
+  // chi(2) Newton-Raphson box (inside pbox): E and P there are left to the NR E kernel
+  // that follows (its neighbour reads need the old P of the whole box)
+  const bool xxy = POL && gx >= a.xbox.lo[0] && gx <= a.xbox.hi[0] && gy >= a.xbox.lo[1] &&
+                   gy <= a.xbox.hi[1];
   auto ownz_of = [&](int z) -> unsigned {
     return (rng(z, a.osh_lo[2], a.osh_hi[2]) ? 1u : 0u) | (rng(z, a.oun_lo[2], a.oun_hi[2]) ? 2u : 0u);
   };
@@ -2097,7 +2101,8 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
           // src/step_generic.cpp:576-906, src/susceptibility.cpp:188-262
           const double Dn3[3] = {Dx, Dy, Dz}, Do3[3] = {dx, dy, dz}, Eo3[3] = {ex, ey, ez};
           const double kk3[3] = {k0, k1, k2};
-          const unsigned oo3[3] = {o0, o1, o2};
+          const bool xin = xxy && kl >= a.xbox.lo[2] && kl <= a.xbox.hi[2];
+          const unsigned oo3[3] = {xin ? MNL_OOB : o0, xin ? MNL_OOB : o1, xin ? MNL_OOB : o2};
           const bool w3[3] = {fxs, fys, fzs};
           const TabE tw3[3] = {tx_s, ty_s, tz_s};
           if (POL == 1) {  // one susceptibility: all loads first, one memory wait

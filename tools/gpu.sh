@@ -8,6 +8,7 @@
 #                                        rocprofv3 --kernel-trace --stats (csv) of bench.py
 #   pmc:<tag>:<COUNTER+COUNTER...>[:<bench.py args>]
 #                                        one rocprofv3 --pmc pass (counters of one pass only)
+#   py:<tag>:<script and args>           python -u <script args> -> gpurun_out/<tag>.txt
 #   smoke                                __graft_entry__.smoke()
 # Every step runs under its own time limit; a step that crashes, times out or fails stops
 # the session (pytest exit 1 = test failures: the session goes on).
@@ -59,6 +60,11 @@ run_step() {
           > "$ROOT/gpurun_out/$tag.log" 2>&1 )
       rc=$?
       echo "=== pmc $tag ($ctr) rc=$rc"
+      return $rc ;;
+    py)
+      tag=${rest%%:*}; args=${rest#"$tag"}; args=${args#:}
+      timeout -k 10 600 python -u $args > gpurun_out/$tag.txt 2>&1
+      rc=$?; echo "=== py $tag rc=$rc"; tail -n 12 gpurun_out/$tag.txt | cut -c1-300
       return $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
