@@ -202,6 +202,8 @@ struct DftFluxH {
   std::vector<DftChunkH> E, H;        // list order (next_in_dft)
   size_t npts = 0;                    // E points, then H points
   std::vector<int> h_pj;              // 3 local indices per point (-1: not this rank's)
+  Box bbox{};                         // this rank's points, +1 along every axis (dft_layout;
+                                      // empty: lo > hi)
   int *d_pj = nullptr, *d_pch = nullptr;
   double *d_pw = nullptr;             // w * 0.25 / 0.5 / 1 per point
   DftChunkDev *d_ch = nullptr;        // per chunk (E list, then H list)
@@ -216,11 +218,13 @@ struct DftFluxH {
   double bytes = 0;                   // algorithmic bytes of one update (DESIGN.md "DFT")
   void *d_sidx = nullptr;             // sampling plan (k_dft_plan): 4 int32 indices per point
   unsigned short *d_ssel = nullptr;   // ... and a selector per point
+  void *d_su = nullptr;               // ... and 4 chi1inv values (implicit E) per point
   long long plan_key = -1;            // the mode the plan was built for (dft_plan_key)
   ~DftFluxH() {
     if (d_ph) (void)hipFree(d_ph);
     if (d_sidx) (void)hipFree(d_sidx);
     if (d_ssel) (void)hipFree(d_ssel);
+    if (d_su) (void)hipFree(d_su);
   }
 };
 
@@ -279,6 +283,11 @@ struct mnl_fields {
   bool tb_env = false, tb_zchunk_env = false;  // MNL_TB / MNL_TB_ZCHUNK given (the same)
   bool nr_defer = true;       // MNL_NR_DEFER=0: every NR problem solved in place
   bool tile_stats = false, tb_stats = false;  // MNL_TILE_STATS / MNL_TB_STATS: print
+  // MNL_ITEM_CLOCK=<file>: per-item start / end records of the persistent kernels, appended
+  // to <file> after every batch (ItemClock; tools/item_clock.py)
+  std::string clk_path;
+  unsigned long long *d_clk = nullptr;
+  unsigned *d_clk_n = nullptr;
   std::vector<int> titems;   // tile-kernel items (FusedArgs::titems)
   int *d_titems = nullptr;
   size_t d_titems_cap = 0;
@@ -1895,15 +1904,16 @@ int dft_layout(mnl_fields *F, std::unique_ptr<DftFluxH> &o, DftFluxH &ho, std::v
     for (auto &dc : *L)
       o->bytes += double(dc.N) * (12 + 4 + 8 + 8.0 * (1 << dc.avgmode) + 16 +
                                   (12 + 4 + 32.0 * nfreq) / o->kb);
-  // Device slots: the points sorted by component, then z, y, x (x fastest like
+  // Device slots: the points sorted by component and chunk, then z, y, x (x fastest like
   // the field arrays), so that a wave's field reads are as contiguous as the
-  // plane's orientation allows; other ranks' points last.  Only the storage
+  // plane's orientation allows and a workgroup of the accumulation almost always holds one
+  // chunk (one phase row, staged in LDS once); other ranks' points last.  Only the storage
   // order changes -- every point keeps its own reference-order accumulation.
   std::vector<int> ord(o->npts);
   for (size_t p = 0; p < o->npts; p++) ord[p] = (int)p;
   auto key = [&](int p) {
     const int *j = &o->h_pj[3 * (size_t)p];
-    return std::make_tuple(j[0] < 0, chd[pch[p]].c, j[2], j[1], j[0], p);
+    return std::make_tuple(j[0] < 0, chd[pch[p]].c, pch[p], j[2], j[1], j[0], p);
   };
   std::sort(ord.begin(), ord.end(), [&](int a, int b) { return key(a) < key(b); });
   o->slot.assign(o->npts, 0);
@@ -1915,6 +1925,14 @@ int dft_layout(mnl_fields *F, std::unique_ptr<DftFluxH> &o, DftFluxH &ho, std::v
     for (int e = 0; e < 3; e++) spj[3 * t + e] = o->h_pj[3 * (size_t)p + e];
     spch[t] = pch[p];
     spw[t] = pwE[p];
+  }
+  for (int k = 0; k < 3; k++) o->bbox.lo[k] = INT32_MAX, o->bbox.hi[k] = -1;
+  for (size_t p = 0; p < o->npts; p++) {
+    if (o->h_pj[3 * p] < 0) continue;
+    for (int k = 0; k < 3; k++) {
+      o->bbox.lo[k] = std::min(o->bbox.lo[k], o->h_pj[3 * p + k]);
+      o->bbox.hi[k] = std::max(o->bbox.hi[k], o->h_pj[3 * p + k] + 1);
+    }
   }
   if (o->npts) {
     if (dev_alloc(F, &o->d_pj, o->h_pj.size(), false) || dev_alloc(F, &o->d_pch, o->npts, false) ||
@@ -1995,15 +2013,38 @@ int dft_prepare(mnl_fields *F, long long t0, int ns) {
     o.row = 0;
     const size_t nch = o.E.size() + o.H.size();
     std::vector<double> ph;
+    ph.reserve((size_t)ns * nch * o.nfreq * 2);
+    std::vector<cplx> pe(o.nfreq), phh(o.nfreq);
     for (int s = 0; s < ns; s++) {
       const long long t = t0 + s + 1;
       if (t % o.decim) continue;
       const double tE = t * F->dt, tH = tE - 0.5 * F->dt;  // fields::update_dfts
+      // exp(i omega t) once per frequency and time (E / H), then times each chunk's scale:
+      // the same operations as the reference's per-chunk polar(1, omega t) * scale
+      for (int i = 0; i < o.nfreq; i++) {
+        pe[i] = std::polar(1.0, o.omega[i] * tE);
+        phh[i] = std::polar(1.0, o.omega[i] * tH);
+      }
+      // chunks with the same time and the same scale (bitwise) share one row of products
+      std::vector<std::pair<std::pair<bool, cplx>, size_t>> done;
+      auto same = [](const cplx &x, const cplx &y) {
+        return memcmp(&x, &y, sizeof(cplx)) == 0;
+      };
       auto add = [&](const std::vector<DftChunkH> &L) {
         for (auto &dc : L) {
-          const double tm = ctype(dc.c) == T_H ? tH : tE;
+          const bool isH = ctype(dc.c) == T_H;
+          size_t from = SIZE_MAX;
+          for (auto &d : done)
+            if (d.first.first == isH && same(d.first.second, dc.scale)) from = d.second;
+          const size_t at = ph.size();
+          if (from != SIZE_MAX) {
+            for (int i = 0; i < 2 * o.nfreq; i++) ph.push_back(ph[from + i]);
+            continue;
+          }
+          done.push_back({{isH, dc.scale}, at});
+          const std::vector<cplx> &pt = isH ? phh : pe;
           for (int i = 0; i < o.nfreq; i++) {
-            const cplx p = std::polar(1.0, o.omega[i] * tm) * dc.scale;
+            const cplx p = pt[i] * dc.scale;
             ph.push_back(p.real());
             ph.push_back(p.imag());
           }
@@ -2062,13 +2103,14 @@ int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr) {
         if (!o.d_sidx) {
           HIPCHK(hipMalloc(&o.d_sidx, o.npts * 16));
           HIPCHK(hipMalloc(&o.d_ssel, o.npts * 2));
+          HIPCHK(hipMalloc(&o.d_su, o.npts * 32));
         }
         if (k_dft_plan(o.d_pj, o.d_pch, o.d_ch, (long long)o.npts, F->g, F->f, o.d_sidx,
-                       o.d_ssel, F->stream))
+                       o.d_ssel, o.d_su, F->stream))
           return fail("dft plan launch failed");
         o.plan_key = key;
       }
-      if (k_dft_sample_plan(o.d_sidx, o.d_ssel, o.d_pw, fr, (long long)o.npts,
+      if (k_dft_sample_plan(o.d_sidx, o.d_ssel, o.d_su, o.d_pw, fr, (long long)o.npts,
                             fields ? *fields : F->f, F->stream))
         return fail("dft sample launch failed");
     } else if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, fr, (long long)o.npts, F->g,
@@ -3241,6 +3283,7 @@ FusedArgs &fused_args(mnl_fields *F) {
   }
   F->uflag_active = fa.uflag || fa.gflag || fa.tflag;
   fa.ctr = F->d_fused_ctr;
+  fa.clk = ItemClock{F->d_clk, F->d_clk_n, F->d_clk ? CLK_CAP : 0u, 0};
   fa.ngrp = F->lean_groups;  // lean queue groups; general: gen_groups
   fa.ngrp_gen = F->gen_groups;
   return fa;
@@ -3596,18 +3639,8 @@ int tb_plan(mnl_fields *F) {
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
   // the two-step items store step n+1 there too (the middle-step sample reads the mid set)
   std::vector<Box> dbox;
-  for (auto &op : F->dfts) {
-    Box b;
-    for (int k = 0; k < 3; k++) b.lo[k] = INT32_MAX, b.hi[k] = -1;
-    for (size_t p = 0; p < op->h_pj.size() / 3; p++) {
-      if (op->h_pj[3 * p] < 0) continue;
-      for (int k = 0; k < 3; k++) {
-        b.lo[k] = std::min(b.lo[k], op->h_pj[3 * p + k]);
-        b.hi[k] = std::max(b.hi[k], op->h_pj[3 * p + k] + 1);
-      }
-    }
-    if (b.hi[0] >= 0) dbox.push_back(b);
-  }
+  for (auto &op : F->dfts)  // (built once per monitor: this runs every batch)
+    if (op->bbox.hi[0] >= 0) dbox.push_back(op->bbox);
   mix((long long)dbox.size());
   for (const Box &b : dbox)
     for (int k = 0; k < 3; k++) mix(b.lo[k]), mix(b.hi[k]);
@@ -4003,6 +4036,7 @@ FusedArgs rim_args(mnl_fields *F, const FusedArgs &fa, const Set5 &o, const Set5
   r.tgeo = F->d_tb_rgeo;
   r.tflag = F->d_uidx ? F->d_tb_rflag : nullptr;
   r.gbeg = 0, r.gend = (int)F->tb_ritems.size();
+  r.clk.kind = 1;
   return r;
 }
 
@@ -4027,6 +4061,7 @@ TB2Args tb_args(mnl_fields *F, const Set5 &o, const Set5 &m, const Set5 &n) {
   t.C = F->S.courant;
   t.ctr = F->d_fused_ctr;
   t.ctr_line = 3;
+  t.clk = ItemClock{F->d_clk, F->d_clk_n, F->d_clk ? CLK_CAP : 0u, 2};
   return t;
 }
 
@@ -4244,6 +4279,24 @@ int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begi
 
 // Before a one-step step after a multi-rank pair: the pair's last slab-face chain (top plane,
 // sources, E ghost) ran on s_comm; the one-step kernels on the main stream read its results.
+// diagnostics: append this batch's item records (rank-tagged binary, CLK_REC u64 each,
+// preceded per batch by {magic, rank, count}) to clk_path and reset the counter
+int clk_dump(mnl_fields *F) {
+  unsigned n = 0;
+  HIPCHK(hipMemcpy(&n, F->d_clk_n, sizeof n, hipMemcpyDeviceToHost));
+  n = std::min(n, CLK_CAP);
+  std::vector<unsigned long long> h((size_t)n * CLK_REC);
+  if (n) HIPCHK(hipMemcpy(h.data(), F->d_clk, h.size() * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(F->d_clk_n, 0, sizeof(unsigned)));
+  FILE *fp = fopen(F->clk_path.c_str(), "ab");
+  if (!fp) return fail("MNL_ITEM_CLOCK: cannot open " + F->clk_path);
+  const unsigned long long hd[CLK_REC] = {0x4b4c434d4e4dull, (unsigned long long)F->rank, n, 0, 0, 0, 0, 0};
+  fwrite(hd, 8, CLK_REC, fp);
+  if (n) fwrite(h.data(), 8, h.size(), fp);
+  fclose(fp);
+  return 0;
+}
+
 int tb_chain_join(mnl_fields *F) {
   if (!F->tb_chain_pending) return 0;
   F->tb_chain_pending = false;
@@ -4586,6 +4639,7 @@ int step_batch(mnl_fields *F, int nsteps) {
   F->tb_chain_pending = false;
   HIPCHK(hipStreamSynchronize(F->stream));
   HIPCHK(hipGetLastError());
+  if (F->d_clk && clk_dump(F)) return -1;
   return nan_result(F);
 }
 
@@ -5880,7 +5934,11 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   F->nr_defer = !env_is("MNL_NR_DEFER", '0');
   F->tile_stats = getenv("MNL_TILE_STATS") != nullptr;
   F->tb_stats = getenv("MNL_TB_STATS") != nullptr;
+  if (const char *ck = getenv("MNL_ITEM_CLOCK")) F->clk_path = ck;
   if (finalize_fields(F.get())) return nullptr;
+  if (!F->clk_path.empty() && (dev_alloc(F.get(), &F->d_clk, (size_t)CLK_CAP * CLK_REC) ||
+                               dev_alloc(F.get(), &F->d_clk_n, 1)))
+    return nullptr;
   return F.release();
 }
 

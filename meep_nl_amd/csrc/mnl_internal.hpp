@@ -257,6 +257,19 @@ struct FusedTab {                // per direction, indexed by global half-coordi
   const double *kps[3];          // kap + sig
   const double *siginv[3];       // 1 / (kap + sig)
 };
+// Diagnostics (MNL_ITEM_CLOCK, tools/item_clock.py): every persistent-kernel item appends
+// one record {start, end (wall clock, 100 MHz), kernel | workgroup << 8, item code, x0 | x1 << 16,
+// y0 | y1 << 16, zs | ze << 16, paired strip or -1} to rec (slot from an atomic counter n;
+// records past cap are dropped)
+struct ItemClock {
+  unsigned long long *rec;
+  unsigned *n;
+  unsigned cap;
+  int kind;  // kernel tag written into the records
+};
+constexpr int CLK_REC = 8;               // u64 per record
+constexpr unsigned CLK_CAP = 1u << 20;  // records per batch
+
 struct FusedArgs {
   Box L;              // lean box
   Box G;              // fused domain (stores only inside G)
@@ -325,6 +338,7 @@ struct FusedArgs {
   // and a second x-face strip of at most 32 columns sharing the workgroup (xb0 | xb1 << 16,
   // both strips <= 32 columns, body AX = 1) or -1
   const int *tgeo;
+  ItemClock clk;                // diagnostics: per-item start / end times (clk.rec null: off)
 };
 
 // Temporal blocking: two Yee steps per z-march over the region L2
@@ -363,6 +377,7 @@ struct TB2Args {
   unsigned long long cbase;
   int wg_limit;                 // > 0: at most this many persistent workgroups (CUs left to
                                 // the slab-face kernels of multi-rank pairs)
+  ItemClock clk;                // diagnostics: per-item start / end times (clk.rec null: off)
 };
 // NaN guard of fields::step (src/step.cpp:138-139): get_field(D_EnergyDensity, gv.center())
 // = 1/2 sum_d E_d(c) D_d(c), each value the interpolation of src/monitor.cpp:127-160 over
@@ -417,17 +432,19 @@ int k_fill(double *p, double v, size_t n, void *stream);
 // blocked over up to DFT_KB updates: sample the averaged field of one update
 // into fr, then accumulate n buffered updates (phases: n rows, rstride
 // complex values apart) into the DFT array
-constexpr int DFT_KB = 16;
-constexpr int DFT_FT = 16;  // frequency tile of the accumulation
+constexpr int DFT_KB = 32;  // updates buffered per accumulation (the DFT array is read and
+                            // written once per DFT_KB updates)
+constexpr int DFT_FT = 8;   // frequency tile of the accumulation
 int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch, double *fr,
                  long long npts, const DevGrid &g, const DevFields &f, void *stream);
-// sampling plan of one flux object (per point: 4 int32 Yee indices, a 16-bit selector; see
-// dft_plan_kernel), then the sample of one update through it
+// sampling plan of one flux object (per point: 4 int32 Yee indices, a 16-bit selector, the
+// chi1inv of its implicit-E values; see dft_plan_kernel), then the sample of one update
 int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
-               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel,
+               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel, void *su,
                void *stream);
-int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const double *pw, double *fr,
-                      long long npts, const DevFields &f, void *stream);
+int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const void *su,
+                      const double *pw, double *fr, long long npts, const DevFields &f,
+                      void *stream);
 int k_dft_accum(const int *pj, const int *pch, double *dft, const double *fr, int n,
                 const double *ph, long long rstride, int nfreq, long long npts, void *stream);
 int k_init_add(double *dst, double *alt, const double *src, const DevGrid &g, const DevFields &f,

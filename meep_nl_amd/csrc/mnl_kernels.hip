@@ -3075,6 +3075,23 @@ __device__ __forceinline__ void tile_item_body(const FusedArgs &a, int item, con
   }
 }
 
+// diagnostics (ItemClock): one record per item, written by thread 0 with vector stores
+__device__ __forceinline__ void clk_record(const ItemClock &c, unsigned long long t0, int code, int g0,
+                                        int g1, int g2, int g3) {
+  const unsigned long long t1 = wall_clock64();
+  const unsigned slot = atomicAdd(c.n, 1u);
+  if (slot >= c.cap) return;
+  unsigned long long *r = c.rec + (size_t)slot * CLK_REC;
+  r[0] = t0;
+  r[1] = t1;
+  r[2] = (unsigned long long)(unsigned)c.kind | ((unsigned long long)blockIdx.x << 8);
+  r[3] = (unsigned)code;
+  r[4] = (unsigned)g0;
+  r[5] = (unsigned)g1;
+  r[6] = (unsigned)g2;
+  r[7] = (unsigned long long)(long long)g3;
+}
+
 // own box of tile item `idx`: explicit (FusedArgs::tgeo) or tile / chunk indices
 __device__ __forceinline__ ItemGeo tile_item_geo(const FusedArgs &a, int item, int idx) {
   ItemGeo itg;
@@ -3102,7 +3119,7 @@ __device__ __forceinline__ ItemGeo tile_item_geo(const FusedArgs &a, int item, i
   return itg;
 }
 
-template <int UMODE, int DIST>
+template <int UMODE, int DIST, bool CLK>
 __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
   __shared__ double sE[3][FR + 1][FXL];
@@ -3110,22 +3127,52 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
   __shared__ PTabL sP;
   __shared__ int s_item, s_idx;
   __shared__ unsigned s_uw;
+  __shared__ unsigned long long s_t0;
   if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
     for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
   }
+  if (CLK && threadIdx.x == 0) s_t0 = 0ull;  // no previous item
   const long long n = a.gend - a.gbeg;
   unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
   for (;;) {
     if (threadIdx.x == 0) {
+      // diagnostics (MNL_ITEM_CLOCK): the previous item of this workgroup ends when wave 0
+      // comes back for the next one (its last plane barrier has passed)
+      if (CLK && s_t0 != 0ull) {
+        const ItemGeo g = tile_item_geo(a, s_item, s_idx);
+        clk_record(a.clk, s_t0, s_item, g.x0 | (g.x1 << 16), (g.y0 + 1) | (g.y1 << 16),
+                   g.zs | (g.ze << 16), g.xb0 >= 0 ? (g.xb0 | (g.xb1 << 16)) : -1);
+      }
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
       s_item = (long long)v < n ? a.titems[a.gbeg + v] : -1;
       s_idx = a.gbeg + (int)v;
       s_uw = ((long long)v < n && UMODE == 2 && a.tflag) ? a.tflag[a.gbeg + v] : ~0u;
+      if (CLK) s_t0 = wall_clock64();
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
     if (item == -1) break;
     tile_item_body<UMODE, DIST>(a, item, tile_item_geo(a, item, s_idx), s_uw, sU, sE, sB, sP);
+  }
+}
+
+// the tile kernel for palette mode um (2 palette, 1 f64 chi1inv, 0 none); the diagnostics
+// build when the item clock is on
+void launch_tile(const FusedArgs &t, int um, dim3 grd, hipStream_t s) {
+  const dim3 blk(1024);
+  if (t.clk.rec) {
+    if (um == 2)
+      fused_tile_kernel<2, 1, true><<<grd, blk, 0, s>>>(t);
+    else if (um == 1)
+      fused_tile_kernel<1, 1, true><<<grd, blk, 0, s>>>(t);
+    else
+      fused_tile_kernel<0, 1, true><<<grd, blk, 0, s>>>(t);
+  } else if (um == 2) {
+    fused_tile_kernel<2, 1, false><<<grd, blk, 0, s>>>(t);
+  } else if (um == 1) {
+    fused_tile_kernel<1, 1, false><<<grd, blk, 0, s>>>(t);
+  } else {
+    fused_tile_kernel<0, 1, false><<<grd, blk, 0, s>>>(t);
   }
 }
 
@@ -3408,13 +3455,7 @@ int k_fused(const FusedArgs &a, int which, void *stream, unsigned long long *bas
     bases[line] += (unsigned long long)(ie - ib) + nb;
     const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grd((unsigned)nb), blk(1024);
-    if (um == 2)
-      fused_tile_kernel<2, 1><<<grd, blk, 0, s>>>(t);
-    else if (um == 1)
-      fused_tile_kernel<1, 1><<<grd, blk, 0, s>>>(t);
-    else
-      fused_tile_kernel<0, 1><<<grd, blk, 0, s>>>(t);
+    launch_tile(t, um, dim3((unsigned)nb), s);
     return hipPeekAtLastError() == hipSuccess ? 0 : 9;
   }
   if (a.nx < 1 || a.nx > FUSED_MAXX || a.ny < 0 || a.ny > FUSED_MAXY || a.nch < 1 ||
@@ -3517,13 +3558,7 @@ int k_tile_items(const FusedArgs &a, const int *items, const int *geo, const uns
   bases[line] += (unsigned long long)n + nb;
   const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grd((unsigned)nb), blk(1024);
-  if (um == 2)
-    fused_tile_kernel<2, 1><<<grd, blk, 0, s>>>(t);
-  else if (um == 1)
-    fused_tile_kernel<1, 1><<<grd, blk, 0, s>>>(t);
-  else
-    fused_tile_kernel<0, 1><<<grd, blk, 0, s>>>(t);
+  launch_tile(t, um, dim3((unsigned)nb), s);
   return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 
@@ -3724,20 +3759,28 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
   }
 }
 
-template <int UMODE>
+template <int UMODE, bool CLK>
 __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
   __shared__ double sE1[3][TB_LY][TB_LX], sH1[3][TB_LY][TB_LX];
   __shared__ double sE2[3][TB_LY][TB_LX], sH2[3][TB_LY][TB_LX];
   __shared__ int s_idx;
+  __shared__ unsigned long long s_t0;
   if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
     for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
   }
   unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
+  if (CLK && threadIdx.x == 0) s_t0 = 0ull;  // no previous item
   for (;;) {
     if (threadIdx.x == 0) {
+      if (CLK && s_t0 != 0ull) {  // diagnostics: the previous item (see fused_tile_kernel)
+        const TB2Item it = a.items[s_idx];
+        const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[s_idx] : ~0u;
+        clk_record(a.clk, s_t0, it.faces | (uw != ~0u ? 64 : 0), it.x, it.y, it.z, -1);
+      }
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
       s_idx = (long long)v < a.n ? (int)v : -1;
+      if (CLK) s_t0 = wall_clock64();
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int idx = s_idx;
@@ -3868,12 +3911,20 @@ int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
   const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grd((unsigned)nb), blk(1024);
-  if (um == 2)
-    tb2_kernel<2><<<grd, blk, 0, s>>>(t);
-  else if (um == 1)
-    tb2_kernel<1><<<grd, blk, 0, s>>>(t);
-  else
-    tb2_kernel<0><<<grd, blk, 0, s>>>(t);
+  if (t.clk.rec) {  // diagnostics build of the kernel (MNL_ITEM_CLOCK)
+    if (um == 2)
+      tb2_kernel<2, true><<<grd, blk, 0, s>>>(t);
+    else if (um == 1)
+      tb2_kernel<1, true><<<grd, blk, 0, s>>>(t);
+    else
+      tb2_kernel<0, true><<<grd, blk, 0, s>>>(t);
+  } else if (um == 2) {
+    tb2_kernel<2, false><<<grd, blk, 0, s>>>(t);
+  } else if (um == 1) {
+    tb2_kernel<1, false><<<grd, blk, 0, s>>>(t);
+  } else {
+    tb2_kernel<0, false><<<grd, blk, 0, s>>>(t);
+  }
   return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 
@@ -4009,12 +4060,13 @@ __global__ void dft_sample_kernel(const int *__restrict__ pj, const double *__re
 __global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restrict__ pch,
                                 const DftChunkDev *__restrict__ ch, long long npts, DevGrid g,
                                 DevFields f, int4 *__restrict__ sidx,
-                                unsigned short *__restrict__ ssel) {
+                                unsigned short *__restrict__ ssel, double4 *__restrict__ su) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npts) return;
   if (pj[3 * p] < 0) {
     ssel[p] = 0xFFFF;
     sidx[p] = make_int4(0, 0, 0, 0);
+    su[p] = make_double4(1.0, 1.0, 1.0, 1.0);
     return;
   }
   const DftChunkDev cd = ch[pch[p]];
@@ -4047,21 +4099,26 @@ __global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restric
   }
   unsigned sel = (unsigned)d | ((unsigned)cd.avgmode << 2);
   int idx[4] = {0, 0, 0, 0};
+  double uv[4] = {1.0, 1.0, 1.0, 1.0};  // chi1inv of implicit-E values (x * 1.0 == x otherwise)
   for (int v = 0; v < nv; v++) {
-    sel |= kind(q[v]) << (4 + 2 * v);
+    const unsigned k = kind(q[v]);
+    sel |= k << (4 + 2 * v);
     idx[v] = (int)q[v].idx;
+    if (k == 1 && f.inveps[d]) uv[v] = f.inveps[d][q[v].idx];
   }
   ssel[p] = (unsigned short)sel;
   sidx[p] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+  su[p] = make_double4(uv[0], uv[1], uv[2], uv[3]);
 }
 
-struct DftSrc {  // the current buffer set: E, D, chi1inv, B, H per direction
-  const double *E[3], *D[3], *U[3], *B[3], *H[3];
+struct DftSrc {  // the current buffer set: E, D, B, H per direction
+  const double *E[3], *D[3], *B[3], *H[3];
 };
 
-__device__ __forceinline__ double dft_val(const DftSrc &s, int d, unsigned k, int i) {
+// implicit E = D * chi1inv with chi1inv from the plan (constant in time; 1.0 where none)
+__device__ __forceinline__ double dft_val(const DftSrc &s, int d, unsigned k, int i, double u) {
   if (k == 0) return s.E[d][i];
-  if (k == 1) return s.U[d] ? s.D[d][i] * s.U[d][i] : s.D[d][i];
+  if (k == 1) return s.D[d][i] * u;
   return k == 2 ? s.B[d][i] : s.H[d][i];
 }
 
@@ -4069,24 +4126,33 @@ __device__ __forceinline__ double dft_val(const DftSrc &s, int d, unsigned k, in
 // average (w * 0.25) * (((f0 + f1) + f2) + f3) through the plan
 __global__ void dft_sample_plan_kernel(const int4 *__restrict__ sidx,
                                        const unsigned short *__restrict__ ssel,
+                                       const double4 *__restrict__ su,
                                        const double *__restrict__ pw, double *__restrict__ fr_out,
                                        long long npts, DftSrc s) {
-  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8), so
+  // each XCD takes one contiguous eighth of the points instead; the 2 x 2 averages of
+  // neighbouring rows then meet their shared lines in that XCD's L2
+  const unsigned nb = gridDim.x, xcd = blockIdx.x % 8u, q = nb / 8u, r = nb % 8u;
+  const unsigned lb = xcd * q + min(xcd, r) + blockIdx.x / 8u;
+  const long long p = (long long)lb * blockDim.x + threadIdx.x;
   if (p >= npts) return;
   const unsigned sel = ssel[p];
   if (sel == 0xFFFFu) return;  // another rank's point
   const int4 ix = sidx[p];
   const double w = pw[p];
   const int d = sel & 3, mode = (sel >> 2) & 3;
-  const double v0 = dft_val(s, d, (sel >> 4) & 3, ix.x);
+  // chi1inv only for implicit-E values (kind 1 in any slot)
+  const bool any1 = ((sel >> 4) & 0x55u & ~((sel >> 5) & 0x55u)) != 0;
+  const double4 u = any1 ? su[p] : make_double4(1.0, 1.0, 1.0, 1.0);
+  const double v0 = dft_val(s, d, (sel >> 4) & 3, ix.x, u.x);
   double fr;
   if (mode == 2) {
-    const double v1 = dft_val(s, d, (sel >> 6) & 3, ix.y);
-    const double v2 = dft_val(s, d, (sel >> 8) & 3, ix.z);
-    const double v3 = dft_val(s, d, (sel >> 10) & 3, ix.w);
+    const double v1 = dft_val(s, d, (sel >> 6) & 3, ix.y, u.y);
+    const double v2 = dft_val(s, d, (sel >> 8) & 3, ix.z, u.z);
+    const double v3 = dft_val(s, d, (sel >> 10) & 3, ix.w, u.w);
     fr = w * (v0 + v1 + v2 + v3);
   } else if (mode == 1) {
-    fr = w * (v0 + dft_val(s, d, (sel >> 6) & 3, ix.y));
+    fr = w * (v0 + dft_val(s, d, (sel >> 6) & 3, ix.y, u.y));
   } else {
     fr = w * v0;
   }
@@ -4094,22 +4160,22 @@ __global__ void dft_sample_plan_kernel(const int4 *__restrict__ sidx,
 }
 
 int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
-               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel,
+               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel, void *su,
                void *stream) {
   if (npts <= 0) return 0;
   dft_plan_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      pj, pch, ch, npts, g, f, (int4 *)sidx, ssel);
+      pj, pch, ch, npts, g, f, (int4 *)sidx, ssel, (double4 *)su);
   return rc();
 }
 
-int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const double *pw, double *fr,
-                      long long npts, const DevFields &f, void *stream) {
+int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const void *su,
+                      const double *pw, double *fr, long long npts, const DevFields &f,
+                      void *stream) {
   if (npts <= 0) return 0;
   DftSrc s;
-  for (int d = 0; d < 3; d++)
-    s.E[d] = f.E[d], s.D[d] = f.D[d], s.U[d] = f.inveps[d], s.B[d] = f.B[d], s.H[d] = f.H[d];
+  for (int d = 0; d < 3; d++) s.E[d] = f.E[d], s.D[d] = f.D[d], s.B[d] = f.B[d], s.H[d] = f.H[d];
   dft_sample_plan_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      (const int4 *)sidx, ssel, pw, fr, npts, s);
+      (const int4 *)sidx, ssel, (const double4 *)su, pw, fr, npts, s);
   return rc();
 }
 
@@ -4156,24 +4222,69 @@ __device__ __forceinline__ void dft_accum_point(double2 *__restrict__ dp,
   if (nfreq - i0 >= 1) dft_accum_tile<1>(dp, php, frv, n, rstride, i0);
 }
 
+// one tile of FT frequencies at i0 with the phases of the block's chunk staged in LDS
+// (sph[u][DFT_FT], tile-relative column woff + w): broadcast LDS reads instead of a dependent
+// global / scalar load per phase
+template <int FT>
+__device__ __forceinline__ void dft_accum_tile_lds(double2 *__restrict__ dp, const double2 *sph,
+                                                   const double *frv, int n, int i0, int woff) {
+  double2 v[FT];
+#pragma unroll
+  for (int w = 0; w < FT; w++) v[w] = dp[(i0 + woff + w) * 64];
+#pragma unroll
+  for (int u = 0; u < DFT_KB; u++) {
+    if (u < n) {
+#pragma unroll
+      for (int w = 0; w < FT; w++) {
+        const double2 q = sph[u * DFT_FT + woff + w];
+        v[w].x = v[w].x + frv[u] * q.x;
+        v[w].y = v[w].y + frv[u] * q.y;
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < FT; w++) dp[(i0 + woff + w) * 64] = v[w];
+}
+
 __global__ void __launch_bounds__(256)
     dft_accum_kernel(const int *__restrict__ pj, const int *__restrict__ pch,
                      double2 *__restrict__ dft, const double *__restrict__ fr, int n,
                      const double2 *__restrict__ ph, long long rstride, int nfreq,
                      long long npts) {
+  __shared__ double2 sph[DFT_KB * DFT_FT];
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npts) return;
-  if (pj[3 * p] < 0) return;
+  const bool live = p < npts && pj[3 * p] >= 0;
+  const int k = pch[p < npts ? p : npts - 1];
+  const int kb = pch[(long long)blockIdx.x * blockDim.x];
+  const bool uni = __syncthreads_and(k == kb);  // one chunk (one phase row) for the block
   double frv[DFT_KB];
 #pragma unroll
-  for (int u = 0; u < DFT_KB; u++) frv[u] = u < n ? fr[u * npts + p] : 0.0;
+  for (int u = 0; u < DFT_KB; u++) frv[u] = (live && u < n) ? fr[u * npts + p] : 0.0;
   double2 *__restrict__ dp = dft + (p >> 6) * nfreq * 64 + (p & 63);
-  const int k = pch[p];
-  const int k0 = __builtin_amdgcn_readfirstlane(k);
-  if (__all(k == k0))  // phases are wave-uniform: scalar loads
-    dft_accum_point(dp, ph + (long long)k0 * nfreq, frv, n, rstride, nfreq);
-  else
-    dft_accum_point(dp, ph + (long long)k * nfreq, frv, n, rstride, nfreq);
+  if (!uni) {
+    if (live) dft_accum_point(dp, ph + (long long)k * nfreq, frv, n, rstride, nfreq);
+    return;
+  }
+  const double2 *php = ph + (long long)kb * nfreq;
+  for (int i0 = 0; i0 < nfreq; i0 += DFT_FT) {  // block-uniform loop
+    const int ft = min(DFT_FT, nfreq - i0);
+    __syncthreads();  // the previous tile's readers are done
+    for (int e = threadIdx.x; e < n * DFT_FT; e += blockDim.x) {
+      const int u = e / DFT_FT, w = e % DFT_FT;
+      if (w < ft) sph[e] = php[u * rstride + i0 + w];
+    }
+    __syncthreads();
+    if (!live) continue;
+    if (ft == DFT_FT) {
+      dft_accum_tile_lds<DFT_FT>(dp, sph, frv, n, i0, 0);
+    } else {  // the last, partial tile in pieces of 8, 4, 2, 1
+      int w0 = 0;
+      if (ft - w0 >= 8) dft_accum_tile_lds<8>(dp, sph, frv, n, i0, w0), w0 += 8;
+      if (ft - w0 >= 4) dft_accum_tile_lds<4>(dp, sph, frv, n, i0, w0), w0 += 4;
+      if (ft - w0 >= 2) dft_accum_tile_lds<2>(dp, sph, frv, n, i0, w0), w0 += 2;
+      if (ft - w0 >= 1) dft_accum_tile_lds<1>(dp, sph, frv, n, i0, w0);
+    }
+  }
 }
 
 int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch, double *fr,

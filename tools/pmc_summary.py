@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise a tools/gpu_pmc.sh run (gpurun_out/prof_<tag>/) into profiles/.
+"""Summarise rocprofv3 stats / PMC runs (tools/gpu.sh prof: and pmc: steps, or the round-1
+to-3 layout gpurun_out/prof_<tag>/{stats,fetch,write}) into profiles/.
 
 Per kernel: calls, average duration (kernel-trace stats pass), HBM bytes per
 launch from the PMC passes, corrected as MI355X_MICROARCH.md prescribes and
