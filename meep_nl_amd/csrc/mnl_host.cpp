@@ -3711,7 +3711,12 @@ int tb_plan(mnl_fields *F) {
     split_range(xs, b.lo[0], b.hi[0] + 1, FX_HOST, 16);
     xs.push_back(b.hi[0] + 1);
     std::vector<int> zcut = {b.lo[2], b.hi[2] + 1};
-    for (int v : {L.lo[2] + 1, L.hi[2], lower ? 2 : -1, upper ? N2 - 2 : -1})
+    // cuts at the lean box's z range (lean bodies for the planes inside it), unless a piece
+    // would be thinner than 4 planes (the ring between L and L2: a 1-2-plane item costs more
+    // per cell as a lean item than inside its PML neighbour); slab-face cuts always
+    for (int v : {L.lo[2] + 1, L.hi[2]})
+      if (v - b.lo[2] >= 4 && b.hi[2] + 1 - v >= 4) zcut.push_back(v);
+    for (int v : {lower ? 2 : -1, upper ? N2 - 2 : -1})
       if (v > b.lo[2] && v < b.hi[2] + 1) zcut.push_back(v);
     std::sort(zcut.begin(), zcut.end());
     zcut.erase(std::unique(zcut.begin(), zcut.end()), zcut.end());
