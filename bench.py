@@ -197,22 +197,46 @@ def roofline(f, kind=0):
     return roof
 
 
-def pmc_traffic(size, vacuum):
-    """HBM bytes per launch of the lean kernel from the committed PMC profile of
-    THIS kernel source (profiles/pmc_traffic.json), else None."""
+def _traffic_file():
+    """profiles/pmc_traffic.json and the hash of THIS kernel source, or (None, None)."""
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(tpath):
-        return None
+        return None, None
     try:
         import hashlib
         with open(tpath) as fh:
             tj = json.load(fh)
         with open(os.path.join(ROOT, "meep_nl_amd", "csrc", "mnl_kernels.hip"), "rb") as fh:
             khash = hashlib.sha256(fh.read()).hexdigest()[:16]
-        if (tj.get("size") == size and tj.get("vacuum", False) == vacuum
+        return tj, khash
+    except (OSError, ValueError):
+        return None, None
+
+
+def pmc_traffic(size, vacuum):
+    """HBM bytes per launch of the headline's dominant kernel (the pair of temporal
+    blocking) from the committed PMC profile of THIS kernel source
+    (profiles/pmc_traffic.json), else None."""
+    tj, khash = _traffic_file()
+    try:
+        if (tj and tj.get("size") == size and tj.get("vacuum", False) == vacuum
                 and tj.get("kernels_hash") == khash):
             return round(tj["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
+    except (KeyError, TypeError):
+        return None
+    return None
+
+
+def pmc_traffic_config(workload, size, tb_active):
+    """The same for a BASELINE sub-config (configs.<workload>): its entry
+    <workload>_<size>_<tb|1s> in pmc_traffic.json "configs" (pairs or one-step stepping,
+    profiled with this kernel source), else None."""
+    tj, khash = _traffic_file()
+    try:
+        e = (tj or {}).get("configs", {}).get(f"{workload}_{size}_{'tb' if tb_active else '1s'}")
+        if e and e.get("kernels_hash") == khash:
+            return round(e["hbm_bytes_per_launch"])
+    except (KeyError, TypeError, AttributeError):
         return None
     return None
 
@@ -273,6 +297,8 @@ def measure_extra(workload, size, steps, warmup, tune=True):
            "fused": f.fused_active(), "tuned_zchunk_gen_cus": zc, "model_bytes_per_cell_step": round(bpc, 2),
            "model_fraction_of_peak": round(bpc * cells / (el / steps) / 1e9 / HBM_PEAK_GBS, 4),
            "roofline": roofline(f)}
+    tb_on = f.fused_active() and f.tb_info()["active"]
+    out["roofline"]["traffic"] = pmc_traffic_config(workload, size, tb_on) if f.fused_active() else None
     if workload == "kerr_nr":
         nv = nr_voxels(gv)
         e_n, e_ms, _ = f.kernel_stats(4)

@@ -242,8 +242,8 @@ int mnl_fields_step(mnl_fields *f, int nsteps);
  * polarization chunks, the CUs of their general kernel running beside the tile kernel
  * (0 and five splits around the balanced one; skipped with MNL_TILE_GEN_CUS set), and keeps
  * the fastest; with temporal blocking also the planes of the two-step
- * items.  Each candidate: two warm-up steps, reps (rounded up to even) timed.  Advances the
- * fields by at most 2 + 18 * (2 + reps) steps, with results
+ * items (automatic, 32, 48, 64, 96, 128) and pairs vs one-step stepping.  Each candidate: two warm-up steps, reps (rounded up to even) timed.  Advances the
+ * fields by at most 2 + 19 * (2 + reps) steps, with results
  * identical to plain stepping.  *zchunk = the length kept (0 = automatic), *gen_cus = the
  * CUs kept (0 = one launch after the other); -1 = not tuned (not in the fused tile mode:
  * at most 2 steps taken). */
@@ -367,7 +367,8 @@ int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, doubl
  * items, border points (upper bound), own cells of mixed-palette two-step items,
  * rim cells, mixed-palette rim cells, two-step items, rim items, planes of the
  * first two-step item, split (1: three launches per pair; 0: pipelined phases),
- * enabled (pairs allowed: set_temporal_blocking / MNL_TB / the tuner). */
+ * enabled (pairs allowed: set_temporal_blocking / MNL_TB / the tuner), the two-step chunk
+ * setting (0: automatic). */
 int mnl_fields_tb_info(mnl_fields *f, double *out, int n);
 /* Allow (1, the default; MNL_TB=0 at creation turns it off) or forbid (0) stepping
  * pairs of steps with the two-step kernel.  Results are identical either way. */

@@ -400,7 +400,7 @@ class Fields:
         the tile kernel's z-chunk length, then on one rank with polarization chunks the CUs
         of their general kernel beside the tile kernel; with temporal blocking the planes of
         its two-step items).  Every candidate runs two warm-up steps and reps (rounded up to
-        even) timed ones: at most 2 + 18 * (2 + reps) steps, results identical to plain
+        even) timed ones: at most 2 + 19 * (2 + reps) steps, results identical to plain
         stepping.  Returns (zchunk, gen_cus); -1 = not tuned (not in the fused tile mode)."""
         z, g = ctypes.c_int(0), ctypes.c_int(0)
         check(lib().mnl_fields_tune(self.h, int(reps), ctypes.byref(z), ctypes.byref(g)))
@@ -575,11 +575,13 @@ class Fields:
     def tb_info(self):
         """Temporal blocking of the current fused geometry: dict of
         active, two-step own cells / border points / mixed-palette cells, rim cells /
-        mixed-palette rim cells, item counts and the first item's planes."""
-        v = (ctypes.c_double * 11)()
-        check(lib().mnl_fields_tb_info(self.h, v, 11))
+        mixed-palette rim cells, item counts, the first item's planes, and the two-step chunk
+        setting (0: automatic)."""
+        v = (ctypes.c_double * 12)()
+        check(lib().mnl_fields_tb_info(self.h, v, 12))
         keys = ("active", "tb_cells", "tb_border", "tb_cells_mixed", "rim_cells",
-                "rim_cells_mixed", "tb_items", "rim_items", "tb_planes", "split", "enabled")
+                "rim_cells_mixed", "tb_items", "rim_items", "tb_planes", "split", "enabled",
+                "tb_zchunk")
         flags = ("active", "split", "enabled")
         return {k: (bool(x) if k in flags else int(x)) for k, x in zip(keys, v)}
 

@@ -7024,7 +7024,7 @@ int mnl_fields_set_temporal_blocking(mnl_fields *F, int on) {
 
 int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
   if (!F || !out || n < 1) return fail("bad argument");
-  const double v[11] = {F->fused && F->tb_have && F->tb_enabled ? 1.0 : 0.0,
+  const double v[12] = {F->fused && F->tb_have && F->tb_enabled ? 1.0 : 0.0,
                        F->tb_cells,
                        F->tb_border,
                        F->tb_cells_nu,
@@ -7035,8 +7035,9 @@ int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
                        F->tb_items.empty() ? 0.0 : double((F->tb_items[0].z >> 16) -
                                                           (F->tb_items[0].z & 0xFFFF)),
                        F->tb_split ? 1.0 : 0.0,
-                       F->tb_enabled ? 1.0 : 0.0};
-  for (int i = 0; i < n && i < 11; i++) out[i] = v[i];
+                       F->tb_enabled ? 1.0 : 0.0,
+                       double(F->tb_zchunk)};  // the setting (0: automatic)
+  for (int i = 0; i < n && i < 12; i++) out[i] = v[i];
   return 0;
 }
 

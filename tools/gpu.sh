@@ -8,6 +8,7 @@
 #                                        rocprofv3 --kernel-trace --stats (csv) of bench.py
 #   pmc:<tag>:<COUNTER+COUNTER...>[:<bench.py args>]
 #                                        one rocprofv3 --pmc pass (counters of one pass only)
+#   pmce:<tag>:<ENV=V,...>:<COUNTER+...>[:<bench.py args>]   the same with environment settings
 #   py:<tag>:<script and args>           python -u <script args> -> gpurun_out/<tag>.txt
 #   smoke                                __graft_entry__.smoke()
 # Every step runs under its own time limit; a step that crashes, times out or fails stops
@@ -51,10 +52,13 @@ run_step() {
       echo "=== $kind $tag ($envs) rc=$rc"
       [ "$kind" = bench ] && head -c 600 gpurun_out/$tag.json && echo && tail -n 3 gpurun_out/$tag.err
       return $rc ;;
-    pmc)
+    pmc|pmce)
       tag=${rest%%:*}; rest=${rest#"$tag"}; rest=${rest#:}
+      envs=""
+      if [ "$kind" = pmce ]; then envs=${rest%%:*}; rest=${rest#"$envs"}; rest=${rest#:}; fi
       local ctr=${rest%%:*}; args=${rest#"$ctr"}; args=${args#:}
-      ( cd /tmp && export TMPDIR=/tmp
+      ( envset "$envs"
+        cd /tmp && export TMPDIR=/tmp
         timeout -s KILL 300 rocprofv3 --pmc ${ctr//+/ } --output-format csv \
           -d "$ROOT/gpurun_out/$tag" -o run -- python3 "$ROOT/bench.py" $args \
           > "$ROOT/gpurun_out/$tag.log" 2>&1 )

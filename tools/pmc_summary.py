@@ -44,6 +44,19 @@ def counters(d):
     return out
 
 
+def write_headline(path, doc):
+    """the headline entry of the traffic file; the sub-config entries ("configs") are kept"""
+    try:
+        with open(path) as fh:
+            old = json.load(fh)
+    except (OSError, ValueError):
+        old = {}
+    if "configs" in old:
+        doc["configs"] = old["configs"]
+    with open(path, "w") as fh:
+        json.dump(doc, fh, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
@@ -55,6 +68,10 @@ def main():
     ap.add_argument("--pair", action="store_true",
                     help="temporal blocking: the traffic of a pair of steps = tb2_kernel + 2 x "
                          "fused_tile_kernel (the rim launches)")
+    ap.add_argument("--config", metavar="WORKLOAD",
+                    help="with --traffic: write the entry configs.<WORKLOAD>_<size>_<tb|1s> of the file "
+                         "(a bench.py sub-config; --kernel names its dominant kernel, --pair a "
+                         "temporal-blocking pair) and keep the rest of the file")
     ap.add_argument("--dirs", nargs=3, metavar=("STATS", "FETCH", "WRITE"),
                     help="separate directories of the stats / FETCH_SIZE / WRITE_SIZE runs "
                          "(tools/gpu.sh prof: / pmc: steps) instead of src/{stats,fetch,write}")
@@ -92,27 +109,50 @@ def main():
     print(json.dumps({k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                           for kk, vv in v.items() if kk in ("avg_ms", "hbm_bytes", "hbm_GBps")}
                       for k, v in res.items()}, indent=1))
+    if a.traffic and a.config:
+        try:
+            with open(a.traffic) as fh:
+                doc_t = json.load(fh)
+        except (OSError, ValueError):
+            doc_t = {}
+        if a.pair:
+            tb = [k for k in res if k.startswith("tb2_kernel") and "hbm_bytes" in res[k]]
+            rim = [k for k in res if k.startswith("fused_tile_kernel") and "hbm_bytes" in res[k]]
+            if not (tb and rim):
+                return
+            entry = {"kernel": "pair: tb2_kernel + 2 x fused_tile_kernel (rim)", "tb": True,
+                     "hbm_bytes_per_launch": res[tb[0]]["hbm_bytes"] + 2 * res[rim[0]]["hbm_bytes"]}
+        else:
+            ks = [k for k in res if k.startswith(a.kernel) and "hbm_bytes" in res[k]]
+            if not ks:
+                return
+            entry = {"kernel": ks[0], "tb": False, "hbm_bytes_per_launch": res[ks[0]]["hbm_bytes"]}
+        entry.update({"kernels_hash": kernels_hash(), "profile": os.path.basename(a.dst)})
+        doc_t.setdefault("configs", {})[f"{a.config}_{a.size}_{'tb' if a.pair else '1s'}"] = entry
+        with open(a.traffic, "w") as fh:
+            json.dump(doc_t, fh, indent=1)
+        return
     if a.traffic and a.pair:
         tb = [k for k in res if k.startswith("tb2_kernel") and "hbm_bytes" in res[k]]
         rim = [k for k in res if k.startswith("fused_tile_kernel") and "hbm_bytes" in res[k]]
         if tb and rim:
             hb = res[tb[0]]["hbm_bytes"] + 2 * res[rim[0]]["hbm_bytes"]
-            with open(a.traffic, "w") as fh:
-                json.dump({"kernels_hash": kernels_hash(), "size": a.size, "vacuum": a.vacuum,
-                           "kernel": "pair: tb2_kernel + 2 x fused_tile_kernel (rim)",
-                           "unit": "pair of steps", "hbm_bytes_per_launch": hb,
-                           "tb2_bytes": res[tb[0]]["hbm_bytes"],
-                           "rim_bytes": res[rim[0]]["hbm_bytes"],
-                           "profile": os.path.basename(a.dst)}, fh, indent=1)
+            doc_t = {"kernels_hash": kernels_hash(), "size": a.size, "vacuum": a.vacuum,
+                     "kernel": "pair: tb2_kernel + 2 x fused_tile_kernel (rim)",
+                     "unit": "pair of steps", "hbm_bytes_per_launch": hb,
+                     "tb2_bytes": res[tb[0]]["hbm_bytes"],
+                     "rim_bytes": res[rim[0]]["hbm_bytes"],
+                     "profile": os.path.basename(a.dst)}
+            write_headline(a.traffic, doc_t)
         return
     if a.traffic:
         ks = [k for k in res if k.startswith(a.kernel) and "hbm_bytes" in res[k]]
         if ks:
             k = ks[0]
-            with open(a.traffic, "w") as fh:
-                json.dump({"kernels_hash": kernels_hash(), "size": a.size, "vacuum": a.vacuum,
-                           "kernel": k, "hbm_bytes_per_launch": res[k]["hbm_bytes"],
-                           "profile": os.path.basename(a.dst)}, fh, indent=1)
+            write_headline(a.traffic, {"kernels_hash": kernels_hash(), "size": a.size,
+                                       "vacuum": a.vacuum, "kernel": k,
+                                       "hbm_bytes_per_launch": res[k]["hbm_bytes"],
+                                       "profile": os.path.basename(a.dst)})
 
 
 if __name__ == "__main__":
