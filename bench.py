@@ -426,7 +426,17 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # the gloo group (host-side barriers, the max over ranks) prints its connection
+        # messages to stdout from C++: send them to stderr, stdout carries the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         from meep_nl_amd import core
         transport, device = core.pick_transport(world, local_rank)
         obj = [core.comm_id(world, transport) if rank == 0 else None]
