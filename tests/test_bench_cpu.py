@@ -32,3 +32,30 @@ def test_help_runs_without_a_gpu():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "--no-tune" in r.stdout
+
+
+def test_traffic_lookup_is_hash_and_mode_gated(tmp_path, monkeypatch):
+    """roofline.traffic comes from profiles/pmc_traffic.json only for the kernel source it
+    was measured on, the same size, and (sub-configs) the same stepping mode."""
+    import hashlib
+    import json
+    import bench
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "meep_nl_amd" / "csrc").mkdir(parents=True)
+    src = tmp_path / "meep_nl_amd" / "csrc" / "mnl_kernels.hip"
+    src.write_text("// kernels v1\n")
+    h = hashlib.sha256(src.read_bytes()).hexdigest()[:16]
+    doc = {"kernels_hash": h, "size": 512, "vacuum": False, "hbm_bytes_per_launch": 26.9e9,
+           "configs": {"c2_256_1s": {"kernels_hash": h, "hbm_bytes_per_launch": 2.38e9},
+                       "kerr_256_1s": {"kernels_hash": "stale", "hbm_bytes_per_launch": 2.0e9}}}
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(doc))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_traffic(512, False) == round(26.9e9)
+    assert bench.pmc_traffic(256, False) is None
+    assert bench.pmc_traffic(512, True) is None
+    assert bench.pmc_traffic_config("c2", 256, False) == round(2.38e9)
+    assert bench.pmc_traffic_config("c2", 256, True) is None       # measured one-step only
+    assert bench.pmc_traffic_config("kerr", 256, False) is None    # other kernel source
+    src.write_text("// kernels v2\n")                              # the kernels changed
+    assert bench.pmc_traffic(512, False) is None
+    assert bench.pmc_traffic_config("c2", 256, False) is None

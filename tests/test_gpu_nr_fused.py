@@ -55,3 +55,13 @@ def test_nr_fused_full_size():
     o = sc_c4_nr(make_oracle, steps=30)
     assert o.nr_random_fallbacks() > 0
     _same(p, o)
+
+
+def test_nr_box_in_pml_stays_unfused():
+    """A chi2 box reaching the PML (C4-NR at 64^3: |x| <= 3 crosses the 1.0-thick PML of a
+    6.4-wide cell) cannot leave its E to the NR box kernel (the PML E update is the W form):
+    the run stays unfused and bitwise."""
+    p = sc_c4_nr(ProductSim, steps=0, n=64)
+    p.step(30)
+    assert not p._fields().fused_active()
+    _same(p, sc_c4_nr(make_oracle, steps=30, n=64))
