@@ -4137,7 +4137,7 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   const TB2Args t = tb_args(F, cur, mid, nxt);
   const int nr = (int)F->tb_ritems.size();
   int k, kr;
-  if (F->tb_split) {  // diagnostics: R1, two-step kernel, R2 as three launches
+  if (F->tb_split) {  // default: R1, two-step kernel, R2 as three launches
     const FusedArgs r1 = rim_args(F, fa, cur, mid), r2 = rim_args(F, fa, mid, nxt);
     k = ev_begin(TM_RIM);
     kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
