@@ -2667,7 +2667,8 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   const long long st1 = a.st1;
   const int ox = (w < FR) ? sl : -1;
   const int gx = sx0 + ox, gy = y0 + row;
-  const bool inA = ownlike && gx >= 0 && gx < N0 && gy >= 0 && gy < N1;
+  // lanes right of x1 + 1 (a narrow item or PAIR half) feed nothing that is stored: no loads
+  const bool inA = ownlike && gx >= 0 && gx < N0 && gx <= sx1 + 1 && gy >= 0 && gy < N1;
   const unsigned cb = (unsigned)((gx + (long long)gy * st1) * 8);
   const unsigned cbl = inA ? cb : 0u;
   // per-axis ownership (within G): bit0 = components shifted along the axis, bit1 = unshifted
@@ -2682,7 +2683,7 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
   };
   const bool stl = ownlike && w < FR && row >= 1 && gx <= sx1 && gy <= it.y1;
   const int hx = sx0 + hdx, hy = y0 + hdy;
-  const bool hA = hslot && hx >= 0 && hx < N0 && hy >= 0 && hy < N1;
+  const bool hA = hslot && hx >= 0 && hx < N0 && hx <= sx1 + 1 && hy >= 0 && hy < N1;
   const unsigned hbl = hA ? (unsigned)((hx + (long long)hy * st1) * 8) : cbl;
   const unsigned hownx = own_bits_of(hx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
   const unsigned howny = OWNC ? 3u : own_bits_of(hy, a.osh_lo[1], a.osh_hi[1], a.oun_lo[1], a.oun_hi[1]);
