@@ -142,7 +142,12 @@ def roofline(f, kind=0):
     achieved = k_bytes / (avg_ms * 1e-3) / 1e9 if n_launch and avg_ms > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": (("fused_tile_kernel (one persistent launch over the fused box: lean "
+            "kernel": (("fused_tile_kernel + fused_general_kernel concurrently on a CU split "
+                        "(tile kernel: lean tiles + per-direction PML bodies; general kernel: the "
+                        "polarization chunks with the Lorentzian P update); one step, both "
+                        "launches' bytes over the span of both"
+                        if f.tile_mode() and f.fused_concurrent() else
+                        "fused_tile_kernel (one persistent launch over the fused box: lean "
                         "tiles + per-direction PML bodies; curl B + H + curl D + E, one pass)"
                         if f.tile_mode() else
                         "fused_kernel + fused_general_kernel concurrently (whole step, one pass)"
@@ -154,8 +159,8 @@ def roofline(f, kind=0):
     tb = f.tb_info() if f.fused_active() else {"active": False}
     t_n, t_ms, t_bytes = f.kernel_stats(5)
     if tb["active"] and t_n:
-        # temporal blocking: a pair of steps is two persistent launches
-        # of tb_phase_kernel (rim items one step each + two-step items over L2); the
+        # temporal blocking: a pair of steps is three persistent
+        # launches (the two-step kernel over L2, then the tile kernel over the rim twice); the
         # algorithmic bytes of a pair are the two-step items' two steps (B, D read once and
         # written once, palette words of mixed items, border points' step n+1) plus two rim
         # steps.  frac_one_step_model prices the same pair at the one-step model (two steps of
@@ -165,11 +170,8 @@ def roofline(f, kind=0):
         r_n, r_ms, r_bytes = f.kernel_stats(6)
         roof.update({
             "kernel": ("tb2_kernel (two-step z-march over the lean region L2) + 2 x "
-                       "fused_tile_kernel over the rim items (PML, walls, ring, source holes), "
-                       "one pair of steps" if tb.get("split", True) else
-                       "tb_phase_kernel x2 per pair of steps (two-step z-march over the lean "
-                       "region L2 + one-step tile bodies over the PML / wall / ring / "
-                       "source-hole rim, interleaved in one persistent queue)"),
+                       "fused_tile_kernel over the rim items (PML, walls, ring, source holes; "
+                       "x-face strips in the narrow 16 x 63 strip body), one pair of steps"),
             "bytes_per_launch": t_bytes, "avg_launch_ms": round(t_avg, 4), "launches": t_n,
             "launch_unit": "pair of steps (all its launches)",
             "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -357,23 +359,29 @@ def measure_c5(args, rank, world, device, dist):
 
 
 def cpu_baseline(args):
-    """Time the oracle (CPU restatement, oracle/) on a bounded sample of the
-    headline workload on this host's cores: a 128^3 grid of the same waveguide
-    whose PML (0.15 -> 3 cells per face) keeps about the PML-cell fraction of
-    the 512^3 config (13.3 % vs 12.3 %)."""
+    """Time the oracle (CPU restatement, oracle/) on the headline config itself: the
+    512^3 waveguide (eps = 12 core) + PML(1.0) with the same Gaussian source, OpenMP on this
+    host's share of cores (OMP_NUM_THREADS; 16 per GPU on the driver's boxes), a few steps
+    after two untimed ones (about 10-20 s of stepping at ~1 s per step)."""
     from oracle import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 64))
     orc.set_threads(threads)
     import numpy as np
-    L = 128
+    L = args.size
+    t_setup = time.perf_counter()
     o = orc.Oracle(3, [L, L, L], 10.0, 0.5, [-L, -L, -L])
-    o.add_pml(0.15)
+    o.add_pml(1.0)
     if not args.vacuum:
         for c in (0, 1, 2):
             x, y, z = o.coords(c)
-            o.set_chi1inv(c, c, np.where((np.abs(y) < 0.5) & (np.abs(z) < 0.5), 1 / 12.0, 1.0))
+            del x
+            core = (np.abs(y) < 0.5 - 1e-12) & (np.abs(z) < 0.5 - 1e-12)
+            del y, z
+            o.set_chi1inv(c, c, np.where(core, 1 / 12.0, 1.0))
+            del core
     o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    t_setup = time.perf_counter() - t_setup
     o.step(2)
     steps, t0 = 0, time.perf_counter()
     while True:
@@ -383,11 +391,12 @@ def cpu_baseline(args):
         if el >= args.cpu_seconds or steps >= 400:
             break
     v = L ** 3 * steps / el / 1e6
-    pml_frac = 1 - ((L - 2 * 3) / L) ** 3
+    wl = "vacuum" if args.vacuum else "waveguide (eps = 12 core)"
     return {"value": round(v, 2), "unit": "Mcells*steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ CPU restatement, {L}^3 {'vacuum' if args.vacuum else 'waveguide'}"
-                      f" + PML(0.15) ({100 * pml_frac:.1f}% PML cells; the 512^3 config has "
-                      f"12.3%), {steps} steps in {el:.1f} s, OpenMP {threads} threads"}
+            "sample": f"oracle/ CPU restatement of the headline config itself: {L}^3 {wl} + "
+                      f"PML(1.0), Ez Gaussian source, {steps} timed steps after 2 untimed in "
+                      f"{el:.1f} s (set-up {t_setup:.0f} s not timed), OpenMP {threads} threads "
+                      f"(OMP_NUM_THREADS; the host reports {os.cpu_count()} CPUs)"}
 
 
 def launch_ranks(args):

@@ -541,6 +541,13 @@ class Fields:
         check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
         return bool(v.value & 16)
 
+    def fused_concurrent(self):
+        """True if the last fused step ran the polarization chunks' general kernel beside the
+        tile (or lean) kernel on a CU split: kernel_stats(0) then spans both launches."""
+        v = ctypes.c_int()
+        check(lib().mnl_fields_mode(self.h, ctypes.byref(v)))
+        return bool(v.value & 32)
+
     def fused_palette(self):
         """True if the fused kernel reads chi1inv through the byte palette."""
         v = ctypes.c_int()
@@ -574,15 +581,16 @@ class Fields:
 
     def tb_info(self):
         """Temporal blocking of the current fused geometry: dict of
-        active, two-step own cells / border points / mixed-palette cells, rim cells /
-        mixed-palette rim cells, item counts, the first item's planes, and the two-step chunk
-        setting (0: automatic)."""
+        active (the last call of >= 2 steps stepped in pairs), two-step own cells / border
+        points / mixed-palette cells, rim cells / mixed-palette rim cells, item counts, the
+        first item's planes, the narrow x-face strip items among the rim items, and the
+        two-step chunk setting (0: automatic)."""
         v = (ctypes.c_double * 12)()
         check(lib().mnl_fields_tb_info(self.h, v, 12))
         keys = ("active", "tb_cells", "tb_border", "tb_cells_mixed", "rim_cells",
-                "rim_cells_mixed", "tb_items", "rim_items", "tb_planes", "split", "enabled",
+                "rim_cells_mixed", "tb_items", "rim_items", "tb_planes", "narrow_items", "enabled",
                 "tb_zchunk")
-        flags = ("active", "split", "enabled")
+        flags = ("active", "enabled")
         return {k: (bool(x) if k in flags else int(x)) for k, x in zip(keys, v)}
 
     def traffic_model(self):

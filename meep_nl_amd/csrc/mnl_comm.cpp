@@ -190,12 +190,11 @@ int Comm::ipc_barrier() {
     return 0;
   }
   // Setup waits are bounded by MNL_IPC_TIMEOUT (default 300 s).  Once every rank has joined,
-  // a wait ends when a peer's process exits (or turns zombie), and otherwise after
-  // MNL_IPC_TIMEOUT when set, else 1800 s: a rank-0-only output or a whole-cell setup can
-  // legitimately keep the others waiting for minutes, a peer that took another code path
-  // must not hang them forever.
+  // a wait ends when a peer's process exits (or turns zombie) -- liveness comes from the
+  // peers' pids -- and otherwise only after MNL_IPC_TIMEOUT when it is set: a rank-0-only
+  // output or a whole-cell setup can legitimately keep the others waiting for a long time.
   static const bool explicit_timeout = getenv("MNL_IPC_TIMEOUT") != nullptr;
-  const double limit = (ipc_ready_ && !explicit_timeout) ? 1800.0 : ipc_timeout_s_;
+  const double limit = (ipc_ready_ && !explicit_timeout) ? 1e300 : ipc_timeout_s_;
   auto t0 = std::chrono::steady_clock::now();
   long spins = 0;
   while (C.gen.load(std::memory_order_acquire) == g) {

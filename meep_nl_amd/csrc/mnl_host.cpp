@@ -38,9 +38,14 @@ namespace {
 constexpr int FX_HOST = 64;    // fused tile width (FX in mnl_kernels.hip)
 constexpr int FOWN_HOST = 14;  // own rows of a tile item (FOWN in mnl_kernels.hip)
 constexpr int TB_RES_CUS = 8;  // multi-rank: CUs left to the slab-face work (one per XCD)
+constexpr int SW_HOST = 16;     // narrow strip columns (SW_N in mnl_kernels.hip)
+constexpr int SOWN_HOST = 63;   // narrow strip own rows (SR_N - 1)
+constexpr int NAN_CH = 256;     // steps per chunk of a batch: the NaN flag is read after each
 
 const double pi = 3.141592653589793238462643383276;  // meep::pi
 thread_local std::string g_err;
+
+static int g_verbosity = 1;  // meep::verbosity (src/meep.hpp: default 1)
 
 int fail(const std::string &m) {
   g_err = "meep: " + m;
@@ -358,20 +363,14 @@ struct mnl_fields {
   unsigned *d_tb_rflag = nullptr, *d_tb_uflag = nullptr;
   TB2Item *d_tb_items = nullptr;
   size_t tb_rcap = 0, tb_gcap = 0, tb_icap = 0;
-  // queue orders of the two phases (k_tb_phase): A = rim step n+1 of the previous pair +
-  // inner two-step items, I = inner items only (first pair of a batch), B = rim step n +
-  // outer two-step items (those whose distance-2 footprint meets the rim)
-  std::vector<int> tb_order[3];
-  int *d_tb_order[3] = {nullptr, nullptr, nullptr};
-  size_t tb_ocap[3] = {0, 0, 0};
-  // rim / two-step / rim as three launches per pair (default: measured faster than the
-  // pipelined phases, whose merged kernel spills registers; MNL_TB_SPLIT=0 selects those)
-  bool tb_split = true;
-  bool tb_pending = false;  // the last pair's rim step n+1 has not run yet (tb_drain)
   bool tb_nopair = false;   // MNL_TB_NOPAIR=1: x-face rim strips one per workgroup (A/B)
+  bool tb_last = false;     // the last batch of >= 2 steps stepped in pairs (tb_usable)
+  bool tb_oom = false;      // the middle buffer set did not fit: temporal blocking off
+  bool tb_oom_test = false; // MNL_TB_OOM=1: its allocation fails (tests)
+  bool tb_narrow = true;    // MNL_TB_NARROW=0: no narrow x-face strip items (A/B)
+  int tb_nnarrow = 0;       // narrow x-face strip items of the current plan
   int tb_rfree = 0;         // leading rim items that read no slab-face data (multi-rank)
   bool tb_chain_pending = false;  // the last multi-rank pair's s_comm chain not yet joined
-  SrcDev tb_pend_src{};     // ... and the source currents applied after it
   double *pp3_B[3] = {nullptr, nullptr, nullptr}, *pp3_D[3] = {nullptr, nullptr, nullptr};
   double *pp3_E[3] = {nullptr, nullptr, nullptr}, *pp3_H[3] = {nullptr, nullptr, nullptr};
   double *pp3_UB[3] = {nullptr, nullptr, nullptr};
@@ -381,7 +380,8 @@ struct mnl_fields {
   int nan_every = 1;                // NaN guard cadence (src/step.cpp:138-139: every step)
   int since_nan = 0;                // steps since the last NaN guard (across calls)
   bool nan_due = false;             // a guard is due once the state is complete (pending rim)
-  int nan_launched = 0;             // guards launched in this batch (flag read at its end)
+  int nan_launched = 0;             // guards launched in this chunk (flag read at its end)
+  long long nan_at = 0;             // time step of the state the next guard checks
   NanTerms nan_terms{};             // this batch's interpolation terms (nan_terms_build)
   int *d_nanflag = nullptr;         // [flag, step]
   CurlPlan planB, planD;
@@ -437,8 +437,7 @@ struct mnl_fields {
     if (d_uflag) hipFree(d_uflag);
     if (d_gflag) hipFree(d_gflag);
     for (void *p : {(void *)d_tb_ritems, (void *)d_tb_rgeo, (void *)d_tb_rflag, (void *)d_tb_uflag,
-                    (void *)d_tb_items, (void *)d_tb_order[0], (void *)d_tb_order[1],
-                    (void *)d_tb_order[2]})
+                    (void *)d_tb_items})
       if (p) hipFree(p);
     comm.reset();
     for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
@@ -452,7 +451,8 @@ struct mnl_fields {
 namespace {
 
 bool in_fused_box(const mnl_fields *F, int c, const int jg[3]);
-int nan_launch(mnl_fields *F, hipStream_t st = nullptr);
+int nan_launch(mnl_fields *F, hipStream_t st = nullptr, double *const *E = nullptr,
+               double *const *D = nullptr);
 void nan_count(mnl_fields *F, int k);
 int nan_result(mnl_fields *F);
 int nan_terms_build(mnl_fields *F);
@@ -2428,6 +2428,25 @@ int tile_item_code(const mnl_fields *F, const FusedArgs &a, const Box &L, int x0
   return (body << 24) | (ownc << 29);
 }
 
+// Item code of a narrow x-face strip (strip_body: body 1 | OWNC | bit 30) with own columns
+// x0 .. x1 (at most 16, x0 128-byte aligned), halo row y0, own rows y0+1 .. y1 (at most 63)
+// and planes [zs, ze), or -1 when its footprint (columns x0-1 .. x1+1, rows y0 .. y1+1,
+// planes zs-1 .. ze) meets PML along y or z or a point not owned in y or z.
+int strip_item_code(const mnl_fields *F, const FusedArgs &a, int x0, int x1, int y0, int y1, int zs,
+                    int ze) {
+  const DevGrid &g = F->g;
+  if (x1 - x0 + 1 > SW_HOST || (x0 & 15) || y1 - y0 > SOWN_HOST || y1 < y0 + 1 || ze <= zs)
+    return -1;
+  const int lo[3] = {x0 - 1, y0, zs - 1}, hi[3] = {x1 + 1, y1 + 1, ze};
+  if (pml_dirs_in(F, lo, hi) != 1) return -1;
+  const int ylo = std::max(a.osh_lo[1], a.oun_lo[1]), yhi = std::min(a.osh_hi[1], a.oun_hi[1]);
+  const int zlo = std::max(a.osh_lo[2], a.oun_lo[2]), zhi = std::min(a.osh_hi[2], a.oun_hi[2]);
+  if (!(y0 >= ylo && y1 + 1 <= yhi && zs - 1 >= zlo && ze <= zhi && y1 + 1 <= g.N[1] - 1 &&
+        ze <= g.N[2] - 1))
+    return -1;
+  return (1 << 24) | (1 << 29) | (1 << 30);
+}
+
 bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
   const DevGrid &g = F->g;
   FusedArgs &a = F->fgeo;
@@ -3641,6 +3660,20 @@ int tb_plan(mnl_fields *F) {
   std::vector<Box> dbox;
   for (auto &op : F->dfts)  // (built once per monitor: this runs every batch)
     if (op->bbox.hi[0] >= 0) dbox.push_back(op->bbox);
+  // the NaN guard's points (it checks the middle state of every pair, src/step.cpp:138-139)
+  if (F->nan_terms.n > 0) {
+    Box nb;
+    for (int i = 0; i < F->nan_terms.n; i++) {
+      const long long li = F->nan_terms.idx[i];
+      const int p[3] = {(int)(li % F->g.st[1]), (int)((li % F->g.st[2]) / F->g.st[1]),
+                        (int)(li / F->g.st[2])};
+      for (int k = 0; k < 3; k++) {
+        nb.lo[k] = i ? std::min(nb.lo[k], p[k]) : p[k];
+        nb.hi[k] = i ? std::max(nb.hi[k], p[k]) : p[k];
+      }
+    }
+    dbox.push_back(nb);
+  }
   mix((long long)dbox.size());
   for (const Box &b : dbox)
     for (int k = 0; k < 3; k++) mix(b.lo[k]), mix(b.hi[k]);
@@ -3654,15 +3687,25 @@ int tb_plan(mnl_fields *F) {
   if (F->S.dim != 3 || g.N[0] > 65535 || g.N[1] > 65535 || g.N[2] > 65535) return 0;
   Box L2;
   for (int k = 0; k < 3; k++) L2.lo[k] = L.lo[k] + 2, L2.hi[k] = L.hi[k] - 2;
-  // two-step tiles start 4 columns past a 64-byte boundary (their lanes start on it); the rim
-  // to the right of L2 starts on a 128-byte boundary (tile-kernel items)
-  L2.lo[0] += ((4 - L2.lo[0]) % 8 + 8) % 8;
+  // x: the rim to the right of L2 starts on a 128-byte boundary (tile-kernel items); the rim
+  // to the left ends on one when that costs no more columns than starting the two-step tiles
+  // 4 columns past a 64-byte boundary (their lanes' line) -- a 16-column left rim runs as
+  // narrow strips (strip_body), and the first two-step tile of a row starts its lanes on the
+  // line below its own columns
+  {
+    const int a16 = G.lo[0] + (L2.lo[0] - G.lo[0] + 15) / 16 * 16;
+    const int a4 = L2.lo[0] + ((4 - L2.lo[0]) % 8 + 8) % 8;
+    L2.lo[0] = (F->tb_narrow && a16 <= a4) ? a16 : a4;
+  }
   L2.hi[0] = (L2.hi[0] + 1) / 16 * 16 - 1;
   bool l2 = true;
   for (int k = 0; k < 3; k++) l2 = l2 && L2.hi[k] - L2.lo[k] >= 7;
   // one rank: no two-step region, no pairs.  Multi-rank: a rank without one (thin slab, PML)
   // still steps pairs as two rim launches (every rank runs the same exchange sequence)
-  if (!l2 && F->nranks == 1) return 0;
+  if (!l2 && F->nranks == 1) {
+    if (F->tb_stats) fprintf(stderr, "tb: L2 empty\n");
+    return 0;
+  }
   if (!l2)
     for (int k = 0; k < 3; k++) L2.lo[k] = 1, L2.hi[k] = 0;
   // holes: no source point within distance 1 of a two-step own point (the march's D^{n+1}
@@ -3705,11 +3748,29 @@ int tb_plan(mnl_fields *F) {
   }
   std::vector<RI> heavy, lean;
   F->rim_cells = F->rim_lean = 0;
+  F->tb_nnarrow = 0;
+  // a column box (x fixed, rows / planes inclusive) of two-step points
+  auto col_two = [&](int x, int ylo, int yhi, int zlo, int zhi) {
+    if (!l2 || x < L2.lo[0] || x > L2.hi[0] || ylo < L2.lo[1] || yhi > L2.hi[1] || zlo < L2.lo[2] ||
+        zhi > L2.hi[2])
+      return false;
+    Box c;
+    c.lo[0] = c.hi[0] = x, c.lo[1] = ylo, c.hi[1] = yhi, c.lo[2] = zlo, c.hi[2] = zhi;
+    for (const Box &h : holes)
+      if (box_meets(c, h)) return false;
+    return true;
+  };
   for (const Box &b : rim) {
-    if (b.lo[0] % 16) return 0;  // cannot happen with the alignments above
+    if (b.lo[0] % 16) {  // cannot happen with the alignments above
+      if (F->tb_stats) fprintf(stderr, "tb: rim box at x %d not 128-byte aligned\n", b.lo[0]);
+      return 0;
+    }
     std::vector<int> xs, zs;
     split_range(xs, b.lo[0], b.hi[0] + 1, FX_HOST, 16);
     xs.push_back(b.hi[0] + 1);
+    // a 16-column x-face box whose x-1 column is outside the grid or two-step: narrow strips
+    const bool narrow = F->tb_narrow && b.hi[0] - b.lo[0] + 1 == SW_HOST &&
+                        (b.lo[0] == 0 || col_two(b.lo[0] - 1, b.lo[1], b.hi[1], b.lo[2], b.hi[2]));
     std::vector<int> zcut = {b.lo[2], b.hi[2] + 1};
     // cuts at the lean box's z range (lean bodies for the planes inside it), unless a piece
     // would be thinner than 4 planes (the ring between L and L2: a 1-2-plane item costs more
@@ -3726,6 +3787,38 @@ int tb_plan(mnl_fields *F) {
       for (int t = 0; t < nt; t++) zs.push_back(zcut[s] + (int)((long long)n * t / nt));
     }
     zs.push_back(b.hi[2] + 1);
+    if (narrow) {
+      const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + SOWN_HOST - 1) / SOWN_HOST;
+      std::vector<RI> items;
+      bool ok = true;
+      for (size_t iz = 0; iz + 1 < zs.size() && ok; iz++)
+        for (int ty = 0; ty < nty && ok; ty++) {
+          const int x0 = b.lo[0], x1 = b.hi[0];
+          const int yf = b.lo[1] + (int)((long long)ny * ty / nty);
+          const int y1 = b.lo[1] + (int)((long long)ny * (ty + 1) / nty) - 1;
+          const int z0 = zs[iz], z1 = zs[iz + 1];
+          const int code = strip_item_code(F, a, x0, x1, yf - 1, y1, z0, z1);
+          if (code < 0) {
+            ok = false;
+            break;
+          }
+          bool src_in = false;
+          if (F->nranks > 1)
+            for (const auto &sp : spts)
+              src_in = src_in || (sp[0] >= x0 - 1 && sp[0] <= x1 + 1 && sp[1] >= yf - 1 &&
+                                  sp[1] <= y1 + 1 && sp[2] >= z0 - 1 && sp[2] <= z1);
+          items.push_back(RI{code, x0 | (x1 << 16), yf | (y1 << 16), z0 | (z1 << 16), -1, z1 - z0,
+                             (lower && z0 <= 1) || (upper && z1 >= N2 - 1) || src_in});
+        }
+      if (ok) {
+        for (const RI &it : items) {
+          heavy.push_back(it);
+          F->rim_cells += double(SW_HOST) * (((it.g1 >> 16) - (it.g1 & 0xFFFF)) + 1) * it.planes;
+        }
+        F->tb_nnarrow += (int)items.size();
+        continue;
+      }
+    }
     const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + FOWN_HOST - 1) / FOWN_HOST;
     for (size_t iz = 0; iz + 1 < zs.size(); iz++)
       for (int ty = 0; ty < nty; ty++)
@@ -3759,7 +3852,7 @@ int tb_plan(mnl_fields *F) {
     std::vector<size_t> open;  // unpaired strips, by (rows, planes, code)
     for (const RI &it : heavy) {
       const int w = (it.g0 >> 16) - (it.g0 & 0xFFFF) + 1;
-      if (((it.code >> 24) & 7) != 1 || w > 32) {
+      if (((it.code >> 24) & 7) != 1 || w > 32 || ((it.code >> 30) & 1)) {
         keep.push_back(it);
         continue;
       }
@@ -3779,13 +3872,13 @@ int tb_plan(mnl_fields *F) {
     }
     heavy.swap(keep);
   }
+  // longest first; a narrow strip plane costs ~1.3 wide-tile planes (item clock, round 5)
   auto longest_first = [](std::vector<RI> &v) {
-    std::stable_sort(v.begin(), v.end(), [](const RI &x, const RI &y) { return x.planes > y.planes; });
+    auto cost = [](const RI &r) { return r.planes * (((r.code >> 30) & 1) ? 1.3 : 1.0); };
+    std::stable_sort(v.begin(), v.end(), [&](const RI &x, const RI &y) { return cost(x) > cost(y); });
   };
   longest_first(heavy);
   longest_first(lean);
-  std::vector<double> rcost;  // estimated time of a rim item: planes (+ the halo plane), PML
-                              // bodies about twice a lean plane
   // items that need no slab-face data first (multi-rank: they run before the face exchange)
   std::vector<RI> order;
   for (int dep = 0; dep < 2; dep++)
@@ -3799,7 +3892,6 @@ int tb_plan(mnl_fields *F) {
       F->tb_ritems.push_back(it.code);
       F->tb_rgeo.push_back(it.g0), F->tb_rgeo.push_back(it.g1), F->tb_rgeo.push_back(it.g2);
       F->tb_rgeo.push_back(it.g3);
-      rcost.push_back((it.planes + 1) * (((it.code >> 24) & 7) ? 2.0 : 1.0));
     }
   // ---- two-step items: 56 x 12 own points, z chunks of tz planes (automatic: the length
   // whose item count fills whole rounds of one workgroup per CU best, with the three
@@ -3825,15 +3917,18 @@ int tb_plan(mnl_fields *F) {
     }
   }
   F->tb_cells = F->tb_border = 0;
-  std::vector<int> t_inner, t_outer;
   for (const Box &b : two) {
     const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + TB_OY - 1) / TB_OY;
     const int nz = b.hi[2] - b.lo[2] + 1, nch = (nz + tz - 1) / tz;
     for (int ch = 0; ch < nch; ch++)
       for (int ty = 0; ty < nty; ty++)
-        for (int x0 = b.lo[0]; x0 <= b.hi[0]; x0 += TB_OX) {
+        for (int x0 = b.lo[0]; x0 <= b.hi[0];) {
+          // lanes from the 64-byte line at or below x0 - 2 (TB_HX = 4 columns left of x0 when
+          // x0 = 4 mod 8); own columns up to lane 59, so the next item starts 4 mod 8 again
+          const int lx = (x0 - 2) >> 3 << 3;
           Box o;
-          o.lo[0] = x0, o.hi[0] = std::min(x0 + TB_OX - 1, b.hi[0]);
+          o.lo[0] = x0, o.hi[0] = std::min(lx + TB_HX + TB_OX - 1, b.hi[0]);
+          x0 = o.hi[0] + 1;
           o.lo[1] = b.lo[1] + (int)((long long)ny * ty / nty);
           o.hi[1] = b.lo[1] + (int)((long long)ny * (ty + 1) / nty) - 1;
           o.lo[2] = b.lo[2] + (int)((long long)nz * ch / nch);
@@ -3858,18 +3953,12 @@ int tb_plan(mnl_fields *F) {
               nb += fc;
             }
           }
-          // outer: the distance-2 footprint meets the rim (reads rim values of step n)
-          Box fp = o;
-          for (int k = 0; k < 3; k++) fp.lo[k] -= 2, fp.hi[k] += 2;
-          bool outer = false;
-          for (const Box &r : rim) outer = outer || box_meets(fp, r);
-          (outer ? t_outer : t_inner).push_back((int)F->tb_items.size());
           TB2Item it;
           it.x = o.lo[0] | (o.hi[0] << 16);
           it.y = o.lo[1] | (o.hi[1] << 16);
           it.z = o.lo[2] | ((o.hi[2] + 1) << 16);
           it.faces = faces;
-          it.bx = it.by = it.bz = -1, it.pad = 0;
+          it.bx = it.by = it.bz = -1, it.lx = lx;
           {
             Box u;  // bounding box of the item's intersections with the DFT boxes
             bool any = false;
@@ -3903,36 +3992,6 @@ int tb_plan(mnl_fields *F) {
           F->tb_border += nb;  // an upper bound (edges counted twice)
         }
   }
-  // ---- phase orders: the two kinds interleaved so that both advance in proportion to their
-  // estimated work (a two-step item: two steps of a plane per plane, plus three halo planes)
-  auto tcost = [&](int i) {
-    const TB2Item &q = F->tb_items[i];
-    return ((q.z >> 16) - (q.z & 0xFFFF) + 3) * 2.2;
-  };
-  auto interleave = [&](const std::vector<int> &tl, bool with_rim) {
-    std::vector<int> o;
-    double rt = 0, tt = 0, ra = 0, ta = 0;
-    if (with_rim)
-      for (double c : rcost) rt += c;
-    for (int i : tl) tt += tcost(i);
-    size_t i = 0, j = 0;
-    const size_t nr = with_rim ? rcost.size() : 0;
-    while (i < nr || j < tl.size()) {
-      if (j >= tl.size() || (i < nr && ra / rt <= ta / tt)) {
-        o.push_back((int)i);
-        ra += rcost[i++];
-      } else {
-        o.push_back(~tl[j]);
-        ta += tcost(tl[j++]);
-      }
-    }
-    return o;
-  };
-  F->tb_order[0] = interleave(t_inner, true);
-  F->tb_order[1] = interleave(t_inner, false);
-  F->tb_order[2] = interleave(t_outer, true);
-  for (int k = 0; k < 3; k++)
-    if (dev_upload(F, &F->d_tb_order[k], F->tb_ocap[k], F->tb_order[k])) return -1;
   // ---- upload, palette-uniform flags, mixed-palette cell counts (traffic model)
   if (dev_upload(F, &F->d_tb_ritems, F->tb_rcap, F->tb_ritems) ||
       dev_upload(F, &F->d_tb_rgeo, F->tb_gcap, F->tb_rgeo) ||
@@ -3980,20 +4039,72 @@ int tb_plan(mnl_fields *F) {
   if (F->tb_stats)
     fprintf(stderr, "tb: L2 [%d..%d]x[%d..%d]x[%d..%d], %zu holes, %zu two-step boxes, %zu rim "
             "boxes; %d two-step items (%d planes, %.0f cells, %.0f border), %d rim items "
-            "(%.0f cells, %.0f lean); inner %zu, outer %zu\n",
+            "(%.0f cells, %.0f lean, %d narrow strips)\n",
             L2.lo[0], L2.hi[0], L2.lo[1], L2.hi[1], L2.lo[2], L2.hi[2], holes.size(), two.size(),
             rim.size(), ni, tz, F->tb_cells, F->tb_border, nr, F->rim_cells, F->rim_lean,
-            t_inner.size(), t_outer.size());
+            F->tb_nnarrow);
   return 0;
+}
+
+// The middle buffer set of the pairs (the arrays the fused step ping-pongs: B, D, stored E,
+// separate H, f_u of B).  Allocated on the first pair; when device memory is short, whatever
+// this call allocated is freed again and temporal blocking is switched off on this rank (the
+// ranks agree in tb_usable), so a grid that fits with two sets keeps stepping one step at a
+// time instead of failing.  MNL_TB_OOM=1 simulates the failure (tests).
+int tb_mid_alloc(mnl_fields *F) {
+  DevFields &f = F->f;
+  std::vector<double **> got;
+  bool bad = false;
+  auto one = [&](double **pp, double *cur) {
+    if (!cur || *pp || bad) return;
+    void *q = nullptr;
+    if (F->tb_oom_test || hipMalloc(&q, F->nlocal * 8) != hipSuccess) {
+      bad = true;
+      (void)hipGetLastError();
+      return;
+    }
+    *pp = (double *)q;
+    got.push_back(pp);
+  };
+  for (int d = 0; d < 3; d++) {
+    one(&F->pp3_B[d], f.B[d]);
+    one(&F->pp3_D[d], f.D[d]);
+    one(&F->pp3_E[d], f.E[d]);
+    one(&F->pp3_H[d], f.H[d]);
+    one(&F->pp3_UB[d], f.UB[d]);
+  }
+  if (!bad) {
+    for (double **pp : got) F->dev_allocs.push_back(*pp);
+    return 0;
+  }
+  for (double **pp : got) {
+    (void)hipFree(*pp);
+    *pp = nullptr;
+  }
+  (void)hipGetLastError();
+  F->tb_enabled = false;
+  F->tb_oom = true;
+  if (g_verbosity > 0 && F->rank == 0)
+    fprintf(stderr, "meep_nl_amd: not enough device memory for the temporal-blocking buffer set; "
+                    "stepping one step at a time\n");
+  return 1;
 }
 
 // Can the batch step in pairs?  Builds the plan when needed (-1: HIP error).
 int tb_usable(mnl_fields *F, bool *ok) {
   *ok = false;
-  bool local = F->tb_enabled && F->fused && F->tile_mode && F->fgeo.ngen == 0 &&
+  // (no chi(2) NR box, upstream nonlinearity or polarization: the pairs have no E phase of
+  // their own; today ngen == 0 implies it, stated so it does not hang on the tile geometry)
+  bool local = F->tb_enabled && F->fused && F->tile_mode && F->fgeo.ngen == 0 && !F->nr &&
+               !F->upnl && F->f.npol == 0 &&
                F->S.dim == 3 && F->slab_dir == 2 &&
-               (F->dfts.empty() || (F->nranks == 1 && F->tb_split));
+               (F->dfts.empty() || F->nranks == 1);
   if (local && tb_plan(F)) return -1;
+  if (local && F->tb_have && tb_mid_alloc(F)) local = false;
+  if (F->tb_stats && !(local && F->tb_have))
+    fprintf(stderr, "tb: no pairs (enabled %d fused %d tile %d ngen %d dim %d slab %d dfts %zu have %d)\n",
+            (int)F->tb_enabled, (int)F->fused, (int)F->tile_mode, F->fgeo.ngen, F->S.dim,
+            F->slab_dir, F->dfts.size(), (int)F->tb_have);
   local = local && F->tb_have;
   if (F->nranks > 1) {  // every rank or none (their exchange sequences differ by mode)
     double v = local ? 1.0 : 0.0;
@@ -4078,13 +4189,14 @@ int tb_src(mnl_fields *F, const SrcDev &s, double *const D[3]) {
   return 0;
 }
 
-// the middle set starts as a copy of the state (entries no launch writes: walls, ghosts)
+// the middle set starts as a copy of the state (entries no launch writes: walls, ghosts);
+// its arrays exist (tb_mid_alloc ran in tb_usable)
 int tb_mid_init(mnl_fields *F) {
   if (F->tb_mid_fresh) return 0;
   DevFields &f = F->f;
   auto fresh = [&](double **pp, double *cur) -> int {
     if (!cur) return 0;
-    if (!*pp && dev_alloc(F, pp, F->nlocal, false)) return -1;
+    if (!*pp) return fail("temporal blocking: middle buffer set missing");
     HIPCHK(hipMemcpyAsync(*pp, cur, F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
     return 0;
   };
@@ -4106,28 +4218,12 @@ void swap_cur_nxt(DevFields &f) {
   }
 }
 
-// The rim's step n+1 of the last pair (pending until the next pair's phase A): alone.
-template <class EB, class EE>
-int tb_drain(mnl_fields *F, EB &ev_begin, EE &ev_end) {
-  if (!F->tb_pending) return 0;
-  F->tb_pending = false;
-  const FusedArgs &fa = fused_args(F);
-  const Set5 cur = set_cur(F), mid = set_mid(F);
-  FusedArgs r = rim_args(F, fa, mid, cur);
-  const int k = ev_begin(TM_RIM);
-  const int kr = k_tile_items(r, F->d_tb_ritems, F->d_tb_rgeo, r.tflag, (int)F->tb_ritems.size(), 4,
-                              F->stream, F->ctr_base);
-  ev_end(k);
-  if (kr) return fused_fail("rim kernel launch failed", kr);
-  if (tb_src(F, F->tb_pend_src, cur.D)) return -1;
-  return nan_launch(F);  // the state of the last pair is complete now
-}
-
-// Steps n, n+1 (sources s0, s1).  Pipelined (default): phase A = the previous pair's rim step
-// (mid -> cur) beside the inner two-step items (cur -> nxt); phase B = this pair's rim step n
-// (cur -> mid) beside the outer two-step items (cur -> nxt, border -> mid); the rim's step
-// n+1 stays pending for the next phase A or tb_drain.  Every launch reads and writes disjoint
-// points of its sets (DESIGN.md section 24 has the hazard argument).
+// Steps n, n+1 (sources s0, s1) as three launches: L = the two-step
+// kernel (cur -> nxt for the L2 points, their border values of step n+1 -> mid), R1 = the
+// tile kernel over the rim items (cur -> mid), source(n) into mid, R2 = the rim items again
+// (mid -> nxt), source(n+1) into nxt.  L runs first: the narrow x-face strips of R1 / R2 read
+// the new B of their x-1 column (two-step points) from mid / nxt.  Every launch reads one set
+// and writes disjoint points of others.
 template <class EB, class EE>
 int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end,
             long long t_mid) {
@@ -4136,57 +4232,39 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   const Set5 cur = set_cur(F), mid = set_mid(F), nxt = set_nxt(F);
   const TB2Args t = tb_args(F, cur, mid, nxt);
   const int nr = (int)F->tb_ritems.size();
-  int k, kr;
-  if (F->tb_split) {  // default: R1, two-step kernel, R2 as three launches
-    const FusedArgs r1 = rim_args(F, fa, cur, mid), r2 = rim_args(F, fa, mid, nxt);
-    k = ev_begin(TM_RIM);
-    kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
-    ev_end(k);
-    if (kr) return fused_fail("rim kernel launch failed", kr);
-    if (tb_src(F, s0, mid.D)) return -1;
-    k = ev_begin(TM_TB);
-    kr = k_tb2(t, F->stream, F->ctr_base);
-    ev_end(k);
-    if (kr) return fused_fail("two-step kernel launch failed", kr);
-    if (dft_due(F, t_mid)) {  // fields::update_dfts after the pair's first step, from mid
-      DevFields fm = F->f;
-      for (int d = 0; d < 3; d++)
-        fm.B[d] = mid.B[d], fm.D[d] = mid.D[d], fm.E[d] = mid.E[d], fm.H[d] = mid.H[d];
-      k = ev_begin(TM_DFT);
-      const int r = dft_update(F, t_mid, &fm);
-      ev_end(k);
-      if (r) return -1;
-    }
-    k = ev_begin(TM_RIM);
-    kr = k_tile_items(r2, r2.titems, r2.tgeo, r2.tflag, nr, 4, F->stream, F->ctr_base);
-    ev_end(k);
-    if (kr) return fused_fail("rim kernel launch failed", kr);
-    if (tb_src(F, s1, nxt.D)) return -1;
-    swap_cur_nxt(F->f);
-    nan_count(F, 2);
-    return nan_launch(F);
-  }
-  // phase A
-  const FusedArgs ra = rim_args(F, fa, mid, cur);
-  const int oa = F->tb_pending ? 0 : 1;
-  k = ev_begin(TM_TB);
-  kr = k_tb_phase(ra, t, F->d_tb_order[oa], (int)F->tb_order[oa].size(), F->stream, F->ctr_base);
+  const FusedArgs r1 = rim_args(F, fa, cur, mid), r2 = rim_args(F, fa, mid, nxt);
+  int k = ev_begin(TM_TB);
+  int kr = k_tb2(t, F->stream, F->ctr_base);
   ev_end(k);
-  if (kr) return fused_fail("temporal-blocking phase launch failed", kr);
-  if (F->tb_pending && tb_src(F, F->tb_pend_src, cur.D)) return -1;
-  if (F->tb_pending && nan_launch(F)) return -1;  // the previous pair's state is complete
-  // phase B
-  const FusedArgs rb = rim_args(F, fa, cur, mid);
-  k = ev_begin(TM_TB);
-  kr = k_tb_phase(rb, t, F->d_tb_order[2], (int)F->tb_order[2].size(), F->stream, F->ctr_base);
+  if (kr) return fused_fail("two-step kernel launch failed", kr);
+  k = ev_begin(TM_RIM);
+  kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
   ev_end(k);
-  if (kr) return fused_fail("temporal-blocking phase launch failed", kr);
+  if (kr) return fused_fail("rim kernel launch failed", kr);
   if (tb_src(F, s0, mid.D)) return -1;
+  // the guard of the middle step (its terms' points hold step n+1 in mid: rim items, or the
+  // two-step items' store box)
+  nan_count(F, 1);
+  F->nan_at = t_mid;
+  if (nan_launch(F, nullptr, mid.E, mid.D)) return -1;
+  if (dft_due(F, t_mid)) {  // fields::update_dfts after the pair's first step, from mid
+    DevFields fm = F->f;
+    for (int d = 0; d < 3; d++)
+      fm.B[d] = mid.B[d], fm.D[d] = mid.D[d], fm.E[d] = mid.E[d], fm.H[d] = mid.H[d];
+    k = ev_begin(TM_DFT);
+    const int r = dft_update(F, t_mid, &fm);
+    ev_end(k);
+    if (r) return -1;
+  }
+  k = ev_begin(TM_RIM);
+  kr = k_tile_items(r2, r2.titems, r2.tgeo, r2.tflag, nr, 4, F->stream, F->ctr_base);
+  ev_end(k);
+  if (kr) return fused_fail("rim kernel launch failed", kr);
+  if (tb_src(F, s1, nxt.D)) return -1;
   swap_cur_nxt(F->f);
-  F->tb_pending = true;
-  F->tb_pend_src = s1;
-  nan_count(F, 2);  // a due guard runs once the pending rim step has (next phase A / drain)
-  return 0;
+  nan_count(F, 1);
+  F->nan_at = t_mid + 1;
+  return nan_launch(F);
 }
 
 // Multi-rank pair (one rank of a z-slab decomposition; fused, no D source on the top
@@ -4240,7 +4318,8 @@ int tb_face_chain(mnl_fields *F, const Set5 &o, const Set5 &n, const SrcDev &src
 }
 
 template <class EB, class EE>
-int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end) {
+int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE &ev_end,
+                  long long t_mid) {
   if (tb_mid_init(F)) return -1;
   const FusedArgs &fa = fused_args(F);
   const Set5 cur = set_cur(F), mid = set_mid(F), nxt = set_nxt(F);
@@ -4261,6 +4340,9 @@ int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begi
   if (kr) return fused_fail("rim kernel launch failed", kr);
   HIPCHK(hipEventRecord(F->ev_early, F->stream));
   if (tb_face_chain(F, cur, mid, s0, F->ev_early)) return -1;
+  nan_count(F, 1);  // the middle step's guard, after its top plane and sources (s_comm)
+  F->nan_at = t_mid;
+  if (nan_launch(F, F->s_comm, mid.E, mid.D)) return -1;
   // R2: the items without slab-face reads beside the chain, then the others
   FusedArgs r2 = rim_args(F, fa, mid, nxt);
   r2.wg_limit = cus - TB_RES_CUS;
@@ -4278,7 +4360,8 @@ int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begi
   if (tb_face_chain(F, mid, nxt, s1, F->ev_early)) return -1;
   swap_cur_nxt(F->f);
   F->tb_chain_pending = true;  // a one-step step next waits for it (tb_chain_join)
-  nan_count(F, 2);
+  nan_count(F, 1);
+  F->nan_at = t_mid + 1;
   return nan_launch(F, F->s_comm);  // after the chain: the top plane of the new state
 }
 
@@ -4325,9 +4408,10 @@ int step_batch(mnl_fields *F, int nsteps) {
     }
   }
   if (F->fused && F->nranks > 1 && multi_begin(F)) return -1;
-  bool tb_ok = false;  // step in pairs (temporal blocking)
-  if (nsteps >= 2 && tb_usable(F, &tb_ok)) return -1;
   if (nan_terms_build(F)) return -1;  // NaN guard terms of this batch's mode / arrays
+  bool tb_ok = false;  // step in pairs (temporal blocking; its plan stores the guard's points)
+  if (nsteps >= 2 && tb_usable(F, &tb_ok)) return -1;
+  if (nsteps >= 2) F->tb_last = tb_ok;
   const double dt = F->dt;
   // per-step source values, computed on the host exactly as the reference
   size_t nB = F->srcB_idx.size(), nD = F->srcD_idx.size(), nI = F->isrc_idx.size();
@@ -4336,7 +4420,7 @@ int step_batch(mnl_fields *F, int nsteps) {
   const size_t ng = F->groups.size();
   size_t per = (nB || nD ? 4 * ng : 0) + nI;
   const size_t jofs = (nB || nD) ? 4 * ng : 0;
-  const int CH = 1024;
+  const int CH = NAN_CH;  // steps per source table / NaN flag read
   std::vector<EvPair> evs;
   size_t evi = 0;
   auto ev_begin = [&](int cat) -> int {
@@ -4448,17 +4532,18 @@ int step_batch(mnl_fields *F, int nsteps) {
       is.val = vs + jofs;  // kernels index val[step * n + orig] with step 0
       if (tb_ok && s + 1 < ns) {  // steps s and s + 1 as one pair (no DFT)
         const SrcDev sD1 = src_dev(F, 1, vs + per + 2 * ng);
-        if ((F->nranks > 1 ? tb_pair_multi(F, sD, sD1, ev_begin, ev_end)
+        if ((F->nranks > 1 ? tb_pair_multi(F, sD, sD1, ev_begin, ev_end, F->t + s + 1)
                            : tb_pair(F, sD, sD1, ev_begin, ev_end, F->t + s + 1)))
           return -1;
         s++;
         if (post_step(s)) return -1;  // DFT of the pair's second step (the new state)
         continue;
       }
-      if (tb_drain(F, ev_begin, ev_end) || tb_chain_join(F)) return -1;
+      if (tb_chain_join(F)) return -1;
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
         nan_count(F, 1);
+        F->nan_at = F->t + s + 1;
         if (nan_launch(F)) return -1;
         continue;
       }
@@ -4625,9 +4710,9 @@ int step_batch(mnl_fields *F, int nsteps) {
         }
       if (post_step(s)) return -1;
       nan_count(F, 1);
+      F->nan_at = F->t + s + 1;
       if (nan_launch(F)) return -1;
     }
-    if (tb_drain(F, ev_begin, ev_end)) return -1;  // sources of this batch's table
     if (!F->dfts.empty()) {
       const int k = ev_begin(TM_DFTF);
       for (auto &o : F->dfts)
@@ -4636,6 +4721,7 @@ int step_batch(mnl_fields *F, int nsteps) {
     }
     F->t += ns;
     if (flush_events() != 0) return -1;
+    if (nan_result(F)) return -1;  // stop within NAN_CH steps of a failing guard
   }
   if (F->s_comm) {
     HIPCHK(hipStreamSynchronize(F->s_comm));
@@ -4697,15 +4783,17 @@ int nan_terms_build(mnl_fields *F) {
   return 0;
 }
 
-// launch the guard on the current state if one is due
-int nan_launch(mnl_fields *F, hipStream_t st) {
+// launch the guard on the current state (or the given E / D arrays: the middle state of a
+// pair) if one is due
+int nan_launch(mnl_fields *F, hipStream_t st, double *const *Es, double *const *Ds) {
   if (!F->nan_due) return 0;
   F->nan_due = false;
   if (!st) st = F->stream;
   if (!F->d_nanflag && dev_alloc(F, &F->d_nanflag, 2)) return -1;  // zeroed; reset by nan_result
   const double *E[3], *D[3], *U[3];
-  for (int d = 0; d < 3; d++) E[d] = F->f.E[d], D[d] = F->f.D[d], U[d] = F->f.inveps[d];
-  if (k_nan_check(F->nan_terms, E, D, U, F->d_nanflag, 0, st))
+  for (int d = 0; d < 3; d++)
+    E[d] = Es ? Es[d] : F->f.E[d], D[d] = Ds ? Ds[d] : F->f.D[d], U[d] = F->f.inveps[d];
+  if (k_nan_check(F->nan_terms, E, D, U, F->d_nanflag, (int)F->nan_at, st))
     return fail("NaN guard launch failed");
   F->nan_launched++;
   return 0;
@@ -4720,17 +4808,30 @@ void nan_count(mnl_fields *F, int k) {
   }
 }
 
-// end of a batch (stream synchronized): the reference's abort if a guard saw NaN / Inf
+// end of a chunk of a batch: the reference's abort (src/step.cpp:138-139) if a guard saw NaN /
+// Inf.  The time goes back to the first failing step (the step after which the reference's
+// check aborts); the steps the device ran past it inside the chunk (at most NAN_CH) are not
+// counted.  Multi-rank: every rank learns the earliest failing step of any rank.
 int nan_result(mnl_fields *F) {
   if (F->nan_launched == 0) return 0;  // the same on every rank (same step counts)
+  if (F->s_comm) HIPCHK(hipStreamSynchronize(F->s_comm));
+  HIPCHK(hipStreamSynchronize(F->stream));
   int h[2] = {0, 0};
   HIPCHK(hipMemcpy(h, F->d_nanflag, sizeof h, hipMemcpyDeviceToHost));
   if (h[0]) HIPCHK(hipMemset(F->d_nanflag, 0, sizeof h));
   F->nan_launched = 0;
-  bool ok = h[0] == 0;
-  if (F->nranks > 1 && F->comm->agree_ok(ok, F->stream)) ok = false;
-  if (!ok) return fail("simulation fields are NaN or Inf");
-  return 0;
+  long long bad_t = h[0] ? (long long)h[1] : -1;
+  if (F->nranks > 1) {
+    std::vector<double> v(F->nranks, 0.0);
+    v[F->rank] = double(bad_t);
+    if (F->comm->allreduce_sum(v.data(), F->nranks, F->stream)) return fail("allreduce failed");
+    bad_t = -1;
+    for (double x : v)
+      if (x >= 0 && (bad_t < 0 || (long long)x < bad_t)) bad_t = (long long)x;
+  }
+  if (bad_t < 0) return 0;
+  F->t = bad_t;
+  return fail("simulation fields are NaN or Inf (at time step " + std::to_string(bad_t) + ")");
 }
 
 int finalize_fields(mnl_fields *F) {
@@ -5727,7 +5828,6 @@ int energy_in_box(mnl_fields *F, int which, const double wmin[3], const double w
 // step (default every step; counted across calls) on the device, its flag read at the end of
 // each batch; the first step after construction (or after E / H were set directly) runs
 // unfused (see e_first_done)
-static int g_verbosity = 1;  // meep::verbosity (src/meep.hpp: default 1)
 
 static double wall_now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -5910,7 +6010,8 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tb = getenv("MNL_TB")) F->tb_enabled = atoi(tb) != 0, F->tb_env = true;
   if (const char *tz = getenv("MNL_TB_ZCHUNK"))
     F->tb_zchunk = std::max(0, atoi(tz)), F->tb_zchunk_env = true;
-  if (const char *ts = getenv("MNL_TB_SPLIT")) F->tb_split = atoi(ts) != 0;
+  if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
+  if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
@@ -6946,7 +7047,7 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
     // the pairs (two phase launches each, the drains of the rim's last step), bytes per pair =
     // the two-step items' two steps (B, D read once and written once, the palette word where
     // the item is mixed, the border points' step n+1 B, D) + two rim steps.  6 = the rim
-    // launches that run alone (drains; every rim step with MNL_TB_SPLIT), one step each
+    // launches, one step each
     int nu = 0;
     for (int d = 0; d < 3; d++) nu += F->f.inveps[d] ? 1 : 0;
     const double ub = F->d_uidx ? 4.0 : 8.0 * nu;
@@ -6962,7 +7063,7 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
               (F->d_uidx ? F->rim_cells_nu : F->rim_cells) * ub;
     }
     if (which == 5) {
-      *launches = F->timer_count[TM_TB] / (F->tb_split ? 1 : 2);
+      *launches = F->timer_count[TM_TB];
       *total_ms = F->timer_ms[TM_TB] + F->timer_ms[TM_RIM];
       *bytes_per_launch = tb_b + 2.0 * rim_b;
     } else {
@@ -7024,7 +7125,7 @@ int mnl_fields_set_temporal_blocking(mnl_fields *F, int on) {
 
 int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
   if (!F || !out || n < 1) return fail("bad argument");
-  const double v[12] = {F->fused && F->tb_have && F->tb_enabled ? 1.0 : 0.0,
+  const double v[12] = {F->fused && F->tb_have && F->tb_enabled && F->tb_last ? 1.0 : 0.0,
                        F->tb_cells,
                        F->tb_border,
                        F->tb_cells_nu,
@@ -7034,7 +7135,7 @@ int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
                        double(F->tb_ritems.size()),
                        F->tb_items.empty() ? 0.0 : double((F->tb_items[0].z >> 16) -
                                                           (F->tb_items[0].z & 0xFFFF)),
-                       F->tb_split ? 1.0 : 0.0,
+                       double(F->tb_nnarrow),
                        F->tb_enabled ? 1.0 : 0.0,
                        double(F->tb_zchunk)};  // the setting (0: automatic)
   for (int i = 0; i < n && i < 12; i++) out[i] = v[i];
@@ -7044,7 +7145,8 @@ int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
 int mnl_fields_mode(mnl_fields *F, int *fused) {
   if (!F) return fail("null fields");
   *fused = (F->fused ? 1 : 0) | (F->fused && F->d_uidx ? 2 : 0) | (F->contig ? 4 : 0) |
-           (F->fused && F->tile_mode ? 16 : 0) | (std::min(F->contig_fallbacks, 255) << 8);
+           (F->fused && F->tile_mode ? 16 : 0) | (F->fused && F->fused_concurrent ? 32 : 0) |
+           (std::min(F->contig_fallbacks, 255) << 8);
   return 0;
 }
 

@@ -343,9 +343,11 @@ struct FusedArgs {
 
 // Temporal blocking: two Yee steps per z-march over the region L2
 // (points whose L-infinity distance-2 neighbourhood lies in the lean box and holds no
-// source point).  A workgroup's 64 x 16 lanes (one row per wave) cover own columns x0 ..
-// x0+55 (lanes 4 .. 59) and own rows y0 .. y0+11 (waves 2 .. 13); step n runs on every lane,
-// step n+1 is valid on lanes 2 .. 61 and waves 2 .. 13.
+// source point).  A workgroup's 64 x 16 lanes (one row per wave) cover columns lx .. lx+63
+// (lx on a 64-byte line) and rows y0-2 .. y0+13; own columns x0 .. x1 lie in lanes 2 .. 61
+// (x0 = lx + 4, x1 = x0 + 55 except the first item of a row of items, which starts wherever
+// L2 starts) and own rows y0 .. y0+11 (waves 2 .. 13); step n runs on every lane, step n+1
+// is valid on lanes 2 .. 61 and waves 2 .. 13.
 constexpr int TB_LX = 64, TB_LY = 16, TB_HX = 4, TB_OX = 56, TB_HY = 2, TB_OY = 12;
 constexpr int TB_MAXCH = 512;  // planes per item (any length: the march keeps 3 planes)
 struct TB2Item {
@@ -357,7 +359,8 @@ struct TB2Item {
   // a box of own points whose step n+1 values are also stored into the middle set (the DFT
   // monitors sample step n+1 there): x0 | x1 << 16, y0 | y1 << 16, z0 | z1 << 16 (inclusive);
   // bx < 0: none
-  int bx, by, bz, pad;
+  int bx, by, bz;
+  int lx;     // column of lane 0 (a multiple of 8: 64-byte line)
 };
 struct TB2Args {
   int n;                  // items
@@ -394,11 +397,6 @@ struct NanTerms {
 int k_nan_check(const NanTerms &t, const double *const E[3], const double *const D[3],
                 const double *const U[3], int *flag, int step, void *stream);
 int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases);
-// one phase of a pair: rim items (tile kernel, pointer set of a; a.titems / tgeo / tflag
-// index the rim list) and two-step items (t) from one queue: order[v] >= 0 rim item, < 0
-// two-step item ~order[v]; counter line t.ctr_line
-int k_tb_phase(const FusedArgs &a, const TB2Args &t, const int *order, int n, void *stream,
-               unsigned long long *bases);
 int k_tb2_uniform(const TB2Args &a, unsigned *flags, void *stream);
 // the tile kernel over an explicit item list (FusedArgs::tgeo boxes), counter line `line`
 int k_tile_items(const FusedArgs &a, const int *items, const int *geo, const unsigned *flags,

@@ -3024,21 +3024,331 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
 #undef F
 #undef Wz
 
+// ---------------------------------------------------------------------------
+// Narrow x-face strip body (temporal-blocking rim, DESIGN.md section 24, item bit 30).  The
+// rim's x-face strips are 16 columns wide (one 128-byte line per row); in the 64-lane row
+// layout a strip filled 16-32 of a wave's 64 lanes and cost a whole tile per plane.  Here all
+// 1024 lanes are own-like: wave w holds rows 4w .. 4w+3 (lane -> column lane & 15, row
+// 4w + lane / 16; row 0 = the y-1 halo row, B recomputed there), i.e. 16 columns x 63 own rows
+// per plane.  The halo columns are loads only, one slot per thread 0..142:
+//   * E of the x+16 column (rows 0..63) and of the y+64 row (columns 0..15), from the old set;
+//   * B_new (= H: the column is lean) of the x-1 column (rows 1..63), read from this launch's
+//     output set: the host takes this body only where x0 = 0 (no x-1 column) or where the x-1
+//     column of every own row and plane is a two-step point, whose new values the two-step
+//     kernel stored there before this launch (step n+1 border values in the middle set for R1,
+//     its own step n+2 values in the next set for R2).
+// AX = 1 (PML along x only) with every footprint point owned in y and z (OWNC): the update is
+// pml_body<AX = 1, OWNC>'s, operand for operand (src/step_generic.cpp:69-253, 576-906).
+constexpr int SW_N = 16, SR_N = 64, SXL = SW_N + 2;
+template <int UMODE>
+__device__ __forceinline__ void strip_body(const FusedArgs &a, const ItemGeo &it, unsigned uw,
+                                           const double (*sU)[256], double (*sE)[SR_N + 1][SXL],
+                                           double (*sB)[SR_N][SXL], PTabL &P) {
+  constexpr bool HAS_U = UMODE != 0;
+  constexpr bool RSAT = MNL_RS_AT;
+  const int x0 = it.x0, x1 = it.x1, y0 = it.y0, y1 = it.y1, zs = it.zs, ze = it.ze;
+  // ---- x PML tables of the footprint (positions 0 .. 17 = columns x0-1 .. x0+16) -> LDS
+  for (int i = threadIdx.x; i < 2 * SXL; i += 1024) {
+    const int pos = i >> 1, sft = i & 1;
+    const int jj = min(max(x0 - 1 + pos, 0), a.N[0] - 1);
+    const int q = 2 * (jj + a.off[0]) + sft;
+    P.v[0][0][sft][pos] = a.tab.kms[0][q];
+    P.v[0][1][sft][pos] = a.tab.siginv[0][q];
+    P.v[0][2][sft][pos] = a.tab.kps[0][q];
+    P.f[0][sft][pos] = a.tab.flag[0][q];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = 4 * w + (lane >> 4), col = 1 + (lane & 15);
+  const int N0 = a.N[0], N1 = a.N[1];
+  const long long st1 = a.st1;
+  const int gx = x0 + (lane & 15), gy = y0 + row;
+  // lanes right of x1 + 1 or below y1 + 1 feed nothing that is stored: no loads
+  const bool inA = gx < N0 && gx <= x1 + 1 && gy < N1 && gy <= y1 + 1;
+  const unsigned cb = (unsigned)((gx + (long long)gy * st1) * 8);
+  const unsigned cbl = inA ? cb : 0u;
+  // x ownership (y, z: every point owned): bit0 = shifted along x, bit1 = unshifted
+  const unsigned ownx = own_bits_of(gx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
+  const bool ox0 = (ownx & 1u) != 0, ox1 = (ownx & 2u) != 0;
+  const bool o0 = inA && ox0, o12 = inA && ox1;  // E comp 0 / comps 1, 2 owned (D loaded)
+  const bool stl = row >= 1 && gx <= x1 && gy <= y1;
+  // ---- halo slot of this thread: 1 = E of the x+16 column (row t), 2 = E of the y+64 row
+  // (column t - 64), 3 = B_new of the x-1 column (row t - 79)
+  const int t = threadIdx.x;
+  const int skind = t < SR_N ? 1 : t < SR_N + SW_N ? 2 : t < 2 * SR_N + SW_N - 1 ? 3 : 0;
+  const int srow = skind == 1 ? t : skind == 2 ? SR_N : skind == 3 ? t - SR_N - SW_N + 1 : 0;
+  const int scol = skind == 1 ? SW_N + 1 : skind == 2 ? 1 + (t - SR_N) : 0;
+  const int hx = x0 - 1 + scol, hy = y0 + srow;
+  const bool hA = skind != 0 && hx >= 0 && hx < N0 && hy < N1 && hy <= y1 + 1;
+  const unsigned hbl = hA ? (unsigned)((hx + (long long)hy * st1) * 8) : cbl;
+  const unsigned hownx = own_bits_of(hx, a.osh_lo[0], a.osh_hi[0], a.oun_lo[0], a.oun_hi[0]);
+  const int hc0 = skind == 2 ? 0 : 1;
+  const int zlo = zs - 1;
+  const unsigned s2 = (unsigned)(a.st2 * 8);
+  const double C = a.C;
+  const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
+#define RSV(x) (RsArr<RSAT>::make((x), nrec))
+#define RS(p) (RsArr<RSAT>::get((p), nrec))
+  const auto pBn0 = RSV(a.Bn[0]);
+  const auto pBn1 = RSV(a.Bn[1]);
+  const auto pBn2 = RSV(a.Bn[2]);
+  const auto pDn0 = RSV(a.Dn[0]);
+  const auto pDn1 = RSV(a.Dn[1]);
+  const auto pDn2 = RSV(a.Dn[2]);
+  const auto pEo0 = RSV(a.E[0]);
+  const auto pEn0 = RSV(a.En[0]);
+  const auto pUBo1 = RSV(a.UBo[1]);
+  const auto pUBn1 = RSV(a.UBn[1]);
+  const auto pHo0 = RSV(a.Ho[0]);
+  const auto pHn0 = RSV(a.Hn[0]);
+  const auto pUD1 = RSV(a.UD[1]);
+  const gdp D0 = sgpr_ptr(a.Do[0]), D1 = sgpr_ptr(a.Do[1]), D2 = sgpr_ptr(a.Do[2]);
+  const gdp E0 = sgpr_ptr(a.E[0]), E1 = sgpr_ptr(a.E[1]), E2 = sgpr_ptr(a.E[2]);
+  const gdp B0 = sgpr_ptr(a.Bo[0]), B1 = sgpr_ptr(a.Bo[1]), B2 = sgpr_ptr(a.Bo[2]);
+  const gdp NB1 = sgpr_ptr(a.Bn[1]), NB2 = sgpr_ptr(a.Bn[2]);
+  const gdp U0 = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[0]) : nullptr;
+  const gdp U1 = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[1]) : nullptr;
+  const gdp U2 = HAS_U && UMODE == 1 ? sgpr_ptr(a.u[2]) : nullptr;
+  const gup uix = (gup)sgpr_ptr(a.uidx);
+#define pu(ui, c) sU[UMODE == 2 ? (c) : 0][((ui) >> (8 * (c))) & 255]
+  const bool uni = __builtin_amdgcn_readfirstlane(uw) != ~0u;
+  const unsigned ufix = (unsigned)((max(x0 - 1, 0) + (long long)max(y0, 0) * st1 +
+                                    (long long)max(zs - 1, 0) * a.st2) * 4);
+#define uoff(o8) (uni ? ufix : ((o8) >> 1))
+  __syncthreads();  // tables visible
+  // x coefficients / flags of this lane's column (T(0, coef, sft) / F(0, sft) of pml_body)
+#define TX(coef, sft) P.v[0][coef][sft][col]
+  const bool fxs = P.f[0][1][col] != 0, fxu = P.f[0][0][col] != 0;
+  const bool Wx = fxs;
+  // slot sources: implicit E (chi1inv * D) where owned and not W-form, else stored E; B_new
+  const bool hW0 = hc0 == 0 && P.f[0][1][scol] != 0;
+  const bool hi0 = hA && skind != 3 && ((hc0 == 0 ? hownx : hownx >> 1) & 1u) && !hW0;
+  const bool hi2 = hA && skind != 3 && ((hownx >> 1) & 1u);
+  const gdp hs0 = skind == 3 ? NB1 : (hi0 ? (hc0 ? D1 : D0) : (hc0 ? E1 : E0));
+  const gdp hs1 = skind == 3 ? NB2 : (hi2 ? D2 : E2);
+  const gdp hU0 = hc0 ? U1 : U0;
+  const bool swave = w < 3;  // waves holding slots (threads 0 .. 142)
+
+  struct SBatch {  // plane k: D(k+1) (or stored E where not owned), u(k+1), stored Ex(k+1),
+                   // B(k), slot values of plane k
+    double d0, d1, d2, u0, u1, u2, es0, b0, b1, b2, h0, h1, hu0, hu1;
+    unsigned ui, hui;
+  };
+#define STRIP_LOAD(QQ, KK) \
+  do { \
+    const unsigned o = cbl + (unsigned)((KK) + 1) * s2; \
+    QQ.d0 = ldg(o0 ? D0 : E0, o); \
+    QQ.d1 = ldg(o12 ? D1 : E1, o); \
+    QQ.d2 = ldg(o12 ? D2 : E2, o); \
+    if (UMODE == 2) { \
+      QQ.ui = ldu(uix, uoff(o)); \
+    } else if (HAS_U) { \
+      QQ.u0 = ldg(U0, o); \
+      QQ.u1 = ldg(U1, o); \
+      QQ.u2 = ldg(U2, o); \
+    } else { \
+      QQ.u0 = QQ.u1 = QQ.u2 = 1.0; \
+    } \
+    QQ.es0 = bld(RS(pEo0), (o0 && Wx) ? o : MNL_OOB); \
+    const unsigned ob = cbl + (unsigned)(KK) * s2; \
+    QQ.b0 = ldg(B0, ob); \
+    QQ.b1 = ldg(B1, row == 0 ? 0u : ob); /* By of the y-1 row feeds no update */ \
+    QQ.b2 = ldg(B2, ob); \
+    QQ.h0 = QQ.h1 = 0.0; \
+    QQ.hu0 = QQ.hu1 = 1.0; \
+    QQ.hui = 0; \
+    if (swave) { \
+      const unsigned oh = hbl + (unsigned)(KK) * s2; \
+      QQ.h0 = ldg(hs0, oh); \
+      QQ.h1 = ldg(hs1, oh); \
+      if (UMODE == 2) { \
+        QQ.hui = ldu(uix, uoff(oh)); \
+      } else if (HAS_U) { \
+        QQ.hu0 = ldg(hU0, oh); \
+        QQ.hu1 = ldg(U2, oh); \
+      } \
+    } \
+  } while (0)
+
+  // prologue: E_old(zs-1): implicit (chi1inv * D) where owned and not W-form, else stored
+  double ex, ey, ez;
+  {
+    const unsigned o = cbl + (unsigned)zlo * s2;
+    const bool i0 = o0 && !Wx;
+    ex = ldg(i0 ? D0 : E0, o);
+    ey = ldg(o12 ? D1 : E1, o);
+    ez = ldg(o12 ? D2 : E2, o);
+    if (UMODE == 2) {
+      const unsigned ui = ldu(uix, uoff(o));
+      if (i0) ex *= pu(ui, 0);
+      if (o12) ey *= pu(ui, 1), ez *= pu(ui, 2);
+    } else if (HAS_U) {
+      if (i0) ex *= ldg(U0, o);
+      if (o12) ey *= ldg(U1, o), ez *= ldg(U2, o);
+    }
+  }
+  SBatch q[2];
+  STRIP_LOAD(q[0], zs - 1);
+  // PML state of plane KK (own lanes): f_u of By (PML along x, shifted), separate Hx, f_u of
+  // Dy (owner lanes); loaded one iteration ahead
+  double ub1 = 0, ho0 = 0, ud1 = 0;
+#define STRIP_AUX(KK) \
+  do { \
+    const unsigned aob = cbl + (unsigned)(KK) * s2; \
+    ub1 = bld(RS(pUBo1), (inA && fxs) ? aob : MNL_OOB); \
+    ho0 = bld(RS(pHo0), (inA && fxu) ? aob : MNL_OOB); \
+    ud1 = bld(RS(pUD1), (stl && fxu) ? aob : MNL_OOB); \
+  } while (0)
+  STRIP_AUX(zs - 1);
+  double dx = 0, dy = 0, dz = 0, hmx = 0, hmy = 0;
+  unsigned uik = 0;
+  double uk0 = 1;
+  const int rowm = row > 0 ? row - 1 : 0;
+  const int ngrp = (ze - zs + 2) / 2;
+  for (int g = 0; g < ngrp; g++) {
+#pragma unroll
+    for (int j = 0; j <= 1; j++) {
+      const int k = zs - 1 + g * 2 + j;
+      STRIP_LOAD(q[(j + 1) & 1], min(k + 1, ze - 1));
+      const SBatch &c = q[j];
+      const bool kin = k >= zs && k < ze;
+      const bool sk = stl && kin;
+      const unsigned ok = cb + (unsigned)k * s2;
+      // E_old(k+1) of this lane
+      double e1x, e1y, e1z;
+      {
+        double v0 = c.d0, v1 = c.d1, v2 = c.d2;
+        if (UMODE == 2) {
+          v0 = v0 * pu(c.ui, 0);
+          v1 = v1 * pu(c.ui, 1);
+          v2 = v2 * pu(c.ui, 2);
+        } else if (HAS_U) {
+          v0 = v0 * c.u0;
+          v1 = v1 * c.u1;
+          v2 = v2 * c.u2;
+        }
+        e1x = o0 ? (Wx ? c.es0 : v0) : c.d0;
+        e1y = o12 ? v1 : c.d1;
+        e1z = o12 ? v2 : c.d2;
+      }
+      sE[0][row][col] = ex;
+      sE[1][row][col] = ey;
+      sE[2][row][col] = ez;
+      if (skind == 1 || skind == 2) {
+        double h0 = c.h0, h1 = c.h1;
+        if (UMODE == 2) {
+          if (hi0) h0 = h0 * pu(c.hui, hc0);
+          if (hi2) h1 = h1 * pu(c.hui, 2);
+        } else if (HAS_U) {
+          if (hi0) h0 = h0 * c.hu0;
+          if (hi2) h1 = h1 * c.hu1;
+        }
+        sE[hc0][srow][scol] = h0;
+        sE[2][srow][scol] = h1;
+      }
+      __syncthreads();
+      // ---- curl B (E_old) with the x-PML branches of step_curl, then H (update_eh)
+      const double Ez_yp = sE[2][row + 1][col], Ex_yp = sE[0][row + 1][col];
+      const double Ey_xp = sE[1][row][col + 1], Ez_xp = sE[2][row][col + 1];
+      double ubx, uby, ubz;
+      const double Bx = pml_curl(c.b0, 0.0, Ez_yp - ez + ey - e1y, C, false, 1.0, 1.0, 1.0, 1.0, &ubx);
+      const double By = pml_curl(c.b1, ub1, e1x - ex + ez - Ez_xp, C, fxs, 1.0, 1.0, TX(0, 1),
+                                 TX(1, 1), &uby);
+      const double Bz = pml_curl(c.b2, 0.0, Ey_xp - ey + ex - Ex_yp, C, false, TX(0, 1), TX(1, 1),
+                                 1.0, 1.0, &ubz);
+      const double Hx = fxu ? ho0 + (TX(2, 0) * Bx - TX(0, 0) * c.b0) : Bx;
+      {
+        const unsigned b0 = (sk && ox1) ? ok : MNL_OOB;
+        const unsigned b12 = (sk && ox0) ? ok : MNL_OOB;
+        bst(RS(pBn0), b0, Bx);
+        bst(RS(pBn1), b12, By);
+        bst(RS(pBn2), b12, Bz);
+        bst(RS(pUBn1), fxs ? b12 : MNL_OOB, uby);
+        bst(RS(pHn0), fxu ? b0 : MNL_OOB, Hx);
+      }
+      sB[0][row][col] = Hx;
+      sB[1][row][col] = By;
+      sB[2][row][col] = Bz;
+      if (skind == 3) {  // B_new == H of the lean x-1 column
+        sB[1][srow][0] = c.h0;
+        sB[2][srow][0] = c.h1;
+      }
+      __syncthreads();
+      // ---- curl D (H_new) with the x-PML branches, then E in the W form where PML lies
+      // along x (src/step_generic.cpp:576-600: W_E(old) == chi1inv * D_old)
+      const double Hz_ym = sB[2][rowm][col], Hx_ym = sB[0][rowm][col];
+      const double Hz_xm = sB[2][row][col - 1], Hy_xm = sB[1][row][col - 1];
+      double udx, udy, udz;
+      const double Dx = pml_curl(dx, 0.0, Hz_ym - Bz + By - hmy, C, false, 1.0, 1.0, 1.0, 1.0, &udx);
+      const double Dy = pml_curl(dy, ud1, hmx - Hx + Bz - Hz_xm, C, fxu, 1.0, 1.0, TX(0, 0),
+                                 TX(1, 0), &udy);
+      const double Dz = pml_curl(dz, 0.0, Hy_xm - By + Hx - Hx_ym, C, false, TX(0, 0), TX(1, 0),
+                                 1.0, 1.0, &udz);
+      {
+        const unsigned e0 = (sk && ox0) ? ok : MNL_OOB;
+        const unsigned e12 = (sk && ox1) ? ok : MNL_OOB;
+        bst(RS(pDn0), e0, Dx);
+        bst(RS(pDn1), e12, Dy);
+        bst(RS(pDn2), e12, Dz);
+        bst(RS(pUD1), fxu ? e12 : MNL_OOB, udy);
+        double k0 = 1;
+        if (UMODE == 2) {
+          k0 = pu(uik, 0);
+        } else if (HAS_U) {
+          k0 = uk0;
+        }
+        const double fw = HAS_U ? Dx * k0 : Dx, fp = HAS_U ? dx * k0 : dx;
+        bst(RS(pEn0), fxs ? e0 : MNL_OOB, ex + (TX(2, 1) * fw - TX(0, 1) * fp));
+      }
+      hmx = Hx;
+      hmy = By;
+      dx = c.d0;
+      dy = c.d1;
+      dz = c.d2;
+      if (UMODE == 2) {
+        uik = c.ui;
+      } else if (HAS_U) {
+        uk0 = c.u0;
+      }
+      ex = e1x;
+      ey = e1y;
+      ez = e1z;
+      STRIP_AUX(min(k + 1, ze - 1));
+    }
+  }
+}
+#undef STRIP_AUX
+#undef STRIP_LOAD
+#undef RS
+#undef RSV
+#undef pu
+#undef uoff
+#undef TX
+
 // body codes of tile items (bits 24-26): 0 lean, 1..7 pml_body<AX = 1, 2, 4, 0, 7, 3, 5>
-// (y-z edges, AX = 6, are few: they take the AX = 7 body); bit 29: OWNC
+// (y-z edges, AX = 6, are few: they take the AX = 7 body); bit 29: OWNC; bit 30 (with body 1
+// and OWNC): the narrow x-face strip body (strip_body)
+// LDS of the tile bodies (one raw array, carved per body shape)
+constexpr int TILE_SE = 3 * (FR + 1) * FXL, TILE_SB = 3 * FR * FXL;
+constexpr int STRIP_SE = 3 * (SR_N + 1) * SXL, STRIP_SB = 3 * SR_N * SXL;
+constexpr int TILE_SM = TILE_SE + TILE_SB > STRIP_SE + STRIP_SB ? TILE_SE + TILE_SB
+                                                                : STRIP_SE + STRIP_SB;
 template <int UMODE, int DIST>
 __device__ __forceinline__ void tile_item_body(const FusedArgs &a, int item, const ItemGeo &itg,
-                                               unsigned uw, const double (*sU)[256],
-                                               double (*sE)[FR + 1][FXL],
-                                               double (*sB)[FR][FXL], PTabL &sP) {
+                                               unsigned uw, const double (*sU)[256], double *sm,
+                                               PTabL &sP) {
   constexpr int MD = MNL_MULTI_DIST;
   const bool ownc = MNL_OWNC && ((item >> 29) & 1);
+  double(*sE)[FR + 1][FXL] = reinterpret_cast<double(*)[FR + 1][FXL]>(sm);
+  double(*sB)[FR][FXL] = reinterpret_cast<double(*)[FR][FXL]>(sm + TILE_SE);
   switch ((item >> 24) & 7) {
     case 0:
       lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
       break;
     case 1:
-      if (itg.xb0 >= 0) {  // paired x-face strips (temporal-blocking rim)
+      if ((item >> 30) & 1) {  // narrow x-face strip (temporal-blocking rim; host: OWNC)
+        strip_body<UMODE>(a, itg, uw, sU, reinterpret_cast<double(*)[SR_N + 1][SXL]>(sm),
+                          reinterpret_cast<double(*)[SR_N][SXL]>(sm + STRIP_SE), sP);
+      } else if (itg.xb0 >= 0) {  // paired x-face strips (temporal-blocking rim)
         if (ownc)
           pml_body<UMODE, DIST, 1, true, true>(a, itg, uw, sU, sE, sB, sP);
         else
@@ -3123,8 +3433,7 @@ __device__ __forceinline__ ItemGeo tile_item_geo(const FusedArgs &a, int item, i
 template <int UMODE, int DIST, bool CLK>
 __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
-  __shared__ double sE[3][FR + 1][FXL];
-  __shared__ double sB[3][FR][FXL];
+  __shared__ double sm[TILE_SM];
   __shared__ PTabL sP;
   __shared__ int s_item, s_idx;
   __shared__ unsigned s_uw;
@@ -3153,7 +3462,7 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
     if (item == -1) break;
-    tile_item_body<UMODE, DIST>(a, item, tile_item_geo(a, item, s_idx), s_uw, sU, sE, sB, sP);
+    tile_item_body<UMODE, DIST>(a, item, tile_item_geo(a, item, s_idx), s_uw, sU, sm, sP);
   }
 }
 
@@ -3386,12 +3695,15 @@ int k_general_uniform(const FusedArgs &a, unsigned *flags, void *stream) {
 }
 
 // Per tile item (index in titems): the palette word if every cell of its footprint
-// (columns x0-1 .. x0+FX, rows y0 .. y0+FR, planes zs-1 .. ze) inside G has the same
-// word, else ~0u (chi1inv is used only at owned points of G).
+// (columns x0-1 .. x0+FX, rows y0 .. y0+FR, planes zs-1 .. ze; a narrow strip: columns
+// x0-1 .. x0+SW_N, rows y0 .. y0+SR_N) inside G has the same word, else ~0u (chi1inv is used
+// only at owned points of G).
 __global__ void tile_uniform_kernel(FusedArgs a, unsigned *flags) {
   const int idx = blockIdx.x;
   const int item = a.titems[idx];
   const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
+  const bool narrow = ((item >> 24) & 7) == 1 && ((item >> 30) & 1);
+  const int fw = narrow ? SW_N : FX, fr = narrow ? SR_N : FR;
   int ix0, iy0, izs, ize;  // tile column start, halo row, planes [izs, ize)
   if (a.tgeo) {
     if (a.tgeo[4 * idx + 3] >= 0) {  // paired item: per-cell palette words
@@ -3405,8 +3717,8 @@ __global__ void tile_uniform_kernel(FusedArgs a, unsigned *flags) {
   } else {
     ix0 = a.xb[tx], iy0 = a.yb[ty] - 1, izs = a.zb[ch], ize = a.zb[ch + 1];
   }
-  const int x0 = max(ix0 - 1, a.G.lo[0]), x1 = min(ix0 + FX, a.G.hi[0]);
-  const int y0 = max(iy0, a.G.lo[1]), y1 = min(iy0 + FR, a.G.hi[1]);
+  const int x0 = max(ix0 - 1, a.G.lo[0]), x1 = min(ix0 + fw, a.G.hi[0]);
+  const int y0 = max(iy0, a.G.lo[1]), y1 = min(iy0 + fr, a.G.hi[1]);
   const int z0 = max(izs - 1, a.G.lo[2]), z1 = min(ize, a.G.hi[2]);
   __shared__ int bad;
   if (threadIdx.x == 0) bad = 0;
@@ -3594,7 +3906,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
   const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
   const int zs = it.z & 0xFFFF, ze = it.z >> 16;
   const int faces = it.faces;
-  const int gx = x0 - TB_HX + lane, gy = y0 - TB_HY + w;
+  const int gx = it.lx + lane, gy = y0 - TB_HY + w;  // lanes from the item's 64-byte line
   const int N0 = a.N[0], N1 = a.N[1], zmax = a.N[2] - 1;
   const int cx = min(max(gx, 0), N0 - 1), cy = min(max(gy, 0), N1 - 1);
   const unsigned col = (unsigned)((cx + (long long)cy * a.st1) * 8);
@@ -3793,82 +4105,6 @@ __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
     else
       tb2_body<UMODE, false>(a, it, uw, sU, sE1, sH1, sE2, sH2);
   }
-}
-
-// One phase of a temporal-blocking pair: rim items of the tile kernel
-// (one step, the pointer set of `a`) and two-step items (`t`) from one queue.  order[v] >= 0
-// is a rim item (index into a.titems / a.tgeo / a.tflag), < 0 the two-step item ~order[v];
-// the host interleaves the two kinds so latency-bound rim items run beside
-// bandwidth-bound two-step items.  The LDS of the two body families is one union.
-constexpr int TILE_LDS_D = 3 * (FR + 1) * FXL + 3 * FR * FXL + (int)(sizeof(PTabL) + 7) / 8;
-constexpr int TB_LDS_D = 4 * 3 * TB_LY * TB_LX;
-template <int UMODE>
-__global__ __launch_bounds__(1024) void tb_phase_kernel(FusedArgs a, TB2Args t, const int *order,
-                                                        int n) {
-  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
-  __shared__ double sm[TILE_LDS_D > TB_LDS_D ? TILE_LDS_D : TB_LDS_D];
-  __shared__ int s_e, s_item;
-  __shared__ unsigned s_uw;
-  if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
-    for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
-  }
-  double(*sE)[FR + 1][FXL] = reinterpret_cast<double(*)[FR + 1][FXL]>(sm);
-  double(*sB)[FR][FXL] = reinterpret_cast<double(*)[FR][FXL]>(sm + 3 * (FR + 1) * FXL);
-  PTabL &sP = *reinterpret_cast<PTabL *>(sm + 3 * (FR + 1) * FXL + 3 * FR * FXL);
-  constexpr int TBA = 3 * TB_LY * TB_LX;
-  double(*sE1)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm);
-  double(*sH1)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm + TBA);
-  double(*sE2)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm + 2 * TBA);
-  double(*sH2)[TB_LY][TB_LX] = reinterpret_cast<double(*)[TB_LY][TB_LX]>(sm + 3 * TBA);
-  unsigned long long *ctr = t.ctr + 16 * t.ctr_line;
-  constexpr int DONE = -2147483647 - 1;
-  for (;;) {
-    if (threadIdx.x == 0) {
-      const unsigned long long v = atomicAdd(ctr, 1ULL) - t.cbase;
-      const int e = (long long)v < n ? order[v] : DONE;
-      s_e = e;
-      s_item = e >= 0 ? a.titems[e] : 0;
-      unsigned uw = ~0u;
-      if (UMODE == 2 && e >= 0 && a.tflag) uw = a.tflag[e];
-      if (UMODE == 2 && e < 0 && e != DONE && t.uflag) uw = t.uflag[~e];
-      s_uw = uw;
-    }
-    __syncthreads();  // also separates LDS use of consecutive items
-    const int e = s_e;
-    if (e == DONE) break;
-    const unsigned uw = s_uw;
-    if (e >= 0) {
-      const int item = s_item;
-      tile_item_body<UMODE, 1>(a, item, tile_item_geo(a, item, e), uw, sU, sE, sB, sP);
-    } else if (UMODE == 2 && __builtin_amdgcn_readfirstlane(uw) != ~0u) {
-      tb2_body<UMODE, true>(t, t.items[~e], uw, sU, sE1, sH1, sE2, sH2);
-    } else {
-      tb2_body<UMODE, false>(t, t.items[~e], uw, sU, sE1, sH1, sE2, sH2);
-    }
-  }
-}
-
-int k_tb_phase(const FusedArgs &a, const TB2Args &t, const int *order, int n, void *stream,
-               unsigned long long *bases) {
-  if (n <= 0) return 0;
-  if (a.nelem * 8 >= (long long)MNL_OOB || t.nelem * 8 >= (long long)MNL_OOB || !t.ctr ||
-      !order || !a.titems || !a.tgeo || t.ctr_line < 0 || t.ctr_line >= FUSED_NCTR)
-    return 2;
-  long long nb = fused_grid_blocks(1);
-  if (nb > n) nb = n;
-  TB2Args tt = t;
-  tt.cbase = bases[t.ctr_line];
-  bases[t.ctr_line] += (unsigned long long)n + nb;
-  const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
-  hipStream_t s = (hipStream_t)stream;
-  const dim3 grd((unsigned)nb), blk(1024);
-  if (um == 2)
-    tb_phase_kernel<2><<<grd, blk, 0, s>>>(a, tt, order, n);
-  else if (um == 1)
-    tb_phase_kernel<1><<<grd, blk, 0, s>>>(a, tt, order, n);
-  else
-    tb_phase_kernel<0><<<grd, blk, 0, s>>>(a, tt, order, n);
-  return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 
 // Per TB item: the palette word if every cell within distance 2 of its own box (the cells

@@ -114,7 +114,14 @@ def test_nan_guard():
     f2.set_nan_check(2)
     with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
         f2.step(50)  # one call: the guard fires inside the batch, the call raises
+    assert f2.t in (f.t, f.t + 1)  # stopped at its first check at or after the failing step
     f3 = core.Fields(s)  # default cadence: every step
     f3.initialize_field(8, v)
-    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
+    with pytest.raises(RuntimeError, match=r"NaN or Inf \(at time step"):
         f3.step(10)  # one call of a few steps: checked (the old host guard ran every 100)
+    assert f3.t == f.t  # the time stops at the failing step, as the reference's abort
+    f4 = core.Fields(s)  # a long call: the flag is read every 256 steps, not only at the end
+    f4.initialize_field(8, v)
+    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
+        f4.step(2000)
+    assert f4.t == f.t

@@ -121,29 +121,30 @@ def test_tb_too_small_for_l2():
     _same(p, sc_tb(make_oracle, sizes=(3.2, 3.2, 3.2), srcs=((0.05, 0.05, 0.05),), steps=(1, 4)))
 
 
-def test_tb_pipelined_phases():
-    """MNL_TB_SPLIT=0 (pipelined phases: the previous pair's rim step beside the inner
-    two-step items, rim step n beside the outer ones, in one persistent kernel) gives the
-    same fields as the default three launches per pair."""
-    os.environ["MNL_TB_SPLIT"] = "0"
-    try:
-        p = sc_tb(ProductSim, steps=(1, 9, 1, 4))
-    finally:
-        del os.environ["MNL_TB_SPLIT"]
-    _same(p, sc_tb(ProductSim, steps=(1, 9, 1, 4)))
-
-
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_tb_long_batch(split):
-    """Many pairs in one batch (pipelined: every phase A carries the previous pair's rim
-    step), an odd step at the end (drain, then one step), NaN guards inside."""
+def test_tb_long_batch():
+    """Many pairs in one batch, an odd step at the end (one step), NaN guards inside."""
     kw = dict(steps=(1, 125))
-    os.environ["MNL_TB_SPLIT"] = split
-    try:
-        p = sc_tb(ProductSim, **kw)
-    finally:
-        del os.environ["MNL_TB_SPLIT"]
+    _same(sc_tb(ProductSim, **kw), sc_tb(make_oracle, **kw))
+
+
+@pytest.mark.parametrize("sizes", [(9.6, 6.4, 8.0), (9.6, 16.0, 6.4)])
+def test_tb_narrow_strips(sizes):
+    """PML 1.0 (10 cells): L2 starts 16 columns from the low x face, so both x-face rim strips
+    are 16 columns wide and run in the narrow strip body (the left one without an x-1 column,
+    the right one reading the new B of its x-1 column from the two-step kernel's stores);
+    16.0 in y gives three row blocks per strip.  Bitwise the oracle and the wide-strip path."""
+    kw = dict(sizes=sizes, dpml=1.0, steps=(1, 10, 3), srcs=SRCS[:1] + SRCS[3:])
+    p = sc_tb(ProductSim, profile=True, **kw)
+    info = p._fields().tb_info()
+    assert info["active"] and info["narrow_items"] >= 2, info
     _same(p, sc_tb(make_oracle, **kw))
+    os.environ["MNL_TB_NARROW"] = "0"
+    try:
+        q = sc_tb(ProductSim, **kw)
+    finally:
+        del os.environ["MNL_TB_NARROW"]
+    assert q._fields().tb_info()["narrow_items"] == 0
+    _same(p, q)
 
 
 @pytest.mark.parametrize("group", [GroupSim, GroupSim3])
@@ -170,7 +171,7 @@ def test_tb_dft_flux():
     from test_gpu_dft import _same_dft
     kw = dict(sizes=[9.6, 6.4, 8.0], steps=24)
     p, hs = sc_flux_3d(ProductSim, **kw)
-    assert p._fields().tb_info()["active"]
+    assert p._fields().tb_info()["active"]  # the last call stepped pairs
     o, _ = sc_flux_3d(make_oracle, **kw)
     _same_dft(p, o, hs)
 
@@ -182,6 +183,20 @@ def test_tb_dft_fields():
     from test_gpu_dft_fields import _same as same_fields
     kw = dict(sizes=[9.6, 6.4, 8.0], steps=20)
     p, objs = sc_dft_fields_3d(ProductSim, **kw)
-    assert p._fields().tb_info()["active"]
+    assert p._fields().tb_info()["active"]  # the last call stepped pairs
     o, _ = sc_dft_fields_3d(make_oracle, **kw)
     same_fields(p, o, objs)
+
+
+def test_tb_middle_set_oom_fallback():
+    """When the middle buffer set does not fit (MNL_TB_OOM=1 simulates the failed hipMalloc),
+    temporal blocking switches itself off and the fields step one step at a time, bitwise
+    the oracle, instead of failing the step."""
+    os.environ["MNL_TB_OOM"] = "1"
+    try:
+        p = sc_tb(ProductSim, steps=(1, 9, 4))
+    finally:
+        del os.environ["MNL_TB_OOM"]
+    info = p._fields().tb_info()
+    assert not info["active"] and not info["enabled"], info
+    _same(p, sc_tb(make_oracle, steps=(1, 9, 4)))

@@ -123,10 +123,17 @@ def main():
             entry = {"kernel": "pair: tb2_kernel + 2 x fused_tile_kernel (rim)", "tb": True,
                      "hbm_bytes_per_launch": res[tb[0]]["hbm_bytes"] + 2 * res[rim[0]]["hbm_bytes"]}
         else:
-            ks = [k for k in res if k.startswith(a.kernel) and "hbm_bytes" in res[k]]
-            if not ks:
-                return
-            entry = {"kernel": ks[0], "tb": False, "hbm_bytes_per_launch": res[ks[0]]["hbm_bytes"]}
+            # --kernel a,b: kernels launched once per step side by side (the tile kernel and the
+            # polarization chunks' general kernel on a CU split): their bytes add up
+            ks = []
+            for pre in a.kernel.split(","):
+                m = [k for k in res if k.startswith(pre) and "hbm_bytes" in res[k]]
+                if not m:
+                    return
+                ks.append(m[0])
+            entry = {"kernel": " + ".join(ks), "tb": False,
+                     "hbm_bytes_per_launch": sum(res[k]["hbm_bytes"] for k in ks),
+                     "per_kernel": {k: res[k]["hbm_bytes"] for k in ks}}
         entry.update({"kernels_hash": kernels_hash(), "profile": os.path.basename(a.dst)})
         doc_t.setdefault("configs", {})[f"{a.config}_{a.size}_{'tb' if a.pair else '1s'}"] = entry
         with open(a.traffic, "w") as fh:
