@@ -2287,17 +2287,42 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
   }
 }
 
+// The tile bodies read the kernel's FusedArgs through kargs_opaque(): the kernarg segment
+// (constant address space, scalar loads) behind an empty asm, taken once per item.  Every
+// value a body derives from its arguments is then live inside that body only; reading the
+// by-value kernel parameter instead lets the compiler hoist every body's pointers to the
+// kernel entry, where the union of all bodies' values overflows the SGPRs and each plane
+// loop reloads them from VGPR lanes (v_readlane: 40-60 % of a PML body's instructions in
+// the combined kernel, none with one body per kernel).
+typedef const FusedArgs __attribute__((address_space(4))) KFA;
+// The thread index behind an empty asm, per item: lane-derived offsets are then computed in
+// the body that uses them instead of being hoisted to the kernel entry as a union over all
+// bodies (kept in VGPRs across the item loop: scratch spills reloaded inside plane loops).
+#ifndef MNL_TID_OPQ
+#define MNL_TID_OPQ 1
+#endif
+__device__ __forceinline__ int tid_item() {
+  int t = threadIdx.x;
+  if (MNL_TID_OPQ) asm volatile("" : "+v"(t));
+  return t;
+}
+__device__ __forceinline__ KFA *kargs_opaque() {
+  KFA *p = (KFA *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // Lean body over one item (tile columns x0..x1, own rows y0+1..y1, planes [zs, ze)):
 // its whole footprint (columns x0-1 .. x1+1, rows y0 .. y1+1, planes zs-1 .. ze) lies in
 // the lean box L: no PML, every component owned, H == B, E implicit.  1024 threads:
 // waves 0..FR-1 hold one row each (row 0 = the y-1 halo row, B recomputed), wave FR the
 // x-1 column (B recomputed), the E of the x+64 column and a corner.
 template <int UMODE, int DIST>
-__device__ __forceinline__ void lean_body(const FusedArgs &a, const ItemGeo &itg, unsigned uw,
+__device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned uw,
                                           const double (*sU)[256], double (*sE)[FR + 1][FXL],
                                           double (*sB)[FR][FXL]) {
   constexpr bool HAS_U = UMODE != 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = tid_item(), lane = tid & 63, w = tid >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform
   const bool hwave = wu >= FR - 1;
   constexpr bool SKIPB = MNL_SKIP_B;
@@ -2598,12 +2623,12 @@ __device__ __forceinline__ unsigned own_bits_of(int v, int sl, int sh, int ul, i
 // columns 0 and 33), lanes 32..63 the second (it.xb0 .. it.xb1; LDS columns 35..66, halo 34 and
 // 67); the halo wave serves both.  Row and z logic are unchanged.
 template <int UMODE, int DIST, int AX, bool OWNC, bool PAIR = false>
-__device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, unsigned uw,
+__device__ __forceinline__ void pml_body(KFA &a, const ItemGeo &it, unsigned uw,
                                          const double (*sU)[256], double (*sE)[FR + 1][FXL],
                                          double (*sB)[FR][FXL], PTabL &P) {
   constexpr bool HAS_U = UMODE != 0;
   constexpr bool PX = (AX & 1) != 0, PY = (AX & 2) != 0, PZ = (AX & 4) != 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = tid_item(), lane = tid & 63, w = tid >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform
   const bool hwave = wu >= FR - 1;
   constexpr bool SKIPB = MNL_SKIP_B;
@@ -3041,7 +3066,7 @@ __device__ __forceinline__ void pml_body(const FusedArgs &a, const ItemGeo &it, 
 // pml_body<AX = 1, OWNC>'s, operand for operand (src/step_generic.cpp:69-253, 576-906).
 constexpr int SW_N = 16, SR_N = 64, SXL = SW_N + 2;
 template <int UMODE>
-__device__ __forceinline__ void strip_body(const FusedArgs &a, const ItemGeo &it, unsigned uw,
+__device__ __forceinline__ void strip_body(KFA &a, const ItemGeo &it, unsigned uw,
                                            const double (*sU)[256], double (*sE)[SR_N + 1][SXL],
                                            double (*sB)[SR_N][SXL], PTabL &P) {
   constexpr bool HAS_U = UMODE != 0;
@@ -3057,7 +3082,7 @@ __device__ __forceinline__ void strip_body(const FusedArgs &a, const ItemGeo &it
     P.v[0][2][sft][pos] = a.tab.kps[0][q];
     P.f[0][sft][pos] = a.tab.flag[0][q];
   }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = tid_item(), lane = tid & 63, w = tid >> 6;
   const int row = 4 * w + (lane >> 4), col = 1 + (lane & 15);
   const int N0 = a.N[0], N1 = a.N[1];
   const long long st1 = a.st1;
@@ -3073,7 +3098,7 @@ __device__ __forceinline__ void strip_body(const FusedArgs &a, const ItemGeo &it
   const bool stl = row >= 1 && gx <= x1 && gy <= y1;
   // ---- halo slot of this thread: 1 = E of the x+16 column (row t), 2 = E of the y+64 row
   // (column t - 64), 3 = B_new of the x-1 column (row t - 79)
-  const int t = threadIdx.x;
+  const int t = tid;
   const int skind = t < SR_N ? 1 : t < SR_N + SW_N ? 2 : t < 2 * SR_N + SW_N - 1 ? 3 : 0;
   const int srow = skind == 1 ? t : skind == 2 ? SR_N : skind == 3 ? t - SR_N - SW_N + 1 : 0;
   const int scol = skind == 1 ? SW_N + 1 : skind == 2 ? 1 + (t - SR_N) : 0;
@@ -3333,7 +3358,7 @@ constexpr int STRIP_SE = 3 * (SR_N + 1) * SXL, STRIP_SB = 3 * SR_N * SXL;
 constexpr int TILE_SM = TILE_SE + TILE_SB > STRIP_SE + STRIP_SB ? TILE_SE + TILE_SB
                                                                 : STRIP_SE + STRIP_SB;
 template <int UMODE, int DIST>
-__device__ __forceinline__ void tile_item_body(const FusedArgs &a, int item, const ItemGeo &itg,
+__device__ __forceinline__ void tile_item_body(KFA &a, int item, const ItemGeo &itg,
                                                unsigned uw, const double (*sU)[256], double *sm,
                                                PTabL &sP) {
   constexpr int MD = MNL_MULTI_DIST;
@@ -3462,9 +3487,47 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
     if (item == -1) break;
-    tile_item_body<UMODE, DIST>(a, item, tile_item_geo(a, item, s_idx), s_uw, sU, sm, sP);
+    tile_item_body<UMODE, DIST>(*kargs_opaque(), item, tile_item_geo(a, item, s_idx), s_uw, sU, sm,
+                                sP);
   }
 }
+
+#ifdef MNL_ISA_PROBE
+// ISA inspection only (hipcc -DMNL_ISA_PROBE -S): one body per persistent kernel
+template <int UMODE, int BODY>
+__global__ __launch_bounds__(1024) void probe_kernel(FusedArgs a) {
+  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
+  __shared__ double sm[TILE_SM];
+  __shared__ PTabL sP;
+  __shared__ int s_item;
+  unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
+      s_item = (long long)v < a.gend ? a.titems[v] : -1;
+    }
+    __syncthreads();
+    const int item = s_item;
+    if (item == -1) break;
+    const ItemGeo itg = tile_item_geo(a, item, 0);
+    double(*sE)[FR + 1][FXL] = reinterpret_cast<double(*)[FR + 1][FXL]>(sm);
+    double(*sB)[FR][FXL] = reinterpret_cast<double(*)[FR][FXL]>(sm + TILE_SE);
+    if (BODY == 0)
+      strip_body<UMODE>(*kargs_opaque(), itg, ~0u, sU, reinterpret_cast<double(*)[SR_N + 1][SXL]>(sm),
+                        reinterpret_cast<double(*)[SR_N][SXL]>(sm + STRIP_SE), sP);
+    else if (BODY == 1)
+      pml_body<UMODE, 1, 1, true>(*kargs_opaque(), itg, ~0u, sU, sE, sB, sP);
+    else if (BODY == 2)
+      pml_body<UMODE, 1, 2, true>(*kargs_opaque(), itg, ~0u, sU, sE, sB, sP);
+    else
+      lean_body<UMODE, 1>(*kargs_opaque(), itg, ~0u, sU, sE, sB);
+  }
+}
+template __global__ void probe_kernel<2, 0>(FusedArgs);
+template __global__ void probe_kernel<2, 1>(FusedArgs);
+template __global__ void probe_kernel<2, 2>(FusedArgs);
+template __global__ void probe_kernel<2, 3>(FusedArgs);
+#endif
 
 // the tile kernel for palette mode um (2 palette, 1 f64 chi1inv, 0 none); the diagnostics
 // build when the item clock is on
@@ -3538,7 +3601,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
     itg.zs = a.zb[ch];
     itg.ze = a.zb[ch + 1];
     const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[(long long)tile * a.nch + ch] : ~0u;
-    lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
+    lean_body<UMODE, DIST>(*kargs_opaque(), itg, uw, sU, sE, sB);
   }
 }
 
