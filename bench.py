@@ -327,6 +327,23 @@ def measure_extra(workload, size, steps, warmup, tune=True):
     return out
 
 
+def rank_breakdown(f, rank, el_ms_per_step):
+    """Per-rank timing of a multi-rank run (HIP events): per pair of steps the two-step
+    kernel, the rim launches (R1 + both parts of R2), the slab-face chains on the comm stream
+    (top plane's step, sources, B/H and E plane exchanges: two per pair, beside the main
+    stream) and the main stream's waits for a chain's E ghost (two per pair); one-step steps
+    (odd leftovers) are not in it."""
+    pairs, pair_ms, _ = f.kernel_stats(5)
+    _, rim_ms, _ = f.kernel_stats(6)
+    _, chain_ms, _ = f.kernel_stats(7)
+    _, wait_ms, _ = f.kernel_stats(8)
+    n = max(pairs, 1)
+    return {"rank": rank, "pairs": pairs, "ms_per_step": round(el_ms_per_step, 4),
+            "pair_ms": round(pair_ms / n, 4), "two_step_ms": round((pair_ms - rim_ms) / n, 4),
+            "rim_ms": round(rim_ms / n, 4), "face_chain_ms": round(chain_ms / n, 4),
+            "exchange_wait_ms": round(wait_ms / n, 4)}
+
+
 def measure_c5(args, rank, world, device, dist):
     """BASELINE C5 on the ranks of this run: per GPU a S x S x S/4 z-slab of the vacuum +
     PML(1.0) grid (S = --size; 512: the 1024x512x512 domain at N = 8), tuned, warmed up,
@@ -340,19 +357,25 @@ def measure_c5(args, rank, world, device, dist):
     zc = None if args.no_tune else f.tune()
     f.step(args.warmup)
     dist.barrier()
+    f.set_profiling(not args.no_events)
     t0 = time.perf_counter()
     f.step(args.steps)
     dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    el_own = time.perf_counter() - t0
+    t = torch.tensor([el_own], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, rank_breakdown(f, rank, el_own / args.steps * 1e3))
     cells = float(gv.n[0]) * gv.n[1] * gv.n[2]
     out = {"workload": WORKLOADS["c5"] + f", global {gv.n[0]}x{gv.n[1]}x{gv.n[2]} cells "
                        f"({world} z-slabs), res 10, real fields",
            "value": round(cells * args.steps / el / 1e6, 1), "unit": "Mcells*steps/s",
            "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps,
            "n_gpus": world, "scaling": "weak", "transport": f.transport(),
-           "fused": f.fused_active(), "tuned_zchunk_gen_cus": zc}
+           "fused": f.fused_active(), "tuned_zchunk_gen_cus": zc,
+           "temporal_blocking": f.fused_active() and f.tb_info()["active"],
+           "per_rank": per_rank}
     del f, s
     gc.collect()
     return out
@@ -492,6 +515,7 @@ def main():
     f.step(args.steps)  # returns after the device work is complete (stream synchronized)
     barrier()
     el = time.perf_counter() - t0
+    el_own = el
     state_after = gpu_state_finish(gpu_state_start()) if rank == 0 and not args.no_smi else None
     if dist is not None:
         import torch
@@ -516,6 +540,10 @@ def main():
                            "achieved": round(d_bytes / (d_avg * 1e-3) / 1e9, 1)}
     transport = f.transport()
     fused = f.fused_active()
+    per_rank = None
+    if dist is not None:  # per-rank pair / rim / slab-face chain / exchange-wait breakdown
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, rank_breakdown(f, rank, el_own / args.steps * 1e3))
     del f, s
     gc.collect()
     extra = None
@@ -571,6 +599,7 @@ def main():
             "model_fraction_of_peak": round(bpc * total_cells / world / (el / args.steps) / 1e9
                                             / HBM_PEAK_GBS, 4)},
         "roofline": roof,
+        "per_rank": per_rank,
         "cpu_baseline": cpu,
         "configs": extra,
         "gpu_state": {"while_stepping": state_busy, "after": state_after},

@@ -364,7 +364,11 @@ struct mnl_fields {
   TB2Item *d_tb_items = nullptr;
   size_t tb_rcap = 0, tb_gcap = 0, tb_icap = 0;
   bool tb_nopair = false;   // MNL_TB_NOPAIR=1: x-face rim strips one per workgroup (A/B)
+  bool pol_lean = true;     // MNL_POL_LEAN=0: every polarization chunk in the general kernel
+  int tile_pol_items = 0;   // lean polarization items (lean_body<POLB>) of the tile kernel
   bool tb_last = false;     // the last batch of >= 2 steps stepped in pairs (tb_usable)
+  int tb_res = -1;          // MNL_TB_RES: CUs the pairs' persistent launches leave free (-1:
+                            // TB_RES_CUS with several ranks, 0 with one; A/B of the reservation)
   bool tb_oom = false;      // the middle buffer set did not fit: temporal blocking off
   bool tb_oom_test = false; // MNL_TB_OOM=1: its allocation fails (tests)
   bool tb_narrow = true;    // MNL_TB_NARROW=0: no narrow x-face strip items (A/B)
@@ -2456,6 +2460,30 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
     const int ny = G.hi[1] - G.lo[1] + 1, nt = (ny + 13) / 14;
     for (int t = 0; t < nt; t++) yb.push_back(G.lo[1] + (int)((long long)ny * t / nt));
   }
+  // lean tiles of the polarization chunks (one isotropic Lorentzian): the tile kernel's
+  // lean_body<POLB> takes the tiles whose x / y footprint lies in L ([ltx0, ltx1] x [lty0,
+  // lty1] in tile indices), the general kernel the rest of those chunks; its rows are cut at
+  // the same y bounds
+  int ltx0 = 0, ltx1 = -1, lty0 = 0, lty1 = -1;
+  if (F->pol_lean && F->f.npol == 1 && !F->upnl && !F->f.aniso) {
+    for (size_t t = 0; t < xb.size(); t++) {
+      const int x0 = xb[t], x1 = (t + 1 < xb.size() ? xb[t + 1] : G.hi[0] + 1) - 1;
+      if (x0 - 1 >= L.lo[0] && x1 + 1 <= L.hi[0]) {
+        if (ltx1 < ltx0) ltx0 = (int)t;
+        ltx1 = (int)t;
+      }
+    }
+    for (size_t t = 0; t < yb.size(); t++) {
+      const int y0 = yb[t] - 1, y1 = (t + 1 < yb.size() ? yb[t + 1] : G.hi[1] + 1) - 1;
+      if (y0 >= L.lo[1] && y1 + 1 <= L.hi[1]) {
+        if (lty1 < lty0) lty0 = (int)t;
+        lty1 = (int)t;
+      }
+    }
+  }
+  const bool polt = ltx1 >= ltx0 && lty1 >= lty0;
+  const int PY0 = polt ? yb[lty0] : 0;
+  const int PY1 = polt ? (lty1 + 1 < (int)yb.size() ? yb[lty1 + 1] : G.hi[1] + 1) - 1 : -1;
   int pzl = INT32_MAX, pzh = -1;
   for (int k = 0; k < F->f.npol; k++)
     if (F->f.pol[k].nz.lo[2] <= F->f.pol[k].nz.hi[2]) {
@@ -2530,7 +2558,13 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
     }
   };
   for (auto &sg : seg) split_bal(sg.first.first, sg.first.second, sg.second ? pzc : zc, sg.second);
-  split_range(gyb, G.lo[1], G.hi[1] + 1, FUSED_GW_ROWS, 1);
+  if (polt) {  // general rows cut at the lean polarization tiles' y bounds
+    split_range(gyb, G.lo[1], PY0, FUSED_GW_ROWS, 1);
+    split_range(gyb, PY0, PY1 + 1, FUSED_GW_ROWS, 1);
+    split_range(gyb, PY1 + 1, G.hi[1] + 1, FUSED_GW_ROWS, 1);
+  } else {
+    split_range(gyb, G.lo[1], G.hi[1] + 1, FUSED_GW_ROWS, 1);
+  }
   if ((int)xb.size() > FUSED_MAXX || (int)yb.size() > FUSED_MAXY ||
       (int)gyb.size() > FUSED_MAXGY || (int)zb.size() > FUSED_MAXZ)
     return false;
@@ -2562,13 +2596,32 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
   F->titems.clear();
   F->gitems.clear();
   F->tile_cells = F->lean_cells = F->gen_cells = 0;
+  F->tile_pol_items = 0;
   F->tile_z.assign(std::max(g.N[2], 1), 0);
   std::vector<int> early, heavy, lean, gen_e, gen_r;
   for (int ch = 0; ch < a.nch; ch++) {
     const int zs = a.zb[ch], ze = a.zb[ch + 1];
     if (polch[ch]) {
+      // lean tiles of the chunk (its planes' footprint in L too): tile kernel, body 0 | POLB
+      const bool pl = polt && zs - 1 >= L.lo[2] && ze <= L.hi[2];
+      if (pl)
+        for (int ty = lty0; ty <= lty1; ty++)
+          for (int tx = ltx0; tx <= ltx1; tx++) {
+            const int x0 = a.xb[tx], x1 = a.xb[tx + 1] - 1, y0 = a.yb[ty] - 1, y1 = a.yb[ty + 1] - 1;
+            bool in_l;
+            const int code = tile_item_code(F, a, L, x0, x1, y0, y1, zs, ze, &in_l);
+            if (!in_l) return false;  // cannot happen (the footprint lies in L)
+            const long long cells = (long long)(x1 - x0 + 1) * (y1 - y0) * (ze - zs);
+            F->tile_cells += cells;
+            F->lean_cells += cells;
+            const int v = tx | (ty << 8) | (ch << 16) | code | (1 << 30);
+            F->tile_pol_items++;
+            (F->nranks > 1 && ch == 0 ? early : lean).push_back(v);
+          }
       for (int ty = 0; ty < a.ngy; ty++)
         for (int tx = 0; tx < a.nx; tx++) {
+          if (pl && tx >= ltx0 && tx <= ltx1 && a.gyb[ty] >= PY0 && a.gyb[ty + 1] - 1 <= PY1)
+            continue;  // in the tile kernel's lean polarization items
           const int y0 = a.gyb[ty] - 1;
           const int lo[3] = {a.xb[tx] - 1, y0, zs - 1};
           const int hi[3] = {a.xb[tx] + FX_HOST, y0 + FUSED_GW_ROWS + 1, ze + 1};
@@ -3172,6 +3225,8 @@ enum {
   TM_B = 0, TM_H, TM_D, TM_E, TM_SRC, TM_HALO, TM_BINT, TM_DINT, TM_GEN, TM_DFT, TM_DFTF,
   TM_TB,   // two-step kernel (temporal blocking), one launch per pair of steps
   TM_RIM,  // rim launches of the pairs (two per pair)
+  TM_CHAIN,  // multi-rank pairs: a slab-face chain on the comm stream (two per pair)
+  TM_WAIT,   // multi-rank pairs: the main stream waiting for the chain's E ghost (two per pair)
   TM_N
 };
 
@@ -4230,9 +4285,11 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   if (tb_mid_init(F)) return -1;
   const FusedArgs &fa = fused_args(F);
   const Set5 cur = set_cur(F), mid = set_mid(F), nxt = set_nxt(F);
-  const TB2Args t = tb_args(F, cur, mid, nxt);
+  TB2Args t = tb_args(F, cur, mid, nxt);
   const int nr = (int)F->tb_ritems.size();
-  const FusedArgs r1 = rim_args(F, fa, cur, mid), r2 = rim_args(F, fa, mid, nxt);
+  FusedArgs r1 = rim_args(F, fa, cur, mid), r2 = rim_args(F, fa, mid, nxt);
+  if (F->tb_res > 0)  // A/B: the multi-rank reservation on one rank
+    t.wg_limit = r1.wg_limit = r2.wg_limit = std::max(1, k_cu_count() - F->tb_res);
   int k = ev_begin(TM_TB);
   int kr = k_tb2(t, F->stream, F->ctr_base);
   ev_end(k);
@@ -4279,11 +4336,13 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
 //   s_comm: the same chain for nxt -- beside the next pair's L.
 // Every kernel reads and writes disjoint points of its sets.
 
+template <class EB, class EE>
 int tb_face_chain(mnl_fields *F, const Set5 &o, const Set5 &n, const SrcDev &src,
-                  hipEvent_t after) {
+                  hipEvent_t after, EB &ev_begin, EE &ev_end) {
   DevFields &f = F->f;
   const DevGrid &g = F->g;
   HIPCHK(hipStreamWaitEvent(F->s_comm, after, 0));
+  const int kc = ev_begin(TM_CHAIN, F->s_comm);
   // exchanges and shell kernels read F->f's pointers when enqueued: point them at the sets
   const DevFields keep = f;
   for (int d = 0; d < 3; d++) {
@@ -4313,6 +4372,7 @@ int tb_face_chain(mnl_fields *F, const Set5 &o, const Set5 &n, const SrcDev &src
   f = keep;
   (void)fresh;
   if (r) return r;
+  ev_end(kc, F->s_comm);
   HIPCHK(hipEventRecord(F->ev_x0, F->s_comm));
   return 0;
 }
@@ -4325,31 +4385,38 @@ int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begi
   const Set5 cur = set_cur(F), mid = set_mid(F), nxt = set_nxt(F);
   TB2Args t = tb_args(F, cur, mid, nxt);
   const int cus = k_cu_count();
-  t.wg_limit = cus - TB_RES_CUS;
+  const int res = F->tb_res >= 0 ? F->tb_res : TB_RES_CUS;
+  t.wg_limit = res > 0 ? cus - res : 0;
   const int nr = (int)F->tb_ritems.size(), nf = F->tb_rfree;
   int k = ev_begin(TM_TB);
   int kr = k_tb2(t, F->stream, F->ctr_base);
   ev_end(k);
   if (kr) return fused_fail("two-step kernel launch failed", kr);
   // R1 once the E ghost (and top plane) of step n are in
+  k = ev_begin(TM_WAIT);
   HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
+  ev_end(k);
   FusedArgs r1 = rim_args(F, fa, cur, mid);
   k = ev_begin(TM_RIM);
   kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
   ev_end(k);
   if (kr) return fused_fail("rim kernel launch failed", kr);
   HIPCHK(hipEventRecord(F->ev_early, F->stream));
-  if (tb_face_chain(F, cur, mid, s0, F->ev_early)) return -1;
+  if (tb_face_chain(F, cur, mid, s0, F->ev_early, ev_begin, ev_end)) return -1;
   nan_count(F, 1);  // the middle step's guard, after its top plane and sources (s_comm)
   F->nan_at = t_mid;
   if (nan_launch(F, F->s_comm, mid.E, mid.D)) return -1;
   // R2: the items without slab-face reads beside the chain, then the others
   FusedArgs r2 = rim_args(F, fa, mid, nxt);
-  r2.wg_limit = cus - TB_RES_CUS;
+  r2.wg_limit = res > 0 ? cus - res : 0;
   k = ev_begin(TM_RIM);
   kr = k_tile_items(r2, r2.titems, r2.tgeo, r2.tflag, nf, 4, F->stream, F->ctr_base);
+  ev_end(k);
   if (!kr) {
+    const int kw = ev_begin(TM_WAIT);
     HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
+    ev_end(kw);
+    k = ev_begin(TM_RIM);
     r2.wg_limit = 0;
     kr = k_tile_items(r2, r2.titems + nf, r2.tgeo + 4 * nf, r2.tflag ? r2.tflag + nf : nullptr,
                       nr - nf, 4, F->stream, F->ctr_base);
@@ -4357,7 +4424,7 @@ int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begi
   ev_end(k);
   if (kr) return fused_fail("rim kernel launch failed", kr);
   HIPCHK(hipEventRecord(F->ev_early, F->stream));
-  if (tb_face_chain(F, mid, nxt, s1, F->ev_early)) return -1;
+  if (tb_face_chain(F, mid, nxt, s1, F->ev_early, ev_begin, ev_end)) return -1;
   swap_cur_nxt(F->f);
   F->tb_chain_pending = true;  // a one-step step next waits for it (tb_chain_join)
   nan_count(F, 1);
@@ -4423,7 +4490,8 @@ int step_batch(mnl_fields *F, int nsteps) {
   const int CH = NAN_CH;  // steps per source table / NaN flag read
   std::vector<EvPair> evs;
   size_t evi = 0;
-  auto ev_begin = [&](int cat) -> int {
+  // timing events of a phase on the main stream (or st)
+  auto ev_begin = [&](int cat, hipStream_t st = nullptr) -> int {
     if (!F->profiling) return -1;
     while (F->ev_pool.size() < 2 * (evi + 1)) {
       hipEvent_t e;
@@ -4431,13 +4499,13 @@ int step_batch(mnl_fields *F, int nsteps) {
       F->ev_pool.push_back(e);
     }
     EvPair p{F->ev_pool[2 * evi], F->ev_pool[2 * evi + 1], cat};
-    hipEventRecord(p.a, F->stream);
+    hipEventRecord(p.a, st ? st : F->stream);
     evs.push_back(p);
     evi++;
     return (int)evs.size() - 1;
   };
-  auto ev_end = [&](int k) {
-    if (k >= 0) hipEventRecord(evs[k].b, F->stream);
+  auto ev_end = [&](int k, hipStream_t st = nullptr) {
+    if (k >= 0) hipEventRecord(evs[k].b, st ? st : F->stream);
   };
   // a phase that starts where phase k ended: its start is k's end event (one
   // record fewer between two back-to-back kernels)
@@ -4456,6 +4524,7 @@ int step_batch(mnl_fields *F, int nsteps) {
   auto flush_events = [&]() -> int {
     if (!F->profiling || evs.empty()) return 0;
     HIPCHK(hipStreamSynchronize(F->stream));
+    if (F->s_comm) HIPCHK(hipStreamSynchronize(F->s_comm));
     for (auto &p : evs) {
       float ms = 0;
       hipEventElapsedTime(&ms, p.a, p.b);
@@ -6011,7 +6080,9 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tz = getenv("MNL_TB_ZCHUNK"))
     F->tb_zchunk = std::max(0, atoi(tz)), F->tb_zchunk_env = true;
   if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
+  if (const char *pl = getenv("MNL_POL_LEAN")) F->pol_lean = atoi(pl) != 0;
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
+  if (const char *tr = getenv("MNL_TB_RES")) F->tb_res = std::max(0, atoi(tr));
   if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
   if (const char *fd = getenv("MNL_FUSED_DIST")) F->fused_dist = atoi(fd) == 2 ? 2 : 1;
@@ -7041,7 +7112,14 @@ void fused_bytes(const mnl_fields *F, double *lean_bytes, double *gen_bytes) {
 
 int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, double *total_ms,
                             double *bytes_per_launch) {
-  if (!F || which < 0 || which > 6) return fail("bad kernel id");
+  if (!F || which < 0 || which > 8) return fail("bad kernel id");
+  if (which == 7 || which == 8) {  // multi-rank pairs: slab-face chains / E-ghost waits
+    const int cat = which == 7 ? TM_CHAIN : TM_WAIT;
+    *launches = F->timer_count[cat];
+    *total_ms = F->timer_ms[cat];
+    *bytes_per_launch = 0;
+    return 0;
+  }
   if (which == 5 || which == 6) {
     // temporal blocking.  5 = whole pairs of steps: launches = pairs, time = every launch of
     // the pairs (two phase launches each, the drains of the rim's last step), bytes per pair =

@@ -1621,10 +1621,44 @@ __device__ __forceinline__ unsigned ldu(gup p, unsigned off) {
   return *(gup)((const char __attribute__((address_space(1))) *)p + off);
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, unsigned nrec) {
+  // null: zero records, every access out of range (loads 0, stores dropped)
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, p ? (int)nrec : 0,
+                                           0x00020000);
+}
+// descriptor of a scalar pointer built where it is used (the empty asm keeps the compiler
+// from hoisting it out of the loop); null: zero records, every access out of range
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc_at(unsigned long long v, unsigned nrec) {
+  asm volatile("" : "+s"(v));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, v ? (int)nrec : 0, 0x00020000);
+}
+// a PML-state array as pml_body holds it: a scalar pointer turned into a descriptor at each
+// use (R) or a descriptor built once
+template <bool R>
+struct RsArr {
+  __device__ static unsigned long long make(const void *p, unsigned) {
+    return (unsigned long long)sgpr_ptr(p);
+  }
+  __device__ static __amdgpu_buffer_rsrc_t get(unsigned long long v, unsigned nrec) {
+    return brsrc_at(v, nrec);
+  }
+};
+template <>
+struct RsArr<false> {
+  __device__ static __amdgpu_buffer_rsrc_t make(const void *p, unsigned nrec) {
+    return brsrc(p, nrec);
+  }
+  __device__ static __amdgpu_buffer_rsrc_t get(__amdgpu_buffer_rsrc_t r, unsigned) { return r; }
+};
+__device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
 struct FBatch {  // what B(k) needs besides E(k): own raw at k+1, B_old(k), halo raw at k
   double d0, d1, d2, u0, u1, u2, b0, b1, b2, h0, h1, hu0, hu1;
+  double e0, e1, e2;  // lean_body<POLB>: stored E(k+1) of polarization-box points
   unsigned ui, hui;  // UMODE 2: chi1inv palette indices (byte per component)
-  bool f, hf;
+  bool f, hf, ps;
 };
 // UMODE: 0 = no chi1inv (E = D), 1 = f64 chi1inv arrays, 2 = chi1inv palette:
 // a byte index per cell and component (packed in one 32-bit word) into a
@@ -1682,13 +1716,38 @@ struct GAux {  // general body, PML state of plane k (own lanes), loaded masked
   double ud0, ud1, ud2;  // f_u of D, plane k
 };
 
+// The tile and general bodies read the kernel's FusedArgs through kargs_opaque(): the kernarg segment
+// (constant address space, scalar loads) behind an empty asm, taken once per item.  Every
+// value a body derives from its arguments is then live inside that body only; reading the
+// by-value kernel parameter instead lets the compiler hoist every body's pointers to the
+// kernel entry, where the union of all bodies' values overflows the SGPRs and each plane
+// loop reloads them from VGPR lanes (v_readlane: 40-60 % of a PML body's instructions in
+// the combined kernel, none with one body per kernel).
+typedef const FusedArgs __attribute__((address_space(4))) KFA;
+// The thread index behind an empty asm, per item: lane-derived offsets are then computed in
+// the body that uses them instead of being hoisted to the kernel entry as a union over all
+// bodies (kept in VGPRs across the item loop: scratch spills reloaded inside plane loops).
+#ifndef MNL_TID_OPQ
+#define MNL_TID_OPQ 1
+#endif
+__device__ __forceinline__ int tid_item() {
+  int t = threadIdx.x;
+  if (MNL_TID_OPQ) asm volatile("" : "+v"(t));
+  return t;
+}
+__device__ __forceinline__ KFA *kargs_opaque() {
+  KFA *p = (KFA *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // General body over one item: any mix of PML chunks, walls, ghosts and owned
 // ranges (src/step_generic.cpp:69-253 and 576-906 per point; H and E by
 // update_eh, src/update_eh.cpp:67-363, with the W aux of PML chunks
 // represented by its value: W_H == B_old, W_E == chi1inv * D_old, which the
 // reference stores one step earlier).
 template <int UMODE, int TX, int R, int NW, int POL, int AX>
-__device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo &it,
+__device__ __forceinline__ void fused_general(KFA &a, const ItemGeo &it,
                                               double (*sE)[R + 1][TX + 2],
                                               double (*sB)[R][TX + 1], const double (*sU)[256],
                                               TabE (*sTx)[2], TabE (*sTy)[2], TabE (*sTz)[2],
@@ -1700,7 +1759,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
   constexpr bool HAS_U = UMODE != 0;
   constexpr int RPW = 64 / TX, TPX = TX + 2, TPY = R + 1;
   static_assert(NW * RPW == R, "rows");
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = tid_item(), lane = tid & 63, w = tid >> 6;
   const bool hwave = __builtin_amdgcn_readfirstlane(w) >= NW - 1;
   const double C = a.C;
   const unsigned s2 = (unsigned)(a.st2 * 8);
@@ -2106,7 +2165,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
           const bool w3[3] = {fxs, fys, fzs};
           const TabE tw3[3] = {tx_s, ty_s, tz_s};
           if (POL == 1) {  // one susceptibility: all loads first, one memory wait
-            const PolDev &pd = a.pol[0];
+            const auto &pd = a.pol[0];
             double pv[3], ppv[3], sg[3];
 #pragma unroll
             for (int cc = 0; cc < 3; cc++) {
@@ -2145,7 +2204,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
             double pv[MAX_POL], ppv[MAX_POL];
             double gs = Dn3[cc], gp = Do3[cc];
             for (int q = 0; q < a.npol; q++) {
-              const PolDev &pd = a.pol[q];
+              const auto &pd = a.pol[q];
               pv[q] = pd.P[cc] ? ldg(sgpr_ptr(pd.P[cc]), oc) : 0.0;
               ppv[q] = pd.P[cc] ? ldg(sgpr_ptr(pd.Pp[cc]), oc) : 0.0;
               if (pd.P[cc]) {
@@ -2164,7 +2223,7 @@ __device__ __forceinline__ void fused_general(const FusedArgs &a, const ItemGeo 
               wv = fw;
             }
             for (int q = 0; q < a.npol; q++) {
-              const PolDev &pd = a.pol[q];
+              const auto &pd = a.pol[q];
               if (!pd.P[cc]) continue;
               const double sg = ldg(sgpr_ptr(pd.sigma[cc]), oc);
               stg(pd.P[cc], oc,
@@ -2221,10 +2280,10 @@ struct GenLds {  // LDS of one tile shape (the two shapes share it through a uni
 };
 
 template <int UMODE, int TX, int POL, int AX>
-__device__ __forceinline__ void general_item(const FusedArgs &a, int item, unsigned uw,
+__device__ __forceinline__ void general_item(KFA &a, int item, unsigned uw,
                                              GenLds<TX> &L, const double (*sU)[256]) {
   const int tx = item & 255, ty = (item >> 8) & 255, ch = (item >> 16) & 255;
-  const int *yb = TX == 64 ? a.gyb : a.nyb;
+  const auto *yb = TX == 64 ? a.gyb : a.nyb;
   ItemGeo itg;
   itg.x0 = a.xb[tx];
   itg.x1 = a.xb[tx + 1] - 1;
@@ -2262,8 +2321,8 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
   for (;;) {
     if (threadIdx.x == 0) {
       const unsigned long long v = atomicAdd(ctr, 1ULL) - cb;
-      s_item = (long long)v < n ? a.gitems[base + v] : -1;
-      s_uw = ((long long)v < n && UMODE == 2 && a.gflag) ? a.gflag[base + v] : ~0u;
+      s_item = v < (unsigned long long)(n) ? a.gitems[base + v] : -1;
+      s_uw = (v < (unsigned long long)(n) && UMODE == 2 && a.gflag) ? a.gflag[base + v] : ~0u;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const int item = s_item;
@@ -2274,42 +2333,17 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
     const int ax = (item >> 24) & 7;
     if (item & (int)0x80000000u) {
       if (ax == 1)
-        general_item<UMODE, 16, POL, 1>(a, item, uw, L.n, sU);
+        general_item<UMODE, 16, POL, 1>(*kargs_opaque(), item, uw, L.n, sU);
       else
-        general_item<UMODE, 16, POL, 7>(a, item, uw, L.n, sU);
+        general_item<UMODE, 16, POL, 7>(*kargs_opaque(), item, uw, L.n, sU);
     } else if (ax == 2) {
-      general_item<UMODE, 64, POL, 2>(a, item, uw, L.w, sU);
+      general_item<UMODE, 64, POL, 2>(*kargs_opaque(), item, uw, L.w, sU);
     } else if (ax == 4) {
-      general_item<UMODE, 64, POL, 4>(a, item, uw, L.w, sU);
+      general_item<UMODE, 64, POL, 4>(*kargs_opaque(), item, uw, L.w, sU);
     } else {
-      general_item<UMODE, 64, POL, 7>(a, item, uw, L.w, sU);
+      general_item<UMODE, 64, POL, 7>(*kargs_opaque(), item, uw, L.w, sU);
     }
   }
-}
-
-// The tile bodies read the kernel's FusedArgs through kargs_opaque(): the kernarg segment
-// (constant address space, scalar loads) behind an empty asm, taken once per item.  Every
-// value a body derives from its arguments is then live inside that body only; reading the
-// by-value kernel parameter instead lets the compiler hoist every body's pointers to the
-// kernel entry, where the union of all bodies' values overflows the SGPRs and each plane
-// loop reloads them from VGPR lanes (v_readlane: 40-60 % of a PML body's instructions in
-// the combined kernel, none with one body per kernel).
-typedef const FusedArgs __attribute__((address_space(4))) KFA;
-// The thread index behind an empty asm, per item: lane-derived offsets are then computed in
-// the body that uses them instead of being hoisted to the kernel entry as a union over all
-// bodies (kept in VGPRs across the item loop: scratch spills reloaded inside plane loops).
-#ifndef MNL_TID_OPQ
-#define MNL_TID_OPQ 1
-#endif
-__device__ __forceinline__ int tid_item() {
-  int t = threadIdx.x;
-  if (MNL_TID_OPQ) asm volatile("" : "+v"(t));
-  return t;
-}
-__device__ __forceinline__ KFA *kargs_opaque() {
-  KFA *p = (KFA *)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return p;
 }
 
 // Lean body over one item (tile columns x0..x1, own rows y0+1..y1, planes [zs, ze)):
@@ -2317,7 +2351,13 @@ __device__ __forceinline__ KFA *kargs_opaque() {
 // the lean box L: no PML, every component owned, H == B, E implicit.  1024 threads:
 // waves 0..FR-1 hold one row each (row 0 = the y-1 halo row, B recomputed), wave FR the
 // x-1 column (B recomputed), the E of the x+64 column and a corner.
-template <int UMODE, int DIST>
+// POLB (item bit 30 with body 0): the item lies in a polarization chunk (one isotropic
+// Lorentzian susceptibility).  Points of the polarization box store E = chi1inv (D - P)
+// (src/update_eh.cpp:84-146, src/step_generic.cpp:888-903 with f_minus_p) and update P / P_prev
+// (update_pols -> lorentzian update_P, src/susceptibility.cpp:251-258) -- the general body's
+// polarization branch, operand for operand; their E is read as stored E, never as chi1inv * D.
+// Points of the chi(2) box (FusedArgs::xbox) leave E and P to the NR kernel.
+template <int UMODE, int DIST, bool POLB = false>
 __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned uw,
                                           const double (*sU)[256], double (*sE)[FR + 1][FXL],
                                           double (*sB)[FR][FXL]) {
@@ -2419,16 +2459,36 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
         (unsigned)((max(x0 - 1, flo0) + (long long)max(y0, flo1) * a.st1 +
                     (long long)max(zs - 1, flo2) * a.st2) * 4);
     auto uoff = [&](unsigned o8) { return uni ? ufix : (o8 >> 1); };
+    // POLB: the polarization box (stored E) and the chi(2) box, per lane in x / y
+    const bool pxy = POLB && gx >= a.pbox.lo[0] && gx <= a.pbox.hi[0] && gy >= a.pbox.lo[1] &&
+                     gy <= a.pbox.hi[1];
+    const bool hpxy = POLB && hx >= a.pbox.lo[0] && hx <= a.pbox.hi[0] && hy >= a.pbox.lo[1] &&
+                      hy <= a.pbox.hi[1];
+    const bool xxy = POLB && gx >= a.xbox.lo[0] && gx <= a.xbox.hi[0] && gy >= a.xbox.lo[1] &&
+                     gy <= a.xbox.hi[1];
+    const int pzl = POLB ? a.pbox.lo[2] : 1, pzh = POLB ? a.pbox.hi[2] : 0;
+    const int xzl = POLB ? a.xbox.lo[2] : 1, xzh = POLB ? a.xbox.hi[2] : 0;
+    auto pin = [&](int z) { return POLB && z >= pzl && z <= pzh; };
 
     auto load = [&](int k) -> FBatch {
       FBatch q;
       const int z1 = k + 1;
-      q.f = colF && zin(z1);
+      const bool ps = pxy && colF && pin(z1);  // stored E at this own point (polarization box)
+      q.ps = ps;
+      q.f = colF && zin(z1) && !ps;
       const unsigned o = cbl + (unsigned)z1 * s2;
       const bool zf = zin(z1);  // uniform
       q.d0 = ldg(zf ? pO0 : Ev[0], o);
       q.d1 = ldg(zf ? pO1 : Ev[1], o);
       q.d2 = ldg(zf ? pO2 : Ev[2], o);
+      q.e0 = q.e1 = q.e2 = 0.0;
+      if (POLB) {
+        KFA &ai = *kargs_opaque();  // (pointers re-read per plane, as the P arrays')
+        const unsigned oe = ps ? o : MNL_OOB;
+        q.e0 = bld(brsrc_at((unsigned long long)sgpr_ptr(ai.E[0]), nrec), oe);
+        q.e1 = bld(brsrc_at((unsigned long long)sgpr_ptr(ai.E[1]), nrec), oe);
+        q.e2 = bld(brsrc_at((unsigned long long)sgpr_ptr(ai.E[2]), nrec), oe);
+      }
       if (UMODE == 2) {
         q.ui = ldu(uix, uoff(o));
       } else if (HAS_U) {
@@ -2444,13 +2504,14 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
       q.b0 = ldg(Bv[0], (SKIPB && wu == FR) ? safe : ob);
       q.b1 = ldg(Bv[1], (SKIPB && wu == 0) ? safe : ob);
       q.b2 = ldg(Bv[2], ob);
-      q.hf = hF && zin(k);
+      const bool hps = hpxy && pin(k);  // halo point of the polarization box: stored E
+      q.hf = hF && zin(k) && !hps;
       q.h0 = q.h1 = 0.0;
       q.hu0 = q.hu1 = 1.0;
       q.hui = 0;
       if (hwave) {  // only waves FR-1 and FR carry halo slots
         const unsigned oh = hbl + (unsigned)k * s2;
-        const bool zk = zin(k);  // uniform
+        const bool zk = zin(k) && !hps;
         q.h0 = ldg(zk ? pH0 : hE0, oh);
         q.h1 = ldg(zk ? pH1 : hE1, oh);
         if (UMODE == 2) {
@@ -2467,7 +2528,7 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
     double ex, ey, ez;
     {
       const int z = zs - 1;
-      const bool f0 = colF && zin(z);
+      const bool f0 = colF && zin(z) && !(pxy && pin(z));
       const unsigned o = cbl + (unsigned)z * s2;
       ex = ldg(f0 ? Dv[0] : Ev[0], o);
       ey = ldg(f0 ? Dv[1] : Ev[1], o);
@@ -2489,6 +2550,8 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
 #pragma unroll
     for (int j = 0; j < DIST; j++) q[j] = load(min(zs - 1 + j, ze - 1));
     double dx = 0, dy = 0, dz = 0, hmx = 0, hmy = 0;
+    unsigned uik = 0;                  // POLB: palette word of plane k (UMODE 2)
+    double uk0 = 1, uk1 = 1, uk2 = 1;  // POLB: chi1inv of plane k (UMODE 1)
     const int rowm = row > 0 ? row - 1 : 0, colm = col > 0 ? col - 1 : 0;
     const int ngrp = (ze - zs + 1 + DIST) / (DIST + 1);  // iterations k = zs-1 .. ze-1, padded
     for (int g = 0; g < ngrp; g++) {
@@ -2497,6 +2560,25 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
         const int k = zs - 1 + g * (DIST + 1) + j;
         q[(j + DIST) % (DIST + 1)] = load(min(k + DIST, ze - 1));
         const FBatch &c = q[j];
+        // POLB: P, P_prev, sigma of this own point at plane k (used after the D update)
+        double pv[3] = {0, 0, 0}, ppv[3] = {0, 0, 0}, sg[3] = {0, 0, 0};
+        const bool pk = POLB && store && k >= zs && k < ze && pxy && pin(k) &&
+                        !(xxy && k >= xzl && k <= xzh);
+        // (the polarization arrays' pointers are re-read per plane through an opaque kernarg
+        // pointer: scalar loads instead of SGPRs live across the loop, which would spill)
+        KFA &ai = *kargs_opaque();
+        if (POLB) {
+          const unsigned op = pk ? cb + (unsigned)k * s2 : MNL_OOB;
+#pragma unroll
+          for (int cc = 0; cc < 3; cc++) {
+            const unsigned long long pP = (unsigned long long)sgpr_ptr(ai.pol[0].P[cc]);
+            const unsigned long long pQ = (unsigned long long)sgpr_ptr(ai.pol[0].Pp[cc]);
+            const unsigned long long pS = (unsigned long long)sgpr_ptr(ai.pol[0].sigma[cc]);
+            pv[cc] = bld(brsrc_at(pP, nrec), op);
+            ppv[cc] = bld(brsrc_at(pQ, nrec), op);
+            sg[cc] = bld(brsrc_at(pS, nrec), op);
+          }
+        }
         double e1x, e1y, e1z;
         if (UMODE == 2) {
           e1x = e_of(c.d0, pu(c.ui, 0), c.f);
@@ -2507,6 +2589,7 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
           e1y = e_of(c.d1, c.u1, c.f);
           e1z = e_of(c.d2, c.u2, c.f);
         }
+        if (POLB && c.ps) e1x = c.e0, e1y = c.e1, e1z = c.e2;
         if (ownlike) {
           sE[0][row][col] = ex;
           sE[1][row][col] = ey;
@@ -2539,14 +2622,44 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
         __syncthreads();
         const double Hz_ym = sB[2][rowm][col], Hx_ym = sB[0][rowm][col];
         const double Hz_xm = sB[2][row][colm], Hy_xm = sB[1][row][colm];
-        bst(rD[0], os, dx - C * (Hz_ym - Bz + By - hmy));
-        bst(rD[1], os, dy - C * (hmx - Bx + Bz - Hz_xm));
-        bst(rD[2], os, dz - C * (Hy_xm - By + Bx - Hx_ym));
+        const double Dn0 = dx - C * (Hz_ym - Bz + By - hmy);
+        const double Dn1 = dy - C * (hmx - Bx + Bz - Hz_xm);
+        const double Dn2 = dz - C * (Hy_xm - By + Bx - Hx_ym);
+        bst(rD[0], os, Dn0);
+        bst(rD[1], os, Dn1);
+        bst(rD[2], os, Dn2);
+        if (POLB) {  // E = chi1inv (D - P), then update_P with W = E (general body's branch)
+          const unsigned op = pk ? cb + (unsigned)k * s2 : MNL_OOB;
+          const double Dn3[3] = {Dn0, Dn1, Dn2};
+#pragma unroll
+          for (int cc = 0; cc < 3; cc++) {
+            const bool hp = ai.pol[0].P[cc] != nullptr;
+            const double kk = UMODE == 2 ? pu(uik, cc) : (cc == 0 ? uk0 : (cc == 1 ? uk1 : uk2));
+            const double gs = hp ? Dn3[cc] - pv[cc] : Dn3[cc];
+            const double fw = HAS_U ? gs * kk : gs;
+            bst(brsrc_at((unsigned long long)sgpr_ptr(ai.En[cc]), nrec), op, fw);
+            if (hp) {
+              const auto &pd = ai.pol[0];
+              bst(brsrc_at((unsigned long long)sgpr_ptr(pd.P[cc]), nrec), op,
+                  pd.gamma1inv * (pv[cc] * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * ppv[cc] +
+                                  pd.omega0dtsqr * (sg[cc] * fw)));
+              bst(brsrc_at((unsigned long long)sgpr_ptr(pd.Pp[cc]), nrec), op, pv[cc]);
+            }
+          }
+        }
         hmx = Bx;
         hmy = By;
+        // D_old of the next plane (a polarization-box point loaded D and its stored E apart)
         dx = c.d0;
         dy = c.d1;
         dz = c.d2;
+        if (POLB) {
+          if (UMODE == 2) {
+            uik = c.ui;
+          } else if (HAS_U) {
+            uk0 = c.u0, uk1 = c.u1, uk2 = c.u2;
+          }
+        }
         ex = e1x;
         ey = e1y;
         ez = e1z;
@@ -2575,39 +2688,6 @@ struct PTabL {
   unsigned char f[3][2][TPZ];
 };
 static_assert(TPZ >= FXL && TPZ >= FR + 1, "table positions");
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p, unsigned nrec) {
-  // null: zero records, every access out of range (loads 0, stores dropped)
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, p ? (int)nrec : 0,
-                                           0x00020000);
-}
-// descriptor of a scalar pointer built where it is used (the empty asm keeps the compiler
-// from hoisting it out of the loop); null: zero records, every access out of range
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc_at(unsigned long long v, unsigned nrec) {
-  asm volatile("" : "+s"(v));
-  return __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, v ? (int)nrec : 0, 0x00020000);
-}
-// a PML-state array as pml_body holds it: a scalar pointer turned into a descriptor at each
-// use (R) or a descriptor built once
-template <bool R>
-struct RsArr {
-  __device__ static unsigned long long make(const void *p, unsigned) {
-    return (unsigned long long)sgpr_ptr(p);
-  }
-  __device__ static __amdgpu_buffer_rsrc_t get(unsigned long long v, unsigned nrec) {
-    return brsrc_at(v, nrec);
-  }
-};
-template <>
-struct RsArr<false> {
-  __device__ static __amdgpu_buffer_rsrc_t make(const void *p, unsigned nrec) {
-    return brsrc(p, nrec);
-  }
-  __device__ static __amdgpu_buffer_rsrc_t get(__amdgpu_buffer_rsrc_t r, unsigned) { return r; }
-};
-__device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
 
 // ownership bits of an index along one axis: bit0 = shifted components owned, bit1 = unshifted
 __device__ __forceinline__ unsigned own_bits_of(int v, int sl, int sh, int ul, int uh) {
@@ -3367,7 +3447,10 @@ __device__ __forceinline__ void tile_item_body(KFA &a, int item, const ItemGeo &
   double(*sB)[FR][FXL] = reinterpret_cast<double(*)[FR][FXL]>(sm + TILE_SE);
   switch ((item >> 24) & 7) {
     case 0:
-      lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
+      if ((item >> 30) & 1)  // lean item of a polarization chunk (one isotropic Lorentzian)
+        lean_body<UMODE, DIST, true>(a, itg, uw, sU, sE, sB);
+      else
+        lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
       break;
     case 1:
       if ((item >> 30) & 1) {  // narrow x-face strip (temporal-blocking rim; host: OWNC)
@@ -3479,9 +3562,9 @@ __global__ __launch_bounds__(1024) void fused_tile_kernel(FusedArgs a) {
                    g.zs | (g.ze << 16), g.xb0 >= 0 ? (g.xb0 | (g.xb1 << 16)) : -1);
       }
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
-      s_item = (long long)v < n ? a.titems[a.gbeg + v] : -1;
+      s_item = v < (unsigned long long)(n) ? a.titems[a.gbeg + v] : -1;
       s_idx = a.gbeg + (int)v;
-      s_uw = ((long long)v < n && UMODE == 2 && a.tflag) ? a.tflag[a.gbeg + v] : ~0u;
+      s_uw = (v < (unsigned long long)(n) && UMODE == 2 && a.tflag) ? a.tflag[a.gbeg + v] : ~0u;
       if (CLK) s_t0 = wall_clock64();
     }
     __syncthreads();  // also separates LDS use of consecutive items
@@ -3504,7 +3587,7 @@ __global__ __launch_bounds__(1024) void probe_kernel(FusedArgs a) {
   for (;;) {
     if (threadIdx.x == 0) {
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
-      s_item = (long long)v < a.gend ? a.titems[v] : -1;
+      s_item = v < (unsigned long long)(a.gend) ? a.titems[v] : -1;
     }
     __syncthreads();
     const int item = s_item;
@@ -3577,7 +3660,7 @@ __global__ __launch_bounds__(1024) void fused_kernel(FusedArgs a) {
   for (;;) {
     if (threadIdx.x == 0) {
       const unsigned long long v = atomicAdd(gctr, 1ULL) - gbase;
-      s_item = (long long)v < gtile * nlch ? (long long)v : -1;
+      s_item = v < (unsigned long long)(gtile * nlch) ? (long long)v : -1;
     }
     __syncthreads();  // also separates LDS use of consecutive items
     const long long item = s_item;
@@ -3965,7 +4048,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
                                          double (*sH1)[TB_LY][TB_LX], double (*sE2)[TB_LY][TB_LX],
                                          double (*sH2)[TB_LY][TB_LX]) {
   constexpr bool HAS_U = UMODE != 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = tid_item(), lane = tid & 63, w = tid >> 6;
   const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
   const int zs = it.z & 0xFFFF, ze = it.z >> 16;
   const int faces = it.faces;
@@ -4155,7 +4238,7 @@ __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
         clk_record(a.clk, s_t0, it.faces | (uw != ~0u ? 64 : 0), it.x, it.y, it.z, -1);
       }
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
-      s_idx = (long long)v < a.n ? (int)v : -1;
+      s_idx = v < (unsigned long long)(a.n) ? (int)v : -1;
       if (CLK) s_t0 = wall_clock64();
     }
     __syncthreads();  // also separates LDS use of consecutive items

@@ -35,6 +35,14 @@ def make_dist(rank, nranks, nid):
 
 def run_case(name, make):
     extra = {}
+    if name == "c5_full":  # full-size C5: per-plane checksums, not arrays (2 GB each)
+        def log(m):
+            print(f"c5_full: {m}", flush=True)
+        o = S.sc_c5_full(make, log=log)
+        log("stepped")
+        cs = np.stack([S.plane_checksums(o.get_array(c)) for c in range(12)])
+        return {"cs": cs, "transport": np.array(o._fields().transport()),
+                "tb": np.array([o._fields().tb_info()["active"]]), "t": np.array([o.t])}
     if name == "vacuum_pml":
         o = S.sc_vacuum_pml_3d(make)
     elif name == "big_box":

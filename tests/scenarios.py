@@ -374,6 +374,45 @@ def sc_c5_small(make, nranks=8, nxy=64, nz_per=16, steps=30):
     return o
 
 
+def sc_c5_full(make, steps=7, log=None):
+    """BASELINE configs[4] (C5) at full size: the 512 x 512 x 1024 vacuum + PML(1.0) grid (the
+    8-GPU decomposition is 8 z-slabs of 512 x 512 x 128), seeded random D and B everywhere
+    (every slab face and PML chunk carries data from the first step on), the Ez Gaussian
+    current at the centre (on the middle slab seam), stepped 1 + 6 (the first step unfused
+    after initialize_field, then three pairs of steps)."""
+    o = vol(make, 3, [51.2, 51.2, 102.4], 10, center_origin=True)
+    o.add_pml(1.0)
+    o.add_gaussian_source(2, 0.15, 10.0, 0.0, 100.0, (0.05, 0.05, 0.05), 1.0)
+    for c in (6, 7, 8, 9, 10, 11):
+        rng = np.random.default_rng(7 + 31 * c)
+        v = rng.standard_normal(o.shape())
+        o.initialize_field(c, v)
+        del v
+        if log:
+            log(f"initialized component {c}")
+    o.step(1)
+    o.step(steps - 1)
+    return o
+
+
+def plane_checksums(arr):
+    """Per plane of the last (z, the slab) axis: the sum over the plane of each value's IEEE
+    bit pattern times an odd weight of its (x, y, z) position, mod 2^64.  Entries a rank does
+    not own are 0 in its get_array, and every entry has one owner, so the ranks' checksums
+    add up (mod 2^64) to the one-rank run's exactly when every entry is bitwise equal (a
+    differing, swapped or misplaced value changes its plane's sum)."""
+    a = np.ascontiguousarray(arr).view(np.uint64)
+    nx, ny, nz = a.shape
+    out = np.zeros(nz, dtype=np.uint64)
+    ky = (np.arange(ny, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))[:, None]
+    kz = (np.arange(nz, dtype=np.uint64) * np.uint64(0xD6E8FEB86659FD93))[None, :]
+    with np.errstate(over="ignore"):
+        for i in range(nx):
+            w = (np.uint64(i) * np.uint64(0xBF58476D1CE4E5B9) + ky + kz) | np.uint64(1)
+            out += (a[i] * w).sum(axis=0, dtype=np.uint64)
+    return out
+
+
 def sc_waveguide_3d(make, L=3.2, steps=40, eps=12.0):
     """Config 3 shape scaled down: eps=12 core |y|,|z| < 0.5 along x, PML, no averaging."""
     o = vol(make, 3, [L, L, L], 10, center_origin=True)

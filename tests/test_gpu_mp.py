@@ -28,23 +28,27 @@ CASES3 = ["big_box", "flux", "averaged_up", "fuzz5", "fuzz24"]
 CASES8 = ["c5_small"]  # BASELINE C5's decomposition (8 z-slabs) at reduced x-y
 
 
-def _launch(nranks, cases, out):
+def _launch(nranks, cases, out, stream=False, timeout=400):
+    """One worker process per rank; stream=True: their output goes straight to this
+    process's real stderr (progress of long cases), else it is collected for failures."""
     from meep_nl_amd import core
     ids = ",".join(core.ipc_id(nranks).hex() for _ in cases)
     env = dict(os.environ, MNL_IPC_TIMEOUT="120")
+    pipe = None if stream else subprocess.PIPE
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "mp_worker.py"), str(r),
                                str(nranks), ids, str(out)] + cases, env=env,
-                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                              stdout=pipe if pipe else sys.__stderr__,
+                              stderr=subprocess.STDOUT, text=True)
              for r in range(nranks)]
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=400)
+            o, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
             raise
-        logs.append(o)
+        logs.append(o or "")
     for p, o in zip(procs, logs):
         assert p.returncode == 0, o[-3000:]
 
@@ -125,3 +129,30 @@ def test_rccl_selftest():
     from meep_nl_amd import core
     core.rccl_selftest(0, 1 << 20)
     core.rccl_selftest(0, 37)
+
+
+def test_c5_full_size_chunk_invariance(tmp_path):
+    """BASELINE configs[4] (C5) at full size: 8 processes stepping 512 x 512 x 128 z-slabs of
+    the 512 x 512 x 1024 vacuum + PML grid (IPC transport: the ranks share this GPU) against one
+    rank stepping the whole grid, from the same random fields, 1 + 6 steps (three pairs of
+    multi-rank temporal blocking).  The reference's chunk invariance (tests/three_d.cpp:35-39)
+    at 0: every entry of all twelve components bitwise equal, checked through per-plane
+    position-weighted bit-pattern sums (scenarios.plane_checksums), whose rank sums equal the
+    one-rank sums exactly when the arrays do."""
+    _launch(8, ["c5_full"], tmp_path, stream=True, timeout=900)
+    ranks = _load(tmp_path, "c5_full", 8)
+    assert all(str(r["transport"]) == "ipc" for r in ranks)
+    assert all(bool(r["tb"][0]) for r in ranks)  # the slabs stepped pairs
+    with np.errstate(over="ignore"):
+        got = sum(r["cs"] for r in ranks[1:]) + ranks[0]["cs"]
+    def log(m):
+        sys.__stderr__.write(f"c5_full one rank: {m}\n")
+        sys.__stderr__.flush()
+    o = S.sc_c5_full(S.ProductSim, log=log)
+    assert o._fields().tb_info()["active"]
+    assert int(ranks[0]["t"][0]) == o.t
+    for c in range(12):
+        ref = S.plane_checksums(o.get_array(c))
+        bad = np.nonzero(got[c] != ref)[0]
+        assert bad.size == 0, (c, bad[:10].tolist())
+    log("all planes equal")
