@@ -476,6 +476,8 @@ def main():
         nid = obj[0]
     elif os.environ.get("MNL_BENCH_DEVICE"):
         device = int(os.environ["MNL_BENCH_DEVICE"])
+    from meep_nl_amd import core as _core
+    _core.set_verbosity(0)  # no "on time step" lines: stdout carries the one JSON line
     try:
         gv, s, f = build_fields(args.workload, args.size, rank, world, device, nid)
     except RuntimeError as e:  # a failed RCCL setup names RCCL and exits non-zero

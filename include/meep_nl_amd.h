@@ -366,13 +366,18 @@ int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, doubl
  * active (1: the current fused geometry steps pairs), own cells of the two-step
  * items, border points (upper bound), own cells of mixed-palette two-step items,
  * rim cells, mixed-palette rim cells, two-step items, rim items, planes of the
- * first two-step item, split (1: three launches per pair; 0: pipelined phases),
+ * first two-step item (the longest), narrow x-face strip items among the rim items,
  * enabled (pairs allowed: set_temporal_blocking / MNL_TB / the tuner), the two-step chunk
  * setting (0: automatic). */
 int mnl_fields_tb_info(mnl_fields *f, double *out, int n);
 /* Allow (1, the default; MNL_TB=0 at creation turns it off) or forbid (0) stepping
  * pairs of steps with the two-step kernel.  Results are identical either way. */
 int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
+/* Scheduling options of the fused step (no reference counterpart; an option only changes how
+ * the same per-point arithmetic is scheduled, results are identical): which = 0 the narrow
+ * x-face strip body of the temporal-blocking rim (MNL_TB_NARROW).  The pair plan is rebuilt at
+ * the next step.  For in-process A/B measurements (tools/ab_inproc.py). */
+int mnl_fields_set_schedule(mnl_fields *f, int which, int value);
 
 /* ---- checkpoint (src/fields_dump.cpp, src/structure_dump.cpp) -----------
  * fields::dump / fields::load (src/fields_dump.cpp:108-145, 232-270): t and

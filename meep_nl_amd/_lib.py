@@ -99,6 +99,7 @@ _SIGS = {
     "mnl_fields_traffic_model": (c_int, [c_void, dptr, dptr]),
     "mnl_fields_tb_info": (c_int, [c_void, dptr, c_int]),
     "mnl_fields_set_temporal_blocking": (c_int, [c_void, c_int]),
+    "mnl_fields_set_schedule": (c_int, [c_void, c_int, c_int]),
     "mnl_fields_add_dft_flux": (c_int, [c_void, c_int, dptr, dptr, c_int, c_int, iptr]),
     "mnl_fields_dft_flux": (c_int, [c_void, c_int, dptr]),
     "mnl_fields_dft_size": (c_int, [c_void, c_int, llptr]),

@@ -579,6 +579,12 @@ class Fields:
         results either way)."""
         check(lib().mnl_fields_set_temporal_blocking(self.h, 1 if on else 0))
 
+    def set_schedule(self, which, value):
+        """Scheduling option (identical results): 'narrow' = the narrow x-face strip body of
+        the temporal-blocking rim (mnl_fields_set_schedule)."""
+        idx = {"narrow": 0}[which]
+        check(lib().mnl_fields_set_schedule(self.h, idx, 1 if value else 0))
+
     def tb_info(self):
         """Temporal blocking of the current fused geometry: dict of
         active (the last call of >= 2 steps stepped in pairs), two-step own cells / border

@@ -364,8 +364,6 @@ struct mnl_fields {
   TB2Item *d_tb_items = nullptr;
   size_t tb_rcap = 0, tb_gcap = 0, tb_icap = 0;
   bool tb_nopair = false;   // MNL_TB_NOPAIR=1: x-face rim strips one per workgroup (A/B)
-  bool pol_lean = true;     // MNL_POL_LEAN=0: every polarization chunk in the general kernel
-  int tile_pol_items = 0;   // lean polarization items (lean_body<POLB>) of the tile kernel
   bool tb_last = false;     // the last batch of >= 2 steps stepped in pairs (tb_usable)
   int tb_res = -1;          // MNL_TB_RES: CUs the pairs' persistent launches leave free (-1:
                             // TB_RES_CUS with several ranks, 0 with one; A/B of the reservation)
@@ -2460,30 +2458,6 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
     const int ny = G.hi[1] - G.lo[1] + 1, nt = (ny + 13) / 14;
     for (int t = 0; t < nt; t++) yb.push_back(G.lo[1] + (int)((long long)ny * t / nt));
   }
-  // lean tiles of the polarization chunks (one isotropic Lorentzian): the tile kernel's
-  // lean_body<POLB> takes the tiles whose x / y footprint lies in L ([ltx0, ltx1] x [lty0,
-  // lty1] in tile indices), the general kernel the rest of those chunks; its rows are cut at
-  // the same y bounds
-  int ltx0 = 0, ltx1 = -1, lty0 = 0, lty1 = -1;
-  if (F->pol_lean && F->f.npol == 1 && !F->upnl && !F->f.aniso) {
-    for (size_t t = 0; t < xb.size(); t++) {
-      const int x0 = xb[t], x1 = (t + 1 < xb.size() ? xb[t + 1] : G.hi[0] + 1) - 1;
-      if (x0 - 1 >= L.lo[0] && x1 + 1 <= L.hi[0]) {
-        if (ltx1 < ltx0) ltx0 = (int)t;
-        ltx1 = (int)t;
-      }
-    }
-    for (size_t t = 0; t < yb.size(); t++) {
-      const int y0 = yb[t] - 1, y1 = (t + 1 < yb.size() ? yb[t + 1] : G.hi[1] + 1) - 1;
-      if (y0 >= L.lo[1] && y1 + 1 <= L.hi[1]) {
-        if (lty1 < lty0) lty0 = (int)t;
-        lty1 = (int)t;
-      }
-    }
-  }
-  const bool polt = ltx1 >= ltx0 && lty1 >= lty0;
-  const int PY0 = polt ? yb[lty0] : 0;
-  const int PY1 = polt ? (lty1 + 1 < (int)yb.size() ? yb[lty1 + 1] : G.hi[1] + 1) - 1 : -1;
   int pzl = INT32_MAX, pzh = -1;
   for (int k = 0; k < F->f.npol; k++)
     if (F->f.pol[k].nz.lo[2] <= F->f.pol[k].nz.hi[2]) {
@@ -2558,13 +2532,7 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
     }
   };
   for (auto &sg : seg) split_bal(sg.first.first, sg.first.second, sg.second ? pzc : zc, sg.second);
-  if (polt) {  // general rows cut at the lean polarization tiles' y bounds
-    split_range(gyb, G.lo[1], PY0, FUSED_GW_ROWS, 1);
-    split_range(gyb, PY0, PY1 + 1, FUSED_GW_ROWS, 1);
-    split_range(gyb, PY1 + 1, G.hi[1] + 1, FUSED_GW_ROWS, 1);
-  } else {
-    split_range(gyb, G.lo[1], G.hi[1] + 1, FUSED_GW_ROWS, 1);
-  }
+  split_range(gyb, G.lo[1], G.hi[1] + 1, FUSED_GW_ROWS, 1);
   if ((int)xb.size() > FUSED_MAXX || (int)yb.size() > FUSED_MAXY ||
       (int)gyb.size() > FUSED_MAXGY || (int)zb.size() > FUSED_MAXZ)
     return false;
@@ -2596,32 +2564,13 @@ bool make_tile_boxes(mnl_fields *F, const Box &G, const Box &L) {
   F->titems.clear();
   F->gitems.clear();
   F->tile_cells = F->lean_cells = F->gen_cells = 0;
-  F->tile_pol_items = 0;
   F->tile_z.assign(std::max(g.N[2], 1), 0);
   std::vector<int> early, heavy, lean, gen_e, gen_r;
   for (int ch = 0; ch < a.nch; ch++) {
     const int zs = a.zb[ch], ze = a.zb[ch + 1];
     if (polch[ch]) {
-      // lean tiles of the chunk (its planes' footprint in L too): tile kernel, body 0 | POLB
-      const bool pl = polt && zs - 1 >= L.lo[2] && ze <= L.hi[2];
-      if (pl)
-        for (int ty = lty0; ty <= lty1; ty++)
-          for (int tx = ltx0; tx <= ltx1; tx++) {
-            const int x0 = a.xb[tx], x1 = a.xb[tx + 1] - 1, y0 = a.yb[ty] - 1, y1 = a.yb[ty + 1] - 1;
-            bool in_l;
-            const int code = tile_item_code(F, a, L, x0, x1, y0, y1, zs, ze, &in_l);
-            if (!in_l) return false;  // cannot happen (the footprint lies in L)
-            const long long cells = (long long)(x1 - x0 + 1) * (y1 - y0) * (ze - zs);
-            F->tile_cells += cells;
-            F->lean_cells += cells;
-            const int v = tx | (ty << 8) | (ch << 16) | code | (1 << 30);
-            F->tile_pol_items++;
-            (F->nranks > 1 && ch == 0 ? early : lean).push_back(v);
-          }
       for (int ty = 0; ty < a.ngy; ty++)
         for (int tx = 0; tx < a.nx; tx++) {
-          if (pl && tx >= ltx0 && tx <= ltx1 && a.gyb[ty] >= PY0 && a.gyb[ty + 1] - 1 <= PY1)
-            continue;  // in the tile kernel's lean polarization items
           const int y0 = a.gyb[ty] - 1;
           const int lo[3] = {a.xb[tx] - 1, y0, zs - 1};
           const int hi[3] = {a.xb[tx] + FX_HOST, y0 + FUSED_GW_ROWS + 1, ze + 1};
@@ -3972,10 +3921,21 @@ int tb_plan(mnl_fields *F) {
     }
   }
   F->tb_cells = F->tb_border = 0;
+  // z pieces of a column of items: balanced chunks of <= tz planes.  (Long pieces over most
+  // of a column with short ones queued last, to save most pieces' three halo planes, measured
+  // no faster in-process: 2.2685 vs 2.2693 ms/step at 512^3, round 5 -- not kept.)
+  auto zpieces = [&](int z0, int nz) {
+    std::vector<std::pair<int, int>> v;  // [lo, hi] inclusive
+    const int nch = (nz + tz - 1) / tz;
+    for (int ch = 0; ch < nch; ch++)
+      v.push_back({z0 + (int)((long long)nz * ch / nch), z0 + (int)((long long)nz * (ch + 1) / nch) - 1});
+    return v;
+  };
+  std::vector<TB2Item> items;
   for (const Box &b : two) {
     const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + TB_OY - 1) / TB_OY;
-    const int nz = b.hi[2] - b.lo[2] + 1, nch = (nz + tz - 1) / tz;
-    for (int ch = 0; ch < nch; ch++)
+    const int nz = b.hi[2] - b.lo[2] + 1;
+    for (const auto &zp : zpieces(b.lo[2], nz))
       for (int ty = 0; ty < nty; ty++)
         for (int x0 = b.lo[0]; x0 <= b.hi[0];) {
           // lanes from the 64-byte line at or below x0 - 2 (TB_HX = 4 columns left of x0 when
@@ -3986,8 +3946,8 @@ int tb_plan(mnl_fields *F) {
           x0 = o.hi[0] + 1;
           o.lo[1] = b.lo[1] + (int)((long long)ny * ty / nty);
           o.hi[1] = b.lo[1] + (int)((long long)ny * (ty + 1) / nty) - 1;
-          o.lo[2] = b.lo[2] + (int)((long long)nz * ch / nch);
-          o.hi[2] = b.lo[2] + (int)((long long)nz * (ch + 1) / nch) - 1;
+          o.lo[2] = zp.first;
+          o.hi[2] = zp.second;
           // faces bordering the rim: the layer outside the face, widened by 1 along the other
           // axes (points of an edge / corner see diagonal neighbours), meets a rim box
           int faces = 0;
@@ -4041,12 +4001,17 @@ int tb_plan(mnl_fields *F) {
               nb += nb2;
             }
           }
-          F->tb_items.push_back(it);
+          items.push_back(it);
           F->tb_cells += double(o.hi[0] - o.lo[0] + 1) * (o.hi[1] - o.lo[1] + 1) *
                          (o.hi[2] - o.lo[2] + 1);
           F->tb_border += nb;  // an upper bound (edges counted twice)
         }
   }
+  // the work queue takes the items in list order: longest first
+  std::stable_sort(items.begin(), items.end(), [](const TB2Item &p, const TB2Item &q) {
+    return (p.z >> 16) - (p.z & 0xFFFF) > (q.z >> 16) - (q.z & 0xFFFF);
+  });
+  F->tb_items = items;
   // ---- upload, palette-uniform flags, mixed-palette cell counts (traffic model)
   if (dev_upload(F, &F->d_tb_ritems, F->tb_rcap, F->tb_ritems) ||
       dev_upload(F, &F->d_tb_rgeo, F->tb_gcap, F->tb_rgeo) ||
@@ -6080,7 +6045,6 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tz = getenv("MNL_TB_ZCHUNK"))
     F->tb_zchunk = std::max(0, atoi(tz)), F->tb_zchunk_env = true;
   if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
-  if (const char *pl = getenv("MNL_POL_LEAN")) F->pol_lean = atoi(pl) != 0;
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *tr = getenv("MNL_TB_RES")) F->tb_res = std::max(0, atoi(tr));
   if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
@@ -7198,6 +7162,18 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
 int mnl_fields_set_temporal_blocking(mnl_fields *F, int on) {
   if (!F) return fail("null fields");
   F->tb_enabled = on != 0;
+  return 0;
+}
+
+int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
+  if (!F) return fail("null fields");
+  const bool v = value != 0;
+  if (which == 0) {
+    F->tb_narrow = v;
+  } else {
+    return fail("bad schedule option");
+  }
+  F->tb_sig = 0;  // the pair plan is rebuilt at the next batch
   return 0;
 }
 

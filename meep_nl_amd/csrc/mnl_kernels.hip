@@ -1656,9 +1656,8 @@ __device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
 
 struct FBatch {  // what B(k) needs besides E(k): own raw at k+1, B_old(k), halo raw at k
   double d0, d1, d2, u0, u1, u2, b0, b1, b2, h0, h1, hu0, hu1;
-  double e0, e1, e2;  // lean_body<POLB>: stored E(k+1) of polarization-box points
   unsigned ui, hui;  // UMODE 2: chi1inv palette indices (byte per component)
-  bool f, hf, ps;
+  bool f, hf;
 };
 // UMODE: 0 = no chi1inv (E = D), 1 = f64 chi1inv arrays, 2 = chi1inv palette:
 // a byte index per cell and component (packed in one 32-bit word) into a
@@ -2351,13 +2350,7 @@ __global__ __launch_bounds__(64 * GEN_WAVES, FUSED_GEN_WPE) void fused_general_k
 // the lean box L: no PML, every component owned, H == B, E implicit.  1024 threads:
 // waves 0..FR-1 hold one row each (row 0 = the y-1 halo row, B recomputed), wave FR the
 // x-1 column (B recomputed), the E of the x+64 column and a corner.
-// POLB (item bit 30 with body 0): the item lies in a polarization chunk (one isotropic
-// Lorentzian susceptibility).  Points of the polarization box store E = chi1inv (D - P)
-// (src/update_eh.cpp:84-146, src/step_generic.cpp:888-903 with f_minus_p) and update P / P_prev
-// (update_pols -> lorentzian update_P, src/susceptibility.cpp:251-258) -- the general body's
-// polarization branch, operand for operand; their E is read as stored E, never as chi1inv * D.
-// Points of the chi(2) box (FusedArgs::xbox) leave E and P to the NR kernel.
-template <int UMODE, int DIST, bool POLB = false>
+template <int UMODE, int DIST>
 __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned uw,
                                           const double (*sU)[256], double (*sE)[FR + 1][FXL],
                                           double (*sB)[FR][FXL]) {
@@ -2459,36 +2452,16 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
         (unsigned)((max(x0 - 1, flo0) + (long long)max(y0, flo1) * a.st1 +
                     (long long)max(zs - 1, flo2) * a.st2) * 4);
     auto uoff = [&](unsigned o8) { return uni ? ufix : (o8 >> 1); };
-    // POLB: the polarization box (stored E) and the chi(2) box, per lane in x / y
-    const bool pxy = POLB && gx >= a.pbox.lo[0] && gx <= a.pbox.hi[0] && gy >= a.pbox.lo[1] &&
-                     gy <= a.pbox.hi[1];
-    const bool hpxy = POLB && hx >= a.pbox.lo[0] && hx <= a.pbox.hi[0] && hy >= a.pbox.lo[1] &&
-                      hy <= a.pbox.hi[1];
-    const bool xxy = POLB && gx >= a.xbox.lo[0] && gx <= a.xbox.hi[0] && gy >= a.xbox.lo[1] &&
-                     gy <= a.xbox.hi[1];
-    const int pzl = POLB ? a.pbox.lo[2] : 1, pzh = POLB ? a.pbox.hi[2] : 0;
-    const int xzl = POLB ? a.xbox.lo[2] : 1, xzh = POLB ? a.xbox.hi[2] : 0;
-    auto pin = [&](int z) { return POLB && z >= pzl && z <= pzh; };
 
     auto load = [&](int k) -> FBatch {
       FBatch q;
       const int z1 = k + 1;
-      const bool ps = pxy && colF && pin(z1);  // stored E at this own point (polarization box)
-      q.ps = ps;
-      q.f = colF && zin(z1) && !ps;
+      q.f = colF && zin(z1);
       const unsigned o = cbl + (unsigned)z1 * s2;
       const bool zf = zin(z1);  // uniform
       q.d0 = ldg(zf ? pO0 : Ev[0], o);
       q.d1 = ldg(zf ? pO1 : Ev[1], o);
       q.d2 = ldg(zf ? pO2 : Ev[2], o);
-      q.e0 = q.e1 = q.e2 = 0.0;
-      if (POLB) {
-        KFA &ai = *kargs_opaque();  // (pointers re-read per plane, as the P arrays')
-        const unsigned oe = ps ? o : MNL_OOB;
-        q.e0 = bld(brsrc_at((unsigned long long)sgpr_ptr(ai.E[0]), nrec), oe);
-        q.e1 = bld(brsrc_at((unsigned long long)sgpr_ptr(ai.E[1]), nrec), oe);
-        q.e2 = bld(brsrc_at((unsigned long long)sgpr_ptr(ai.E[2]), nrec), oe);
-      }
       if (UMODE == 2) {
         q.ui = ldu(uix, uoff(o));
       } else if (HAS_U) {
@@ -2504,14 +2477,13 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
       q.b0 = ldg(Bv[0], (SKIPB && wu == FR) ? safe : ob);
       q.b1 = ldg(Bv[1], (SKIPB && wu == 0) ? safe : ob);
       q.b2 = ldg(Bv[2], ob);
-      const bool hps = hpxy && pin(k);  // halo point of the polarization box: stored E
-      q.hf = hF && zin(k) && !hps;
+      q.hf = hF && zin(k);
       q.h0 = q.h1 = 0.0;
       q.hu0 = q.hu1 = 1.0;
       q.hui = 0;
       if (hwave) {  // only waves FR-1 and FR carry halo slots
         const unsigned oh = hbl + (unsigned)k * s2;
-        const bool zk = zin(k) && !hps;
+        const bool zk = zin(k);  // uniform
         q.h0 = ldg(zk ? pH0 : hE0, oh);
         q.h1 = ldg(zk ? pH1 : hE1, oh);
         if (UMODE == 2) {
@@ -2528,7 +2500,7 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
     double ex, ey, ez;
     {
       const int z = zs - 1;
-      const bool f0 = colF && zin(z) && !(pxy && pin(z));
+      const bool f0 = colF && zin(z);
       const unsigned o = cbl + (unsigned)z * s2;
       ex = ldg(f0 ? Dv[0] : Ev[0], o);
       ey = ldg(f0 ? Dv[1] : Ev[1], o);
@@ -2550,8 +2522,6 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
 #pragma unroll
     for (int j = 0; j < DIST; j++) q[j] = load(min(zs - 1 + j, ze - 1));
     double dx = 0, dy = 0, dz = 0, hmx = 0, hmy = 0;
-    unsigned uik = 0;                  // POLB: palette word of plane k (UMODE 2)
-    double uk0 = 1, uk1 = 1, uk2 = 1;  // POLB: chi1inv of plane k (UMODE 1)
     const int rowm = row > 0 ? row - 1 : 0, colm = col > 0 ? col - 1 : 0;
     const int ngrp = (ze - zs + 1 + DIST) / (DIST + 1);  // iterations k = zs-1 .. ze-1, padded
     for (int g = 0; g < ngrp; g++) {
@@ -2560,25 +2530,6 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
         const int k = zs - 1 + g * (DIST + 1) + j;
         q[(j + DIST) % (DIST + 1)] = load(min(k + DIST, ze - 1));
         const FBatch &c = q[j];
-        // POLB: P, P_prev, sigma of this own point at plane k (used after the D update)
-        double pv[3] = {0, 0, 0}, ppv[3] = {0, 0, 0}, sg[3] = {0, 0, 0};
-        const bool pk = POLB && store && k >= zs && k < ze && pxy && pin(k) &&
-                        !(xxy && k >= xzl && k <= xzh);
-        // (the polarization arrays' pointers are re-read per plane through an opaque kernarg
-        // pointer: scalar loads instead of SGPRs live across the loop, which would spill)
-        KFA &ai = *kargs_opaque();
-        if (POLB) {
-          const unsigned op = pk ? cb + (unsigned)k * s2 : MNL_OOB;
-#pragma unroll
-          for (int cc = 0; cc < 3; cc++) {
-            const unsigned long long pP = (unsigned long long)sgpr_ptr(ai.pol[0].P[cc]);
-            const unsigned long long pQ = (unsigned long long)sgpr_ptr(ai.pol[0].Pp[cc]);
-            const unsigned long long pS = (unsigned long long)sgpr_ptr(ai.pol[0].sigma[cc]);
-            pv[cc] = bld(brsrc_at(pP, nrec), op);
-            ppv[cc] = bld(brsrc_at(pQ, nrec), op);
-            sg[cc] = bld(brsrc_at(pS, nrec), op);
-          }
-        }
         double e1x, e1y, e1z;
         if (UMODE == 2) {
           e1x = e_of(c.d0, pu(c.ui, 0), c.f);
@@ -2589,7 +2540,6 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
           e1y = e_of(c.d1, c.u1, c.f);
           e1z = e_of(c.d2, c.u2, c.f);
         }
-        if (POLB && c.ps) e1x = c.e0, e1y = c.e1, e1z = c.e2;
         if (ownlike) {
           sE[0][row][col] = ex;
           sE[1][row][col] = ey;
@@ -2622,44 +2572,14 @@ __device__ __forceinline__ void lean_body(KFA &a, const ItemGeo &itg, unsigned u
         __syncthreads();
         const double Hz_ym = sB[2][rowm][col], Hx_ym = sB[0][rowm][col];
         const double Hz_xm = sB[2][row][colm], Hy_xm = sB[1][row][colm];
-        const double Dn0 = dx - C * (Hz_ym - Bz + By - hmy);
-        const double Dn1 = dy - C * (hmx - Bx + Bz - Hz_xm);
-        const double Dn2 = dz - C * (Hy_xm - By + Bx - Hx_ym);
-        bst(rD[0], os, Dn0);
-        bst(rD[1], os, Dn1);
-        bst(rD[2], os, Dn2);
-        if (POLB) {  // E = chi1inv (D - P), then update_P with W = E (general body's branch)
-          const unsigned op = pk ? cb + (unsigned)k * s2 : MNL_OOB;
-          const double Dn3[3] = {Dn0, Dn1, Dn2};
-#pragma unroll
-          for (int cc = 0; cc < 3; cc++) {
-            const bool hp = ai.pol[0].P[cc] != nullptr;
-            const double kk = UMODE == 2 ? pu(uik, cc) : (cc == 0 ? uk0 : (cc == 1 ? uk1 : uk2));
-            const double gs = hp ? Dn3[cc] - pv[cc] : Dn3[cc];
-            const double fw = HAS_U ? gs * kk : gs;
-            bst(brsrc_at((unsigned long long)sgpr_ptr(ai.En[cc]), nrec), op, fw);
-            if (hp) {
-              const auto &pd = ai.pol[0];
-              bst(brsrc_at((unsigned long long)sgpr_ptr(pd.P[cc]), nrec), op,
-                  pd.gamma1inv * (pv[cc] * (2 - pd.omega0dtsqr_denom) - pd.gamma1 * ppv[cc] +
-                                  pd.omega0dtsqr * (sg[cc] * fw)));
-              bst(brsrc_at((unsigned long long)sgpr_ptr(pd.Pp[cc]), nrec), op, pv[cc]);
-            }
-          }
-        }
+        bst(rD[0], os, dx - C * (Hz_ym - Bz + By - hmy));
+        bst(rD[1], os, dy - C * (hmx - Bx + Bz - Hz_xm));
+        bst(rD[2], os, dz - C * (Hy_xm - By + Bx - Hx_ym));
         hmx = Bx;
         hmy = By;
-        // D_old of the next plane (a polarization-box point loaded D and its stored E apart)
         dx = c.d0;
         dy = c.d1;
         dz = c.d2;
-        if (POLB) {
-          if (UMODE == 2) {
-            uik = c.ui;
-          } else if (HAS_U) {
-            uk0 = c.u0, uk1 = c.u1, uk2 = c.u2;
-          }
-        }
         ex = e1x;
         ey = e1y;
         ez = e1z;
@@ -3447,10 +3367,7 @@ __device__ __forceinline__ void tile_item_body(KFA &a, int item, const ItemGeo &
   double(*sB)[FR][FXL] = reinterpret_cast<double(*)[FR][FXL]>(sm + TILE_SE);
   switch ((item >> 24) & 7) {
     case 0:
-      if ((item >> 30) & 1)  // lean item of a polarization chunk (one isotropic Lorentzian)
-        lean_body<UMODE, DIST, true>(a, itg, uw, sU, sE, sB);
-      else
-        lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
+      lean_body<UMODE, DIST>(a, itg, uw, sU, sE, sB);
       break;
     case 1:
       if ((item >> 30) & 1) {  // narrow x-face strip (temporal-blocking rim; host: OWNC)

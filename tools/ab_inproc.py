@@ -1,0 +1,62 @@
+"""In-process A/B of a scheduling option of the fused step (Fields.set_schedule: identical
+results, different scheduling): one process, one allocation, the two settings alternated
+--rounds times, --steps timed steps each after a re-plan warm-up, medians reported.  Between
+processes the same kernel varies with page placement, so options are
+compared inside one process.
+
+  python tools/ab_inproc.py --option narrow [--workload waveguide] [--size 512] [--rounds 4]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--option", required=True, choices=["narrow"])
+    ap.add_argument("--workload", default="waveguide")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--tune", action="store_true")
+    ap.add_argument("--retune", action="store_true",
+                    help="tune again after every switch (options that change the tuner's choice)")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    import bench
+    from meep_nl_amd import core
+    core.set_verbosity(0)
+    gv, s, f = bench.build_fields(a.workload, a.size, 0, 1, 0, None)
+    if a.tune:
+        f.tune()
+    f.step(6)
+    res = {0: [], 1: []}
+    for r in range(a.rounds):
+        for v in ((1, 0) if r % 2 else (0, 1)):
+            f.set_schedule(a.option, v)
+            if a.retune:
+                f.tune()
+            f.step(4)  # re-plan / re-enter the fused mode outside the timed steps
+            t0 = time.perf_counter()
+            f.step(a.steps)
+            ms = (time.perf_counter() - t0) / a.steps * 1e3
+            res[v].append(ms)
+            print(f"round {r} {a.option}={v}: {ms:.4f} ms/step", flush=True)
+    out = {"option": a.option, "workload": a.workload, "size": a.size, "steps": a.steps,
+           "ms_per_step": {str(k): v for k, v in res.items()},
+           "median": {str(k): statistics.median(v) for k, v in res.items()}}
+    out["gain"] = 1.0 - out["median"]["1"] / out["median"]["0"]
+    print(json.dumps(out))
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
