@@ -375,8 +375,10 @@ int mnl_fields_tb_info(mnl_fields *f, double *out, int n);
 int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
 /* Scheduling options of the fused step (no reference counterpart; an option only changes how
  * the same per-point arithmetic is scheduled, results are identical): which = 0 the narrow
- * x-face strip body of the temporal-blocking rim (MNL_TB_NARROW).  The pair plan is rebuilt at
- * the next step.  For in-process A/B measurements (tools/ab_inproc.py). */
+ * x-face strip body of the temporal-blocking rim (MNL_TB_NARROW; the pair plan is rebuilt at
+ * the next step), 1 DFT sampling plans with chi1inv as palette bytes (MNL_DFT_PAL; the plans
+ * are rebuilt at the next update).  For in-process A/B measurements
+ * (tools/ab_inproc.py). */
 int mnl_fields_set_schedule(mnl_fields *f, int which, int value);
 
 /* ---- checkpoint (src/fields_dump.cpp, src/structure_dump.cpp) -----------

@@ -581,8 +581,9 @@ class Fields:
 
     def set_schedule(self, which, value):
         """Scheduling option (identical results): 'narrow' = the narrow x-face strip body of
-        the temporal-blocking rim (mnl_fields_set_schedule)."""
-        idx = {"narrow": 0}[which]
+        the temporal-blocking rim, 'dft_pal' = DFT sampling plans carrying chi1inv as palette
+        bytes (mnl_fields_set_schedule)."""
+        idx = {"narrow": 0, "dft_pal": 1}[which]
         check(lib().mnl_fields_set_schedule(self.h, idx, 1 if value else 0))
 
     def tb_info(self):

@@ -221,15 +221,20 @@ struct DftFluxH {
   int nbuf = 0;                       // buffered updates (rows row-nbuf .. row-1)
   int kb = DFT_KB;                    // updates per accumulation
   double bytes = 0;                   // algorithmic bytes of one update (DESIGN.md "DFT")
-  void *d_sidx = nullptr;             // sampling plan (k_dft_plan): 4 int32 indices per point
+  int *d_sidx = nullptr;              // sampling plan (k_dft_plan): first Yee index per point
   unsigned short *d_ssel = nullptr;   // ... and a selector per point
-  void *d_su = nullptr;               // ... and 4 chi1inv values (implicit E) per point
+  unsigned *d_spal = nullptr;         // ... and the palette bytes of its implicit-E chi1inv
+  void *d_su = nullptr;               // ... or those chi1inv values as doubles (fallback)
+  int *d_bad = nullptr;               // palette check of the plan (k_dft_plan)
+  bool usepal = false;                // the plan's palette bytes are exact
   long long plan_key = -1;            // the mode the plan was built for (dft_plan_key)
   ~DftFluxH() {
     if (d_ph) (void)hipFree(d_ph);
     if (d_sidx) (void)hipFree(d_sidx);
     if (d_ssel) (void)hipFree(d_ssel);
+    if (d_spal) (void)hipFree(d_spal);
     if (d_su) (void)hipFree(d_su);
+    if (d_bad) (void)hipFree(d_bad);
   }
 };
 
@@ -370,6 +375,7 @@ struct mnl_fields {
   bool tb_oom = false;      // the middle buffer set did not fit: temporal blocking off
   bool tb_oom_test = false; // MNL_TB_OOM=1: its allocation fails (tests)
   bool tb_narrow = true;    // MNL_TB_NARROW=0: no narrow x-face strip items (A/B)
+  bool dft_pal = true;      // MNL_DFT_PAL=0: DFT sampling plans carry chi1inv as doubles (A/B)
   int tb_nnarrow = 0;       // narrow x-face strip items of the current plan
   int tb_rfree = 0;         // leading rim items that read no slab-face data (multi-rank)
   bool tb_chain_pending = false;  // the last multi-rank pair's s_comm chain not yet joined
@@ -2095,6 +2101,15 @@ long long dft_plan_key(const mnl_fields *F) {
 // step of a pair from the mid set)
 int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr) {
   const bool planned = F->nlocal < (size_t(1) << 31);  // int32 indices in the plan
+  const DevFields &fs = fields ? *fields : F->f;
+  // the samples of every flux object due: planned ones in merged launches of up to DFT_MAXJ
+  DftSampleJobs J{};
+  auto launch = [&]() -> int {
+    if (J.n && k_dft_sample_jobs(J, F->g, fs, F->d_utab, F->stream))
+      return fail("dft sample launch failed");
+    J = DftSampleJobs{};
+    return 0;
+  };
   for (auto &op : F->dfts) {
     DftFluxH &o = *op;
     if (t % o.decim || !o.npts) continue;
@@ -2103,22 +2118,41 @@ int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr) {
       const long long key = dft_plan_key(F);
       if (o.plan_key != key) {
         if (!o.d_sidx) {
-          HIPCHK(hipMalloc(&o.d_sidx, o.npts * 16));
+          HIPCHK(hipMalloc(&o.d_sidx, o.npts * 4));
           HIPCHK(hipMalloc(&o.d_ssel, o.npts * 2));
+          HIPCHK(hipMalloc(&o.d_spal, o.npts * 4));
           HIPCHK(hipMalloc(&o.d_su, o.npts * 32));
+          HIPCHK(hipMalloc(&o.d_bad, sizeof(int)));
         }
-        if (k_dft_plan(o.d_pj, o.d_pch, o.d_ch, (long long)o.npts, F->g, F->f, o.d_sidx,
-                       o.d_ssel, o.d_su, F->stream))
+        const bool pal = F->fused && F->d_uidx && F->d_utab && F->dft_pal;
+        HIPCHK(hipMemsetAsync(o.d_bad, 0, sizeof(int), F->stream));
+        if (k_dft_plan(o.d_pj, o.d_pch, o.d_ch, (long long)o.npts, F->g, F->f,
+                       pal ? F->d_uidx : nullptr, pal ? F->d_utab : nullptr, o.d_sidx, o.d_ssel,
+                       o.d_spal, o.d_su, o.d_bad, F->stream))
           return fail("dft plan launch failed");
+        int bad = 1;
+        if (pal) {  // once per plan: are the palette bytes exact for every implicit value?
+          HIPCHK(hipMemcpyAsync(&bad, o.d_bad, sizeof(int), hipMemcpyDeviceToHost, F->stream));
+          HIPCHK(hipStreamSynchronize(F->stream));
+        }
+        o.usepal = pal && bad == 0;
         o.plan_key = key;
       }
-      if (k_dft_sample_plan(o.d_sidx, o.d_ssel, o.d_su, o.d_pw, fr, (long long)o.npts,
-                            fields ? *fields : F->f, F->stream))
-        return fail("dft sample launch failed");
-    } else if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, fr, (long long)o.npts, F->g,
-                            fields ? *fields : F->f, F->stream)) {
+      if (J.n == DFT_MAXJ && launch()) return -1;
+      DftSampleJob &jb = J.j[J.n++];
+      jb.sidx = o.d_sidx, jb.ssel = o.d_ssel, jb.spal = o.d_spal, jb.su = o.d_su;
+      jb.pw = o.d_pw, jb.fr = fr, jb.npts = (long long)o.npts, jb.blk0 = J.nblk;
+      jb.usepal = o.usepal ? 1 : 0;
+      J.nblk += ((long long)o.npts + 255) / 256;
+    } else if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, fr, (long long)o.npts, F->g, fs,
+                            F->stream)) {
       return fail("dft sample launch failed");
     }
+  }
+  if (launch()) return -1;
+  for (auto &op : F->dfts) {
+    DftFluxH &o = *op;
+    if (t % o.decim || !o.npts) continue;
     o.nbuf++;
     o.row++;
     if (o.nbuf == o.kb && dft_flush(F, o)) return -1;
@@ -6046,6 +6080,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
     F->tb_zchunk = std::max(0, atoi(tz)), F->tb_zchunk_env = true;
   if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
+  if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
   if (const char *tr = getenv("MNL_TB_RES")) F->tb_res = std::max(0, atoi(tr));
   if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
@@ -7170,6 +7205,9 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
   const bool v = value != 0;
   if (which == 0) {
     F->tb_narrow = v;
+  } else if (which == 1) {
+    F->dft_pal = v;
+    for (auto &o : F->dfts) o->plan_key = -1;  // plans rebuilt at the next update
   } else {
     return fail("bad schedule option");
   }

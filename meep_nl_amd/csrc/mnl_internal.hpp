@@ -435,14 +435,32 @@ constexpr int DFT_KB = 32;  // updates buffered per accumulation (the DFT array 
 constexpr int DFT_FT = 8;   // frequency tile of the accumulation
 int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunkDev *ch, double *fr,
                  long long npts, const DevGrid &g, const DevFields &f, void *stream);
-// sampling plan of one flux object (per point: 4 int32 Yee indices, a 16-bit selector, the
-// chi1inv of its implicit-E values; see dft_plan_kernel), then the sample of one update
+// sampling plan of one flux object (per point: the first Yee index, a 16-bit selector, the
+// palette bytes and the doubles of the chi1inv of its implicit-E values; see
+// dft_plan_kernel), then the sample of one update of every flux object due (one launch)
 int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
-               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel, void *su,
-               void *stream);
-int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const void *su,
-                      const double *pw, double *fr, long long npts, const DevFields &f,
-                      void *stream);
+               const DevGrid &g, const DevFields &f, const unsigned *uidx, const double *utab,
+               int *sidx, unsigned short *ssel, unsigned *spal, void *su, int *bad, void *stream);
+constexpr int DFT_MAXJ = 8;  // flux objects per sample launch
+struct DftSampleJob {
+  const int *sidx;
+  const unsigned short *ssel;
+  const unsigned *spal;
+  const void *su;
+  const double *pw;
+  double *fr;       // this update's sample row
+  long long npts;
+  long long blk0;   // first workgroup of the job
+  int usepal;       // chi1inv from the palette bytes (else the doubles)
+};
+struct DftSampleJobs {
+  DftSampleJob j[DFT_MAXJ];
+  int n;
+  long long nblk;   // workgroups of all jobs
+  long long sd[3];  // set by k_dft_sample_jobs (grid strides per direction)
+};
+int k_dft_sample_jobs(const DftSampleJobs &J, const DevGrid &g, const DevFields &f,
+                      const double *utab, void *stream);
 int k_dft_accum(const int *pj, const int *pch, double *dft, const double *fr, int n,
                 const double *ph, long long rstride, int nfreq, long long npts, void *stream);
 int k_init_add(double *dst, double *alt, const double *src, const DevGrid &g, const DevFields &f,

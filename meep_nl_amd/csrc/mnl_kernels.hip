@@ -4351,21 +4351,27 @@ __global__ void dft_sample_kernel(const int *__restrict__ pj, const double *__re
   fr_out[p] = fr;
 }
 
-// Sampling plan (built once per fused-mode epoch): per point the linear indices of the 1-4
-// Yee values its centred average reads and, per value, where it lives (0 stored E, 1 implicit
-// E = D * chi1inv, 2 B (H == B), 3 separate H) -- the per-point table lookups of
-// dft_sample_kernel (PML flags, ownership, fused box) done once, so that the per-step sample
-// is one metadata load and independent value loads.  sel: bits 0-1 component direction,
-// 2-3 avgmode, 4 + 2v: kind of value v; 0xFFFF: another rank's point.
+// Sampling plan (built once per fused-mode epoch): per point the linear index of the first
+// of the 1-4 Yee values its centred average reads (the others are +d1, +d2, +d1+d2) and, per
+// value, where it lives (0 stored E, 1 implicit E = D * chi1inv, 2 B (H == B), 3 separate H)
+// -- the per-point table lookups of dft_sample_kernel (PML flags, ownership, fused box) done
+// once, so that the per-step sample is one metadata load and independent value loads.
+// sel: bits 0-1 component direction, 2-3 avgmode, 4 + 2v: kind of value v, 12-13 d1, 14-15
+// d2; 0xFFFF: another rank's point.  The chi1inv of implicit-E values: as the palette bytes of
+// the four values (spal, with uidx / utab: 4 B per point instead of 32) and as doubles (su,
+// the fallback); *bad is set when a palette value is not bitwise the chi1inv array's.
 __global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restrict__ pch,
                                 const DftChunkDev *__restrict__ ch, long long npts, DevGrid g,
-                                DevFields f, int4 *__restrict__ sidx,
-                                unsigned short *__restrict__ ssel, double4 *__restrict__ su) {
+                                DevFields f, const unsigned *__restrict__ uidx,
+                                const double *__restrict__ utab, int *__restrict__ sidx,
+                                unsigned short *__restrict__ ssel, unsigned *__restrict__ spal,
+                                double4 *__restrict__ su, int *__restrict__ bad) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npts) return;
   if (pj[3 * p] < 0) {
     ssel[p] = 0xFFFF;
-    sidx[p] = make_int4(0, 0, 0, 0);
+    sidx[p] = 0;
+    spal[p] = 0;
     su[p] = make_double4(1.0, 1.0, 1.0, 1.0);
     return;
   }
@@ -4397,17 +4403,31 @@ __global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restric
     q[1] = nb(P, cd.d1);
     nv = 2;
   }
-  unsigned sel = (unsigned)d | ((unsigned)cd.avgmode << 2);
-  int idx[4] = {0, 0, 0, 0};
+  unsigned sel = (unsigned)d | ((unsigned)cd.avgmode << 2) |
+                 ((unsigned)max(cd.d1, 0) << 12) | ((unsigned)max(cd.d2, 0) << 14);
   double uv[4] = {1.0, 1.0, 1.0, 1.0};  // chi1inv of implicit-E values (x * 1.0 == x otherwise)
+  unsigned pal = 0;
+  bool mism = false;
   for (int v = 0; v < nv; v++) {
     const unsigned k = kind(q[v]);
     sel |= k << (4 + 2 * v);
-    idx[v] = (int)q[v].idx;
-    if (k == 1 && f.inveps[d]) uv[v] = f.inveps[d][q[v].idx];
+    if (k == 1 && f.inveps[d]) {
+      uv[v] = f.inveps[d][q[v].idx];
+      if (uidx) {
+        const unsigned b = (uidx[q[v].idx] >> (8 * d)) & 255u;
+        pal |= b << (8 * v);
+        mism = mism || utab[d * 256 + b] != uv[v];
+      }
+    } else if (k == 1 && uidx) {  // chi1inv == 1: a palette entry equal to 1.0
+      const unsigned b = (uidx[q[v].idx] >> (8 * d)) & 255u;
+      pal |= b << (8 * v);
+      mism = mism || utab[d * 256 + b] != 1.0;
+    }
   }
+  if (mism) atomicOr(bad, 1);
   ssel[p] = (unsigned short)sel;
-  sidx[p] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+  sidx[p] = (int)P.idx;
+  spal[p] = pal;
   su[p] = make_double4(uv[0], uv[1], uv[2], uv[3]);
 }
 
@@ -4423,59 +4443,78 @@ __device__ __forceinline__ double dft_val(const DftSrc &s, int d, unsigned k, in
 }
 
 // fields::update_dfts' sample of one update (src/dft.cpp:265-300): the reference's centred
-// average (w * 0.25) * (((f0 + f1) + f2) + f3) through the plan
-__global__ void dft_sample_plan_kernel(const int4 *__restrict__ sidx,
-                                       const unsigned short *__restrict__ ssel,
-                                       const double4 *__restrict__ su,
-                                       const double *__restrict__ pw, double *__restrict__ fr_out,
-                                       long long npts, DftSrc s) {
+// average (w * 0.25) * (((f0 + f1) + f2) + f3) through the plan, for every flux object due at
+// this step in one launch (DftSampleJobs: the workgroups of job i are blk0[i] ..)
+typedef const DftSampleJobs __attribute__((address_space(4))) KDJ;
+__global__ void __launch_bounds__(256) dft_sample_jobs_kernel(DftSampleJobs J, DftSrc s,
+                                                              const double *__restrict__ utab) {
   // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8), so
   // each XCD takes one contiguous eighth of the points instead; the 2 x 2 averages of
   // neighbouring rows then meet their shared lines in that XCD's L2
   const unsigned nb = gridDim.x, xcd = blockIdx.x % 8u, q = nb / 8u, r = nb % 8u;
-  const unsigned lb = xcd * q + min(xcd, r) + blockIdx.x / 8u;
-  const long long p = (long long)lb * blockDim.x + threadIdx.x;
-  if (p >= npts) return;
-  const unsigned sel = ssel[p];
+  const long long lb = xcd * q + min(xcd, r) + blockIdx.x / 8u;
+  // the job table through the kernarg pointer (wave-uniform index: scalar loads, no copy)
+  KDJ *jt = (KDJ *)__builtin_amdgcn_kernarg_segment_ptr();
+  int ji = 0;
+  for (int i = 1; i < jt->n; i++)
+    if (lb >= jt->j[i].blk0) ji = i;
+  const auto &jb = jt->j[ji];
+  const long long p = (lb - jb.blk0) * 256 + threadIdx.x;
+  if (p >= jb.npts) return;
+  const unsigned sel = jb.ssel[p];
   if (sel == 0xFFFFu) return;  // another rank's point
-  const int4 ix = sidx[p];
-  const double w = pw[p];
-  const int d = sel & 3, mode = (sel >> 2) & 3;
+  const long long i0 = jb.sidx[p];
+  const double w = jb.pw[p];
+  const int d = sel & 3, mode = (sel >> 2) & 3, d1 = (sel >> 12) & 3, d2 = (sel >> 14) & 3;
+  const long long s1 = d1 == 0 ? J.sd[0] : (d1 == 1 ? J.sd[1] : J.sd[2]);
+  const long long s2 = d2 == 0 ? J.sd[0] : (d2 == 1 ? J.sd[1] : J.sd[2]);
   // chi1inv only for implicit-E values (kind 1 in any slot)
   const bool any1 = ((sel >> 4) & 0x55u & ~((sel >> 5) & 0x55u)) != 0;
-  const double4 u = any1 ? su[p] : make_double4(1.0, 1.0, 1.0, 1.0);
-  const double v0 = dft_val(s, d, (sel >> 4) & 3, ix.x, u.x);
+  double u[4] = {1.0, 1.0, 1.0, 1.0};
+  if (any1) {
+    if (jb.usepal) {
+      const unsigned pal = jb.spal[p];
+#pragma unroll
+      for (int v = 0; v < 4; v++)
+        if (((sel >> (4 + 2 * v)) & 3) == 1) u[v] = utab[d * 256 + ((pal >> (8 * v)) & 255u)];
+    } else {
+      const double4 uu = ((const double4 *)jb.su)[p];
+      u[0] = uu.x, u[1] = uu.y, u[2] = uu.z, u[3] = uu.w;
+    }
+  }
+  const double v0 = dft_val(s, d, (sel >> 4) & 3, (int)i0, u[0]);
   double fr;
   if (mode == 2) {
-    const double v1 = dft_val(s, d, (sel >> 6) & 3, ix.y, u.y);
-    const double v2 = dft_val(s, d, (sel >> 8) & 3, ix.z, u.z);
-    const double v3 = dft_val(s, d, (sel >> 10) & 3, ix.w, u.w);
+    const double v1 = dft_val(s, d, (sel >> 6) & 3, (int)(i0 + s1), u[1]);
+    const double v2 = dft_val(s, d, (sel >> 8) & 3, (int)(i0 + s2), u[2]);
+    const double v3 = dft_val(s, d, (sel >> 10) & 3, (int)(i0 + s1 + s2), u[3]);
     fr = w * (v0 + v1 + v2 + v3);
   } else if (mode == 1) {
-    fr = w * (v0 + dft_val(s, d, (sel >> 6) & 3, ix.y, u.y));
+    fr = w * (v0 + dft_val(s, d, (sel >> 6) & 3, (int)(i0 + s1), u[1]));
   } else {
     fr = w * v0;
   }
-  fr_out[p] = fr;
+  jb.fr[p] = fr;
 }
 
 int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
-               const DevGrid &g, const DevFields &f, void *sidx, unsigned short *ssel, void *su,
-               void *stream) {
+               const DevGrid &g, const DevFields &f, const unsigned *uidx, const double *utab,
+               int *sidx, unsigned short *ssel, unsigned *spal, void *su, int *bad, void *stream) {
   if (npts <= 0) return 0;
   dft_plan_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      pj, pch, ch, npts, g, f, (int4 *)sidx, ssel, (double4 *)su);
+      pj, pch, ch, npts, g, f, uidx, utab, sidx, ssel, spal, (double4 *)su, bad);
   return rc();
 }
 
-int k_dft_sample_plan(const void *sidx, const unsigned short *ssel, const void *su,
-                      const double *pw, double *fr, long long npts, const DevFields &f,
-                      void *stream) {
-  if (npts <= 0) return 0;
+int k_dft_sample_jobs(const DftSampleJobs &J, const DevGrid &g, const DevFields &f,
+                      const double *utab, void *stream) {
+  if (J.n <= 0 || J.n > DFT_MAXJ || J.nblk <= 0) return 0;
+  if (J.j[0].blk0 != 0) return 2;
+  DftSampleJobs t = J;
+  for (int d = 0; d < 3; d++) t.sd[d] = g.sdir[d];
   DftSrc s;
   for (int d = 0; d < 3; d++) s.E[d] = f.E[d], s.D[d] = f.D[d], s.B[d] = f.B[d], s.H[d] = f.H[d];
-  dft_sample_plan_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      (const int4 *)sidx, ssel, (const double4 *)su, pw, fr, npts, s);
+  dft_sample_jobs_kernel<<<(unsigned)J.nblk, 256, 0, (hipStream_t)stream>>>(t, s, utab);
   return rc();
 }
 

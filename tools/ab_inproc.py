@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--option", required=True, choices=["narrow"])
+    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal"])
     ap.add_argument("--workload", default="waveguide")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=4)
@@ -27,12 +27,21 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--retune", action="store_true",
                     help="tune again after every switch (options that change the tuner's choice)")
+    ap.add_argument("--flux", type=int, default=0,
+                    help="N x-normal DFT flux planes as in bench.py --flux")
+    ap.add_argument("--nfreq", type=int, default=50)
     ap.add_argument("--json")
     a = ap.parse_args()
     import bench
     from meep_nl_amd import core
     core.set_verbosity(0)
     gv, s, f = bench.build_fields(a.workload, a.size, 0, 1, 0, None)
+    if a.flux:  # the same monitors as bench.py --flux
+        hx, hy, hz = 0.5 * gv.n[0] / 10.0, 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
+        freqs = [0.1 + 0.1 * i / max(a.nfreq - 1, 1) for i in range(a.nfreq)]
+        for i in range(a.flux):
+            x = -hx + 2 * hx * (i + 1) / (a.flux + 1) + 0.05
+            f.add_dft_flux([([x, -hy, -hz], [x, hy, hz], 0, 1.0)], freqs, 1)
     if a.tune:
         f.tune()
     f.step(6)
@@ -49,6 +58,7 @@ def main():
             res[v].append(ms)
             print(f"round {r} {a.option}={v}: {ms:.4f} ms/step", flush=True)
     out = {"option": a.option, "workload": a.workload, "size": a.size, "steps": a.steps,
+           "flux_planes": a.flux, "nfreq": a.nfreq if a.flux else 0,
            "ms_per_step": {str(k): v for k, v in res.items()},
            "median": {str(k): statistics.median(v) for k, v in res.items()}}
     out["gain"] = 1.0 - out["median"]["1"] / out["median"]["0"]
