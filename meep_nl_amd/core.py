@@ -582,9 +582,13 @@ class Fields:
     def set_schedule(self, which, value):
         """Scheduling option (identical results): 'narrow' = the narrow x-face strip body of
         the temporal-blocking rim, 'dft_pal' = DFT sampling plans carrying chi1inv as palette
-        bytes (mnl_fields_set_schedule)."""
-        idx = {"narrow": 0, "dft_pal": 1}[which]
-        check(lib().mnl_fields_set_schedule(self.h, idx, 1 if value else 0))
+        bytes, 'res' / 'res_tb2' / 'res_rim' = CUs left free by the pair launches (an integer;
+        -1 the default) (mnl_fields_set_schedule)."""
+        idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4}[which]
+        if idx >= 2:  # CUs left free by the pair launches (-1: the default)
+            check(lib().mnl_fields_set_schedule(self.h, idx, int(value)))
+        else:
+            check(lib().mnl_fields_set_schedule(self.h, idx, 1 if value else 0))
 
     def tb_info(self):
         """Temporal blocking of the current fused geometry: dict of

@@ -370,6 +370,7 @@ struct mnl_fields {
   size_t tb_rcap = 0, tb_gcap = 0, tb_icap = 0;
   bool tb_nopair = false;   // MNL_TB_NOPAIR=1: x-face rim strips one per workgroup (A/B)
   bool tb_last = false;     // the last batch of >= 2 steps stepped in pairs (tb_usable)
+  int res_l = -1, res_r = -1;  // schedule options: the same for the two-step / rim launches only
   int tb_res = -1;          // MNL_TB_RES: CUs the pairs' persistent launches leave free (-1:
                             // TB_RES_CUS with several ranks, 0 with one; A/B of the reservation)
   bool tb_oom = false;      // the middle buffer set did not fit: temporal blocking off
@@ -4287,8 +4288,11 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   TB2Args t = tb_args(F, cur, mid, nxt);
   const int nr = (int)F->tb_ritems.size();
   FusedArgs r1 = rim_args(F, fa, cur, mid), r2 = rim_args(F, fa, mid, nxt);
-  if (F->tb_res > 0)  // A/B: the multi-rank reservation on one rank
-    t.wg_limit = r1.wg_limit = r2.wg_limit = std::max(1, k_cu_count() - F->tb_res);
+  {  // CUs left free by the two-step launch / the rim launches (A/B; the multi-rank default)
+    const int rl = F->res_l >= 0 ? F->res_l : F->tb_res, rr = F->res_r >= 0 ? F->res_r : F->tb_res;
+    if (rl > 0) t.wg_limit = std::max(1, k_cu_count() - rl);
+    if (rr > 0) r1.wg_limit = r2.wg_limit = std::max(1, k_cu_count() - rr);
+  }
   int k = ev_begin(TM_TB);
   int kr = k_tb2(t, F->stream, F->ctr_base);
   ev_end(k);
@@ -7205,6 +7209,10 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
   const bool v = value != 0;
   if (which == 0) {
     F->tb_narrow = v;
+  } else if (which >= 2 && which <= 4) {  // CUs left free by the pair launches (single rank)
+    if (value < -1 || value > 1024) return fail("bad reservation");
+    (which == 2 ? F->tb_res : which == 3 ? F->res_l : F->res_r) = value;
+    return 0;
   } else if (which == 1) {
     F->dft_pal = v;
     for (auto &o : F->dfts) o->plan_key = -1;  // plans rebuilt at the next update

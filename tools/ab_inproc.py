@@ -1,6 +1,7 @@
 """In-process A/B of a scheduling option of the fused step (Fields.set_schedule: identical
 results, different scheduling): one process, one allocation, the two settings alternated
---rounds times, --steps timed steps each after a re-plan warm-up, medians reported.  Between
+--rounds times (--values: two or more settings, rotated), --steps timed steps each after a
+re-plan warm-up, medians reported.  Between
 processes the same kernel varies with page placement, so options are
 compared inside one process.
 
@@ -19,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal"])
+    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal", "res", "res_tb2", "res_rim"])
     ap.add_argument("--workload", default="waveguide")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=4)
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--retune", action="store_true",
                     help="tune again after every switch (options that change the tuner's choice)")
+    ap.add_argument("--values", default="0,1",
+                    help="the two settings compared (integers; 0,1 = off / on)")
     ap.add_argument("--flux", type=int, default=0,
                     help="N x-normal DFT flux planes as in bench.py --flux")
     ap.add_argument("--nfreq", type=int, default=50)
@@ -45,9 +48,11 @@ def main():
     if a.tune:
         f.tune()
     f.step(6)
-    res = {0: [], 1: []}
+    vals = [int(x) for x in a.values.split(",")]
+    res = {v: [] for v in vals}
     for r in range(a.rounds):
-        for v in ((1, 0) if r % 2 else (0, 1)):
+        k = r % len(vals)
+        for v in (vals[k:] + vals[:k]) if r % 2 == 0 else (vals[k:] + vals[:k])[::-1]:
             f.set_schedule(a.option, v)
             if a.retune:
                 f.tune()
@@ -61,7 +66,10 @@ def main():
            "flux_planes": a.flux, "nfreq": a.nfreq if a.flux else 0,
            "ms_per_step": {str(k): v for k, v in res.items()},
            "median": {str(k): statistics.median(v) for k, v in res.items()}}
-    out["gain"] = 1.0 - out["median"]["1"] / out["median"]["0"]
+    base = out["median"][str(vals[0])]
+    out["gain"] = {str(v): 1.0 - out["median"][str(v)] / base for v in vals[1:]}
+    if vals == [0, 1]:
+        out["gain"] = out["gain"]["1"]
     print(json.dumps(out))
     if a.json:
         with open(a.json, "w") as fh:
