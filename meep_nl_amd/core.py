@@ -583,8 +583,10 @@ class Fields:
         """Scheduling option (identical results): 'narrow' = the narrow x-face strip body of
         the temporal-blocking rim, 'dft_pal' = DFT sampling plans carrying chi1inv as palette
         bytes, 'res' / 'res_tb2' / 'res_rim' = CUs left free by the pair launches (an integer;
-        -1 the default) (mnl_fields_set_schedule)."""
-        idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4}[which]
+        -1 the default), 'dft_cmp' = pairs sample DFT monitors from the two-step kernel's compact
+        boxes (mnl_fields_set_schedule)."""
+        idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4,
+               "dft_cmp": 5}[which]
         if idx >= 2:  # CUs left free by the pair launches (-1: the default)
             check(lib().mnl_fields_set_schedule(self.h, idx, int(value)))
         else:

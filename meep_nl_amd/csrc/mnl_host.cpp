@@ -227,6 +227,13 @@ struct DftFluxH {
   void *d_su = nullptr;               // ... or those chi1inv values as doubles (fallback)
   int *d_bad = nullptr;               // palette check of the plan (k_dft_plan)
   bool usepal = false;                // the plan's palette bytes are exact
+  // compact box (pairs of steps): bbox's D / B of the two-step points
+  // for both steps of a pair, stored by the two-step kernel; per point its compact index
+  double *d_cmp = nullptr;
+  unsigned cmp_cells = 0;             // 0: the box is too large for a compact copy
+  unsigned cmp_mask = 0;              // arrays the samples read (D0..D2, B0..B2)
+  int *d_sci = nullptr;
+  bool cmp_on = false;                // the current pair plan stores this monitor's box
   long long plan_key = -1;            // the mode the plan was built for (dft_plan_key)
   ~DftFluxH() {
     if (d_ph) (void)hipFree(d_ph);
@@ -235,6 +242,8 @@ struct DftFluxH {
     if (d_spal) (void)hipFree(d_spal);
     if (d_su) (void)hipFree(d_su);
     if (d_bad) (void)hipFree(d_bad);
+    if (d_cmp) (void)hipFree(d_cmp);
+    if (d_sci) (void)hipFree(d_sci);
   }
 };
 
@@ -377,6 +386,8 @@ struct mnl_fields {
   bool tb_oom_test = false; // MNL_TB_OOM=1: its allocation fails (tests)
   bool tb_narrow = true;    // MNL_TB_NARROW=0: no narrow x-face strip items (A/B)
   bool dft_pal = true;      // MNL_DFT_PAL=0: DFT sampling plans carry chi1inv as doubles (A/B)
+  bool dft_cmp = true;      // MNL_DFT_CMP=0: pairs sample DFT monitors from the field arrays
+  std::vector<TBCmp> tb_cmp;  // the compact DFT boxes of the current pair plan
   int tb_nnarrow = 0;       // narrow x-face strip items of the current plan
   int tb_rfree = 0;         // leading rim items that read no slab-face data (multi-rank)
   bool tb_chain_pending = false;  // the last multi-rank pair's s_comm chain not yet joined
@@ -1943,6 +1954,15 @@ int dft_layout(mnl_fields *F, std::unique_ptr<DftFluxH> &o, DftFluxH &ho, std::v
       o->bbox.hi[k] = std::max(o->bbox.hi[k], o->h_pj[3 * p + k] + 1);
     }
   }
+  // compact box (two-step pairs, 3-D): every bbox cell, 2 states x 6 arrays, <= 1 GiB
+  o->cmp_cells = 0, o->cmp_mask = 0;
+  if (F->S.dim == 3 && o->bbox.hi[0] >= 0) {
+    double nc = 1;
+    for (int k = 0; k < 3; k++) nc *= o->bbox.hi[k] - o->bbox.lo[k] + 1;
+    if (nc * 96 <= double(1u << 30)) o->cmp_cells = (unsigned)nc;
+    for (const auto *L : {&o->E, &o->H})
+      for (auto &dc : *L) o->cmp_mask |= 1u << (dc.c >= 3 ? 3 + dc.c % 3 : dc.c % 3);
+  }
   if (o->npts) {
     if (dev_alloc(F, &o->d_pj, o->h_pj.size(), false) || dev_alloc(F, &o->d_pch, o->npts, false) ||
         dev_alloc(F, &o->d_pw, o->npts, false) || dev_alloc(F, &o->d_ch, chd.size(), false) ||
@@ -2100,7 +2120,9 @@ long long dft_plan_key(const mnl_fields *F) {
 
 // fields: the buffer set to sample (null: the current one; temporal blocking samples the middle
 // step of a pair from the mid set)
-int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr) {
+// cstate >= 0: a pair's middle (0) or new (1) state, whose two-step points are also in the
+// monitors' compact boxes
+int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr, int cstate = -1) {
   const bool planned = F->nlocal < (size_t(1) << 31);  // int32 indices in the plan
   const DevFields &fs = fields ? *fields : F->f;
   // the samples of every flux object due: planned ones in merged launches of up to DFT_MAXJ
@@ -2125,11 +2147,13 @@ int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr) {
           HIPCHK(hipMalloc(&o.d_su, o.npts * 32));
           HIPCHK(hipMalloc(&o.d_bad, sizeof(int)));
         }
+        if (o.cmp_cells && !o.d_sci) HIPCHK(hipMalloc(&o.d_sci, o.npts * 4));
         const bool pal = F->fused && F->d_uidx && F->d_utab && F->dft_pal;
         HIPCHK(hipMemsetAsync(o.d_bad, 0, sizeof(int), F->stream));
         if (k_dft_plan(o.d_pj, o.d_pch, o.d_ch, (long long)o.npts, F->g, F->f,
                        pal ? F->d_uidx : nullptr, pal ? F->d_utab : nullptr, o.d_sidx, o.d_ssel,
-                       o.d_spal, o.d_su, o.d_bad, F->stream))
+                       o.d_spal, o.d_su, o.d_bad, o.bbox, o.cmp_cells ? o.d_sci : nullptr,
+                       F->stream))
           return fail("dft plan launch failed");
         int bad = 1;
         if (pal) {  // once per plan: are the palette bytes exact for every implicit value?
@@ -2144,6 +2168,16 @@ int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr) {
       jb.sidx = o.d_sidx, jb.ssel = o.d_ssel, jb.spal = o.d_spal, jb.su = o.d_su;
       jb.pw = o.d_pw, jb.fr = fr, jb.npts = (long long)o.npts, jb.blk0 = J.nblk;
       jb.usepal = o.usepal ? 1 : 0;
+      if (cstate >= 0 && o.cmp_on && o.d_cmp && o.d_sci) {
+        jb.sci = o.d_sci;
+        jb.cmp = o.d_cmp + (size_t)cstate * 6 * o.cmp_cells;
+        jb.ncell = o.cmp_cells;
+        const int n0 = o.bbox.hi[0] - o.bbox.lo[0] + 1, n1 = o.bbox.hi[1] - o.bbox.lo[1] + 1;
+        for (int e = 0; e < 3; e++) {
+          const int ax = F->g.ax[e];
+          jb.cs[e] = ax == 0 ? 1 : ax == 1 ? n0 : ax == 2 ? n0 * n1 : 0;
+        }
+      }
       J.nblk += ((long long)o.npts + 255) / 256;
     } else if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, fr, (long long)o.npts, F->g, fs,
                             F->stream)) {
@@ -3697,8 +3731,17 @@ int tb_plan(mnl_fields *F) {
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
   // the two-step items store step n+1 there too (the middle-step sample reads the mid set)
   std::vector<Box> dbox;
-  for (auto &op : F->dfts)  // (built once per monitor: this runs every batch)
-    if (op->bbox.hi[0] >= 0) dbox.push_back(op->bbox);
+  std::vector<DftFluxH *> cmon;  // monitors whose box the two-step kernel stores compactly
+  for (auto &op : F->dfts) {  // (built once per monitor: this runs every batch)
+    if (op->bbox.hi[0] < 0) continue;
+    if (F->dft_cmp && op->cmp_cells && (int)cmon.size() < TB_MAXCMP)
+      cmon.push_back(op.get());
+    else
+      dbox.push_back(op->bbox);
+  }
+  mix((long long)cmon.size());
+  for (auto *o : cmon)
+    for (int k = 0; k < 3; k++) mix(o->bbox.lo[k]), mix(o->bbox.hi[k]);
   // the NaN guard's points (it checks the middle state of every pair, src/step.cpp:138-139)
   if (F->nan_terms.n > 0) {
     Box nb;
@@ -3720,6 +3763,27 @@ int tb_plan(mnl_fields *F) {
   F->tb_sig = sig;
   F->tb_have = false;
   F->tb_ritems.clear(), F->tb_rgeo.clear(), F->tb_items.clear();
+  // compact DFT boxes: allocated once, emptied (DFT_CMP_EMPTY) with every new plan
+  F->tb_cmp.clear();
+  for (auto &op : F->dfts) op->cmp_on = false;
+  for (auto *o : cmon) {
+    const size_t nd = (size_t)12 * o->cmp_cells;
+    if (!o->d_cmp && hipMalloc(&o->d_cmp, nd * 8) != hipSuccess) {
+      (void)hipGetLastError();
+      o->d_cmp = nullptr;
+      dbox.push_back(o->bbox);  // no memory for it: the middle state in mid, as before
+      continue;
+    }
+    double empty;
+    const unsigned long long e = DFT_CMP_EMPTY;
+    memcpy(&empty, &e, 8);
+    if (k_fill(o->d_cmp, empty, nd, F->stream)) return fail("fill launch failed");
+    TBCmp c{};
+    for (int k = 0; k < 3; k++) c.lo[k] = o->bbox.lo[k], c.n[k] = o->bbox.hi[k] - o->bbox.lo[k] + 1;
+    c.p = o->d_cmp, c.mask = o->cmp_mask, c.ncell = o->cmp_cells;
+    F->tb_cmp.push_back(c);
+    o->cmp_on = true;
+  }
   const Box &G = F->fusedG, &L = F->fusedL;
   const FusedArgs &a = F->fgeo;
   const DevGrid &g = F->g;
@@ -4010,9 +4074,28 @@ int tb_plan(mnl_fields *F) {
           it.faces = faces;
           it.bx = it.by = it.bz = -1, it.lx = lx;
           {
+            // the first compact DFT box the own points meet goes to the kernel's compact
+            // stores; other compact boxes the item meets take the middle-set stores below
+            std::vector<Box> ibox = dbox;
+            int cm = -1;
+            for (size_t m = 0; m < F->tb_cmp.size(); m++) {
+              const TBCmp &c = F->tb_cmp[m];
+              bool meet = true;
+              Box cb;
+              for (int k = 0; k < 3; k++) {
+                cb.lo[k] = c.lo[k], cb.hi[k] = c.lo[k] + c.n[k] - 1;
+                meet = meet && std::max(o.lo[k], cb.lo[k]) <= std::min(o.hi[k], cb.hi[k]);
+              }
+              if (!meet) continue;
+              if (cm < 0)
+                cm = (int)m;
+              else
+                ibox.push_back(cb);
+            }
+            if (cm >= 0) it.faces |= (cm + 1) << 8;
             Box u;  // bounding box of the item's intersections with the DFT boxes
             bool any = false;
-            for (const Box &db : dbox) {
+            for (const Box &db : ibox) {
               Box x;
               bool ok = true;
               for (int k = 0; k < 3; k++) {
@@ -4233,6 +4316,8 @@ TB2Args tb_args(mnl_fields *F, const Set5 &o, const Set5 &m, const Set5 &n) {
   t.ctr = F->d_fused_ctr;
   t.ctr_line = 3;
   t.clk = ItemClock{F->d_clk, F->d_clk_n, F->d_clk ? CLK_CAP : 0u, 2};
+  t.ncmp = (int)F->tb_cmp.size();
+  for (int i = 0; i < t.ncmp; i++) t.cmp[i] = F->tb_cmp[i];
   return t;
 }
 
@@ -4312,7 +4397,7 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
     for (int d = 0; d < 3; d++)
       fm.B[d] = mid.B[d], fm.D[d] = mid.D[d], fm.E[d] = mid.E[d], fm.H[d] = mid.H[d];
     k = ev_begin(TM_DFT);
-    const int r = dft_update(F, t_mid, &fm);
+    const int r = dft_update(F, t_mid, &fm, 0);
     ev_end(k);
     if (r) return -1;
   }
@@ -4540,7 +4625,7 @@ int step_batch(mnl_fields *F, int nsteps) {
   };
   // fields::update_dfts after t += 1 (src/step.cpp:125-127); a rank's averages
   // read its low ghost planes, which must hold this step's values first
-  auto post_step = [&](int s) -> int {
+  auto post_step = [&](int s, int cstate = -1) -> int {
     const long long tn = F->t + s + 1;
     if (!dft_due(F, tn)) return 0;
     if (F->nranks > 1) {
@@ -4551,7 +4636,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       if (exchange(F, 3)) return fail("DFT halo exchange failed");
     }
     const int k = ev_begin(TM_DFT);
-    const int r = dft_update(F, tn);
+    const int r = dft_update(F, tn, nullptr, cstate);
     ev_end(k);
     return r;
   };
@@ -4608,7 +4693,7 @@ int step_batch(mnl_fields *F, int nsteps) {
                            : tb_pair(F, sD, sD1, ev_begin, ev_end, F->t + s + 1)))
           return -1;
         s++;
-        if (post_step(s)) return -1;  // DFT of the pair's second step (the new state)
+        if (post_step(s, 1)) return -1;  // DFT of the pair's second step (the new state)
         continue;
       }
       if (tb_chain_join(F)) return -1;
@@ -6085,6 +6170,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
+  if (const char *dc = getenv("MNL_DFT_CMP")) F->dft_cmp = atoi(dc) != 0;
   if (const char *tr = getenv("MNL_TB_RES")) F->tb_res = std::max(0, atoi(tr));
   if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
@@ -7213,6 +7299,8 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     if (value < -1 || value > 1024) return fail("bad reservation");
     (which == 2 ? F->tb_res : which == 3 ? F->res_l : F->res_r) = value;
     return 0;
+  } else if (which == 5) {
+    F->dft_cmp = v;
   } else if (which == 1) {
     F->dft_pal = v;
     for (auto &o : F->dfts) o->plan_key = -1;  // plans rebuilt at the next update

@@ -355,13 +355,28 @@ struct TB2Item {
   int y;      // y0 | y1 << 16 (own rows, inclusive)
   int z;      // zs | ze << 16 (own planes [zs, ze))
   int faces;  // bits 0..5: own face x-lo, x-hi, y-lo, y-hi, z-lo, z-hi borders the rim (its
-              // points' step n+1 values are stored into the middle buffer set)
+              // points' step n+1 values are stored into the middle buffer set); bits 8..10:
+              // 1 + the compact DFT box (TB2Args::cmp) the item's own points meet, 0 none
   // a box of own points whose step n+1 values are also stored into the middle set (the DFT
   // monitors sample step n+1 there): x0 | x1 << 16, y0 | y1 << 16, z0 | z1 << 16 (inclusive);
   // bx < 0: none
   int bx, by, bz;
   int lx;     // column of lane 0 (a multiple of 8: 64-byte line)
 };
+// A DFT monitor's compact box: the two-step kernel stores the D and B
+// of its own points inside the box, for the middle (state 0) and the new (state 1) step of a
+// pair, at p[((state * 6 + a) * ncell + i)] (a = D0..D2, B0..B2 where mask bit a is set;
+// i = x + n0 * (y + n1 * z) relative to lo), so the pair's DFT samples read them densely.
+constexpr int TB_MAXCMP = 4;
+struct TBCmp {
+  int lo[3], n[3];
+  double *p;
+  unsigned mask;   // arrays stored
+  unsigned ncell;  // n0 * n1 * n2 (ncell * 96 bytes < 4 GiB)
+};
+// Entries no two-step point wrote (rim points, or before the first pair of a plan): this
+// signalling-NaN bit pattern, which no arithmetic produces
+constexpr unsigned long long DFT_CMP_EMPTY = 0x7FF4D5F7A3E1C9B1ULL;
 struct TB2Args {
   int n;                  // items
   const TB2Item *items;
@@ -381,6 +396,8 @@ struct TB2Args {
   int wg_limit;                 // > 0: at most this many persistent workgroups (CUs left to
                                 // the slab-face kernels of multi-rank pairs)
   ItemClock clk;                // diagnostics: per-item start / end times (clk.rec null: off)
+  int ncmp;                     // DFT compact boxes
+  TBCmp cmp[TB_MAXCMP];
 };
 // NaN guard of fields::step (src/step.cpp:138-139): get_field(D_EnergyDensity, gv.center())
 // = 1/2 sum_d E_d(c) D_d(c), each value the interpolation of src/monitor.cpp:127-160 over
@@ -440,7 +457,8 @@ int k_dft_sample(const int *pj, const double *pw, const int *pch, const DftChunk
 // dft_plan_kernel), then the sample of one update of every flux object due (one launch)
 int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
                const DevGrid &g, const DevFields &f, const unsigned *uidx, const double *utab,
-               int *sidx, unsigned short *ssel, unsigned *spal, void *su, int *bad, void *stream);
+               int *sidx, unsigned short *ssel, unsigned *spal, void *su, int *bad,
+               const Box &cbox, int *sci, void *stream);
 constexpr int DFT_MAXJ = 8;  // flux objects per sample launch
 struct DftSampleJob {
   const int *sidx;
@@ -452,6 +470,10 @@ struct DftSampleJob {
   long long npts;
   long long blk0;   // first workgroup of the job
   int usepal;       // chi1inv from the palette bytes (else the doubles)
+  const int *sci;   // compact box index of the first value (-1: some value outside the box)
+  const double *cmp;  // the compact box's state of this update (null: none)
+  unsigned ncell;
+  int cs[3];        // compact strides per direction
 };
 struct DftSampleJobs {
   DftSampleJob j[DFT_MAXJ];

@@ -3959,6 +3959,34 @@ int k_tile_items_uniform(const FusedArgs &a, const int *items, const int *geo, i
 // step n+1 reads).  The arithmetic of each update is the lean body's expression, operand
 // for operand (src/step_generic.cpp:106-113 curl, 888-903 E = chi1inv * D), so two steps
 // here are bitwise two one-step launches.
+// the compact DFT box of an item (TB2Item::faces bits 8..10), read once per item
+struct TB2Cmp {
+  int lo0, lo1, lo2, n0, n1, n2;
+  unsigned long long p;
+  unsigned mask, ncell;
+};
+typedef const TB2Args __attribute__((address_space(4))) KTB;
+__device__ __forceinline__ TB2Cmp tb2_cmp_of(int m) {
+  KTB *kt = (KTB *)__builtin_amdgcn_kernarg_segment_ptr();
+  const auto &c = kt->cmp[m];
+  return TB2Cmp{c.lo[0], c.lo[1], c.lo[2], c.n[0], c.n[1], c.n[2],
+                (unsigned long long)c.p, c.mask, c.ncell};
+}
+// the D, B of this lane's own point at plane kk into the item's compact DFT box
+__device__ __forceinline__ void tb2_cmp_store(const TB2Cmp &c, int state, bool own, int gx,
+                                              int gy, int kk, double d0, double d1, double d2,
+                                              double b0, double b1, double b2) {
+  const int cx = gx - c.lo0, cy = gy - c.lo1, cz = kk - c.lo2;
+  const bool in = own && cx >= 0 && cx < c.n0 && cy >= 0 && cy < c.n1 && cz >= 0 && cz < c.n2;
+  const unsigned ci = (unsigned)(cx + c.n0 * (cy + c.n1 * cz));
+  const unsigned st = (unsigned)state * 6u;
+  const auto r = brsrc_at(c.p, c.ncell * 96u);
+  const double v[6] = {d0, d1, d2, b0, b1, b2};
+#pragma unroll
+  for (int q = 0; q < 6; q++)
+    if ((c.mask >> q) & 1u) bst(r, in ? ((st + q) * c.ncell + ci) * 8u : MNL_OOB, v[q]);
+}
+
 template <int UMODE, bool UNI>
 __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, unsigned uw,
                                          const double (*sU)[256], double (*sE1)[TB_LY][TB_LX],
@@ -3969,6 +3997,9 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
   const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
   const int zs = it.z & 0xFFFF, ze = it.z >> 16;
   const int faces = it.faces;
+  const int cmi = ((faces >> 8) & 7) - 1;  // the item's compact DFT box (-1: none)
+  TB2Cmp cmb{};
+  if (cmi >= 0) cmb = tb2_cmp_of(cmi);
   const int gx = it.lx + lane, gy = y0 - TB_HY + w;  // lanes from the item's 64-byte line
   const int N0 = a.N[0], N1 = a.N[1], zmax = a.N[2] - 1;
   const int cx = min(max(gx, 0), N0 - 1), cy = min(max(gy, 0), N1 - 1);
@@ -4104,6 +4135,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
       bst(brsrc_at(pDm0, nrec), ob, Dx);
       bst(brsrc_at(pDm1, nrec), ob, Dy);
       bst(brsrc_at(pDm2, nrec), ob, Dz);
+      if (cmi >= 0) tb2_cmp_store(cmb, 0, own && kin, gx, gy, k, Dx, Dy, Dz, Bx, By, Bz);
     }
     // ---- step n+1 at plane k-1: B^{n+2}(k-1) from E^{n+1}(k-1) (sE2), E^{n+1}(k) (Ex..)
     const double Fx = b1x - C * (sE2[2][wp][lane] - f1z + f1y - Ey);
@@ -4123,6 +4155,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
       bst(brsrc_at(pDn0, nrec), os, Gx);
       bst(brsrc_at(pDn1, nrec), os, Gy);
       bst(brsrc_at(pDn2, nrec), os, Gz);
+      if (cmi >= 0) tb2_cmp_store(cmb, 1, st, gx, gy, k - 1, Gx, Gy, Gz, Fx, Fy, Fz);
     }
     h2x = Fx, h2y = Fy;
     h1x = Bx, h1y = By;
@@ -4152,7 +4185,7 @@ __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
       if (CLK && s_t0 != 0ull) {  // diagnostics: the previous item (see fused_tile_kernel)
         const TB2Item it = a.items[s_idx];
         const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[s_idx] : ~0u;
-        clk_record(a.clk, s_t0, it.faces | (uw != ~0u ? 64 : 0), it.x, it.y, it.z, -1);
+        clk_record(a.clk, s_t0, (it.faces & 63) | (uw != ~0u ? 64 : 0), it.x, it.y, it.z, -1);
       }
       const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
       s_idx = v < (unsigned long long)(a.n) ? (int)v : -1;
@@ -4365,7 +4398,8 @@ __global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restric
                                 DevFields f, const unsigned *__restrict__ uidx,
                                 const double *__restrict__ utab, int *__restrict__ sidx,
                                 unsigned short *__restrict__ ssel, unsigned *__restrict__ spal,
-                                double4 *__restrict__ su, int *__restrict__ bad) {
+                                double4 *__restrict__ su, int *__restrict__ bad, Box cb,
+                                int *__restrict__ sci) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npts) return;
   if (pj[3 * p] < 0) {
@@ -4373,6 +4407,7 @@ __global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restric
     sidx[p] = 0;
     spal[p] = 0;
     su[p] = make_double4(1.0, 1.0, 1.0, 1.0);
+    if (sci) sci[p] = -1;
     return;
   }
   const DftChunkDev cd = ch[pch[p]];
@@ -4425,6 +4460,18 @@ __global__ void dft_plan_kernel(const int *__restrict__ pj, const int *__restric
     }
   }
   if (mism) atomicOr(bad, 1);
+  if (sci) {  // compact-box index of the first value if every value lies in the box
+    int c[3], n[3];
+    bool in = true;
+    for (int e = 0; e < 3; e++) {
+      const int ax = g.ax[e] >= 0 ? g.ax[e] : e;
+      c[ax] = P.j[e] - cb.lo[ax];
+      const int top = c[ax] + ((nv > 1 && cd.d1 == e) || (nv > 2 && cd.d2 == e) ? 1 : 0);
+      n[ax] = cb.hi[ax] - cb.lo[ax] + 1;
+      in = in && g.ax[e] >= 0 && c[ax] >= 0 && top < n[ax];
+    }
+    sci[p] = in ? c[0] + n[0] * (c[1] + n[1] * c[2]) : -1;
+  }
   ssel[p] = (unsigned short)sel;
   sidx[p] = (int)P.idx;
   spal[p] = pal;
@@ -4482,15 +4529,29 @@ __global__ void __launch_bounds__(256) dft_sample_jobs_kernel(DftSampleJobs J, D
       u[0] = uu.x, u[1] = uu.y, u[2] = uu.z, u[3] = uu.w;
     }
   }
-  const double v0 = dft_val(s, d, (sel >> 4) & 3, (int)i0, u[0]);
+  // values of two-step points from the compact box of this state (dense), the others (and
+  // entries no two-step point wrote) from the field arrays
+  const int ci = jb.cmp ? jb.sci[p] : -1;
+  const int c1 = d1 == 0 ? jb.cs[0] : (d1 == 1 ? jb.cs[1] : jb.cs[2]);
+  const int c2 = d2 == 0 ? jb.cs[0] : (d2 == 1 ? jb.cs[1] : jb.cs[2]);
+  auto val = [&](int v, long long li, int cix) -> double {
+    const unsigned k = (sel >> (4 + 2 * v)) & 3;
+    if (ci >= 0 && (k == 1 || k == 2)) {
+      const double c = jb.cmp[(size_t)((k == 1 ? d : 3 + d) * jb.ncell) + cix];
+      if ((unsigned long long)__double_as_longlong(c) != DFT_CMP_EMPTY)
+        return k == 1 ? c * u[v] : c;
+    }
+    return dft_val(s, d, k, (int)li, u[v]);
+  };
+  const double v0 = val(0, i0, ci);
   double fr;
   if (mode == 2) {
-    const double v1 = dft_val(s, d, (sel >> 6) & 3, (int)(i0 + s1), u[1]);
-    const double v2 = dft_val(s, d, (sel >> 8) & 3, (int)(i0 + s2), u[2]);
-    const double v3 = dft_val(s, d, (sel >> 10) & 3, (int)(i0 + s1 + s2), u[3]);
+    const double v1 = val(1, i0 + s1, ci + c1);
+    const double v2 = val(2, i0 + s2, ci + c2);
+    const double v3 = val(3, i0 + s1 + s2, ci + c1 + c2);
     fr = w * (v0 + v1 + v2 + v3);
   } else if (mode == 1) {
-    fr = w * (v0 + dft_val(s, d, (sel >> 6) & 3, (int)(i0 + s1), u[1]));
+    fr = w * (v0 + val(1, i0 + s1, ci + c1));
   } else {
     fr = w * v0;
   }
@@ -4499,10 +4560,11 @@ __global__ void __launch_bounds__(256) dft_sample_jobs_kernel(DftSampleJobs J, D
 
 int k_dft_plan(const int *pj, const int *pch, const DftChunkDev *ch, long long npts,
                const DevGrid &g, const DevFields &f, const unsigned *uidx, const double *utab,
-               int *sidx, unsigned short *ssel, unsigned *spal, void *su, int *bad, void *stream) {
+               int *sidx, unsigned short *ssel, unsigned *spal, void *su, int *bad,
+               const Box &cbox, int *sci, void *stream) {
   if (npts <= 0) return 0;
   dft_plan_kernel<<<(unsigned)((npts + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      pj, pch, ch, npts, g, f, uidx, utab, sidx, ssel, spal, (double4 *)su, bad);
+      pj, pch, ch, npts, g, f, uidx, utab, sidx, ssel, spal, (double4 *)su, bad, cbox, sci);
   return rc();
 }
 

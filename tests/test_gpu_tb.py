@@ -176,6 +176,31 @@ def test_tb_dft_flux():
     _same_dft(p, o, hs)
 
 
+def test_tb_dft_compact_fallbacks(monkeypatch):
+    """The pairs' samples of two-step points come from the monitors' compact boxes (DESIGN.md
+    section 10); the paths around them stay bitwise the oracle: compact boxes switched off
+    (MNL_DFT_CMP=0: the middle state in the mid set), and a fifth monitor beyond the four
+    compact boxes, added half-way (its middle state in the mid set, the others compact)."""
+    from scenarios import FLUX3D_FREQS, sc_flux_3d
+    from test_gpu_dft import _same_dft
+    kw = dict(sizes=[9.6, 6.4, 8.0], steps=24)
+    o, hs = sc_flux_3d(make_oracle, **kw)
+    monkeypatch.setenv("MNL_DFT_CMP", "0")
+    p, _ = sc_flux_3d(ProductSim, **kw)
+    monkeypatch.delenv("MNL_DFT_CMP")
+    assert p._fields().tb_info()["active"]
+    _same_dft(p, o, hs)
+
+    def fifth(sim):
+        hy, hz = 0.5 * kw["sizes"][1], 0.5 * kw["sizes"][2]
+        sim.add_dft_flux([([-0.9, -hy, -hz], [-0.9, hy, hz], 0, 1.0)], FLUX3D_FREQS, 1)
+
+    o5, hs5 = sc_flux_3d(make_oracle, extra=fifth, **kw)
+    p5, _ = sc_flux_3d(ProductSim, extra=fifth, **kw)
+    assert p5._fields().tb_info()["active"]
+    _same_dft(p5, o5, hs5 + [len(hs5)])
+
+
 def test_tb_dft_fields():
     """DFT field monitors (whole-cell components, boxes across PML chunks, planes, lines)
     with pairs of steps: bitwise the oracle."""
