@@ -3948,6 +3948,37 @@ int k_tile_items_uniform(const FusedArgs &a, const int *items, const int *geo, i
 }
 
 // ---------------------------------------------------------------------------
+// the compact DFT box of an item (TB2Item::faces bits 8..10)
+struct TB2Cmp {
+  int lo0, lo1, lo2, n0, n1, n2;
+  unsigned long long p;
+  unsigned mask, ncell;
+};
+typedef const TB2Args __attribute__((address_space(4))) KTB;
+// the D, B of this lane's own point at plane kk into the item's compact DFT box m (a wave with
+// no lane in the box issues no store).  The box's parameters are read from the kernel
+// arguments at each call through an opaque pointer, so they are not hoisted out of the plane
+// loop into SGPRs (which are full there: held across the loop they spill and reload per plane)
+__device__ __forceinline__ void tb2_cmp_store(int m, int state, bool own, int gx, int gy, int kk,
+                                              double d0, double d1, double d2, double b0,
+                                              double b1, double b2) {
+  KTB *kt = (KTB *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kt));
+  const auto &cc = kt->cmp[m];
+  const TB2Cmp c{cc.lo[0], cc.lo[1], cc.lo[2], cc.n[0], cc.n[1], cc.n[2],
+                 (unsigned long long)cc.p, cc.mask, cc.ncell};
+  const int cx = gx - c.lo0, cy = gy - c.lo1, cz = kk - c.lo2;
+  const bool in = own && cx >= 0 && cx < c.n0 && cy >= 0 && cy < c.n1 && cz >= 0 && cz < c.n2;
+  if (__builtin_amdgcn_ballot_w64(in) == 0) return;
+  const unsigned ci = (unsigned)(cx + c.n0 * (cy + c.n1 * cz));
+  const unsigned st = (unsigned)state * 6u;
+  const auto r = brsrc_at(c.p, c.ncell * 96u);
+  const double v[6] = {d0, d1, d2, b0, b1, b2};
+#pragma unroll
+  for (int q = 0; q < 6; q++)
+    if ((c.mask >> q) & 1u) bst(r, in ? ((st + q) * c.ncell + ci) * 8u : MNL_OOB, v[q]);
+}
+
 // Temporal blocking: steps n -> n+1 -> n+2 in one z-march over an
 // item of the region L2, where every point within L-infinity distance 2 of an own point is
 // lean (no PML, every component owned, H == B, E implicit) and no source point lies within
@@ -3959,35 +3990,7 @@ int k_tile_items_uniform(const FusedArgs &a, const int *items, const int *geo, i
 // step n+1 reads).  The arithmetic of each update is the lean body's expression, operand
 // for operand (src/step_generic.cpp:106-113 curl, 888-903 E = chi1inv * D), so two steps
 // here are bitwise two one-step launches.
-// the compact DFT box of an item (TB2Item::faces bits 8..10), read once per item
-struct TB2Cmp {
-  int lo0, lo1, lo2, n0, n1, n2;
-  unsigned long long p;
-  unsigned mask, ncell;
-};
-typedef const TB2Args __attribute__((address_space(4))) KTB;
-__device__ __forceinline__ TB2Cmp tb2_cmp_of(int m) {
-  KTB *kt = (KTB *)__builtin_amdgcn_kernarg_segment_ptr();
-  const auto &c = kt->cmp[m];
-  return TB2Cmp{c.lo[0], c.lo[1], c.lo[2], c.n[0], c.n[1], c.n[2],
-                (unsigned long long)c.p, c.mask, c.ncell};
-}
-// the D, B of this lane's own point at plane kk into the item's compact DFT box
-__device__ __forceinline__ void tb2_cmp_store(const TB2Cmp &c, int state, bool own, int gx,
-                                              int gy, int kk, double d0, double d1, double d2,
-                                              double b0, double b1, double b2) {
-  const int cx = gx - c.lo0, cy = gy - c.lo1, cz = kk - c.lo2;
-  const bool in = own && cx >= 0 && cx < c.n0 && cy >= 0 && cy < c.n1 && cz >= 0 && cz < c.n2;
-  const unsigned ci = (unsigned)(cx + c.n0 * (cy + c.n1 * cz));
-  const unsigned st = (unsigned)state * 6u;
-  const auto r = brsrc_at(c.p, c.ncell * 96u);
-  const double v[6] = {d0, d1, d2, b0, b1, b2};
-#pragma unroll
-  for (int q = 0; q < 6; q++)
-    if ((c.mask >> q) & 1u) bst(r, in ? ((st + q) * c.ncell + ci) * 8u : MNL_OOB, v[q]);
-}
-
-template <int UMODE, bool UNI>
+template <int UMODE, bool UNI, bool CMP>
 __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, unsigned uw,
                                          const double (*sU)[256], double (*sE1)[TB_LY][TB_LX],
                                          double (*sH1)[TB_LY][TB_LX], double (*sE2)[TB_LY][TB_LX],
@@ -3997,9 +4000,8 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
   const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
   const int zs = it.z & 0xFFFF, ze = it.z >> 16;
   const int faces = it.faces;
-  const int cmi = ((faces >> 8) & 7) - 1;  // the item's compact DFT box (-1: none)
-  TB2Cmp cmb{};
-  if (cmi >= 0) cmb = tb2_cmp_of(cmi);
+  // the item's compact DFT box (-1: none; CMP = false: no box in this launch, none compiled)
+  const int cmi = CMP ? ((faces >> 8) & 7) - 1 : -1;
   const int gx = it.lx + lane, gy = y0 - TB_HY + w;  // lanes from the item's 64-byte line
   const int N0 = a.N[0], N1 = a.N[1], zmax = a.N[2] - 1;
   const int cx = min(max(gx, 0), N0 - 1), cy = min(max(gy, 0), N1 - 1);
@@ -4135,7 +4137,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
       bst(brsrc_at(pDm0, nrec), ob, Dx);
       bst(brsrc_at(pDm1, nrec), ob, Dy);
       bst(brsrc_at(pDm2, nrec), ob, Dz);
-      if (cmi >= 0) tb2_cmp_store(cmb, 0, own && kin, gx, gy, k, Dx, Dy, Dz, Bx, By, Bz);
+      if (CMP && cmi >= 0) tb2_cmp_store(cmi, 0, own && kin, gx, gy, k, Dx, Dy, Dz, Bx, By, Bz);
     }
     // ---- step n+1 at plane k-1: B^{n+2}(k-1) from E^{n+1}(k-1) (sE2), E^{n+1}(k) (Ex..)
     const double Fx = b1x - C * (sE2[2][wp][lane] - f1z + f1y - Ey);
@@ -4155,7 +4157,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
       bst(brsrc_at(pDn0, nrec), os, Gx);
       bst(brsrc_at(pDn1, nrec), os, Gy);
       bst(brsrc_at(pDn2, nrec), os, Gz);
-      if (cmi >= 0) tb2_cmp_store(cmb, 1, st, gx, gy, k - 1, Gx, Gy, Gz, Fx, Fy, Fz);
+      if (CMP && cmi >= 0) tb2_cmp_store(cmi, 1, st, gx, gy, k - 1, Gx, Gy, Gz, Fx, Fy, Fz);
     }
     h2x = Fx, h2y = Fy;
     h1x = Bx, h1y = By;
@@ -4168,7 +4170,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
   }
 }
 
-template <int UMODE, bool CLK>
+template <int UMODE, bool CLK, bool CMP>
 __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
   __shared__ double sE1[3][TB_LY][TB_LX], sH1[3][TB_LY][TB_LX];
@@ -4197,9 +4199,9 @@ __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
     const TB2Item it = a.items[idx];
     const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[idx] : ~0u;
     if (UMODE == 2 && __builtin_amdgcn_readfirstlane(uw) != ~0u)
-      tb2_body<UMODE, true>(a, it, uw, sU, sE1, sH1, sE2, sH2);
+      tb2_body<UMODE, true, CMP>(a, it, uw, sU, sE1, sH1, sE2, sH2);
     else
-      tb2_body<UMODE, false>(a, it, uw, sU, sE1, sH1, sE2, sH2);
+      tb2_body<UMODE, false, CMP>(a, it, uw, sU, sE1, sH1, sE2, sH2);
   }
 }
 
@@ -4244,19 +4246,28 @@ int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
   const int um = a.uidx ? 2 : (a.u[0] ? 1 : 0);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grd((unsigned)nb), blk(1024);
-  if (t.clk.rec) {  // diagnostics build of the kernel (MNL_ITEM_CLOCK)
+  // compact DFT boxes (t.ncmp > 0): the variant with their stores; the diagnostics build
+  // (MNL_ITEM_CLOCK) always has them
+  if (t.clk.rec) {
     if (um == 2)
-      tb2_kernel<2, true><<<grd, blk, 0, s>>>(t);
+      tb2_kernel<2, true, true><<<grd, blk, 0, s>>>(t);
     else if (um == 1)
-      tb2_kernel<1, true><<<grd, blk, 0, s>>>(t);
+      tb2_kernel<1, true, true><<<grd, blk, 0, s>>>(t);
     else
-      tb2_kernel<0, true><<<grd, blk, 0, s>>>(t);
+      tb2_kernel<0, true, true><<<grd, blk, 0, s>>>(t);
+  } else if (t.ncmp > 0) {
+    if (um == 2)
+      tb2_kernel<2, false, true><<<grd, blk, 0, s>>>(t);
+    else if (um == 1)
+      tb2_kernel<1, false, true><<<grd, blk, 0, s>>>(t);
+    else
+      tb2_kernel<0, false, true><<<grd, blk, 0, s>>>(t);
   } else if (um == 2) {
-    tb2_kernel<2, false><<<grd, blk, 0, s>>>(t);
+    tb2_kernel<2, false, false><<<grd, blk, 0, s>>>(t);
   } else if (um == 1) {
-    tb2_kernel<1, false><<<grd, blk, 0, s>>>(t);
+    tb2_kernel<1, false, false><<<grd, blk, 0, s>>>(t);
   } else {
-    tb2_kernel<0, false><<<grd, blk, 0, s>>>(t);
+    tb2_kernel<0, false, false><<<grd, blk, 0, s>>>(t);
   }
   return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
@@ -4508,19 +4519,24 @@ __global__ void __launch_bounds__(256) dft_sample_jobs_kernel(DftSampleJobs J, D
   const auto &jb = jt->j[ji];
   const long long p = (lb - jb.blk0) * 256 + threadIdx.x;
   if (p >= jb.npts) return;
+  // the point's plan entries, loaded together (one round trip), then the values: compact-box
+  // entries first (all in flight together), field-array loads only for the values the box
+  // does not hold
   const unsigned sel = jb.ssel[p];
-  if (sel == 0xFFFFu) return;  // another rank's point
   const long long i0 = jb.sidx[p];
   const double w = jb.pw[p];
+  const int ci = jb.cmp ? jb.sci[p] : -1;
+  const unsigned pal = jb.usepal ? jb.spal[p] : 0u;
+  if (sel == 0xFFFFu) return;  // another rank's point
   const int d = sel & 3, mode = (sel >> 2) & 3, d1 = (sel >> 12) & 3, d2 = (sel >> 14) & 3;
   const long long s1 = d1 == 0 ? J.sd[0] : (d1 == 1 ? J.sd[1] : J.sd[2]);
   const long long s2 = d2 == 0 ? J.sd[0] : (d2 == 1 ? J.sd[1] : J.sd[2]);
+  const int nv = mode == 2 ? 4 : (mode == 1 ? 2 : 1);
   // chi1inv only for implicit-E values (kind 1 in any slot)
   const bool any1 = ((sel >> 4) & 0x55u & ~((sel >> 5) & 0x55u)) != 0;
   double u[4] = {1.0, 1.0, 1.0, 1.0};
   if (any1) {
     if (jb.usepal) {
-      const unsigned pal = jb.spal[p];
 #pragma unroll
       for (int v = 0; v < 4; v++)
         if (((sel >> (4 + 2 * v)) & 3) == 1) u[v] = utab[d * 256 + ((pal >> (8 * v)) & 255u)];
@@ -4529,31 +4545,35 @@ __global__ void __launch_bounds__(256) dft_sample_jobs_kernel(DftSampleJobs J, D
       u[0] = uu.x, u[1] = uu.y, u[2] = uu.z, u[3] = uu.w;
     }
   }
-  // values of two-step points from the compact box of this state (dense), the others (and
-  // entries no two-step point wrote) from the field arrays
-  const int ci = jb.cmp ? jb.sci[p] : -1;
   const int c1 = d1 == 0 ? jb.cs[0] : (d1 == 1 ? jb.cs[1] : jb.cs[2]);
   const int c2 = d2 == 0 ? jb.cs[0] : (d2 == 1 ? jb.cs[1] : jb.cs[2]);
-  auto val = [&](int v, long long li, int cix) -> double {
+  const long long li[4] = {i0, i0 + s1, i0 + s2, i0 + s1 + s2};
+  const int cix[4] = {ci, ci + c1, ci + c2, ci + c1 + c2};
+  double val[4];
+  bool got[4];
+#pragma unroll
+  for (int v = 0; v < 4; v++) {  // two-step points from the compact box of this state (dense)
     const unsigned k = (sel >> (4 + 2 * v)) & 3;
-    if (ci >= 0 && (k == 1 || k == 2)) {
-      const double c = jb.cmp[(size_t)((k == 1 ? d : 3 + d) * jb.ncell) + cix];
-      if ((unsigned long long)__double_as_longlong(c) != DFT_CMP_EMPTY)
-        return k == 1 ? c * u[v] : c;
-    }
-    return dft_val(s, d, k, (int)li, u[v]);
-  };
-  const double v0 = val(0, i0, ci);
+    const bool use = v < nv && ci >= 0 && (k == 1 || k == 2);
+    val[v] = use ? jb.cmp[(size_t)((k == 1 ? d : 3 + d) * jb.ncell) + cix[v]] : 0.0;
+    got[v] = use;
+  }
+#pragma unroll
+  for (int v = 0; v < 4; v++) {  // the others (and entries no two-step point wrote)
+    const unsigned k = (sel >> (4 + 2 * v)) & 3;
+    if (v >= nv) continue;
+    if (got[v] && (unsigned long long)__double_as_longlong(val[v]) != DFT_CMP_EMPTY)
+      val[v] = k == 1 ? val[v] * u[v] : val[v];
+    else
+      val[v] = dft_val(s, d, k, (int)li[v], u[v]);
+  }
   double fr;
   if (mode == 2) {
-    const double v1 = val(1, i0 + s1, ci + c1);
-    const double v2 = val(2, i0 + s2, ci + c2);
-    const double v3 = val(3, i0 + s1 + s2, ci + c1 + c2);
-    fr = w * (v0 + v1 + v2 + v3);
+    fr = w * (val[0] + val[1] + val[2] + val[3]);
   } else if (mode == 1) {
-    fr = w * (v0 + val(1, i0 + s1, ci + c1));
+    fr = w * (val[0] + val[1]);
   } else {
-    fr = w * v0;
+    fr = w * val[0];
   }
   jb.fr[p] = fr;
 }
