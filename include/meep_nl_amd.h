@@ -379,7 +379,9 @@ int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
  * the next step), 1 DFT sampling plans with chi1inv as palette bytes (MNL_DFT_PAL; the plans
  * are rebuilt at the next update), 2 / 3 / 4 the CUs the pair launches / the two-step launch /
  * the rim launches leave free (value = a count, -1 the default; MNL_TB_RES), 5 pairs sample DFT
- * monitors from the two-step kernel's compact boxes (MNL_DFT_CMP; the pair plan is rebuilt).  For in-process A/B measurements
+ * monitors from the two-step kernel's compact boxes (MNL_DFT_CMP; the pair plan is rebuilt),
+ * 6 planes per rim item of a pair (value; 0 = the one-step chunk length), 7 the chi(2) NR box's
+ * E phase beside the tile kernel (MNL_NR_EARLY).  For in-process A/B measurements
  * (tools/ab_inproc.py). */
 int mnl_fields_set_schedule(mnl_fields *f, int which, int value);
 

@@ -367,6 +367,8 @@ struct mnl_fields {
   // L2 (two-step kernel) + rim, over three buffer sets
   bool tb_enabled = true;           // MNL_TB=0 at creation: never
   int tb_zchunk = 0;                // planes per two-step item (0: automatic)
+  int rim_zchunk = 0;               // planes per rim item of a pair (0: fused_zchunk)
+  bool nr_early = true;             // MNL_NR_EARLY=0: the NR box's E phase after both kernels
   unsigned fused_epoch = 0;         // bumped on every entry into the fused mode
   unsigned long long tb_sig = 0;    // inputs of the current plan (0: none)
   bool tb_have = false;             // the current plan has two-step items
@@ -3598,15 +3600,16 @@ constexpr int NR_HARD_CAP = 4096;  // deferred NR problems per E update (more: s
 
 // Before an E update that may run the NR branch: enable deferral (MNL_NR_DEFER=0 solves
 // every problem in place, sequentially) and clear the list; after it, the parallel pass.
-int nr_defer_begin(mnl_fields *F) {
+int nr_defer_begin(mnl_fields *F, hipStream_t st = nullptr) {
   if (!F->d_nr_hard) return 0;
   F->f.nr_hard = F->nr_defer ? F->d_nr_hard : nullptr;
-  if (F->f.nr_hard) HIPCHK(hipMemsetAsync(F->d_nr_hard_cnt, 0, sizeof(unsigned), F->stream));
+  if (F->f.nr_hard)
+    HIPCHK(hipMemsetAsync(F->d_nr_hard_cnt, 0, sizeof(unsigned), st ? st : F->stream));
   return 0;
 }
-int nr_defer_end(mnl_fields *F) {
+int nr_defer_end(mnl_fields *F, hipStream_t st = nullptr) {
   if (!F->f.nr_hard) return 0;
-  if (k_nr_hard(F->f, F->stream)) return fail("NR parallel-attempt kernel launch failed");
+  if (k_nr_hard(F->f, st ? st : F->stream)) return fail("NR parallel-attempt kernel launch failed");
   return 0;
 }
 
@@ -3615,15 +3618,32 @@ int nr_defer_end(mnl_fields *F) {
 // kernel (Newton-Raphson where chi2 != 0, chi1inv * (D - P) at the other points, the
 // values the fused kernels would have stored), then update_P over it, as the unfused
 // NR path orders them (src/step_generic.cpp:730-816, src/susceptibility.cpp:251-258)
-int nr_fused_e(mnl_fields *F, const ISrcDev &is) {
+int nr_fused_e(mnl_fields *F, const ISrcDev &is, hipStream_t st = nullptr) {
   const Box &x = F->nr_xbox;
   if (x.hi[0] < x.lo[0]) return 0;
-  if (nr_defer_begin(F)) return -1;
-  if (k_update_e(x, nullptr, F->g, F->f, is, 0, false, F->stream))
-    return fail("update E launch failed");
-  if (nr_defer_end(F)) return -1;
-  if (k_update_pols(x, nullptr, F->g, F->f, F->stream)) return fail("pols launch failed");
+  if (!st) st = F->stream;
+  if (nr_defer_begin(F, st)) return -1;
+  if (k_update_e(x, nullptr, F->g, F->f, is, 0, false, st)) return fail("update E launch failed");
+  if (nr_defer_end(F, st)) return -1;
+  if (k_update_pols(x, nullptr, F->g, F->f, st)) return fail("pols launch failed");
   return 0;
+}
+
+// The NR box's E phase may run right after the polarization chunks' general kernel, on its
+// stream beside the tile kernel (it reads the new D of the box and the old E, writes only the
+// box's new E / P -- points the tile kernel neither reads nor writes), when no D source point
+// lies in the box (sources are added to the new D after the fused kernels)
+bool nr_early_ok(const mnl_fields *F) {
+  const Box &x = F->nr_xbox;
+  if (!F->nr_early || x.hi[0] < x.lo[0]) return false;
+  for (long long idx : F->srcD_idx) {
+    const long long z = idx / F->g.st[2], r = idx % F->g.st[2];
+    const long long y = r / F->g.st[1], xx = r % F->g.st[1];
+    if (xx >= x.lo[0] && xx <= x.hi[0] && y >= x.lo[1] && y <= x.hi[1] && z >= x.lo[2] &&
+        z <= x.hi[2])
+      return false;
+  }
+  return true;
 }
 
 // ------------------------------------------------------------ temporal blocking
@@ -3726,6 +3746,7 @@ int tb_plan(mnl_fields *F) {
   unsigned long long sig = 1469598103934665603ULL;
   auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
   mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
+  mix(F->rim_zchunk);
   mix((long long)F->srcD_idx.size());
   for (long long v : F->srcD_idx) mix(v);
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
@@ -3837,7 +3858,9 @@ int tb_plan(mnl_fields *F) {
   if (two.empty() && F->nranks == 1) return 0;
   // ---- rim items: tile-kernel shapes (columns <= 64 from 128-byte boundaries, rows <= 14,
   // chunks <= zc cut at the lean box's z range), bodies as make_tile_boxes
-  const int zc = F->fused_zchunk > 0 ? std::min(F->fused_zchunk, FUSED_MAXCH) : 24;
+  // planes per rim item: its own setting (tuned with pairs), else the one-step chunk length
+  const int zc = F->rim_zchunk > 0 ? std::min(F->rim_zchunk, FUSED_MAXCH)
+                 : F->fused_zchunk > 0 ? std::min(F->fused_zchunk, FUSED_MAXCH) : 24;
   struct RI {
     int code, g0, g1, g2, g3, planes;
     bool dep;  // multi-rank: reads the ghost plane 0 or the top plane N-1 (slab-face data)
@@ -4713,6 +4736,7 @@ int step_batch(mnl_fields *F, int nsteps) {
       }
       const BoxList *sl = F->fused ? &F->fused_shell : &F->shell_list;
       int k = ev_begin(TM_BINT);
+      bool nr_done = false;  // the NR box's E phase already launched (beside the tile kernel)
       if (F->fused) {
         FusedArgs &fa = fused_args(F);
         const int split = F->tile_mode ? 0 : gen_split(F);
@@ -4751,6 +4775,12 @@ int step_batch(mnl_fields *F, int nsteps) {
           fa.wg_limit = ts;
           kr = k_fused(fa, 1, F->s_aux, F->ctr_base);
           if (kr) return fused_fail("fused general kernel launch failed", kr);
+          if (F->nr && F->nranks == 1 && nr_early_ok(F)) {
+            const int ke = ev_begin(TM_E, F->s_aux);
+            if (nr_fused_e(F, is, F->s_aux)) return -1;
+            ev_end(ke, F->s_aux);
+            nr_done = true;
+          }
           HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
           fa.wg_limit = k_cu_count() - ts;
           kr = k_fused(fa, 4, F->stream, F->ctr_base);
@@ -4819,9 +4849,11 @@ int step_batch(mnl_fields *F, int nsteps) {
       // ---- E (+ Lorentzian P)
       if (!F->e_first_done && e_lazy_copy(F)) return -1;
       if (F->fused && F->nr) {  // one rank: the fused kernels did all but the NR box
-        k = ev_begin(TM_E);
-        if (nr_fused_e(F, is)) return -1;
-        ev_end(k);
+        if (!nr_done) {
+          k = ev_begin(TM_E);
+          if (nr_fused_e(F, is)) return -1;
+          ev_end(k);
+        }
       } else {
         // neighbour reads of D - P (NR, upstream chi) or of W (anisotropic sigma):
         // P after all of E
@@ -6171,6 +6203,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
   if (const char *dc = getenv("MNL_DFT_CMP")) F->dft_cmp = atoi(dc) != 0;
+  if (const char *ne = getenv("MNL_NR_EARLY")) F->nr_early = atoi(ne) != 0;
   if (const char *tr = getenv("MNL_TB_RES")) F->tb_res = std::max(0, atoi(tr));
   if (const char *tp = getenv("MNL_TB_NOPAIR")) F->tb_nopair = atoi(tp) != 0;
   if (const char *bm = getenv("MNL_TILE_BODY_MASK")) F->tile_body_mask = atoi(bm);
@@ -7301,6 +7334,11 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     return 0;
   } else if (which == 5) {
     F->dft_cmp = v;
+  } else if (which == 7) {
+    F->nr_early = v;
+  } else if (which == 6) {  // planes per rim item (0: the one-step chunk length)
+    if (value < 0 || value > FUSED_MAXCH) return fail("bad rim chunk");
+    F->rim_zchunk = value;
   } else if (which == 1) {
     F->dft_pal = v;
     for (auto &o : F->dfts) o->plan_key = -1;  // plans rebuilt at the next update

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal", "res", "res_tb2", "res_rim", "dft_cmp"])
+    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal", "res", "res_tb2", "res_rim", "dft_cmp", "rim_zchunk", "nr_early"])
     ap.add_argument("--workload", default="waveguide")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=4)
@@ -33,26 +33,36 @@ def main():
     ap.add_argument("--flux", type=int, default=0,
                     help="N x-normal DFT flux planes as in bench.py --flux")
     ap.add_argument("--nfreq", type=int, default=50)
+    ap.add_argument("--fresh", action="store_true",
+                    help="new fields for every measurement (workloads whose cost grows with the "
+                         "fields, e.g. kerr_nr's Newton-Raphson fallbacks)")
     ap.add_argument("--json")
     a = ap.parse_args()
     import bench
     from meep_nl_amd import core
     core.set_verbosity(0)
-    gv, s, f = bench.build_fields(a.workload, a.size, 0, 1, 0, None)
-    if a.flux:  # the same monitors as bench.py --flux
-        hx, hy, hz = 0.5 * gv.n[0] / 10.0, 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
-        freqs = [0.1 + 0.1 * i / max(a.nfreq - 1, 1) for i in range(a.nfreq)]
-        for i in range(a.flux):
-            x = -hx + 2 * hx * (i + 1) / (a.flux + 1) + 0.05
-            f.add_dft_flux([([x, -hy, -hz], [x, hy, hz], 0, 1.0)], freqs, 1)
-    if a.tune:
-        f.tune()
-    f.step(6)
+    def build():
+        gv, s, f = bench.build_fields(a.workload, a.size, 0, 1, 0, None)
+        if a.flux:  # the same monitors as bench.py --flux
+            hx, hy, hz = 0.5 * gv.n[0] / 10.0, 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
+            freqs = [0.1 + 0.1 * i / max(a.nfreq - 1, 1) for i in range(a.nfreq)]
+            for i in range(a.flux):
+                x = -hx + 2 * hx * (i + 1) / (a.flux + 1) + 0.05
+                f.add_dft_flux([([x, -hy, -hz], [x, hy, hz], 0, 1.0)], freqs, 1)
+        if a.tune:
+            f.tune()
+        f.step(6)
+        return s, f
+
+    s, f = build()
     vals = [int(x) for x in a.values.split(",")]
     res = {v: [] for v in vals}
     for r in range(a.rounds):
         k = r % len(vals)
         for v in (vals[k:] + vals[:k]) if r % 2 == 0 else (vals[k:] + vals[:k])[::-1]:
+            if a.fresh:
+                del f, s
+                s, f = build()
             f.set_schedule(a.option, v)
             if a.retune:
                 f.tune()
