@@ -65,3 +65,33 @@ def test_nr_box_in_pml_stays_unfused():
     p.step(30)
     assert not p._fields().fused_active()
     _same(p, sc_c4_nr(make_oracle, steps=30, n=64))
+
+
+@pytest.mark.parametrize("early", ["1", "0"])
+def test_nr_fused_beside_tile_kernel(oracle96, monkeypatch, early):
+    """With the polarization chunks' general kernel on a CU split beside the tile kernel
+    (MNL_TILE_GEN_CUS), the NR box's E phase runs on the general kernel's stream right after
+    it (MNL_NR_EARLY=1, the default) or after both kernels (0): bitwise the oracle either way."""
+    monkeypatch.setenv("MNL_TILE_GEN_CUS", "64")
+    monkeypatch.setenv("MNL_NR_EARLY", early)
+    p = sc_c4_nr(ProductSim, steps=0, n=96)
+    p.step(40)
+    assert p._fields().fused_active() and p._fields().fused_concurrent()
+    _same(p, oracle96)
+
+
+def test_nr_source_in_box_with_split(monkeypatch):
+    """A D source inside the chi2 box (inside the polarization box, so the run leaves the fused
+    mode: E would need recomputing after the source; nr_early_ok checks the same case again)
+    with the CU split requested: bitwise the oracle."""
+    monkeypatch.setenv("MNL_TILE_GEN_CUS", "64")
+
+    def run(make):
+        o = sc_c4_nr(make, steps=0, n=96)
+        o.add_gaussian_source(1, 0.3, 5.0, 0.0, 50.0, (0.15, -0.25, 0.35), 20.0)
+        o.step(30)
+        return o
+
+    p = run(ProductSim)
+    assert not p._fields().fused_active()
+    _same(p, run(make_oracle))
