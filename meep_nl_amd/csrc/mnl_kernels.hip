@@ -4276,21 +4276,30 @@ int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
 // density at the cell centre in the host's order (get_field: res += w * value) and flags a
 // non-finite result; no host round trip (the host reads the flag once per batch).
 __global__ void nan_check_kernel(NanTerms t, Ptr3 E, Ptr3 D, Ptr3 U, int *flag, int step) {
+  // every term's value loaded by its own lane (one round trip), then summed by thread 0 in
+  // the host's order from LDS
+  __shared__ double sv[NAN_MAXT];
+  const int i0 = threadIdx.x;
+  if (i0 < t.n) {
+    const int d = t.dir[i0];
+    const long long k = t.idx[i0];
+    double v;
+    if (t.kind[i0] == 0)
+      v = E.p[d][k];
+    else if (t.kind[i0] == 1)
+      v = U.ci[d] ? D.p[d][k] * U.ci[d][k] : D.p[d][k];
+    else
+      v = D.p[d][k];
+    sv[i0] = v;
+  }
+  __syncthreads();
   if (threadIdx.x != 0) return;
   double sum = 0.0;
   int i = 0;
   for (int d = 0; d < 3; d++) {
     double e = 0.0, dd = 0.0;
-    for (; i < t.n && t.dir[i] == d && t.kind[i] != 2; i++) {
-      const long long k = t.idx[i];
-      double v;
-      if (t.kind[i] == 0)
-        v = E.p[d][k];
-      else
-        v = U.ci[d] ? D.p[d][k] * U.ci[d][k] : D.p[d][k];
-      e += t.w[i] * v;
-    }
-    for (; i < t.n && t.dir[i] == d && t.kind[i] == 2; i++) dd += t.w[i] * D.p[d][t.idx[i]];
+    for (; i < t.n && t.dir[i] == d && t.kind[i] != 2; i++) e += t.w[i] * sv[i];
+    for (; i < t.n && t.dir[i] == d && t.kind[i] == 2; i++) dd += t.w[i] * sv[i];
     sum += e * dd;
   }
   if (!isfinite(sum * 0.5) && atomicOr(flag, 1) == 0) flag[1] = step;
