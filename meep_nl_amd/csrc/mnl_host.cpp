@@ -9,528 +9,11 @@
 // component), the per-step launch sequence (src/step.cpp:35-140), point-source
 // weights (src/loop_in_chunks.cpp:263-500) and get_field interpolation
 // (src/vec.cpp:558-621, src/monitor.cpp:127-160).
-#include <hip/hip_runtime_api.h>
+#include "mnl_host.hpp"
 
-#include <algorithm>
-#include <array>
-#include <chrono>
-#include <cmath>
-#include <complex>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <memory>
-#include <set>
-#include <unordered_set>
-#include <string>
-#include <tuple>
-#include <unordered_map>
-#include <vector>
-
-#include "../../include/meep_nl_amd.h"
-#include "mnl_comm.hpp"
-#include "mnl_internal.hpp"
-
-using namespace mnl;
-typedef std::complex<double> cplx;
-
-namespace {
-constexpr int FX_HOST = 64;    // fused tile width (FX in mnl_kernels.hip)
-constexpr int FOWN_HOST = 14;  // own rows of a tile item (FOWN in mnl_kernels.hip)
-constexpr int TB_RES_CUS = 8;  // multi-rank: CUs left to the slab-face work (one per XCD)
-constexpr int SW_HOST = 16;     // narrow strip columns (SW_N in mnl_kernels.hip)
-constexpr int SOWN_HOST = 63;   // narrow strip own rows (SR_N - 1)
-constexpr int NAN_CH = 256;     // steps per chunk of a batch: the NaN flag is read after each
-
-const double pi = 3.141592653589793238462643383276;  // meep::pi
+namespace mnlh {
 thread_local std::string g_err;
-
-static int g_verbosity = 1;  // meep::verbosity (src/meep.hpp: default 1)
-
-int fail(const std::string &m) {
-  g_err = "meep: " + m;
-  return -1;
-}
-#define HIPCHK(x)                                                                 \
-  do {                                                                            \
-    hipError_t e_ = (x);                                                          \
-    if (e_ != hipSuccess)                                                         \
-      return fail(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x); \
-  } while (0)
-
-inline int cdir(int c) { return c % 3; }
-inline int ctype(int c) { return c / 3; }
-
-// ------------------------------------------------------------- source time
-// gaussian_src_time / continuous_src_time (src/sources.cpp:85-141,
-// src/meep.hpp:937-1056).
-struct SrcTime {
-  int kind = 0;
-  bool is_integrated = false;
-  double freq = 0, width = 0, peak_time = 0, cutoff = 0;
-  cplx cfreq;
-  double cwidth = 0, start_time = 0, end_time = 0, slowness = 3;
-  double cur_time = NAN;
-  cplx cur_dipole, cur_current;
-  mnl_src_func func = nullptr;  // kind 2: custom_src_time (src/meep.hpp:1059-1092)
-  void *fdata = nullptr;
-
-  cplx dipole(double time) const {
-    if (kind == 2) {
-      const float rtime = float(time);
-      if (!(rtime >= start_time && rtime <= end_time)) return 0.0;
-      double re = 0, im = 0;
-      func(time, fdata, &re, &im);
-      return cplx(re, im);
-    }
-    if (kind == 0) {
-      double tt = time - peak_time;
-      if (float(fabs(tt)) > cutoff) return 0.0;
-      cplx amp = 1.0 / cplx(0, -2 * pi * freq);
-      return exp(-tt * tt / (2 * width * width)) * std::polar(1.0, -2 * pi * freq * tt) * amp;
-    }
-    float rtime = float(time);
-    if (rtime < start_time || rtime > end_time) return 0.0;
-    cplx amp = 1.0 / (cplx(0, -1.0) * (2 * pi) * cfreq);
-    if (cwidth == 0.0) return exp(cplx(0, -1.0) * (2 * pi) * cfreq * time) * amp;
-    double ts = (time - start_time) / cwidth - slowness;
-    double te = (end_time - time) / cwidth - slowness;
-    return exp(cplx(0, -1.0) * (2 * pi) * cfreq * time) * amp * (1.0 + tanh(ts)) *
-           (1.0 + tanh(te)) * 0.25;
-  }
-  void update(double time, double dt) {  // src_time::update, src/meep.hpp:972-978
-    if (time != cur_time) {
-      cur_dipole = dipole(time);
-      // custom_src_time::current: the dipole itself unless integrated
-      cur_current = (kind == 2 && !is_integrated) ? dipole(time)
-                                                 : (dipole(time + dt) - dipole(time)) / dt;
-      cur_time = time;
-    }
-  }
-  bool same(const SrcTime &o) const {
-    return kind == o.kind && is_integrated == o.is_integrated && freq == o.freq &&
-           width == o.width && peak_time == o.peak_time && cutoff == o.cutoff &&
-           cfreq == o.cfreq && cwidth == o.cwidth && start_time == o.start_time &&
-           end_time == o.end_time && slowness == o.slowness && func == o.func && fdata == o.fdata;
-  }
-};
-
-struct SrcGroup {  // src_vol (src/meep_internals.hpp:49-82) over the whole cell
-  int comp;        // E or H component
-  int st;
-  std::vector<long long> gidx;  // global canonical index of comp
-  std::vector<int> jglob;       // 3 global indices per point
-  std::vector<cplx> amp;
-};
-
-struct Lorentz {
-  double omega0, gamma;
-  int drude;
-  std::vector<double> sigma[3];  // canonical arrays (empty = 0)
-  std::vector<double> off[3][3];  // off-diagonal sigma[c][d], d != c (empty = 0)
-  bool aniso() const {
-    for (int c = 0; c < 3; c++)
-      for (int d = 0; d < 3; d++)
-        if (!off[c][d].empty()) return true;
-    return false;
-  }
-};
-
-struct BoxSpec {
-  int kind, index;
-  double box[6];
-  double value;
-};
-
-}  // namespace
-
-// =============================================================== structure
-struct mnl_structure {
-  int dim;
-  int n[3];
-  int io[3];
-  bool has[3];
-  double a, courant, dt;
-  double pml_thick[3][2] = {{0, 0}, {0, 0}, {0, 0}};
-  double pml_R[3][2], pml_stretch[3][2];
-  std::vector<double> chi1inv[3][3];  // [E comp][dir], canonical
-  std::vector<double> chi2[3], chi3[3];
-  std::vector<double> cond[2][3];     // conductivity of [B, D][dir], canonical (empty = 0)
-  std::vector<Lorentz> lor;
-  // H side: chi1inv of the H components (structure::set_mu ->
-  // set_chi1inv(H_stuff), [H comp][dir], canonical) and the magnetic susceptibilities
-  // (add_susceptibility(sigma, H_stuff, ...), diagonal sigma at the H components' points)
-  std::vector<double> mu1inv[3][3];
-  std::vector<Lorentz> hlor;
-  std::vector<BoxSpec> boxes;
-  size_t ntot;
-  int nl_mode = 0;  // 0: the fork (NR chi2, inert chi3); 1: upstream Meep (Pade chi2/chi3)
-
-  int shift(int c, int d) const {
-    if (!has[d]) return 0;
-    int t = ctype(c);
-    if (t == T_E || t == T_D) return d == cdir(c);
-    return d != cdir(c);
-  }
-  long long cstride(int d) const {
-    if (!has[d]) return 0;
-    long long nz = has[2] ? n[2] + 1 : 1, ny = has[1] ? n[1] + 1 : 1;
-    return d == 2 ? 1 : (d == 1 ? nz : nz * ny);
-  }
-};
-
-// ------------------------------------------------------------- DFT flux
-// fields::add_dft_flux / add_dft / update_dfts / dft_flux::flux (src/dft.cpp:
-// 51-300, 533-547, 578-640; loop_in_chunks src/loop_in_chunks.cpp:225-520),
-// Cartesian, no symmetry, centered grid.  The point set, interpolation weights
-// and list order are those of the reference's single-process chunk layout
-// (PML regions broken off, structure.cpp:118-137), so every per-point DFT is
-// bitwise the reference's; each rank accumulates the points it owns on the
-// device, and flux() sums the pairs in list order on the host.
-struct DftChunkH {
-  int c;
-  cplx scale;
-  int avgmode;       // 0: point, 1: two Yee points, 2: four
-  size_t N, p0;      // points, first point in the flux object's point arrays
-  // the chunk's loop (for get_dft_array): corners, boundary weights, dV0,
-  // include_dV_and_interp_weights, stored_weight
-  int is[3], ie[3];
-  double s0[3], s1[3], e0[3], e1[3], dV0;
-  bool incl;
-  cplx stored;
-};
-struct DftFluxH {
-  std::vector<double> omega;
-  int nfreq = 0, decim = 1;
-  bool fields = false;                // dft_fields (add_dft_fields): chunks in E only
-  double wmin[3] = {0, 0, 0}, wmax[3] = {0, 0, 0};  // `where` (get_dft_array's collapse)
-  std::vector<DftChunkH> E, H;        // list order (next_in_dft)
-  size_t npts = 0;                    // E points, then H points
-  std::vector<int> h_pj;              // 3 local indices per point (-1: not this rank's)
-  Box bbox{};                         // this rank's points, +1 along every axis (dft_layout;
-                                      // empty: lo > hi)
-  int *d_pj = nullptr, *d_pch = nullptr;
-  double *d_pw = nullptr;             // w * 0.25 / 0.5 / 1 per point
-  DftChunkDev *d_ch = nullptr;        // per chunk (E list, then H list)
-  double *d_dft = nullptr;            // [slot/64][freq][slot%64] complex (re, im)
-  double *d_ph = nullptr;             // phases of one batch: [update][chunk][freq] complex
-  size_t ph_cap = 0;
-  int row = 0;                        // next phase row of this batch
-  std::vector<int> slot;              // device slot of each point (reference order -> slot)
-  double *d_fr = nullptr;             // [update][slot] sampled fields awaiting accumulation
-  int nbuf = 0;                       // buffered updates (rows row-nbuf .. row-1)
-  int kb = DFT_KB;                    // updates per accumulation
-  double bytes = 0;                   // algorithmic bytes of one update (DESIGN.md "DFT")
-  int *d_sidx = nullptr;              // sampling plan (k_dft_plan): first Yee index per point
-  unsigned short *d_ssel = nullptr;   // ... and a selector per point
-  unsigned *d_spal = nullptr;         // ... and the palette bytes of its implicit-E chi1inv
-  void *d_su = nullptr;               // ... or those chi1inv values as doubles (fallback)
-  int *d_bad = nullptr;               // palette check of the plan (k_dft_plan)
-  bool usepal = false;                // the plan's palette bytes are exact
-  // compact box (pairs of steps): bbox's D / B of the two-step points
-  // for both steps of a pair, stored by the two-step kernel; per point its compact index
-  double *d_cmp = nullptr;
-  unsigned cmp_cells = 0;             // 0: the box is too large for a compact copy
-  unsigned cmp_mask = 0;              // arrays the samples read (D0..D2, B0..B2)
-  int *d_sci = nullptr;
-  bool cmp_on = false;                // the current pair plan stores this monitor's box
-  long long plan_key = -1;            // the mode the plan was built for (dft_plan_key)
-  ~DftFluxH() {
-    if (d_ph) (void)hipFree(d_ph);
-    if (d_sidx) (void)hipFree(d_sidx);
-    if (d_ssel) (void)hipFree(d_ssel);
-    if (d_spal) (void)hipFree(d_spal);
-    if (d_su) (void)hipFree(d_su);
-    if (d_bad) (void)hipFree(d_bad);
-    if (d_cmp) (void)hipFree(d_cmp);
-    if (d_sci) (void)hipFree(d_sci);
-  }
-};
-
-
-// =============================================================== fields
-struct mnl_fields {
-  mnl_structure S;  // copy of the global structure description
-  int device = 0;
-  hipStream_t stream = nullptr;
-  int rank = 0, nranks = 1;
-  std::unique_ptr<Comm> comm;
-  int slab_dir = 2;  // direction decomposed across ranks
-  DevGrid g;
-  DevFields f;
-  size_t nlocal = 0;  // doubles per local array
-  bool allocated[MNL_NUM_COMPONENTS] = {false};
-  bool pml_any[3] = {false, false, false};
-  std::vector<uint8_t> h_flag[3], h_zone[3];
-  std::vector<double> h_sig[3], h_kap[3], h_siginv[3];
-  std::vector<void *> dev_allocs;
-  Box interior;
-  // chi(2) Newton-Raphson runs only where chi2 != 0: the interior E update splits
-  // into the bounding box of those points (NR kernel) and the rest (plain kernel)
-  bool nr_split_done = false;
-  bool nr_shell_free = false;  // the chi2 box lies inside the interior: plain shell E kernels
-  Box nr_in{};
-  std::vector<Box> nr_rest;
-  Box nr_chi2{};  // bounding box of chi2 != 0 (device coordinates; empty: lo > hi)
-  // fused mode with chi(2): the chi2 box grown by one point, whose E / P the fused
-  // kernels leave to the NR E kernel (nr_fused_e); empty: no NR point anywhere
-  Box nr_xbox{};
-  std::vector<Box> shell;
-  BoxList shell_list;
-  // fused mode (DESIGN.md "Fused step")
-  bool fused = false;        // currently stepping in fused mode
-  Box fusedG;                // fused domain (local indices)
-  Box fusedL;                // lean box (no PML, every component owned)
-  BoxList fused_shell;       // everything else (multi-rank: the top plane)
-  FusedArgs fgeo;            // tile / chunk bounds (filled by make_fused_boxes)
-  std::vector<int> gitems;   // general-kernel items
-  int *d_gitems = nullptr;
-  size_t d_gitems_cap = 0;
-  // tile mode (MNL_TILE, default on): one tile kernel over every chunk outside the
-  // polarization chunks (lean + PML bodies), the general kernel over those chunks only
-  bool tile_mode = true;
-  bool tile_zcut = true;      // cut z chunks at the lean box's z range (short z-PML items)
-  int tile_body_mask = -1;   // MNL_TILE_BODY_MASK: step only these bodies (timing experiments)
-  // diagnostic / A-B switches, read once when the fields are created (mnl_fields_create)
-  bool ownc = true;           // MNL_NO_OWNC=1: no OWNC item flag
-  bool lean_halo = true;      // MNL_LEAN_HALO=0: general tiles recompute the lean halo
-  bool no_palette = false;    // MNL_NO_PALETTE=1: per-cell chi1inv loads, no byte palette
-  bool uniform = true;        // MNL_UNIFORM=0: per-cell palette loads in uniform items too
-  int lean_groups = 1, gen_groups = 1;  // MNL_LEAN_GROUPS / MNL_GEN_GROUPS: 1 or 8 queues
-  bool tile_gen_cus_env = false;        // MNL_TILE_GEN_CUS given (the tuner keeps it)
-  bool fused_zchunk_env = false;        // MNL_FUSED_ZCHUNK given (the tuner keeps it)
-  bool tb_env = false, tb_zchunk_env = false;  // MNL_TB / MNL_TB_ZCHUNK given (the same)
-  bool nr_defer = true;       // MNL_NR_DEFER=0: every NR problem solved in place
-  bool tile_stats = false, tb_stats = false;  // MNL_TILE_STATS / MNL_TB_STATS: print
-  // MNL_ITEM_CLOCK=<file>: per-item start / end records of the persistent kernels, appended
-  // to <file> after every batch (ItemClock; tools/item_clock.py)
-  std::string clk_path;
-  unsigned long long *d_clk = nullptr;
-  unsigned *d_clk_n = nullptr;
-  std::vector<int> titems;   // tile-kernel items (FusedArgs::titems)
-  int *d_titems = nullptr;
-  size_t d_titems_cap = 0;
-  unsigned *d_tflag = nullptr;  // per tile item: uniform palette word or ~0u
-  size_t tflag_n = 0;
-  long long tile_cells = 0;     // own cells of the tile items
-  double tile_cells_nu = -1;    // ... of those that read a palette index per cell
-  std::vector<char> tile_z;     // per local z plane: stepped by the tile kernel
-  long long lean_cells = 0, gen_cells = 0;
-  FusedTab d_tab{};          // per-direction PML coefficient tables for the fused kernels
-  // multi-rank fused stepping: chunk 0 on s_aux, halo exchange on s_comm,
-  // overlapped with the interior kernels on `stream` (DESIGN.md "Multi-GPU")
-  hipStream_t s_aux = nullptr, s_comm = nullptr;
-  hipEvent_t ev_start = nullptr, ev_early = nullptr, ev_x1 = nullptr, ev_shell = nullptr,
-             ev_x0 = nullptr;
-  double *pp_B[3] = {nullptr, nullptr, nullptr}, *pp_D[3] = {nullptr, nullptr, nullptr};
-  double *pp_E[3] = {nullptr, nullptr, nullptr}, *pp_H[3] = {nullptr, nullptr, nullptr};
-  double *pp_UB[3] = {nullptr, nullptr, nullptr};
-  int fused_zchunk = 0;
-  int fused_bpc = 1;
-  int fused_dist = 1;
-  int gen_cus = -1;  // CUs for the general kernel running beside the lean one (0: serial)
-  bool fused_concurrent = false;  // last fused step ran lean + general concurrently
-  int tile_gen_cus = 0;           // tile mode: general kernel beside the tile kernel (CUs)
-  unsigned long long *d_fused_ctr = nullptr;  // work-item counters of the fused kernels
-  unsigned long long ctr_base[FUSED_NCTR] = {0};  // their values at the next launch
-  int stagger = 0, nstagger = 0;  // dev_alloc offset step (bytes) for field arrays
-  void *arena = nullptr;           // optional single allocation for field-sized arrays
-  size_t arena_cap = 0, arena_used = 0, arena_gap = 0;
-  int arena_req = 0;               // MNL_ARENA: field arrays to reserve (0: off)
-  bool contig = false;             // MNL_CONTIG: physically contiguous field allocations
-  int contig_fallbacks = 0;        // contiguous requests the driver could not satisfy
-  bool palette_tried = false;
-  bool dsrc_in_shell = false;  // a D source point lies outside the interior box
-  bool any_srcB = false, any_isrc = false;  // anywhere in the cell (all ranks agree)
-  bool any_dsrc_w = false;  // a D current source on a W-form (PML-along-E) point
-  unsigned *d_uidx = nullptr;  // chi1inv palette indices over fusedG (null: f64 chi1inv)
-  double *d_utab = nullptr;    // 3 x 256 palette values
-  unsigned *d_uflag = nullptr;  // per lean item: uniform palette word or ~0u (k_lean_uniform)
-  size_t uflag_n = 0;
-  unsigned long long uflag_sig = 0;  // geometry the flags were built for
-  unsigned *d_gflag = nullptr;  // per general item (k_general_uniform)
-  size_t gflag_n = 0;
-  // cells of lean / general items that still read a palette index per cell (the
-  // algorithmic bytes of bench.py's roofline count 4 B of chi1inv for those only)
-  double lean_cells_nu = -1, gen_cells_nu = -1;
-  bool uflag_active = false;
-  bool allow_fused = true;
-  // the reference allocates H (as a copy of B) and the W auxiliary fields (as a
-  // copy of E / H) on the first update_eh (src/update_eh.cpp:204-216); the first
-  // step runs unfused and performs those copies at the same points of the step
-  bool e_first_done = false, h_first_done = false;
-  bool u_first_done[2] = {false, false};  // f_u of B / D: a copy of f on the first step_db
-                                          // (src/step_db.cpp:71-75)
-  bool first_step_mode = false;
-  bool force_unfused_next = false;  // E / H set directly (initialize_field): E != chi1inv D
-  // temporal blocking: pairs of steps as rim (one-step tile kernel) +
-  // L2 (two-step kernel) + rim, over three buffer sets
-  bool tb_enabled = true;           // MNL_TB=0 at creation: never
-  int tb_zchunk = 0;                // planes per two-step item (0: automatic)
-  int rim_zchunk = 0;               // planes per rim item of a pair (0: fused_zchunk)
-  bool nr_early = true;             // MNL_NR_EARLY=0: the NR box's E phase after both kernels
-  unsigned fused_epoch = 0;         // bumped on every entry into the fused mode
-  unsigned long long tb_sig = 0;    // inputs of the current plan (0: none)
-  bool tb_have = false;             // the current plan has two-step items
-  bool tb_mid_fresh = false;        // middle set holds a copy of the state (ghost / wall entries)
-  std::vector<int> tb_ritems, tb_rgeo;  // rim items (tile-kernel codes) and their own boxes
-  std::vector<TB2Item> tb_items;        // two-step items
-  int *d_tb_ritems = nullptr, *d_tb_rgeo = nullptr;
-  unsigned *d_tb_rflag = nullptr, *d_tb_uflag = nullptr;
-  TB2Item *d_tb_items = nullptr;
-  size_t tb_rcap = 0, tb_gcap = 0, tb_icap = 0;
-  bool tb_nopair = false;   // MNL_TB_NOPAIR=1: x-face rim strips one per workgroup (A/B)
-  bool tb_last = false;     // the last batch of >= 2 steps stepped in pairs (tb_usable)
-  int res_l = -1, res_r = -1;  // schedule options: the same for the two-step / rim launches only
-  int tb_res = -1;          // MNL_TB_RES: CUs the pairs' persistent launches leave free (-1:
-                            // TB_RES_CUS with several ranks, 0 with one; A/B of the reservation)
-  bool tb_oom = false;      // the middle buffer set did not fit: temporal blocking off
-  bool tb_oom_test = false; // MNL_TB_OOM=1: its allocation fails (tests)
-  bool tb_narrow = true;    // MNL_TB_NARROW=0: no narrow x-face strip items (A/B)
-  bool dft_pal = true;      // MNL_DFT_PAL=0: DFT sampling plans carry chi1inv as doubles (A/B)
-  bool dft_cmp = true;      // MNL_DFT_CMP=0: pairs sample DFT monitors from the field arrays
-  std::vector<TBCmp> tb_cmp;  // the compact DFT boxes of the current pair plan
-  int tb_nnarrow = 0;       // narrow x-face strip items of the current plan
-  int tb_rfree = 0;         // leading rim items that read no slab-face data (multi-rank)
-  bool tb_chain_pending = false;  // the last multi-rank pair's s_comm chain not yet joined
-  double *pp3_B[3] = {nullptr, nullptr, nullptr}, *pp3_D[3] = {nullptr, nullptr, nullptr};
-  double *pp3_E[3] = {nullptr, nullptr, nullptr}, *pp3_H[3] = {nullptr, nullptr, nullptr};
-  double *pp3_UB[3] = {nullptr, nullptr, nullptr};
-  double tb_cells = 0, tb_border = 0, tb_cells_nu = 0;  // own / border points of the items,
-                                                        // own points of the mixed-palette ones
-  double rim_cells = 0, rim_lean = 0, rim_cells_nu = 0;  // rim items: own / lean / mixed cells
-  int nan_every = 1;                // NaN guard cadence (src/step.cpp:138-139: every step)
-  int since_nan = 0;                // steps since the last NaN guard (across calls)
-  bool nan_due = false;             // a guard is due once the state is complete (pending rim)
-  int nan_launched = 0;             // guards launched in this chunk (flag read at its end)
-  long long nan_at = 0;             // time step of the state the next guard checks
-  NanTerms nan_terms{};             // this batch's interpolation terms (nan_terms_build)
-  int *d_nanflag = nullptr;         // [flag, step]
-  CurlPlan planB, planD;
-  bool nr = false;
-  bool upnl = false;  // upstream chi2/chi3 update active (nl_mode 1 with nonzero chi)
-  bool hall = false;  // H-side materials: H stored everywhere (DevFields::hall)
-  std::vector<uint8_t> h_hsep_zone;  // host copy of DevFields::hsep_zone (27 zone boxes)
-  // sources
-  std::vector<SrcTime> srcs;
-  std::vector<SrcGroup> groups;
-  bool src_dirty = true;
-  std::vector<long long> srcB_idx, srcD_idx, isrc_idx;  // local linear indices
-  std::vector<int> srcB_comp, srcD_comp, isrc_comp;
-  std::vector<unsigned char> isrc_zone;  // owning reference chunk (zone box) per isrc point
-  ISrcDev isrc_dev{};                    // device copy (sorted), built with the lists
-  std::vector<std::pair<int, int>> srcB_ref, srcD_ref, isrc_ref;  // (group, point)
-  // current sources per field type ([0] B, [1] D), in layer order (SrcDev)
-  std::vector<double> src_amp[2];
-  std::vector<int> src_gid[2], src_layer[2];
-  long long *d_srcB_idx = nullptr, *d_srcD_idx = nullptr;
-  int *d_srcB_comp = nullptr, *d_srcD_comp = nullptr;
-  double *d_src_amp[2] = {nullptr, nullptr};
-  int *d_src_gid[2] = {nullptr, nullptr};
-  double *d_vals = nullptr;
-  size_t d_vals_cap = 0;
-  long long t = 0;
-  double dt;
-  // timers / profiling
-  bool profiling = false;
-  // fields::times_spent by time_sink (src/meep.hpp:1610-1633 order), seconds
-  double sink_s[MNL_NUM_TIME_SINKS] = {0};
-  double last_out_wall = -1;  // "on time step" output (src/step.cpp:44-56)
-  long long last_out_t = 0;
-  double timer_ms[16] = {0};
-  long long timer_count[16] = {0};
-  std::vector<hipEvent_t> ev_pool;
-  unsigned long long *d_nr_fallbacks = nullptr;
-  NRHard *d_nr_hard = nullptr;      // deferred Newton-Raphson problems (NR runs only)
-  unsigned *d_nr_hard_cnt = nullptr;
-  double *d_scratch = nullptr;  // canonical-size staging buffer
-  size_t scratch_cap = 0;
-  std::vector<std::unique_ptr<DftFluxH>> dfts;  // DFT flux objects (add_dft_flux order)
-
-  ~mnl_fields() {
-    if (device >= 0) hipSetDevice(device);
-    for (void *p : dev_allocs) hipFree(p);
-    for (auto e : ev_pool) hipEventDestroy(e);
-    if (d_scratch) hipFree(d_scratch);
-    if (d_vals) hipFree(d_vals);
-    if (d_gitems) hipFree(d_gitems);
-    if (d_titems) hipFree(d_titems);
-    if (d_tflag) hipFree(d_tflag);
-    if (d_uflag) hipFree(d_uflag);
-    if (d_gflag) hipFree(d_gflag);
-    for (void *p : {(void *)d_tb_ritems, (void *)d_tb_rgeo, (void *)d_tb_rflag, (void *)d_tb_uflag,
-                    (void *)d_tb_items})
-      if (p) hipFree(p);
-    comm.reset();
-    for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
-      if (e) hipEventDestroy(e);
-    if (s_aux) hipStreamDestroy(s_aux);
-    if (s_comm) hipStreamDestroy(s_comm);
-    if (stream) hipStreamDestroy(stream);
-  }
-};
-
-namespace {
-
-bool in_fused_box(const mnl_fields *F, int c, const int jg[3]);
-int nan_launch(mnl_fields *F, hipStream_t st = nullptr, double *const *E = nullptr,
-               double *const *D = nullptr);
-void nan_count(mnl_fields *F, int k);
-int nan_result(mnl_fields *F);
-int nan_terms_build(mnl_fields *F);
-
-// Field-sized arrays start at staggered offsets (a multiple of 128 B, different
-// for every array) so that the many streams one fused step reads and writes at
-// the same element index do not start on the same HBM channel / bank.
-template <class T>
-int dev_alloc(mnl_fields *F, T **p, size_t n, bool zero = true) {
-  void *q = nullptr;
-  const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-  if (F->arena_req > 0 && !F->arena && F->nlocal && bytes >= (size_t(64) << 20)) {
-    const size_t cap = size_t(F->arena_req) * (F->nlocal * 8 + F->arena_gap + 4096);
-    const hipError_t ea = F->contig ? hipExtMallocWithFlags(&F->arena, cap, hipDeviceMallocContiguous)
-                                    : hipMalloc(&F->arena, cap);
-    if (ea == hipSuccess) {
-      F->arena_cap = cap;
-      F->dev_allocs.push_back(F->arena);
-    } else {
-      F->arena_req = 0;
-      (void)hipGetLastError();
-    }
-  }
-  if (F->arena_cap && bytes >= (size_t(64) << 20)) {  // field-sized: bump-allocate in the arena
-    const size_t at = (F->arena_used + 255) & ~size_t(255);
-    if (at + bytes <= F->arena_cap) {
-      F->arena_used = at + bytes + F->arena_gap;
-      *p = (T *)((char *)F->arena + at);
-      if (zero) {
-        hipError_t e = hipMemsetAsync(*p, 0, bytes, F->stream);
-        if (e != hipSuccess) return fail(std::string("hipMemset failed: ") + hipGetErrorString(e));
-      }
-      return 0;
-    }
-  }
-  const bool big = bytes >= (size_t(64) << 20) && F->stagger > 0;
-  const size_t off = big ? (size_t(F->stagger) * F->nstagger++) % (size_t(1) << 20) : 0;
-  const size_t nb = bytes + (big ? (size_t(1) << 20) : 0);
-  hipError_t e = hipErrorUnknown;
-  if (F->contig && bytes >= (size_t(64) << 20)) {
-    e = hipExtMallocWithFlags(&q, nb, hipDeviceMallocContiguous);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      F->contig_fallbacks++;
-    }
-  }
-  if (e != hipSuccess) e = hipMalloc(&q, nb);
-  if (e != hipSuccess) return fail(std::string("hipMalloc failed: ") + hipGetErrorString(e));
-  if (zero) {
-    e = hipMemsetAsync((char *)q + off, 0, bytes, F->stream);
-    if (e != hipSuccess) return fail(std::string("hipMemset failed: ") + hipGetErrorString(e));
-  }
-  F->dev_allocs.push_back(q);
-  *p = (T *)((char *)q + off);
-  return 0;
-}
+int g_verbosity = 1;
 
 // ------------------------------------------------------------- PML zones
 // structure::use_pml + effort volumes (src/structure.cpp:509-523, 118-137)
@@ -541,9 +24,6 @@ inline double pml_x(int i, double dx, double bloc, double a) {
   return (0.5 / a * ((int)(dx * (2 * a) + 0.5) - (int)(fabs(bloc - here) * (2 * a) + 0.5)));
 }
 
-struct ZoneIv {
-  int c0, c1, zone;  // chunk covers half-coords [c0, c1] relative to io
-};
 
 std::vector<ZoneIv> zone_intervals(const mnl_structure &S, int d) {
   std::vector<ZoneIv> iv;
@@ -1664,579 +1144,7 @@ SrcDev src_dev(mnl_fields *F, int t, const double *J) {
   return s;
 }
 
-// ------------------------------------------------------------- interpolation
-inline int my_round(double x) { return int(floor(fabs(x) + 0.5) * (x < 0 ? -1 : 1)); }
-
-// complex slot of (device slot, frequency) in the wave-blocked DFT array
-inline size_t dft_at(size_t p, size_t i, size_t nf) { return ((p >> 6) * nf + i) * 64 + (p & 63); }
-
-// compute_boundary_weights (src/loop_in_chunks.cpp:257-300), snap_empty_dimensions = false
-void dft_boundary_weights(const mnl_structure &S, const double wmin[3], const double wmax[3],
-                          const int is[3], const int ie[3], double s0[3], double e0[3],
-                          double s1[3], double e1[3]) {
-  for (int d = 0; d < 3; d++) {
-    s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
-    if (!S.has[d]) continue;
-    double w0 = 1. - wmin[d] * S.a + 0.5 * is[d];
-    double w1 = 1. + wmax[d] * S.a - 0.5 * ie[d];
-    if (ie[d] >= is[d] + 3 * 2) {
-      s0[d] = w0 * w0 / 2;
-      s1[d] = 1 - (1 - w0) * (1 - w0) / 2;
-      e0[d] = w1 * w1 / 2;
-      e1[d] = 1 - (1 - w1) * (1 - w1) / 2;
-    } else if (ie[d] == is[d] + 2 * 2) {
-      s0[d] = w0 * w0 / 2;
-      s1[d] = 1 - (1 - w0) * (1 - w0) / 2 - (1 - w1) * (1 - w1) / 2;
-      e0[d] = w1 * w1 / 2;
-      e1[d] = s1[d];
-    } else if (wmin[d] == wmax[d]) {
-      s0[d] = w0;
-      s1[d] = w1;
-      e0[d] = w1;
-      e1[d] = w0;
-    } else if (ie[d] == is[d] + 1 * 2) {
-      s0[d] = w0 * w0 / 2 - (1 - w1) * (1 - w1) / 2;
-      e0[d] = w1 * w1 / 2 - (1 - w0) * (1 - w0) / 2;
-      s1[d] = e0[d];
-      e1[d] = s0[d];
-    }
-  }
-}
-
-// the reference's chunks in creation order: x zones outer, then y, then z
-// (absolute little corner io and cell counts n per direction)
-std::vector<std::array<int, 6>> reference_chunks(const mnl_structure &S) {
-  std::vector<std::pair<int, int>> iv[3];
-  for (int d = 0; d < 3; d++) {
-    if (!S.has[d]) {
-      iv[d].push_back({0, 0});
-      continue;
-    }
-    for (auto &z : zone_intervals(S, d)) iv[d].push_back({S.io[d] + z.c0, (z.c1 - z.c0) / 2});
-  }
-  std::vector<std::array<int, 6>> out;
-  for (auto &ix : iv[0])
-    for (auto &iy : iv[1])
-      for (auto &iz : iv[2]) out.push_back({ix.first, iy.first, iz.first, ix.second, iy.second, iz.second});
-  return out;
-}
-
-// fields::add_dft for component c over [wmin, wmax]: the chunks loop_in_chunks
-// creates, prepended to `list` (their points appended to the flux object's point
-// arrays).  Centered grid, or with yee the component's own grid (loop_in_chunks(...,
-// cgrid = c), src/loop_in_chunks.cpp:350-356: where shifted by yee_shift(Centered) -
-// yee_shift(c), rounded to the dielectric grid, shifted back by iyee_c).
-void dft_add(mnl_fields *F, DftFluxH &o, int c, const double wmin[3], const double wmax[3],
-             bool incl, cplx stored_weight, double dt_factor, std::vector<DftChunkH> &list,
-             std::vector<double> &pw, bool yee = false) {
-  const mnl_structure &S = F->S;
-  const DevGrid &g = F->g;
-  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0}, sh[3] = {1, 1, 1};
-  for (int d = 0; d < 3; d++) {
-    if (!S.has[d]) continue;
-    if (yee) sh[d] = S.shift(c, d);
-    const int iyc = 1 - sh[d];                                          // iyee_c
-    const double yc = 1 * (0.5 * (1.0 / S.a)) - sh[d] * (0.5 * (1.0 / S.a));  // yee_c
-    is[d] = 1 + 2 * int(floor((wmin[d] + yc) * S.a - .5)) - iyc;  // vec2diel_floor, equal_shift 0
-    ie[d] = 1 + 2 * int(ceil((wmax[d] + yc) * S.a - .5)) - iyc;
-  }
-  double s0[3], s1[3], e0[3], e1[3];
-  dft_boundary_weights(S, wmin, wmax, is, ie, s0, e0, s1, e1);
-  double dV0 = 1.0;
-  for (int d = 0; d < 3; d++)
-    if (S.has[d] && wmax[d] - wmin[d] > 0.0) dV0 *= 1.0 / S.a;
-  if (!F->allocated[c]) return;
-  int yd[3];  // yucky loop directions (3D: X,Y,Z; 2D: Z,X,Y; 1D: X,Y,Z)
-  if (S.dim == 2)
-    yd[0] = 2, yd[1] = 0, yd[2] = 1;
-  else
-    yd[0] = 0, yd[1] = 1, yd[2] = 2;
-  std::vector<DftChunkH> made;
-  for (auto &ch : reference_chunks(S)) {
-    int isc[3], iec[3];
-    double s0c[3], s1c[3], e0c[3], e1c[3];
-    bool emp = false;
-    for (int d = 0; d < 3; d++) {
-      s0c[d] = s1c[d] = e0c[d] = e1c[d] = 1.0;
-      if (!S.has[d]) {
-        isc[d] = iec[d] = 0;
-        continue;
-      }
-      // little_owned_corner(cgrid) = io + 2 - iyee_shift, big_owned_corner = big - iyee_shift
-      const int uoc = S.io[d] + 2 - sh[d], coc = ch[d] + 2 - sh[d],
-                cbo = ch[d] + 2 * ch[3 + d] - sh[d];
-      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
-      isc[d] = std::max(is[d], iscoS);
-      iec[d] = std::min(ie[d], iecoS);
-      if (isc[d] > iec[d]) emp = true;
-    }
-    if (emp) continue;
-    for (int d = 0; d < 3; d++) {
-      if (!S.has[d]) continue;
-      if (isc[d] == is[d]) {
-        s0c[d] = s0[d];
-        s1c[d] = s1[d];
-      } else if (isc[d] == is[d] + 2) {
-        s0c[d] = s1[d];
-      }
-      if (iec[d] == ie[d]) {
-        e0c[d] = e0[d];
-        e1c[d] = e1[d];
-      } else if (iec[d] == ie[d] - 2) {
-        e0c[d] = e1[d];
-      }
-      if (iec[d] == isc[d]) {
-        double w = std::min(s0c[d], e0c[d]);
-        s0c[d] = e0c[d] = s1c[d] = e1c[d] = w;
-      } else if (iec[d] == isc[d] + 2) {
-        double w = std::min(s0c[d], e1c[d]);
-        s0c[d] = w, e1c[d] = w;
-        w = std::min(s1c[d], e0c[d]);
-        s1c[d] = w, e0c[d] = w;
-      } else if (iec[d] == isc[d] + 4) {
-        double w = std::min(s1c[d], e1c[d]);
-        s1c[d] = w, e1c[d] = w;
-      }
-    }
-    DftChunkH dc;
-    dc.c = c;
-    dc.scale = stored_weight * cplx(1.0) * dt_factor;
-    int nun = 0;
-    for (int d = 0; d < 3; d++)
-      if (!yee && S.has[d] && !S.shift(c, d)) nun++;
-    dc.avgmode = nun;
-    for (int d = 0; d < 3; d++) {
-      dc.is[d] = isc[d], dc.ie[d] = iec[d];
-      dc.s0[d] = s0c[d], dc.s1[d] = s1c[d], dc.e0[d] = e0c[d], dc.e1[d] = e1c[d];
-    }
-    dc.dV0 = dV0;
-    dc.incl = incl;
-    dc.stored = stored_weight;
-    long ln[3];
-    for (int k = 0; k < 3; k++) ln[k] = S.has[yd[k]] ? (iec[yd[k]] - isc[yd[k]]) / 2 + 1 : 1;
-    dc.N = size_t(ln[0] * ln[1] * ln[2]);
-    dc.p0 = 0;  // set when the lists are laid out
-    auto W1 = [&](int k, long i) -> double {
-      const int d = yd[k];
-      const long n = ln[k];
-      if (i > 1 && i < n - 2) return 1.0;
-      if (i == 0) return s0c[d];
-      if (i == 1) return s1c[d];
-      if (i == n - 1) return e0c[d];
-      if (i == n - 2) return e1c[d];
-      return 1.0;
-    };
-    const double fac = nun == 2 ? 0.25 : (nun == 1 ? 0.5 : 1.0);
-    // points in IVEC_LOOP_COUNTER order; local indices of the Yee base point
-    std::vector<int> pj;
-    std::vector<double> w;
-    for (long i1 = 0; i1 < ln[0]; i1++)
-      for (long i2 = 0; i2 < ln[1]; i2++)
-        for (long i3 = 0; i3 < ln[2]; i3++) {
-          const long ii[3] = {i1, i2, i3};
-          int p[3] = {0, 0, 0};  // centered point, absolute half-coords
-          for (int k = 0; k < 3; k++)
-            if (S.has[yd[k]]) p[yd[k]] = isc[yd[k]] + 2 * int(ii[k]);
-          double wt = incl ? (W1(2, i3) * (W1(1, i2) * ((dV0 + 0.0 * i2) * W1(0, i1)))) : 1.0;
-          w.push_back(wt * fac);
-          // this rank owns the centered point if its slab index is in the owned range
-          int j[3] = {0, 0, 0};
-          bool mine = true;
-          for (int d = 0; d < 3; d++) {
-            if (!S.has[d]) continue;
-            if (yee) {  // the Yee point itself; owned along d by one rank (walls included)
-              j[d] = (p[d] - S.io[d] - sh[d]) / 2 - g.off[d];
-              const int nloc = g.N[g.ax[d]] - 1;  // this rank's cells along d
-              if (sh[d] ? (j[d] < 0 || j[d] > nloc - 1) : (j[d] < 1 || j[d] > nloc)) mine = false;
-              continue;
-            }
-            const int base = p[d] - (S.shift(c, d) ? 0 : 1);  // Yee point of c at/below p
-            j[d] = (base - S.io[d] - S.shift(c, d)) / 2 - g.off[d];
-            const int jc = (p[d] - S.io[d] - 1) / 2 - g.off[d];  // centered index
-            if (jc < g.owned_lo_sh[d] || jc > g.owned_hi_sh[d]) mine = false;
-          }
-          for (int d = 0; d < 3; d++) pj.push_back(mine ? j[d] : -1);
-        }
-    dc.p0 = o.h_pj.size() / 3;
-    o.h_pj.insert(o.h_pj.end(), pj.begin(), pj.end());
-    pw.insert(pw.end(), w.begin(), w.end());
-    made.push_back(dc);
-  }
-  for (auto &m : made) list.insert(list.begin(), m);
-}
-
-// decimation_factor of fields::add_dft (src/dft.cpp:190-213)
-int dft_decimation(mnl_fields *F, const double *freqs, int nfreq, int decim) {
-  if (decim != 0) return decim;
-  double src_freq_max = 0;
-  for (auto &st : F->srcs) {
-    const double fw = st.kind == 0 ? sqrt(-2.0 * log(1e-7)) / (st.width * pi) : 0.0;
-    if (fw == 0)
-      decim = 1;
-    else
-      src_freq_max =
-          std::max(src_freq_max, std::abs(st.kind == 0 ? st.freq : st.cfreq.real()) + 0.5 * fw);
-  }
-  double freq_max = 0;
-  for (int i = 0; i < nfreq; ++i) freq_max = std::max(freq_max, std::abs(freqs[i]));
-  bool nonlinear = false;  // structure_chunk::has_nonlinearities: nonzero chi2/chi3
-  for (int c = 0; c < 3; c++) {
-    for (double v : F->S.chi2[c]) nonlinear = nonlinear || v != 0.0;
-    for (double v : F->S.chi3[c]) nonlinear = nonlinear || v != 0.0;
-  }
-  for (auto &b : F->S.boxes) nonlinear = nonlinear || ((b.kind == 1 || b.kind == 2) && b.value != 0.0);
-  // (src/dft.cpp:207-210 overwrites the fwidth == 0 case above)
-  if ((freq_max > 0) && (src_freq_max > 0) && !nonlinear)
-    return std::max(1, int(std::floor(1 / (F->dt * (freq_max + src_freq_max)))));
-  return 1;
-}
-
-// Device layout of a DFT object whose E list holds the points of `pwE` and whose
-// H points (ho) follow: per-point chunk ids, wave-blocked DFT array, slots.
-int dft_layout(mnl_fields *F, std::unique_ptr<DftFluxH> &o, DftFluxH &ho, std::vector<double> &pwE,
-               std::vector<double> &pwH) {
-  const int nfreq = o->nfreq;
-  // lay out: E points (creation order), then H points; chunks keep their p0
-  const size_t nE = o->h_pj.size() / 3;
-  for (auto &h : o->H) h.p0 += nE;
-  o->h_pj.insert(o->h_pj.end(), ho.h_pj.begin(), ho.h_pj.end());
-  pwE.insert(pwE.end(), pwH.begin(), pwH.end());
-  o->npts = o->h_pj.size() / 3;
-  // per-point chunk id: chunks numbered E list then H list
-  std::vector<int> pch(o->npts, 0);
-  std::vector<DftChunkDev> chd;
-  auto lay = [&](const std::vector<DftChunkH> &L) {
-    for (auto &dc : L) {
-      DftChunkDev cd;
-      cd.c = dc.c;
-      cd.avgmode = dc.avgmode;
-      cd.d1 = cd.d2 = -1;  // grid_volume::yee2cent_offsets order (X, Y, Z)
-      for (int dd = 0; dd < 3; dd++)
-        if (F->S.has[dd] && !F->S.shift(dc.c, dd)) (cd.d1 < 0 ? cd.d1 : cd.d2) = dd;
-      for (size_t k = 0; k < dc.N; k++) pch[dc.p0 + k] = (int)chd.size();
-      chd.push_back(cd);
-    }
-  };
-  lay(o->E);
-  lay(o->H);
-  // per point and update: 3 indices + chunk id + weight, the averaged field
-  // values, the sample written and read back, and 1/kb of a read-modify-write
-  // of one complex value per frequency (DESIGN.md "DFT")
-  for (const auto *L : {&o->E, &o->H})
-    for (auto &dc : *L)
-      o->bytes += double(dc.N) * (12 + 4 + 8 + 8.0 * (1 << dc.avgmode) + 16 +
-                                  (12 + 4 + 32.0 * nfreq) / o->kb);
-  // Device slots: the points sorted by component and chunk, then z, y, x (x fastest like
-  // the field arrays), so that a wave's field reads are as contiguous as the
-  // plane's orientation allows and a workgroup of the accumulation almost always holds one
-  // chunk (one phase row, staged in LDS once); other ranks' points last.  Only the storage
-  // order changes -- every point keeps its own reference-order accumulation.
-  std::vector<int> ord(o->npts);
-  for (size_t p = 0; p < o->npts; p++) ord[p] = (int)p;
-  auto key = [&](int p) {
-    const int *j = &o->h_pj[3 * (size_t)p];
-    return std::make_tuple(j[0] < 0, chd[pch[p]].c, pch[p], j[2], j[1], j[0], p);
-  };
-  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return key(a) < key(b); });
-  o->slot.assign(o->npts, 0);
-  std::vector<int> spj(3 * o->npts), spch(o->npts);
-  std::vector<double> spw(o->npts);
-  for (size_t t = 0; t < o->npts; t++) {
-    const int p = ord[t];
-    o->slot[p] = (int)t;
-    for (int e = 0; e < 3; e++) spj[3 * t + e] = o->h_pj[3 * (size_t)p + e];
-    spch[t] = pch[p];
-    spw[t] = pwE[p];
-  }
-  for (int k = 0; k < 3; k++) o->bbox.lo[k] = INT32_MAX, o->bbox.hi[k] = -1;
-  for (size_t p = 0; p < o->npts; p++) {
-    if (o->h_pj[3 * p] < 0) continue;
-    for (int k = 0; k < 3; k++) {
-      o->bbox.lo[k] = std::min(o->bbox.lo[k], o->h_pj[3 * p + k]);
-      o->bbox.hi[k] = std::max(o->bbox.hi[k], o->h_pj[3 * p + k] + 1);
-    }
-  }
-  // compact box (two-step pairs, 3-D): every bbox cell, 2 states x 6 arrays, <= 1 GiB
-  o->cmp_cells = 0, o->cmp_mask = 0;
-  if (F->S.dim == 3 && o->bbox.hi[0] >= 0) {
-    double nc = 1;
-    for (int k = 0; k < 3; k++) nc *= o->bbox.hi[k] - o->bbox.lo[k] + 1;
-    if (nc * 96 <= double(1u << 30)) o->cmp_cells = (unsigned)nc;
-    for (const auto *L : {&o->E, &o->H})
-      for (auto &dc : *L) o->cmp_mask |= 1u << (dc.c >= 3 ? 3 + dc.c % 3 : dc.c % 3);
-  }
-  if (o->npts) {
-    if (dev_alloc(F, &o->d_pj, o->h_pj.size(), false) || dev_alloc(F, &o->d_pch, o->npts, false) ||
-        dev_alloc(F, &o->d_pw, o->npts, false) || dev_alloc(F, &o->d_ch, chd.size(), false) ||
-        dev_alloc(F, &o->d_dft, 2 * ((o->npts + 63) & ~size_t(63)) * (size_t)nfreq) ||
-        dev_alloc(F, &o->d_fr, o->npts * (size_t)o->kb))
-      return -1;
-    HIPCHK(hipMemcpyAsync(o->d_pj, spj.data(), spj.size() * 4, hipMemcpyHostToDevice, F->stream));
-    HIPCHK(hipMemcpyAsync(o->d_pch, spch.data(), spch.size() * 4, hipMemcpyHostToDevice, F->stream));
-    HIPCHK(hipMemcpyAsync(o->d_pw, spw.data(), spw.size() * 8, hipMemcpyHostToDevice, F->stream));
-    HIPCHK(hipMemcpyAsync(o->d_ch, chd.data(), chd.size() * sizeof(DftChunkDev), hipMemcpyHostToDevice,
-                          F->stream));
-    HIPCHK(hipStreamSynchronize(F->stream));
-  }
-  F->dfts.push_back(std::move(o));
-  return int(F->dfts.size()) - 1;
-}
-
-int dft_add_flux(mnl_fields *F, int nreg, const double *regions, const double *freqs, int nfreq,
-                 int decimation) {
-  if (F->src_dirty && build_source_lists(F)) return -1;
-  if (nreg < 1 || nfreq < 1) return fail("add_dft_flux: no regions / frequencies");
-  std::unique_ptr<DftFluxH> o(new DftFluxH);
-  o->nfreq = nfreq;
-  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
-  o->decim = dft_decimation(F, freqs, nfreq, decimation);
-  for (int d = 0; d < 3; d++) o->wmin[d] = regions[d], o->wmax[d] = regions[3 + d];
-  if (const char *e = getenv("MNL_DFT_BLOCK")) o->kb = std::max(1, std::min(DFT_KB, atoi(e)));
-  const double dt_factor = F->dt / sqrt(2.0 * pi) * o->decim;
-  std::vector<double> pwE, pwH;
-  DftFluxH ho;  // H points collected separately, appended after the E points
-  for (int r = 0; r < nreg; r++) {
-    const double *R = regions + 8 * r;
-    const int d = int(R[6]);
-    const double wgt = R[7];
-    int cE[2], cH[2];
-    switch (d) {  // fields::add_dft_flux (src/dft.cpp:601-617)
-      case 0: cE[0] = MNL_EY, cE[1] = MNL_EZ, cH[0] = MNL_HZ, cH[1] = MNL_HY; break;
-      case 1: cE[0] = MNL_EZ, cE[1] = MNL_EX, cH[0] = MNL_HX, cH[1] = MNL_HZ; break;
-      default: cE[0] = MNL_EX, cE[1] = MNL_EY, cH[0] = MNL_HY, cH[1] = MNL_HX; break;
-    }
-    for (int i = 0; i < 2; ++i) {
-      dft_add(F, *o, cE[i], R, R + 3, true, cplx(wgt * double(1 - 2 * i)), dt_factor, o->E, pwE);
-      dft_add(F, ho, cH[i], R, R + 3, false, cplx(1.0), dt_factor, o->H, pwH);
-    }
-  }
-  return dft_layout(F, o, ho, pwE, pwH);
-}
-
-// fields::add_dft_fields (src/dft.cpp:889-903): per component (in order) add_dft
-// without dV / interpolation weights, stored_weight 1, prepended to one list; on
-// the centered grid or (yee) each component's own grid
-int dft_add_fields(mnl_fields *F, int ncomp, const int *comps, const double wmin[3],
-                   const double wmax[3], const double *freqs, int nfreq, int yee, int decimation) {
-  if (F->src_dirty && build_source_lists(F)) return -1;
-  if (ncomp < 1 || nfreq < 1) return fail("add_dft_fields: no components / frequencies");
-  for (int k = 0; k < ncomp; k++)
-    if (comps[k] < 0 || comps[k] >= 6) return fail("add_dft_fields: E or H components only");
-  std::unique_ptr<DftFluxH> o(new DftFluxH);
-  o->fields = true;
-  o->nfreq = nfreq;
-  for (int i = 0; i < nfreq; i++) o->omega.push_back(2 * pi * freqs[i]);
-  o->decim = dft_decimation(F, freqs, nfreq, decimation);
-  for (int d = 0; d < 3; d++) o->wmin[d] = wmin[d], o->wmax[d] = wmax[d];
-  if (const char *e = getenv("MNL_DFT_BLOCK")) o->kb = std::max(1, std::min(DFT_KB, atoi(e)));
-  const double dt_factor = F->dt / sqrt(2.0 * pi) * o->decim;
-  std::vector<double> pwE, pwH;
-  DftFluxH ho;
-  for (int k = 0; k < ncomp; k++)
-    dft_add(F, *o, comps[k], wmin, wmax, false, cplx(1.0), dt_factor, o->E, pwE, yee != 0);
-  return dft_layout(F, o, ho, pwE, pwH);
-}
-
-// phases of every DFT update in steps [t0+1, t0+ns] -> device (one row per update)
-int dft_prepare(mnl_fields *F, long long t0, int ns) {
-  for (auto &op : F->dfts) {
-    DftFluxH &o = *op;
-    o.row = 0;
-    const size_t nch = o.E.size() + o.H.size();
-    std::vector<double> ph;
-    ph.reserve((size_t)ns * nch * o.nfreq * 2);
-    std::vector<cplx> pe(o.nfreq), phh(o.nfreq);
-    for (int s = 0; s < ns; s++) {
-      const long long t = t0 + s + 1;
-      if (t % o.decim) continue;
-      const double tE = t * F->dt, tH = tE - 0.5 * F->dt;  // fields::update_dfts
-      // exp(i omega t) once per frequency and time (E / H), then times each chunk's scale:
-      // the same operations as the reference's per-chunk polar(1, omega t) * scale
-      for (int i = 0; i < o.nfreq; i++) {
-        pe[i] = std::polar(1.0, o.omega[i] * tE);
-        phh[i] = std::polar(1.0, o.omega[i] * tH);
-      }
-      // chunks with the same time and the same scale (bitwise) share one row of products
-      std::vector<std::pair<std::pair<bool, cplx>, size_t>> done;
-      auto same = [](const cplx &x, const cplx &y) {
-        return memcmp(&x, &y, sizeof(cplx)) == 0;
-      };
-      auto add = [&](const std::vector<DftChunkH> &L) {
-        for (auto &dc : L) {
-          const bool isH = ctype(dc.c) == T_H;
-          size_t from = SIZE_MAX;
-          for (auto &d : done)
-            if (d.first.first == isH && same(d.first.second, dc.scale)) from = d.second;
-          const size_t at = ph.size();
-          if (from != SIZE_MAX) {
-            for (int i = 0; i < 2 * o.nfreq; i++) ph.push_back(ph[from + i]);
-            continue;
-          }
-          done.push_back({{isH, dc.scale}, at});
-          const std::vector<cplx> &pt = isH ? phh : pe;
-          for (int i = 0; i < o.nfreq; i++) {
-            const cplx p = pt[i] * dc.scale;
-            ph.push_back(p.real());
-            ph.push_back(p.imag());
-          }
-        }
-      };
-      add(o.E);
-      add(o.H);
-    }
-    if (ph.empty()) continue;
-    if (o.ph_cap < ph.size()) {
-      HIPCHK(hipStreamSynchronize(F->stream));
-      if (o.d_ph) hipFree(o.d_ph);
-      HIPCHK(hipMalloc(&o.d_ph, ph.size() * 8));
-      o.ph_cap = ph.size();
-    }
-    (void)nch;
-    HIPCHK(hipMemcpyAsync(o.d_ph, ph.data(), ph.size() * 8, hipMemcpyHostToDevice, F->stream));
-    HIPCHK(hipStreamSynchronize(F->stream));
-  }
-  return 0;
-}
-
-// accumulate the buffered updates of one flux object
-int dft_flush(mnl_fields *F, DftFluxH &o) {
-  if (!o.nbuf) return 0;
-  const size_t nch = o.E.size() + o.H.size();
-  const long long rstride = (long long)(nch * o.nfreq);
-  if (k_dft_accum(o.d_pj, o.d_pch, o.d_dft, o.d_fr, o.nbuf,
-                  o.d_ph + 2 * (size_t)(o.row - o.nbuf) * rstride, rstride, o.nfreq,
-                  (long long)o.npts, F->stream))
-    return fail("dft accumulate launch failed");
-  o.nbuf = 0;
-  return 0;
-}
-
-// after step t (fields::update_dfts, src/dft.cpp:249-263)
-// what a sampling plan depends on: implicit E (the fused mode and its geometry) and which H
-// components are stored separately
-long long dft_plan_key(const mnl_fields *F) {
-  long long k = (long long)F->fused_epoch * 2 + (F->fused ? 1 : 0);
-  for (int d = 0; d < 3; d++) k = k * 2 + (F->f.H[d] ? 1 : 0);
-  return k * 2 + (F->f.hall ? 1 : 0);
-}
-
-// fields: the buffer set to sample (null: the current one; temporal blocking samples the middle
-// step of a pair from the mid set)
-// cstate >= 0: a pair's middle (0) or new (1) state, whose two-step points are also in the
-// monitors' compact boxes
-int dft_update(mnl_fields *F, long long t, const DevFields *fields = nullptr, int cstate = -1) {
-  const bool planned = F->nlocal < (size_t(1) << 31);  // int32 indices in the plan
-  const DevFields &fs = fields ? *fields : F->f;
-  // the samples of every flux object due: planned ones in merged launches of up to DFT_MAXJ
-  DftSampleJobs J{};
-  auto launch = [&]() -> int {
-    if (J.n && k_dft_sample_jobs(J, F->g, fs, F->d_utab, F->stream))
-      return fail("dft sample launch failed");
-    J = DftSampleJobs{};
-    return 0;
-  };
-  for (auto &op : F->dfts) {
-    DftFluxH &o = *op;
-    if (t % o.decim || !o.npts) continue;
-    double *fr = o.d_fr + (size_t)o.nbuf * o.npts;
-    if (planned) {
-      const long long key = dft_plan_key(F);
-      if (o.plan_key != key) {
-        if (!o.d_sidx) {
-          HIPCHK(hipMalloc(&o.d_sidx, o.npts * 4));
-          HIPCHK(hipMalloc(&o.d_ssel, o.npts * 2));
-          HIPCHK(hipMalloc(&o.d_spal, o.npts * 4));
-          HIPCHK(hipMalloc(&o.d_su, o.npts * 32));
-          HIPCHK(hipMalloc(&o.d_bad, sizeof(int)));
-        }
-        if (o.cmp_cells && !o.d_sci) HIPCHK(hipMalloc(&o.d_sci, o.npts * 4));
-        const bool pal = F->fused && F->d_uidx && F->d_utab && F->dft_pal;
-        HIPCHK(hipMemsetAsync(o.d_bad, 0, sizeof(int), F->stream));
-        if (k_dft_plan(o.d_pj, o.d_pch, o.d_ch, (long long)o.npts, F->g, F->f,
-                       pal ? F->d_uidx : nullptr, pal ? F->d_utab : nullptr, o.d_sidx, o.d_ssel,
-                       o.d_spal, o.d_su, o.d_bad, o.bbox, o.cmp_cells ? o.d_sci : nullptr,
-                       F->stream))
-          return fail("dft plan launch failed");
-        int bad = 1;
-        if (pal) {  // once per plan: are the palette bytes exact for every implicit value?
-          HIPCHK(hipMemcpyAsync(&bad, o.d_bad, sizeof(int), hipMemcpyDeviceToHost, F->stream));
-          HIPCHK(hipStreamSynchronize(F->stream));
-        }
-        o.usepal = pal && bad == 0;
-        o.plan_key = key;
-      }
-      if (J.n == DFT_MAXJ && launch()) return -1;
-      DftSampleJob &jb = J.j[J.n++];
-      jb.sidx = o.d_sidx, jb.ssel = o.d_ssel, jb.spal = o.d_spal, jb.su = o.d_su;
-      jb.pw = o.d_pw, jb.fr = fr, jb.npts = (long long)o.npts, jb.blk0 = J.nblk;
-      jb.usepal = o.usepal ? 1 : 0;
-      if (cstate >= 0 && o.cmp_on && o.d_cmp && o.d_sci) {
-        jb.sci = o.d_sci;
-        jb.cmp = o.d_cmp + (size_t)cstate * 6 * o.cmp_cells;
-        jb.ncell = o.cmp_cells;
-        const int n0 = o.bbox.hi[0] - o.bbox.lo[0] + 1, n1 = o.bbox.hi[1] - o.bbox.lo[1] + 1;
-        for (int e = 0; e < 3; e++) {
-          const int ax = F->g.ax[e];
-          jb.cs[e] = ax == 0 ? 1 : ax == 1 ? n0 : ax == 2 ? n0 * n1 : 0;
-        }
-      }
-      J.nblk += ((long long)o.npts + 255) / 256;
-    } else if (k_dft_sample(o.d_pj, o.d_pw, o.d_pch, o.d_ch, fr, (long long)o.npts, F->g, fs,
-                            F->stream)) {
-      return fail("dft sample launch failed");
-    }
-  }
-  if (launch()) return -1;
-  for (auto &op : F->dfts) {
-    DftFluxH &o = *op;
-    if (t % o.decim || !o.npts) continue;
-    o.nbuf++;
-    o.row++;
-    if (o.nbuf == o.kb && dft_flush(F, o)) return -1;
-  }
-  return 0;
-}
-
-bool dft_due(const mnl_fields *F, long long t) {
-  for (auto &op : F->dfts)
-    if (op->npts && t % op->decim == 0) return true;
-  return false;
-}
-
-int timed_allreduce(mnl_fields *F, double *v, int n);
-
-int dft_flux_values(mnl_fields *F, int h, double *out) {
-  if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
-  DftFluxH &o = *F->dfts[h];
-  const size_t nf = o.nfreq;
-  std::vector<double> v(2 * ((o.npts + 63) & ~size_t(63)) * nf);
-  bool ok = true;
-  if (!v.empty())
-    ok = hipMemcpyAsync(v.data(), o.d_dft, v.size() * 8, hipMemcpyDeviceToHost, F->stream) ==
-             hipSuccess &&
-         hipStreamSynchronize(F->stream) == hipSuccess;
-  if (F->nranks > 1 && F->comm->agree_ok(ok, F->stream))  // every rank fails together
-    return fail(ok ? "flux: a rank failed" : "flux: device copy failed");
-  if (!ok) return fail("flux: device copy failed");
-  for (size_t i = 0; i < nf; ++i) out[i] = 0;
-  for (size_t k = 0; k < o.E.size() && k < o.H.size(); k++)  // dft_flux::flux (src/dft.cpp:533-547)
-    for (size_t p = 0; p < o.E[k].N; ++p) {
-      const size_t pe = o.E[k].p0 + p, ph = o.H[k].p0 + p;
-      if (o.h_pj[3 * pe] < 0 && o.h_pj[3 * pe + 1] < 0 && o.h_pj[3 * pe + 2] < 0) continue;
-      for (size_t i = 0; i < nf; ++i) {
-        const size_t ie = dft_at(o.slot[pe], i, nf), ih = dft_at(o.slot[ph], i, nf);
-        const cplx e(v[2 * ie], v[2 * ie + 1]);
-        const cplx hv(v[2 * ih], v[2 * ih + 1]);
-        out[i] += real(e * conj(hv));
-      }
-    }
-  if (F->nranks > 1)
-    for (size_t i0 = 0; i0 < nf; i0 += 64)
-      if (timed_allreduce(F, out + i0, (int)std::min<size_t>(64, nf - i0)))
-        return fail("flux allreduce failed");
-  return 0;
-}
-
+// (the interpolation helpers and the DFT monitors: mnl_dft.cpp)
 void interpolate(const mnl_structure &S, int c, const double pc[3], int locs[8][3], double w[8]) {
   const double SMALL = 1e-13;
   double p[3] = {0, 0, 0}, midv[3] = {0, 0, 0}, dv[3] = {0, 0, 0};
@@ -2376,7 +1284,7 @@ int get_field(mnl_fields *F, int c, const double pos[3], double *out, bool reduc
 // kind 2 (before NR E update): D comps (and Lorentz P), both directions.
 // kind 3 (before a DFT update): H comps unshifted along the slab axis need the
 //   low ghost plane, which the centred-grid average reads (src/dft.cpp:281-287).
-int exchange(mnl_fields *F, int kind, hipStream_t st = nullptr) {
+int exchange(mnl_fields *F, int kind, hipStream_t st) {
   if (!st) st = F->stream;
   const DevGrid &g = F->g;
   const int sd = F->slab_dir, ax = g.ax[sd];
@@ -5041,994 +3949,7 @@ int finalize_fields(mnl_fields *F) {
   return 0;
 }
 
-// ------------------------------------------------------------- checkpoint
-// fields::dump / fields::load (src/fields_dump.cpp:108-145, 232-270) and
-// structure::dump / load (src/structure_dump.cpp).  The reference writes HDF5
-// (absent from this image); here a flat binary file per rank: a header (grid,
-// decomposition, t) and every per-point state array of the rank -- the
-// reference's f, f_u, f_w, f_cond plus the polarizations P / P_prev, which it
-// does not save, and the DFT accumulators -- raw in the rank-local device
-// layout, so a load into fields built the same way resumes bit for bit.
-constexpr char CK_MAGIC[8] = {'M', 'N', 'L', 'F', 'L', 'D', '0', '1'};
-constexpr char CS_MAGIC[8] = {'M', 'N', 'L', 'S', 'T', 'R', '0', '1'};
-
-struct CkEntry {
-  int kind, a, b;
-  double *p;
-  size_t n;
-};
-
-std::vector<CkEntry> ckpt_entries(mnl_fields *F) {
-  DevFields &f = F->f;
-  std::vector<CkEntry> v;
-  auto add = [&](int kind, int a, int b, double *p, size_t n) {
-    if (p) v.push_back({kind, a, b, p, n});
-  };
-  const size_t n = F->nlocal;
-  for (int d = 0; d < 3; d++) {
-    add(0, d, 0, f.E[d], n);
-    add(1, d, 0, f.D[d], n);
-    add(2, d, 0, f.B[d], n);
-    add(3, d, 0, f.H[d], n);
-    add(4, d, 0, f.UB[d], n);
-    add(5, d, 0, f.UD[d], n);
-    add(6, d, 0, f.WE[d], n);
-    add(7, d, 0, f.WH[d], n);
-  }
-  for (int t = 0; t < 2; t++)
-    for (int d = 0; d < 3; d++) add(8, t, d, f.fcnd[t][d], n);
-  for (int k = 0; k < f.npol; k++)
-    for (int d = 0; d < 3; d++) {
-      add(9, k, d, f.pol[k].P[d], n);
-      add(10, k, d, f.pol[k].Pp[d], n);
-    }
-  for (size_t h = 0; h < F->dfts.size(); h++) {
-    DftFluxH &o = *F->dfts[h];
-    add(11, (int)h, o.nfreq, o.d_dft, 2 * ((o.npts + 63) & ~size_t(63)) * o.nfreq);
-  }
-  for (int k = 0; k < f.nhpol; k++)  // magnetic polarizations
-    for (int d = 0; d < 3; d++) {
-      add(12, k, d, f.hpol[k].P[d], n);
-      add(13, k, d, f.hpol[k].Pp[d], n);
-    }
-  return v;
-}
-
-struct CkHeader {
-  char magic[8];
-  int32_t dim, n[3], io[3], nranks, rank, nentries;
-  uint64_t nlocal;
-  int64_t t;
-};
-
-CkHeader ckpt_header(mnl_fields *F, int nentries) {
-  CkHeader h{};
-  memcpy(h.magic, CK_MAGIC, 8);
-  h.dim = F->S.dim;
-  for (int d = 0; d < 3; d++) h.n[d] = F->S.n[d], h.io[d] = F->S.io[d];
-  h.nranks = F->nranks;
-  h.rank = F->rank;
-  h.nentries = nentries;
-  h.nlocal = F->nlocal;
-  h.t = F->t;
-  return h;
-}
-
-// a consistent unfused state: implicit E and the W aux fields materialised,
-// buffered DFT updates accumulated
-int ckpt_quiesce(mnl_fields *F) {
-  if (set_fused(F, false)) return -1;
-  for (auto &op : F->dfts)
-    if (dft_flush(F, *op)) return -1;
-  HIPCHK(hipStreamSynchronize(F->stream));
-  return 0;
-}
-
-int fields_dump(mnl_fields *F, const char *path) {
-  if (ckpt_quiesce(F)) return -1;
-  auto es = ckpt_entries(F);
-  FILE *fp = fopen(path, "wb");
-  if (!fp) return fail(std::string("cannot create fields output file ") + path);
-  std::unique_ptr<FILE, int (*)(FILE *)> guard(fp, fclose);
-  CkHeader h = ckpt_header(F, (int)es.size());
-  if (fwrite(&h, sizeof h, 1, fp) != 1) return fail("write error");
-  std::vector<double> buf;
-  for (auto &e : es) {
-    int32_t id[3] = {e.kind, e.a, e.b};
-    uint64_t n = e.n;
-    buf.resize(e.n);
-    HIPCHK(hipMemcpy(buf.data(), e.p, e.n * 8, hipMemcpyDeviceToHost));
-    if (fwrite(id, sizeof id, 1, fp) != 1 || fwrite(&n, 8, 1, fp) != 1 ||
-        fwrite(buf.data(), 8, e.n, fp) != e.n)
-      return fail("write error");
-  }
-  return 0;
-}
-
-int fields_load(mnl_fields *F, const char *path) {
-  if (F->src_dirty && build_source_lists(F)) return -1;
-  if (ckpt_quiesce(F)) return -1;
-  FILE *fp = fopen(path, "rb");
-  if (!fp) return fail(std::string("cannot open fields file ") + path);
-  std::unique_ptr<FILE, int (*)(FILE *)> guard(fp, fclose);
-  CkHeader h{};
-  if (fread(&h, sizeof h, 1, fp) != 1 || memcmp(h.magic, CK_MAGIC, 8))
-    return fail("not a fields checkpoint file");
-  auto es = ckpt_entries(F);
-  CkHeader me = ckpt_header(F, (int)es.size());
-  if (h.dim != me.dim || memcmp(h.n, me.n, sizeof h.n) || memcmp(h.io, me.io, sizeof h.io) ||
-      h.nranks != me.nranks || h.rank != me.rank || h.nlocal != me.nlocal)
-    return fail("fields file has a different grid or chunk layout");
-  // every field-state array must match; DFT accumulators are loaded into the
-  // flux objects that exist (same creation order), extra ones are skipped
-  size_t nfield = 0, matched = 0;
-  for (auto &e : es) nfield += e.kind != 11;
-  std::vector<double> buf;
-  for (int k = 0; k < h.nentries; k++) {
-    int32_t id[3];
-    uint64_t n;
-    if (fread(id, sizeof id, 1, fp) != 1 || fread(&n, 8, 1, fp) != 1) return fail("read error");
-    const CkEntry *dst = nullptr;
-    for (auto &e : es)
-      if (e.kind == id[0] && e.a == id[1] && e.b == id[2]) dst = &e;
-    if (!dst && id[0] != 11)
-      return fail("fields file does not match these fields (allocated arrays differ)");
-    if (dst && dst->n != n) return fail("fields file does not match these fields (array sizes differ)");
-    buf.resize(n);
-    if (fread(buf.data(), 8, n, fp) != n) return fail("read error (truncated file)");
-    if (!dst) continue;
-    HIPCHK(hipMemcpy(dst->p, buf.data(), n * 8, hipMemcpyHostToDevice));
-    matched += dst->kind != 11;
-  }
-  if (matched != nfield) return fail("fields file does not match these fields (allocated arrays differ)");
-  F->t = h.t;
-  // the loaded state comes from fields that were stepped: H and the W fields are
-  // already separate (a dump taken before the first step holds zeros in them)
-  F->e_first_done = F->h_first_done = true;
-  F->u_first_done[0] = F->u_first_done[1] = true;
-  return 0;
-}
-
-template <class T>
-void put(std::string &o, const T &v) {
-  o.append(reinterpret_cast<const char *>(&v), sizeof v);
-}
-void put_vec(std::string &o, const std::vector<double> &v) {
-  put(o, (uint64_t)v.size());
-  o.append(reinterpret_cast<const char *>(v.data()), v.size() * 8);
-}
-struct Rd {
-  const std::string &s;
-  size_t i = 0;
-  bool ok = true;
-  template <class T>
-  void get(T &v) {
-    if (i + sizeof v > s.size()) {
-      ok = false;
-      return;
-    }
-    memcpy(&v, s.data() + i, sizeof v);
-    i += sizeof v;
-  }
-  void get_vec(std::vector<double> &v) {
-    uint64_t n = 0;
-    get(n);
-    if (!ok || i + n * 8 > s.size()) {
-      ok = false;
-      return;
-    }
-    v.resize(n);
-    memcpy(v.data(), s.data() + i, n * 8);
-    i += n * 8;
-  }
-};
-
-int structure_dump(const mnl_structure *S, const char *path) {
-  std::string o(CS_MAGIC, 8);
-  put(o, S->dim);
-  for (int d = 0; d < 3; d++) put(o, S->n[d]), put(o, S->io[d]);
-  put(o, S->a), put(o, S->courant), put(o, S->nl_mode);
-  for (int d = 0; d < 3; d++)
-    for (int e = 0; e < 2; e++) put(o, S->pml_thick[d][e]), put(o, S->pml_R[d][e]), put(o, S->pml_stretch[d][e]);
-  for (int c = 0; c < 3; c++)
-    for (int d = 0; d < 3; d++) put_vec(o, S->chi1inv[c][d]);
-  for (int c = 0; c < 3; c++) put_vec(o, S->chi2[c]), put_vec(o, S->chi3[c]);
-  for (int t = 0; t < 2; t++)
-    for (int d = 0; d < 3; d++) put_vec(o, S->cond[t][d]);
-  put(o, (uint64_t)S->lor.size());
-  for (auto &L : S->lor) {
-    put(o, L.omega0), put(o, L.gamma), put(o, L.drude);
-    for (int d = 0; d < 3; d++) put_vec(o, L.sigma[d]);
-    for (int c = 0; c < 3; c++)
-      for (int d = 0; d < 3; d++) put_vec(o, L.off[c][d]);
-  }
-  put(o, (uint64_t)S->boxes.size());
-  for (auto &b : S->boxes) put(o, b);
-  bool hside = !S->hlor.empty();  // optional H-side section (absent in older files)
-  for (int c = 0; c < 3; c++)
-    for (int d = 0; d < 3; d++) hside = hside || !S->mu1inv[c][d].empty();
-  if (hside) {
-    put(o, (uint64_t)0x4853494445ull);  // "HSIDE"
-    for (int c = 0; c < 3; c++)
-      for (int d = 0; d < 3; d++) put_vec(o, S->mu1inv[c][d]);
-    put(o, (uint64_t)S->hlor.size());
-    for (auto &L : S->hlor) {
-      put(o, L.omega0), put(o, L.gamma), put(o, L.drude);
-      for (int d = 0; d < 3; d++) put_vec(o, L.sigma[d]);
-    }
-  }
-  FILE *fp = fopen(path, "wb");
-  if (!fp) return fail(std::string("cannot create structure output file ") + path);
-  size_t w = fwrite(o.data(), 1, o.size(), fp);
-  fclose(fp);
-  return w == o.size() ? 0 : fail("write error");
-}
-
-int structure_load(mnl_structure *S, const char *path) {
-  FILE *fp = fopen(path, "rb");
-  if (!fp) return fail(std::string("cannot open structure file ") + path);
-  std::string s;
-  char buf[1 << 16];
-  size_t r;
-  while ((r = fread(buf, 1, sizeof buf, fp)) > 0) s.append(buf, r);
-  fclose(fp);
-  if (s.size() < 8 || memcmp(s.data(), CS_MAGIC, 8)) return fail("not a structure file");
-  Rd in{s, 8};
-  int dim = 0, n[3] = {0, 0, 0}, io[3] = {0, 0, 0};
-  in.get(dim);
-  for (int d = 0; d < 3; d++) in.get(n[d]), in.get(io[d]);
-  double a = 0, courant = 0;
-  in.get(a), in.get(courant);
-  if (!in.ok || dim != S->dim || memcmp(n, S->n, sizeof n) || memcmp(io, S->io, sizeof io) ||
-      a != S->a || courant != S->courant)
-    return fail("structure file has a different grid volume");
-  mnl_structure T = *S;
-  in.get(T.nl_mode);
-  for (int d = 0; d < 3; d++)
-    for (int e = 0; e < 2; e++) in.get(T.pml_thick[d][e]), in.get(T.pml_R[d][e]), in.get(T.pml_stretch[d][e]);
-  for (int c = 0; c < 3; c++)
-    for (int d = 0; d < 3; d++) in.get_vec(T.chi1inv[c][d]);
-  for (int c = 0; c < 3; c++) in.get_vec(T.chi2[c]), in.get_vec(T.chi3[c]);
-  for (int t = 0; t < 2; t++)
-    for (int d = 0; d < 3; d++) in.get_vec(T.cond[t][d]);
-  uint64_t nl = 0;
-  in.get(nl);
-  T.lor.assign(in.ok && nl < 1024 ? nl : 0, Lorentz{});
-  for (auto &L : T.lor) {
-    in.get(L.omega0), in.get(L.gamma), in.get(L.drude);
-    for (int d = 0; d < 3; d++) in.get_vec(L.sigma[d]);
-    for (int c = 0; c < 3; c++)
-      for (int d = 0; d < 3; d++) in.get_vec(L.off[c][d]);
-  }
-  uint64_t nb = 0;
-  in.get(nb);
-  T.boxes.assign(in.ok && nb < (1u << 20) ? nb : 0, BoxSpec{});
-  for (auto &b : T.boxes) in.get(b);
-  for (int c = 0; c < 3; c++)
-    for (int d = 0; d < 3; d++) T.mu1inv[c][d].clear();
-  T.hlor.clear();
-  if (in.ok && in.i < s.size()) {  // H-side section
-    uint64_t tag = 0, nh = 0;
-    in.get(tag);
-    if (tag != 0x4853494445ull) in.ok = false;
-    for (int c = 0; c < 3; c++)
-      for (int d = 0; d < 3; d++) in.get_vec(T.mu1inv[c][d]);
-    in.get(nh);
-    T.hlor.assign(in.ok && nh <= (uint64_t)MAX_HPOL ? nh : 0, Lorentz{});
-    for (auto &L : T.hlor) {
-      in.get(L.omega0), in.get(L.gamma), in.get(L.drude);
-      for (int d = 0; d < 3; d++) in.get_vec(L.sigma[d]);
-    }
-  }
-  if (!in.ok || in.i != s.size()) return fail("structure file is truncated or corrupt");
-  bool sizes_ok = true;  // every per-point array is absent or whole-cell
-  auto chk = [&](const std::vector<double> &v) { sizes_ok = sizes_ok && (v.empty() || v.size() == T.ntot); };
-  for (int c = 0; c < 3; c++) {
-    for (int d = 0; d < 3; d++) chk(T.chi1inv[c][d]);
-    chk(T.chi2[c]), chk(T.chi3[c]);
-  }
-  for (int t = 0; t < 2; t++)
-    for (int d = 0; d < 3; d++) chk(T.cond[t][d]);
-  for (auto &L : T.lor) {
-    for (int d = 0; d < 3; d++) chk(L.sigma[d]);
-    for (int c = 0; c < 3; c++)
-      for (int d = 0; d < 3; d++) chk(L.off[c][d]);
-  }
-  for (int c = 0; c < 3; c++)
-    for (int d = 0; d < 3; d++) chk(T.mu1inv[c][d]);
-  for (auto &L : T.hlor)
-    for (int d = 0; d < 3; d++) chk(L.sigma[d]);
-  if (!sizes_ok) return fail("structure file holds an array of the wrong size");
-  *S = std::move(T);
-  return 0;
-}
-
-// ------------------------------------------------------------- array slices
-// H-side materials: H_d separate in the reference chunk holding the point at absolute
-// half-coordinates p (not counting PML along d; DevFields::hsep_zone / hsep_all)
-bool h_sep_zone(const mnl_fields *F, const int p[3], int d) {
-  if (!F->hall || !F->h_first_done) return false;
-  if (F->f.hsep_all) return true;
-  int zb = 0;
-  for (int e = 0; e < 3; e++)
-    zb = zb * 3 + (F->S.has[e] ? F->h_zone[e][p[e] - F->S.io[e]] : 1);
-  return (F->h_hsep_zone[zb] >> d) & 1;
-}
-
-// fields::get_array_slice(volume, c) for real fields without symmetry
-// (src/array_slice.cpp:251-433, 447-507, 525-601, 611-704): loop_in_chunks over
-// the Centered grid in the reference's chunks, each point the average of the
-// component's four Yee neighbours (yee2cent_offsets, src/vec.cpp:333-344)
-// times the interpolation weights of the empty dimensions only
-// (IVEC_LOOP_WEIGHT with s0i..e1i, src/meep/vec.hpp:372-383), then the empty
-// dimensions collapsed by summation (collapse_array, snap = false).  Host-side
-// from the whole-cell component array, as the reference's CPU loop.
-inline double loop_w1(double s0, double s1, double e0, double e1, int i, int n) {
-  return (i > 1 && i < n - 2) ? 1.0 : (i == 0 ? s0 : (i == 1 ? s1 : i == n - 1 ? e0 : (i == n - 2 ? e1 : 1.0)));
-}
-
-// This rank's entries of component c inside the whole-cell index box lo..hi
-// (global indices per direction) into out (strides hs, zero elsewhere).
-int copy_component_box(mnl_fields *F, int c, const int lo[3], const int hi[3],
-                       const long long hs[3], double *out) {
-  const mnl_structure &S = F->S;
-  long long n = 1;
-  for (int d = 0; d < 3; d++)
-    if (S.has[d]) n *= hi[d] - lo[d] + 1;
-  if (n <= 0) return 0;
-  memset(out, 0, (size_t)n * sizeof(double));
-  if (!has_field(S, c) || !F->allocated[c]) return 0;
-  const int t = ctype(c), d = cdir(c);
-  const double *src = t == T_E ? F->f.E[d] : t == T_D ? F->f.D[d] : F->f.B[d];
-  const double *hsep = (t == T_H && !(F->hall && !F->h_first_done)) ? F->f.H[d] : nullptr;
-  if (!src) return 0;
-  if (hipSetDevice(F->device) != hipSuccess) return fail("hipSetDevice failed");
-  double *buf = nullptr;
-  HIPCHK(hipMalloc(&buf, (size_t)n * sizeof(double)));
-  std::unique_ptr<void, void (*)(void *)> guard(buf, [](void *p) { (void)hipFree(p); });
-  HIPCHK(hipMemsetAsync(buf, 0, (size_t)n * sizeof(double), F->stream));
-  const bool fe = F->fused && t == T_E;
-  if (k_to_box(buf, src, hsep, F->g, t, d, F->f, fe ? &F->fusedG : nullptr, fe ? F->f.D[d] : nullptr,
-               fe ? F->f.inveps[d] : nullptr, lo, hi, hs, F->stream))
-    return fail("to_box launch failed");
-  HIPCHK(hipMemcpyAsync(out, buf, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, F->stream));
-  HIPCHK(hipStreamSynchronize(F->stream));
-  return 0;
-}
-
-// Diagonal chi1inv of E (t = T_E, epsilon) or H (mu) component k at global index j, as
-// structure_chunk::get_chi1inv_at_pt returns it (src/structure.cpp; 1 where the row is
-// absent or was deleted as trivial): the host arrays, then the epsilon boxes rasterised
-// exactly as box_fill_kernel does (later boxes win).
-double mat_diag_at(const mnl_structure &S, int t, int k, const int j[3]) {
-  const auto &v = t == T_E ? S.chi1inv[k][k] : S.mu1inv[k][k];
-  long long idx = 0;
-  for (int d = 0; d < 3; d++) idx += (long long)j[d] * S.cstride(d);
-  double val = v.empty() ? 1.0 : v[idx];
-  if (t == T_E)
-    for (const BoxSpec &b : S.boxes) {
-      if (b.kind != 0) continue;
-      bool in = true;
-      for (int d = 0; d < 3 && in; d++) {
-        if (!S.has[d]) continue;
-        const double pos = (S.io[d] + 2 * j[d] + S.shift(k, d)) * (0.5 * (1.0 / S.a));
-        in = !(pos < b.box[2 * d] || pos > b.box[2 * d + 1]);
-      }
-      if (in) val = 1.0 / b.value;
-    }
-  return val;
-}
-
-int array_slice(mnl_fields *F, int c, const double vmin[3], const double vmax[3], int snap,
-                int *rank, long long dims[3], double *out, long long nout) {
-  const mnl_structure &S = F->S;
-  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
-  for (int d = 0; d < 3; d++) {
-    if (!S.has[d]) continue;
-    is[d] = 1 + 2 * int(floor(vmin[d] * S.a - .5));
-    ie[d] = 1 + 2 * int(ceil(vmax[d] * S.a - .5));
-  }
-  double s0[3], s1[3], e0[3], e1[3];
-  dft_boundary_weights(S, vmin, vmax, is, ie, s0, e0, s1, e1);
-  if (snap)  // snap_empty_dimensions (src/loop_in_chunks.cpp:275-287): nearest point, weight 1
-    for (int d = 0; d < 3; d++) {
-      if (!S.has[d] || vmin[d] != vmax[d] || ie[d] >= is[d] + 4) continue;
-      const double w0 = 1. - vmin[d] * S.a + 0.5 * is[d], w1 = 1. + vmax[d] * S.a - 0.5 * ie[d];
-      if (w0 > w1)
-        ie[d] = is[d];
-      else
-        is[d] = ie[d];
-      s0[d] = s1[d] = e0[d] = e1[d] = 1.0;
-    }
-  struct Lp {
-    int is[3], ie[3];
-    double s0[3], s1[3], e0[3], e1[3];
-  };
-  std::vector<Lp> loops;
-  for (auto &ch : reference_chunks(S)) {
-    Lp L;
-    bool emp = false;
-    for (int d = 0; d < 3; d++) {
-      L.s0[d] = L.s1[d] = L.e0[d] = L.e1[d] = 1.0;
-      if (!S.has[d]) {
-        L.is[d] = L.ie[d] = 0;
-        continue;
-      }
-      const int uoc = S.io[d] + 1, coc = ch[d] + 1, cbo = ch[d] + 2 * ch[3 + d] - 1;
-      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
-      L.is[d] = std::max(is[d], iscoS);
-      L.ie[d] = std::min(ie[d], iecoS);
-      if (L.is[d] > L.ie[d]) emp = true;
-    }
-    if (emp) continue;
-    for (int d = 0; d < 3; d++) {  // per-chunk weights (loop_in_chunks.cpp:430-470)
-      if (!S.has[d]) continue;
-      if (L.is[d] == is[d]) {
-        L.s0[d] = s0[d];
-        L.s1[d] = s1[d];
-      } else if (L.is[d] == is[d] + 2) {
-        L.s0[d] = s1[d];
-      }
-      if (L.ie[d] == ie[d]) {
-        L.e0[d] = e0[d];
-        L.e1[d] = e1[d];
-      } else if (L.ie[d] == ie[d] - 2) {
-        L.e0[d] = e1[d];
-      }
-      if (L.ie[d] == L.is[d]) {
-        double w = std::min(L.s0[d], L.e0[d]);
-        L.s0[d] = L.e0[d] = L.s1[d] = L.e1[d] = w;
-      } else if (L.ie[d] == L.is[d] + 2) {
-        double w = std::min(L.s0[d], L.e1[d]);
-        L.s0[d] = w, L.e1[d] = w;
-        w = std::min(L.s1[d], L.e0[d]);
-        L.s1[d] = w, L.e0[d] = w;
-      } else if (L.ie[d] == L.is[d] + 4) {
-        double w = std::min(L.s1[d], L.e1[d]);
-        L.s1[d] = w, L.e1[d] = w;
-      }
-    }
-    loops.push_back(L);
-  }
-  // get_array_slice_dimensions: corners over all chunks, directions with n > 1
-  int mn[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, mx[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
-  for (auto &L : loops)
-    for (int d = 0; d < 3; d++) mn[d] = std::min(mn[d], L.is[d]), mx[d] = std::max(mx[d], L.ie[d]);
-  int r = 0, ds[3] = {0, 0, 0};
-  long long full[3] = {1, 1, 1};
-  if (!loops.empty())
-    for (int d = 0; d < 3; d++) {
-      if (!S.has[d]) continue;
-      long long n = (mx[d] - mn[d]) / 2 + 1;
-      if (n > 1) ds[r] = d, full[r++] = n;
-    }
-  int rr = 0;
-  long long rd[3] = {1, 1, 1};
-  for (int k = 0; k < r; k++)
-    if (vmax[ds[k]] - vmin[ds[k]] != 0.0) rd[rr++] = full[k];
-  *rank = rr;
-  for (int k = 0; k < 3; k++) dims[k] = k < rr ? rd[k] : 1;
-  if (!out) return 0;
-  long long rs[3] = {0, 0, 0}, nred = 1;
-  for (int k = r - 1; k >= 0; k--)
-    if (vmax[ds[k]] - vmin[ds[k]] != 0.0) rs[k] = nred, nred *= full[k];
-  if (nout < nred) return fail("output buffer too small");
-  for (long long k = 0; k < nred; k++) out[k] = 0.0;
-  if (loops.empty()) return 0;
-  long long ntot = 1;
-  for (int k = 0; k < r; k++) ntot *= full[k];
-  std::vector<double> arr(ntot, 0.0);
-  if (c == MNL_DIELECTRIC || c == MNL_PERMEABILITY) {
-    // Dielectric / Permeability (src/array_slice.cpp:385-408, 649-676): per centred point
-    // (4 n) / sum over the n E (H) components of the grid of the four diagonal chi1inv
-    // values at the component's yee2cent points, times the empty-dimension weights;
-    // from the host structure every rank holds (no device access, no collective)
-    const int t = c == MNL_DIELECTRIC ? T_E : T_H;
-    std::vector<int> ks;
-    for (int k = 0; k < 3; k++)
-      if (has_field(S, 3 * t + k)) ks.push_back(k);
-    bool empty_dim[3];
-    for (int d = 0; d < 3; d++) empty_dim[d] = S.has[d] && vmax[d] - vmin[d] == 0.0;
-    const int yd[3] = {S.dim == 2 ? 2 : 0, S.dim == 2 ? 0 : 1, S.dim == 2 ? 1 : 2};
-    for (auto &L : loops) {
-      int n[3];
-      for (int k = 0; k < 3; k++) n[k] = S.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
-      for (int i1 = 0; i1 < n[0]; i1++)
-        for (int i2 = 0; i2 < n[1]; i2++)
-          for (int i3 = 0; i3 < n[2]; i3++) {
-            const int ii[3] = {i1, i2, i3};
-            int p[3] = {0, 0, 0};
-            for (int k = 0; k < 3; k++)
-              if (S.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
-            double w[3];
-            for (int k = 0; k < 3; k++) {
-              const int d = yd[k];
-              w[k] = empty_dim[d] ? loop_w1(L.s0[d], L.s1[d], L.e0[d], L.e1[d], ii[k], n[k])
-                                  : loop_w1(1.0, 1.0, 1.0, 1.0, ii[k], n[k]);
-            }
-            const double wt = w[2] * (w[1] * (1.0 * w[0]));
-            cplx tr(0.0, 0.0);
-            for (int k : ks) {
-              const int ck = 3 * t + k;
-              int j0[3] = {0, 0, 0}, o[2] = {-1, -1}, no = 0;
-              for (int d = 0; d < 3; d++)
-                if (S.has[d]) {
-                  j0[d] = (p[d] - S.io[d]) / 2;
-                  if (!S.shift(ck, d)) o[no++] = d;
-                }
-              double v[4];
-              for (int q = 0; q < 4; q++) {
-                int jq[3] = {j0[0], j0[1], j0[2]};
-                if ((q & 1) && o[0] >= 0) jq[o[0]]++;
-                if ((q & 2) && o[1] >= 0) jq[o[1]]++;
-                v[q] = mat_diag_at(S, t, k, jq);
-              }
-              tr += v[0] + v[1] + v[2] + v[3];
-              if (std::abs(tr) == 0.0) tr += 4.0;
-            }
-            const cplx val = wt * (4.0 * (double)ks.size()) / tr;
-            long long oi = 0;
-            for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
-            arr[oi] = real(val);
-          }
-    }
-    for (long long q = 0; q < ntot; q++) {  // collapse_array: in full-index order
-      long long tq = q, ri = 0;
-      for (int k = r - 1; k >= 0; k--) {
-        ri += (tq % full[k]) * rs[k];
-        tq /= full[k];
-      }
-      out[ri] += arr[q];
-    }
-    return 0;
-  }
-  // c's global indices the slice reads: the base point of each centred point
-  // and +1 along c's unshifted directions (the four Yee values, o1 / o2)
-  bool unsh[3];
-  int blo[3] = {0, 0, 0}, bhi[3] = {0, 0, 0};
-  for (int d = 0; d < 3; d++) {
-    unsh[d] = S.has[d] && !S.shift(c, d);
-    if (!S.has[d]) continue;
-    blo[d] = (mn[d] - S.io[d]) / 2;
-    bhi[d] = (mx[d] - S.io[d]) / 2 + (unsh[d] ? 1 : 0);
-  }
-  // Distributed: this rank forms the points whose base value it owns along the
-  // slab axis (one owner each), reading its own entries of the box plus, for
-  // components unshifted along that axis, the next rank's first owned plane;
-  // the finished slice is then summed over ranks (every entry has one
-  // contributor, so the sums are exact).  No whole-cell buffers on any rank.
-  const bool dist = F->nranks > 1;
-  const int sd = F->slab_dir;
-  int rlo = 0, rhi = S.n[sd];  // base indices along sd this rank forms
-  if (dist) {
-    const int lo_cell = F->g.off[sd], hi_cell = lo_cell + F->g.N[F->g.ax[sd]] - 1;
-    if (S.shift(c, sd)) {
-      rlo = lo_cell;
-      rhi = F->rank == F->nranks - 1 ? S.n[sd] : hi_cell - 1;
-    } else {
-      rlo = F->rank == 0 ? 0 : lo_cell + 1;
-      rhi = hi_cell;
-    }
-  }
-  int hlo[3], hhi[3];  // this rank's box of values
-  for (int d = 0; d < 3; d++) hlo[d] = blo[d], hhi[d] = bhi[d];
-  hlo[sd] = std::max(blo[sd], rlo);
-  hhi[sd] = std::min(bhi[sd], rhi + (unsh[sd] ? 1 : 0));
-  long long hs[3] = {0, 0, 0}, hn = 1;  // slab axis slowest: a plane of it is contiguous
-  for (int d = 2; d >= 0; d--)
-    if (S.has[d] && d != sd) {
-      hs[d] = hn;
-      hn *= std::max(0, hhi[d] - hlo[d] + 1);
-    }
-  hs[sd] = hn;
-  hn *= std::max(0, hhi[sd] - hlo[sd] + 1);
-  // B components: a reference chunk without PML along c aliases B to H, so its
-  // ghost copy of a neighbour chunk's point holds that chunk's H (the H
-  // exchange writes through the alias, src/boundaries.cpp:347-460) -- hbh keeps
-  // the H values for those reads
-  const bool bq = ctype(c) == T_B;
-  std::vector<double> hb, hbh;
-  bool ok = true;
-  std::string why;
-  if (hn > 0) {
-    hb.assign(hn, 0.0);
-    if (copy_component_box(F, c, hlo, hhi, hs, hb.data())) ok = false, why = g_err;
-    if (bq && ok) {
-      hbh.assign(hn, 0.0);
-      if (copy_component_box(F, 3 * T_H + cdir(c), hlo, hhi, hs, hbh.data()))
-        ok = false, why = g_err;
-    }
-  }
-  if (dist) {
-    if (F->comm->agree_ok(ok, F->stream)) return fail(ok ? "array slice: a rank failed" : why);
-    if (unsh[sd]) {  // the plane above this rank's last base index comes from the next rank
-      long long pn = 1;
-      for (int d = 0; d < 3; d++)
-        if (S.has[d] && d != sd) pn *= bhi[d] - blo[d] + 1;
-      const int nv = bq ? 2 : 1;  // B: the H plane too
-      std::vector<double> xp((size_t)pn * F->nranks * nv, 0.0);
-      const int first = F->g.off[sd] + 1;  // first owned plane (unshifted along sd)
-      if (F->rank > 0 && hn > 0 && first >= hlo[sd] && first <= hhi[sd])
-        for (int v = 0; v < nv; v++)
-          for (long long q = 0; q < pn; q++)
-            xp[((size_t)F->rank * nv + v) * pn + q] =
-                (v ? hbh : hb)[(size_t)(first - hlo[sd]) * hs[sd] + q];
-      for (size_t q = 0; q < xp.size(); q += 1 << 20) {
-        const int n = (int)std::min<size_t>(1 << 20, xp.size() - q);
-        if (timed_allreduce(F, xp.data() + q, n)) return fail("slice allreduce failed");
-      }
-      const int top = rhi + 1;
-      if (F->rank + 1 < F->nranks && hn > 0 && top >= hlo[sd] && top <= hhi[sd])
-        for (int v = 0; v < nv; v++)
-          for (long long q = 0; q < pn; q++)
-            (v ? hbh : hb)[(size_t)(top - hlo[sd]) * hs[sd] + q] =
-                xp[((size_t)(F->rank + 1) * nv + v) * pn + q];
-    }
-  } else if (!ok) {
-    return -1;
-  }
-  long long o1 = 0, o2 = 0;  // offsets of the unshifted neighbours in hb
-  int d1 = -1, d2 = -1;      // and their directions
-  for (int d = 0; d < 3; d++)
-    if (unsh[d]) {
-      if (o1)
-        o2 = hs[d], d2 = d;
-      else
-        o1 = hs[d], d1 = d;
-    }
-  const int cd = cdir(c);
-  bool empty_dim[3];
-  for (int d = 0; d < 3; d++) empty_dim[d] = S.has[d] && vmax[d] - vmin[d] == 0.0;
-  const int yd[3] = {S.dim == 2 ? 2 : 0, S.dim == 2 ? 0 : 1, S.dim == 2 ? 1 : 2};
-  for (auto &L : loops) {
-    int n[3];
-    for (int k = 0; k < 3; k++) n[k] = S.has[yd[k]] ? (L.ie[yd[k]] - L.is[yd[k]]) / 2 + 1 : 1;
-    for (int i1 = 0; i1 < n[0]; i1++)
-      for (int i2 = 0; i2 < n[1]; i2++)
-        for (int i3 = 0; i3 < n[2]; i3++) {
-          const int ii[3] = {i1, i2, i3};
-          int p[3] = {0, 0, 0};
-          for (int k = 0; k < 3; k++)
-            if (S.has[yd[k]]) p[yd[k]] = L.is[yd[k]] + 2 * ii[k];
-          const int jb = S.has[sd] ? (p[sd] - S.io[sd]) / 2 : 0;
-          if (jb < rlo || jb > rhi) continue;  // another rank forms this point
-          double w[3];
-          for (int k = 0; k < 3; k++) {
-            const int d = yd[k];
-            w[k] = empty_dim[d] ? loop_w1(L.s0[d], L.s1[d], L.e0[d], L.e1[d], ii[k], n[k])
-                                : loop_w1(1.0, 1.0, 1.0, 1.0, ii[k], n[k]);
-          }
-          const double wt = w[2] * (w[1] * (1.0 * w[0]));
-          long long idx = 0;
-          int jb3[3] = {0, 0, 0};
-          for (int d = 0; d < 3; d++)
-            if (S.has[d]) {
-              jb3[d] = (p[d] - S.io[d]) / 2;
-              idx += (long long)(jb3[d] - hlo[d]) * hs[d];
-            }
-          double a4[4] = {hb[idx], hb[idx + o1], hb[idx + o2], hb[idx + o1 + o2]};
-          if (bq && F->h_zone[cd][p[cd] - S.io[cd]] == 1 && !h_sep_zone(F, p, cd)) {  // reader chunk aliases B to H
-            for (int k = 0; k < 4; k++) {
-              int jn[3] = {jb3[0], jb3[1], jb3[2]};
-              if ((k & 1) && d1 >= 0) jn[d1]++;
-              if ((k & 2) && d2 >= 0) jn[d2]++;
-              bool other = false;  // owned by another reference chunk
-              for (int d = 0; d < 3; d++)
-                if (S.has[d])
-                  other = other || F->h_zone[d][2 * jn[d] + S.shift(c, d)] !=
-                                       F->h_zone[d][p[d] - S.io[d]];
-              if (other) a4[k] = hbh[idx + ((k & 1) ? o1 : 0) + ((k & 2) ? o2 : 0)];
-            }
-          }
-          const double avg = 0.25 * (a4[0] + a4[1] + a4[2] + a4[3]);
-          const cplx v = wt * cplx(avg, 0.0) * cplx(1.0, 0.0);
-          long long oi = 0;
-          for (int k = 0; k < r; k++) oi = oi * full[k] + (p[ds[k]] - mn[ds[k]]) / 2;
-          arr[oi] = real(v);
-        }
-  }
-  if (dist)
-    for (size_t q = 0; q < arr.size(); q += 1 << 20) {
-      const int n = (int)std::min<size_t>(1 << 20, arr.size() - q);
-      if (timed_allreduce(F, arr.data() + q, n)) return fail("slice allreduce failed");
-    }
-  for (long long q = 0; q < ntot; q++) {  // collapse_array: in full-index order
-    long long t = q, ri = 0;
-    for (int k = r - 1; k >= 0; k--) {
-      ri += (t % full[k]) * rs[k];
-      t /= full[k];
-    }
-    out[ri] += arr[q];
-  }
-  return 0;
-}
-
-// ------------------------------------------------------------- field energy
-// loop_in_chunks(where, cgrid = component c) (src/loop_in_chunks.cpp:325-520,
-// no symmetry / Bloch): the reference chunks' boxes on c's Yee grid with their
-// boundary weights, restricted to the points this rank owns; weights tabulated
-// per device axis into wtab.
-std::vector<EBox> energy_boxes(mnl_fields *F, int c, const double wmin[3], const double wmax[3],
-                               std::vector<double> &wtab) {
-  const mnl_structure &S = F->S;
-  const DevGrid &g = F->g;
-  int is[3] = {0, 0, 0}, ie[3] = {0, 0, 0};
-  for (int d = 0; d < 3; d++) {
-    if (!S.has[d]) continue;
-    const int iyc = 1 - S.shift(c, d);        // iyee_shift(Centered) - iyee_shift(c)
-    const double yc = iyc * (0.5 / S.a);      // yee_shift(Centered) - yee_shift(c)
-    is[d] = 1 + 2 * int(floor((wmin[d] + yc) * S.a - .5)) - iyc;  // vec2diel_floor - iyee_c
-    ie[d] = 1 + 2 * int(ceil((wmax[d] + yc) * S.a - .5)) - iyc;
-  }
-  double s0[3], s1[3], e0[3], e1[3];
-  dft_boundary_weights(S, wmin, wmax, is, ie, s0, e0, s1, e1);
-  double dV0 = 1.0;
-  for (int d = 0; d < 3; d++)
-    if (S.has[d] && wmax[d] - wmin[d] > 0.0) dV0 *= 1.0 / S.a;
-  int yd[3];
-  if (S.dim == 2)
-    yd[0] = 2, yd[1] = 0, yd[2] = 1;
-  else
-    yd[0] = 0, yd[1] = 1, yd[2] = 2;
-  std::vector<EBox> out;
-  for (auto &ch : reference_chunks(S)) {
-    int isc[3], iec[3];
-    double s0c[3], s1c[3], e0c[3], e1c[3];
-    bool emp = false;
-    for (int d = 0; d < 3; d++) {
-      s0c[d] = s1c[d] = e0c[d] = e1c[d] = 1.0;
-      if (!S.has[d]) {
-        isc[d] = iec[d] = 0;
-        continue;
-      }
-      const int sh = S.shift(c, d);
-      const int uoc = S.io[d] + 2 - sh, coc = ch[d] + 2 - sh, cbo = ch[d] + 2 * ch[3 + d] - sh;
-      const int iscoS = std::max(uoc, std::min(coc, cbo)), iecoS = std::max(coc, cbo);
-      isc[d] = std::max(is[d], iscoS);
-      iec[d] = std::min(ie[d], iecoS);
-      if (isc[d] > iec[d]) emp = true;
-    }
-    if (emp) continue;
-    for (int d = 0; d < 3; d++) {
-      if (!S.has[d]) continue;
-      if (isc[d] == is[d]) {
-        s0c[d] = s0[d];
-        s1c[d] = s1[d];
-      } else if (isc[d] == is[d] + 2) {
-        s0c[d] = s1[d];
-      }
-      if (iec[d] == ie[d]) {
-        e0c[d] = e0[d];
-        e1c[d] = e1[d];
-      } else if (iec[d] == ie[d] - 2) {
-        e0c[d] = e1[d];
-      }
-      if (iec[d] == isc[d]) {
-        double w = std::min(s0c[d], e0c[d]);
-        s0c[d] = e0c[d] = s1c[d] = e1c[d] = w;
-      } else if (iec[d] == isc[d] + 2) {
-        double w = std::min(s0c[d], e1c[d]);
-        s0c[d] = w, e1c[d] = w;
-        w = std::min(s1c[d], e0c[d]);
-        s1c[d] = w, e0c[d] = w;
-      } else if (iec[d] == isc[d] + 4) {
-        double w = std::min(s1c[d], e1c[d]);
-        s1c[d] = w, e1c[d] = w;
-      }
-    }
-    EBox b;
-    bool none = false;
-    for (int k = 0; k < 3; k++) b.dlo[k] = 0, b.dn[k] = 1, b.wofs[k] = 0, b.yd[k] = yd[k];
-    b.dV0 = dV0 + 0.0 * 0;  // dV0 + dV1 * loop_i2 with dV1 = 0
-    for (int d = 0; d < 3; d++) {
-      if (!S.has[d]) continue;
-      const int ax = g.ax[d], sh = S.shift(c, d);
-      const long nl = (iec[d] - isc[d]) / 2 + 1;           // chunk loop count
-      const int j0 = (isc[d] - S.io[d] - sh) / 2 - g.off[d];  // local index of loop point 0
-      const int lo_own = sh ? g.owned_lo_sh[d] : g.owned_lo_un[d];
-      const int hi_own = sh ? g.owned_hi_sh[d] : g.owned_hi_un[d];
-      int a = std::max(0, lo_own - j0), z = std::min<long>(nl - 1, hi_own - j0);
-      if (z < a) {
-        none = true;
-        break;
-      }
-      b.dlo[ax] = j0 + a;
-      b.dn[ax] = z - a + 1;
-      b.wofs[ax] = (long long)wtab.size();
-      for (long i = a; i <= z; i++) {
-        double w = 1.0;
-        if (!(i > 1 && i < nl - 2))
-          w = i == 0 ? s0c[d] : (i == 1 ? s1c[d] : i == nl - 1 ? e0c[d] : (i == nl - 2 ? e1c[d] : 1.0));
-        wtab.push_back(w);
-      }
-    }
-    if (!none) out.push_back(b);
-    else out.push_back(EBox{{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {yd[0], yd[1], yd[2]}, dV0});
-  }
-  return out;
-}
-
-// real(integrate(2, {A, B}, dot_integrand, where)) over component c's grid:
-// per reference chunk a device sum (rounded to double, as the reference adds
-// each chunk's long-double sum into a complex<double>), chunks added in order,
-// then summed over ranks (sum_to_all)
-int integrate_pair(mnl_fields *F, int c, const double *A, const double *Asep, const double *Bv,
-                   const double wmin[3], const double wmax[3], double *out) {
-  std::vector<double> wtab;
-  auto boxes = energy_boxes(F, c, wmin, wmax, wtab);
-  std::vector<double> chunk(boxes.size(), 0.0);
-  // the local part; a failure is agreed on before the collective so that every
-  // rank returns instead of waiting in the allreduce
-  const int lrc = [&]() -> int {
-    const int NB = 256;
-    double *dw = nullptr, *dp = nullptr;
-    HIPCHK(hipMalloc(&dw, std::max<size_t>(wtab.size(), 1) * 8));
-    std::unique_ptr<void, void (*)(void *)> g1(dw, [](void *p) { (void)hipFree(p); });
-    HIPCHK(hipMalloc(&dp, 2 * NB * 8));
-    std::unique_ptr<void, void (*)(void *)> g2(dp, [](void *p) { (void)hipFree(p); });
-    if (!wtab.empty())
-      HIPCHK(hipMemcpyAsync(dw, wtab.data(), wtab.size() * 8, hipMemcpyHostToDevice, F->stream));
-    std::vector<double> part(2 * NB);
-    for (size_t k = 0; k < boxes.size(); k++) {
-      const EBox &b = boxes[k];
-      const long long n = (long long)b.dn[0] * b.dn[1] * b.dn[2];
-      if (n == 0 || !A || !Bv) continue;
-      const int nb = (int)std::min<long long>(NB, (n + 255) / 256);
-      if (k_energy(A, Asep, Bv, F->g, F->f, ctype(c), cdir(c), b, dw, dp, nb, F->stream))
-        return fail("energy kernel launch failed");
-      HIPCHK(hipMemcpyAsync(part.data(), dp, 2 * nb * 8, hipMemcpyDeviceToHost, F->stream));
-      HIPCHK(hipStreamSynchronize(F->stream));
-      long double acc = 0.0L;
-      for (int i = 0; i < nb; i++) acc += (long double)part[2 * i] + (long double)part[2 * i + 1];
-      chunk[k] = (double)acc;
-    }
-    return 0;
-  }();
-  if (F->nranks > 1) {
-    const std::string why = g_err;
-    if (F->comm->agree_ok(lrc == 0, F->stream)) return fail(lrc ? why : "energy: a rank failed");
-    if (timed_allreduce(F, chunk.data(), (int)chunk.size()))
-      return fail("energy allreduce failed");
-  } else if (lrc) {
-    return -1;
-  }
-  double sum = 0.0;
-  for (double v : chunk) sum += v;
-  *out = sum;
-  return 0;
-}
-
-// fields::field_energy_in_box(c, where) for every E (or H) component, summed
-// in long double (electric_energy_in_box / magnetic_energy_in_box,
-// src/energy_and_flux.cpp:85-95)
-int energy_of_type(mnl_fields *F, int t, const double wmin[3], const double wmax[3], double *out) {
-  long double sum = 0.0L;
-  const DevFields &f = F->f;
-  for (int d = 0; d < 3; d++) {
-    const int c = 3 * t + d;
-    if (!has_field(F->S, c)) continue;
-    double v = 0.0;
-    if (t == T_E) {
-      if (!F->allocated[c] || !F->allocated[3 * T_D + d]) continue;
-      if (integrate_pair(F, c, f.E[d], nullptr, f.D[d], wmin, wmax, &v)) return -1;
-    } else {
-      if (!F->allocated[3 * T_B + d]) continue;
-      const double *hsep = (F->h_first_done && f.H[d]) ? f.H[d] : nullptr;
-      if (integrate_pair(F, c, f.B[d], hsep, f.B[d], wmin, wmax, &v)) return -1;
-    }
-    sum += v * 0.5;
-  }
-  *out = (double)sum;
-  return 0;
-}
-
-// synchronize_magnetic_fields (src/energy_and_flux.cpp:146-167): back up B / H
-// (and f_u, f_w, f_cond where they exist), take one B half step (step_db(B),
-// B sources at time(), step_boundaries, update_eh(H)), average B and H with the
-// backups; restore_magnetic_fields (169-178) copies the backups back.
-struct MagBackup {
-  std::vector<std::pair<double *, double *>> items;  // (field array, backup)
-  std::vector<std::pair<double *, double *>> avg;    // averaged with backup
-  ~MagBackup() {
-    for (auto &it : items) (void)hipFree(it.second);
-  }
-};
-
-int sync_magnetic(mnl_fields *F, MagBackup &bk) {
-  if (F->src_dirty && build_source_lists(F)) return -1;
-  if (F->fused && set_fused(F, false)) return -1;
-  DevFields &f = F->f;
-  const size_t n = F->nlocal;
-  auto save = [&](double *p, bool average) -> int {
-    if (!p) return 0;
-    double *b = nullptr;
-    HIPCHK(hipMalloc(&b, n * 8));
-    HIPCHK(hipMemcpyAsync(b, p, n * 8, hipMemcpyDeviceToDevice, F->stream));
-    bk.items.push_back({p, b});
-    if (average) bk.avg.push_back({p, b});
-    return 0;
-  };
-  const bool have_u = F->u_first_done[0], have_h = F->h_first_done;
-  for (int d = 0; d < 3; d++) {
-    if (!F->allocated[3 * T_B + d]) continue;
-    if (save(f.B[d], true)) return -1;
-    if (have_u && (save(f.UB[d], false) || save(f.fcnd[0][d], false))) return -1;
-    if (have_h && (save(f.H[d], true) || save(f.WH[d], false))) return -1;
-  }
-  // one B step at time(): step_db(B) + step_source(B) + step_boundaries(B) +
-  // update_eh(H) + step_boundaries(H)
-  if (F->nranks > 1 && exchange(F, 0)) return fail("E halo exchange failed");
-  if (!F->u_first_done[0] && u_lazy_copy(F, 0)) return -1;
-  const DevGrid &g = F->g;
-  if (k_curl(T_B, F->interior, nullptr, g, f, F->planB, F->S.courant, F->stream) ||
-      k_curl(T_B, F->interior, &F->shell_list, g, f, F->planB, F->S.courant, F->stream, false))
-    return fail("curl B launch failed");
-  const size_t nB = F->srcB_idx.size();
-  if (nB) {  // calc_sources(time()) + step_source(B_stuff)
-    const double dt = F->dt, time = F->t * dt;
-    for (auto &st : F->srcs) st.update(time, dt);
-    const size_t ng = F->groups.size();
-    std::vector<double> J(2 * ng);
-    for (size_t g2 = 0; g2 < ng; g2++) {
-      const cplx v = F->srcs[F->groups[g2].st].cur_current;
-      J[2 * g2] = real(v), J[2 * g2 + 1] = imag(v);
-    }
-    double *dv = nullptr;
-    HIPCHK(hipMalloc(&dv, J.size() * 8));
-    std::unique_ptr<void, void (*)(void *)> gv(dv, [](void *p) { (void)hipFree(p); });
-    HIPCHK(hipMemcpyAsync(dv, J.data(), J.size() * 8, hipMemcpyHostToDevice, F->stream));
-    if (k_source(T_B, g, f, src_dev(F, 0, dv), 0, F->stream)) return fail("source launch failed");
-    HIPCHK(hipStreamSynchronize(F->stream));
-  }
-  if (!F->h_first_done && h_lazy_copy(F)) return -1;
-  if (update_h_any(F, F->shell_list, false)) return -1;  // no update_pols here (reference)
-  if (F->nranks > 1 && exchange(F, 1)) return fail("H halo exchange failed");
-  for (auto &a : bk.avg)
-    if (k_average(a.first, a.second, (long long)n, F->stream)) return fail("average launch failed");
-  HIPCHK(hipStreamSynchronize(F->stream));
-  return 0;
-}
-
-int restore_magnetic(mnl_fields *F, MagBackup &bk) {
-  for (auto &it : bk.items)
-    HIPCHK(hipMemcpyAsync(it.first, it.second, F->nlocal * 8, hipMemcpyDeviceToDevice, F->stream));
-  HIPCHK(hipStreamSynchronize(F->stream));
-  return 0;
-}
-
-// which: 0 electric_energy_in_box, 1 magnetic_energy_in_box (current B / H),
-// 2 field_energy_in_box (electric + magnetic of the synchronized B / H)
-int energy_in_box(mnl_fields *F, int which, const double wmin[3], const double wmax[3],
-                  double *out) {
-  if (F->fused && set_fused(F, false)) return -1;  // materialise implicit E
-  if (which == 0) return energy_of_type(F, T_E, wmin, wmax, out);
-  if (which == 1) return energy_of_type(F, T_H, wmin, wmax, out);
-  MagBackup bk;
-  double mag = 0.0, el = 0.0;
-  if (sync_magnetic(F, bk)) return -1;
-  const int r = energy_of_type(F, T_H, wmin, wmax, &mag);
-  if (restore_magnetic(F, bk) || r) return -1;
-  if (energy_of_type(F, T_E, wmin, wmax, &el)) return -1;
-  *out = el + mag;
-  return 0;
-}
-
-// fields::step() n times: the NaN guard (src/step.cpp:138-139) after every nan_every-th
-// step (default every step; counted across calls) on the device, its flag read at the end of
-// each batch; the first step after construction (or after E / H were set directly) runs
-// unfused (see e_first_done)
-
-static double wall_now() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-// sum_to_all over the fields' ranks, timed as all-all communication
-int timed_allreduce(mnl_fields *F, double *v, int n) {
-  const double t0 = wall_now();
-  const int r = F->comm->allreduce_sum(v, n, F->stream);
-  F->sink_s[MNL_SINK_MPI_ALL] += wall_now() - t0;
-  return r;
-}
+// (checkpoints, array slices and field energy: mnl_io.cpp)
 
 int fields_step_batches(mnl_fields *F, int nsteps);
 
