@@ -19,7 +19,7 @@ SRCS = ((0.37, -0.21, 0.05), (-3.3, 1.6, 2.15), (2.1, 0.3, -2.9), (0.4, -0.2, 0.
 
 
 def sc_tb(make, sizes=(9.6, 6.4, 8.0), dpml=0.7, eps=6.0, random_eps=False, srcs=SRCS,
-          steps=(1, 10), tb=True, rand=True, profile=False):
+          steps=(1, 10), tb=True, rand=True, profile=False, schedule=()):
     """Dielectric slab across the PML boundary, Gaussian currents inside L2 (holes), near
     its edge and inside the PML; random initial fields; stepped in the given calls."""
     o = vol(make, 3, list(sizes), 10, center_origin=True)
@@ -40,6 +40,8 @@ def sc_tb(make, sizes=(9.6, 6.4, 8.0), dpml=0.7, eps=6.0, random_eps=False, srcs
     if isinstance(o, ProductSim):
         for f in (o._all() if hasattr(o, "_all") else [o._fields()]):
             f.set_temporal_blocking(tb)
+            for opt, val in schedule:  # Fields.set_schedule: same arithmetic, other schedule
+                f.set_schedule(opt, val)
             if profile:
                 f.set_profiling(True)
     for n in steps:
@@ -69,6 +71,23 @@ def test_tb_active_and_bitwise_vs_oracle():
     assert info["tb_items"] > 0 and info["rim_items"] > 0
     assert f.kernel_stats(5)[0] >= 4  # the two-step kernel ran (one launch per pair)
     _same(p, sc_tb(make_oracle))
+
+
+@pytest.fixture(scope="module")
+def oracle_tb():
+    return sc_tb(make_oracle)
+
+
+@pytest.mark.parametrize("schedule", [(("rim_zchunk", 12),), (("res", 16),), (("res_rim", 40),),
+                                      (("res_tb2", 24), ("narrow", 0))],
+                         ids=["rim_zchunk12", "res16", "res_rim40", "res_tb2_24_wide"])
+def test_tb_schedule_options_bitwise(oracle_tb, schedule):
+    """The scheduling options of Fields.set_schedule (rim item length, CUs left free by the
+    pair launches, the strip body) change only how the same per-point arithmetic is laid out:
+    bitwise the oracle."""
+    p = sc_tb(ProductSim, profile=True, schedule=schedule)
+    assert p._fields().tb_info()["active"] and p._fields().kernel_stats(5)[0] >= 4
+    _same(p, oracle_tb)
 
 
 def test_tb_equals_one_step_path():
