@@ -4850,7 +4850,9 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
     const int tz0 = F->tb_zchunk;
     int best = tz0;
     double best_ms = 0;
-    for (int c : {0, 32, 48, 64, 96, 128}) {
+    // (16 / 24 / 40 added in round 5: 256^3 C2 runs 6 % faster at 16-24 planes than with the
+    // automatic length, profiles/r05_ab_tb_zchunk_c2_256.json)
+    for (int c : {0, 16, 24, 32, 40, 48, 64, 96, 128}) {
       if (F->tb_zchunk_env && c != tz0) continue;
       F->tb_zchunk = c;
       double tm, gm;
@@ -5257,6 +5259,9 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->dft_cmp = v;
   } else if (which == 7) {
     F->nr_early = v;
+  } else if (which == 8) {  // planes per two-step item (0: automatic)
+    if (value < 0 || value > 4096) return fail("bad two-step chunk");
+    F->tb_zchunk = value;
   } else if (which == 6) {  // planes per rim item (0: the one-step chunk length)
     if (value < 0 || value > FUSED_MAXCH) return fail("bad rim chunk");
     F->rim_zchunk = value;
