@@ -588,8 +588,8 @@ class Fields:
         'nr_early' = the chi(2) NR box's E phase beside the tile kernel, 'tb_zchunk' = planes per
         two-step item (an integer; 0 automatic) (mnl_fields_set_schedule)."""
         idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4,
-               "dft_cmp": 5, "rim_zchunk": 6, "nr_early": 7, "tb_zchunk": 8}[which]
-        if idx in (2, 3, 4, 6, 8):  # integers: CUs left free (-1: the default), rim planes
+               "dft_cmp": 5, "rim_zchunk": 6, "nr_early": 7, "tb_zchunk": 8, "tb_ox": 9}[which]
+        if idx in (2, 3, 4, 6, 8, 9):  # integers: CUs left free (-1: the default), rim planes
             check(lib().mnl_fields_set_schedule(self.h, idx, int(value)))
         else:
             check(lib().mnl_fields_set_schedule(self.h, idx, 1 if value else 0))

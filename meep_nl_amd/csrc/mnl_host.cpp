@@ -2654,7 +2654,7 @@ int tb_plan(mnl_fields *F) {
   unsigned long long sig = 1469598103934665603ULL;
   auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
   mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
-  mix(F->rim_zchunk);
+  mix(F->rim_zchunk), mix(F->tb_ox);
   mix((long long)F->srcD_idx.size());
   for (long long v : F->srcD_idx) mix(v);
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
@@ -2930,6 +2930,19 @@ int tb_plan(mnl_fields *F) {
   // ---- two-step items: 56 x 12 own points, z chunks of tz planes (automatic: the length
   // whose item count fills whole rounds of one workgroup per CU best, with the three
   // halo planes of a chunk as overhead)
+  // own columns of the two-step items of a box: 60 (lane 0 at x0 - 2, any alignment) when that
+  // takes fewer items across the box than 56 with 64-byte aligned lanes, else 56 (in-process at
+  // 512^3: 2.103 vs 2.207 ms/step; at 256^3 both take 4 items and 56 stays); tb_ox forces one
+  auto next_x1 = [](int ox, int x0, int hi) {
+    return std::min(ox == 60 ? x0 + 59 : ((x0 - 2) >> 3 << 3) + TB_HX + TB_OX - 1, hi);
+  };
+  auto box_ox = [&](const Box &b) {
+    if (F->tb_ox) return F->tb_ox;
+    int n56 = 0, n60 = 0;
+    for (int x = b.lo[0]; x <= b.hi[0]; x = next_x1(56, x, b.hi[0]) + 1) n56++;
+    for (int x = b.lo[0]; x <= b.hi[0]; x = next_x1(60, x, b.hi[0]) + 1) n60++;
+    return n60 < n56 ? 60 : 56;
+  };
   int tz = F->tb_zchunk;
   if (tz <= 0) {
     const long long cus = std::max(1, k_cu_count());
@@ -2937,7 +2950,8 @@ int tb_plan(mnl_fields *F) {
     for (int cand : {32, 40, 48, 56, 64, 80, 96, 128}) {
       long long items = 0, chunks = 0, planes = 0;
       for (const Box &b : two) {
-        const long long ntx = (b.hi[0] - b.lo[0] + TB_OX) / TB_OX;
+        const int ox = box_ox(b);
+        const long long ntx = (b.hi[0] - b.lo[0] + ox) / ox;
         const long long nty = (b.hi[1] - b.lo[1] + TB_OY) / TB_OY;
         const long long nz = b.hi[2] - b.lo[2] + 1, nch = (nz + cand - 1) / cand;
         items += ntx * nty * nch;
@@ -2965,14 +2979,18 @@ int tb_plan(mnl_fields *F) {
   for (const Box &b : two) {
     const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + TB_OY - 1) / TB_OY;
     const int nz = b.hi[2] - b.lo[2] + 1;
+    const int ox = box_ox(b);
     for (const auto &zp : zpieces(b.lo[2], nz))
       for (int ty = 0; ty < nty; ty++)
         for (int x0 = b.lo[0]; x0 <= b.hi[0];) {
-          // lanes from the 64-byte line at or below x0 - 2 (TB_HX = 4 columns left of x0 when
-          // x0 = 4 mod 8); own columns up to lane 59, so the next item starts 4 mod 8 again
-          const int lx = (x0 - 2) >> 3 << 3;
+          // ox = 56: lanes from the 64-byte line at or below x0 - 2 (TB_HX = 4 columns left of
+          // x0 when x0 = 4 mod 8); own columns up to lane 59, so the next item starts 4 mod 8
+          // again.  ox = 60: lane 0 at x0 - 2 whatever its alignment, own lanes 2..61 (the two
+          // halo columns per side the two steps need, no alignment margin)
+          const int lx = ox == 60 ? x0 - 2 : (x0 - 2) >> 3 << 3;
           Box o;
-          o.lo[0] = x0, o.hi[0] = std::min(lx + TB_HX + TB_OX - 1, b.hi[0]);
+          o.lo[0] = x0;
+          o.hi[0] = next_x1(ox, x0, b.hi[0]);
           x0 = o.hi[0] + 1;
           o.lo[1] = b.lo[1] + (int)((long long)ny * ty / nty);
           o.hi[1] = b.lo[1] + (int)((long long)ny * (ty + 1) / nty) - 1;
@@ -5259,6 +5277,9 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->dft_cmp = v;
   } else if (which == 7) {
     F->nr_early = v;
+  } else if (which == 9) {  // own columns of a two-step item (0: per box, the fewer items)
+    if (value != 0 && value != 56 && value != 60) return fail("bad two-step width");
+    F->tb_ox = value;
   } else if (which == 8) {  // planes per two-step item (0: automatic)
     if (value < 0 || value > 4096) return fail("bad two-step chunk");
     F->tb_zchunk = value;

@@ -79,12 +79,15 @@ def oracle_tb():
 
 
 @pytest.mark.parametrize("schedule", [(("rim_zchunk", 12),), (("res", 16),), (("res_rim", 40),),
-                                      (("res_tb2", 24), ("narrow", 0))],
-                         ids=["rim_zchunk12", "res16", "res_rim40", "res_tb2_24_wide"])
+                                      (("res_tb2", 24), ("narrow", 0)), (("tb_ox", 60),),
+                                      (("tb_ox", 60), ("tb_zchunk", 5))],
+                         ids=["rim_zchunk12", "res16", "res_rim40", "res_tb2_24_wide", "ox60",
+                              "ox60_z5"])
 def test_tb_schedule_options_bitwise(oracle_tb, schedule):
     """The scheduling options of Fields.set_schedule (rim item length, CUs left free by the
-    pair launches, the strip body) change only how the same per-point arithmetic is laid out:
-    bitwise the oracle."""
+    pair launches, the strip body, 60-column two-step items at any lane alignment, short
+    two-step chunks) change only how the same per-point arithmetic is laid out: bitwise the
+    oracle."""
     p = sc_tb(ProductSim, profile=True, schedule=schedule)
     assert p._fields().tb_info()["active"] and p._fields().kernel_stats(5)[0] >= 4
     _same(p, oracle_tb)
