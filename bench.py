@@ -71,17 +71,20 @@ def parse():
     ap.add_argument("--nfreq", type=int, default=50, help="frequencies per flux plane")
     ap.add_argument("--no-events", action="store_true",
                     help="diagnostics: no per-kernel HIP events in the timed region")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N > 1: skip the C5 self-check against the one-rank fixture")
     ap.add_argument("--no-smi", action="store_true",
                     help="do not query rocm-smi for clocks / power (gpu_state)")
     return ap.parse_args()
 
 
-def build_fields(workload, size, rank, world, device, nid):
+def build_fields(workload, size, rank, world, device, nid, zslabs=None):
     """Structure + fields of one workload on this rank (global grid
-    size x size x size*world, center_origin, res 10, Courant 0.5)."""
+    size x size x size*world, center_origin, res 10, Courant 0.5; zslabs: the global grid
+    of that many slabs whatever the rank count, e.g. the whole C5 grid on one rank)."""
     from meep_nl_amd import core
     import numpy as np
-    n = [size, size, (size // 4 if workload == "c5" else size) * world]
+    n = [size, size, (size // 4 if workload == "c5" else size) * (zslabs or world)]
     io = [-(v - (v & 1)) for v in n]  # center_origin()
     gv = core.GridVolume(3, n, 10.0, io)
     s = core.Structure(gv, 0.5)
@@ -280,11 +283,25 @@ def gpu_state_finish(proc):
     return out or {"error": "no rocm-smi data", "rc": proc.returncode, "stderr": err_s[-200:]}
 
 
-def measure_extra(workload, size, steps, warmup, tune=True):
+def add_flux_planes(f, gv, planes, nfreq):
+    """N x-normal DFT flux planes through the whole cross-section, nfreq frequencies each,
+    decimation 1 (SURVEY.md 8(f) row 1: fields::add_dft_flux, src/dft.cpp:578-640)."""
+    hx = 0.5 * gv.n[0] / 10.0
+    hy, hz = 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
+    freqs = [0.1 + 0.1 * i / max(nfreq - 1, 1) for i in range(nfreq)]
+    for i in range(planes):
+        x = -hx + 2 * hx * (i + 1) / (planes + 1) + 0.05
+        f.add_dft_flux([([x, -hy, -hz], [x, hy, hz], 0, 1.0)], freqs, 1)
+
+
+def measure_extra(workload, size, steps, warmup, tune=True, flux=0, nfreq=50):
     """One single-GPU BASELINE config in the same process: warm-up, K timed
-    steps (stream-synchronized), its own roofline."""
+    steps (stream-synchronized), its own roofline.  flux > 0: that many DFT flux planes
+    (add_flux_planes) sampled and accumulated every step inside the timed region."""
     dev = int(os.environ.get("MNL_BENCH_DEVICE", "0"))
     gv, s, f = build_fields(workload, size, 0, 1, dev, None)
+    if flux:
+        add_flux_planes(f, gv, flux, nfreq)
     zc = f.tune() if tune else None
     f.step(warmup)
     f.set_profiling(True)
@@ -293,14 +310,17 @@ def measure_extra(workload, size, steps, warmup, tune=True):
     el = time.perf_counter() - t0
     cells = float(size) ** 3
     bpc, _ = f.traffic_model()
-    out = {"workload": WORKLOADS[workload] + f", {size}^3 cells, res 10, real fields, fp64",
+    out = {"workload": WORKLOADS[workload] + f", {size}^3 cells, res 10, real fields, fp64" +
+                       (f", {flux} x-normal DFT flux planes x {nfreq} frequencies (decimation 1)"
+                        if flux else ""),
            "value": round(cells * steps / el / 1e6, 1), "unit": "Mcells*steps/s",
            "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "warmup": warmup,
            "fused": f.fused_active(), "tuned_zchunk_gen_cus": zc, "model_bytes_per_cell_step": round(bpc, 2),
            "model_fraction_of_peak": round(bpc * cells / (el / steps) / 1e9 / HBM_PEAK_GBS, 4),
            "roofline": roofline(f)}
     tb_on = f.fused_active() and f.tb_info()["active"]
-    out["roofline"]["traffic"] = pmc_traffic_config(workload, size, tb_on) if f.fused_active() else None
+    out["roofline"]["traffic"] = (pmc_traffic_config(workload + (f"_flux{flux}" if flux else ""),
+                                                     size, tb_on) if f.fused_active() else None)
     if workload == "kerr_nr":
         nv = nr_voxels(gv)
         e_n, e_ms, _ = f.kernel_stats(4)
@@ -310,6 +330,12 @@ def measure_extra(workload, size, steps, warmup, tune=True):
                      "e_update_ms_per_step": round(e_ms / max(e_n, 1), 4),
                      "nr_random_fallbacks": f.nr_fallbacks(),
                      "bound": "latency/compute (per-voxel 3x3 Newton iterations), not HBM"}
+    if flux:  # the DFT updates (sampling + accumulation) of every timed step
+        d_n, d_ms, d_bytes = f.kernel_stats(3)
+        out["dft"] = {"planes": flux, "nfreq": nfreq, "updates": d_n,
+                      "ms_per_step": round(d_ms / max(steps, 1), 4),
+                      "bytes_per_update": d_bytes}
+        out["temporal_blocking"] = bool(f.fused_active() and f.tb_info()["active"])
     if f.fused_active():  # per-step time of each launch family: which one dominates
         parts = {}
         for name, kind in (("fused_tile_kernel", 0),
@@ -342,6 +368,99 @@ def rank_breakdown(f, rank, el_ms_per_step):
             "pair_ms": round(pair_ms / n, 4), "two_step_ms": round((pair_ms - rim_ms) / n, 4),
             "rim_ms": round(rim_ms / n, 4), "face_chain_ms": round(chain_ms / n, 4),
             "exchange_wait_ms": round(wait_ms / n, 4)}
+
+
+C5_STEPS = 7  # 1 step (unfused after initialize_field) + 3 pairs of steps
+
+
+def c5_fixture_path(n):
+    return os.path.join(ROOT, "tests", "golden", f"c5_parity_{n[0]}x{n[1]}x{n[2]}.npz")
+
+
+def plane_checksums(arr):
+    """Per plane of the last (z, the slab) axis: the sum over the plane of each value's IEEE
+    bit pattern times an odd weight of its (x, y, z) position, mod 2^64 (the same function as
+    tests/scenarios.plane_checksums).  Entries a rank does not own are 0 in its get_array and
+    every entry has one owner, so the ranks' checksums add up (mod 2^64) to the one-rank
+    run's exactly when every entry is bitwise equal."""
+    import numpy as np
+    a = np.ascontiguousarray(arr).view(np.uint64)
+    nx, ny, nz = a.shape
+    out = np.zeros(nz, dtype=np.uint64)
+    ky = (np.arange(ny, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))[:, None]
+    kz = (np.arange(nz, dtype=np.uint64) * np.uint64(0xD6E8FEB86659FD93))[None, :]
+    with np.errstate(over="ignore"):
+        for i in range(nx):
+            w = (np.uint64(i) * np.uint64(0xBF58476D1CE4E5B9) + ky + kz) | np.uint64(1)
+            out += (a[i] * w).sum(axis=0, dtype=np.uint64)
+    return out
+
+
+def c5_parity_run(size, zslabs, rank, world, device, nid, log=None):
+    """The C5 self-check state on this rank: the C5 grid of zslabs slabs (S x S x S/4 each),
+    seeded random D and B everywhere (tests/scenarios.sc_c5_full's seeds), stepped 1 + 6
+    (an unfused first step, then three pairs: the slab-face chains, both rim launches and the
+    two-step kernel all carry data); returns the grid, this rank's per-plane checksums of all
+    twelve components [12, nz] and the run's facts."""
+    import numpy as np
+    gv, s, f = build_fields("c5", size, rank, world, device, nid, zslabs=zslabs)
+    for c in (6, 7, 8, 9, 10, 11):
+        v = np.random.default_rng(7 + 31 * c).standard_normal(gv.shape())
+        f.initialize_field(c, v)
+        del v
+        if log:
+            log(f"initialized component {c}")
+    f.step(1)
+    f.step(C5_STEPS - 1)
+    cs = np.stack([plane_checksums(f.get_array(c)) for c in range(12)])
+    facts = {"t": f.t, "transport": f.transport(), "ranks": world,
+             "temporal_blocking": bool(f.fused_active() and f.tb_info()["active"])}
+    del f, s
+    gc.collect()
+    return gv, cs, facts
+
+
+def c5_parity_compare(parts, ref):
+    """Sum the ranks' plane checksums (mod 2^64) and compare with the one-rank fixture:
+    (equal, [(component, plane), ...] of the first differing planes)."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        tot = np.zeros_like(ref)
+        for p in parts:
+            tot = tot + p.astype(np.uint64)
+    bad = np.argwhere(tot != ref)
+    return bad.size == 0, [tuple(int(x) for x in b) for b in bad[:8]]
+
+
+def c5_parity(args, rank, world, device, dist):
+    """Self-validation of a multi-rank run: step the C5 grid of this run
+    from seeded random fields over the ranks (RCCL with one GPU per rank) and compare every
+    plane of every component, summed over the ranks, with the one-rank fixture
+    tests/golden/c5_parity_<grid>.npz (tools/make_c5_fixture.py) -- the reference's chunk
+    invariance (tests/three_d.cpp:35-39) at 0.  None when no fixture covers this grid."""
+    import numpy as np
+    from meep_nl_amd import core
+    n = [args.size, args.size, args.size // 4 * world]
+    path = c5_fixture_path(n)
+    have = os.path.exists(path)
+    if not have:
+        return {"c5_parity": None, "reason": f"no fixture for the {n[0]}x{n[1]}x{n[2]} grid"}
+    transport, _ = core.pick_transport(world, int(os.environ.get("LOCAL_RANK", "0")))
+    obj = [core.comm_id(world, transport) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    t0 = time.perf_counter()
+    gv, cs, facts = c5_parity_run(args.size, world, rank, world, device, obj[0])
+    parts = [None] * world
+    dist.all_gather_object(parts, cs)
+    out = {"grid": n, "steps": C5_STEPS, "ranks": world, "transport": facts["transport"],
+           "temporal_blocking": facts["temporal_blocking"], "fixture": os.path.relpath(path, ROOT)}
+    if rank == 0:
+        with np.load(path, allow_pickle=False) as z:
+            ref = z["checksums"]
+        ok, bad = c5_parity_compare(parts, ref)
+        out.update({"c5_parity": bool(ok), "bad_planes": bad})
+    out["seconds"] = round(time.perf_counter() - t0, 1)
+    return out
 
 
 def measure_c5(args, rank, world, device, dist):
@@ -484,12 +603,7 @@ def main():
         sys.stderr.write(f"bench.py rank {rank}: {e}\n")
         sys.exit(3)
     if args.flux:  # on-device DFT flux monitors
-        hx = 0.5 * gv.n[0] / 10.0
-        hy, hz = 0.5 * gv.n[1] / 10.0, 0.5 * gv.n[2] / 10.0
-        freqs = [0.1 + 0.1 * i / max(args.nfreq - 1, 1) for i in range(args.nfreq)]
-        for i in range(args.flux):
-            x = -hx + 2 * hx * (i + 1) / (args.flux + 1) + 0.05
-            f.add_dft_flux([([x, -hy, -hz], [x, hy, hz], 0, 1.0)], freqs, 1)
+        add_flux_planes(f, gv, args.flux, args.nfreq)
 
     def barrier():
         if dist is not None:
@@ -556,6 +670,12 @@ def main():
             extra = {"c5": measure_c5(args, rank, world, device, dist)}
         except Exception as e:  # never hides the headline number
             extra = {"c5": {"error": str(e)}}
+    parity = None
+    if world > 1 and not args.no_parity:
+        try:
+            parity = c5_parity(args, rank, world, device, dist)
+        except Exception as e:  # never hides the headline number
+            parity = {"c5_parity": False, "error": str(e)}
     if rank != 0:
         if dist is not None:
             dist.barrier()
@@ -567,6 +687,13 @@ def main():
                 extra[wl] = measure_extra(wl, args.extra_size, 20, 5, not args.no_tune)
             except Exception as e:  # an extra config must never hide the headline number
                 extra[wl] = {"error": str(e)}
+        # the headline grid with 4 whole-cross-section flux planes x 50 frequencies (SURVEY.md
+        # 8(f) row 1 on the C3 config; the same monitors as --flux 4)
+        try:
+            extra["flux4"] = measure_extra(args.workload, args.size, 20, 6, not args.no_tune,
+                                           flux=4, nfreq=50)
+        except Exception as e:
+            extra["flux4"] = {"error": str(e)}
     cpu = None
     if world == 1 and not args.no_cpu and args.workload in ("waveguide", "vacuum") and not args.flux:
         try:
@@ -604,6 +731,9 @@ def main():
         "per_rank": per_rank,
         "cpu_baseline": cpu,
         "configs": extra,
+        "c5_parity": parity.get("c5_parity") if parity else None,
+        "c5_parity_ranks": world if parity else None,
+        "c5_parity_check": parity,
         "gpu_state": {"while_stepping": state_busy, "after": state_after},
     }
     print(json.dumps(out))

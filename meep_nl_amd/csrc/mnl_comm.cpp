@@ -191,10 +191,13 @@ int Comm::ipc_barrier() {
   }
   // Setup waits are bounded by MNL_IPC_TIMEOUT (default 300 s).  Once every rank has joined,
   // a wait ends when a peer's process exits (or turns zombie) -- liveness comes from the
-  // peers' pids -- and otherwise only after MNL_IPC_TIMEOUT when it is set: a rank-0-only
-  // output or a whole-cell setup can legitimately keep the others waiting for a long time.
+  // peers' pids -- or after MNL_IPC_TIMEOUT when it is set, else after IPC_RUN_TIMEOUT_S (2 h):
+  // a rank-0-only output or a whole-cell setup can legitimately keep the others waiting for a
+  // long time, but a peer that is alive and stuck (a GPU hang inside a synchronize, a rank on
+  // another code path) must not hang every other rank forever.
+  constexpr double IPC_RUN_TIMEOUT_S = 7200.0;
   static const bool explicit_timeout = getenv("MNL_IPC_TIMEOUT") != nullptr;
-  const double limit = (ipc_ready_ && !explicit_timeout) ? 1e300 : ipc_timeout_s_;
+  const double limit = (ipc_ready_ && !explicit_timeout) ? IPC_RUN_TIMEOUT_S : ipc_timeout_s_;
   auto t0 = std::chrono::steady_clock::now();
   long spins = 0;
   while (C.gen.load(std::memory_order_acquire) == g) {

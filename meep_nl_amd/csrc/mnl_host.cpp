@@ -3924,9 +3924,11 @@ void nan_count(mnl_fields *F, int k) {
 }
 
 // end of a chunk of a batch: the reference's abort (src/step.cpp:138-139) if a guard saw NaN /
-// Inf.  The time goes back to the first failing step (the step after which the reference's
-// check aborts); the steps the device ran past it inside the chunk (at most NAN_CH) are not
-// counted.  Multi-rank: every rank learns the earliest failing step of any rank.
+// Inf.  The message names the first failing step (the step after which the reference's check
+// aborts); the time stays at the state the device holds -- the fields, the ping-pong buffers
+// and the DFT accumulators have advanced past the failing step to the end of the chunk (at most
+// NAN_CH steps), and t says so, so a caller that catches the error reads arrays labelled with
+// their own time.  Multi-rank: every rank learns the earliest failing step of any rank.
 int nan_result(mnl_fields *F) {
   if (F->nan_launched == 0) return 0;  // the same on every rank (same step counts)
   if (F->s_comm) HIPCHK(hipStreamSynchronize(F->s_comm));
@@ -3945,8 +3947,9 @@ int nan_result(mnl_fields *F) {
       if (x >= 0 && (bad_t < 0 || (long long)x < bad_t)) bad_t = (long long)x;
   }
   if (bad_t < 0) return 0;
-  F->t = bad_t;
-  return fail("simulation fields are NaN or Inf (at time step " + std::to_string(bad_t) + ")");
+  F->nan_bad_t = bad_t;
+  return fail("simulation fields are NaN or Inf (at time step " + std::to_string(bad_t) +
+              "; fields left at time step " + std::to_string(F->t) + ")");
 }
 
 int finalize_fields(mnl_fields *F) {

@@ -397,6 +397,7 @@ struct mnl_fields {
   double rim_cells = 0, rim_lean = 0, rim_cells_nu = 0;  // rim items: own / lean / mixed cells
   int nan_every = 1;                // NaN guard cadence (src/step.cpp:138-139: every step)
   int since_nan = 0;                // steps since the last NaN guard (across calls)
+  long long nan_bad_t = -1;         // first failing step of the last tripped NaN guard (-1: none)
   bool nan_due = false;             // a guard is due once the state is complete (pending rim)
   int nan_launched = 0;             // guards launched in this chunk (flag read at its end)
   long long nan_at = 0;             // time step of the state the next guard checks

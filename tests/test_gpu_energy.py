@@ -96,32 +96,58 @@ def test_nan_guard():
     """fields::step aborts with "simulation fields are NaN or Inf" when the D
     energy density at the cell centre is not finite (src/step.cpp:138-139); the
     check runs on the device every set_nan_check(k) steps inside a batch (default
-    every step), and the call raises at the end of the batch in which it fired."""
+    every step), the flag is read every 256 steps and at the end of each call, and
+    the error names the first failing step.  The time stays at the state the device
+    holds (the steps run past the failing one inside the chunk), so after the error
+    t and the arrays agree: they equal a run of t steps without the guard."""
+    import re
     from meep_nl_amd import core
     gv = core.GridVolume(3, [20, 20, 20], 10.0, [-20, -20, -20])
     s = core.Structure(gv)
-    f = core.Fields(s)
     v = np.zeros(gv.shape())
     v[10, 10, 13] = np.inf  # Dz three cells from the centre
+
+    def bad_step(e):
+        m = re.search(r"NaN or Inf \(at time step (\d+); fields left at time step (\d+)\)", str(e))
+        assert m, str(e)
+        return int(m.group(1)), int(m.group(2))
+
+    f = core.Fields(s)
     f.set_nan_check(1)
     f.initialize_field(8, v)
-    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
+    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf") as ei:
         for _ in range(20):
             f.step(1)
-    assert 1 <= f.t <= 8
+    bad, left = bad_step(ei.value)
+    assert 1 <= bad <= 8 and f.t == bad == left  # one-step calls stop at the failing step
     f2 = core.Fields(s)
     f2.initialize_field(8, v)
     f2.set_nan_check(2)
-    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
+    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf") as ei:
         f2.step(50)  # one call: the guard fires inside the batch, the call raises
-    assert f2.t in (f.t, f.t + 1)  # stopped at its first check at or after the failing step
+    bad2, left2 = bad_step(ei.value)
+    assert bad2 in (bad, bad + 1)  # its first check at or after the failing step
+    # the flag is read at the end of each part of a call (the unfused first step, the pairs,
+    # a one-step leftover) and every 256 steps: the device stopped at the first such point
+    assert f2.t == left2 and bad2 <= left2 <= 50
     f3 = core.Fields(s)  # default cadence: every step
     f3.initialize_field(8, v)
-    with pytest.raises(RuntimeError, match=r"NaN or Inf \(at time step"):
+    with pytest.raises(RuntimeError, match=r"NaN or Inf \(at time step") as ei:
         f3.step(10)  # one call of a few steps: checked (the old host guard ran every 100)
-    assert f3.t == f.t  # the time stops at the failing step, as the reference's abort
+    bad3, left3 = bad_step(ei.value)
+    assert bad3 == bad and f3.t == left3 and bad <= left3 <= 10
     f4 = core.Fields(s)  # a long call: the flag is read every 256 steps, not only at the end
     f4.initialize_field(8, v)
-    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf"):
+    with pytest.raises(RuntimeError, match="simulation fields are NaN or Inf") as ei:
         f4.step(2000)
-    assert f4.t == f.t
+    bad4, left4 = bad_step(ei.value)
+    assert bad4 == bad and f4.t == left4 and bad <= left4 <= 256
+    # t and the arrays agree: the same state as t steps without the guard
+    f5 = core.Fields(s)
+    f5.initialize_field(8, v)
+    f5.set_nan_check(10 ** 9)
+    f5.step(f4.t)
+    assert f5.t == f4.t
+    for c in range(3):
+        for comp in (c, 6 + c, 9 + c):  # E, D, B (MNL_EX.., MNL_DX.., MNL_BX..)
+            assert f4.get_array(comp).tobytes() == f5.get_array(comp).tobytes(), comp

@@ -58,8 +58,12 @@ def main():
     vals = [int(x) for x in a.values.split(",")]
     res = {v: [] for v in vals}
     for r in range(a.rounds):
-        k = r % len(vals)
-        for v in (vals[k:] + vals[:k]) if r % 2 == 0 else (vals[k:] + vals[:k])[::-1]:
+        # rotate every second round and reverse odd rounds, so that each setting runs first
+        # in half of the rounds (two values: 0,1 / 1,0 / 1,0 / 0,1 ...; ADVICE r05: the old
+        # rotation-then-reverse always ran the first value first with two values)
+        k = (r // 2) % len(vals)
+        order = vals[k:] + vals[:k]
+        for v in (order if r % 2 == 0 else order[::-1]):
             if a.fresh:
                 del f, s
                 s, f = build()
