@@ -382,7 +382,8 @@ int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
  * monitors from the two-step kernel's compact boxes (MNL_DFT_CMP; the pair plan is rebuilt),
  * 6 planes per rim item of a pair (value; 0 = the one-step chunk length), 7 the chi(2) NR box's
  * E phase beside the tile kernel (MNL_NR_EARLY), 8 planes per two-step item (value; 0 =
- * automatic; MNL_TB_ZCHUNK).  For in-process A/B measurements
+ * automatic; MNL_TB_ZCHUNK), 9 the most own columns of a two-step item (value 4..124; 0 = 124,
+ * the widest the kernel's 128 columns of lanes hold).  For in-process A/B measurements
  * (tools/ab_inproc.py). */
 int mnl_fields_set_schedule(mnl_fields *f, int which, int value);
 

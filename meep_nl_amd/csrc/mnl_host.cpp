@@ -2654,7 +2654,7 @@ int tb_plan(mnl_fields *F) {
   unsigned long long sig = 1469598103934665603ULL;
   auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
   mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
-  mix(F->rim_zchunk), mix(F->tb_ox);
+  mix(F->rim_zchunk), mix(F->tb_ox), mix(F->tb_px);
   mix((long long)F->srcD_idx.size());
   for (long long v : F->srcD_idx) mix(v);
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
@@ -2927,21 +2927,23 @@ int tb_plan(mnl_fields *F) {
       F->tb_rgeo.push_back(it.g0), F->tb_rgeo.push_back(it.g1), F->tb_rgeo.push_back(it.g2);
       F->tb_rgeo.push_back(it.g3);
     }
-  // ---- two-step items: 56 x 12 own points, z chunks of tz planes (automatic: the length
-  // whose item count fills whole rounds of one workgroup per CU best, with the three
-  // halo planes of a chunk as overhead)
-  // own columns of the two-step items of a box: 60 (lane 0 at x0 - 2, any alignment) when that
-  // takes fewer items across the box than 56 with 64-byte aligned lanes, else 56 (in-process at
-  // 512^3: 2.103 vs 2.207 ms/step; at 256^3 both take 4 items and 56 stays); tb_ox forces one
-  auto next_x1 = [](int ox, int x0, int hi) {
-    return std::min(ox == 60 ? x0 + 59 : ((x0 - 2) >> 3 << 3) + TB_HX + TB_OX - 1, hi);
+  // ---- two-step items: up to 124 x 12 own points (128 x 16 columns of lanes, two per lane),
+  // z chunks of tz planes (automatic: the length whose item count fills whole rounds of one
+  // workgroup per CU best, with the three halo planes of a chunk as overhead)
+  // own columns of the two-step items: x0 .. x1 with lane 0's first column lx = x0 - 2 (x0 - 3
+  // when x0 is odd: lane loads are 16-byte aligned), x1 <= lx + 125 and at most tb_ox columns
+  // (0: TB_OXW = 124); widths of a box are whole pieces of that width plus the remainder
+  // (tb_px = 1, the round-5 kernel for A/B: 60 own columns, lane 0 at x0 - 2, 64 lanes)
+  const int px = F->tb_px;
+  const int oxw = F->tb_ox ? F->tb_ox : (px == 1 ? 60 : TB_OXW);
+  auto lane0 = [px](int x0) { return px == 1 ? x0 - 2 : (x0 & 1) ? x0 - 3 : x0 - 2; };
+  auto next_x1 = [&](int x0, int hi) {
+    return std::min(std::min(lane0(x0) + TB_LX * px - 3, x0 + oxw - 1), hi);
   };
-  auto box_ox = [&](const Box &b) {
-    if (F->tb_ox) return F->tb_ox;
-    int n56 = 0, n60 = 0;
-    for (int x = b.lo[0]; x <= b.hi[0]; x = next_x1(56, x, b.hi[0]) + 1) n56++;
-    for (int x = b.lo[0]; x <= b.hi[0]; x = next_x1(60, x, b.hi[0]) + 1) n60++;
-    return n60 < n56 ? 60 : 56;
+  auto box_items_x = [&](const Box &b) {
+    int n = 0;
+    for (int x = b.lo[0]; x <= b.hi[0]; x = next_x1(x, b.hi[0]) + 1) n++;
+    return n;
   };
   int tz = F->tb_zchunk;
   if (tz <= 0) {
@@ -2950,8 +2952,7 @@ int tb_plan(mnl_fields *F) {
     for (int cand : {32, 40, 48, 56, 64, 80, 96, 128}) {
       long long items = 0, chunks = 0, planes = 0;
       for (const Box &b : two) {
-        const int ox = box_ox(b);
-        const long long ntx = (b.hi[0] - b.lo[0] + ox) / ox;
+        const long long ntx = box_items_x(b);
         const long long nty = (b.hi[1] - b.lo[1] + TB_OY) / TB_OY;
         const long long nz = b.hi[2] - b.lo[2] + 1, nch = (nz + cand - 1) / cand;
         items += ntx * nty * nch;
@@ -2979,18 +2980,13 @@ int tb_plan(mnl_fields *F) {
   for (const Box &b : two) {
     const int ny = b.hi[1] - b.lo[1] + 1, nty = (ny + TB_OY - 1) / TB_OY;
     const int nz = b.hi[2] - b.lo[2] + 1;
-    const int ox = box_ox(b);
     for (const auto &zp : zpieces(b.lo[2], nz))
       for (int ty = 0; ty < nty; ty++)
         for (int x0 = b.lo[0]; x0 <= b.hi[0];) {
-          // ox = 56: lanes from the 64-byte line at or below x0 - 2 (TB_HX = 4 columns left of
-          // x0 when x0 = 4 mod 8); own columns up to lane 59, so the next item starts 4 mod 8
-          // again.  ox = 60: lane 0 at x0 - 2 whatever its alignment, own lanes 2..61 (the two
-          // halo columns per side the two steps need, no alignment margin)
-          const int lx = ox == 60 ? x0 - 2 : (x0 - 2) >> 3 << 3;
+          const int lx = lane0(x0);
           Box o;
           o.lo[0] = x0;
-          o.hi[0] = next_x1(ox, x0, b.hi[0]);
+          o.hi[0] = next_x1(x0, b.hi[0]);
           x0 = o.hi[0] + 1;
           o.lo[1] = b.lo[1] + (int)((long long)ny * ty / nty);
           o.hi[1] = b.lo[1] + (int)((long long)ny * (ty + 1) / nty) - 1;
@@ -3267,6 +3263,7 @@ TB2Args tb_args(mnl_fields *F, const Set5 &o, const Set5 &m, const Set5 &n) {
   t.clk = ItemClock{F->d_clk, F->d_clk_n, F->d_clk ? CLK_CAP : 0u, 2};
   t.ncmp = (int)F->tb_cmp.size();
   for (int i = 0; i < t.ncmp; i++) t.cmp[i] = F->tb_cmp[i];
+  t.px = F->tb_px;
   return t;
 }
 
@@ -4142,6 +4139,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tz = getenv("MNL_TB_ZCHUNK"))
     F->tb_zchunk = std::max(0, atoi(tz)), F->tb_zchunk_env = true;
   if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
+  if (const char *tx = getenv("MNL_TB_PX")) F->tb_px = atoi(tx) == 1 ? 1 : 2;
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
   if (const char *dc = getenv("MNL_DFT_CMP")) F->dft_cmp = atoi(dc) != 0;
@@ -5280,8 +5278,11 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->dft_cmp = v;
   } else if (which == 7) {
     F->nr_early = v;
-  } else if (which == 9) {  // own columns of a two-step item (0: per box, the fewer items)
-    if (value != 0 && value != 56 && value != 60) return fail("bad two-step width");
+  } else if (which == 10) {  // columns per lane of the two-step kernel (1: round-5 kernel)
+    if (value != 1 && value != 2) return fail("bad two-step layout");
+    F->tb_px = value;
+  } else if (which == 9) {  // most own columns of a two-step item (0: TB_OXW = 124)
+    if (value != 0 && (value < 4 || value > TB_OXW)) return fail("bad two-step width");
     F->tb_ox = value;
   } else if (which == 8) {  // planes per two-step item (0: automatic)
     if (value < 0 || value > 4096) return fail("bad two-step chunk");

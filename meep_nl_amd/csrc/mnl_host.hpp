@@ -362,8 +362,10 @@ struct mnl_fields {
   bool tb_enabled = true;           // MNL_TB=0 at creation: never
   int tb_zchunk = 0;                // planes per two-step item (0: automatic)
   int rim_zchunk = 0;               // planes per rim item of a pair (0: fused_zchunk)
-  int tb_ox = 0;                    // own columns of a two-step item: 56 (64-byte aligned lanes),
-                                    // 60 (lane 0 at x0 - 2, any alignment), 0 per box (tb_plan)
+  int tb_px = 2;                    // columns per lane of the two-step kernel (1: the round-5
+                                    // kernel, for A/B; MNL_TB_PX)
+  int tb_ox = 0;                    // most own columns of a two-step item (0: TB_OXW = 124,
+                                    // the 128 columns of lanes less two halo columns per side)
   bool nr_early = true;             // MNL_NR_EARLY=0: the NR box's E phase after both kernels
   unsigned fused_epoch = 0;         // bumped on every entry into the fused mode
   unsigned long long tb_sig = 0;    // inputs of the current plan (0: none)

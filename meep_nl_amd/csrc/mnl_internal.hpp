@@ -343,12 +343,13 @@ struct FusedArgs {
 
 // Temporal blocking: two Yee steps per z-march over the region L2
 // (points whose L-infinity distance-2 neighbourhood lies in the lean box and holds no
-// source point).  A workgroup's 64 x 16 lanes (one row per wave) cover columns lx .. lx+63
-// (lx on a 64-byte line) and rows y0-2 .. y0+13; own columns x0 .. x1 lie in lanes 2 .. 61
-// (x0 = lx + 4, x1 = x0 + 55 except the first item of a row of items, which starts wherever
-// L2 starts) and own rows y0 .. y0+11 (waves 2 .. 13); step n runs on every lane, step n+1
-// is valid on lanes 2 .. 61 and waves 2 .. 13.
-constexpr int TB_LX = 64, TB_LY = 16, TB_HX = 4, TB_OX = 56, TB_HY = 2, TB_OY = 12;
+// source point).  A workgroup's 64 lanes x 16 waves (one row per wave) hold TB_PX = 2 adjacent
+// columns per lane (16-byte loads and stores): columns lx .. lx + 127 (lx even) and rows
+// y0 - 2 .. y0 + 13; own columns x0 .. x1 with x0 >= lx + 2, x1 <= lx + 125 (up to TB_OXW = 124)
+// and own rows y0 .. y0 + 11 (waves 2 .. 13); step n runs on every column, step n+1 is valid two
+// columns / rows inside the lanes' footprint.  Round 6: 128 x 16 lanes for 124 x 12 own points
+// (was 64 x 16 for 60 x 12).
+constexpr int TB_LX = 64, TB_PX = 2, TB_LY = 16, TB_HY = 2, TB_OY = 12, TB_OXW = 124;
 constexpr int TB_MAXCH = 512;  // planes per item (any length: the march keeps 3 planes)
 struct TB2Item {
   int x;      // x0 | x1 << 16 (own columns, inclusive)
@@ -361,7 +362,7 @@ struct TB2Item {
   // monitors sample step n+1 there): x0 | x1 << 16, y0 | y1 << 16, z0 | z1 << 16 (inclusive);
   // bx < 0: none
   int bx, by, bz;
-  int lx;     // column of lane 0 (a multiple of 8: 64-byte line)
+  int lx;     // column of lane 0's first column (even: 16-byte aligned lane loads)
 };
 // A DFT monitor's compact box: the two-step kernel stores the D and B
 // of its own points inside the box, for the middle (state 0) and the new (state 1) step of a
@@ -398,6 +399,7 @@ struct TB2Args {
   ItemClock clk;                // diagnostics: per-item start / end times (clk.rec null: off)
   int ncmp;                     // DFT compact boxes
   TBCmp cmp[TB_MAXCMP];
+  int px;                       // columns per lane: 2 (round 6), 1 (the round-5 kernel, A/B)
 };
 // NaN guard of fields::step (src/step.cpp:138-139): get_field(D_EnergyDensity, gv.center())
 // = 1/2 sum_d E_d(c) D_d(c), each value the interpolation of src/monitor.cpp:127-160 over

@@ -3955,8 +3955,8 @@ struct TB2Cmp {
   unsigned mask, ncell;
 };
 typedef const TB2Args __attribute__((address_space(4))) KTB;
-// the D, B of this lane's own point at plane kk into the item's compact DFT box m (a wave with
-// no lane in the box issues no store).  The box's parameters are read from the kernel
+// the D, B of one own point (column gx) at plane kk into the item's compact DFT box m (a wave
+// with no lane in the box issues no store).  The box's parameters are read from the kernel
 // arguments at each call through an opaque pointer, so they are not hoisted out of the plane
 // loop into SGPRs (which are full there: held across the loop they spill and reload per plane)
 __device__ __forceinline__ void tb2_cmp_store(int m, int state, bool own, int gx, int gy, int kk,
@@ -3979,6 +3979,412 @@ __device__ __forceinline__ void tb2_cmp_store(int m, int state, bool own, int gx
     if ((c.mask >> q) & 1u) bst(r, in ? ((st + q) * c.ncell + ci) * 8u : MNL_OOB, v[q]);
 }
 
+// the kernel arguments behind an empty asm: fields read through it at a use inside the plane
+// loop are scalar loads there (kernarg segment, constant cache) instead of SGPRs held across it
+__device__ __forceinline__ KTB *tb2_kargs() {
+  KTB *kt = (KTB *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kt));
+  return kt;
+}
+
+// a wave-uniform double moved to SGPRs (readfirstlane of both halves)
+__device__ __forceinline__ double sgpr_f64(double v) {
+  const mnl_u2 u = __builtin_bit_cast(mnl_u2, v);
+  mnl_u2 r;
+  r.x = __builtin_amdgcn_readfirstlane(u.x);
+  r.y = __builtin_amdgcn_readfirstlane(u.y);
+  return __builtin_bit_cast(double, r);
+}
+// descriptor of a non-null scalar pointer built where it is used (no null test: s_cselect-free)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc_nn(unsigned long long v, unsigned nrec) {
+  asm volatile("" : "+s"(v));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, (int)nrec, 0x00020000);
+}
+
+// ---- two columns per lane: 16-byte loads / stores, x neighbours across lanes by DPP
+typedef double mnl_d2 __attribute__((ext_vector_type(2)));
+typedef unsigned int mnl_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ mnl_d2 ldg2(gdp p, unsigned off) {
+  return *(const mnl_d2 __attribute__((address_space(1))) *)((const char __attribute__((address_space(1))) *)p + off);
+}
+__device__ __forceinline__ mnl_u2 ldu2(gup p, unsigned off) {
+  return *(const mnl_u2 __attribute__((address_space(1))) *)((const char __attribute__((address_space(1))) *)p + off);
+}
+__device__ __forceinline__ void bst2(__amdgpu_buffer_rsrc_t r, unsigned off, double a, double b) {
+  const mnl_u2 x = __builtin_bit_cast(mnl_u2, a), y = __builtin_bit_cast(mnl_u2, b);
+  mnl_u4 q;
+  q.x = x.x, q.y = x.y, q.z = y.x, q.w = y.y;
+  __builtin_amdgcn_raw_buffer_store_b128(q, r, off, 0, 0);
+}
+// lane i <- lane i + 1 (DPP wave_shl:1) / lane i <- lane i - 1 (wave_shr:1); the end lane keeps
+// its own value (a column outside every own point's stencil)
+__device__ __forceinline__ double lane_next(double x) {
+  const mnl_u2 u = __builtin_bit_cast(mnl_u2, x);
+  mnl_u2 r;
+  r.x = __builtin_amdgcn_update_dpp((int)u.x, (int)u.x, 0x130, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_update_dpp((int)u.y, (int)u.y, 0x130, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double lane_prev(double x) {
+  const mnl_u2 u = __builtin_bit_cast(mnl_u2, x);
+  mnl_u2 r;
+  r.x = __builtin_amdgcn_update_dpp((int)u.x, (int)u.x, 0x138, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_update_dpp((int)u.y, (int)u.y, 0x138, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+// y-neighbour exchange of the two-step kernel: per padded row (rows 0 and TB_LY + 1 pad, so a
+// wave's rows w - 1 / w + 1 are constant offsets from one per-lane address within the 16-bit
+// offset of ds_read_b128) 8 slots of 128 columns: E^n z, x; E^{n+1} z, x; B^{n+1} z, x;
+// B^{n+2} z, x
+struct alignas(16) TB2Lds {
+  double s[TB_LY + 2][8][TB_LX * TB_PX];
+};
+enum { TBS_E1Z, TBS_E1X, TBS_E2Z, TBS_E2X, TBS_H1Z, TBS_H1X, TBS_H2Z, TBS_H2X };
+constexpr int TB_RS = 8 * TB_LX * TB_PX;  // doubles per padded row
+#define TBO(row, slot) ((row) * TB_RS + (slot) * TB_LX * TB_PX)
+__device__ __forceinline__ void tb_put(double *bp, int o, double a, double b) {
+  mnl_d2 t;
+  t.x = a, t.y = b;
+  *(mnl_d2 *)(bp + o) = t;
+}
+__device__ __forceinline__ void tb_get(const double *bp, int o, double &a, double &b) {
+  const mnl_d2 t = *(const mnl_d2 *)(bp + o);
+  a = t.x, b = t.y;
+}
+// chi1inv of one column: UMODE 0 none (E = D), 1 the f64 arrays, 2 a palette word (LDS table)
+template <int UMODE>
+struct TbU {
+  unsigned w;
+  __device__ double get(int c, const double (*sU)[256]) const { return sU[c][(w >> (8 * c)) & 255]; }
+};
+template <>
+struct TbU<1> {
+  double u0, u1, u2;
+  __device__ double get(int c, const double (*)[256]) const { return c == 0 ? u0 : (c == 1 ? u1 : u2); }
+};
+template <>
+struct TbU<0> {
+  __device__ double get(int, const double (*)[256]) const { return 1.0; }
+};
+
+// Temporal blocking: steps n -> n+1 -> n+2 in one z-march over an
+// item of the region L2, where every point within L-infinity distance 2 of an own point is
+// lean (no PML, every component owned, H == B, E implicit) and no source point lies within
+// distance 1 of an own point.  Per plane k of the march: step n at plane k on all 128 x 16
+// columns (B^{n+1}(k), then D^{n+1}(k) from B^{n+1}(k-1) kept in registers), then step n+1 at
+// plane k-1 from E^{n+1}(k-1) and E^{n+1}(k).  Per two steps a point's D and B are read once
+// and written once (plus the step-n+1 values of the points on a face that borders the rim,
+// which the one-step rim launch of step n+1 reads).  The arithmetic of each update is the lean
+// body's expression, operand for operand (src/step_generic.cpp:106-113 curl, 888-903
+// E = chi1inv * D), so two steps here are bitwise two one-step launches.
+//
+// Round 6 layout: two adjacent columns per lane (TB_PX), so a workgroup covers 128 x 16 columns
+// for up to 124 x 12 own points (was 64 x 16 for 60 x 12: the x halo lines and the per-plane
+// barriers are paid for twice the points).  x neighbours: the lane's other column or the next /
+// previous lane's (DPP); y neighbours: LDS (two components per exchange, 16-byte accesses).
+// Carried across planes: D^n(k), B^{n+1}(k-1), D^{n+1}(k-1), B^{n+2}(k-2) x, y and the chi1inv
+// of k and k-1; E^n(k) = chi1inv D^n(k) and E^{n+1}(k-1) are recomputed per plane (the same
+// products, so the same values).  B^n(k+1) is loaded after the B update of plane k (half a
+// plane ahead), D^n(k+2) and chi1inv(k+2) a whole plane ahead.
+template <int UMODE, bool UNI, bool CMP>
+__device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, unsigned uw,
+                                         const double (*sU)[256], TB2Lds &L) {
+  typedef TbU<UMODE> U;
+  constexpr bool HAS_U = UMODE != 0;
+  const int tid = tid_item(), lane = tid & 63, w = tid >> 6;
+  const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
+  const int zs = it.z & 0xFFFF, ze = it.z >> 16;
+  const int faces = it.faces;
+  // the item's compact DFT box (-1: none; CMP = false: no box in this launch, none compiled)
+  const int cmi = CMP ? ((faces >> 8) & 7) - 1 : -1;
+  const int gx = it.lx + TB_PX * lane, gy = y0 - TB_HY + w;  // this lane's columns gx, gx + 1
+  const int N1 = a.N[1], zmax = a.N[2] - 1;
+  const int cx = min(max(gx, 0), (int)a.st1 - TB_PX), cy = min(max(gy, 0), N1 - 1);
+  const unsigned col = (unsigned)((cx + (long long)cy * a.st1) * 8);
+  const unsigned s2 = (unsigned)(a.st2 * 8);
+  const double C = a.C;
+  const bool oy = gy >= y0 && gy <= y1;
+  const bool own0 = oy && gx >= x0 && gx <= x1, own1 = oy && gx + 1 >= x0 && gx + 1 <= x1;
+  // item-uniform: an own range that starts or ends inside a lane's column pair (b64 stores)
+  const bool ragged = ((x0 - it.lx) & 1) != 0 || ((x1 - it.lx) & 1) == 0;
+  // the item stores step-n+1 values of some points (rim-bordering faces, DFT / guard box)
+  const bool anymid = (faces & 63) != 0 || it.bx >= 0;
+  const unsigned nrec = (unsigned)min(a.nelem * 8, 0xFFFFFFFFLL);
+  const gdp D0 = sgpr_ptr(a.Do[0]), D1 = sgpr_ptr(a.Do[1]), D2 = sgpr_ptr(a.Do[2]);
+  const gdp B0 = sgpr_ptr(a.Bo[0]), B1 = sgpr_ptr(a.Bo[1]), B2 = sgpr_ptr(a.Bo[2]);
+  const gdp U0 = UMODE == 1 ? sgpr_ptr(a.u[0]) : nullptr;
+  const gdp U1 = UMODE == 1 ? sgpr_ptr(a.u[1]) : nullptr;
+  const gdp U2 = UMODE == 1 ? sgpr_ptr(a.u[2]) : nullptr;
+  const gup uix = (gup)sgpr_ptr(a.uidx);
+  // chi1inv of a uniform item (wave-uniform: held in SGPRs, VALU operands)
+  double cu0 = 1, cu1 = 1, cu2 = 1;
+  if (UMODE == 2 && UNI) {
+    cu0 = sgpr_f64(sU[0][uw & 255]), cu1 = sgpr_f64(sU[1][(uw >> 8) & 255]);
+    cu2 = sgpr_f64(sU[2][(uw >> 16) & 255]);
+  }
+  auto uv = [&](const U &u, int c) -> double {
+    if (UMODE == 2 && UNI) return c == 0 ? cu0 : (c == 1 ? cu1 : cu2);
+    return u.get(c, sU);
+  };
+  auto zc = [zmax](int z) { return min(max(z, 0), zmax); };
+  auto ldu = [&](unsigned o, U &u0, U &u1) {
+    if constexpr (UMODE == 2) {
+      if (UNI) {
+        u0.w = u1.w = 0;
+      } else {
+        const mnl_u2 t = ldu2(uix, o >> 1);
+        u0.w = t.x, u1.w = t.y;
+      }
+    } else if constexpr (UMODE == 1) {
+      mnl_d2 t = ldg2(U0, o);
+      u0.u0 = t.x, u1.u0 = t.y;
+      t = ldg2(U1, o);
+      u0.u1 = t.x, u1.u1 = t.y;
+      t = ldg2(U2, o);
+      u0.u2 = t.x, u1.u2 = t.y;
+    }
+  };
+  struct QD {  // D and chi1inv of one plane
+    mnl_d2 d0, d1, d2;
+    U u0, u1;
+  };
+  auto loadd = [&](int k) -> QD {
+    QD q;
+    const unsigned o = col + (unsigned)zc(k) * s2;
+    q.d0 = ldg2(D0, o);
+    q.d1 = ldg2(D1, o);
+    q.d2 = ldg2(D2, o);
+    ldu(o, q.u0, q.u1);
+    return q;
+  };
+  struct QB {
+    mnl_d2 b0, b1, b2;
+  };
+  auto loadb = [&](int k) -> QB {
+    QB q;
+    const unsigned o = col + (unsigned)zc(k) * s2;
+    q.b0 = ldg2(B0, o);
+    q.b1 = ldg2(B1, o);
+    q.b2 = ldg2(B2, o);
+    return q;
+  };
+  // this lane's slot in its padded row (row w + 1): rows w / w + 2 are constant offsets
+  double *bp = &L.s[0][0][0] + (w * TB_RS + TB_PX * lane);
+  const int k0 = zs - 2;
+  // prologue: D^n(k0) and chi1inv(k0); then D(k0 + 1) and B(k0)
+  double dn0[3], dn1[3];
+  U uk0, uk1, um0, um1;  // chi1inv of the march plane k and of k - 1, columns 0 / 1
+  {
+    const QD p = loadd(k0);
+    dn0[0] = p.d0.x, dn1[0] = p.d0.y, dn0[1] = p.d1.x, dn1[1] = p.d1.y;
+    dn0[2] = p.d2.x, dn1[2] = p.d2.y;
+    uk0 = p.u0, uk1 = p.u1;
+    um0 = uk0, um1 = uk1;
+  }
+  QD qd = loadd(k0 + 1);
+  QB qb = loadb(k0);
+  double b10[3] = {0, 0, 0}, b11[3] = {0, 0, 0};  // B^{n+1}(k-1)
+  double d10[3] = {0, 0, 0}, d11[3] = {0, 0, 0};  // D^{n+1}(k-1)
+  double h2x0 = 0, h2y0 = 0, h2x1 = 0, h2y1 = 0;  // B^{n+2}(k-2) x, y
+  for (int k = k0; k <= ze; k++) {
+    const QD c = qd;  // D^n(k+1), chi1inv(k+1)
+    const QB cb = qb;  // B^n(k)
+    qd = loadd(min(k + 2, ze + 1));
+    // E^n(k+1) x, y; E^n(k); E^{n+1}(k-1)
+    double e1x0, e1y0, e1x1, e1y1, en0[3], en1[3], f10[3], f11[3];
+    e1x0 = c.d0.x, e1y0 = c.d1.x, e1x1 = c.d0.y, e1y1 = c.d1.y;
+    if (HAS_U) {
+      e1x0 = c.d0.x * uv(c.u0, 0), e1y0 = c.d1.x * uv(c.u0, 1);
+      e1x1 = c.d0.y * uv(c.u1, 0), e1y1 = c.d1.y * uv(c.u1, 1);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      en0[q] = dn0[q], en1[q] = dn1[q], f10[q] = d10[q], f11[q] = d11[q];
+      if (HAS_U) {
+        en0[q] = dn0[q] * uv(uk0, q), en1[q] = dn1[q] * uv(uk1, q);
+        f10[q] = d10[q] * uv(um0, q), f11[q] = d11[q] * uv(um1, q);
+      }
+    }
+    tb_put(bp, TBO(1, TBS_E1Z), en0[2], en1[2]);
+    tb_put(bp, TBO(1, TBS_E1X), en0[0], en1[0]);
+    tb_put(bp, TBO(1, TBS_E2Z), f10[2], f11[2]);
+    tb_put(bp, TBO(1, TBS_E2X), f10[0], f11[0]);
+    __syncthreads();
+    // ---- step n at plane k: B^{n+1}(k) (curl E^n), H == B
+    double Bx0, By0, Bz0, Bx1, By1, Bz1;
+    {
+      double ezy0, ezy1, exy0, exy1;
+      tb_get(bp, TBO(2, TBS_E1Z), ezy0, ezy1);
+      tb_get(bp, TBO(2, TBS_E1X), exy0, exy1);
+      const double ezx1 = lane_next(en0[2]), eyx1 = lane_next(en0[1]);
+      Bx0 = cb.b0.x - C * (ezy0 - en0[2] + en0[1] - e1y0);
+      By0 = cb.b1.x - C * (e1x0 - en0[0] + en0[2] - en1[2]);
+      Bz0 = cb.b2.x - C * (en1[1] - en0[1] + en0[0] - exy0);
+      Bx1 = cb.b0.y - C * (ezy1 - en1[2] + en1[1] - e1y1);
+      By1 = cb.b1.y - C * (e1x1 - en1[0] + en1[2] - ezx1);
+      Bz1 = cb.b2.y - C * (eyx1 - en1[1] + en1[0] - exy1);
+    }
+    tb_put(bp, TBO(1, TBS_H1Z), Bz0, Bz1);
+    tb_put(bp, TBO(1, TBS_H1X), Bx0, Bx1);
+    qb = loadb(min(k + 1, ze));
+    __syncthreads();
+    // D^{n+1}(k) (curl H^{n+1}), E^{n+1}(k) x, y = chi1inv * D^{n+1}(k)
+    double Dx0, Dy0, Dz0, Dx1, Dy1, Dz1;
+    {
+      double hzy0, hzy1, hxy0, hxy1;
+      tb_get(bp, TBO(0, TBS_H1Z), hzy0, hzy1);
+      tb_get(bp, TBO(0, TBS_H1X), hxy0, hxy1);
+      const double hzx0 = lane_prev(Bz1), hyx0 = lane_prev(By1);
+      Dx0 = dn0[0] - C * (hzy0 - Bz0 + By0 - b10[1]);
+      Dy0 = dn0[1] - C * (b10[0] - Bx0 + Bz0 - hzx0);
+      Dz0 = dn0[2] - C * (hyx0 - By0 + Bx0 - hxy0);
+      Dx1 = dn1[0] - C * (hzy1 - Bz1 + By1 - b11[1]);
+      Dy1 = dn1[1] - C * (b11[0] - Bx1 + Bz1 - Bz0);
+      Dz1 = dn1[2] - C * (By0 - By1 + Bx1 - hxy1);
+    }
+    double Ex0 = Dx0, Ey0 = Dy0, Ex1 = Dx1, Ey1 = Dy1;
+    if (HAS_U) {
+      Ex0 = Dx0 * uv(uk0, 0), Ey0 = Dy0 * uv(uk0, 1);
+      Ex1 = Dx1 * uv(uk1, 0), Ey1 = Dy1 * uv(uk1, 1);
+    }
+    // ---- step n+1 at plane k-1: B^{n+2}(k-1) from E^{n+1}(k-1) (f1) and E^{n+1}(k)
+    double Fx0, Fy0, Fz0, Fx1, Fy1, Fz1;
+    {
+      double fzy0, fzy1, fxy0, fxy1;
+      tb_get(bp, TBO(2, TBS_E2Z), fzy0, fzy1);
+      tb_get(bp, TBO(2, TBS_E2X), fxy0, fxy1);
+      const double fzx1 = lane_next(f10[2]), fyx1 = lane_next(f10[1]);
+      Fx0 = b10[0] - C * (fzy0 - f10[2] + f10[1] - Ey0);
+      Fy0 = b10[1] - C * (Ex0 - f10[0] + f10[2] - f11[2]);
+      Fz0 = b10[2] - C * (f11[1] - f10[1] + f10[0] - fxy0);
+      Fx1 = b11[0] - C * (fzy1 - f11[2] + f11[1] - Ey1);
+      Fy1 = b11[1] - C * (Ex1 - f11[0] + f11[2] - fzx1);
+      Fz1 = b11[2] - C * (fyx1 - f11[1] + f11[0] - fxy1);
+    }
+    tb_put(bp, TBO(1, TBS_H2Z), Fz0, Fz1);
+    tb_put(bp, TBO(1, TBS_H2X), Fx0, Fx1);
+    if (anymid) {  // step-n+1 values of the points on a face bordering the rim (read by rim
+                   // step n+1), of the DFT / NaN-guard box, of the compact DFT box
+      const bool kin = k >= zs && k < ze;
+      const bool kz = ((faces & 16) && k == zs) || ((faces & 32) && k == ze - 1);
+      const int bx0 = it.bx & 0xFFFF, bx1 = it.bx >> 16;
+      const bool dy = it.bx >= 0 && gy >= (it.by & 0xFFFF) && gy <= (it.by >> 16) &&
+                      k >= (it.bz & 0xFFFF) && k <= (it.bz >> 16);
+      const bool fy = ((faces & 4) && gy == y0) || ((faces & 8) && gy == y1);
+      const bool bd0 = kin && own0 && (fy || kz || ((faces & 1) && gx == x0) ||
+                                       ((faces & 2) && gx == x1) || (dy && gx >= bx0 && gx <= bx1));
+      const bool bd1 = kin && own1 && (fy || kz || ((faces & 1) && gx + 1 == x0) ||
+                                       ((faces & 2) && gx + 1 == x1) ||
+                                       (dy && gx + 1 >= bx0 && gx + 1 <= bx1));
+      const unsigned ob = col + (unsigned)k * s2;
+      const unsigned o2 = bd0 && bd1 ? ob : MNL_OOB, oa = bd0 && !bd1 ? ob : MNL_OOB,
+                     oc = bd1 && !bd0 ? ob + 8 : MNL_OOB;
+      KTB *kt = tb2_kargs();  // output pointers read at use (not held across the loop)
+      const unsigned long long pm[6] = {
+          (unsigned long long)kt->Bm[0], (unsigned long long)kt->Bm[1],
+          (unsigned long long)kt->Bm[2], (unsigned long long)kt->Dm[0],
+          (unsigned long long)kt->Dm[1], (unsigned long long)kt->Dm[2]};
+      const double v0[6] = {Bx0, By0, Bz0, Dx0, Dy0, Dz0}, v1[6] = {Bx1, By1, Bz1, Dx1, Dy1, Dz1};
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const auto r = brsrc_nn(pm[q], nrec);
+        bst2(r, o2, v0[q], v1[q]);
+        bst(r, oa, v0[q]);
+        bst(r, oc, v1[q]);
+      }
+      if (CMP && cmi >= 0) {
+        tb2_cmp_store(cmi, 0, own0 && kin, gx, gy, k, Dx0, Dy0, Dz0, Bx0, By0, Bz0);
+        tb2_cmp_store(cmi, 0, own1 && kin, gx + 1, gy, k, Dx1, Dy1, Dz1, Bx1, By1, Bz1);
+      }
+    }
+    __syncthreads();
+    double Gx0, Gy0, Gz0, Gx1, Gy1, Gz1;
+    {
+      double gzy0, gzy1, gxy0, gxy1;
+      tb_get(bp, TBO(0, TBS_H2Z), gzy0, gzy1);
+      tb_get(bp, TBO(0, TBS_H2X), gxy0, gxy1);
+      const double gzx0 = lane_prev(Fz1), gyx0 = lane_prev(Fy1);
+      Gx0 = d10[0] - C * (gzy0 - Fz0 + Fy0 - h2y0);
+      Gy0 = d10[1] - C * (h2x0 - Fx0 + Fz0 - gzx0);
+      Gz0 = d10[2] - C * (gyx0 - Fy0 + Fx0 - gxy0);
+      Gx1 = d11[0] - C * (gzy1 - Fz1 + Fy1 - h2y1);
+      Gy1 = d11[1] - C * (h2x1 - Fx1 + Fz1 - Fz0);
+      Gz1 = d11[2] - C * (Fy0 - Fy1 + Fx1 - gxy1);
+    }
+    {
+      const bool st = k - 1 >= zs && k - 1 < ze;
+      const unsigned os = col + (unsigned)(k - 1) * s2;
+      const unsigned o2 = st && own0 && own1 ? os : MNL_OOB;
+      KTB *kt = tb2_kargs();
+      const unsigned long long pn[6] = {
+          (unsigned long long)kt->Bn[0], (unsigned long long)kt->Bn[1],
+          (unsigned long long)kt->Bn[2], (unsigned long long)kt->Dn[0],
+          (unsigned long long)kt->Dn[1], (unsigned long long)kt->Dn[2]};
+      const double v0[6] = {Fx0, Fy0, Fz0, Gx0, Gy0, Gz0}, v1[6] = {Fx1, Fy1, Fz1, Gx1, Gy1, Gz1};
+#pragma unroll
+      for (int q = 0; q < 6; q++) bst2(brsrc_nn(pn[q], nrec), o2, v0[q], v1[q]);
+      if (ragged) {  // an own range starting or ending inside a column pair
+        const unsigned oa = st && own0 && !own1 ? os : MNL_OOB;
+        const unsigned oc = st && own1 && !own0 ? os + 8 : MNL_OOB;
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+          const auto r = brsrc_nn(pn[q], nrec);
+          bst(r, oa, v0[q]);
+          bst(r, oc, v1[q]);
+        }
+      }
+      if (CMP && cmi >= 0) {
+        tb2_cmp_store(cmi, 1, st && own0, gx, gy, k - 1, Gx0, Gy0, Gz0, Fx0, Fy0, Fz0);
+        tb2_cmp_store(cmi, 1, st && own1, gx + 1, gy, k - 1, Gx1, Gy1, Gz1, Fx1, Fy1, Fz1);
+      }
+    }
+    h2x0 = Fx0, h2y0 = Fy0, h2x1 = Fx1, h2y1 = Fy1;
+    b10[0] = Bx0, b10[1] = By0, b10[2] = Bz0, b11[0] = Bx1, b11[1] = By1, b11[2] = Bz1;
+    d10[0] = Dx0, d10[1] = Dy0, d10[2] = Dz0, d11[0] = Dx1, d11[1] = Dy1, d11[2] = Dz1;
+    dn0[0] = c.d0.x, dn1[0] = c.d0.y, dn0[1] = c.d1.x, dn1[1] = c.d1.y;
+    dn0[2] = c.d2.x, dn1[2] = c.d2.y;
+    um0 = uk0, um1 = uk1, uk0 = c.u0, uk1 = c.u1;
+  }
+}
+#undef TBO
+
+template <int UMODE, bool CLK, bool CMP>
+__global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
+  __shared__ double sU[UMODE == 2 ? 3 : 1][256];
+  __shared__ TB2Lds L;
+  __shared__ int s_idx;
+  __shared__ unsigned long long s_t0;
+  if (UMODE == 2) {  // palette -> LDS (visible after the first barrier below)
+    for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
+  }
+  unsigned long long *ctr = a.ctr + 16 * a.ctr_line;
+  if (CLK && threadIdx.x == 0) s_t0 = 0ull;  // no previous item
+  for (;;) {
+    if (threadIdx.x == 0) {
+      if (CLK && s_t0 != 0ull) {  // diagnostics: the previous item (see fused_tile_kernel)
+        const TB2Item it = a.items[s_idx];
+        const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[s_idx] : ~0u;
+        clk_record(a.clk, s_t0, (it.faces & 63) | (uw != ~0u ? 64 : 0), it.x, it.y, it.z, -1);
+      }
+      const unsigned long long v = atomicAdd(ctr, 1ULL) - a.cbase;
+      s_idx = v < (unsigned long long)(a.n) ? (int)v : -1;
+      if (CLK) s_t0 = wall_clock64();
+    }
+    __syncthreads();  // also separates LDS use of consecutive items
+    const int idx = s_idx;
+    if (idx < 0) break;
+    const TB2Item it = a.items[idx];
+    const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[idx] : ~0u;
+    if (UMODE == 2 && __builtin_amdgcn_readfirstlane(uw) != ~0u)
+      tb2_body<UMODE, true, CMP>(a, it, uw, sU, L);
+    else
+      tb2_body<UMODE, false, CMP>(a, it, uw, sU, L);
+  }
+}
+
+// ---- the round-5 two-step kernel (one column per lane, 64 x 16 lanes for up to 60 x 12 own
+// points; x and y neighbours through LDS), kept for in-process A/B against the round-6 layout
+// (set_schedule "tb_px" = 1)
 // Temporal blocking: steps n -> n+1 -> n+2 in one z-march over an
 // item of the region L2, where every point within L-infinity distance 2 of an own point is
 // lean (no PML, every component owned, H == B, E implicit) and no source point lies within
@@ -3991,7 +4397,7 @@ __device__ __forceinline__ void tb2_cmp_store(int m, int state, bool own, int gx
 // for operand (src/step_generic.cpp:106-113 curl, 888-903 E = chi1inv * D), so two steps
 // here are bitwise two one-step launches.
 template <int UMODE, bool UNI, bool CMP>
-__device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, unsigned uw,
+__device__ __forceinline__ void tb2_body1(const TB2Args &a, const TB2Item it, unsigned uw,
                                          const double (*sU)[256], double (*sE1)[TB_LY][TB_LX],
                                          double (*sH1)[TB_LY][TB_LX], double (*sE2)[TB_LY][TB_LX],
                                          double (*sH2)[TB_LY][TB_LX]) {
@@ -4171,7 +4577,7 @@ __device__ __forceinline__ void tb2_body(const TB2Args &a, const TB2Item it, uns
 }
 
 template <int UMODE, bool CLK, bool CMP>
-__global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
+__global__ __launch_bounds__(1024) void tb2_kernel1(TB2Args a) {
   __shared__ double sU[UMODE == 2 ? 3 : 1][256];
   __shared__ double sE1[3][TB_LY][TB_LX], sH1[3][TB_LY][TB_LX];
   __shared__ double sE2[3][TB_LY][TB_LX], sH2[3][TB_LY][TB_LX];
@@ -4199,9 +4605,9 @@ __global__ __launch_bounds__(1024) void tb2_kernel(TB2Args a) {
     const TB2Item it = a.items[idx];
     const unsigned uw = (UMODE == 2 && a.uflag) ? a.uflag[idx] : ~0u;
     if (UMODE == 2 && __builtin_amdgcn_readfirstlane(uw) != ~0u)
-      tb2_body<UMODE, true, CMP>(a, it, uw, sU, sE1, sH1, sE2, sH2);
+      tb2_body1<UMODE, true, CMP>(a, it, uw, sU, sE1, sH1, sE2, sH2);
     else
-      tb2_body<UMODE, false, CMP>(a, it, uw, sU, sE1, sH1, sE2, sH2);
+      tb2_body1<UMODE, false, CMP>(a, it, uw, sU, sE1, sH1, sE2, sH2);
   }
 }
 
@@ -4235,7 +4641,7 @@ int k_tb2_uniform(const TB2Args &a, unsigned *flags, void *stream) {
 int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
   if (a.n <= 0) return 0;
   if (a.nelem * 8 >= (long long)MNL_OOB || !a.ctr || !a.items || a.ctr_line < 0 ||
-      a.ctr_line >= FUSED_NCTR)
+      a.ctr_line >= FUSED_NCTR || (a.px != 1 && a.px != 2))
     return 2;
   long long nb = fused_grid_blocks(1);
   if (a.wg_limit > 0 && nb > a.wg_limit) nb = a.wg_limit;
@@ -4247,28 +4653,36 @@ int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases) {
   hipStream_t s = (hipStream_t)stream;
   const dim3 grd((unsigned)nb), blk(1024);
   // compact DFT boxes (t.ncmp > 0): the variant with their stores; the diagnostics build
-  // (MNL_ITEM_CLOCK) always has them
-  if (t.clk.rec) {
-    if (um == 2)
-      tb2_kernel<2, true, true><<<grd, blk, 0, s>>>(t);
-    else if (um == 1)
-      tb2_kernel<1, true, true><<<grd, blk, 0, s>>>(t);
-    else
-      tb2_kernel<0, true, true><<<grd, blk, 0, s>>>(t);
-  } else if (t.ncmp > 0) {
-    if (um == 2)
-      tb2_kernel<2, false, true><<<grd, blk, 0, s>>>(t);
-    else if (um == 1)
-      tb2_kernel<1, false, true><<<grd, blk, 0, s>>>(t);
-    else
-      tb2_kernel<0, false, true><<<grd, blk, 0, s>>>(t);
-  } else if (um == 2) {
-    tb2_kernel<2, false, false><<<grd, blk, 0, s>>>(t);
-  } else if (um == 1) {
-    tb2_kernel<1, false, false><<<grd, blk, 0, s>>>(t);
-  } else {
-    tb2_kernel<0, false, false><<<grd, blk, 0, s>>>(t);
-  }
+  // (MNL_ITEM_CLOCK) always has them; px 1: the round-5 layout (A/B)
+#define MNL_TB2_LAUNCH(K)                                   \
+  do {                                                      \
+    if (t.clk.rec) {                                        \
+      if (um == 2)                                          \
+        K<2, true, true><<<grd, blk, 0, s>>>(t);            \
+      else if (um == 1)                                     \
+        K<1, true, true><<<grd, blk, 0, s>>>(t);            \
+      else                                                  \
+        K<0, true, true><<<grd, blk, 0, s>>>(t);            \
+    } else if (t.ncmp > 0) {                                \
+      if (um == 2)                                          \
+        K<2, false, true><<<grd, blk, 0, s>>>(t);           \
+      else if (um == 1)                                     \
+        K<1, false, true><<<grd, blk, 0, s>>>(t);           \
+      else                                                  \
+        K<0, false, true><<<grd, blk, 0, s>>>(t);           \
+    } else if (um == 2) {                                   \
+      K<2, false, false><<<grd, blk, 0, s>>>(t);            \
+    } else if (um == 1) {                                   \
+      K<1, false, false><<<grd, blk, 0, s>>>(t);            \
+    } else {                                                \
+      K<0, false, false><<<grd, blk, 0, s>>>(t);            \
+    }                                                       \
+  } while (0)
+  if (t.px == 1)
+    MNL_TB2_LAUNCH(tb2_kernel1);
+  else
+    MNL_TB2_LAUNCH(tb2_kernel);
+#undef MNL_TB2_LAUNCH
   return hipPeekAtLastError() == hipSuccess ? 0 : 9;
 }
 

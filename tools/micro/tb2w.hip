@@ -154,7 +154,7 @@ __device__ __forceinline__ void lds_get(const double *bp, int o, double (&v)[PX]
 }
 
 // BL: B(k) loaded after the B update of plane k - 1 (half a plane ahead) instead of with D(k+1)
-template <int PX, bool UNI, bool BL>
+template <int PX, bool UNI, bool BL, int DIST = 1>
 __device__ __forceinline__ void body(const Args &a, const Item it, LdsT<PX> &L, const double (*sU)[256]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
@@ -235,6 +235,8 @@ __device__ __forceinline__ void body(const Args &a, const Item it, LdsT<PX> &L, 
     ldw(o, uk);
   }
   Q q = load(k0);
+  Q q2;  // DIST 2: the plane after q (loaded two planes ahead of its use)
+  if (DIST == 2) q2 = load(k0 + 1);
   Q qb;  // BL: B(k) loaded after the B update of plane k - 1
   if (BL) loadb(k0, qb);
   double b1[3][PX], d1[3][PX], h2x[PX], h2y[PX];
@@ -255,7 +257,12 @@ __device__ __forceinline__ void body(const Args &a, const Item it, LdsT<PX> &L, 
 #pragma unroll
       for (int j = 0; j < PX; j++)
         for (int cc = 0; cc < 3; cc++) c.b[cc][j] = qb.b[cc][j];
-    q = load(min(k + 1, ze));
+    if (DIST == 2) {
+      q = q2;
+      q2 = load(min(k + 2, ze));
+    } else {
+      q = load(min(k + 1, ze));
+    }
     double e1[2][PX], en[3][PX], f1[3][PX];  // E^n(k+1) x, y; E^n(k); E^{n+1}(k-1)
 #pragma unroll
     for (int j = 0; j < PX; j++) {
@@ -393,9 +400,9 @@ __global__ __launch_bounds__(1024) void tbw_kernel(Args a, unsigned *ctr) {
     if (idx < 0) break;
     const Item it = a.items[idx];
     if (__builtin_amdgcn_readfirstlane(it.uw) != ~0u)
-      body<PX, true, BL>(a, it, L, sU);
+      body<PX, true, BL, (TAG >= 100 ? 2 : 1)>(a, it, L, sU);
     else
-      body<PX, false, BL>(a, it, L, sU);
+      body<PX, false, BL, (TAG >= 100 ? 2 : 1)>(a, it, L, sU);
     if (!PERS) break;
     __syncthreads();
   }
@@ -615,11 +622,10 @@ int main(int argc, char **argv) {
   }
   copy6(A0, A, n);  // the timing loops ping-pong A <-> B: each variant starts from A0
   const Variant vs[] = {
-      {"px1 list", 1, 0, 0, 0},     {"px1 pers", 1, 0, 1, 0},     {"px1 xcd", 1, 0, 0, 1},
-      {"px1 bl xcd", 1, 1, 0, 1},   {"px2 list", 2, 0, 0, 0},     {"px2 xcd", 2, 0, 0, 1},
-      {"px2 bl xcd", 2, 1, 0, 1},   {"px1 blk", 1, 0, 0, 2},      {"px2 bl blk", 2, 1, 0, 2},
-      {"px1 pq blk", 1, 0, 2, 2},   {"px2 bl pq blk", 2, 1, 2, 2}, {"px2 bl pers", 2, 1, 1, 0},
+      {"px1 pers", 1, 0, 1, 0},        {"px1 pers d2", 1, 0, 1, 0},  {"px1 pq blk", 1, 0, 2, 2},
+      {"px1 pq blk d2", 1, 0, 2, 2},   {"px1 blk d2", 1, 0, 0, 2},   {"px2 bl pers", 2, 1, 1, 0},
   };
+
   const int nv = sizeof(vs) / sizeof(vs[0]);
   std::vector<Item *> di(nv);
   std::vector<int> ni(nv), nuni(nv);
@@ -643,18 +649,12 @@ int main(int argc, char **argv) {
     if (q.pers) CK(hipMemsetAsync(ctr, 0, 8 * 32 * 4));
 #define L_(PX, BL, P, T) tbw_kernel<PX, BL, (int)(P), T><<<g, 1024>>>(a, ctr)
     switch (v) {
-      case 0: L_(1, false, false, 0); break;
-      case 1: L_(1, false, true, 1); break;
-      case 2: L_(1, false, false, 2); break;
-      case 3: L_(1, true, false, 3); break;
-      case 4: L_(2, false, false, 4); break;
-      case 5: L_(2, false, false, 5); break;
-      case 6: L_(2, true, false, 6); break;
-      case 7: L_(1, false, false, 7); break;
-      case 8: L_(2, true, false, 8); break;
-      case 9: L_(1, false, 2, 9); break;
-      case 10: L_(2, true, 2, 10); break;
-      case 11: L_(2, true, 1, 11); break;
+      case 0: L_(1, false, 1, 0); break;
+      case 1: L_(1, false, 1, 101); break;
+      case 2: L_(1, false, 2, 2); break;
+      case 3: L_(1, false, 2, 103); break;
+      case 4: L_(1, false, 0, 104); break;
+      case 5: L_(2, true, 1, 5); break;
     }
 #undef L_
   };
