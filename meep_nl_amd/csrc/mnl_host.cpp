@@ -2654,7 +2654,7 @@ int tb_plan(mnl_fields *F) {
   unsigned long long sig = 1469598103934665603ULL;
   auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
   mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
-  mix(F->rim_zchunk), mix(F->tb_ox), mix(F->tb_px);
+  mix(F->rim_zchunk), mix(F->tb_ox), mix(F->tb_px), mix(F->tb_pol_on);
   mix((long long)F->srcD_idx.size());
   for (long long v : F->srcD_idx) mix(v);
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
@@ -2757,11 +2757,48 @@ int tb_plan(mnl_fields *F) {
     if (L2.hi[0] - h.hi[0] < 8) h.hi[0] = L2.hi[0];
     holes.push_back(h);
   }
+  // polarization chunks (tile mode: the planes [pzl - 1, pzh + 2) over the whole x-y extent of
+  // G, make_tile_boxes): stepped by the general kernel, not by rim items; no two-step point
+  // within distance 2 of them (their E is stored, not chi1inv D)
+  Box P;
+  bool have_p = false;
+  if (F->f.npol > 0 && a.ngen > 0) {
+    int pzl = INT32_MAX, pzh = -1;
+    for (int k = 0; k < F->f.npol; k++)
+      if (F->f.pol[k].nz.lo[2] <= F->f.pol[k].nz.hi[2]) {
+        pzl = std::min(pzl, F->f.pol[k].nz.lo[2]);
+        pzh = std::max(pzh, F->f.pol[k].nz.hi[2]);
+      }
+    if (pzh >= 0) {
+      P = G;
+      P.lo[2] = std::max(G.lo[2], pzl - 1), P.hi[2] = std::min(G.hi[2], pzh + 1);
+      have_p = P.lo[2] <= P.hi[2];
+    }
+    if (have_p && l2) {
+      Box h = L2;
+      h.lo[2] = std::max(L2.lo[2], P.lo[2] - 2), h.hi[2] = std::min(L2.hi[2], P.hi[2] + 2);
+      if (h.lo[2] <= h.hi[2]) holes.push_back(h);
+    }
+  }
+  F->tb_pol = have_p;
   std::vector<Box> two, rim;
   if (l2) {
     tb_regions(G, L2, holes, two, rim);
   } else {
     rim.push_back(G);
+  }
+  if (have_p) {  // rim boxes minus P
+    std::vector<Box> keep;
+    for (const Box &b : rim) {
+      if (!box_meets(b, P)) {
+        keep.push_back(b);
+        continue;
+      }
+      std::vector<Box> part, inside;
+      tb_regions(b, b, {P}, part, inside);
+      keep.insert(keep.end(), part.begin(), part.end());
+    }
+    rim.swap(keep);
   }
   if (two.empty() && F->nranks == 1) return 0;
   // ---- rim items: tile-kernel shapes (columns <= 64 from 128-byte boundaries, rows <= 14,
@@ -3176,10 +3213,13 @@ int tb_mid_alloc(mnl_fields *F) {
 // Can the batch step in pairs?  Builds the plan when needed (-1: HIP error).
 int tb_usable(mnl_fields *F, bool *ok) {
   *ok = false;
-  // (no chi(2) NR box, upstream nonlinearity or polarization: the pairs have no E phase of
-  // their own; today ngen == 0 implies it, stated so it does not hang on the tile geometry)
-  bool local = F->tb_enabled && F->fused && F->tile_mode && F->fgeo.ngen == 0 && !F->nr &&
-               !F->upnl && F->f.npol == 0 &&
+  // (no chi(2) NR box or upstream nonlinearity: the pairs have no E phase of their own.
+  // Polarization chunks (tile mode: the general items are exactly those chunks) step one step
+  // at a time in the general kernel beside each rim launch, on one rank (round 6, DESIGN.md
+  // section 27); L2 keeps a distance of 2 from them)
+  const bool pol_ok = F->f.npol > 0 && F->fgeo.ngen > 0 && F->nranks == 1 && F->tb_pol_on;
+  bool local = F->tb_enabled && F->fused && F->tile_mode &&
+               ((F->fgeo.ngen == 0 && F->f.npol == 0) || pol_ok) && !F->nr && !F->upnl &&
                F->S.dim == 3 && F->slab_dir == 2 &&
                (F->dfts.empty() || F->nranks == 1);
   if (local && tb_plan(F)) return -1;
@@ -3236,6 +3276,19 @@ FusedArgs rim_args(mnl_fields *F, const FusedArgs &fa, const Set5 &o, const Set5
   r.tflag = F->d_uidx ? F->d_tb_rflag : nullptr;
   r.gbeg = 0, r.gend = (int)F->tb_ritems.size();
   r.clk.kind = 1;
+  return r;
+}
+
+// general-kernel arguments of the polarization chunks in a pair: one step from `o` to `n`
+// (P / P_prev and the f_u of D in place, as in one-step stepping)
+FusedArgs gen_args(const FusedArgs &fa, const Set5 &o, const Set5 &n) {
+  FusedArgs r = fa;
+  for (int d = 0; d < 3; d++) {
+    r.Bo[d] = o.B[d], r.Do[d] = o.D[d], r.E[d] = o.E[d], r.Ho[d] = o.H[d], r.UBo[d] = o.UB[d];
+    r.Bn[d] = n.B[d], r.Dn[d] = n.D[d], r.En[d] = n.E[d], r.Hn[d] = n.H[d], r.UBn[d] = n.UB[d];
+  }
+  r.wg_limit = 0;
+  r.lean_after = 0;
   return r;
 }
 
@@ -3332,6 +3385,12 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
   ev_end(k);
   if (kr) return fused_fail("rim kernel launch failed", kr);
+  if (F->tb_pol) {  // the polarization chunks' step n (before the sources of the step)
+    k = ev_begin(TM_GEN);
+    kr = k_fused(gen_args(fa, cur, mid), 1, F->stream, F->ctr_base);
+    ev_end(k);
+    if (kr) return fused_fail("fused general kernel launch failed", kr);
+  }
   if (tb_src(F, s0, mid.D)) return -1;
   // the guard of the middle step (its terms' points hold step n+1 in mid: rim items, or the
   // two-step items' store box)
@@ -3351,6 +3410,12 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   kr = k_tile_items(r2, r2.titems, r2.tgeo, r2.tflag, nr, 4, F->stream, F->ctr_base);
   ev_end(k);
   if (kr) return fused_fail("rim kernel launch failed", kr);
+  if (F->tb_pol) {
+    k = ev_begin(TM_GEN);
+    kr = k_fused(gen_args(fa, mid, nxt), 1, F->stream, F->ctr_base);
+    ev_end(k);
+    if (kr) return fused_fail("fused general kernel launch failed", kr);
+  }
   if (tb_src(F, s1, nxt.D)) return -1;
   swap_cur_nxt(F->f);
   nan_count(F, 1);
@@ -4140,6 +4205,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
     F->tb_zchunk = std::max(0, atoi(tz)), F->tb_zchunk_env = true;
   if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
   if (const char *tx = getenv("MNL_TB_PX")) F->tb_px = atoi(tx) == 1 ? 1 : 2;
+  if (const char *tq = getenv("MNL_TB_POL")) F->tb_pol_on = atoi(tq) != 0;
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
   if (const char *dc = getenv("MNL_DFT_CMP")) F->dft_cmp = atoi(dc) != 0;
@@ -5208,6 +5274,12 @@ int mnl_fields_kernel_stats(mnl_fields *F, int which, long long *launches, doubl
       *launches = F->timer_count[TM_TB];
       *total_ms = F->timer_ms[TM_TB] + F->timer_ms[TM_RIM];
       *bytes_per_launch = tb_b + 2.0 * rim_b;
+      if (F->fused && F->tb_have && F->tb_pol) {  // + the polarization chunks' two steps
+        double lb, gb;
+        fused_bytes(F, &lb, &gb);
+        *total_ms += F->timer_ms[TM_GEN];
+        *bytes_per_launch += 2.0 * gb;
+      }
     } else {
       *launches = F->timer_count[TM_RIM];
       *total_ms = F->timer_ms[TM_RIM];
@@ -5278,6 +5350,8 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->dft_cmp = v;
   } else if (which == 7) {
     F->nr_early = v;
+  } else if (which == 11) {  // pairs with polarization chunks (0: one-step stepping there)
+    F->tb_pol_on = v;
   } else if (which == 10) {  // columns per lane of the two-step kernel (1: round-5 kernel)
     if (value != 1 && value != 2) return fail("bad two-step layout");
     F->tb_px = value;

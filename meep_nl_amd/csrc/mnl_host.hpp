@@ -362,6 +362,9 @@ struct mnl_fields {
   bool tb_enabled = true;           // MNL_TB=0 at creation: never
   int tb_zchunk = 0;                // planes per two-step item (0: automatic)
   int rim_zchunk = 0;               // planes per rim item of a pair (0: fused_zchunk)
+  bool tb_pol_on = true;            // MNL_TB_POL=0 / set_schedule 11: no pairs with them
+  bool tb_pol = false;              // the pairs step polarization chunks (general kernel, one
+                                    // step at a time beside the rim launches; one rank)
   int tb_px = 2;                    // columns per lane of the two-step kernel (1: the round-5
                                     // kernel, for A/B; MNL_TB_PX)
   int tb_ox = 0;                    // most own columns of a two-step item (0: TB_OXW = 124,

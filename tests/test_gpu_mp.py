@@ -156,3 +156,23 @@ def test_c5_full_size_chunk_invariance(tmp_path):
         bad = np.nonzero(got[c] != ref)[0]
         assert bad.size == 0, (c, bad[:10].tolist())
     log("all planes equal")
+
+
+def test_bench_two_ranks_self_check():
+    """bench.py --gpus 2 as the driver runs it (torch.distributed.run children; here both ranks
+    share this GPU over IPC): the line carries the multi-GPU self-check -- the C5 grid of the
+    run stepped from seeded random fields over both ranks, every plane of every component
+    summed over the ranks equal to the one-rank fixture tests/golden/c5_parity_256x256x128.npz
+    (tools/make_c5_fixture.py) -- as c5_parity true with the rank count."""
+    import json
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, MNL_BENCH_DEVICE="0", MNL_IPC_TIMEOUT="300")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--size",
+                        "256", "--steps", "4", "--warmup", "2", "--no-tune", "--no-smi"],
+                       env=env, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    chk = line["c5_parity_check"]
+    assert line["c5_parity"] is True and line["c5_parity_ranks"] == 2, chk
+    assert chk["transport"] == "ipc" and chk["temporal_blocking"] and chk["bad_planes"] == []
+    assert chk["grid"] == [256, 256, 128] and chk["steps"] == 7
