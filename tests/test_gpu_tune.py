@@ -11,7 +11,7 @@ from scenarios import ALL_COMPS, GroupSim, ProductSim, make_oracle, sc_random_fi
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 SIZES = (6.4, 5.2, 9.6)  # 64 x 52 x 96 cells at resolution 10: several z chunks per length
-TOTAL = 80  # tune(reps=1) steps at most 2 + 19 * (2 + 2) = 78
+TOTAL = 100  # tune(reps=1) steps at most 2 + 22 * (2 + 2) = 90 (z chunks, CU split, pairs: 9 lengths + one-step)
 ZCS = (0, 16, 20, 24, 32, 48)
 
 
