@@ -408,6 +408,150 @@ __global__ __launch_bounds__(1024) void tbw_kernel(Args a, unsigned *ctr) {
   }
 }
 
+// ---- three steps per z-march (one column per lane, 64 x 16 lanes for 58 x 10 own points):
+// step n at plane k, step n+1 at plane k-1, step n+2 at plane k-2; per three steps a point's D,
+// B are read once and written once.  The same operand order as the two-step body.
+constexpr int HY3 = 3;
+struct alignas(16) LdsT3 {
+  double s[LY + 2][12][64];  // slots 0-5: E^n, E^{n+1}, E^{n+2} (z, x); 6-11: B^{n+1..n+3} (z, x)
+};
+template <bool UNI>
+__device__ __forceinline__ void body3(const Args &a, const Item it, LdsT3 &L, const double (*sU)[256]) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int x0 = it.x & 0xFFFF, x1 = it.x >> 16, y0 = it.y & 0xFFFF, y1 = it.y >> 16;
+  const int zs = it.z & 0xFFFF, ze = it.z >> 16;
+  const int N = a.N, zmax = N - 1;
+  const int gx = it.lx + lane, gy = y0 - HY3 + w;
+  const int cx = min(max(gx, 0), N - 1), cy = min(max(gy, 0), N - 1);
+  const unsigned col = (unsigned)((cx + cy * N) * 8);
+  const unsigned s2 = (unsigned)((long long)N * N * 8);
+  const double C = a.C;
+  const bool own = gx >= x0 && gx <= x1 && gy >= y0 && gy <= y1;
+  const unsigned nrec = (unsigned)min((long long)N * N * N * 8, 0xFFFFFFFFLL);
+  const unsigned long long pBn[3] = {(unsigned long long)sgpr_ptr(a.Bn[0]), (unsigned long long)sgpr_ptr(a.Bn[1]),
+                                     (unsigned long long)sgpr_ptr(a.Bn[2])};
+  const unsigned long long pDn[3] = {(unsigned long long)sgpr_ptr(a.Dn[0]), (unsigned long long)sgpr_ptr(a.Dn[1]),
+                                     (unsigned long long)sgpr_ptr(a.Dn[2])};
+  const gdp D0 = sgpr_ptr(a.Do[0]), D1 = sgpr_ptr(a.Do[1]), D2 = sgpr_ptr(a.Do[2]);
+  const gdp B0 = sgpr_ptr(a.Bo[0]), B1 = sgpr_ptr(a.Bo[1]), B2 = sgpr_ptr(a.Bo[2]);
+  const gup uix = (gup)sgpr_ptr(a.uidx);
+  double cu0 = 1, cu1 = 1, cu2 = 1;
+  if (UNI) cu0 = sU[0][it.uw & 255], cu1 = sU[1][(it.uw >> 8) & 255], cu2 = sU[2][(it.uw >> 16) & 255];
+  auto uv = [&](unsigned ui, int c) -> double {
+    if (UNI) return c == 0 ? cu0 : (c == 1 ? cu1 : cu2);
+    return sU[c][(ui >> (8 * c)) & 255];
+  };
+  struct Q {
+    double d0, d1, d2, b0, b1, b2;
+    unsigned ui;
+  };
+  auto zc = [zmax](int z) { return min(max(z, 0), zmax); };
+  auto load = [&](int k) -> Q {
+    Q q;
+    const unsigned o1 = col + (unsigned)zc(k + 1) * s2, ob = col + (unsigned)zc(k) * s2;
+    q.d0 = ld1(D0, o1), q.d1 = ld1(D1, o1), q.d2 = ld1(D2, o1);
+    q.ui = UNI ? 0u : ldu1(uix, o1 >> 1);
+    q.b0 = ld1(B0, ob), q.b1 = ld1(B1, ob), q.b2 = ld1(B2, ob);
+    return q;
+  };
+  const int k0 = zs - 3;
+  double dn0, dn1, dn2;
+  unsigned uk, u1, u2;
+  {
+    const unsigned o = col + (unsigned)zc(k0) * s2;
+    dn0 = ld1(D0, o), dn1 = ld1(D1, o), dn2 = ld1(D2, o);
+    uk = UNI ? 0u : ldu1(uix, o >> 1);
+    u1 = u2 = uk;
+  }
+  Q q = load(k0);
+  double b1x = 0, b1y = 0, b1z = 0, d1x = 0, d1y = 0, d1z = 0;  // B^{n+1}(k-1), D^{n+1}(k-1)
+  double b2x = 0, b2y = 0, b2z = 0, d2x = 0, d2y = 0, d2z = 0;  // B^{n+2}(k-2), D^{n+2}(k-2)
+  double h3x = 0, h3y = 0;                                      // B^{n+3}(k-3) x, y
+  double *bp = &L.s[0][0][0] + (w * 12 * 64 + lane);
+#define L3(row, slot) bp[(row) * 12 * 64 + (slot) * 64]
+  for (int k = k0; k <= ze + 1; k++) {
+    const Q c = q;
+    q = load(min(k + 1, ze + 1));
+    const double enx = dn0 * uv(uk, 0), eny = dn1 * uv(uk, 1), enz = dn2 * uv(uk, 2);
+    const double e1x = c.d0 * uv(c.ui, 0), e1y = c.d1 * uv(c.ui, 1);
+    const double f1x = d1x * uv(u1, 0), f1y = d1y * uv(u1, 1), f1z = d1z * uv(u1, 2);
+    const double g2x = d2x * uv(u2, 0), g2y = d2y * uv(u2, 1), g2z = d2z * uv(u2, 2);
+    L3(1, 0) = enz, L3(1, 1) = enx, L3(1, 2) = f1z, L3(1, 3) = f1x;
+    L3(1, 4) = g2z, L3(1, 5) = g2x;
+    __syncthreads();
+    // step n at k
+    const double Bx = c.b0 - C * (L3(2, 0) - enz + eny - e1y);
+    const double By = c.b1 - C * (e1x - enx + enz - lane_next(enz));
+    const double Bz = c.b2 - C * (lane_next(eny) - eny + enx - L3(2, 1));
+    // the y-neighbours of E^{n+1}(k-1) and E^{n+2}(k-2) (written at the top of this plane)
+    const double g2zy = L3(2, 4), g2xy = L3(2, 5);
+    const double f1zy = L3(2, 2), f1xy = L3(2, 3);
+    L3(1, 6) = Bz, L3(1, 7) = Bx;
+    __syncthreads();
+    const double Dx = dn0 - C * (L3(0, 6) - Bz + By - b1y);
+    const double Dy = dn1 - C * (b1x - Bx + Bz - lane_prev(Bz));
+    const double Dz = dn2 - C * (lane_prev(By) - By + Bx - L3(0, 7));
+    const double Ex = Dx * uv(uk, 0), Ey = Dy * uv(uk, 1);
+    // step n+1 at k-1
+    const double Fx = b1x - C * (f1zy - f1z + f1y - Ey);
+    const double Fy = b1y - C * (Ex - f1x + f1z - lane_next(f1z));
+    const double Fz = b1z - C * (lane_next(f1y) - f1y + f1x - f1xy);
+    L3(1, 8) = Fz, L3(1, 9) = Fx;
+    __syncthreads();
+    const double Gx = d1x - C * (L3(0, 8) - Fz + Fy - b2y);
+    const double Gy = d1y - C * (b2x - Fx + Fz - lane_prev(Fz));
+    const double Gz = d1z - C * (lane_prev(Fy) - Fy + Fx - L3(0, 9));
+    const double Gex = Gx * uv(u1, 0), Gey = Gy * uv(u1, 1);
+    // step n+2 at k-2
+    const double Kx = b2x - C * (g2zy - g2z + g2y - Gey);
+    const double Ky = b2y - C * (Gex - g2x + g2z - lane_next(g2z));
+    const double Kz = b2z - C * (lane_next(g2y) - g2y + g2x - g2xy);
+    L3(1, 10) = Kz, L3(1, 11) = Kx;
+    __syncthreads();
+    const double Mx = d2x - C * (L3(0, 10) - Kz + Ky - h3y);
+    const double My = d2y - C * (h3x - Kx + Kz - lane_prev(Kz));
+    const double Mz = d2z - C * (lane_prev(Ky) - Ky + Kx - L3(0, 11));
+    {
+      const bool st = own && k - 2 >= zs && k - 2 < ze;
+      const unsigned os = st ? col + (unsigned)(k - 2) * s2 : OOB;
+      st1(brsrc_at(pBn[0], nrec), os, Kx);
+      st1(brsrc_at(pBn[1], nrec), os, Ky);
+      st1(brsrc_at(pBn[2], nrec), os, Kz);
+      st1(brsrc_at(pDn[0], nrec), os, Mx);
+      st1(brsrc_at(pDn[1], nrec), os, My);
+      st1(brsrc_at(pDn[2], nrec), os, Mz);
+    }
+    h3x = Kx, h3y = Ky;
+    b2x = Fx, b2y = Fy, b2z = Fz, d2x = Gx, d2y = Gy, d2z = Gz, u2 = u1;
+    b1x = Bx, b1y = By, b1z = Bz, d1x = Dx, d1y = Dy, d1z = Dz, u1 = uk;
+    dn0 = c.d0, dn1 = c.d1, dn2 = c.d2, uk = c.ui;
+  }
+#undef L3
+}
+
+template <int TAG>
+__global__ __launch_bounds__(1024) void tbw3_kernel(Args a, unsigned *ctr) {
+  __shared__ double sU[3][256];
+  __shared__ LdsT3 L;
+  __shared__ int s_idx;
+  for (int i = threadIdx.x; i < 3 * 256; i += 1024) sU[i >> 8][i & 255] = a.utab[i];
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned v = atomicAdd(ctr, 1u);
+      s_idx = v < (unsigned)a.nitems ? (int)v : -1;
+    }
+    __syncthreads();
+    const int idx = s_idx;
+    if (idx < 0) break;
+    const Item it = a.items[idx];
+    if (__builtin_amdgcn_readfirstlane(it.uw) != ~0u)
+      body3<true>(a, it, L, sU);
+    else
+      body3<false>(a, it, L, sU);
+    __syncthreads();
+  }
+}
+
 // ---- naive pair of steps over [2, N-3]^3 (the same expressions, one point per thread)
 struct NArgs {
   int N;
@@ -513,19 +657,19 @@ static bool same_own(F6 a, F6 b, int N, int lo, int hi, const char *what) {
 // list takes run b % 8's item b / 8, z chunk outer), so each XCD marches a y-band of tiles
 // whose halo rows its L2 shares
 static std::vector<Item> make_items(int N, int lo, int hi, int ow, int tz, const std::vector<unsigned> &u,
-                                    int xcd, int *qoff = nullptr) {
-  const int W = hi - lo + 1, nty = (W + 11) / 12, nch = (W + tz - 1) / tz, ntx = (W + ow - 1) / ow;
+                                    int xcd, int *qoff = nullptr, int H = 2, int OR = 12) {
+  const int W = hi - lo + 1, nty = (W + OR - 1) / OR, nch = (W + tz - 1) / tz, ntx = (W + ow - 1) / ow;
   auto mk = [&](int ch, int ty, int tx) {
     Item it;
     const int x0 = lo + ow * tx, x1 = std::min(x0 + ow - 1, hi);
     const int y0 = lo + W * ty / nty, y1 = lo + W * (ty + 1) / nty - 1;
     const int zs = lo + W * ch / nch, ze = lo + W * (ch + 1) / nch;
-    it.x = x0 | (x1 << 16), it.y = y0 | (y1 << 16), it.z = zs | (ze << 16), it.lx = x0 - 2;
-    unsigned ref = u[(x0 - 2) + (long long)N * ((y0 - 2) + (long long)N * (zs - 2))];
+    it.x = x0 | (x1 << 16), it.y = y0 | (y1 << 16), it.z = zs | (ze << 16), it.lx = x0 - H;
+    unsigned ref = u[(x0 - H) + (long long)N * ((y0 - H) + (long long)N * (zs - H))];
     bool uni = true;
-    for (int k = zs - 2; k <= ze + 1 && uni; k++)
-      for (int j = y0 - 2; j <= y1 + 2 && uni; j++)
-        for (int i = x0 - 2; i <= x1 + 2; i++)
+    for (int k = zs - H; k <= ze + H - 1 && uni; k++)
+      for (int j = y0 - H; j <= y1 + H && uni; j++)
+        for (int i = x0 - H; i <= x1 + H; i++)
           if (u[i + (long long)N * (j + (long long)N * k)] != ref) {
             uni = false;
             break;
@@ -574,7 +718,7 @@ static std::vector<Item> make_items(int N, int lo, int hi, int ow, int tz, const
 
 struct Variant {
   const char *name;
-  int px, bl, pers, xcd;
+  int px, bl, pers, xcd, steps;
 };
 
 int main(int argc, char **argv) {
@@ -588,7 +732,7 @@ int main(int argc, char **argv) {
     fprintf(stderr, "bad shape\n");
     return 1;
   }
-  F6 A = alloc6(n), B = alloc6(n), R = alloc6(n), S = alloc6(n), A0 = alloc6(n);
+  F6 A = alloc6(n), B = alloc6(n), R = alloc6(n), S = alloc6(n), A0 = alloc6(n), R3 = alloc6(n);
   unsigned *du, *ctr;
   double *dt;
   CK(hipMalloc(&du, n * 4));
@@ -618,21 +762,27 @@ int main(int argc, char **argv) {
     for (int c = 0; c < 3; c++) nb.D[c] = S.d[c], nb.B[c] = S.b[c], nb.Dt[c] = R.d[c], nb.Bt[c] = R.b[c];
     naive_b<<<8192, 256>>>(nb);
     naive_d<<<8192, 256>>>(nb);
+    NArgs nc = na;  // a third step R -> R3
+    for (int c = 0; c < 3; c++) nc.D[c] = R.d[c], nc.B[c] = R.b[c], nc.Dt[c] = R3.d[c], nc.Bt[c] = R3.b[c];
+    naive_b<<<8192, 256>>>(nc);
+    naive_d<<<8192, 256>>>(nc);
     CK(hipDeviceSynchronize());
   }
   copy6(A0, A, n);  // the timing loops ping-pong A <-> B: each variant starts from A0
   const Variant vs[] = {
-      {"px1 pers", 1, 0, 1, 0},        {"px1 pers d2", 1, 0, 1, 0},  {"px1 pq blk", 1, 0, 2, 2},
-      {"px1 pq blk d2", 1, 0, 2, 2},   {"px1 blk d2", 1, 0, 0, 2},   {"px2 bl pers", 2, 1, 1, 0},
+      {"px1 pers", 1, 0, 1, 0, 2},   {"px2 bl pers", 2, 1, 1, 0, 2},   {"3-step px1 pers", 1, 0, 1, 0, 3},
   };
+
 
   const int nv = sizeof(vs) / sizeof(vs[0]);
   std::vector<Item *> di(nv);
   std::vector<int> ni(nv), nuni(nv);
   std::vector<std::vector<int>> qo(nv, std::vector<int>(9, 0));
   for (int v = 0; v < nv; v++) {
-    std::vector<Item> items = make_items(N, lo, hi, vs[v].px == 1 ? 60 : 124, tz, hu, vs[v].xcd,
-                                         vs[v].pers == 2 ? qo[v].data() : nullptr);
+    const bool three = vs[v].steps == 3;
+    std::vector<Item> items = make_items(N, lo, hi, three ? 58 : vs[v].px == 1 ? 60 : 124, tz, hu,
+                                         vs[v].xcd, vs[v].pers == 2 ? qo[v].data() : nullptr,
+                                         three ? 3 : 2, three ? 10 : 12);
     CK(hipMalloc(&di[v], items.size() * sizeof(Item)));
     CK(hipMemcpy(di[v], items.data(), items.size() * sizeof(Item), hipMemcpyHostToDevice));
     ni[v] = (int)items.size();
@@ -650,11 +800,8 @@ int main(int argc, char **argv) {
 #define L_(PX, BL, P, T) tbw_kernel<PX, BL, (int)(P), T><<<g, 1024>>>(a, ctr)
     switch (v) {
       case 0: L_(1, false, 1, 0); break;
-      case 1: L_(1, false, 1, 101); break;
-      case 2: L_(1, false, 2, 2); break;
-      case 3: L_(1, false, 2, 103); break;
-      case 4: L_(1, false, 0, 104); break;
-      case 5: L_(2, true, 1, 5); break;
+      case 1: L_(2, true, 1, 5); break;
+      case 2: tbw3_kernel<0><<<g, 1024>>>(a, ctr); break;
     }
 #undef L_
   };
@@ -664,7 +811,7 @@ int main(int argc, char **argv) {
     copy6(B, A, n);
     launch(v, A, B);
     CK(hipDeviceSynchronize());
-    const bool ok = same_own(B, R, N, lo, hi, vs[v].name);
+    const bool ok = same_own(B, vs[v].steps == 3 ? R3 : R, N, lo, hi, vs[v].name);
     printf("%-12s %s (%d items, %d uniform)\n", vs[v].name, ok ? "bitwise" : "DIFFERS", ni[v], nuni[v]);
     all = all && ok;
   }
@@ -691,8 +838,8 @@ int main(int argc, char **argv) {
     const double med = x[x.size() / 2];
     printf("%-12s tz %d: median %.4f ms per launch (2 steps) [", vs[v].name, tz, med);
     for (double y : ms[v]) printf(" %.4f", y);
-    printf(" ], %.1f G cell-steps/s, %.2f TB/s algorithmic (96 B per 2 cell-steps)\n",
-           2 * cells / med / 1e6, cells * 96.0 / med / 1e9);
+    printf(" ], %.1f G cell-steps/s, %.2f TB/s algorithmic (96 B per point per launch)\n",
+           vs[v].steps * cells / med / 1e6, cells * 96.0 / med / 1e9);
   }
   return all ? 0 : 2;
 }
