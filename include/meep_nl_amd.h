@@ -368,7 +368,8 @@ int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, doubl
  * rim cells, mixed-palette rim cells, two-step items, rim items, planes of the
  * first two-step item (the longest), narrow x-face strip items among the rim items,
  * enabled (pairs allowed: set_temporal_blocking / MNL_TB / the tuner), the two-step chunk
- * setting (0: automatic). */
+ * setting (0: automatic), the most own columns of a two-step item (124 unless set or tuned),
+ * polarization chunks stepped inside the pairs (1). */
 int mnl_fields_tb_info(mnl_fields *f, double *out, int n);
 /* Allow (1, the default; MNL_TB=0 at creation turns it off) or forbid (0) stepping
  * pairs of steps with the two-step kernel.  Results are identical either way. */
@@ -383,8 +384,9 @@ int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
  * 6 planes per rim item of a pair (value; 0 = the one-step chunk length), 7 the chi(2) NR box's
  * E phase beside the tile kernel (MNL_NR_EARLY), 8 planes per two-step item (value; 0 =
  * automatic; MNL_TB_ZCHUNK), 9 the most own columns of a two-step item (value 4..124; 0 = 124,
- * the widest the kernel's 128 columns of lanes hold).  For in-process A/B measurements
- * (tools/ab_inproc.py). */
+ * the widest the kernel's 128 columns of lanes hold), 10 columns per lane of the two-step kernel
+ * (2; 1 = the round-5 kernel; MNL_TB_PX), 11 pairs of steps with polarization chunks (1, the
+ * default; MNL_TB_POL).  For in-process A/B measurements (tools/ab_inproc.py). */
 int mnl_fields_set_schedule(mnl_fields *f, int which, int value);
 
 /* ---- checkpoint (src/fields_dump.cpp, src/structure_dump.cpp) -----------

@@ -395,13 +395,14 @@ class Fields:
     def step(self, n=1):
         check(lib().mnl_fields_step(self.h, int(n)))
 
-    def tune(self, reps=3):
+    def tune(self, reps=8):
         """Time the fused step's knobs over real steps and keep the fastest (mnl_fields_tune:
         the tile kernel's z-chunk length, then on one rank with polarization chunks the CUs
-        of their general kernel beside the tile kernel; with temporal blocking the planes of
-        its two-step items).  Every candidate runs two warm-up steps and reps (rounded up to
-        even) timed ones: at most 2 + 19 * (2 + reps) steps, results identical to plain
-        stepping.  Returns (zchunk, gen_cus); -1 = not tuned (not in the fused tile mode)."""
+        of their general kernel beside the tile kernel; with temporal blocking the planes and
+        widths of its two-step items).  Every candidate runs two warm-up steps and reps
+        (rounded up to even) timed ones: at most 2 + 32 * (2 + reps) steps, results identical
+        to plain stepping (round 6: 8 timed steps by default, 4 gave choices off by up to 10 %
+        at 256^3).  Returns (zchunk, gen_cus); -1 = not tuned (not in the fused tile mode)."""
         z, g = ctypes.c_int(0), ctypes.c_int(0)
         check(lib().mnl_fields_tune(self.h, int(reps), ctypes.byref(z), ctypes.byref(g)))
         return z.value, g.value
@@ -602,14 +603,15 @@ class Fields:
         """Temporal blocking of the current fused geometry: dict of
         active (the last call of >= 2 steps stepped in pairs), two-step own cells / border
         points / mixed-palette cells, rim cells / mixed-palette rim cells, item counts, the
-        first item's planes, the narrow x-face strip items among the rim items, and the
-        two-step chunk setting (0: automatic)."""
-        v = (ctypes.c_double * 12)()
-        check(lib().mnl_fields_tb_info(self.h, v, 12))
+        first item's planes, the narrow x-face strip items among the rim items, the
+        two-step chunk setting (0: automatic), the most own columns of a two-step item and
+        whether polarization chunks step inside the pairs."""
+        v = (ctypes.c_double * 14)()
+        check(lib().mnl_fields_tb_info(self.h, v, 14))
         keys = ("active", "tb_cells", "tb_border", "tb_cells_mixed", "rim_cells",
                 "rim_cells_mixed", "tb_items", "rim_items", "tb_planes", "narrow_items", "enabled",
-                "tb_zchunk")
-        flags = ("active", "enabled")
+                "tb_zchunk", "tb_width", "tb_pol")
+        flags = ("active", "enabled", "tb_pol")
         return {k: (bool(x) if k in flags else int(x)) for k, x in zip(keys, v)}
 
     def traffic_model(self):

@@ -4932,21 +4932,32 @@ int mnl_fields_tune(mnl_fields *F, int reps, int *zchunk, int *gen_cus) {
   // rounds), and whether pairs beat one-step stepping at all (small grids: the rim is a
   // large share of the cells)
   if (!rc && F->fused && F->tb_have && F->tb_enabled) {
-    const int tz0 = F->tb_zchunk;
-    int best = tz0;
+    const int tz0 = F->tb_zchunk, ox0 = F->tb_ox;
+    int best = tz0, best_ox = ox0;
     double best_ms = 0;
     // (16 / 24 / 40 added in round 5: 256^3 C2 runs 6 % faster at 16-24 planes than with the
-    // automatic length, profiles/r05_ab_tb_zchunk_c2_256.json)
-    for (int c : {0, 16, 24, 32, 40, 48, 64, 96, 128}) {
-      if (F->tb_zchunk_env && c != tz0) continue;
-      F->tb_zchunk = c;
-      double tm, gm;
-      if (timed(&tm, &gm)) { rc = -1; break; }
-      if (verbose)
-        fprintf(stderr, "tune rank %d: two-step planes %d: %.4f ms/step\n", F->rank, c, tm + gm);
-      if (best_ms == 0 || tm + gm < best_ms) best_ms = tm + gm, best = c;
+    // automatic length, profiles/r05_ab_tb_zchunk_c2_256.json.  Round 6: the items hold up to
+    // 124 columns, so a small grid has few of them per plane; 60-column items (half the lanes
+    // idle, twice the items) and 12 / 20 planes are tried too, against the tail of a launch
+    // with fewer items than a few rounds of CUs)
+    for (int ox : {0, 60}) {
+      if (F->tb_ox_set && ox != ox0) continue;
+      F->tb_ox = ox;
+      for (int c : {0, 12, 16, 20, 24, 32, 40, 48, 64, 96, 128}) {
+        if (F->tb_zchunk_env && c != tz0) continue;
+        if (ox == 60 && c > 48) continue;  // the narrow items only help small grids
+        F->tb_zchunk = c;
+        double tm, gm;
+        if (timed(&tm, &gm)) { rc = -1; break; }
+        if (verbose)
+          fprintf(stderr, "tune rank %d: two-step planes %d, width %d: %.4f ms/step\n", F->rank,
+                  c, ox ? ox : TB_OXW, tm + gm);
+        if (best_ms == 0 || tm + gm < best_ms) best_ms = tm + gm, best = c, best_ox = ox;
+      }
+      if (rc) break;
     }
     F->tb_zchunk = rc ? tz0 : best;
+    F->tb_ox = rc ? ox0 : best_ox;
     if (!rc && !F->tb_env) {
       F->tb_enabled = false;
       double tm, gm;
@@ -5358,6 +5369,7 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
   } else if (which == 9) {  // most own columns of a two-step item (0: TB_OXW = 124)
     if (value != 0 && (value < 4 || value > TB_OXW)) return fail("bad two-step width");
     F->tb_ox = value;
+    F->tb_ox_set = value != 0;  // the tuner keeps a width that was set
   } else if (which == 8) {  // planes per two-step item (0: automatic)
     if (value < 0 || value > 4096) return fail("bad two-step chunk");
     F->tb_zchunk = value;
@@ -5376,7 +5388,7 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
 
 int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
   if (!F || !out || n < 1) return fail("bad argument");
-  const double v[12] = {F->fused && F->tb_have && F->tb_enabled && F->tb_last ? 1.0 : 0.0,
+  const double v[14] = {F->fused && F->tb_have && F->tb_enabled && F->tb_last ? 1.0 : 0.0,
                        F->tb_cells,
                        F->tb_border,
                        F->tb_cells_nu,
@@ -5388,8 +5400,10 @@ int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
                                                           (F->tb_items[0].z & 0xFFFF)),
                        double(F->tb_nnarrow),
                        F->tb_enabled ? 1.0 : 0.0,
-                       double(F->tb_zchunk)};  // the setting (0: automatic)
-  for (int i = 0; i < n && i < 12; i++) out[i] = v[i];
+                       double(F->tb_zchunk),  // the setting (0: automatic)
+                       double(F->tb_ox ? F->tb_ox : TB_OXW),  // most own columns of an item
+                       F->tb_pol ? 1.0 : 0.0};  // polarization chunks stepped inside the pairs
+  for (int i = 0; i < n && i < 14; i++) out[i] = v[i];
   return 0;
 }
 

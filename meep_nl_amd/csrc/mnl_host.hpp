@@ -367,6 +367,7 @@ struct mnl_fields {
                                     // step at a time beside the rim launches; one rank)
   int tb_px = 2;                    // columns per lane of the two-step kernel (1: the round-5
                                     // kernel, for A/B; MNL_TB_PX)
+  bool tb_ox_set = false;           // tb_ox set by set_schedule (the tuner keeps it)
   int tb_ox = 0;                    // most own columns of a two-step item (0: TB_OXW = 124,
                                     // the 128 columns of lanes less two halo columns per side)
   bool nr_early = true;             // MNL_NR_EARLY=0: the NR box's E phase after both kernels
