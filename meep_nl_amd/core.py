@@ -590,10 +590,12 @@ class Fields:
         two-step item (an integer; 0 automatic), 'tb_ox' = the most own columns of a two-step
         item (4..124; 0 = 124), 'tb_px' = columns per lane of the two-step kernel (2; 1 = the
         round-5 kernel, kept for A/B), 'tb_pol' = pairs of steps with polarization chunks
-        (their general kernel one step at a time beside the rim launches) (mnl_fields_set_schedule)."""
+        (their general kernel one step at a time beside the rim launches), 'r1_beside' = the
+        first rim launch's items other than the narrow strips on a side stream beside the
+        two-step kernel (mnl_fields_set_schedule)."""
         idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4, "dft_cmp": 5,
                "rim_zchunk": 6, "nr_early": 7, "tb_zchunk": 8, "tb_ox": 9, "tb_px": 10,
-               "tb_pol": 11}[which]
+               "tb_pol": 11, "r1_beside": 12}[which]
         if idx in (2, 3, 4, 6, 8, 9, 10):  # integers: CUs left free (-1: the default), planes
             check(lib().mnl_fields_set_schedule(self.h, idx, int(value)))
         else:

@@ -2956,6 +2956,15 @@ int tb_plan(mnl_fields *F) {
     for (auto *v : {&heavy, &lean})
       for (const RI &it : *v)
         if (it.dep == (dep == 1)) order.push_back(it);
+  // one rank: the narrow strips (they read the two-step kernel's output) last, so that R1's
+  // other items can run beside the two-step kernel (tb_pair, tb_r1a)
+  F->tb_rs0 = (int)order.size();
+  if (F->nranks == 1) {
+    auto strip = [](const RI &r) { return ((r.code >> 30) & 1) != 0; };
+    std::stable_partition(order.begin(), order.end(), [&](const RI &r) { return !strip(r); });
+    F->tb_rs0 = 0;
+    for (const RI &it : order) F->tb_rs0 += strip(it) ? 0 : 1;
+  }
   F->tb_rfree = 0;
   for (const RI &it : order) F->tb_rfree += it.dep ? 0 : 1;
   for (auto *v : {&order})
@@ -3377,14 +3386,41 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
     if (rl > 0) t.wg_limit = std::max(1, k_cu_count() - rl);
     if (rr > 0) r1.wg_limit = r2.wg_limit = std::max(1, k_cu_count() - rr);
   }
-  int k = ev_begin(TM_TB);
-  int kr = k_tb2(t, F->stream, F->ctr_base);
-  ev_end(k);
+  // R1's items other than the narrow strips read only cur and write rim points of mid: they
+  // run on a side stream beside L, taking the CUs L's workgroups leave at the end of its queue
+  // (the strips read L's border values of mid and follow L).  One timing span covers L and R1
+  const int na = F->tb_r1a && !F->tb_pol ? std::min(F->tb_rs0, nr) : 0;
+  if (na > 0 && !F->s_aux) {
+    HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming));
+  }
+  int k = ev_begin(na > 0 ? TM_TB : TM_TB);
+  int kr = 0;
+  if (na > 0) {
+    HIPCHK(hipEventRecord(F->ev_start, F->stream));
+    HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
+  }
+  kr = k_tb2(t, F->stream, F->ctr_base);
   if (kr) return fused_fail("two-step kernel launch failed", kr);
-  k = ev_begin(TM_RIM);
-  kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
-  ev_end(k);
-  if (kr) return fused_fail("rim kernel launch failed", kr);
+  if (na > 0) {
+    kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, na, 5, F->s_aux, F->ctr_base);
+    if (kr) return fused_fail("rim kernel launch failed", kr);
+    HIPCHK(hipEventRecord(F->ev_early, F->s_aux));
+    if (nr > na) {
+      kr = k_tile_items(r1, r1.titems + na, r1.tgeo + 4 * na, r1.tflag ? r1.tflag + na : nullptr,
+                        nr - na, 4, F->stream, F->ctr_base);
+      if (kr) return fused_fail("rim kernel launch failed", kr);
+    }
+    HIPCHK(hipStreamWaitEvent(F->stream, F->ev_early, 0));
+    ev_end(k);
+  } else {
+    ev_end(k);
+    k = ev_begin(TM_RIM);
+    kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
+    ev_end(k);
+    if (kr) return fused_fail("rim kernel launch failed", kr);
+  }
   if (F->tb_pol) {  // the polarization chunks' step n (before the sources of the step)
     k = ev_begin(TM_GEN);
     kr = k_fused(gen_args(fa, cur, mid), 1, F->stream, F->ctr_base);
@@ -4206,6 +4242,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tn = getenv("MNL_TB_NARROW")) F->tb_narrow = atoi(tn) != 0;
   if (const char *tx = getenv("MNL_TB_PX")) F->tb_px = atoi(tx) == 1 ? 1 : 2;
   if (const char *tq = getenv("MNL_TB_POL")) F->tb_pol_on = atoi(tq) != 0;
+  if (const char *ta = getenv("MNL_TB_R1A")) F->tb_r1a = atoi(ta) != 0;
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
   if (const char *dc = getenv("MNL_DFT_CMP")) F->dft_cmp = atoi(dc) != 0;
@@ -5363,6 +5400,8 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->nr_early = v;
   } else if (which == 11) {  // pairs with polarization chunks (0: one-step stepping there)
     F->tb_pol_on = v;
+  } else if (which == 12) {  // R1's non-strip items beside the two-step kernel (one rank)
+    F->tb_r1a = v;
   } else if (which == 10) {  // columns per lane of the two-step kernel (1: round-5 kernel)
     if (value != 1 && value != 2) return fail("bad two-step layout");
     F->tb_px = value;

@@ -363,6 +363,9 @@ struct mnl_fields {
   int tb_zchunk = 0;                // planes per two-step item (0: automatic)
   int rim_zchunk = 0;               // planes per rim item of a pair (0: fused_zchunk)
   bool tb_pol_on = true;            // MNL_TB_POL=0 / set_schedule 11: no pairs with them
+  bool tb_r1a = true;               // MNL_TB_R1A=0 / set_schedule 12: R1 after the two-step
+                                    // kernel instead of its non-strip items beside it
+  int tb_rs0 = 0;                   // rim items before the narrow strips (one rank)
   bool tb_pol = false;              // the pairs step polarization chunks (general kernel, one
                                     // step at a time beside the rim launches; one rank)
   int tb_px = 2;                    // columns per lane of the two-step kernel (1: the round-5

@@ -80,14 +80,18 @@ def oracle_tb():
 
 @pytest.mark.parametrize("schedule", [(("rim_zchunk", 12),), (("res", 16),), (("res_rim", 40),),
                                       (("res_tb2", 24), ("narrow", 0)), (("tb_ox", 60),),
-                                      (("tb_ox", 60), ("tb_zchunk", 5))],
+                                      (("tb_ox", 60), ("tb_zchunk", 5)), (("tb_ox", 37),),
+                                      (("tb_ox", 9), ("tb_zchunk", 3)), (("tb_px", 1),),
+                                      (("tb_px", 1), ("tb_ox", 60))],
                          ids=["rim_zchunk12", "res16", "res_rim40", "res_tb2_24_wide", "ox60",
-                              "ox60_z5"])
+                              "ox60_z5", "ox37_odd_starts", "ox9_z3", "px1", "px1_ox60"])
 def test_tb_schedule_options_bitwise(oracle_tb, schedule):
     """The scheduling options of Fields.set_schedule (rim item length, CUs left free by the
-    pair launches, the strip body, 60-column two-step items at any lane alignment, short
-    two-step chunks) change only how the same per-point arithmetic is laid out: bitwise the
-    oracle."""
+    pair launches, the strip body, two-step item widths -- 37 columns puts every other item's
+    first column on an odd x (lane 0 three columns left of it, own ranges that start and end
+    inside a lane's column pair: the 8-byte store paths), 9 columns many ragged items -- short
+    two-step chunks, the round-5 one-column-per-lane kernel) change only how the same per-point
+    arithmetic is laid out: bitwise the oracle."""
     p = sc_tb(ProductSim, profile=True, schedule=schedule)
     assert p._fields().tb_info()["active"] and p._fields().kernel_stats(5)[0] >= 4
     _same(p, oracle_tb)
