@@ -369,7 +369,9 @@ int mnl_fields_kernel_stats(mnl_fields *f, int which, long long *launches, doubl
  * first two-step item (the longest), narrow x-face strip items among the rim items,
  * enabled (pairs allowed: set_temporal_blocking / MNL_TB / the tuner), the two-step chunk
  * setting (0: automatic), the most own columns of a two-step item (124 unless set or tuned),
- * polarization chunks stepped inside the pairs (1). */
+ * polarization chunks stepped inside the pairs (1), interior two-step items (their two-step
+ * footprint meets no rim box; one rank runs them beside the previous pair's second rim
+ * launch). */
 int mnl_fields_tb_info(mnl_fields *f, double *out, int n);
 /* Allow (1, the default; MNL_TB=0 at creation turns it off) or forbid (0) stepping
  * pairs of steps with the two-step kernel.  Results are identical either way. */
@@ -386,7 +388,12 @@ int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
  * automatic; MNL_TB_ZCHUNK), 9 the most own columns of a two-step item (value 4..124; 0 = 124,
  * the widest the kernel's 128 columns of lanes hold), 10 columns per lane of the two-step kernel
  * (2; 1 = the round-5 kernel; MNL_TB_PX), 11 pairs of steps with polarization chunks (1, the
- * default; MNL_TB_POL).  For in-process A/B measurements (tools/ab_inproc.py). */
+ * default; MNL_TB_POL), 12 the first rim launch's items other than the narrow x-face strips on a
+ * side stream beside the two-step kernel (1, the default; one rank; MNL_TB_R1A), 13 the
+ * interior two-step items on a third stream beside the previous pair's second rim launch (1;
+ * 0, the default: measured slower at 512^3; one rank, no DFT monitors;
+ * MNL_TB_LINT).  For in-process A/B measurements
+ * (tools/ab_inproc.py). */
 int mnl_fields_set_schedule(mnl_fields *f, int which, int value);
 
 /* ---- checkpoint (src/fields_dump.cpp, src/structure_dump.cpp) -----------

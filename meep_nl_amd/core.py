@@ -592,11 +592,12 @@ class Fields:
         round-5 kernel, kept for A/B), 'tb_pol' = pairs of steps with polarization chunks
         (their general kernel one step at a time beside the rim launches), 'r1_beside' = the
         first rim launch's items other than the narrow strips on a side stream beside the
-        two-step kernel (mnl_fields_set_schedule)."""
+        two-step kernel, 'tb_lint' = the interior two-step items on a third stream beside the
+        previous pair's second rim launch (mnl_fields_set_schedule)."""
         idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4, "dft_cmp": 5,
                "rim_zchunk": 6, "nr_early": 7, "tb_zchunk": 8, "tb_ox": 9, "tb_px": 10,
-               "tb_pol": 11, "r1_beside": 12}[which]
-        if idx in (2, 3, 4, 6, 8, 9, 10):  # integers: CUs left free (-1: the default), planes
+               "tb_pol": 11, "r1_beside": 12, "tb_lint": 13}[which]
+        if idx in (2, 3, 4, 6, 8, 9, 10, 13):  # integers: CUs left free (-1: the default), planes
             check(lib().mnl_fields_set_schedule(self.h, idx, int(value)))
         else:
             check(lib().mnl_fields_set_schedule(self.h, idx, 1 if value else 0))
@@ -606,13 +607,15 @@ class Fields:
         active (the last call of >= 2 steps stepped in pairs), two-step own cells / border
         points / mixed-palette cells, rim cells / mixed-palette rim cells, item counts, the
         first item's planes, the narrow x-face strip items among the rim items, the
-        two-step chunk setting (0: automatic), the most own columns of a two-step item and
-        whether polarization chunks step inside the pairs."""
-        v = (ctypes.c_double * 14)()
-        check(lib().mnl_fields_tb_info(self.h, v, 14))
+        two-step chunk setting (0: automatic), the most own columns of a two-step item,
+        whether polarization chunks step inside the pairs and the interior two-step items (their
+        footprint meets no rim box: one rank runs them beside the previous pair's second rim
+        launch)."""
+        v = (ctypes.c_double * 15)()
+        check(lib().mnl_fields_tb_info(self.h, v, 15))
         keys = ("active", "tb_cells", "tb_border", "tb_cells_mixed", "rim_cells",
                 "rim_cells_mixed", "tb_items", "rim_items", "tb_planes", "narrow_items", "enabled",
-                "tb_zchunk", "tb_width", "tb_pol")
+                "tb_zchunk", "tb_width", "tb_pol", "tb_interior_items")
         flags = ("active", "enabled", "tb_pol")
         return {k: (bool(x) if k in flags else int(x)) for k, x in zip(keys, v)}
 

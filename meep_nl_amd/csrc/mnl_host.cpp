@@ -2651,10 +2651,11 @@ int dev_upload(mnl_fields *F, T **d, size_t &cap, const std::vector<T> &h) {
 // Build (or keep) the plan of the current fused geometry and source points.  No plan (tb_have
 // false) when L2 is empty or an item would not fit the kernels' shapes.
 int tb_plan(mnl_fields *F) {
+  F->tb_r1done_ok = false;
   unsigned long long sig = 1469598103934665603ULL;
   auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
   mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
-  mix(F->rim_zchunk), mix(F->tb_ox), mix(F->tb_px), mix(F->tb_pol_on);
+  mix(F->rim_zchunk), mix(F->tb_ox), mix(F->tb_px), mix(F->tb_pol_on), mix(F->tb_lint != 0);
   mix((long long)F->srcD_idx.size());
   for (long long v : F->srcD_idx) mix(v);
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
@@ -3116,10 +3117,27 @@ int tb_plan(mnl_fields *F) {
           F->tb_border += nb;  // an upper bound (edges counted twice)
         }
   }
-  // the work queue takes the items in list order: longest first
+  // the work queue takes the items in list order: longest first.  One rank: the items whose
+  // two-step footprint (own box + 2) meets no rim box first -- they read only what the previous
+  // pair's two-step kernel wrote, so they can run beside that pair's second rim launch
+  // (tb_pair, tb_lint) -- then the others
+  auto interior = [&](const TB2Item &it) {
+    Box o;
+    o.lo[0] = (it.x & 0xFFFF) - 2, o.hi[0] = (it.x >> 16) + 2;
+    o.lo[1] = (it.y & 0xFFFF) - 2, o.hi[1] = (it.y >> 16) + 2;
+    o.lo[2] = (it.z & 0xFFFF) - 2, o.hi[2] = (it.z >> 16) + 1;
+    for (const Box &r : rim)
+      if (box_meets(o, r)) return false;
+    return (it.faces & 63) == 0;
+  };
   std::stable_sort(items.begin(), items.end(), [](const TB2Item &p, const TB2Item &q) {
     return (p.z >> 16) - (p.z & 0xFFFF) > (q.z >> 16) - (q.z & 0xFFFF);
   });
+  F->tb_nint = 0;
+  if (F->nranks == 1) {
+    for (const TB2Item &it : items) F->tb_nint += interior(it) ? 1 : 0;
+    if (F->tb_lint) std::stable_partition(items.begin(), items.end(), interior);
+  }
   F->tb_items = items;
   // ---- upload, palette-uniform flags, mixed-palette cell counts (traffic model)
   if (dev_upload(F, &F->d_tb_ritems, F->tb_rcap, F->tb_ritems) ||
@@ -3390,18 +3408,45 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   // run on a side stream beside L, taking the CUs L's workgroups leave at the end of its queue
   // (the strips read L's border values of mid and follow L).  One timing span covers L and R1
   const int na = F->tb_r1a && !F->tb_pol ? std::min(F->tb_rs0, nr) : 0;
-  if (na > 0 && !F->s_aux) {
+  // the two-step items whose footprint meets no rim box (tb_plan puts them first) read only
+  // what the previous pair's two-step kernel wrote and write the buffers its rim launches no
+  // longer read after its first rim launch: they run on a third stream, released at that point
+  // of the previous pair (ev_r1done), beside its second rim launch.  Not with DFT monitors
+  // (their samples of the previous pair read the compact boxes these items rewrite)
+  const int ni = t.n;
+  const int nl = (F->tb_lint && F->dfts.empty() && !F->tb_pol) ? std::min(F->tb_nint, ni) : 0;
+  if ((na > 0 || nl > 0) && !F->s_aux) {
     HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming));
   }
-  int k = ev_begin(na > 0 ? TM_TB : TM_TB);
+  if (nl > 0 && !F->s_lint) {
+    HIPCHK(hipStreamCreateWithFlags(&F->s_lint, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_lint, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_r1done, hipEventDisableTiming));
+  }
+  if (nl > 0) {
+    if (!F->tb_r1done_ok || F->tb_lint == 2)  // no previous pair in this batch: after all before
+      HIPCHK(hipEventRecord(F->ev_r1done, F->stream));
+    HIPCHK(hipStreamWaitEvent(F->s_lint, F->ev_r1done, 0));
+    TB2Args ti = t;
+    ti.n = nl;
+    ti.ctr_line = 6;
+    if (F->tb_lint >= 3) ti.wg_limit = std::max(1, k_cu_count() * F->tb_lint / 8);
+    const int kl = k_tb2(ti, F->s_lint, F->ctr_base);
+    if (kl) return fused_fail("two-step kernel launch failed", kl);
+    HIPCHK(hipEventRecord(F->ev_lint, F->s_lint));
+    t.n = ni - nl;
+    t.items = t.items + nl;
+    if (t.uflag) t.uflag = t.uflag + nl;
+  }
+  int k = ev_begin(TM_TB);
   int kr = 0;
   if (na > 0) {
     HIPCHK(hipEventRecord(F->ev_start, F->stream));
     HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
   }
-  kr = k_tb2(t, F->stream, F->ctr_base);
+  kr = t.n > 0 ? k_tb2(t, F->stream, F->ctr_base) : 0;
   if (kr) return fused_fail("two-step kernel launch failed", kr);
   if (na > 0) {
     kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, na, 5, F->s_aux, F->ctr_base);
@@ -3413,8 +3458,10 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
       if (kr) return fused_fail("rim kernel launch failed", kr);
     }
     HIPCHK(hipStreamWaitEvent(F->stream, F->ev_early, 0));
+    if (nl > 0) HIPCHK(hipStreamWaitEvent(F->stream, F->ev_lint, 0));
     ev_end(k);
   } else {
+    if (nl > 0) HIPCHK(hipStreamWaitEvent(F->stream, F->ev_lint, 0));
     ev_end(k);
     k = ev_begin(TM_RIM);
     kr = k_tile_items(r1, r1.titems, r1.tgeo, r1.tflag, nr, 4, F->stream, F->ctr_base);
@@ -3433,6 +3480,15 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   nan_count(F, 1);
   F->nan_at = t_mid;
   if (nan_launch(F, nullptr, mid.E, mid.D)) return -1;
+  // the next pair's interior two-step items may start from here: R1, every two-step item of
+  // this pair and the middle step's guard are done, and what follows (R2, source(n+1), the guard
+  // of nxt) reads only points of mid within one cell of the rim and nxt, which those items
+  // neither write nor, beyond the rim's reach, read
+  F->tb_r1done_ok = false;
+  if (nl > 0) {
+    HIPCHK(hipEventRecord(F->ev_r1done, F->stream));
+    F->tb_r1done_ok = true;
+  }
   if (dft_due(F, t_mid)) {  // fields::update_dfts after the pair's first step, from mid
     DevFields fm = F->f;
     for (int d = 0; d < 3; d++)
@@ -3687,6 +3743,7 @@ int step_batch(mnl_fields *F, int nsteps) {
     ev_end(k);
     return r;
   };
+  F->tb_r1done_ok = false;  // the batch's first pair waits for everything before it
   for (int s0 = 0; s0 < nsteps; s0 += CH) {
     int ns = std::min(CH, nsteps - s0);
     if (!F->dfts.empty() && dft_prepare(F, F->t, ns)) return -1;
@@ -3743,6 +3800,7 @@ int step_batch(mnl_fields *F, int nsteps) {
         if (post_step(s, 1)) return -1;  // DFT of the pair's second step (the new state)
         continue;
       }
+      F->tb_r1done_ok = false;  // a one-step step: the next pair waits for everything before
       if (tb_chain_join(F)) return -1;
       if (F->fused && F->nranks > 1) {
         if (step_fused_multi(F, sD, ev_begin, ev_end) || post_step(s)) return -1;
@@ -4243,6 +4301,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tx = getenv("MNL_TB_PX")) F->tb_px = atoi(tx) == 1 ? 1 : 2;
   if (const char *tq = getenv("MNL_TB_POL")) F->tb_pol_on = atoi(tq) != 0;
   if (const char *ta = getenv("MNL_TB_R1A")) F->tb_r1a = atoi(ta) != 0;
+  if (const char *tl = getenv("MNL_TB_LINT")) F->tb_lint = atoi(tl);
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
   if (const char *dc = getenv("MNL_DFT_CMP")) F->dft_cmp = atoi(dc) != 0;
@@ -5402,6 +5461,8 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->tb_pol_on = v;
   } else if (which == 12) {  // R1's non-strip items beside the two-step kernel (one rank)
     F->tb_r1a = v;
+  } else if (which == 13) {  // interior two-step items beside the previous pair's R2
+    F->tb_lint = v;  // (2: split, released after all before; 3..7: on 3/8..7/8 of the CUs)
   } else if (which == 10) {  // columns per lane of the two-step kernel (1: round-5 kernel)
     if (value != 1 && value != 2) return fail("bad two-step layout");
     F->tb_px = value;
@@ -5427,7 +5488,7 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
 
 int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
   if (!F || !out || n < 1) return fail("bad argument");
-  const double v[14] = {F->fused && F->tb_have && F->tb_enabled && F->tb_last ? 1.0 : 0.0,
+  const double v[15] = {F->fused && F->tb_have && F->tb_enabled && F->tb_last ? 1.0 : 0.0,
                        F->tb_cells,
                        F->tb_border,
                        F->tb_cells_nu,
@@ -5441,8 +5502,9 @@ int mnl_fields_tb_info(mnl_fields *F, double *out, int n) {
                        F->tb_enabled ? 1.0 : 0.0,
                        double(F->tb_zchunk),  // the setting (0: automatic)
                        double(F->tb_ox ? F->tb_ox : TB_OXW),  // most own columns of an item
-                       F->tb_pol ? 1.0 : 0.0};  // polarization chunks stepped inside the pairs
-  for (int i = 0; i < n && i < 14; i++) out[i] = v[i];
+                       F->tb_pol ? 1.0 : 0.0,  // polarization chunks stepped inside the pairs
+                       double(F->tb_nint)};  // interior two-step items (first in the list)
+  for (int i = 0; i < n && i < 15; i++) out[i] = v[i];
   return 0;
 }
 

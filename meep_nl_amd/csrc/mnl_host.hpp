@@ -316,6 +316,8 @@ struct mnl_fields {
   hipStream_t s_aux = nullptr, s_comm = nullptr;
   hipEvent_t ev_start = nullptr, ev_early = nullptr, ev_x1 = nullptr, ev_shell = nullptr,
              ev_x0 = nullptr;
+  hipStream_t s_lint = nullptr;     // pairs: interior two-step items (tb_lint)
+  hipEvent_t ev_lint = nullptr, ev_r1done = nullptr;
   double *pp_B[3] = {nullptr, nullptr, nullptr}, *pp_D[3] = {nullptr, nullptr, nullptr};
   double *pp_E[3] = {nullptr, nullptr, nullptr}, *pp_H[3] = {nullptr, nullptr, nullptr};
   double *pp_UB[3] = {nullptr, nullptr, nullptr};
@@ -366,6 +368,10 @@ struct mnl_fields {
   bool tb_r1a = true;               // MNL_TB_R1A=0 / set_schedule 12: R1 after the two-step
                                     // kernel instead of its non-strip items beside it
   int tb_rs0 = 0;                   // rim items before the narrow strips (one rank)
+  int tb_lint = 0;                  // MNL_TB_LINT=1 / set_schedule 13: the interior two-step
+                                    // items beside the previous pair's second rim launch
+  int tb_nint = 0;                  // two-step items whose footprint meets no rim box (first)
+  bool tb_r1done_ok = false;        // ev_r1done marks the previous pair's R1 join (same batch)
   bool tb_pol = false;              // the pairs step polarization chunks (general kernel, one
                                     // step at a time beside the rim launches; one rank)
   int tb_px = 2;                    // columns per lane of the two-step kernel (1: the round-5
@@ -468,9 +474,10 @@ struct mnl_fields {
                     (void *)d_tb_items})
       if (p) hipFree(p);
     comm.reset();
-    for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0})
+    for (hipEvent_t e : {ev_start, ev_early, ev_x1, ev_shell, ev_x0, ev_lint, ev_r1done})
       if (e) hipEventDestroy(e);
     if (s_aux) hipStreamDestroy(s_aux);
+    if (s_lint) hipStreamDestroy(s_lint);
     if (s_comm) hipStreamDestroy(s_comm);
     if (stream) hipStreamDestroy(stream);
   }

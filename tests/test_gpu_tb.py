@@ -97,6 +97,20 @@ def test_tb_schedule_options_bitwise(oracle_tb, schedule):
     _same(p, oracle_tb)
 
 
+def test_tb_interior_items_beside_previous_rim():
+    """Narrow, short two-step items (9 columns, 3 planes): many have a footprint that meets no
+    rim box, and one rank runs those on a third stream from the previous pair's middle guard on,
+    beside its second rim launch (tb_lint).  Long batches of pairs, odd calls and a one-step
+    step between them: bitwise the oracle and the same run with the option off."""
+    sched = (("tb_ox", 9), ("tb_zchunk", 3))
+    steps = (1, 24, 3, 1, 10)
+    p = sc_tb(ProductSim, profile=True, schedule=sched + (("tb_lint", 1),), steps=steps)
+    info = p._fields().tb_info()
+    assert info["active"] and 0 < info["tb_interior_items"] < info["tb_items"], info
+    _same(p, sc_tb(make_oracle, steps=steps))
+    _same(p, sc_tb(ProductSim, schedule=sched, steps=steps))
+
+
 def test_tb_equals_one_step_path():
     """Odd calls, one-step calls between pairs: identical to stepping one step at a time."""
     steps = (1, 7, 1, 4, 2, 3)
