@@ -428,6 +428,14 @@ int mnl_fields_dft_size(mnl_fields *f, int handle, long long *n);
 int mnl_fields_dft_data(mnl_fields *f, int handle, int which, double *out, long long n);
 /* the decimation factor the object was created with */
 int mnl_fields_dft_decimation(mnl_fields *f, int handle, int *decimation);
+/* Accumulate every buffered DFT update now and wait for the device (no reference
+ * counterpart: the reference adds each update to the DFT array in fields::update_dfts,
+ * src/dft.cpp:249-263; this build samples every update and adds up to 32 of them per pass
+ * over the array, in the same order, so the values are bitwise the same).  Every reader of
+ * DFT values (flux, data, get_dft_array, dump) flushes by itself; buffered updates carry over
+ * between step calls.  For timing: a timed region that includes the accumulation of its own
+ * updates ends with this call. */
+int mnl_fields_dft_flush(mnl_fields *f);
 /* fields::add_dft_fields(components, ncomp, volume(vmin, vmax), freq, Nfreq,
  * use_centered_grid = !yee_grid, decimation_factor) (src/dft.cpp:889-903; Python
  * Simulation.add_dft_fields, python/simulation.py:2976-3036): E / H components

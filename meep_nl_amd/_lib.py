@@ -105,6 +105,7 @@ _SIGS = {
     "mnl_fields_dft_size": (c_int, [c_void, c_int, llptr]),
     "mnl_fields_dft_data": (c_int, [c_void, c_int, c_int, dptr, ctypes.c_longlong]),
     "mnl_fields_dft_decimation": (c_int, [c_void, c_int, iptr]),
+    "mnl_fields_dft_flush": (c_int, [c_void]),
     "mnl_fields_set_time": (c_int, [c_void, ctypes.c_longlong]),
     "mnl_fields_zero_fields": (c_int, [c_void]),
     "mnl_fields_remove_sources": (c_int, [c_void]),

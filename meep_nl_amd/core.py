@@ -665,6 +665,12 @@ class Fields:
         check(lib().mnl_fields_dft_data(self.h, h, int(which), ptr(out), n.value))
         return out[0::2] + 1j * out[1::2]
 
+    def dft_flush(self):
+        """Accumulate every buffered DFT update now and wait for the device
+        (mnl_fields_dft_flush; readers flush by themselves, updates stay buffered between
+        step calls)."""
+        check(lib().mnl_fields_dft_flush(self.h))
+
     def dft_decimation(self, h):
         v = ctypes.c_int()
         check(lib().mnl_fields_dft_decimation(self.h, h, ctypes.byref(v)))

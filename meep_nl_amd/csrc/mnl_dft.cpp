@@ -376,14 +376,23 @@ int dft_add_fields(mnl_fields *F, int ncomp, const int *comps, const double wmin
   return dft_layout(F, o, ho, pwE, pwH);
 }
 
-// phases of every DFT update in steps [t0+1, t0+ns] -> device (one row per update)
+// phases of every DFT update in steps [t0+1, t0+ns] -> device (one row per update), after
+// the rows of the updates still buffered from earlier calls (accumulated by the next flush:
+// when kb updates are buffered or before the DFT array is read, not at the end of every call)
 int dft_prepare(mnl_fields *F, long long t0, int ns) {
   for (auto &op : F->dfts) {
     DftFluxH &o = *op;
-    o.row = 0;
     const size_t nch = o.E.size() + o.H.size();
+    const size_t rowlen = 2 * nch * (size_t)o.nfreq;
     std::vector<double> ph;
-    ph.reserve((size_t)ns * nch * o.nfreq * 2);
+    ph.reserve(((size_t)o.nbuf + ns) * rowlen);
+    if (o.nbuf > 0) {
+      if (o.ph_host.size() < (size_t)o.row * rowlen || o.row < o.nbuf)
+        return fail("dft: buffered phase rows lost");
+      ph.insert(ph.end(), o.ph_host.begin() + (size_t)(o.row - o.nbuf) * rowlen,
+                o.ph_host.begin() + (size_t)o.row * rowlen);
+    }
+    o.row = o.nbuf;
     std::vector<cplx> pe(o.nfreq), phh(o.nfreq);
     for (int s = 0; s < ns; s++) {
       const long long t = t0 + s + 1;
@@ -423,7 +432,10 @@ int dft_prepare(mnl_fields *F, long long t0, int ns) {
       add(o.E);
       add(o.H);
     }
-    if (ph.empty()) continue;
+    if (ph.empty()) {
+      o.ph_host.clear();
+      continue;
+    }
     if (o.ph_cap < ph.size()) {
       HIPCHK(hipStreamSynchronize(F->stream));
       if (o.d_ph) hipFree(o.d_ph);
@@ -433,6 +445,7 @@ int dft_prepare(mnl_fields *F, long long t0, int ns) {
     (void)nch;
     HIPCHK(hipMemcpyAsync(o.d_ph, ph.data(), ph.size() * 8, hipMemcpyHostToDevice, F->stream));
     HIPCHK(hipStreamSynchronize(F->stream));
+    o.ph_host.swap(ph);
   }
   return 0;
 }
@@ -546,6 +559,7 @@ bool dft_due(const mnl_fields *F, long long t) {
 int dft_flux_values(mnl_fields *F, int h, double *out) {
   if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
   DftFluxH &o = *F->dfts[h];
+  if (dft_flush(F, o)) return -1;  // the buffered updates first
   const size_t nf = o.nfreq;
   std::vector<double> v(2 * ((o.npts + 63) & ~size_t(63)) * nf);
   bool ok = true;

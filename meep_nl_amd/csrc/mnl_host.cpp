@@ -3984,12 +3984,8 @@ int step_batch(mnl_fields *F, int nsteps) {
       F->nan_at = F->t + s + 1;
       if (nan_launch(F)) return -1;
     }
-    if (!F->dfts.empty()) {
-      const int k = ev_begin(TM_DFTF);
-      for (auto &o : F->dfts)
-        if (dft_flush(F, *o)) return -1;
-      ev_end(k);
-    }
+    // buffered DFT updates stay buffered across chunks and calls (a run that steps one step
+    // per call accumulates once per kb updates, not once per call); readers flush first
     F->t += ns;
     if (flush_events() != 0) return -1;
     if (nan_result(F)) return -1;  // stop within NAN_CH steps of a failing guard
@@ -5526,6 +5522,7 @@ static int dft_array_values(mnl_fields *F, int h, int c, int num_freq, int *rank
                             long long dims[3], double *out, long long nout) {
   if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
   DftFluxH &o = *F->dfts[h];
+  if (dft_flush(F, o)) return -1;  // the buffered updates first
   if (num_freq < 0 || num_freq > o.nfreq - 1)
     return fail(("process_dft_component: frequency index " + std::to_string(num_freq) +
                  " is outside the range of the frequency array of size " +
@@ -5672,9 +5669,18 @@ int mnl_fields_dft_size(mnl_fields *F, int h, long long *n) {
   return 0;
 }
 
+int mnl_fields_dft_flush(mnl_fields *F) {
+  if (!F) return fail("null fields");
+  for (auto &o : F->dfts)
+    if (dft_flush(F, *o)) return -1;
+  HIPCHK(hipStreamSynchronize(F->stream));
+  return 0;
+}
+
 int mnl_fields_dft_data(mnl_fields *F, int h, int which, double *out, long long n) {
   if (!F || !out) return fail("null argument");
   if (h < 0 || h >= (int)F->dfts.size()) return fail("bad dft handle");
+  if (dft_flush(F, *F->dfts[h])) return -1;  // the buffered updates first
   const DftFluxH &o = *F->dfts[h];
   const size_t nf = o.nfreq;
   std::vector<double> v(2 * ((o.npts + 63) & ~size_t(63)) * nf);

@@ -210,6 +210,7 @@ struct DftFluxH {
   double *d_ph = nullptr;             // phases of one batch: [update][chunk][freq] complex
   size_t ph_cap = 0;
   int row = 0;                        // next phase row of this batch
+  std::vector<double> ph_host;        // host copy of d_ph (the buffered rows move to the front)
   std::vector<int> slot;              // device slot of each point (reference order -> slot)
   double *d_fr = nullptr;             // [update][slot] sampled fields awaiting accumulation
   int nbuf = 0;                       // buffered updates (rows row-nbuf .. row-1)

@@ -783,14 +783,16 @@ def sc_flux_2d(make, xmax=10.0, ymax=10.0, ttot=130.0):
 FLUX3D_FREQS = [0.1, 0.15, 0.2, 0.27]
 
 
-def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=None, freqs=None):
+def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=None, freqs=None,
+               calls=None):
     """Waveguide (eps 12 core along x) + PML with four DFT flux objects: a box around
     the source (six faces, weights +-1), an x-normal plane across the whole cell
     (through the PML), a z-normal plane inside the lower PML, and a y-direction
     volume region (interpolation weights in all three directions).  Optional
     Lorentzian slab (E stored inside the polarization box in fused mode) and a
     callback(o) at half time.  The last object uses the automatic decimation
-    (src/dft.cpp:195-216).  Returns (sim, [handles])."""
+    (src/dft.cpp:195-216).  calls: the step counts of the step calls instead (None entries:
+    call extra(o) there).  Returns (sim, [handles])."""
     sizes = sizes or [3.2, 3.2, 3.2]
     o = vol(make, 3, sizes, 10, center_origin=True)
     o.add_pml(1.0 if sizes[0] < 4 else 0.7)
@@ -812,6 +814,13 @@ def sc_flux_3d(make, steps=80, sizes=None, lorentz=False, decimation=1, extra=No
                            2, -0.5)], FLUX3D_FREQS, decimation),
           o.add_dft_flux([([-0.61, -0.23, -0.17], [0.57, 0.29, 0.66], 1, 1.0)], FLUX3D_FREQS,
                          0)]  # automatic decimation
+    if calls is not None:
+        for n in calls:
+            if n is None:
+                extra(o)
+            else:
+                o.step(n)
+        return o, hs
     o.step(steps // 2)
     if extra:
         extra(o)

@@ -61,6 +61,32 @@ def test_dft_flux_3d_fused(monkeypatch, block):
     _same_dft(p, o, hs)
 
 
+@pytest.mark.parametrize("block", ["32", "5"])
+def test_dft_flux_buffered_across_calls(monkeypatch, block):
+    """Buffered DFT updates carry over between step calls (one step per call, as a Python
+    run loop steps) and are accumulated when `block` are buffered or a reader asks: flux and
+    per-point values read mid-run and at the end are bitwise the oracle's after the same
+    steps, and an explicit flush changes nothing."""
+    monkeypatch.setenv("MNL_DFT_BLOCK", block)
+    mid = {}
+
+    def read(o):
+        mid[len(mid)] = ([o.flux(h) for h in range(4)], o.dft_data(1, 0))
+
+    calls = (1,) * 9 + (3, 1, None, 2, 20, 1, 1, None, 13) + (1,) * 8 + (21,)
+    p, hs = sc_flux_3d(ProductSim, calls=calls, extra=read)
+    assert p._fields().fused_active()
+    pm = dict(mid)
+    mid.clear()
+    o, _ = sc_flux_3d(make_oracle, calls=calls, extra=read)
+    for k in pm:
+        for a, b in zip(pm[k][0], mid[k][0]):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(pm[k][1], mid[k][1])
+    p._fields().dft_flush()
+    _same_dft(p, o, hs)
+
+
 @pytest.mark.parametrize("nfreq", [1, 21, 40])
 def test_dft_flux_3d_nfreq(nfreq):
     """Frequency counts that exercise every accumulation tile (16, 8, 4, 2, 1)."""
