@@ -3247,8 +3247,7 @@ int tb_usable(mnl_fields *F, bool *ok) {
   const bool pol_ok = F->f.npol > 0 && F->fgeo.ngen > 0 && F->nranks == 1 && F->tb_pol_on;
   bool local = F->tb_enabled && F->fused && F->tile_mode &&
                ((F->fgeo.ngen == 0 && F->f.npol == 0) || pol_ok) && !F->nr && !F->upnl &&
-               F->S.dim == 3 && F->slab_dir == 2 &&
-               (F->dfts.empty() || F->nranks == 1);
+               F->S.dim == 3 && F->slab_dir == 2;
   if (local && tb_plan(F)) return -1;
   if (local && F->tb_have && tb_mid_alloc(F)) local = false;
   if (F->tb_stats && !(local && F->tb_have))
@@ -3607,6 +3606,24 @@ int tb_pair_multi(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begi
     const int kw = ev_begin(TM_WAIT);
     HIPCHK(hipStreamWaitEvent(F->stream, F->ev_x0, 0));
     ev_end(kw);
+    if (dft_due(F, t_mid)) {
+      // fields::update_dfts after the pair's first step, from mid (round 6): the chain has
+      // put mid's top plane, sources and E ghost in; the H component normal to the slabs gets
+      // its low ghost now (exchange kind 3, as post_step does after a one-step step).  The
+      // exchange reads F->f's pointers when enqueued: point them at mid meanwhile
+      DevFields &f = F->f;
+      const DevFields keep = f;
+      for (int d = 0; d < 3; d++)
+        f.B[d] = mid.B[d], f.D[d] = mid.D[d], f.E[d] = mid.E[d], f.H[d] = mid.H[d],
+        f.UB[d] = mid.UB[d];
+      const DevFields fm = f;
+      k = ev_begin(TM_DFT);
+      int r = exchange(F, 3) ? fail("DFT halo exchange failed") : 0;
+      f = keep;
+      if (!r) r = dft_update(F, t_mid, &fm, 0);
+      ev_end(k);
+      if (r) return -1;
+    }
     k = ev_begin(TM_RIM);
     r2.wg_limit = 0;
     kr = k_tile_items(r2, r2.titems + nf, r2.tgeo + 4 * nf, r2.tflag ? r2.tflag + nf : nullptr,

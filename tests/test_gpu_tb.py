@@ -216,6 +216,23 @@ def test_tb_dft_flux():
     _same_dft(p, o, hs)
 
 
+@pytest.mark.parametrize("group", [GroupSim, GroupSim3])
+def test_tb_slabs_dft_flux(group):
+    """z-slabs with DFT flux monitors (round 6: multi-rank runs with monitors step pairs too):
+    the middle step is sampled once the slab-face chain has put mid's top plane, sources and
+    E ghost in and mid's H component normal to the slabs has its low ghost (exchange kind 3);
+    the flux monitors cross the slab faces.  Per-point DFT values bitwise the oracle, the flux
+    sums within 1e-12 (sum over ranks), the fields bitwise."""
+    from scenarios import sc_flux_3d
+    from test_gpu_dft import _same_dft
+    kw = dict(sizes=[9.6, 6.4, 9.6], steps=24)
+    p, hs = sc_flux_3d(group, **kw)
+    assert all(f.tb_info()["active"] for f in p._all())
+    o, _ = sc_flux_3d(make_oracle, **kw)
+    _same_dft(p, o, hs, flux_exact=False)
+    _same(p, o)
+
+
 def test_tb_dft_compact_fallbacks(monkeypatch):
     """The pairs' samples of two-step points come from the monitors' compact boxes (DESIGN.md
     section 10); the paths around them stay bitwise the oracle: compact boxes switched off
