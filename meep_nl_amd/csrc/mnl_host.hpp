@@ -372,6 +372,9 @@ struct mnl_fields {
   int tb_lint = 0;                  // MNL_TB_LINT=1 / set_schedule 13: the interior two-step
                                     // items beside the previous pair's second rim launch
   int tb_nint = 0;                  // two-step items whose footprint meets no rim box (first)
+  bool tb_r2lpt = false;            // MNL_TB_R2LPT=1 / set_schedule 14: the second rim launch
+                                    // longest first (default: the first one's order, narrow
+                                    // strips last -- measured faster)
   bool tb_r1done_ok = false;        // ev_r1done marks the previous pair's R1 join (same batch)
   bool tb_pol = false;              // the pairs step polarization chunks (general kernel, one
                                     // step at a time beside the rim launches; one rank)
