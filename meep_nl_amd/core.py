@@ -594,11 +594,13 @@ class Fields:
         first rim launch's items other than the narrow strips on a side stream beside the
         two-step kernel, 'tb_lint' = the interior two-step items on a third stream beside the
         previous pair's second rim launch, 'r2_lpt' = the second rim launch in longest-first
-        order (the first keeps the narrow strips last) (mnl_fields_set_schedule)."""
+        order (the first keeps the narrow strips last), 'strip_zchunk' = planes per narrow
+        x-face strip item of the rim (0: the rim's) (mnl_fields_set_schedule)."""
         idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4, "dft_cmp": 5,
                "rim_zchunk": 6, "nr_early": 7, "tb_zchunk": 8, "tb_ox": 9, "tb_px": 10,
-               "tb_pol": 11, "r1_beside": 12, "tb_lint": 13, "r2_lpt": 14}[which]
-        if idx in (2, 3, 4, 6, 8, 9, 10, 13):  # integers: CUs left free (-1: the default), planes
+               "tb_pol": 11, "r1_beside": 12, "tb_lint": 13, "r2_lpt": 14,
+               "strip_zchunk": 15}[which]
+        if idx in (2, 3, 4, 6, 8, 9, 10, 13, 14, 15):  # integers: CUs left free (-1: the default), planes
             check(lib().mnl_fields_set_schedule(self.h, idx, int(value)))
         else:
             check(lib().mnl_fields_set_schedule(self.h, idx, 1 if value else 0))

@@ -2655,7 +2655,7 @@ int tb_plan(mnl_fields *F) {
   unsigned long long sig = 1469598103934665603ULL;
   auto mix = [&](long long v) { sig = (sig ^ (unsigned long long)v) * 1099511628211ULL; };
   mix(F->fused_epoch), mix(F->tb_zchunk), mix(F->fused_zchunk), mix((long long)F->nlocal);
-  mix(F->rim_zchunk), mix(F->tb_ox), mix(F->tb_px), mix(F->tb_pol_on), mix(F->tb_lint != 0), mix(F->tb_r2lpt);
+  mix(F->rim_zchunk), mix(F->tb_ox), mix(F->tb_px), mix(F->tb_pol_on), mix(F->tb_lint != 0), mix(F->tb_r2lpt), mix(F->tb_szc);
   mix((long long)F->srcD_idx.size());
   for (long long v : F->srcD_idx) mix(v);
   // DFT monitors (one rank): the Yee points their samples average, +1 along every axis --
@@ -2854,8 +2854,11 @@ int tb_plan(mnl_fields *F) {
     std::sort(zcut.begin(), zcut.end());
     zcut.erase(std::unique(zcut.begin(), zcut.end()), zcut.end());
     std::sort(zcut.begin(), zcut.end());
+    // narrow strips: their own planes per item (tb_szc; one strip pair per workgroup, so the
+    // strips of a 512^3 rim make only ~200 workgroups at the rim's chunk length)
+    const int zcb = narrow && F->tb_szc > 0 ? std::min(F->tb_szc, FUSED_MAXCH) : zc;
     for (size_t s = 0; s + 1 < zcut.size(); s++) {
-      const int n = zcut[s + 1] - zcut[s], nt = (n + zc - 1) / zc;
+      const int n = zcut[s + 1] - zcut[s], nt = (n + zcb - 1) / zcb;
       for (int t = 0; t < nt; t++) zs.push_back(zcut[s] + (int)((long long)n * t / nt));
     }
     zs.push_back(b.hi[2] + 1);
@@ -2961,7 +2964,10 @@ int tb_plan(mnl_fields *F) {
   // other items can run beside the two-step kernel (tb_pair, tb_r1a).  The second rim launch
   // reads a second copy of the list after the first: the same order by default (measured
   // faster than longest first, tb_r2lpt: 512^3 -0.8 %, C2 256^3 -3.6 %)
-  const std::vector<RI> order2 = order;
+  std::vector<RI> order2 = order;
+  if (F->tb_r2lpt == 2)  // the narrow strips first
+    std::stable_partition(order2.begin(), order2.end(),
+                          [](const RI &r) { return ((r.code >> 30) & 1) != 0; });
   F->tb_rs0 = (int)order.size();
   if (F->nranks == 1) {
     auto strip = [](const RI &r) { return ((r.code >> 30) & 1) != 0; };
@@ -4320,7 +4326,8 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tq = getenv("MNL_TB_POL")) F->tb_pol_on = atoi(tq) != 0;
   if (const char *ta = getenv("MNL_TB_R1A")) F->tb_r1a = atoi(ta) != 0;
   if (const char *tl = getenv("MNL_TB_LINT")) F->tb_lint = atoi(tl);
-  if (const char *tp = getenv("MNL_TB_R2LPT")) F->tb_r2lpt = atoi(tp) != 0;
+  if (const char *sz = getenv("MNL_TB_STRIP_ZCHUNK")) F->tb_szc = std::max(0, atoi(sz));
+  if (const char *tp = getenv("MNL_TB_R2LPT")) F->tb_r2lpt = std::max(0, std::min(2, atoi(tp)));
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
   if (const char *dp = getenv("MNL_DFT_PAL")) F->dft_pal = atoi(dp) != 0;
   if (const char *dc = getenv("MNL_DFT_CMP")) F->dft_cmp = atoi(dc) != 0;
@@ -5480,8 +5487,12 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->tb_pol_on = v;
   } else if (which == 12) {  // R1's non-strip items beside the two-step kernel (one rank)
     F->tb_r1a = v;
-  } else if (which == 14) {  // the second rim launch in longest-first order (one rank)
-    F->tb_r2lpt = v;
+  } else if (which == 15) {  // planes per narrow strip item (0: the rim's chunk length)
+    if (value < 0 || value > FUSED_MAXCH) return fail("bad strip chunk");
+    F->tb_szc = value;
+  } else if (which == 14) {  // the second rim launch's order (one rank): 1 longest first,
+    if (value < 0 || value > 2) return fail("bad rim order");  // 2 the narrow strips first
+    F->tb_r2lpt = value;
   } else if (which == 13) {  // interior two-step items beside the previous pair's R2
     if (value < 0 || value > 7) return fail("bad interior-items setting");
     F->tb_lint = value;  // (2: split, released after all before; 3..7: on 3/8..7/8 of the CUs)

@@ -372,9 +372,11 @@ struct mnl_fields {
   int tb_lint = 0;                  // MNL_TB_LINT=1 / set_schedule 13: the interior two-step
                                     // items beside the previous pair's second rim launch
   int tb_nint = 0;                  // two-step items whose footprint meets no rim box (first)
-  bool tb_r2lpt = false;            // MNL_TB_R2LPT=1 / set_schedule 14: the second rim launch
-                                    // longest first (default: the first one's order, narrow
-                                    // strips last -- measured faster)
+  int tb_szc = 0;                   // planes per narrow strip item (0: the rim's chunk length;
+                                    // MNL_TB_STRIP_ZCHUNK / set_schedule 15)
+  int tb_r2lpt = 0;                 // MNL_TB_R2LPT / set_schedule 14: the second rim launch
+                                    // longest first (1) or strips first (2); default: the
+                                    // first one's order, narrow strips last
   bool tb_r1done_ok = false;        // ev_r1done marks the previous pair's R1 join (same batch)
   bool tb_pol = false;              // the pairs step polarization chunks (general kernel, one
                                     // step at a time beside the rim launches; one rank)
