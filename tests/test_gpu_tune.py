@@ -11,7 +11,7 @@ from scenarios import ALL_COMPS, GroupSim, ProductSim, make_oracle, sc_random_fi
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 SIZES = (6.4, 5.2, 9.6)  # 64 x 52 x 96 cells at resolution 10: several z chunks per length
-TOTAL = 140  # tune(reps=1) steps at most 2 + 32 * (2 + 2) = 130 (z chunks, CU split, pairs: 19 shapes + one-step)
+TOTAL = 240  # tune(reps=1) steps at most 2 + 55 * (2 + 2) = 222 (z chunks 6, CU split 6, pairs: 19 shapes forward and backward + the best 3 again, one-step twice)
 ZCS = (0, 16, 20, 24, 32, 48)
 
 
