@@ -27,20 +27,26 @@ def main():
     import bench
     from meep_nl_amd import core
     core.set_verbosity(0)
-    out = []
+    out, parts = [], []
     for i in range(a.allocs):
         gv, s, f = bench.build_fields("waveguide", a.size, 0, 1, 0, None)
         f.step(8)
+        f.set_profiling(True)
         ms = []
         for _ in range(a.reps):
             t0 = time.perf_counter()
             f.step(a.steps)
             ms.append((time.perf_counter() - t0) / a.steps * 1e3)
         out.append(min(ms))
-        print(f"allocation {i}: {min(ms):.4f} ms/step (reps {[round(x, 4) for x in ms]})", flush=True)
+        n5, ms5, _ = f.kernel_stats(5)  # pairs: all launches of a pair
+        n6, ms6, _ = f.kernel_stats(6)  # rim launches that run alone
+        parts.append({"pair_ms": ms5 / max(n5, 1), "rim_alone_ms": ms6 / max(n6, 1)})
+        print(f"allocation {i}: {min(ms):.4f} ms/step (reps {[round(x, 4) for x in ms]}) "
+              f"{parts[-1]}", flush=True)
         del f, s, gv
         gc.collect()
-    res = {"size": a.size, "steps": a.steps, "ms_per_step": out, "min": min(out), "max": max(out),
+    res = {"size": a.size, "steps": a.steps, "ms_per_step": out, "parts": parts,
+           "min": min(out), "max": max(out),
            "median": statistics.median(out), "env": {k: v for k, v in os.environ.items() if k.startswith("MNL_")}}
     print(json.dumps(res))
     if a.json:
