@@ -595,11 +595,12 @@ class Fields:
         two-step kernel, 'tb_lint' = the interior two-step items on a third stream beside the
         previous pair's second rim launch, 'r2_lpt' = the second rim launch in longest-first
         order (the first keeps the narrow strips last), 'strip_zchunk' = planes per narrow
-        x-face strip item of the rim (0: the rim's) (mnl_fields_set_schedule)."""
+        x-face strip item of the rim (0: the rim's), 'src_guard' = a pair's step sources and
+        NaN guard in one launch (mnl_fields_set_schedule)."""
         idx = {"narrow": 0, "dft_pal": 1, "res": 2, "res_tb2": 3, "res_rim": 4, "dft_cmp": 5,
                "rim_zchunk": 6, "nr_early": 7, "tb_zchunk": 8, "tb_ox": 9, "tb_px": 10,
                "tb_pol": 11, "r1_beside": 12, "tb_lint": 13, "r2_lpt": 14,
-               "strip_zchunk": 15}[which]
+               "strip_zchunk": 15, "src_guard": 16}[which]
         if idx in (2, 3, 4, 6, 8, 9, 10, 13, 14, 15):  # integers: CUs left free (-1: the default), planes
             check(lib().mnl_fields_set_schedule(self.h, idx, int(value)))
         else:

@@ -3364,6 +3364,31 @@ int tb_src(mnl_fields *F, const SrcDev &s, double *const D[3]) {
   return 0;
 }
 
+// A pair's step tail on one rank: the step's D sources into D, then (when due) the NaN guard of
+// the state E / D at time step `at` -- one launch (k_src_guard) for short source lists, else
+// the two launches as before (tb_srcguard = 0: always two)
+int tb_tail(mnl_fields *F, const SrcDev &s, double *const D[3], double *const E[3], long long at) {
+  nan_count(F, 1);
+  F->nan_at = at;
+  if (F->tb_srcguard && F->nan_due && F->nan_terms.n > 0 && s.n <= SRC_GUARD_MAXN &&
+      s.nlayer <= SRC_GUARD_MAXL) {
+    if (!F->d_nanflag && dev_alloc(F, &F->d_nanflag, 2)) return -1;
+    DevFields fm = F->f;
+    const double *Ec[3], *Dc[3], *U[3];
+    for (int d = 0; d < 3; d++) fm.Dn[d] = D[d], Ec[d] = E[d], Dc[d] = D[d], U[d] = F->f.inveps[d];
+    const int r = k_src_guard(fm, s, F->nan_terms, Ec, Dc, U, F->d_nanflag, (int)F->nan_at,
+                              F->stream);
+    if (r == 0) {
+      F->nan_due = false;
+      F->nan_launched++;
+      return 0;
+    }
+    if (r != 2) return fail("source / guard launch failed");
+  }
+  if (tb_src(F, s, D)) return -1;
+  return nan_launch(F, nullptr, E, D);
+}
+
 // the middle set starts as a copy of the state (entries no launch writes: walls, ghosts);
 // its arrays exist (tb_mid_alloc ran in tb_usable)
 int tb_mid_init(mnl_fields *F) {
@@ -3483,12 +3508,9 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
     ev_end(k);
     if (kr) return fused_fail("fused general kernel launch failed", kr);
   }
-  if (tb_src(F, s0, mid.D)) return -1;
-  // the guard of the middle step (its terms' points hold step n+1 in mid: rim items, or the
-  // two-step items' store box)
-  nan_count(F, 1);
-  F->nan_at = t_mid;
-  if (nan_launch(F, nullptr, mid.E, mid.D)) return -1;
+  // the step's sources, then the guard of the middle step (its terms' points hold step n+1 in
+  // mid: rim items, or the two-step items' store box)
+  if (tb_tail(F, s0, mid.D, mid.E, t_mid)) return -1;
   // the next pair's interior two-step items may start from here: R1, every two-step item of
   // this pair and the middle step's guard are done, and what follows (R2, source(n+1), the guard
   // of nxt) reads only points of mid within one cell of the rim and nxt, which those items
@@ -3518,11 +3540,9 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
     ev_end(k);
     if (kr) return fused_fail("fused general kernel launch failed", kr);
   }
-  if (tb_src(F, s1, nxt.D)) return -1;
+  if (tb_tail(F, s1, nxt.D, nxt.E, t_mid + 1)) return -1;
   swap_cur_nxt(F->f);
-  nan_count(F, 1);
-  F->nan_at = t_mid + 1;
-  return nan_launch(F);
+  return 0;
 }
 
 // Multi-rank pair (one rank of a z-slab decomposition; fused, no D source on the top
@@ -4326,6 +4346,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tq = getenv("MNL_TB_POL")) F->tb_pol_on = atoi(tq) != 0;
   if (const char *ta = getenv("MNL_TB_R1A")) F->tb_r1a = atoi(ta) != 0;
   if (const char *tl = getenv("MNL_TB_LINT")) F->tb_lint = atoi(tl);
+  if (const char *sg = getenv("MNL_TB_SRCGUARD")) F->tb_srcguard = atoi(sg) != 0;
   if (const char *sz = getenv("MNL_TB_STRIP_ZCHUNK")) F->tb_szc = std::max(0, atoi(sz));
   if (const char *tp = getenv("MNL_TB_R2LPT")) F->tb_r2lpt = std::max(0, std::min(2, atoi(tp)));
   if (const char *to = getenv("MNL_TB_OOM")) F->tb_oom_test = atoi(to) != 0;
@@ -5518,6 +5539,9 @@ int mnl_fields_set_schedule(mnl_fields *F, int which, int value) {
     F->tb_pol_on = v;
   } else if (which == 12) {  // R1's non-strip items beside the two-step kernel (one rank)
     F->tb_r1a = v;
+  } else if (which == 16) {  // a pair's source + guard launches merged (one rank)
+    F->tb_srcguard = v;
+    return 0;
   } else if (which == 15) {  // planes per narrow strip item (0: the rim's chunk length)
     if (value < 0 || value > FUSED_MAXCH) return fail("bad strip chunk");
     F->tb_szc = value;

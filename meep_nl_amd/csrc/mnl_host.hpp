@@ -372,6 +372,8 @@ struct mnl_fields {
   int tb_lint = 0;                  // MNL_TB_LINT=1 / set_schedule 13: the interior two-step
                                     // items beside the previous pair's second rim launch
   int tb_nint = 0;                  // two-step items whose footprint meets no rim box (first)
+  bool tb_srcguard = true;          // MNL_TB_SRCGUARD=0 / set_schedule 16: a pair's sources
+                                    // and guard as two launches per step (default: one)
   int tb_szc = 0;                   // planes per narrow strip item (0: the rim's chunk length;
                                     // MNL_TB_STRIP_ZCHUNK / set_schedule 15)
   int tb_r2lpt = 0;                 // MNL_TB_R2LPT / set_schedule 14: the second rim launch

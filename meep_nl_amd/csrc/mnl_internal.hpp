@@ -219,6 +219,12 @@ int k_update_e(const Box &in, const BoxList *shell, const DevGrid &g, const DevF
 int k_update_pols(const Box &in, const BoxList *shell, const DevGrid &g, const DevFields &f,
                   void *stream);
 int k_aniso_wall(const DevGrid &g, const DevFields &f, int zero, void *stream);
+// a pair's step tail in one workgroup: D sources (f.Dn; short lists only) then the NaN guard
+constexpr int SRC_GUARD_MAXN = 4096, SRC_GUARD_MAXL = 8;
+struct SrcLayers {
+  int n;
+  int off[SRC_GUARD_MAXL + 1];
+};
 int k_source(int ft, const DevGrid &g, const DevFields &f, const SrcDev &s, int step,
              void *stream);
 // Fused step (DESIGN.md "Fused step"): one pass per fields::step() over box G
@@ -415,6 +421,11 @@ struct NanTerms {
 // flag[0] |= 1 (and flag[1] = step, once) when the sum is not finite
 int k_nan_check(const NanTerms &t, const double *const E[3], const double *const D[3],
                 const double *const U[3], int *flag, int step, void *stream);
+// a pair's step tail: the D sources of the step into f.Dn, then the guard over E / D (2: the
+// source list is too long for one workgroup -- use k_source + k_nan_check)
+int k_src_guard(const DevFields &f, const SrcDev &s, const NanTerms &t, const double *const E[3],
+                const double *const D[3], const double *const U[3], int *flag, int step,
+                void *stream);
 int k_tb2(const TB2Args &a, void *stream, unsigned long long *bases);
 int k_tb2_uniform(const TB2Args &a, unsigned *flags, void *stream);
 // the tile kernel over an explicit item list (FusedArgs::tgeo boxes), counter line `line`

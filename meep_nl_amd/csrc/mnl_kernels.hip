@@ -4719,6 +4719,73 @@ __global__ void nan_check_kernel(NanTerms t, Ptr3 E, Ptr3 D, Ptr3 U, int *flag, 
   if (!isfinite(sum * 0.5) && atomicOr(flag, 1) == 0) flag[1] = step;
 }
 
+// A pair's step tail in one launch (round 6): the D sources of the step, layer by layer (the
+// same per-point expression as source_kernel; a barrier between layers keeps their list
+// order), then the NaN guard of the state they complete (nan_check_kernel's sum, after a
+// barrier: the guard reads the values with the sources in, as after the two launches).  One
+// workgroup: only for short source lists (SRC_GUARD_MAXN points, SRC_GUARD_MAXL layers).
+__global__ void __launch_bounds__(256) src_guard_kernel(Ptr3 pt, SrcDev s, SrcLayers sl,
+                                                        NanTerms t, Ptr3 E, Ptr3 D, Ptr3 U,
+                                                        int *flag, int step) {
+  __shared__ double sv[NAN_MAXT];
+  for (int l = 0; l < sl.n; l++) {
+    for (int k = sl.off[l] + (int)threadIdx.x; k < sl.off[l + 1]; k += (int)blockDim.x) {
+      const int c = s.comp[k];
+      const long long i = s.idx[k];
+      const int g = s.gid[k];
+      const double ar = s.amp[2 * k], ai = s.amp[2 * k + 1];
+      const double jr = s.J[2 * g], ji = s.J[2 * g + 1];
+      const double v = (ar * jr - ai * ji) * s.dt;
+      pt.p[c][i] -= pt.ci[c] ? v * pt.ci[c][i] : v;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  if (t.n <= 0) return;
+  const int i0 = threadIdx.x;
+  if (i0 < t.n) {
+    const int d = t.dir[i0];
+    const long long k = t.idx[i0];
+    double v;
+    if (t.kind[i0] == 0)
+      v = E.p[d][k];
+    else if (t.kind[i0] == 1)
+      v = U.ci[d] ? D.p[d][k] * U.ci[d][k] : D.p[d][k];
+    else
+      v = D.p[d][k];
+    sv[i0] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double sum = 0.0;
+  int i = 0;
+  for (int d = 0; d < 3; d++) {
+    double e = 0.0, dd = 0.0;
+    for (; i < t.n && t.dir[i] == d && t.kind[i] != 2; i++) e += t.w[i] * sv[i];
+    for (; i < t.n && t.dir[i] == d && t.kind[i] == 2; i++) dd += t.w[i] * sv[i];
+    sum += e * dd;
+  }
+  if (!isfinite(sum * 0.5) && atomicOr(flag, 1) == 0) flag[1] = step;
+}
+
+int k_src_guard(const DevFields &f, const SrcDev &s, const NanTerms &t, const double *const E[3],
+                const double *const D[3], const double *const U[3], int *flag, int step,
+                void *stream) {
+  if (s.n > SRC_GUARD_MAXN || s.nlayer > SRC_GUARD_MAXL || t.n > NAN_MAXT || t.n > 256) return 2;
+  Ptr3 pt, e, d, u;
+  for (int c = 0; c < 3; c++) {
+    pt.p[c] = f.Dn[c], pt.ci[c] = f.cndinv[1][c];
+    e.p[c] = const_cast<double *>(E[c]), e.ci[c] = nullptr;
+    d.p[c] = const_cast<double *>(D[c]), d.ci[c] = nullptr;
+    u.p[c] = nullptr, u.ci[c] = U[c];
+  }
+  SrcLayers sl{};
+  sl.n = s.n > 0 ? s.nlayer : 0;
+  for (int l = 0; l <= sl.n; l++) sl.off[l] = s.layer[l];
+  src_guard_kernel<<<1, 256, 0, (hipStream_t)stream>>>(pt, s, sl, t, e, d, u, flag, step);
+  return rc();
+}
+
 int k_nan_check(const NanTerms &t, const double *const E[3], const double *const D[3],
                 const double *const U[3], int *flag, int step, void *stream) {
   if (t.n <= 0) return 0;

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal", "res", "res_tb2", "res_rim", "dft_cmp", "rim_zchunk", "nr_early", "tb_zchunk", "tb_ox", "tb_px", "tb_pol", "r1_beside", "tb_lint", "r2_lpt", "strip_zchunk"])
+    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal", "res", "res_tb2", "res_rim", "dft_cmp", "rim_zchunk", "nr_early", "tb_zchunk", "tb_ox", "tb_px", "tb_pol", "r1_beside", "tb_lint", "r2_lpt", "strip_zchunk", "src_guard"])
     ap.add_argument("--workload", default="waveguide")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=4)
