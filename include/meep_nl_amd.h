@@ -392,10 +392,11 @@ int mnl_fields_set_temporal_blocking(mnl_fields *f, int on);
  * side stream beside the two-step kernel (1, the default; one rank; MNL_TB_R1A), 13 the
  * interior two-step items on a third stream beside the previous pair's second rim launch (1;
  * 0, the default: measured slower at 512^3; one rank, no DFT monitors;
- * MNL_TB_LINT), 14 the second rim launch of a pair in longest-first order (1; 0, the
- * default: the first launch's order, narrow strips last, measured faster; one rank;
- * MNL_TB_R2LPT).  For in-process
- * A/B measurements
+ * MNL_TB_LINT), 14 the second rim launch's item order (1 longest first, 2 narrow strips
+ * first; 0, the default: the first launch's order, narrow strips last, measured faster; one
+ * rank; MNL_TB_R2LPT), 15 planes per narrow x-face strip item of the rim (value; 0 = the rim's
+ * chunk length; MNL_TB_STRIP_ZCHUNK), 16 a pair's step sources and NaN guard in one launch (1,
+ * the default; one rank; MNL_TB_SRCGUARD).  For in-process A/B measurements
  * (tools/ab_inproc.py). */
 int mnl_fields_set_schedule(mnl_fields *f, int which, int value);
 
