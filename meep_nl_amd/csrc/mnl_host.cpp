@@ -3449,15 +3449,16 @@ int tb_pair(mnl_fields *F, const SrcDev &s0, const SrcDev &s1, EB &ev_begin, EE 
   // (their samples of the previous pair read the compact boxes these items rewrite)
   const int ni = t.n;
   const int nl = (F->tb_lint && F->dfts.empty() && !F->tb_pol) ? std::min(F->tb_nint, ni) : 0;
+  // (the stream-ordering events below release at device scope: every reader is on this device)
   if ((na > 0 || nl > 0) && !F->s_aux) {
     HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming | hipEventReleaseToDevice));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming | hipEventReleaseToDevice));
   }
   if (nl > 0 && !F->s_lint) {
     HIPCHK(hipStreamCreateWithFlags(&F->s_lint, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&F->ev_lint, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&F->ev_r1done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_lint, hipEventDisableTiming | hipEventReleaseToDevice));
+    HIPCHK(hipEventCreateWithFlags(&F->ev_r1done, hipEventDisableTiming | hipEventReleaseToDevice));
   }
   if (nl > 0) {
     if (!F->tb_r1done_ok || F->tb_lint == 2)  // no previous pair in this batch: after all before
@@ -3729,12 +3730,16 @@ int step_batch(mnl_fields *F, int nsteps) {
   const int CH = NAN_CH;  // steps per source table / NaN flag read
   std::vector<EvPair> evs;
   size_t evi = 0;
+  // timing events only (read after a stream synchronize): no system-scope fence when one is
+  // recorded -- with it every record wrote back / invalidated the caches between the kernels,
+  // 0.4 % of a 512^3 step and 2.6 % of a 256^3 one (round 6; MNL_EV_FENCE=1 restores it)
+  const unsigned ev_flags = F->ev_fence ? hipEventDefault : hipEventDisableSystemFence;
   // timing events of a phase on the main stream (or st)
   auto ev_begin = [&](int cat, hipStream_t st = nullptr) -> int {
     if (!F->profiling) return -1;
     while (F->ev_pool.size() < 2 * (evi + 1)) {
       hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) return -1;
+      if (hipEventCreateWithFlags(&e, ev_flags) != hipSuccess) return -1;
       F->ev_pool.push_back(e);
     }
     EvPair p{F->ev_pool[2 * evi], F->ev_pool[2 * evi + 1], cat};
@@ -3752,7 +3757,7 @@ int step_batch(mnl_fields *F, int nsteps) {
     if (!F->profiling || k < 0) return ev_begin(cat);
     while (F->ev_pool.size() < 2 * (evi + 1)) {
       hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) return -1;
+      if (hipEventCreateWithFlags(&e, ev_flags) != hipSuccess) return -1;
       F->ev_pool.push_back(e);
     }
     EvPair p{evs[k].b, F->ev_pool[2 * evi + 1], cat};
@@ -3876,8 +3881,8 @@ int step_batch(mnl_fields *F, int nsteps) {
           // concurrently (disjoint points, old buffers read-only)
           if (!F->s_aux) {
             HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming | hipEventReleaseToDevice));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming | hipEventReleaseToDevice));
           }
           HIPCHK(hipEventRecord(F->ev_start, F->stream));
           HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
@@ -3897,8 +3902,8 @@ int step_batch(mnl_fields *F, int nsteps) {
           // and write the ping-pong partners: no ordering between them)
           if (!F->s_aux) {
             HIPCHK(hipStreamCreateWithFlags(&F->s_aux, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_start, hipEventDisableTiming | hipEventReleaseToDevice));
+            HIPCHK(hipEventCreateWithFlags(&F->ev_early, hipEventDisableTiming | hipEventReleaseToDevice));
           }
           HIPCHK(hipEventRecord(F->ev_start, F->stream));
           HIPCHK(hipStreamWaitEvent(F->s_aux, F->ev_start, 0));
@@ -4346,6 +4351,7 @@ mnl_fields *create_common(mnl_structure *s, int device, int rank, int nranks, co
   if (const char *tq = getenv("MNL_TB_POL")) F->tb_pol_on = atoi(tq) != 0;
   if (const char *ta = getenv("MNL_TB_R1A")) F->tb_r1a = atoi(ta) != 0;
   if (const char *tl = getenv("MNL_TB_LINT")) F->tb_lint = atoi(tl);
+  if (const char *ef = getenv("MNL_EV_FENCE")) F->ev_fence = atoi(ef) != 0;
   if (const char *sg = getenv("MNL_TB_SRCGUARD")) F->tb_srcguard = atoi(sg) != 0;
   if (const char *sz = getenv("MNL_TB_STRIP_ZCHUNK")) F->tb_szc = std::max(0, atoi(sz));
   if (const char *tp = getenv("MNL_TB_R2LPT")) F->tb_r2lpt = std::max(0, std::min(2, atoi(tp)));

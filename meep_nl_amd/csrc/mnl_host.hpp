@@ -372,6 +372,7 @@ struct mnl_fields {
   int tb_lint = 0;                  // MNL_TB_LINT=1 / set_schedule 13: the interior two-step
                                     // items beside the previous pair's second rim launch
   int tb_nint = 0;                  // two-step items whose footprint meets no rim box (first)
+  bool ev_fence = false;            // MNL_EV_FENCE=1: timing events with the default fence
   bool tb_srcguard = true;          // MNL_TB_SRCGUARD=0 / set_schedule 16: a pair's sources
                                     // and guard as two launches per step (default: one)
   int tb_szc = 0;                   // planes per narrow strip item (0: the rim's chunk length;

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal", "res", "res_tb2", "res_rim", "dft_cmp", "rim_zchunk", "nr_early", "tb_zchunk", "tb_ox", "tb_px", "tb_pol", "r1_beside", "tb_lint", "r2_lpt", "strip_zchunk", "src_guard"])
+    ap.add_argument("--option", required=True, choices=["narrow", "dft_pal", "res", "res_tb2", "res_rim", "dft_cmp", "rim_zchunk", "nr_early", "tb_zchunk", "tb_ox", "tb_px", "tb_pol", "r1_beside", "tb_lint", "r2_lpt", "strip_zchunk", "src_guard", "events"])
     ap.add_argument("--workload", default="waveguide")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=4)
@@ -67,7 +67,10 @@ def main():
             if a.fresh:
                 del f, s
                 s, f = build()
-            f.set_schedule(a.option, v)
+            if a.option == "events":  # per-launch HIP timing events on / off (bench.py's)
+                f.set_profiling(bool(v))
+            else:
+                f.set_schedule(a.option, v)
             if a.retune:
                 f.tune()
             f.step(4)  # re-plan / re-enter the fused mode outside the timed steps
