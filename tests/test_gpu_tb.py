@@ -111,6 +111,42 @@ def test_tb_interior_items_beside_previous_rim():
     _same(p, sc_tb(ProductSim, schedule=sched, steps=steps))
 
 
+def sc_tb_volume(make, big, steps=(1, 10, 1, 6), schedule=()):
+    """sc_tb's slab with Ez volume currents inside L2: a 3.0 x 3.0 x 1.2 box (more D source points
+    than one workgroup of the pair's source + guard launch takes: the two-launch fallback) or a
+    plane given twice plus a point on it (several source layers in the one launch)."""
+    o = vol(make, 3, [9.6, 6.4, 8.0], 10, center_origin=True)
+    o.add_pml(0.7)
+    for c in E_COMPS:
+        x, y, z = o.coords(c)
+        o.set_chi1inv(c, c, np.where((np.abs(y) < 0.8) & (z > -0.4) & (z < 3.0), 1.0 / 6.0, 1.0))
+    if big:
+        o.add_gaussian_volume_source(2, 0.25, 4.0, 0.0, 40.0, (-1.53, -1.47, -0.61), (1.51, 1.52, 0.63),
+                                     0.5)  # > 30 x 30 x 12 points
+    else:
+        for a in (0.6, 0.2):
+            o.add_gaussian_volume_source(2, 0.25, 4.0, 0.0, 40.0, (-1.0, -1.0, 0.33), (1.0, 1.0, 0.33), a)
+        o.add_gaussian_source(2, 0.25, 4.0, 0.0, 40.0, (0.05, 0.05, 0.33), 1.0)
+    random_init(o, (6, 7, 8, 9, 10, 11))
+    if isinstance(o, ProductSim):
+        for opt, val in schedule:
+            o._fields().set_schedule(opt, val)
+    for n in steps:
+        o.step(n)
+    return o
+
+
+@pytest.mark.parametrize("big", [False, True], ids=["layers", "long_list"])
+def test_tb_volume_sources_src_guard(big):
+    """A pair's step sources and NaN guard in one launch (src_guard_kernel): several source
+    layers in that launch, and the two-launch fallback for a long source list -- bitwise the
+    oracle and the two-launch path."""
+    p = sc_tb_volume(ProductSim, big)
+    assert p._fields().tb_info()["active"]
+    _same(p, sc_tb_volume(make_oracle, big))
+    _same(p, sc_tb_volume(ProductSim, big, schedule=(("src_guard", 0),)))
+
+
 def test_tb_equals_one_step_path():
     """Odd calls, one-step calls between pairs: identical to stepping one step at a time."""
     steps = (1, 7, 1, 4, 2, 3)
